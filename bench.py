@@ -1,0 +1,215 @@
+"""Benchmark: the fused analyzer suite of BASELINE config C2 on device-resident synthetic columns.
+
+One step = one AnalysisRunner scan pass of the suite over the rank's row shard (49 ops: Size +
+{Completeness, Mean, Sum, Minimum, Maximum, StandardDeviation} over 8 columns: 4 fp64 + 4 int64,
+1 % nulls), the RCCL all-gather of the per-rank states (N > 1) and the rank-ordered
+semigroup fold of those states on the host. Rows are sharded contiguously across ranks (strong
+scaling over the 1e9-row table). Inputs are generated in HBM by the counter-based splitmix64
+generators before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 0x5EED0000
+# C2 column kinds: c0, c1 dyadic (exact sums); c2 U[0,1); c3 N(100, 15^2); c4..c7 int64 U[-2^31, 2^31)
+C2_KINDS = [1, 1, 2, 3, 4, 4, 4, 4]
+
+
+def c2_analyzers(D, names):
+    out = [D.Size()]
+    for c in names:
+        out += [D.Completeness(c), D.Mean(c), D.Sum(c), D.Minimum(c), D.Maximum(c), D.StandardDeviation(c)]
+    return out
+
+
+def build_shard(torch, N, ctx, row0, nrows, dev):
+    from deequ_amd.table import Table, Column
+    cols = []
+    for c, kind in enumerate(C2_KINDS):
+        dt = torch.float64 if kind in (1, 2, 3, 6) else torch.int64
+        vals = torch.empty(max(nrows, 1), dtype=dt, device=dev)
+        valid = torch.zeros(max((nrows + 63) // 64 * 8, 8), dtype=torch.uint8, device=dev)
+        ctx.synth_column(kind, SEED + c, row0, nrows, vals.data_ptr())
+        ctx.synth_validity(SEED + 0x100 + c, row0, nrows, 10, valid.data_ptr())
+        spark_type = N.TYPE_DOUBLE if dt == torch.float64 else N.TYPE_LONG
+        col = Column("c%d" % c, spark_type, None, None, length=nrows)
+        col.device = {"values": vals, "validity": valid}
+        cols.append(col)
+    ctx.synchronize()
+    return Table(cols)
+
+
+def cpu_baseline(seconds, sample_rows):
+    """The oracle's Spark-order restatement (oracle/dq_oracle.c oracle_scan_spark), one thread, over a
+    bounded sample of the same synthetic columns; rows/s of the 8-column suite."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    L = O.lib()
+    L.oracle_scan_spark.restype = ctypes.c_int64
+    L.oracle_scan_spark.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    cols = []
+    for c, kind in enumerate(C2_KINDS):
+        v = O.synth_column(kind, SEED + c, 0, sample_rows)
+        m = O.synth_validity(SEED + 0x100 + c, 0, sample_rows, 10).astype(np.uint8)
+        cols.append((7 if kind in (1, 2, 3) else 5, v, m))
+    out = np.zeros(5)
+    rows, t0 = 0, time.perf_counter()
+    while True:
+        for st, v, m in cols:
+            L.oracle_scan_spark(st, v.ctypes.data, m.ctypes.data, sample_rows, out.ctypes.data)
+        rows += sample_rows
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": rows / el, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": "oracle_scan_spark over %d-row x 8-col sample of the C2 columns, %d passes in %.1f s "
+                      "(Spark-order count/sum/min/max/Welford; not deequ/Spark itself)"
+                      % (sample_rows, rows // sample_rows, el)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=float, default=1e9)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-sample-rows", type=int, default=8_000_000)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import deequ_amd as D
+    import deequ_amd.native as N
+    from deequ_amd import engine
+    from deequ_amd.states import state_from_native
+    engine.set_device(local)
+    ctx = engine.ctx()
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+
+    total = int(args.rows)
+    # contiguous shards, aligned to the 2048-row tile
+    per = (total + world - 1) // world
+    per = (per + 2047) // 2048 * 2048
+    row0 = min(rank * per, total)
+    nrows = max(0, min(total, row0 + per) - row0)
+    table = build_shard(torch, N, ctx, row0, nrows, dev)
+    names = list(table.columns)
+    analyzers = c2_analyzers(D, names)
+    batch = D.ScanBatch(table)
+    offsets = [a.addOps(batch) for a in analyzers]
+    nops = len(batch.ops)
+    out = torch.empty(nops * N.STATE_SIZE, dtype=torch.uint8, device=dev)
+    gathered = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, device=dev)
+    host = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, pin_memory=True)
+    cols = batch.native_columns()
+    preds = [p.to_native() for p in batch.preds]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        ctx.scan(cols, nrows, batch.ops, preds, out_device_ptr=out.data_ptr())
+        if i is not None:
+            ev[i][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)  # RCCL over xGMI
+            src = gathered
+        else:
+            src = out
+        host[:src.numel()].copy_(src, non_blocking=True)
+        stream.synchronize()
+        # rank-ordered fold with the reference semigroup merges (State.sum)
+        raw = host.numpy()
+        states = []
+        for op in range(nops):
+            acc = None
+            for r in range(world):
+                s = N.DqState.from_buffer_copy(raw[(r * nops + op) * N.STATE_SIZE:(r * nops + op + 1) * N.STATE_SIZE])
+                acc = s if acc is None else N.merge_states(acc, s)
+            states.append(acc)
+        return states
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        states = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    scan_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # sanity: the folded Size equals the table size
+    size_state = state_from_native(states[offsets[0][0]])
+    assert size_state.numMatches == total, (size_state, total)
+
+    bytes_per_row = sum(8 + 1.0 / 8 for _ in names)  # values + validity bit, per column
+    alg_bytes = bytes_per_row * nrows
+    achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total / (elapsed / args.steps)
+    result = {
+        "metric": "rows/sec + HBM GB/s (% peak) for fused analyzer suite, 1B rows, 1/2/4/8 GPUs",
+        "value": value,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64+i64",
+        "data": "synthetic (counter-based splitmix64 columns generated in HBM, SURVEY.md §8d)",
+        "config": {"workload": "C2 fused scan suite: Size + {Completeness, Mean, Sum, Minimum, Maximum, "
+                               "StandardDeviation} x 8 cols (4 fp64 + 4 int64, 1% nulls) = 49 ops",
+                   "rows": total, "rows_per_gpu": nrows, "columns": len(names), "ops": nops,
+                   "parallelism": "rows sharded dp%d + RCCL all-gather of states" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBPS, "traffic": None,
+                     "kernel": "dq_scan fused pass (scan_values_kernel launches + partial folds), HIP events "
+                               "on the scan stream, avg %.3f ms over %d steps; algorithmic bytes %.1f B/row x %d rows"
+                               % (scan_ms, args.steps, bytes_per_row, nrows)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_sample_rows)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

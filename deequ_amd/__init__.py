@@ -1,0 +1,19 @@
+"""deequ_amd — MI355X-native engine for deequ's AnalysisRunner metric computation.
+
+The analyzer / state / metric API mirrors com.amazon.deequ.analyzers; the
+per-row work runs in hand-written HIP kernels for gfx950 behind the C-ABI in include/dq.h.
+"""
+from .metrics import (Entity, DoubleMetric, HistogramMetric, Distribution, DistributionValue, Success, Failure,
+                      MetricCalculationException, MetricCalculationRuntimeException, EmptyStateException,
+                      NoSuchColumnException, WrongColumnTypeException, NoColumnsSpecifiedException,
+                      NumberOfSpecifiedColumnsException, IllegalAnalyzerParameterException)
+from .states import (NumMatches, NumMatchesAndCount, MeanState, SumState, MinState, MaxState,
+                     StandardDeviationState, CorrelationState, ApproxCountDistinctState)
+from .analyzers import (Size, Completeness, Compliance, Mean, Sum, Minimum, Maximum, StandardDeviation, Correlation,
+                        ApproxCountDistinct, Uniqueness, Distinctness, UniqueValueRatio, Entropy, CountDistinct,
+                        MutualInformation, Histogram, FrequenciesAndNumRows, Preconditions, computeFrequencies)
+from .runners import (AnalysisRunner, AnalysisRunBuilder, AnalyzerContext, Analysis, InMemoryStateProvider,
+                      ScanBatch)
+from .table import Table, Column
+
+__all__ = [n for n in dir() if not n.startswith("_")]

@@ -1,0 +1,637 @@
+"""deequ analyzers on the MI355X engine — the same case classes, preconditions, states and metrics as
+the reference (A/*.scala), with the per-row work done by libdq.so.
+
+Scan-shareable analyzers describe their Spark aggregations as dq_op records instead of Spark
+Columns (`aggregationFunctions`, A/Analyzer.scala:172) and rebuild their state from the returned
+dq_state (`fromAggregationResult`, A/Analyzer.scala:175). Grouping analyzers read the device
+frequency table built by `computeFrequencies` (A/GroupingAnalyzers.scala:53-79).
+"""
+import math
+
+import numpy as np
+
+from . import native as N
+from .expr import compile_predicate
+from .metrics import (DoubleMetric, Entity, Failure, Success, EmptyStateException, NoSuchColumnException,
+                      WrongColumnTypeException, NoColumnsSpecifiedException, NumberOfSpecifiedColumnsException,
+                      IllegalAnalyzerParameterException, HistogramMetric, Distribution, DistributionValue,
+                      MetricCalculationRuntimeException, wrap_if_necessary)
+from .states import (NumMatches, NumMatchesAndCount, MeanState, SumState, MinState, MaxState, state_from_native)
+from . import engine
+
+COL_PREFIX = "com_amazon_deequ_dq_metrics_"
+COUNT_COL = COL_PREFIX + "count"
+
+
+# ---- Preconditions (A/Analyzer.scala:285-359) ----------------------------------------------------
+class Preconditions:
+    NUMERIC = ("ByteType", "ShortType", "IntegerType", "LongType", "FloatType", "DoubleType")
+
+    @staticmethod
+    def findFirstFailing(schema, conditions):
+        for c in conditions:
+            try:
+                c(schema)
+            except Exception as e:  # only exceptions, as in the reference
+                return e
+        return None
+
+    @staticmethod
+    def atLeastOne(columns):
+        def check(_):
+            if not columns:
+                raise NoColumnsSpecifiedException("At least one column needs to be specified!")
+        return check
+
+    @staticmethod
+    def exactlyNColumns(columns, n):
+        def check(_):
+            if len(columns) != n:
+                raise NumberOfSpecifiedColumnsException(
+                    "%d columns have to be specified! Currently, columns contains only %d column(s): %s!"
+                    % (n, len(columns), ",".join(columns)))
+        return check
+
+    @staticmethod
+    def hasColumn(column):
+        def check(schema):
+            if column not in schema:
+                raise NoSuchColumnException("Input data does not include column %s!" % column)
+        return check
+
+    @staticmethod
+    def isNumeric(column):
+        def check(schema):
+            t = schema[column]
+            if not (t in Preconditions.NUMERIC or t.startswith("DecimalType")):
+                raise WrongColumnTypeException(
+                    "Expected type of column %s to be one of (%s), but found %s instead!"
+                    % (column, ",".join(Preconditions.NUMERIC + ("DecimalType",)), t))
+        return check
+
+    @staticmethod
+    def isString(column):
+        def check(schema):
+            t = schema[column]
+            if t != "StringType":
+                raise WrongColumnTypeException(
+                    "Expected type of column %s to be StringType, but found %s instead!" % (column, t))
+        return check
+
+
+def entityFrom(columns):
+    return Entity.Column if len(columns) == 1 else Entity.Mutlicolumn
+
+
+def metricFromValue(value, name, instance, entity=Entity.Column):
+    return DoubleMetric(entity, name, instance, Success(value))
+
+
+def emptyStateException(analyzer):
+    return EmptyStateException("Empty state for analyzer %r, all input values were NULL." % (analyzer,))
+
+
+def metricFromFailure(exception, name, instance, entity=Entity.Column):
+    return DoubleMetric(entity, name, instance, Failure(wrap_if_necessary(exception)))
+
+
+def metricFromEmpty(analyzer, name, instance, entity=Entity.Column):
+    return metricFromFailure(emptyStateException(analyzer), name, instance, entity)
+
+
+def merge(*states):
+    """Analyzers.merge (A/Analyzer.scala:367-386): None is the identity."""
+    out = None
+    for s in states:
+        if s is None:
+            continue
+        out = s if out is None else out.sum(s)
+    return out
+
+
+# ---- Analyzer base classes (A/Analyzer.scala:56-197) ---------------------------------------------
+class Analyzer:
+    _fields = ()
+
+    def _key(self):
+        return (type(self).__name__,) + tuple(
+            tuple(v) if isinstance(v, list) else v for v in (getattr(self, f) for f in self._fields))
+
+    def __eq__(self, other):
+        return type(self) is type(other) and self._key() == other._key()
+
+    def __hash__(self):
+        return hash(self._key())
+
+    def __repr__(self):
+        args = []
+        for f in self._fields:
+            v = getattr(self, f)
+            if isinstance(v, list):
+                v = "List(%s)" % ", ".join(v)
+            elif v is None:
+                v = "None"
+            elif f == "where":
+                v = "Some(%s)" % v
+            args.append(str(v))
+        return "%s(%s)" % (type(self).__name__, ",".join(args))
+
+    def preconditions(self):
+        return []
+
+    def computeStateFrom(self, data):
+        raise NotImplementedError
+
+    def computeMetricFrom(self, state):
+        raise NotImplementedError
+
+    def toFailureMetric(self, exception):
+        raise NotImplementedError
+
+    def calculate(self, data, aggregateWith=None, saveStatesWith=None):
+        """Analyzer.calculate (A/Analyzer.scala:88-103)."""
+        try:
+            for c in self.preconditions():
+                c(data.schema)
+            state = self.computeStateFrom(data)
+            return self.calculateMetric(state, aggregateWith, saveStatesWith)
+        except Exception as e:
+            return self.toFailureMetric(e)
+
+    def calculateMetric(self, state, aggregateWith=None, saveStatesWith=None):
+        """A/Analyzer.scala:107-128."""
+        loaded = aggregateWith.load(self) if aggregateWith is not None else None
+        to_use = merge(state, loaded)
+        if to_use is not None and saveStatesWith is not None:
+            saveStatesWith.persist(self, to_use)
+        return self.computeMetricFrom(to_use)
+
+    def aggregateStateTo(self, sourceA, sourceB, target):
+        a, b = sourceA.load(self), sourceB.load(self)
+        agg = merge(a, b)
+        if agg is not None:
+            target.persist(self, agg)
+
+    def loadStateAndComputeMetric(self, source):
+        s = source.load(self)
+        return None if s is None else self.computeMetricFrom(s)
+
+    def copyStateTo(self, source, target):
+        s = source.load(self)
+        if s is not None:
+            target.persist(self, s)
+
+
+class ScanShareableAnalyzer(Analyzer):
+    """Contributes dq_ops to the fused scan instead of Spark aggregation Columns."""
+
+    def addOps(self, batch):
+        """Register this analyzer's ops; return the op indices (the `offset` into the result)."""
+        raise NotImplementedError
+
+    def fromAggregationResult(self, states, ops):
+        raise NotImplementedError
+
+    def computeStateFrom(self, data):
+        from .runners import ScanBatch
+        batch = ScanBatch(data)
+        ops = self.addOps(batch)
+        states = batch.run()
+        return self.fromAggregationResult(states, ops)
+
+    def metricFromAggregationResult(self, states, ops, aggregateWith=None, saveStatesWith=None):
+        return self.calculateMetric(self.fromAggregationResult(states, ops), aggregateWith, saveStatesWith)
+
+
+class StandardScanShareableAnalyzer(ScanShareableAnalyzer):
+    name = None
+    entity = Entity.Column
+
+    @property
+    def instance(self):
+        raise NotImplementedError
+
+    def computeMetricFrom(self, state):
+        if state is not None:
+            return metricFromValue(state.metricValue(), self.name, self.instance, self.entity)
+        return metricFromEmpty(self, self.name, self.instance, self.entity)
+
+    def toFailureMetric(self, exception):
+        return metricFromFailure(exception, self.name, self.instance, self.entity)
+
+    def additionalPreconditions(self):
+        return []
+
+    def preconditions(self):
+        return self.additionalPreconditions()
+
+    def _one_state(self, states, ops):
+        return state_from_native(states[ops[0]])
+
+    def fromAggregationResult(self, states, ops):
+        return self._one_state(states, ops)
+
+
+# ---- scan-shareable analyzers --------------------------------------------------------------------
+class Size(StandardScanShareableAnalyzer):
+    """A/Size.scala:33-47."""
+    _fields = ("where",)
+    name = "Size"
+    entity = Entity.Dataset
+
+    def __init__(self, where=None):
+        self.where = where
+
+    instance = property(lambda self: "*")
+
+    def addOps(self, batch):
+        return [batch.add_op(N.OP_SIZE, where=self.where)]
+
+
+class Completeness(StandardScanShareableAnalyzer):
+    """A/Completeness.scala:26-46."""
+    _fields = ("column", "where")
+    name = "Completeness"
+
+    def __init__(self, column, where=None):
+        self.column, self.where = column, where
+
+    instance = property(lambda self: self.column)
+
+    def additionalPreconditions(self):
+        return [Preconditions.hasColumn(self.column)]
+
+    def addOps(self, batch):
+        return [batch.add_op(N.OP_COMPLETENESS, (self.column,), where=self.where)]
+
+
+class Compliance(StandardScanShareableAnalyzer):
+    """A/Compliance.scala:37-53."""
+    _fields = ("instance_", "predicate", "where")
+    name = "Compliance"
+
+    def __init__(self, instance, predicate, where=None):
+        self.instance_, self.predicate, self.where = instance, predicate, where
+
+    instance = property(lambda self: self.instance_)
+
+    def addOps(self, batch):
+        return [batch.add_op(N.OP_COMPLIANCE, where=self.where, predicate=self.predicate)]
+
+
+class _NumericColumnAnalyzer(StandardScanShareableAnalyzer):
+    _fields = ("column", "where")
+    op_kind = None
+
+    def __init__(self, column, where=None):
+        self.column, self.where = column, where
+
+    instance = property(lambda self: self.column)
+
+    def additionalPreconditions(self):
+        return [Preconditions.hasColumn(self.column), Preconditions.isNumeric(self.column)]
+
+    def addOps(self, batch):
+        return [batch.add_op(self.op_kind, (self.column,), where=self.where)]
+
+
+class Mean(_NumericColumnAnalyzer):
+    """A/Mean.scala:36-54."""
+    name, op_kind = "Mean", N.OP_MEAN
+
+
+class Sum(_NumericColumnAnalyzer):
+    """A/Sum.scala:34-52."""
+    name, op_kind = "Sum", N.OP_SUM
+
+
+class Minimum(_NumericColumnAnalyzer):
+    """A/Minimum.scala:34-53."""
+    name, op_kind = "Minimum", N.OP_MINIMUM
+
+
+class Maximum(_NumericColumnAnalyzer):
+    """A/Maximum.scala:34-53."""
+    name, op_kind = "Maximum", N.OP_MAXIMUM
+
+
+class StandardDeviation(_NumericColumnAnalyzer):
+    """A/StandardDeviation.scala:47-73."""
+    name, op_kind = "StandardDeviation", N.OP_STANDARD_DEVIATION
+
+
+class Correlation(StandardScanShareableAnalyzer):
+    """A/Correlation.scala:66-105."""
+    _fields = ("firstColumn", "secondColumn", "where")
+    name = "Correlation"
+    entity = Entity.Mutlicolumn
+
+    def __init__(self, firstColumn, secondColumn, where=None):
+        self.firstColumn, self.secondColumn, self.where = firstColumn, secondColumn, where
+
+    instance = property(lambda self: "%s,%s" % (self.firstColumn, self.secondColumn))
+
+    def additionalPreconditions(self):
+        return [Preconditions.hasColumn(self.firstColumn), Preconditions.isNumeric(self.firstColumn),
+                Preconditions.hasColumn(self.secondColumn), Preconditions.isNumeric(self.secondColumn)]
+
+    def addOps(self, batch):
+        return [batch.add_op(N.OP_CORRELATION, (self.firstColumn, self.secondColumn), where=self.where)]
+
+
+class ApproxCountDistinct(StandardScanShareableAnalyzer):
+    """A/ApproxCountDistinct.scala:43-64 (HLL++ registers, XXH64 seed 42)."""
+    _fields = ("column", "where")
+    name = "ApproxCountDistinct"
+
+    def __init__(self, column, where=None):
+        self.column, self.where = column, where
+
+    instance = property(lambda self: self.column)
+
+    def additionalPreconditions(self):
+        return [Preconditions.hasColumn(self.column)]
+
+    def addOps(self, batch):
+        return [batch.add_op(N.OP_APPROX_COUNT_DISTINCT, (self.column,), where=self.where)]
+
+
+# ---- grouping analyzers (A/GroupingAnalyzers.scala) ----------------------------------------------
+class FrequenciesAndNumRows:
+    """A/GroupingAnalyzers.scala:123-156. `frequencies` is a device (key -> count) table produced by
+    dq_frequencies, or a host dict after a state merge (outer join with counts added)."""
+
+    def __init__(self, frequencies, numRows, columns=None, summary=None):
+        self.frequencies = frequencies  # engine.FrequencyTable or dict[tuple -> int]
+        self.numRows = int(numRows)
+        self.columns = columns
+
+    def as_dict(self):
+        if isinstance(self.frequencies, dict):
+            return self.frequencies
+        return self.frequencies.to_dict()
+
+    def sum(self, other):
+        """Null-safe full outer join on the keys, counts added (A/GroupingAnalyzers.scala:127-147)."""
+        merged = dict(self.as_dict())
+        for k, v in other.as_dict().items():
+            merged[k] = merged.get(k, 0) + v
+        return FrequenciesAndNumRows(merged, self.numRows + other.numRows, self.columns)
+
+    def summary(self, entropy_rows=None):
+        n = self.numRows if entropy_rows is None else entropy_rows
+        if isinstance(self.frequencies, dict):
+            counts = np.fromiter(self.frequencies.values(), dtype=np.float64, count=len(self.frequencies))
+            ent = 0.0
+            if len(counts):
+                p = counts / n
+                ent = float(-(p * np.log(p)).sum())
+            return {"num_groups": len(counts), "num_unique": int((counts == 1).sum()), "entropy": ent}
+        return self.frequencies.summary(n)
+
+
+def computeFrequencies(data, groupingColumns, include_nulls=False):
+    """FrequencyBasedAnalyzer.computeFrequencies (A/GroupingAnalyzers.scala:53-79) on the GPU."""
+    table = engine.frequencies(data, list(groupingColumns), include_nulls=include_nulls)
+    return FrequenciesAndNumRows(table, table.num_rows, list(groupingColumns))
+
+
+class GroupingAnalyzer(Analyzer):
+    def groupingColumns(self):
+        raise NotImplementedError
+
+    def preconditions(self):
+        return [Preconditions.hasColumn(c) for c in self.groupingColumns()]
+
+
+class FrequencyBasedAnalyzer(GroupingAnalyzer):
+    _fields = ("columns",)
+
+    def __init__(self, columns):
+        self.columns = [columns] if isinstance(columns, str) else list(columns)
+
+    def groupingColumns(self):
+        return self.columns
+
+    def computeStateFrom(self, data):
+        return computeFrequencies(data, self.groupingColumns())
+
+    def preconditions(self):
+        return [Preconditions.atLeastOne(self.columns)] + [Preconditions.hasColumn(c) for c in self.columns]
+
+
+class ScanShareableFrequencyBasedAnalyzer(FrequencyBasedAnalyzer):
+    """A/GroupingAnalyzers.scala:83-120: one fused aggregation over the frequency table."""
+    name = None
+
+    @property
+    def instance(self):
+        return ",".join(self.columns)
+
+    @property
+    def entity(self):
+        return entityFrom(self.columns)
+
+    def valueFromSummary(self, summary, numRows):
+        """The analyzer's aggregation over the table; None when Spark's aggregate is NULL."""
+        raise NotImplementedError
+
+    def computeMetricFrom(self, state):
+        if state is None:
+            return metricFromEmpty(self, self.name, self.instance, self.entity)
+        try:
+            summ = state.summary()
+            v = self.valueFromSummary(summ, state.numRows)
+        except Exception as e:
+            return self.toFailureMetric(e)
+        if v is None:
+            return metricFromEmpty(self, self.name, self.instance, self.entity)
+        return metricFromValue(v, self.name, self.instance, self.entity)
+
+    def toFailureMetric(self, exception):
+        return metricFromFailure(exception, self.name, self.instance, self.entity)
+
+
+class Uniqueness(ScanShareableFrequencyBasedAnalyzer):
+    """A/Uniqueness.scala:26-32: sum(count == 1) / numRows."""
+    name = "Uniqueness"
+
+    def valueFromSummary(self, s, numRows):
+        return None if s["num_groups"] == 0 else s["num_unique"] / numRows
+
+
+class Distinctness(ScanShareableFrequencyBasedAnalyzer):
+    """A/Distinctness.scala:29-35: sum(count >= 1) / numRows."""
+    name = "Distinctness"
+
+    def valueFromSummary(self, s, numRows):
+        return None if s["num_groups"] == 0 else s["num_groups"] / numRows
+
+
+class UniqueValueRatio(ScanShareableFrequencyBasedAnalyzer):
+    """A/UniqueValueRatio.scala:25-38: #unique / #groups (getDouble of a NULL sum throws on empty)."""
+    name = "UniqueValueRatio"
+
+    def valueFromSummary(self, s, numRows):
+        if s["num_groups"] == 0:
+            raise MetricCalculationRuntimeException(cause=TypeError("Value at index 0 is null"))
+        return s["num_unique"] / s["num_groups"]
+
+
+class CountDistinct(ScanShareableFrequencyBasedAnalyzer):
+    """A/CountDistinct.scala:24-34: count(*) over the table."""
+    name = "CountDistinct"
+
+    def valueFromSummary(self, s, numRows):
+        return float(s["num_groups"])
+
+
+class Entropy(ScanShareableFrequencyBasedAnalyzer):
+    """A/Entropy.scala:28-42: sum over groups of -(c/N) ln(c/N)."""
+    name = "Entropy"
+    _fields = ("column",)
+
+    def __init__(self, column):
+        super().__init__([column])
+        self.column = column
+
+    def valueFromSummary(self, s, numRows):
+        return None if s["num_groups"] == 0 else s["entropy"]
+
+
+class MutualInformation(FrequencyBasedAnalyzer):
+    """A/MutualInformation.scala:35-97 (joint table + marginals)."""
+    name = "MutualInformation"
+
+    def preconditions(self):
+        return [Preconditions.exactlyNColumns(self.columns, 2)] + super().preconditions()
+
+    def computeMetricFrom(self, state):
+        inst = ",".join(self.columns)
+        if state is None:
+            return metricFromEmpty(self, self.name, inst, Entity.Mutlicolumn)
+        joint = state.as_dict()
+        if not joint:
+            return metricFromEmpty(self, self.name, inst, Entity.Mutlicolumn)
+        total = state.numRows
+        px, py = {}, {}
+        for (a, b), c in joint.items():
+            px[a] = px.get(a, 0) + c
+            py[b] = py.get(b, 0) + c
+        mi = 0.0
+        for (a, b), c in joint.items():
+            if a is None or b is None:
+                continue  # Spark's equi-join on the marginals drops NULL keys
+            pxy = c / total
+            mi += pxy * math.log(pxy / ((px[a] / total) * (py[b] / total)))
+        return metricFromValue(mi, self.name, inst, Entity.Mutlicolumn)
+
+    def toFailureMetric(self, exception):
+        return metricFromFailure(exception, self.name, ",".join(self.columns), Entity.Mutlicolumn)
+
+
+class Histogram(Analyzer):
+    """A/Histogram.scala:41-117: counts per value (nulls as "NullValue"), top-N details."""
+    NullFieldReplacement = "NullValue"
+    MaximumAllowedDetailBins = 1000
+    _fields = ("column", "maxDetailBins")
+
+    def __init__(self, column, binningUdf=None, maxDetailBins=MaximumAllowedDetailBins):
+        self.column, self.binningUdf, self.maxDetailBins = column, binningUdf, maxDetailBins
+
+    def preconditions(self):
+        def param_check(_):
+            if self.maxDetailBins > Histogram.MaximumAllowedDetailBins:
+                raise IllegalAnalyzerParameterException(
+                    "Cannot return histogram values for more than %d values" % Histogram.MaximumAllowedDetailBins)
+        return [param_check, Preconditions.hasColumn(self.column)]
+
+    def computeStateFrom(self, data):
+        if self.binningUdf is not None:
+            # The binning UDF is an arbitrary host function: apply it to the key column, then group.
+            from .table import Table, _column_from_pylist
+            vals = data[self.column].to_pylist()
+            binned = [self.binningUdf(None if v is None else _spark_string(v, data[self.column])) for v in vals]
+            t = Table([_column_from_pylist(self.column, "string", binned)])
+            table = engine.frequencies(t, [self.column], include_nulls=True)
+        else:
+            table = engine.frequencies(data, [self.column], include_nulls=True)
+        return FrequenciesAndNumRows(table, data.count(), [self.column])
+
+    def computeMetricFrom(self, state):
+        if state is None:
+            return HistogramMetric(self.column, Failure(emptyStateException(self)))
+        try:
+            if isinstance(state.frequencies, dict):
+                items = sorted(state.frequencies.items(), key=lambda kv: -kv[1])[:self.maxDetailBins]
+                nbins = len(state.frequencies)
+                details = {(_hist_key(k[0])): DistributionValue(c, c / state.numRows) for k, c in items}
+            else:
+                nbins = state.frequencies.num_groups
+                details = {}
+                for key, c in state.frequencies.top(self.maxDetailBins):
+                    details[_hist_key(key[0], state.frequencies.key_columns[0])] = \
+                        DistributionValue(int(c), int(c) / state.numRows)
+            return HistogramMetric(self.column, Success(Distribution(details, nbins)))
+        except Exception as e:
+            return HistogramMetric(self.column, Failure(wrap_if_necessary(e)))
+
+    def toFailureMetric(self, exception):
+        return HistogramMetric(self.column, Failure(wrap_if_necessary(exception)))
+
+
+def _spark_string(v, column=None):
+    """Spark `Cast(x AS STRING)` for a host value (only top-N keys are ever formatted)."""
+    if v is None:
+        return None
+    t = column.spark_type if column is not None else None
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, float) or t in (N.TYPE_FLOAT, N.TYPE_DOUBLE):
+        return _java_double_to_string(float(v), t == N.TYPE_FLOAT)
+    return str(v)
+
+
+def _hist_key(v, column=None):
+    return Histogram.NullFieldReplacement if v is None else _spark_string(v, column)
+
+
+def _java_double_to_string(d, is_float=False):
+    """java.lang.Double.toString / Float.toString: shortest repr, sci notation outside [1e-3, 1e7)."""
+    if math.isnan(d):
+        return "NaN"
+    if math.isinf(d):
+        return "Infinity" if d > 0 else "-Infinity"
+    if d == 0.0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    r = repr(float(np.float32(d))) if is_float else repr(d)
+    a = abs(d)
+    if 1e-3 <= a < 1e7:
+        if "e" in r or "E" in r:
+            r = ("%f" % d).rstrip("0")
+        if "." not in r:
+            r += ".0"
+        return r
+    mant, _, exp = ("%.17e" % d).partition("e")
+    digits = repr(d if not is_float else float(np.float32(d)))
+    # shortest digits via repr, reformatted as Java's d.dddE<exp>
+    m, e = _sci_parts(digits)
+    return "%sE%d" % (m, e)
+
+
+def _sci_parts(r):
+    sign = "-" if r.startswith("-") else ""
+    r = r.lstrip("-")
+    if "e" in r:
+        m, e = r.split("e")
+        e = int(e)
+    else:
+        m, e = r, 0
+    digits = m.replace(".", "")
+    point = m.index(".") if "." in m else len(m)
+    stripped = digits.lstrip("0")
+    lead = len(digits) - len(stripped)
+    e += point - lead - 1
+    stripped = stripped.rstrip("0") or "0"
+    mant = stripped[0] + "." + (stripped[1:] or "0")
+    return sign + mant, e

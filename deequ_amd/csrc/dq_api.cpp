@@ -1,0 +1,858 @@
+// dq_api.cpp — host runtime behind include/dq.h.
+//
+// Plans a batch of deequ ops into fused-scan slots (one HBM read per column), evaluates `where`
+// / Compliance predicates into bitmaps, launches the kernels on the context's stream and turns
+// the final slot partials into per-op states. Mirrors, per entry point:
+//   dq_scan            runScanningAnalyzers            R/AnalysisRunner.scala:289-336
+//   dq_state_merge     State.sum / Analyzers.merge     A/Analyzer.scala:367-386 (+ each state's sum)
+//   dq_hll_count       DeequHyperLogLogPlusPlusUtils   C/StatefulHyperloglogPlus.scala:210-298
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "dq_common.h"
+#include "dq_internal.h"
+#include "hll_bias_p9.h"
+
+using namespace dq;
+
+struct dq_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // Device arena, re-used by every call (grown outside of any timed/captured region).
+    uint8_t* arena = nullptr;
+    size_t arena_cap = 0;
+    // Pinned host staging for plan uploads and state downloads.
+    uint8_t* pinned = nullptr;
+    size_t pinned_cap = 0;
+    int cus = 256;
+    std::map<int, int> occupancy;  // launch shape -> workgroups per CU
+    int64_t scan_launches = 0;
+};
+
+namespace {
+
+int fail(dq_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (ctx) ctx->err = buf;
+    return code;
+}
+
+#define DQ_HIP(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail((ctx), DQ_ERR_DEVICE, "%s failed: %s", #expr, hipGetErrorString(e_));     \
+    } while (0)
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Bump allocator over the context arena. Two passes: measure, then (after growth) assign.
+struct Bump {
+    size_t off = 0;
+    uint8_t* base = nullptr;
+    void* take(size_t bytes, size_t align = 256) {
+        off = align_up(off, align);
+        void* p = base ? base + off : nullptr;
+        off += bytes;
+        return p;
+    }
+};
+
+int ensure_arena(dq_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->arena_cap) return DQ_OK;
+    if (ctx->arena) {
+        DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        DQ_HIP(ctx, hipFree(ctx->arena));
+        ctx->arena = nullptr;
+        ctx->arena_cap = 0;
+    }
+    size_t cap = std::max(bytes, (size_t)64 << 20);
+    if (hipMalloc(&ctx->arena, cap) != hipSuccess) {
+        ctx->arena = nullptr;
+        return fail(ctx, DQ_ERR_OUT_OF_MEMORY, "device arena allocation of %zu bytes failed", cap);
+    }
+    ctx->arena_cap = cap;
+    return DQ_OK;
+}
+
+int ensure_pinned(dq_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->pinned_cap) return DQ_OK;
+    if (ctx->pinned) {
+        DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        DQ_HIP(ctx, hipHostFree(ctx->pinned));
+        ctx->pinned = nullptr;
+        ctx->pinned_cap = 0;
+    }
+    size_t cap = std::max(bytes, (size_t)1 << 20);
+    DQ_HIP(ctx, hipHostMalloc((void**)&ctx->pinned, cap, hipHostMallocDefault));
+    ctx->pinned_cap = cap;
+    return DQ_OK;
+}
+
+bool is_numeric_type(int t) {
+    // Preconditions.isNumeric (A/Analyzer.scala:329-343)
+    return t == DQ_TYPE_BYTE || t == DQ_TYPE_SHORT || t == DQ_TYPE_INT || t == DQ_TYPE_LONG ||
+           t == DQ_TYPE_FLOAT || t == DQ_TYPE_DOUBLE || t == DQ_TYPE_DECIMAL;
+}
+bool is_fixed_width(int t) { return elem_of(t) != ET_NONE; }
+
+int64_t padded_words_for(int64_t nrows) {
+    const int64_t tiles = std::max<int64_t>(1, (nrows + kTileRows - 1) / kTileRows);
+    return tiles * (kTileRows / 64);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host state algebra (State.sum of each reference state)
+// ------------------------------------------------------------------------------------------------
+void hll_merge_words(const int64_t* a, const int64_t* b, int64_t* out) {
+    // DeequHyperLogLogPlusPlusUtils.merge (C/StatefulHyperloglogPlus.scala:188-208)
+    int idx = 0;
+    for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) {
+        uint64_t wa = (uint64_t)a[w], wb = (uint64_t)b[w], word = 0;
+        uint64_t mask = 63;
+        for (int i = 0; idx < DQ_HLL_REGISTERS && i < 10; ++i, ++idx) {
+            word |= std::max(wa & mask, wb & mask);
+            mask <<= 6;
+        }
+        out[w] = (int64_t)word;
+    }
+}
+
+double java_math_min(double a, double b) {
+    if (a != a) return a;
+    if (b != b) return b;
+    if (a == 0.0 && b == 0.0) return signbit(a) ? a : b;
+    return a <= b ? a : b;
+}
+double java_math_max(double a, double b) {
+    if (a != a) return a;
+    if (b != b) return b;
+    if (a == 0.0 && b == 0.0) return signbit(a) ? b : a;
+    return a >= b ? a : b;
+}
+
+}  // namespace
+
+// =================================================================================================
+// C-ABI
+// =================================================================================================
+extern "C" {
+
+int dq_abi_version(void) { return DQ_ABI_VERSION; }
+
+dq_ctx* dq_open(int device, int* status) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        if (status) *status = DQ_ERR_NO_DEVICE;
+        return nullptr;
+    }
+    if (device < 0 || device >= n) {
+        if (status) *status = DQ_ERR_INVALID_ARGUMENT;
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        if (status) *status = DQ_ERR_DEVICE;
+        return nullptr;
+    }
+    dq_ctx* ctx = new dq_ctx();
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        if (status) *status = DQ_ERR_DEVICE;
+        return nullptr;
+    }
+    ctx->stream = ctx->own_stream;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ctx->cus = prop.multiProcessorCount;
+    if (status) *status = DQ_OK;
+    return ctx;
+}
+
+void dq_close(dq_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->arena) (void)hipFree(ctx->arena);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+}
+
+const char* dq_last_error(const dq_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int dq_set_stream(dq_ctx* ctx, void* stream) {
+    if (!ctx) return DQ_ERR_INVALID_ARGUMENT;
+    ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+    return DQ_OK;
+}
+
+int dq_synchronize(dq_ctx* ctx) {
+    if (!ctx) return DQ_ERR_INVALID_ARGUMENT;
+    DQ_HIP(ctx, hipSetDevice(ctx->device));
+    DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return DQ_OK;
+}
+
+int64_t dq_scan_launch_count(const dq_ctx* ctx) { return ctx ? ctx->scan_launches : -1; }
+
+int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const dq_op* ops, int nops,
+            const dq_predicate* preds, int npreds, dq_state* out, uint32_t flags) {
+    if (!ctx) return DQ_ERR_INVALID_ARGUMENT;
+    ctx->err.clear();
+    if (nops < 0 || ncols < 0 || npreds < 0 || nrows < 0 || (nops > 0 && (!ops || !out)))
+        return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "invalid arguments");
+    if (nops == 0) return DQ_OK;
+    DQ_HIP(ctx, hipSetDevice(ctx->device));
+
+    // ---- validation ---------------------------------------------------------------------------
+    for (int c = 0; c < ncols; ++c) {
+        const dq_column& col = columns[c];
+        if (col.length != nrows)
+            return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "column %d has %lld rows, batch has %lld", c,
+                        (long long)col.length, (long long)nrows);
+        if (col.spark_type < DQ_TYPE_BOOLEAN || col.spark_type > DQ_TYPE_DECIMAL)
+            return fail(ctx, DQ_ERR_UNSUPPORTED, "column %d: unknown spark type %d", c, col.spark_type);
+        if (col.spark_type == DQ_TYPE_STRING && nrows > 0 && !col.offsets)
+            return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "string column %d without offsets", c);
+        if (col.spark_type == DQ_TYPE_DECIMAL && (col.decimal_precision > 18 || col.decimal_scale < 0 || col.decimal_scale > 18))
+            return fail(ctx, DQ_ERR_UNSUPPORTED, "column %d: decimal precision > 18 unsupported", c);
+        if ((col.flags & DQ_COL_DEVICE) && nrows > 0) {
+            const int e = elem_of(col.spark_type);
+            const size_t va = e == ET_NONE ? 1 : (elem_size(e) == 1 ? 8 : 16);
+            if (((uintptr_t)col.values % va) != 0 || ((uintptr_t)col.validity % 8) != 0)
+                return fail(ctx, DQ_ERR_ALIGNMENT, "device column %d: values must be %zu-byte and validity 8-byte aligned", c, va);
+        }
+    }
+    auto col_ok = [&](int c) { return c >= 0 && c < ncols; };
+    std::vector<char> pred_used(npreds, 0);
+    std::vector<char> col_used(ncols, 0);
+    for (int i = 0; i < nops; ++i) {
+        const dq_op& op = ops[i];
+        if (op.where >= npreds || op.where < -1) return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "op %d: bad where index", i);
+        if (op.where >= 0) pred_used[op.where] = 1;
+        switch (op.kind) {
+            case DQ_OP_SIZE: break;
+            case DQ_OP_COMPLIANCE:
+                if (op.predicate < 0 || op.predicate >= npreds)
+                    return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "op %d: Compliance needs a predicate", i);
+                pred_used[op.predicate] = 1;
+                break;
+            case DQ_OP_COMPLETENESS:
+                if (!col_ok(op.column[0])) return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "op %d: bad column", i);
+                col_used[op.column[0]] = 1;
+                break;
+            case DQ_OP_MEAN: case DQ_OP_SUM: case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM: case DQ_OP_STANDARD_DEVIATION:
+                if (!col_ok(op.column[0])) return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "op %d: bad column", i);
+                if (!is_numeric_type(columns[op.column[0]].spark_type))
+                    return fail(ctx, DQ_ERR_UNSUPPORTED, "op %d: column %d is not numeric", i, op.column[0]);
+                col_used[op.column[0]] = 1;
+                break;
+            case DQ_OP_CORRELATION:
+                if (!col_ok(op.column[0]) || !col_ok(op.column[1]))
+                    return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "op %d: bad column", i);
+                if (!is_numeric_type(columns[op.column[0]].spark_type) || !is_numeric_type(columns[op.column[1]].spark_type))
+                    return fail(ctx, DQ_ERR_UNSUPPORTED, "op %d: correlation needs numeric columns", i);
+                col_used[op.column[0]] = col_used[op.column[1]] = 1;
+                break;
+            case DQ_OP_APPROX_COUNT_DISTINCT:
+                if (!col_ok(op.column[0])) return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "op %d: bad column", i);
+                if (!is_fixed_width(columns[op.column[0]].spark_type))
+                    return fail(ctx, DQ_ERR_UNSUPPORTED, "op %d: ApproxCountDistinct on this type is not implemented", i);
+                col_used[op.column[0]] = 1;
+                break;
+            default:
+                return fail(ctx, DQ_ERR_UNSUPPORTED, "op %d: kind %d not implemented by the fused scan", i, op.kind);
+        }
+    }
+    for (int p = 0; p < npreds; ++p) {
+        if (!pred_used[p]) continue;
+        const dq_predicate& pr = preds[p];
+        if (pr.code_len <= 0 || (pr.code_len & 1) || !pr.code)
+            return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: empty or odd-length program", p);
+        int depth = 0, maxd = 0;
+        for (int k = 0; k < pr.code_len; k += 2) {
+            const int op = pr.code[k], arg = pr.code[k + 1];
+            if (op == DQ_P_COL) {
+                if (!col_ok(arg)) return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: bad column %d", p, arg);
+                col_used[arg] = 1;
+                ++depth;
+            } else if (op == DQ_P_CONST || op == DQ_P_NULL) {
+                if (op == DQ_P_CONST && (arg < 0 || arg >= pr.n_consts)) return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: bad constant", p);
+                ++depth;
+            } else if (op == DQ_P_IN) {
+                depth -= arg;
+            } else if (op == DQ_P_COALESCE) {
+                depth -= arg - 1;
+            } else if (op == DQ_P_NOT || op == DQ_P_IS_NULL || op == DQ_P_IS_NOT_NULL || op == DQ_P_NEG ||
+                       op == DQ_P_LIKE || op == DQ_P_LENGTH || op == DQ_P_CAST_DOUBLE || op == DQ_P_CAST_LONG ||
+                       op == DQ_P_CAST_STRING_NUM) {
+                if (op == DQ_P_LIKE && (arg < 0 || arg >= pr.n_consts)) return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: bad LIKE pattern", p);
+            } else {
+                --depth;
+            }
+            if (depth < 1) return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: stack underflow", p);
+            maxd = std::max(maxd, depth);
+        }
+        if (depth != 1 || maxd > kPredStack) return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: malformed program", p);
+    }
+
+    // ---- plan: column uses -> slots -----------------------------------------------------------
+    struct Use { uint32_t flags = 0; int slot = -1; int pos = 0; int hll = -1; };
+    std::map<std::pair<int, int>, Use> uses;  // (column, where) -> use
+    for (int i = 0; i < nops; ++i) {
+        const dq_op& op = ops[i];
+        const auto key = std::make_pair(op.column[0], op.where);
+        switch (op.kind) {
+            case DQ_OP_MEAN: case DQ_OP_SUM: case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM: uses[key].flags |= CF_STATS; break;
+            case DQ_OP_STANDARD_DEVIATION: uses[key].flags |= CF_MOMENTS; break;
+            case DQ_OP_APPROX_COUNT_DISTINCT: uses[key].flags |= CF_HLL; break;
+            default: break;
+        }
+    }
+    std::vector<SlotDesc> slots;
+    auto new_slot = [&](int kind) {
+        SlotDesc sd;
+        memset(&sd, 0, sizeof(sd));
+        sd.kind = kind;
+        sd.col[0].hll_slot = sd.col[1].hll_slot = -1;
+        sd.col[0].elem = sd.col[1].elem = ET_NONE;
+        sd.rows_per_load = 8;
+        slots.push_back(sd);
+        return (int)slots.size() - 1;
+    };
+    struct PairKey { int x, y, w; bool operator<(const PairKey& o) const { return std::tie(x, y, w) < std::tie(o.x, o.y, o.w); } };
+    std::map<PairKey, int> pair_slots;  // (x, y, where) -> slot with corr
+    std::vector<std::pair<int, int>> op_slot(nops, {-1, 0});  // slot, colpos (corr: 1 = swapped)
+    // Correlation pairs first: fuse both columns' uses into one pair slot when element sizes match.
+    for (int i = 0; i < nops; ++i) {
+        const dq_op& op = ops[i];
+        if (op.kind != DQ_OP_CORRELATION) continue;
+        const int x = op.column[0], y = op.column[1], w = op.where;
+        auto it = pair_slots.find({x, y, w});
+        if (it != pair_slots.end()) { op_slot[i] = {it->second, 0}; continue; }
+        it = pair_slots.find({y, x, w});
+        if (it != pair_slots.end()) { op_slot[i] = {it->second, 1}; continue; }
+        const int ex = elem_of(columns[x].spark_type), ey = elem_of(columns[y].spark_type);
+        const int s = new_slot(SK_VALUES);
+        slots[s].ncols = 2;
+        slots[s].corr = 1;
+        slots[s].rows_per_load = elem_size(ex) == elem_size(ey) ? rows_per_load_of(ex) : 8;
+        slots[s].col[0].elem = ex;
+        slots[s].col[1].elem = ey;
+        if (x != y) {
+            auto ux = uses.find({x, w}), uy = uses.find({y, w});
+            if (ux != uses.end() && ux->second.slot < 0) { ux->second.slot = s; ux->second.pos = 0; }
+            if (uy != uses.end() && uy->second.slot < 0) { uy->second.slot = s; uy->second.pos = 1; }
+        }
+        slots[s].col[0].values = (const void*)(intptr_t)x;  // column index until pointers are known
+        slots[s].col[1].values = (const void*)(intptr_t)y;
+        slots[s].where_t = (const uint64_t*)(intptr_t)(w + 1);
+        pair_slots[{x, y, w}] = s;
+        op_slot[i] = {s, 0};
+    }
+    for (auto& kv : uses) {
+        if (kv.second.slot >= 0) continue;
+        const int c = kv.first.first, w = kv.first.second;
+        const int s = new_slot(SK_VALUES);
+        slots[s].ncols = 1;
+        slots[s].rows_per_load = rows_per_load_of(elem_of(columns[c].spark_type));
+        slots[s].col[0].elem = elem_of(columns[c].spark_type);
+        slots[s].col[0].values = (const void*)(intptr_t)c;
+        slots[s].where_t = (const uint64_t*)(intptr_t)(w + 1);
+        kv.second.slot = s;
+        kv.second.pos = 0;
+    }
+    int nhll = 0;
+    for (auto& kv : uses) {
+        SlotDesc& sd = slots[kv.second.slot];
+        sd.col[kv.second.pos].flags |= kv.second.flags;
+        if (kv.second.flags & CF_HLL) {
+            kv.second.hll = nhll++;
+            sd.col[kv.second.pos].hll_slot = kv.second.hll;
+        }
+    }
+    // Ops -> OpMap; bits-only slots for Size(where), Completeness of unread columns, Compliance.
+    std::vector<OpMap> opmap(nops);
+    std::map<std::tuple<int, int, int>, int> bits_slots;  // (kind, col/pred, where) -> slot
+    auto bits_slot = [&](int tag, int ref, int w) {
+        auto key = std::make_tuple(tag, ref, w);
+        auto it = bits_slots.find(key);
+        if (it != bits_slots.end()) return it->second;
+        const int s = new_slot(SK_BITS);
+        slots[s].where_t = (const uint64_t*)(intptr_t)(w + 1);
+        slots[s].col[0].values = (const void*)(intptr_t)ref;
+        slots[s].col[0].flags = (uint32_t)tag;  // 1 = completeness column, 2 = compliance predicate, 0 = size
+        bits_slots[key] = s;
+        return s;
+    };
+    for (int i = 0; i < nops; ++i) {
+        const dq_op& op = ops[i];
+        OpMap& m = opmap[i];
+        memset(&m, 0, sizeof(m));
+        m.kind = op.kind;
+        m.slot = -1;
+        m.hll_slot = -1;
+        m.has_where = op.where >= 0;
+        m.nrows = nrows;
+        const int c = op.column[0];
+        if (op.kind != DQ_OP_SIZE && op.kind != DQ_OP_COMPLIANCE && col_ok(c)) {
+            const int t = columns[c].spark_type;
+            m.is_float = (t == DQ_TYPE_FLOAT || t == DQ_TYPE_DOUBLE);
+            m.decimal_scale = t == DQ_TYPE_DECIMAL ? columns[c].decimal_scale : 0;
+        }
+        switch (op.kind) {
+            case DQ_OP_SIZE:
+                if (op.where >= 0) m.slot = bits_slot(0, -1, op.where);
+                break;
+            case DQ_OP_COMPLIANCE:
+                m.slot = bits_slot(2, op.predicate, op.where);
+                break;
+            case DQ_OP_COMPLETENESS: {
+                auto it = uses.find({c, op.where});
+                if (it != uses.end()) {
+                    m.slot = it->second.slot;
+                    m.colpos = it->second.pos;
+                } else if (columns[c].validity == nullptr) {
+                    m.from_bits = 2;  // all rows valid: matches = conditionalCount
+                    if (op.where >= 0) m.slot = bits_slot(0, -1, op.where);
+                } else {
+                    m.slot = bits_slot(1, c, op.where);
+                    m.from_bits = 1;
+                }
+                break;
+            }
+            case DQ_OP_CORRELATION:
+                m.slot = op_slot[i].first;
+                m.colpos = op_slot[i].second;
+                break;
+            default: {
+                const Use& u = uses.at({c, op.where});
+                m.slot = u.slot;
+                m.colpos = u.pos;
+                m.hll_slot = u.hll;
+                break;
+            }
+        }
+    }
+    const int nslots = (int)slots.size();
+    if (nslots > kMaxSlots) return fail(ctx, DQ_ERR_UNSUPPORTED, "too many slots (%d)", nslots);
+
+    // ---- device memory layout -----------------------------------------------------------------
+    // Launch groups: one kernel launch per slot shape; each gets a grid sized to fill the chip once.
+    const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+    struct Group { int kind, P, nc; bool f0, f1; int grid; std::vector<int32_t> slots; };
+    std::vector<Group> groups;
+    auto shape_key = [](int kind, int P, int nc, bool f0, bool f1) { return ((((kind * 16 + P) * 4 + nc) * 2 + f0) * 2 + f1); };
+    std::map<int, int> group_of;
+    for (int s = 0; s < (int)slots.size(); ++s) {
+        const SlotDesc& sd = slots[s];
+        const bool f0 = sd.kind == SK_VALUES && (sd.col[0].elem == ET_F32 || sd.col[0].elem == ET_F64);
+        const bool f1 = sd.kind == SK_VALUES && sd.ncols > 1 && (sd.col[1].elem == ET_F32 || sd.col[1].elem == ET_F64);
+        const int P = sd.kind == SK_VALUES ? sd.rows_per_load : 8;
+        const int nc = sd.kind == SK_VALUES ? sd.ncols : 1;
+        const int key = shape_key(sd.kind, P, nc, f0, f1);
+        auto it = group_of.find(key);
+        if (it == group_of.end()) {
+            int occ;
+            auto oc = ctx->occupancy.find(key);
+            if (oc != ctx->occupancy.end()) occ = oc->second;
+            else occ = ctx->occupancy[key] = std::max(1, scan_group_blocks_per_cu(sd.kind, P, nc, f0, f1));
+            const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(ntiles, 1), (int64_t)ctx->cus * occ));
+            groups.push_back(Group{sd.kind, P, nc, f0, f1, (int)grid, {}});
+            it = group_of.emplace(key, (int)groups.size() - 1).first;
+        }
+        groups[it->second].slots.push_back(s);
+    }
+    int gstride = 1;
+    for (const Group& g : groups) gstride = std::max(gstride, g.grid);
+    std::vector<int32_t> slot_nblocks(std::max<size_t>(slots.size(), 1), 1);
+    for (const Group& g : groups)
+        for (int32_t s : g.slots) slot_nblocks[s] = g.grid;
+    std::vector<int32_t> hll_nblocks(std::max(nhll, 1), 1);
+    for (const auto& kv : uses)
+        if (kv.second.hll >= 0) hll_nblocks[kv.second.hll] = slot_nblocks[kv.second.slot];
+    const int64_t pwords = padded_words_for(nrows);
+    const size_t bitmap_bytes = (size_t)(nrows + 7) / 8;
+
+    std::vector<const void*> dval(ncols, nullptr), dvalid(ncols, nullptr), doffs(ncols, nullptr);
+    size_t arena_need = 0;
+    std::vector<size_t> stage_off(ncols, 0);
+    int npred_used = 0;
+    for (int p = 0; p < npreds; ++p) npred_used += pred_used[p];
+    for (int pass = 0; pass < 2; ++pass) {
+        Bump b;
+        b.base = pass ? ctx->arena : nullptr;
+        for (int c = 0; c < ncols; ++c) {
+            const dq_column& col = columns[c];
+            if (!col_used[c]) continue;
+            if (col.flags & DQ_COL_DEVICE) {
+                dval[c] = col.values;
+                dvalid[c] = col.validity;
+                doffs[c] = col.offsets;
+                continue;
+            }
+            size_t vbytes;
+            if (col.spark_type == DQ_TYPE_STRING) vbytes = nrows > 0 ? (size_t)col.offsets[nrows] : 0;
+            else vbytes = (size_t)nrows * elem_size(elem_of(col.spark_type));
+            void* v = b.take(vbytes + 16);
+            void* vd = col.validity ? b.take(align_up(bitmap_bytes, 8) + 8) : nullptr;
+            void* od = col.spark_type == DQ_TYPE_STRING ? b.take(((size_t)nrows + 1) * 4) : nullptr;
+            if (pass) {
+                if (vbytes) DQ_HIP(ctx, hipMemcpyAsync(v, col.values, vbytes, hipMemcpyHostToDevice, ctx->stream));
+                if (vd && bitmap_bytes) DQ_HIP(ctx, hipMemcpyAsync(vd, col.validity, bitmap_bytes, hipMemcpyHostToDevice, ctx->stream));
+                if (od) DQ_HIP(ctx, hipMemcpyAsync(od, col.offsets, ((size_t)nrows + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+                dval[c] = v;
+                dvalid[c] = col.validity ? vd : nullptr;
+                doffs[c] = od;
+            }
+        }
+        // predicate outputs + programs
+        std::vector<uint64_t*> pt(npreds, nullptr), pn(npreds, nullptr);
+        for (int p = 0; p < npreds; ++p) {
+            if (!pred_used[p]) continue;
+            pt[p] = (uint64_t*)b.take((size_t)pwords * 8);
+            pn[p] = (uint64_t*)b.take((size_t)pwords * 8);
+        }
+        void* pcols = b.take(sizeof(PredColumn) * std::max(ncols, 1));
+        std::vector<void*> pprog(npreds, nullptr), pcode(npreds, nullptr), pconst(npreds, nullptr), pstr(npreds, nullptr);
+        for (int p = 0; p < npreds; ++p) {
+            if (!pred_used[p]) continue;
+            pprog[p] = b.take(sizeof(PredProgram));
+            pcode[p] = b.take(sizeof(int32_t) * preds[p].code_len);
+            pconst[p] = b.take(sizeof(dq_const) * std::max(preds[p].n_consts, 1));
+            pstr[p] = b.take(std::max<int64_t>(preds[p].strings_len, 1));
+        }
+        SlotDesc* dslots = (SlotDesc*)b.take(sizeof(SlotDesc) * std::max(nslots, 1));
+        OpMap* dops = (OpMap*)b.take(sizeof(OpMap) * nops);
+        SlotPartial* partials = (SlotPartial*)b.take(sizeof(SlotPartial) * (size_t)std::max(nslots, 1) * gstride);
+        int32_t* dgroups = (int32_t*)b.take(sizeof(int32_t) * std::max(nslots, 1));
+        int32_t* dslot_nb = (int32_t*)b.take(sizeof(int32_t) * slot_nblocks.size());
+        int32_t* dhll_nb = (int32_t*)b.take(sizeof(int32_t) * hll_nblocks.size());
+        SlotPartial* finals = (SlotPartial*)b.take(sizeof(SlotPartial) * std::max(nslots, 1));
+        uint8_t* hllp = (uint8_t*)b.take((size_t)std::max(nhll, 1) * gstride * kHllRegs);
+        uint8_t* hllf = (uint8_t*)b.take((size_t)std::max(nhll, 1) * kHllRegs);
+        dq_state* dout = (flags & DQ_SCAN_OUT_DEVICE) ? out : (dq_state*)b.take(sizeof(dq_state) * nops);
+        if (!pass) {
+            arena_need = b.off;
+            int rc = ensure_arena(ctx, arena_need);
+            if (rc) return rc;
+            // plan bytes uploaded through pinned staging
+            size_t pin = sizeof(PredColumn) * std::max(ncols, 1) + sizeof(SlotDesc) * std::max(nslots, 1) +
+                         sizeof(OpMap) * nops + sizeof(dq_state) * nops + 4 * (slot_nblocks.size() + hll_nblocks.size() + nslots) + 8192;
+            for (int p = 0; p < npreds; ++p)
+                if (pred_used[p])
+                    pin += sizeof(PredProgram) + sizeof(int32_t) * preds[p].code_len +
+                           sizeof(dq_const) * std::max(preds[p].n_consts, 1) + std::max<int64_t>(preds[p].strings_len, 1) + 256;
+            rc = ensure_pinned(ctx, pin);
+            if (rc) return rc;
+            continue;
+        }
+        // ---- pass 1: fill descriptors, upload, launch ------------------------------------------
+        // The pinned buffer may still be read by a previous call's async copies: wait for them.
+        DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        Bump hb;
+        hb.base = ctx->pinned;
+        auto upload = [&](void* dst, const void* src, size_t n) -> int {
+            void* h = hb.take(n, 16);
+            memcpy(h, src, n);
+            DQ_HIP(ctx, hipMemcpyAsync(dst, h, n, hipMemcpyHostToDevice, ctx->stream));
+            return DQ_OK;
+        };
+        if (npred_used) {
+            std::vector<PredColumn> pc(std::max(ncols, 1));
+            for (int c = 0; c < ncols; ++c) {
+                memset(&pc[c], 0, sizeof(PredColumn));
+                pc[c].values = dval[c];
+                pc[c].validity = (const uint64_t*)dvalid[c];
+                pc[c].offsets = (const int32_t*)doffs[c];
+                pc[c].spark_type = columns[c].spark_type;
+                pc[c].elem = elem_of(columns[c].spark_type);
+                pc[c].decimal_scale = columns[c].decimal_scale;
+            }
+            int rc = upload(pcols, pc.data(), sizeof(PredColumn) * pc.size());
+            if (rc) return rc;
+            for (int p = 0; p < npreds; ++p) {
+                if (!pred_used[p]) continue;
+                const dq_predicate& pr = preds[p];
+                rc = upload(pcode[p], pr.code, sizeof(int32_t) * pr.code_len);
+                if (rc) return rc;
+                if (pr.n_consts > 0) {
+                    rc = upload(pconst[p], pr.consts, sizeof(dq_const) * pr.n_consts);
+                    if (rc) return rc;
+                }
+                if (pr.strings_len > 0) {
+                    rc = upload(pstr[p], pr.strings, (size_t)pr.strings_len);
+                    if (rc) return rc;
+                }
+                PredProgram pg;
+                pg.code = (const int32_t*)pcode[p];
+                pg.consts = (const dq_const*)pconst[p];
+                pg.strings = (const uint8_t*)pstr[p];
+                pg.code_len = pr.code_len;
+                pg.n_consts = pr.n_consts;
+                rc = upload(pprog[p], &pg, sizeof(pg));
+                if (rc) return rc;
+                launch_predicate((const PredProgram*)pprog[p], (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p], ctx->stream);
+                DQ_HIP(ctx, hipGetLastError());
+            }
+        }
+        // resolve slot descriptors
+        for (int s = 0; s < nslots; ++s) {
+            SlotDesc& sd = slots[s];
+            const int w = (int)(intptr_t)sd.where_t - 1;
+            sd.where_t = w >= 0 ? pt[w] : nullptr;
+            sd.where_nn = w >= 0 ? pn[w] : nullptr;
+            if (sd.kind == SK_VALUES) {
+                for (int k = 0; k < sd.ncols; ++k) {
+                    const int c = (int)(intptr_t)sd.col[k].values;
+                    sd.col[k].values = dval[c];
+                    sd.col[k].validity = (const uint64_t*)dvalid[c];
+                    sd.col[k].spark_type = columns[c].spark_type;
+                    sd.col[k].elem = elem_of(columns[c].spark_type);
+                }
+            } else {
+                const int tag = (int)sd.col[0].flags;
+                const int ref = (int)(intptr_t)sd.col[0].values;
+                memset(&sd.col[0], 0, sizeof(ColDesc));
+                sd.col[0].hll_slot = -1;
+                sd.ncols = 1;
+                if (tag == 1) sd.bits_valid = (const uint64_t*)dvalid[ref];
+                if (tag == 2) { sd.pred_t = pt[ref]; sd.pred_nn = pn[ref]; }
+            }
+        }
+        int rc = nslots ? upload(dslots, slots.data(), sizeof(SlotDesc) * nslots) : DQ_OK;
+        if (rc) return rc;
+        rc = upload(dops, opmap.data(), sizeof(OpMap) * nops);
+        if (rc) return rc;
+        if (nslots) {
+            std::vector<int32_t> order;
+            for (const Group& g : groups) order.insert(order.end(), g.slots.begin(), g.slots.end());
+            rc = upload(dgroups, order.data(), sizeof(int32_t) * order.size());
+            if (rc) return rc;
+            rc = upload(dslot_nb, slot_nblocks.data(), sizeof(int32_t) * slot_nblocks.size());
+            if (rc) return rc;
+            rc = upload(dhll_nb, hll_nblocks.data(), sizeof(int32_t) * hll_nblocks.size());
+            if (rc) return rc;
+            size_t off = 0;
+            for (const Group& g : groups) {
+                if (launch_scan_group(g.kind, g.P, g.nc, g.f0, g.f1, dslots, dgroups + off, (int)g.slots.size(), nrows,
+                                      ntiles, gstride, g.grid, partials, hllp, ctx->stream) != 0)
+                    return fail(ctx, DQ_ERR_DEVICE, "scan launch failed for shape (%d,%d,%d)", g.kind, g.P, g.nc);
+                DQ_HIP(ctx, hipGetLastError());
+                off += g.slots.size();
+            }
+            ctx->scan_launches++;
+            launch_reduce_partials(partials, dslot_nb, nslots, gstride, finals, ctx->stream);
+            DQ_HIP(ctx, hipGetLastError());
+            launch_reduce_hll(hllp, dhll_nb, nhll, gstride, hllf, ctx->stream);
+            DQ_HIP(ctx, hipGetLastError());
+        }
+        launch_finalize(dops, nops, finals, hllf, dout, ctx->stream);
+        DQ_HIP(ctx, hipGetLastError());
+        if (!(flags & DQ_SCAN_OUT_DEVICE)) {
+            void* h = hb.take(sizeof(dq_state) * nops, 16);
+            DQ_HIP(ctx, hipMemcpyAsync(h, dout, sizeof(dq_state) * nops, hipMemcpyDeviceToHost, ctx->stream));
+            DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            memcpy(out, h, sizeof(dq_state) * nops);
+        } else {
+            // Host columns were staged into the arena: keep them alive until the kernels finish.
+            bool staged = false;
+            for (int c = 0; c < ncols; ++c) staged |= col_used[c] && !(columns[c].flags & DQ_COL_DEVICE);
+            if (staged) DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        }
+    }
+    return DQ_OK;
+}
+
+int dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out) {
+    if (!a || !b || !out || a->kind != b->kind) return DQ_ERR_INVALID_ARGUMENT;
+    // Analyzers.merge (A/Analyzer.scala:367-386): None is the identity.
+    if (!a->present) { *out = *b; return DQ_OK; }
+    if (!b->present) { *out = *a; return DQ_OK; }
+    dq_state r = *a;
+    switch (a->kind) {
+        case DQ_OP_SIZE:
+            r.u.num_matches.num_matches = a->u.num_matches.num_matches + b->u.num_matches.num_matches;
+            break;
+        case DQ_OP_COMPLETENESS:
+        case DQ_OP_COMPLIANCE:
+            r.u.num_matches_and_count.num_matches += b->u.num_matches_and_count.num_matches;
+            r.u.num_matches_and_count.count += b->u.num_matches_and_count.count;
+            break;
+        case DQ_OP_MEAN:
+            r.u.mean.sum = a->u.mean.sum + b->u.mean.sum;
+            r.u.mean.count = a->u.mean.count + b->u.mean.count;
+            break;
+        case DQ_OP_SUM:
+            r.u.dbl.value = a->u.dbl.value + b->u.dbl.value;
+            break;
+        case DQ_OP_MINIMUM:
+        case DQ_OP_MIN_LENGTH:
+            r.u.dbl.value = java_math_min(a->u.dbl.value, b->u.dbl.value);
+            break;
+        case DQ_OP_MAXIMUM:
+        case DQ_OP_MAX_LENGTH:
+            r.u.dbl.value = java_math_max(a->u.dbl.value, b->u.dbl.value);
+            break;
+        case DQ_OP_STANDARD_DEVIATION: {  // A/StandardDeviation.scala:37-44
+            const double n = a->u.stddev.n, on = b->u.stddev.n;
+            const double newN = n + on;
+            const double delta = b->u.stddev.avg - a->u.stddev.avg;
+            const double deltaN = newN == 0.0 ? 0.0 : delta / newN;
+            r.u.stddev.n = newN;
+            r.u.stddev.avg = a->u.stddev.avg + deltaN * on;
+            r.u.stddev.m2 = a->u.stddev.m2 + b->u.stddev.m2 + delta * deltaN * n * on;
+            break;
+        }
+        case DQ_OP_CORRELATION: {  // A/Correlation.scala:37-52
+            const double n1 = a->u.corr.n, n2 = b->u.corr.n, newN = n1 + n2;
+            const double dx = b->u.corr.x_avg - a->u.corr.x_avg;
+            const double dxN = newN == 0.0 ? 0.0 : dx / newN;
+            const double dy = b->u.corr.y_avg - a->u.corr.y_avg;
+            const double dyN = newN == 0.0 ? 0.0 : dy / newN;
+            r.u.corr.n = newN;
+            r.u.corr.x_avg = a->u.corr.x_avg + dxN * n2;
+            r.u.corr.y_avg = a->u.corr.y_avg + dyN * n2;
+            r.u.corr.ck = a->u.corr.ck + b->u.corr.ck + dx * dyN * n1 * n2;
+            r.u.corr.x_mk = a->u.corr.x_mk + b->u.corr.x_mk + dx * dxN * n1 * n2;
+            r.u.corr.y_mk = a->u.corr.y_mk + b->u.corr.y_mk + dy * dyN * n1 * n2;
+            break;
+        }
+        case DQ_OP_APPROX_COUNT_DISTINCT:
+            hll_merge_words(a->u.hll.words, b->u.hll.words, r.u.hll.words);
+            break;
+        case DQ_OP_DATATYPE:
+            r.u.datatype.num_null += b->u.datatype.num_null;
+            r.u.datatype.num_fractional += b->u.datatype.num_fractional;
+            r.u.datatype.num_integral += b->u.datatype.num_integral;
+            r.u.datatype.num_boolean += b->u.datatype.num_boolean;
+            r.u.datatype.num_string += b->u.datatype.num_string;
+            break;
+        default:
+            return DQ_ERR_UNSUPPORTED;
+    }
+    *out = r;
+    return DQ_OK;
+}
+
+// DeequHyperLogLogPlusPlusUtils.estimateBias (C/StatefulHyperloglogPlus.scala:259-297), P = 9, K = 6.
+static double hll_estimate_bias(double e) {
+    const double* est = DQ_HLL_P9_RAW;
+    const int num = DQ_HLL_P9_N;
+    // java.util.Arrays.binarySearch: index if found, else -(insertion point) - 1 -> insertion point
+    int lo = 0, hi = num - 1, nearest = -1;
+    while (lo <= hi) {
+        const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
+        const double mv = est[mid];
+        if (mv < e) lo = mid + 1;
+        else if (mv > e) hi = mid - 1;
+        else {
+            // Double.compare semantics; the table holds no NaN / signed zeros.
+            nearest = mid;
+            break;
+        }
+    }
+    if (nearest < 0) nearest = lo;
+    auto distance = [&](int i) {
+        const double d = e - est[i];
+        return d * d;
+    };
+    const int K = 6;
+    int low = std::max(nearest - K + 1, 0);
+    int high = std::min(low + K, num);
+    while (high < num && distance(high) < distance(low)) {
+        ++low;
+        ++high;
+    }
+    double bias = 0.0;
+    for (int i = low; i < high; ++i) bias += DQ_HLL_P9_BIAS[i];
+    return bias / (high - low);
+}
+
+double dq_hll_count(const int64_t words[DQ_HLL_NUM_WORDS]) {
+    const int P = 9, M = 512;
+    const double alphaM2 = (0.7213 / (1.0 + 1.079 / M)) * M * M;
+    double zInverse = 0.0, V = 0.0;
+    int idx = 0;
+    for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) {
+        const uint64_t word = (uint64_t)words[w];
+        int shift = 0;
+        for (int i = 0; idx < M && i < 10; ++i, ++idx, shift += 6) {
+            const int64_t Midx = (int64_t)((word >> shift) & 63u);
+            // Scala `1 << Midx` on an Int: JVM shift distance is Midx & 31, result is a 32-bit int.
+            const int32_t pow2 = (int32_t)((uint32_t)1u << (Midx & 31));
+            zInverse += 1.0 / (double)pow2;
+            if (Midx == 0) V += 1.0;
+        }
+    }
+    auto corrected = [&]() {
+        const double e = alphaM2 / zInverse;
+        return (P < 19 && e < 5.0 * M) ? e - hll_estimate_bias(e) : e;
+    };
+    double estimate;
+    if (V > 0) {
+        const double H = M * log(M / V);
+        estimate = H <= DQ_HLL_P9_THRESHOLD ? H : corrected();
+    } else {
+        estimate = corrected();
+    }
+    // Math.round(double): floor(x + 0.5) as a long
+    return (double)(int64_t)floor(estimate + 0.5);
+}
+
+int64_t dq_spark_hash64(int32_t spark_type, const void* value, int64_t len) {
+    if (!value) return 0;
+    switch (spark_type) {
+        case DQ_TYPE_BOOLEAN: return (int64_t)xxh_int(*(const uint8_t*)value ? 1u : 0u, SPARK_HLL_SEED);
+        case DQ_TYPE_BYTE: return (int64_t)xxh_int((uint32_t)(int32_t)*(const int8_t*)value, SPARK_HLL_SEED);
+        case DQ_TYPE_SHORT: return (int64_t)xxh_int((uint32_t)(int32_t)*(const int16_t*)value, SPARK_HLL_SEED);
+        case DQ_TYPE_INT:
+        case DQ_TYPE_DATE: return (int64_t)xxh_int((uint32_t)*(const int32_t*)value, SPARK_HLL_SEED);
+        case DQ_TYPE_LONG:
+        case DQ_TYPE_TIMESTAMP:
+        case DQ_TYPE_DECIMAL: return (int64_t)xxh_long((uint64_t)*(const int64_t*)value, SPARK_HLL_SEED);
+        case DQ_TYPE_FLOAT: return (int64_t)xxh_int(float_to_int_bits(*(const float*)value), SPARK_HLL_SEED);
+        case DQ_TYPE_DOUBLE: return (int64_t)xxh_long(double_to_long_bits(*(const double*)value), SPARK_HLL_SEED);
+        case DQ_TYPE_STRING: return (int64_t)xxh_bytes((const uint8_t*)value, len, SPARK_HLL_SEED);
+        default: return 0;
+    }
+}
+
+int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int64_t nrows, void* values_dev) {
+    if (!ctx || nrows < 0 || (!values_dev && nrows > 0) || kind < DQ_SYNTH_DYADIC || kind > DQ_SYNTH_GAUSS01)
+        return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_synth_column: invalid arguments");
+    if (nrows == 0) return DQ_OK;
+    DQ_HIP(ctx, hipSetDevice(ctx->device));
+    launch_synth_column(kind, seed, row0, nrows, values_dev, ctx->stream);
+    DQ_HIP(ctx, hipGetLastError());
+    return DQ_OK;
+}
+
+int dq_synth_validity(dq_ctx* ctx, uint64_t seed, int64_t row0, int64_t nrows, int32_t null_permille, uint8_t* validity_dev) {
+    if (!ctx || nrows < 0 || (!validity_dev && nrows > 0) || null_permille < 0 || null_permille > 1000)
+        return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_synth_validity: invalid arguments");
+    if (nrows == 0) return DQ_OK;
+    DQ_HIP(ctx, hipSetDevice(ctx->device));
+    launch_synth_validity(seed, row0, nrows, null_permille, validity_dev, ctx->stream);
+    DQ_HIP(ctx, hipGetLastError());
+    return DQ_OK;
+}
+
+}  // extern "C"

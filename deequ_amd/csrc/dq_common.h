@@ -1,0 +1,145 @@
+// dq_common.h — host+device helpers shared by the HIP kernels and the host runtime.
+//
+// Spark's XXH64 (org.apache.spark.sql.catalyst.expressions.XXH64, spark-catalyst 2.2.2, called by
+// XxHash64Function.hash in C/StatefulHyperloglogPlus.scala:93) is the standard XXH64 over the
+// little-endian bytes of the value; hashInt/hashLong are its 4- and 8-byte specialisations.
+// The counter-based splitmix64 generator defines the synthetic BASELINE inputs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DQ_HD __host__ __device__ __forceinline__
+
+namespace dq {
+
+constexpr uint64_t P64_1 = 0x9E3779B185EBCA87ULL;
+constexpr uint64_t P64_2 = 0xC2B2AE3D27D4EB4FULL;
+constexpr uint64_t P64_3 = 0x165667B19E3779F9ULL;
+constexpr uint64_t P64_4 = 0x85EBCA77C2B2AE63ULL;
+constexpr uint64_t P64_5 = 0x27D4EB2F165667C5ULL;
+constexpr uint64_t SPARK_HLL_SEED = 42;  // C/StatefulHyperloglogPlus.scala:93
+
+DQ_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+DQ_HD uint64_t xxh_fmix(uint64_t h) {
+    h ^= h >> 33;
+    h *= P64_2;
+    h ^= h >> 29;
+    h *= P64_3;
+    h ^= h >> 32;
+    return h;
+}
+
+// XXH64.hashInt: 4-byte input.
+DQ_HD uint64_t xxh_int(uint32_t v, uint64_t seed) {
+    uint64_t h = seed + P64_5 + 4ULL;
+    h ^= (uint64_t)v * P64_1;
+    h = rotl64(h, 23) * P64_2 + P64_3;
+    return xxh_fmix(h);
+}
+
+// XXH64.hashLong: 8-byte input.
+DQ_HD uint64_t xxh_long(uint64_t v, uint64_t seed) {
+    uint64_t h = seed + P64_5 + 8ULL;
+    h ^= rotl64(v * P64_2, 31) * P64_1;
+    h = rotl64(h, 27) * P64_1 + P64_4;
+    return xxh_fmix(h);
+}
+
+DQ_HD uint64_t load_le64(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+}
+DQ_HD uint32_t load_le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+DQ_HD uint64_t xxh_round(uint64_t acc, uint64_t input) {
+    acc += input * P64_2;
+    acc = rotl64(acc, 31);
+    return acc * P64_1;
+}
+DQ_HD uint64_t xxh_merge_round(uint64_t acc, uint64_t val) {
+    val = xxh_round(0, val);
+    acc ^= val;
+    return acc * P64_1 + P64_4;
+}
+
+// XXH64.hashUnsafeBytes: arbitrary byte string (UTF-8 strings, binary).
+DQ_HD uint64_t xxh_bytes(const uint8_t* p, int64_t len, uint64_t seed) {
+    const uint8_t* end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        const uint8_t* limit = end - 32;
+        uint64_t v1 = seed + P64_1 + P64_2, v2 = seed + P64_2, v3 = seed, v4 = seed - P64_1;
+        do {
+            v1 = xxh_round(v1, load_le64(p));
+            v2 = xxh_round(v2, load_le64(p + 8));
+            v3 = xxh_round(v3, load_le64(p + 16));
+            v4 = xxh_round(v4, load_le64(p + 24));
+            p += 32;
+        } while (p <= limit);
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = xxh_merge_round(h, v1);
+        h = xxh_merge_round(h, v2);
+        h = xxh_merge_round(h, v3);
+        h = xxh_merge_round(h, v4);
+    } else {
+        h = seed + P64_5;
+    }
+    h += (uint64_t)len;
+    while (p + 8 <= end) {
+        h ^= xxh_round(0, load_le64(p));
+        h = rotl64(h, 27) * P64_1 + P64_4;
+        p += 8;
+    }
+    if (p + 4 <= end) {
+        h ^= (uint64_t)load_le32(p) * P64_1;
+        h = rotl64(h, 23) * P64_2 + P64_3;
+        p += 4;
+    }
+    while (p < end) {
+        h ^= (uint64_t)(*p) * P64_5;
+        h = rotl64(h, 11) * P64_1;
+        ++p;
+    }
+    return xxh_fmix(h);
+}
+
+// java.lang.Double.doubleToLongBits / Float.floatToIntBits: NaN canonicalised.
+DQ_HD uint64_t double_to_long_bits(double d) {
+    if (d != d) return 0x7ff8000000000000ULL;
+    union { double d; uint64_t u; } c;
+    c.d = d;
+    return c.u;
+}
+DQ_HD uint32_t float_to_int_bits(float f) {
+    if (f != f) return 0x7fc00000U;
+    union { float f; uint32_t u; } c;
+    c.f = f;
+    return c.u;
+}
+
+// HLL++ register update inputs (C/StatefulHyperloglogPlus.scala:96-100, P = 9):
+// idx = x >>> 55; pw = numberOfLeadingZeros((x << 9) | 1 << 8) + 1.
+DQ_HD uint32_t hll_index(uint64_t x) { return (uint32_t)(x >> 55); }
+DQ_HD uint32_t hll_rank(uint64_t x) {
+    uint64_t w = (x << 9) | (1ULL << 8);
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)__clzll((long long)w) + 1u;
+#else
+    return (uint32_t)__builtin_clzll(w) + 1u;
+#endif
+}
+
+// Counter-based splitmix64: output i of the stream seeded by `seed`.
+DQ_HD uint64_t splitmix64(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+}  // namespace dq

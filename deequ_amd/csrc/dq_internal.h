@@ -1,0 +1,173 @@
+// dq_internal.h — layouts shared by the host runtime (dq_api.cpp) and the HIP kernels.
+//
+// The fused scan works on "slots". A slot is one pass over one or two columns (two for a
+// Correlation pair) under one `where` mask, or a bits-only pass over validity/predicate bitmaps
+// (Size(where), Completeness of an otherwise unread column, Compliance). Every op of the batch
+// is answered from the final slot partial it maps to (OpMap), so every column is read once.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dq.h"
+
+namespace dq {
+
+constexpr int kBlock = 256;          // threads per workgroup (4 wave64)
+constexpr int kRowsPerThread = 8;    // rows per thread per tile
+constexpr int kTileRows = kBlock * kRowsPerThread;  // 2048 rows = 32 bitmap words per tile
+constexpr int kMaxSlots = 256;
+constexpr int kHllRegs = 512;
+
+// Element storage classes of the fused scan.
+enum ElemType : int32_t {
+    ET_U8 = 0,   // BOOLEAN
+    ET_I8 = 1,   // BYTE
+    ET_I16 = 2,  // SHORT
+    ET_I32 = 3,  // INT, DATE
+    ET_I64 = 4,  // LONG, TIMESTAMP, DECIMAL (unscaled)
+    ET_F32 = 5,  // FLOAT
+    ET_F64 = 6,  // DOUBLE
+    ET_NONE = 7
+};
+
+enum ColFlags : uint32_t {
+    CF_STATS = 1u,    // count/sum/min/max (+ NaN count)
+    CF_MOMENTS = 2u,  // (n, avg, m2) Welford/Chan state
+    CF_HLL = 4u,      // HLL++ registers
+};
+
+// Row mapping inside a 2048-row tile: L loads of P consecutive rows per thread, L * P = 8.
+// Striped (coalesced) for a single element size; pairs of different sizes use P = 8.
+struct ColDesc {
+    const void* values;
+    const uint64_t* validity;  // nullptr = all valid
+    int32_t spark_type;
+    int32_t elem;              // ElemType
+    uint32_t flags;            // ColFlags
+    int32_t hll_slot;          // index into the HLL partial arrays, -1 = none
+};
+
+enum SlotKind : int32_t { SK_VALUES = 0, SK_BITS = 1 };
+
+struct SlotDesc {
+    ColDesc col[2];
+    const uint64_t* where_t;   // where evaluated TRUE   (padded bitmap) or nullptr
+    const uint64_t* where_nn;  // where evaluated NOT NULL
+    const uint64_t* pred_t;    // SK_BITS: predicate TRUE, or nullptr
+    const uint64_t* pred_nn;   // SK_BITS: predicate NOT NULL
+    const uint64_t* bits_valid;// SK_BITS: validity to count (Completeness), nullptr = none
+    int32_t kind;              // SlotKind
+    int32_t ncols;             // SK_VALUES: 1 or 2
+    int32_t corr;              // compute CorrelationState of (col0, col1)
+    int32_t rows_per_load;     // P: 2, 4 or 8
+};
+
+struct ColPartial {
+    int64_t n;     // valid & where-true rows
+    int64_t nnan;  // of which NaN (floating columns)
+    int64_t isum;  // integral sum (Spark LongType wrap-around)
+    int64_t imin, imax;
+    double dsum;
+    double dmin, dmax;  // NaN-free min/max (NaN handled through nnan, Spark orders NaN largest)
+    double mean, m2;    // Welford/Chan state over the same rows (n)
+};
+
+struct CorrPartial {
+    double n, xa, ya, ck, xm, ym;
+};
+
+struct SlotPartial {
+    ColPartial c[2];
+    CorrPartial corr;
+    int64_t wt;    // rows with where TRUE (or all rows if no where)
+    int64_t wnn;   // rows with where NOT NULL
+    int64_t pt;    // SK_BITS: rows with where TRUE and predicate TRUE
+    int64_t pnn;   // SK_BITS: rows with where TRUE and predicate NOT NULL
+    int64_t vt;    // SK_BITS: rows with where TRUE and bits_valid set
+    int64_t pad;
+};
+
+// How each op is answered from a final slot partial.
+struct OpMap {
+    int32_t kind;        // dq_op_kind
+    int32_t slot;        // slot index
+    int32_t colpos;      // 0/1 inside the slot
+    int32_t has_where;
+    int32_t is_float;    // column is FLOAT/DOUBLE
+    int32_t hll_slot;    // ApproxCountDistinct register set
+    int32_t decimal_scale;
+    int32_t from_bits;   // Completeness answered from a bits-only slot (vt) instead of c[colpos].n
+    int64_t nrows;       // count(*) of the batch
+};
+
+// Predicate VM limits.
+constexpr int kPredStack = 16;
+
+struct PredColumn {
+    const void* values;
+    const uint64_t* validity;
+    const int32_t* offsets;
+    int32_t spark_type;
+    int32_t elem;
+    int32_t decimal_scale;
+    int32_t pad;
+};
+
+struct PredProgram {
+    const int32_t* code;
+    const dq_const* consts;
+    const uint8_t* strings;
+    int32_t code_len;
+    int32_t n_consts;
+};
+
+inline int elem_of(int32_t spark_type) {
+    switch (spark_type) {
+        case DQ_TYPE_BOOLEAN: return ET_U8;
+        case DQ_TYPE_BYTE: return ET_I8;
+        case DQ_TYPE_SHORT: return ET_I16;
+        case DQ_TYPE_INT:
+        case DQ_TYPE_DATE: return ET_I32;
+        case DQ_TYPE_LONG:
+        case DQ_TYPE_TIMESTAMP:
+        case DQ_TYPE_DECIMAL: return ET_I64;
+        case DQ_TYPE_FLOAT: return ET_F32;
+        case DQ_TYPE_DOUBLE: return ET_F64;
+        default: return ET_NONE;
+    }
+}
+inline int elem_size(int e) {
+    switch (e) {
+        case ET_U8: case ET_I8: return 1;
+        case ET_I16: return 2;
+        case ET_I32: case ET_F32: return 4;
+        case ET_I64: case ET_F64: return 8;
+        default: return 0;
+    }
+}
+inline int rows_per_load_of(int e) {
+    int s = elem_size(e);
+    return s == 8 ? 2 : (s == 4 ? 4 : 8);
+}
+
+// Kernel launchers (defined in the .hip files).
+// One launch per slot shape (kind, P, column count, float/integral storage); each launch walks its
+// slots with tiles interleaved over `grid` workgroups and writes partials[slot * gstride + block].
+int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, const SlotDesc* slots, const int32_t* group,
+                      int ngroup, int64_t nrows, int64_t ntiles, int gstride, int grid, SlotPartial* partials,
+                      uint8_t* hll_partials, hipStream_t s);
+int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1);
+void launch_reduce_partials(const SlotPartial* partials, const int32_t* nblocks_of, int nslots, int gstride,
+                            SlotPartial* finals, hipStream_t s);
+void launch_reduce_hll(const uint8_t* hll_partials, const int32_t* nblocks_of, int nhll, int gstride,
+                       uint8_t* hll_final, hipStream_t s);
+void launch_finalize(const OpMap* ops, int nops, const SlotPartial* finals, const uint8_t* hll_final,
+                     dq_state* out, hipStream_t s);
+void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
+                      int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s);
+void launch_synth_column(int kind, uint64_t seed, int64_t row0, int64_t nrows, void* out, hipStream_t s);
+void launch_synth_validity(uint64_t seed, int64_t row0, int64_t nrows, int permille, uint8_t* out,
+                           hipStream_t s);
+
+}  // namespace dq

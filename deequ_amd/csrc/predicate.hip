@@ -1,0 +1,511 @@
+// predicate.hip — row predicates for `where` filters and Compliance (gfx950).
+//
+// deequ passes Spark SQL strings: `where` (conditionalSelection / conditionalCount,
+// A/Analyzer.scala:409-432) and Compliance predicates (A/Compliance.scala:49-52). The host
+// compiles them to a postfix program (dq_pred_opcode, include/dq.h); this kernel evaluates it for
+// one row per lane with SQL three-valued logic and emits two bitmaps per 64 rows via wave ballots:
+// TRUE rows and NOT-NULL rows. Rows past nrows (up to the padded length) get zero bits.
+// The program is wave-uniform, so every dispatch branch below is a uniform (scalar) branch.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include "dq_common.h"
+#include "dq_internal.h"
+
+namespace dq {
+
+namespace {
+
+struct Val {
+    int32_t tag;   // dq_value_tag
+    int32_t null;
+    int64_t i;     // BOOL / LONG
+    double d;      // DOUBLE
+    const uint8_t* s;
+    int32_t slen;
+};
+
+__device__ __forceinline__ Val vnull() {
+    Val v;
+    v.tag = DQ_V_BOOL;
+    v.null = 1;
+    v.i = 0;
+    v.d = 0.0;
+    v.s = nullptr;
+    v.slen = 0;
+    return v;
+}
+__device__ __forceinline__ Val vbool(bool b) {
+    Val v = vnull();
+    v.null = 0;
+    v.i = b ? 1 : 0;
+    return v;
+}
+__device__ __forceinline__ Val vlong(int64_t x) {
+    Val v = vnull();
+    v.tag = DQ_V_LONG;
+    v.null = 0;
+    v.i = x;
+    return v;
+}
+__device__ __forceinline__ Val vdouble(double x) {
+    Val v = vnull();
+    v.tag = DQ_V_DOUBLE;
+    v.null = 0;
+    v.d = x;
+    return v;
+}
+
+__device__ __forceinline__ bool is_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+__device__ const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                      1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// Spark Cast(string -> double): trimmed decimal literal, NULL when it does not parse.
+__device__ bool parse_double(const uint8_t* s, int n, double& out) {
+    int i = 0;
+    while (i < n && is_ws(s[i])) ++i;
+    while (n > i && is_ws(s[n - 1])) --n;
+    if (i >= n) return false;
+    bool neg = false;
+    if (s[i] == '+' || s[i] == '-') {
+        neg = s[i] == '-';
+        ++i;
+    }
+    uint64_t mant = 0;
+    int digits = 0, exp10 = 0, nd = 0;
+    bool seen_dot = false;
+    for (; i < n; ++i) {
+        const uint8_t c = s[i];
+        if (c >= '0' && c <= '9') {
+            ++nd;
+            if (digits < 19) {
+                mant = mant * 10 + (c - '0');
+                if (mant) ++digits;
+                if (seen_dot) --exp10;
+            } else if (!seen_dot) {
+                ++exp10;
+            }
+        } else if (c == '.' && !seen_dot) {
+            seen_dot = true;
+        } else {
+            break;
+        }
+    }
+    if (nd == 0) return false;
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+        ++i;
+        bool eneg = false;
+        if (i < n && (s[i] == '+' || s[i] == '-')) {
+            eneg = s[i] == '-';
+            ++i;
+        }
+        int e = 0, ed = 0;
+        for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i, ++ed) e = e < 10000 ? e * 10 + (s[i] - '0') : e;
+        if (ed == 0) return false;
+        exp10 += eneg ? -e : e;
+    }
+    if (i < n) {
+        // Java's parser accepts a trailing type suffix such as 'd' / 'f'.
+        if (i + 1 == n && (s[i] == 'd' || s[i] == 'D' || s[i] == 'f' || s[i] == 'F')) {
+        } else {
+            return false;
+        }
+    }
+    double v = (double)mant;
+    if (exp10 >= 0) {
+        while (exp10 > 22) { v *= 1e22; exp10 -= 22; }
+        v *= kPow10[exp10];
+    } else {
+        while (exp10 < -22) { v /= 1e22; exp10 += 22; }
+        v /= kPow10[-exp10];
+    }
+    out = neg ? -v : v;
+    return true;
+}
+
+__device__ bool parse_long(const uint8_t* s, int n, int64_t& out) {
+    int i = 0;
+    while (i < n && is_ws(s[i])) ++i;
+    while (n > i && is_ws(s[n - 1])) --n;
+    if (i >= n) return false;
+    bool neg = false;
+    if (s[i] == '+' || s[i] == '-') {
+        neg = s[i] == '-';
+        ++i;
+    }
+    if (i >= n) return false;
+    uint64_t v = 0;
+    for (; i < n; ++i) {
+        if (s[i] < '0' || s[i] > '9') break;
+        v = v * 10 + (s[i] - '0');
+    }
+    if (i < n) {
+        // Spark truncates a fractional part when casting "1.5" to long.
+        if (s[i] != '.') return false;
+        for (++i; i < n; ++i)
+            if (s[i] < '0' || s[i] > '9') return false;
+    }
+    out = neg ? -(int64_t)v : (int64_t)v;
+    return true;
+}
+
+__device__ __forceinline__ bool numeric(const Val& v) { return v.tag == DQ_V_LONG || v.tag == DQ_V_DOUBLE || v.tag == DQ_V_BOOL; }
+__device__ __forceinline__ double as_double(const Val& v) { return v.tag == DQ_V_DOUBLE ? v.d : (double)v.i; }
+
+// Spark's NaN-aware double ordering (NaN = NaN, NaN greatest).
+__device__ __forceinline__ int cmp_double(double a, double b) {
+    const bool an = a != a, bn = b != b;
+    if (an && bn) return 0;
+    if (an) return 1;
+    if (bn) return -1;
+    return a < b ? -1 : (a > b ? 1 : 0);
+}
+
+__device__ int cmp_bytes(const uint8_t* a, int na, const uint8_t* b, int nb) {
+    const int n = na < nb ? na : nb;
+    for (int i = 0; i < n; ++i)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+
+// Coerce a string operand against a numeric one the way Spark 2.x PromoteStrings does
+// (string -> double). Returns false when the string does not parse (comparison is NULL).
+__device__ bool compare(const Val& a, const Val& b, int& c) {
+    if (a.tag == DQ_V_STRING && b.tag == DQ_V_STRING) {
+        c = cmp_bytes(a.s, a.slen, b.s, b.slen);
+        return true;
+    }
+    if (a.tag == DQ_V_STRING || b.tag == DQ_V_STRING) {
+        double x, y;
+        if (a.tag == DQ_V_STRING) {
+            if (!parse_double(a.s, a.slen, x)) return false;
+        } else {
+            x = as_double(a);
+        }
+        if (b.tag == DQ_V_STRING) {
+            if (!parse_double(b.s, b.slen, y)) return false;
+        } else {
+            y = as_double(b);
+        }
+        c = cmp_double(x, y);
+        return true;
+    }
+    if (a.tag != DQ_V_DOUBLE && b.tag != DQ_V_DOUBLE) {
+        c = a.i < b.i ? -1 : (a.i > b.i ? 1 : 0);
+        return true;
+    }
+    c = cmp_double(as_double(a), as_double(b));
+    return true;
+}
+
+// SQL LIKE with % and _ over UTF-8 (one _ = one character); '\' escapes.
+__device__ bool like_match(const uint8_t* s, int ns, const uint8_t* p, int np) {
+    int si = 0, pi = 0, star_p = -1, star_s = 0;
+    while (si < ns) {
+        if (pi < np && p[pi] == '%') {
+            star_p = ++pi;
+            star_s = si;
+            continue;
+        }
+        if (pi < np) {
+            bool esc = p[pi] == '\\' && pi + 1 < np;
+            const uint8_t pc = esc ? p[pi + 1] : p[pi];
+            if (!esc && pc == '_') {
+                int len = 1;
+                const uint8_t c = s[si];
+                if (c >= 0xF0) len = 4;
+                else if (c >= 0xE0) len = 3;
+                else if (c >= 0xC0) len = 2;
+                si += len;
+                pi += 1;
+                continue;
+            }
+            if (pc == s[si]) {
+                si += 1;
+                pi += esc ? 2 : 1;
+                continue;
+            }
+        }
+        if (star_p >= 0) {
+            pi = star_p;
+            si = ++star_s;
+            continue;
+        }
+        return false;
+    }
+    while (pi < np && p[pi] == '%') ++pi;
+    return pi == np;
+}
+
+__device__ __forceinline__ int utf8_chars(const uint8_t* s, int n) {
+    int c = 0;
+    for (int i = 0; i < n; ++i) c += (s[i] & 0xC0) != 0x80;
+    return c;
+}
+
+__device__ Val load_col(const PredColumn& c, int64_t row) {
+    if (c.validity) {
+        const uint8_t* vb = reinterpret_cast<const uint8_t*>(c.validity);
+        if (!((vb[row >> 3] >> (row & 7)) & 1)) return vnull();
+    }
+    switch (c.spark_type) {
+        case DQ_TYPE_BOOLEAN: return vbool(static_cast<const uint8_t*>(c.values)[row] != 0);
+        case DQ_TYPE_BYTE: return vlong(static_cast<const int8_t*>(c.values)[row]);
+        case DQ_TYPE_SHORT: return vlong(static_cast<const int16_t*>(c.values)[row]);
+        case DQ_TYPE_INT:
+        case DQ_TYPE_DATE: return vlong(static_cast<const int32_t*>(c.values)[row]);
+        case DQ_TYPE_LONG:
+        case DQ_TYPE_TIMESTAMP: return vlong(static_cast<const int64_t*>(c.values)[row]);
+        case DQ_TYPE_DECIMAL: {
+            double d = (double)static_cast<const int64_t*>(c.values)[row];
+            for (int k = 0; k < c.decimal_scale; ++k) d /= 10.0;
+            return vdouble(d);
+        }
+        case DQ_TYPE_FLOAT: return vdouble((double)static_cast<const float*>(c.values)[row]);
+        case DQ_TYPE_DOUBLE: return vdouble(static_cast<const double*>(c.values)[row]);
+        case DQ_TYPE_STRING: {
+            Val v = vnull();
+            v.tag = DQ_V_STRING;
+            v.null = 0;
+            const int32_t o0 = c.offsets[row], o1 = c.offsets[row + 1];
+            v.s = static_cast<const uint8_t*>(c.values) + o0;
+            v.slen = o1 - o0;
+            return v;
+        }
+        default: return vnull();
+    }
+}
+
+__device__ Val arith(int op, const Val& a, const Val& b) {
+    if (a.null || b.null) return vnull();
+    Val x = a, y = b;
+    if (x.tag == DQ_V_STRING) {
+        double d;
+        if (!parse_double(x.s, x.slen, d)) return vnull();
+        x = vdouble(d);
+    }
+    if (y.tag == DQ_V_STRING) {
+        double d;
+        if (!parse_double(y.s, y.slen, d)) return vnull();
+        y = vdouble(d);
+    }
+    const bool integral = x.tag != DQ_V_DOUBLE && y.tag != DQ_V_DOUBLE;
+    switch (op) {
+        case DQ_P_ADD: return integral ? vlong((int64_t)((uint64_t)x.i + (uint64_t)y.i)) : vdouble(as_double(x) + as_double(y));
+        case DQ_P_SUB: return integral ? vlong((int64_t)((uint64_t)x.i - (uint64_t)y.i)) : vdouble(as_double(x) - as_double(y));
+        case DQ_P_MUL: return integral ? vlong((int64_t)((uint64_t)x.i * (uint64_t)y.i)) : vdouble(as_double(x) * as_double(y));
+        case DQ_P_DIV: {  // Spark `/` is fractional division; x / 0 is NULL
+            const double dy = as_double(y);
+            if (dy == 0.0) return vnull();
+            return vdouble(as_double(x) / dy);
+        }
+        case DQ_P_MOD:
+            if (integral) {
+                if (y.i == 0) return vnull();
+                return vlong(x.i % y.i);
+            } else {
+                const double dy = as_double(y);
+                if (dy == 0.0) return vnull();
+                return vdouble(fmod(as_double(x), dy));
+            }
+        default: return vnull();
+    }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(256)
+predicate_kernel(const PredProgram* __restrict__ progp, const PredColumn* __restrict__ cols, int64_t nrows,
+                 int64_t padded_words, uint64_t* __restrict__ out_t, uint64_t* __restrict__ out_nn) {
+    const PredProgram prog = *progp;
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool t = false, nn = false;
+    if (row < nrows) {
+        Val st[kPredStack];
+        int sp = 0;
+        for (int pc = 0; pc + 1 < prog.code_len; pc += 2) {
+            const int op = prog.code[pc];
+            const int arg = prog.code[pc + 1];
+            switch (op) {
+                case DQ_P_COL: st[sp++] = load_col(cols[arg], row); break;
+                case DQ_P_CONST: {
+                    const dq_const k = prog.consts[arg];
+                    Val v = vnull();
+                    v.null = 0;
+                    v.tag = k.tag;
+                    v.i = k.i64;
+                    v.d = k.f64;
+                    v.s = prog.strings + k.str_offset;
+                    v.slen = k.str_len;
+                    st[sp++] = v;
+                    break;
+                }
+                case DQ_P_NULL: st[sp++] = vnull(); break;
+                case DQ_P_EQ: case DQ_P_NE: case DQ_P_LT: case DQ_P_LE: case DQ_P_GT: case DQ_P_GE: {
+                    const Val b = st[--sp];
+                    const Val a = st[--sp];
+                    int c = 0;
+                    if (a.null || b.null || !compare(a, b, c)) {
+                        st[sp++] = vnull();
+                        break;
+                    }
+                    bool r = false;
+                    switch (op) {
+                        case DQ_P_EQ: r = c == 0; break;
+                        case DQ_P_NE: r = c != 0; break;
+                        case DQ_P_LT: r = c < 0; break;
+                        case DQ_P_LE: r = c <= 0; break;
+                        case DQ_P_GT: r = c > 0; break;
+                        default: r = c >= 0; break;
+                    }
+                    st[sp++] = vbool(r);
+                    break;
+                }
+                case DQ_P_EQ_NULLSAFE: {
+                    const Val b = st[--sp];
+                    const Val a = st[--sp];
+                    int c = 1;
+                    if (a.null || b.null) st[sp++] = vbool(a.null && b.null);
+                    else st[sp++] = vbool(compare(a, b, c) && c == 0);
+                    break;
+                }
+                case DQ_P_AND: {
+                    const Val b = st[--sp];
+                    const Val a = st[--sp];
+                    const bool af = !a.null && a.i == 0, bf = !b.null && b.i == 0;
+                    if (af || bf) st[sp++] = vbool(false);
+                    else if (a.null || b.null) st[sp++] = vnull();
+                    else st[sp++] = vbool(true);
+                    break;
+                }
+                case DQ_P_OR: {
+                    const Val b = st[--sp];
+                    const Val a = st[--sp];
+                    const bool at = !a.null && a.i != 0, bt = !b.null && b.i != 0;
+                    if (at || bt) st[sp++] = vbool(true);
+                    else if (a.null || b.null) st[sp++] = vnull();
+                    else st[sp++] = vbool(false);
+                    break;
+                }
+                case DQ_P_NOT: {
+                    Val a = st[sp - 1];
+                    if (!a.null) st[sp - 1] = vbool(a.i == 0);
+                    break;
+                }
+                case DQ_P_IS_NULL: st[sp - 1] = vbool(st[sp - 1].null != 0); break;
+                case DQ_P_IS_NOT_NULL: st[sp - 1] = vbool(st[sp - 1].null == 0); break;
+                case DQ_P_IN: {
+                    const int n = arg;
+                    const int base = sp - n - 1;
+                    const Val x = st[base];
+                    Val r = vbool(false);
+                    if (x.null) {
+                        r = vnull();
+                    } else {
+                        bool any_null = false, hit = false;
+                        for (int k = 0; k < n; ++k) {
+                            const Val& e = st[base + 1 + k];
+                            int c = 1;
+                            if (e.null) any_null = true;
+                            else if (compare(x, e, c) && c == 0) hit = true;
+                        }
+                        r = hit ? vbool(true) : (any_null ? vnull() : vbool(false));
+                    }
+                    sp = base;
+                    st[sp++] = r;
+                    break;
+                }
+                case DQ_P_COALESCE: {
+                    const int n = arg;
+                    const int base = sp - n;
+                    Val r = vnull();
+                    for (int k = n - 1; k >= 0; --k)
+                        if (!st[base + k].null) r = st[base + k];
+                    sp = base;
+                    st[sp++] = r;
+                    break;
+                }
+                case DQ_P_ADD: case DQ_P_SUB: case DQ_P_MUL: case DQ_P_DIV: case DQ_P_MOD: {
+                    const Val b = st[--sp];
+                    const Val a = st[--sp];
+                    st[sp++] = arith(op, a, b);
+                    break;
+                }
+                case DQ_P_NEG: {
+                    Val a = st[sp - 1];
+                    if (!a.null) {
+                        if (a.tag == DQ_V_DOUBLE) a.d = -a.d;
+                        else a.i = -a.i;
+                        st[sp - 1] = a;
+                    }
+                    break;
+                }
+                case DQ_P_LIKE: {
+                    const Val a = st[sp - 1];
+                    if (!a.null && a.tag == DQ_V_STRING) {
+                        const dq_const k = prog.consts[arg];
+                        st[sp - 1] = vbool(like_match(a.s, a.slen, prog.strings + k.str_offset, k.str_len));
+                    } else {
+                        st[sp - 1] = vnull();
+                    }
+                    break;
+                }
+                case DQ_P_LENGTH: {
+                    const Val a = st[sp - 1];
+                    if (!a.null && a.tag == DQ_V_STRING) st[sp - 1] = vlong(utf8_chars(a.s, a.slen));
+                    else if (!a.null) st[sp - 1] = vnull();
+                    break;
+                }
+                case DQ_P_CAST_DOUBLE: {
+                    const Val a = st[sp - 1];
+                    if (a.null) break;
+                    if (a.tag == DQ_V_STRING) {
+                        double d;
+                        st[sp - 1] = parse_double(a.s, a.slen, d) ? vdouble(d) : vnull();
+                    } else {
+                        st[sp - 1] = vdouble(as_double(a));
+                    }
+                    break;
+                }
+                case DQ_P_CAST_LONG: {
+                    const Val a = st[sp - 1];
+                    if (a.null) break;
+                    if (a.tag == DQ_V_STRING) {
+                        int64_t x;
+                        st[sp - 1] = parse_long(a.s, a.slen, x) ? vlong(x) : vnull();
+                    } else if (a.tag == DQ_V_DOUBLE) {
+                        st[sp - 1] = a.d != a.d ? vlong(0) : vlong((int64_t)a.d);
+                    } else {
+                        st[sp - 1] = vlong(a.i);
+                    }
+                    break;
+                }
+                default: break;
+            }
+        }
+        if (sp > 0) {
+            const Val r = st[sp - 1];
+            nn = !r.null;
+            t = nn && (r.tag == DQ_V_DOUBLE ? r.d != 0.0 : r.i != 0);
+        }
+    }
+    const uint64_t bt = __ballot(t);
+    const uint64_t bn = __ballot(nn);
+    const int64_t w = row >> 6;
+    if ((threadIdx.x & 63) == 0 && w < padded_words) {
+        out_t[w] = bt;
+        out_nn[w] = bn;
+    }
+}
+
+void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
+                      int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s) {
+    const int64_t rows = padded_words * 64;
+    const int64_t blocks = (rows + 255) / 256;
+    hipLaunchKernelGGL(predicate_kernel, dim3((unsigned)blocks), dim3(256), 0, s, prog_dev, cols_dev, nrows,
+                       padded_words, out_t, out_nn);
+}
+
+}  // namespace dq

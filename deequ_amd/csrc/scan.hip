@@ -1,0 +1,984 @@
+// scan.hip — the fused scan of all scan-shareable analyzers (gfx950 / CDNA4).
+//
+// Replaces the single Spark aggregation `data.agg(aggregations...).collect()` issued by
+// runScanningAnalyzers (R/AnalysisRunner.scala:289-336). Each op's Spark aggregate is restated in
+// SURVEY.md §8a; the per-row semantics implemented here:
+//   Size / Completeness / Compliance  A/Size.scala:33-47, A/Completeness.scala:38-41,
+//                                     A/Compliance.scala:49-52, where: A/Analyzer.scala:409-432
+//   Mean / Sum                        A/Mean.scala:36-40, A/Sum.scala:34-37 (Long sum for integral)
+//   Minimum / Maximum                 A/Minimum.scala:34-37, A/Maximum.scala:34-37
+//   StandardDeviation                 C/StatefulStdDevPop.scala:24-34 + merge A/StandardDeviation.scala:37-44
+//   Correlation                       C/StatefulCorrelation.scala:24-49 + merge A/Correlation.scala:37-52
+//   ApproxCountDistinct               C/StatefulHyperloglogPlus.scala:89-112 (XXH64 seed 42, P = 9)
+//
+// Layout: rows are split into contiguous per-workgroup ranges (multiples of a 2048-row tile).
+// Inside a tile each of the 256 lanes owns 8 rows: L = 8/P coalesced loads of P rows
+// (P = 16 B / element size: one global_load_dwordx4 per load for 4/8-byte types). The validity
+// and `where` bits of those rows come from 64-bit bitmap words (2 distinct words per wave per
+// load). Per-lane states are folded per 8-row batch (batch mean + Chan merge: one division per
+// batch, not per row), reduced wave64 -> workgroup through shuffles and a 4-entry LDS array, and
+// written as one SlotPartial per workgroup. A second launch folds the workgroup partials in a
+// fixed order (results are bitwise reproducible run to run). No fp atomics are used.
+// HLL registers live in LDS (512 x u32 per column) and are max-merged per workgroup.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include "dq_common.h"
+#include "dq_internal.h"
+
+namespace dq {
+
+__device__ __forceinline__ double as_f64(uint64_t u) { return __longlong_as_double((long long)u); }
+__device__ __forceinline__ uint64_t f64_bits(double d) { return (uint64_t)__double_as_longlong(d); }
+
+__device__ __forceinline__ uint64_t shfl_down_u64(uint64_t x, int off) {
+    int lo = (int)(uint32_t)x, hi = (int)(uint32_t)(x >> 32);
+    lo = __shfl_down(lo, off, 64);
+    hi = __shfl_down(hi, off, 64);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ int64_t shfl_down_i64(int64_t x, int off) {
+    return (int64_t)shfl_down_u64((uint64_t)x, off);
+}
+__device__ __forceinline__ double shfl_down_f64(double x, int off) {
+    return as_f64(shfl_down_u64(f64_bits(x), off));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Partial-state algebra (the reference's State.sum for each state, applied to lane/workgroup partials)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void col_init(ColPartial& a) {
+    a.n = 0;
+    a.nnan = 0;
+    a.isum = 0;
+    a.imin = INT64_MAX;
+    a.imax = INT64_MIN;
+    a.dsum = 0.0;
+    a.dmin = INFINITY;
+    a.dmax = -INFINITY;
+    a.mean = 0.0;
+    a.m2 = 0.0;
+}
+
+// StandardDeviationState.sum (A/StandardDeviation.scala:37-44) with an explicit empty side.
+__device__ __forceinline__ void moments_merge(int64_t na, double& mean, double& m2, int64_t nb,
+                                              double meanb, double m2b) {
+    if (nb == 0) return;
+    if (na == 0) {
+        mean = meanb;
+        m2 = m2b;
+        return;
+    }
+    const double n1 = (double)na, n2 = (double)nb;
+    const double newN = n1 + n2;
+    const double delta = meanb - mean;
+    const double deltaN = delta / newN;
+    mean = mean + deltaN * n2;
+    m2 = m2 + m2b + delta * deltaN * n1 * n2;
+}
+
+__device__ __forceinline__ void col_merge(ColPartial& a, const ColPartial& b) {
+    moments_merge(a.n, a.mean, a.m2, b.n, b.mean, b.m2);
+    a.n += b.n;
+    a.nnan += b.nnan;
+    a.isum = (int64_t)((uint64_t)a.isum + (uint64_t)b.isum);
+    a.imin = b.imin < a.imin ? b.imin : a.imin;
+    a.imax = b.imax > a.imax ? b.imax : a.imax;
+    a.dsum += b.dsum;
+    a.dmin = fmin(a.dmin, b.dmin);
+    a.dmax = fmax(a.dmax, b.dmax);
+}
+
+// CorrelationState.sum (A/Correlation.scala:37-52) with an explicit empty side.
+__device__ __forceinline__ void corr_merge(CorrPartial& a, const CorrPartial& b) {
+    if (b.n == 0.0) return;
+    if (a.n == 0.0) {
+        a = b;
+        return;
+    }
+    const double n1 = a.n, n2 = b.n;
+    const double newN = n1 + n2;
+    const double dx = b.xa - a.xa;
+    const double dxN = dx / newN;
+    const double dy = b.ya - a.ya;
+    const double dyN = dy / newN;
+    a.xa = a.xa + dxN * n2;
+    a.ya = a.ya + dyN * n2;
+    a.ck = a.ck + b.ck + dx * dyN * n1 * n2;
+    a.xm = a.xm + b.xm + dx * dxN * n1 * n2;
+    a.ym = a.ym + b.ym + dy * dyN * n1 * n2;
+    a.n = newN;
+}
+
+__device__ __forceinline__ void slot_init(SlotPartial& p) {
+    col_init(p.c[0]);
+    col_init(p.c[1]);
+    p.corr.n = p.corr.xa = p.corr.ya = p.corr.ck = p.corr.xm = p.corr.ym = 0.0;
+    p.wt = p.wnn = p.pt = p.pnn = p.vt = p.pad = 0;
+}
+
+__device__ __forceinline__ void slot_merge(SlotPartial& a, const SlotPartial& b) {
+    col_merge(a.c[0], b.c[0]);
+    col_merge(a.c[1], b.c[1]);
+    corr_merge(a.corr, b.corr);
+    a.wt += b.wt;
+    a.wnn += b.wnn;
+    a.pt += b.pt;
+    a.pnn += b.pnn;
+    a.vt += b.vt;
+}
+
+__device__ __forceinline__ void col_shfl(ColPartial& o, const ColPartial& a, int off) {
+    o.n = shfl_down_i64(a.n, off);
+    o.nnan = shfl_down_i64(a.nnan, off);
+    o.isum = shfl_down_i64(a.isum, off);
+    o.imin = shfl_down_i64(a.imin, off);
+    o.imax = shfl_down_i64(a.imax, off);
+    o.dsum = shfl_down_f64(a.dsum, off);
+    o.dmin = shfl_down_f64(a.dmin, off);
+    o.dmax = shfl_down_f64(a.dmax, off);
+    o.mean = shfl_down_f64(a.mean, off);
+    o.m2 = shfl_down_f64(a.m2, off);
+}
+
+__device__ __forceinline__ void slot_shfl(SlotPartial& o, const SlotPartial& a, int off, int ncols,
+                                          bool corr) {
+    col_shfl(o.c[0], a.c[0], off);
+    if (ncols > 1) col_shfl(o.c[1], a.c[1], off);
+    else col_init(o.c[1]);
+    if (corr) {
+        o.corr.n = shfl_down_f64(a.corr.n, off);
+        o.corr.xa = shfl_down_f64(a.corr.xa, off);
+        o.corr.ya = shfl_down_f64(a.corr.ya, off);
+        o.corr.ck = shfl_down_f64(a.corr.ck, off);
+        o.corr.xm = shfl_down_f64(a.corr.xm, off);
+        o.corr.ym = shfl_down_f64(a.corr.ym, off);
+    } else {
+        o.corr.n = o.corr.xa = o.corr.ya = o.corr.ck = o.corr.xm = o.corr.ym = 0.0;
+    }
+    o.wt = shfl_down_i64(a.wt, off);
+    o.wnn = shfl_down_i64(a.wnn, off);
+    o.pt = shfl_down_i64(a.pt, off);
+    o.pnn = shfl_down_i64(a.pnn, off);
+    o.vt = shfl_down_i64(a.vt, off);
+    o.pad = 0;
+}
+
+// wave64 tree (fixed order) -> 4 wave results in LDS -> lane 0 of wave 0 folds them in order.
+__device__ void block_reduce_slot(SlotPartial& acc, SlotPartial* lds4, int ncols, bool corr) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll 1
+    for (int off = 32; off > 0; off >>= 1) {
+        SlotPartial other;
+        slot_shfl(other, acc, off, ncols, corr);
+        if (lane < off) slot_merge(acc, other);
+    }
+    if (lane == 0) lds4[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) slot_merge(acc, lds4[w]);
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tile loaders. Row of (load j, element k) for lane `tid`: tile + j * 256 * P + tid * P + k.
+// ------------------------------------------------------------------------------------------------
+template <int P>
+__device__ __forceinline__ int64_t row_of(int64_t tile, int tid, int j, int k) {
+    return tile + (int64_t)j * (kBlock * P) + (int64_t)tid * P + k;
+}
+
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+
+// Buffer descriptor over one tile's bytes (T8/T20: 32-bit per-lane voffset, wave-uniform base
+// built from the slot descriptor and the tile index only, so it lives in SGPRs).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int64_t byte_off, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)base + byte_off), (short)0, bytes, 0x00020000);
+}
+
+// Bits of a padded bitmap (predicate outputs: always readable up to the tile end).
+template <int P>
+__device__ __forceinline__ uint32_t bits_padded(const uint64_t* __restrict__ bm, int64_t tile, int tid) {
+    constexpr int L = 8 / P;
+    constexpr uint32_t pm = (1u << P) - 1u;
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(bm, tile >> 3, kTileRows / 8);
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        // row0 = tile + j * 256 * P + tid * P; its 64-bit word inside the tile and bit offset:
+        const int rel = j * (kBlock * P) + tid * P;
+        const v2i_t w = __builtin_amdgcn_raw_buffer_load_b64(r, (rel >> 6) * 8, 0, 0);
+        const uint64_t word = ((uint64_t)(uint32_t)w.y << 32) | (uint32_t)w.x;
+        m |= (uint32_t)((word >> (rel & 63)) & pm) << (j * P);
+    }
+    return m;
+}
+
+// Rows of this lane that exist (tail tile).
+template <int P>
+__device__ __forceinline__ uint32_t in_range_mask(int64_t tile, int tid, int64_t nrows) {
+    constexpr int L = 8 / P;
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+#pragma unroll
+        for (int k = 0; k < P; ++k)
+            if (row_of<P>(tile, tid, j, k) < nrows) m |= 1u << (j * P + k);
+    return m;
+}
+
+// Validity bits of a user bitmap (exactly ceil(nrows/8) bytes long: bounded in the tail tile).
+template <int P>
+__device__ __forceinline__ uint32_t bits_valid(const uint64_t* __restrict__ bm, int64_t tile, int tid,
+                                               bool full, int64_t nrows) {
+    if (bm == nullptr) return full ? 0xFFu : in_range_mask<P>(tile, tid, nrows);
+    if (full) return bits_padded<P>(bm, tile, tid);
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(bm);
+    constexpr int L = 8 / P;
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const int64_t r = row_of<P>(tile, tid, j, k);
+            if (r < nrows && ((b[r >> 3] >> (r & 7)) & 1)) m |= 1u << (j * P + k);
+        }
+    return m;
+}
+
+// Loads the lane's 8 values in canonical form: int64 for integral storage, double bits for
+// FLOAT/DOUBLE. Missing rows (tail) load 0 and are masked off by the caller.
+__device__ __forceinline__ uint64_t pack64(int lo, int hi) { return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo; }
+
+template <int P, bool F>
+__device__ __forceinline__ void load_values(const ColDesc& c, int64_t tile, int tid, bool full,
+                                            int64_t nrows, uint64_t (&v)[8]) {
+    constexpr int L = 8 / P;
+    // Only the element types a (P, F) kernel can be planned for are compiled into it.
+    int e = c.elem;
+    if (P == 2) e = F ? ET_F64 : ET_I64;
+    if (P == 4) e = F ? ET_F32 : ET_I32;
+    if (P == 8 && F && e != ET_F32) e = ET_F64;
+    if (full) {
+        // One descriptor per tile; lane byte offsets: striped (P = 16 B / elem) or 8 contiguous rows.
+        const int esz = (e == ET_F64 || e == ET_I64) ? 8 : (e == ET_F32 || e == ET_I32) ? 4 : (e == ET_I16 ? 2 : 1);
+        const __amdgpu_buffer_rsrc_t r = tile_rsrc(c.values, tile * esz, kTileRows * esz);
+        if (esz == 8) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                // P == 2: load i covers rows i*512 + 2*tid (+0, +1); P == 8: rows 8*tid + 2i (+0, +1)
+                const int voff = P == 8 ? tid * 64 + i * 16 : tid * 16;
+                const int soff = P == 8 ? 0 : i * 4096;
+                const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+                v[2 * i] = pack64(x.x, x.y);
+                v[2 * i + 1] = pack64(x.z, x.w);
+            }
+            return;
+        }
+        if (esz == 4) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int voff = P == 8 ? tid * 32 + i * 16 : tid * 16;
+                const int soff = P == 8 ? 0 : i * 4096;
+                const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+                const int xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (e == ET_F32) v[4 * i + k] = f64_bits((double)__int_as_float(xs[k]));
+                    else v[4 * i + k] = (uint64_t)(int64_t)xs[k];
+                }
+            }
+            return;
+        }
+        if (esz == 2) {
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16, 0, 0);
+            const uint32_t w[4] = {(uint32_t)x.x, (uint32_t)x.y, (uint32_t)x.z, (uint32_t)x.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v[2 * i] = (uint64_t)(int64_t)(int16_t)(w[i] & 0xFFFFu);
+                v[2 * i + 1] = (uint64_t)(int64_t)(int16_t)(w[i] >> 16);
+            }
+            return;
+        }
+        const v2i_t x = __builtin_amdgcn_raw_buffer_load_b64(r, tid * 8, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t b = ((uint32_t)(i < 4 ? x.x : x.y) >> (8 * (i & 3))) & 0xFFu;
+            v[i] = e == ET_I8 ? (uint64_t)(int64_t)(int8_t)b : (uint64_t)b;
+        }
+        return;
+    }
+    // Tail tile: bounded element loads.
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+#pragma unroll
+        for (int k = 0; k < P; ++k) {
+            const int64_t r = row_of<P>(tile, tid, j, k);
+            const bool in = r < nrows;
+            uint64_t x = 0;
+            switch (e) {
+                case ET_F64:
+                case ET_I64: x = in ? static_cast<const uint64_t*>(c.values)[r] : 0; break;
+                case ET_F32: x = f64_bits(in ? (double)static_cast<const float*>(c.values)[r] : 0.0); break;
+                case ET_I32: x = (uint64_t)(int64_t)(in ? static_cast<const int32_t*>(c.values)[r] : 0); break;
+                case ET_I16: x = (uint64_t)(int64_t)(in ? static_cast<const int16_t*>(c.values)[r] : 0); break;
+                case ET_I8: x = (uint64_t)(int64_t)(in ? static_cast<const int8_t*>(c.values)[r] : 0); break;
+                default: x = in ? static_cast<const uint8_t*>(c.values)[r] : 0; break;
+            }
+            v[j * P + k] = x;
+        }
+}
+
+__device__ __forceinline__ bool is_float_elem(int e) { return e == ET_F32 || e == ET_F64; }
+
+__device__ __forceinline__ double to_double(uint64_t v, bool is_float) {
+    return is_float ? as_f64(v) : (double)(int64_t)v;
+}
+
+// Spark XxHash64Function.hash(value, dataType, 42) for the canonical lane value.
+__device__ __forceinline__ uint64_t spark_hash(uint64_t v, int spark_type) {
+    switch (spark_type) {
+        case DQ_TYPE_BOOLEAN:
+        case DQ_TYPE_BYTE:
+        case DQ_TYPE_SHORT:
+        case DQ_TYPE_INT:
+        case DQ_TYPE_DATE:
+            return xxh_int((uint32_t)(int32_t)(int64_t)v, SPARK_HLL_SEED);
+        case DQ_TYPE_FLOAT:
+            return xxh_int(float_to_int_bits((float)as_f64(v)), SPARK_HLL_SEED);
+        case DQ_TYPE_DOUBLE:
+            return xxh_long(double_to_long_bits(as_f64(v)), SPARK_HLL_SEED);
+        default:  // LONG, TIMESTAMP, DECIMAL(p <= 18): hashLong of the (unscaled) long
+            return xxh_long(v, SPARK_HLL_SEED);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-lane accumulators, specialised by storage class so only live state occupies VGPRs.
+// ------------------------------------------------------------------------------------------------
+struct FAcc {  // FLOAT / DOUBLE column
+    int64_t n, nnan;
+    double sum, mn, mx, mean, m2;
+};
+struct IAcc {  // integral column (Long sum with wrap-around, integer min/max)
+    int64_t n, sum, mn, mx;
+    double mean, m2;
+};
+template <bool F> struct AccOf { using type = IAcc; };
+template <> struct AccOf<true> { using type = FAcc; };
+
+__device__ __forceinline__ void acc_init(FAcc& a) {
+    a.n = a.nnan = 0;
+    a.sum = 0.0;
+    a.mn = INFINITY;
+    a.mx = -INFINITY;
+    a.mean = a.m2 = 0.0;
+}
+__device__ __forceinline__ void acc_init(IAcc& a) {
+    a.n = a.sum = 0;
+    a.mn = INT64_MAX;
+    a.mx = INT64_MIN;
+    a.mean = a.m2 = 0.0;
+}
+
+__device__ __forceinline__ void acc_merge(FAcc& a, const FAcc& b) {
+    moments_merge(a.n, a.mean, a.m2, b.n, b.mean, b.m2);
+    a.n += b.n;
+    a.nnan += b.nnan;
+    a.sum += b.sum;
+    a.mn = fmin(a.mn, b.mn);
+    a.mx = fmax(a.mx, b.mx);
+}
+__device__ __forceinline__ void acc_merge(IAcc& a, const IAcc& b) {
+    moments_merge(a.n, a.mean, a.m2, b.n, b.mean, b.m2);
+    a.n += b.n;
+    a.sum = (int64_t)((uint64_t)a.sum + (uint64_t)b.sum);
+    a.mn = b.mn < a.mn ? b.mn : a.mn;
+    a.mx = b.mx > a.mx ? b.mx : a.mx;
+}
+
+__device__ __forceinline__ void acc_shfl(FAcc& o, const FAcc& a, int off) {
+    o.n = shfl_down_i64(a.n, off);
+    o.nnan = shfl_down_i64(a.nnan, off);
+    o.sum = shfl_down_f64(a.sum, off);
+    o.mn = shfl_down_f64(a.mn, off);
+    o.mx = shfl_down_f64(a.mx, off);
+    o.mean = shfl_down_f64(a.mean, off);
+    o.m2 = shfl_down_f64(a.m2, off);
+}
+__device__ __forceinline__ void acc_shfl(IAcc& o, const IAcc& a, int off) {
+    o.n = shfl_down_i64(a.n, off);
+    o.sum = shfl_down_i64(a.sum, off);
+    o.mn = shfl_down_i64(a.mn, off);
+    o.mx = shfl_down_i64(a.mx, off);
+    o.mean = shfl_down_f64(a.mean, off);
+    o.m2 = shfl_down_f64(a.m2, off);
+}
+__device__ __forceinline__ void corr_shfl(CorrPartial& o, const CorrPartial& a, int off) {
+    o.n = shfl_down_f64(a.n, off);
+    o.xa = shfl_down_f64(a.xa, off);
+    o.ya = shfl_down_f64(a.ya, off);
+    o.ck = shfl_down_f64(a.ck, off);
+    o.xm = shfl_down_f64(a.xm, off);
+    o.ym = shfl_down_f64(a.ym, off);
+}
+
+__device__ __forceinline__ void store_empty(ColPartial& p) {
+    p.n = p.nnan = p.isum = 0;
+    p.imin = INT64_MAX;
+    p.imax = INT64_MIN;
+    p.dsum = 0.0;
+    p.dmin = INFINITY;
+    p.dmax = -INFINITY;
+    p.mean = p.m2 = 0.0;
+}
+__device__ __forceinline__ void store_partial(ColPartial& p, const FAcc& a) {
+    store_empty(p);
+    p.n = a.n;
+    p.nnan = a.nnan;
+    p.dsum = a.sum;
+    p.dmin = a.mn;
+    p.dmax = a.mx;
+    p.mean = a.mean;
+    p.m2 = a.m2;
+}
+__device__ __forceinline__ void store_partial(ColPartial& p, const IAcc& a) {
+    store_empty(p);
+    p.n = a.n;
+    p.isum = a.sum;
+    p.imin = a.mn;
+    p.imax = a.mx;
+    p.mean = a.mean;
+    p.m2 = a.m2;
+}
+__device__ __forceinline__ void to_partial(ColPartial& p, const FAcc& a) {
+    col_init(p);
+    p.n = a.n;
+    p.nnan = a.nnan;
+    p.dsum = a.sum;
+    p.dmin = a.mn;
+    p.dmax = a.mx;
+    p.mean = a.mean;
+    p.m2 = a.m2;
+}
+__device__ __forceinline__ void to_partial(ColPartial& p, const IAcc& a) {
+    col_init(p);
+    p.n = a.n;
+    p.isum = a.sum;
+    p.imin = a.mn;
+    p.imax = a.mx;
+    p.mean = a.mean;
+    p.m2 = a.m2;
+}
+
+// Per-lane fold of one 8-row batch (Spark's per-row updates restated as a batch + Chan merge).
+__device__ __forceinline__ void accumulate(FAcc& a, const uint64_t (&v)[8], uint32_t m, uint32_t flags) {
+    const int cnt = __popc(m);
+    if (cnt == 0) return;
+    if (flags & (CF_STATS | CF_MOMENTS)) {
+        uint32_t nanm = 0;
+        double s = 0.0, mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double x = as_f64(v[k]);
+            const bool on = (m >> k) & 1u;
+            const bool nan = x != x;
+            nanm |= (on && nan) ? (1u << k) : 0u;
+            const bool use = on && !nan;
+            s += on ? x : 0.0;
+            mn = fmin(mn, use ? x : INFINITY);
+            mx = fmax(mx, use ? x : -INFINITY);
+        }
+        a.nnan += __popc(nanm);
+        a.sum += s;
+        a.mn = fmin(a.mn, mn);
+        a.mx = fmax(a.mx, mx);
+        if (flags & CF_MOMENTS) {
+            const double mb = s / (double)cnt;
+            double m2b = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double d = as_f64(v[k]) - mb;
+                m2b += ((m >> k) & 1u) ? d * d : 0.0;
+            }
+            moments_merge(a.n, a.mean, a.m2, cnt, mb, m2b);
+        }
+    }
+    a.n += cnt;
+}
+
+__device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint32_t m, uint32_t flags) {
+    const int cnt = __popc(m);
+    if (cnt == 0) return;
+    if (flags & CF_STATS) {
+        int64_t s = 0, mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t x = (int64_t)v[k];
+            const bool on = (m >> k) & 1u;
+            s = (int64_t)((uint64_t)s + (on ? (uint64_t)x : 0ull));
+            mn = (on && x < mn) ? x : mn;
+            mx = (on && x > mx) ? x : mx;
+        }
+        a.sum = (int64_t)((uint64_t)a.sum + (uint64_t)s);
+        a.mn = mn < a.mn ? mn : a.mn;
+        a.mx = mx > a.mx ? mx : a.mx;
+    }
+    if (flags & CF_MOMENTS) {
+        // Spark casts each value to Double before the moment update (C/StatefulStdDevPop.scala:24).
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += ((m >> k) & 1u) ? (double)(int64_t)v[k] : 0.0;
+        const double mb = s / (double)cnt;
+        double m2b = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double d = (double)(int64_t)v[k] - mb;
+            m2b += ((m >> k) & 1u) ? d * d : 0.0;
+        }
+        moments_merge(a.n, a.mean, a.m2, cnt, mb, m2b);
+    }
+    a.n += cnt;
+}
+
+template <bool FX, bool FY>
+__device__ __forceinline__ void accumulate_corr(CorrPartial& c, const uint64_t (&x)[8], const uint64_t (&y)[8],
+                                                uint32_t m) {
+    const int cnt = __popc(m);
+    if (cnt == 0) return;
+    double sx = 0.0, sy = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const bool on = (m >> k) & 1u;
+        sx += on ? to_double(x[k], FX) : 0.0;
+        sy += on ? to_double(y[k], FY) : 0.0;
+    }
+    CorrPartial b;
+    b.n = (double)cnt;
+    b.xa = sx / b.n;
+    b.ya = sy / b.n;
+    b.ck = b.xm = b.ym = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const bool on = (m >> k) & 1u;
+        const double dx = to_double(x[k], FX) - b.xa;
+        const double dy = to_double(y[k], FY) - b.ya;
+        b.ck += on ? dx * dy : 0.0;
+        b.xm += on ? dx * dx : 0.0;
+        b.ym += on ? dy * dy : 0.0;
+    }
+    corr_merge(c, b);
+}
+
+__device__ __forceinline__ void hll_update(uint32_t* regs, const uint64_t (&v)[8], uint32_t m, int spark_type) {
+#pragma unroll 1
+    for (int k = 0; k < 8; ++k) {
+        if ((m >> k) & 1u) {
+            const uint64_t x = spark_hash(v[k], spark_type);
+            const uint32_t idx = hll_index(x);
+            const uint32_t pw = hll_rank(x);
+            // Registers only grow: skip the LDS atomic when it cannot raise the register.
+            if (pw > regs[idx]) atomicMax(&regs[idx], pw);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Value slots: P rows per load, NC columns (2 = Correlation pair), F0/F1 = floating storage.
+// Workgroup g handles tiles g, g + G, g + 2G, ... (balanced for any grid size); the next tile's
+// loads are issued before the current tile is folded (register double buffer).
+// ------------------------------------------------------------------------------------------------
+template <int NC, bool F0, bool F1>
+struct BlockRed {
+    typename AccOf<F0>::type a0[kBlock / 64];
+    typename AccOf<F1>::type a1[kBlock / 64];
+    CorrPartial cp[kBlock / 64];
+    int64_t wt[kBlock / 64], wnn[kBlock / 64];
+};
+
+template <int P, int NC, bool F0, bool F1>
+__global__ void __launch_bounds__(kBlock)
+scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__ group, int ngroup,
+                   int64_t nrows, int64_t ntiles, int gstride, SlotPartial* __restrict__ partials,
+                   uint8_t* __restrict__ hll_partials) {
+    using A0 = typename AccOf<F0>::type;
+    using A1 = typename AccOf<F1>::type;
+    __shared__ uint32_t hll_lds[NC][kHllRegs];
+    __shared__ BlockRed<NC, F0, F1> red;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int64_t G = gridDim.x;
+    for (int gi = 0; gi < ngroup; ++gi) {
+        const int s = group[gi];
+        const SlotDesc sd = slots[s];
+        const ColDesc c0 = sd.col[0];
+        const ColDesc c1 = sd.col[1];
+        const bool has_where = sd.where_t != nullptr;
+        const bool hll0 = (c0.flags & CF_HLL) != 0;
+        const bool hll1 = NC > 1 && (c1.flags & CF_HLL) != 0;
+        A0 a0;
+        A1 a1;
+        acc_init(a0);
+        acc_init(a1);
+        CorrPartial cp;
+        cp.n = cp.xa = cp.ya = cp.ck = cp.xm = cp.ym = 0.0;
+        int64_t wt = 0, wnn = 0;
+        if (hll0 || hll1) {
+            for (int i = tid; i < NC * kHllRegs; i += kBlock) (&hll_lds[0][0])[i] = 0;
+            __syncthreads();
+        }
+        // Folds one loaded tile into the lane state.
+        auto fold = [&](int64_t tb, bool full, const uint64_t (&xv)[8], const uint64_t (&yv)[8]) {
+            uint32_t mx = bits_valid<P>(c0.validity, tb, tid, full, nrows);
+            uint32_t my = NC > 1 ? bits_valid<P>(c1.validity, tb, tid, full, nrows) : 0u;
+            if (has_where) {
+                const uint32_t w = bits_padded<P>(sd.where_t, tb, tid);
+                wt += __popc(w);
+                wnn += __popc(bits_padded<P>(sd.where_nn, tb, tid));
+                mx &= w;
+                my &= w;
+            }
+            accumulate(a0, xv, mx, c0.flags);
+            if (hll0) hll_update(hll_lds[0], xv, mx, c0.spark_type);
+            if (NC > 1) {
+                accumulate(a1, yv, my, c1.flags);
+                if (hll1) hll_update(hll_lds[NC - 1], yv, my, c1.spark_type);
+                accumulate_corr<F0, F1>(cp, xv, yv, mx & my);
+            }
+        };
+        // Full tiles: buffer loads only, next tile's loads in flight while the current one folds.
+        const int64_t nfull = nrows / kTileRows;
+        int64_t t = blockIdx.x;
+        uint64_t x[8], y[8], xn[8], yn[8];
+        if (t < nfull) {
+            load_values<P, F0>(c0, t * kTileRows, tid, true, nrows, x);
+            if (NC > 1) load_values<P, F1>(c1, t * kTileRows, tid, true, nrows, y);
+        }
+        for (; t < nfull; t += G) {
+            const int64_t tn = t + G;
+            if (tn < nfull) {
+                load_values<P, F0>(c0, tn * kTileRows, tid, true, nrows, xn);
+                if (NC > 1) load_values<P, F1>(c1, tn * kTileRows, tid, true, nrows, yn);
+            }
+            fold(t * kTileRows, true, x, y);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                x[k] = xn[k];
+                if (NC > 1) y[k] = yn[k];
+            }
+        }
+        // The partial last tile (if any) goes to the workgroup next in the interleave.
+        if (nfull < ntiles && blockIdx.x == nfull % G) {
+            load_values<P, F0>(c0, nfull * kTileRows, tid, false, nrows, x);
+            if (NC > 1) load_values<P, F1>(c1, nfull * kTileRows, tid, false, nrows, y);
+            fold(nfull * kTileRows, false, x, y);
+        }
+        // wave64 tree, then the 4 wave results in a fixed order.
+#pragma unroll 1
+        for (int off = 32; off > 0; off >>= 1) {
+            A0 o0;
+            acc_shfl(o0, a0, off);
+            const int64_t owt = shfl_down_i64(wt, off), ownn = shfl_down_i64(wnn, off);
+            A1 o1;
+            CorrPartial oc;
+            if (NC > 1) {
+                acc_shfl(o1, a1, off);
+                corr_shfl(oc, cp, off);
+            }
+            if (lane < off) {
+                acc_merge(a0, o0);
+                wt += owt;
+                wnn += ownn;
+                if (NC > 1) {
+                    acc_merge(a1, o1);
+                    corr_merge(cp, oc);
+                }
+            }
+        }
+        if (lane == 0) {
+            red.a0[wave] = a0;
+            red.wt[wave] = wt;
+            red.wnn[wave] = wnn;
+            if (NC > 1) {
+                red.a1[wave] = a1;
+                red.cp[wave] = cp;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < kBlock / 64; ++w) {
+                acc_merge(a0, red.a0[w]);
+                wt += red.wt[w];
+                wnn += red.wnn[w];
+                if (NC > 1) {
+                    acc_merge(a1, red.a1[w]);
+                    corr_merge(cp, red.cp[w]);
+                }
+            }
+            // Field-wise stores: a whole SlotPartial temporary would cost ~70 VGPRs here.
+            SlotPartial* dst = partials + (int64_t)s * gstride + blockIdx.x;
+            store_partial(dst->c[0], a0);
+            if (NC > 1) {
+                store_partial(dst->c[1], a1);
+                dst->corr = cp;
+            } else {
+                store_empty(dst->c[1]);
+                dst->corr.n = dst->corr.xa = dst->corr.ya = dst->corr.ck = dst->corr.xm = dst->corr.ym = 0.0;
+            }
+            dst->wt = wt;
+            dst->wnn = wnn;
+            dst->pt = dst->pnn = dst->vt = dst->pad = 0;
+        }
+        if (hll0 || hll1) {
+            for (int c = 0; c < NC; ++c) {
+                const int hs = c == 0 ? c0.hll_slot : c1.hll_slot;
+                if (hs >= 0 && (c == 0 ? hll0 : hll1)) {
+                    uint8_t* dst = hll_partials + ((int64_t)hs * gstride + blockIdx.x) * kHllRegs;
+                    for (int i = tid; i < kHllRegs; i += kBlock) dst[i] = (uint8_t)hll_lds[c][i];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Bits-only slots (Size(where), Completeness of an unread column, Compliance): one 64-row bitmap
+// word per lane per step, tiles interleaved over workgroups like the value kernels.
+__global__ void __launch_bounds__(kBlock)
+scan_bits_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__ group, int ngroup, int64_t nrows,
+                 int64_t ntiles, int gstride, SlotPartial* __restrict__ partials) {
+    __shared__ SlotPartial red[kBlock / 64];
+    constexpr int kWordsPerTile = kTileRows / 64;
+    const int64_t nwords_total = (nrows + 63) >> 6;
+    for (int gi = 0; gi < ngroup; ++gi) {
+        const int s = group[gi];
+        const SlotDesc sd = slots[s];
+        const uint8_t* vb = reinterpret_cast<const uint8_t*>(sd.bits_valid);
+        SlotPartial acc;
+        slot_init(acc);
+        for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+            for (int i = threadIdx.x; i < kWordsPerTile; i += kBlock) {
+                const int64_t w = t * kWordsPerTile + i;
+                if (w >= nwords_total) break;
+                const int64_t base = w << 6;
+                const int64_t nin = nrows - base;
+                const uint64_t range = nin >= 64 ? ~0ull : ((1ull << nin) - 1ull);
+                const uint64_t wtb = sd.where_t ? sd.where_t[w] : range;
+                const uint64_t wnb = sd.where_t ? sd.where_nn[w] : range;
+                acc.wt += __popcll(wtb);
+                acc.wnn += __popcll(wnb);
+                if (sd.pred_t) {
+                    acc.pt += __popcll(wtb & sd.pred_t[w]);
+                    acc.pnn += __popcll(wtb & sd.pred_nn[w]);
+                }
+                if (vb) {
+                    uint64_t vw;
+                    if (nin >= 64) {
+                        vw = sd.bits_valid[w];
+                    } else {
+                        vw = 0;
+                        for (int64_t b = 0; b < (nin + 7) / 8; ++b) vw |= (uint64_t)vb[(base >> 3) + b] << (8 * b);
+                        vw &= range;
+                    }
+                    acc.vt += __popcll(wtb & vw);
+                }
+            }
+        }
+        block_reduce_slot(acc, red, 1, false);
+        if (threadIdx.x == 0) partials[(int64_t)s * gstride + blockIdx.x] = acc;
+    }
+}
+
+// Folds each slot's workgroup partials in a fixed order.
+__global__ void __launch_bounds__(kBlock)
+reduce_partials_kernel(const SlotPartial* __restrict__ partials, const int32_t* __restrict__ nblocks_of,
+                       int gstride, SlotPartial* __restrict__ finals) {
+    __shared__ SlotPartial red[kBlock / 64];
+    const int s = blockIdx.x;
+    const int nb = nblocks_of[s];
+    SlotPartial acc;
+    slot_init(acc);
+    for (int b = threadIdx.x; b < nb; b += kBlock) slot_merge(acc, partials[(int64_t)s * gstride + b]);
+    block_reduce_slot(acc, red, 2, true);
+    if (threadIdx.x == 0) finals[s] = acc;
+}
+
+__global__ void __launch_bounds__(kHllRegs)
+reduce_hll_kernel(const uint8_t* __restrict__ hll_partials, const int32_t* __restrict__ nblocks_of, int gstride,
+                  uint8_t* __restrict__ hll_final) {
+    const int h = blockIdx.x;
+    const int r = threadIdx.x;
+    const int nb = nblocks_of[h];
+    uint32_t m = 0;
+    for (int b = 0; b < nb; ++b) {
+        const uint32_t v = hll_partials[((int64_t)h * gstride + b) * kHllRegs + r];
+        m = v > m ? v : m;
+    }
+    hll_final[(int64_t)h * kHllRegs + r] = (uint8_t)m;
+}
+
+__device__ __forceinline__ double pow10i(int scale) {
+    double d = 1.0;
+    for (int i = 0; i < scale; ++i) d *= 10.0;
+    return d;
+}
+
+// Builds each op's dq_state from its slot (fromAggregationResult + ifNoNullsIn of every analyzer).
+__global__ void finalize_kernel(const OpMap* __restrict__ ops, int nops, const SlotPartial* __restrict__ finals,
+                                const uint8_t* __restrict__ hll_final, dq_state* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nops) return;
+    const OpMap om = ops[i];
+    dq_state* st = out + i;
+    for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) st->u.hll.words[w] = 0;
+    st->kind = om.kind;
+    int present = 0;
+    SlotPartial sp;
+    if (om.slot >= 0) sp = finals[om.slot];
+    else slot_init(sp);
+    const ColPartial& c = sp.c[om.colpos > 0 ? 1 : 0];
+    // conditionalCount(where) (A/Analyzer.scala:426-432): count(*), or sum(cast(where AS long)),
+    // which is NULL when no row has a non-null `where` value.
+    const int64_t cond_count = om.has_where ? sp.wt : om.nrows;
+    const bool cond_count_present = om.has_where ? (sp.wnn > 0) : true;
+    const double scale = om.decimal_scale > 0 ? pow10i(om.decimal_scale) : 1.0;
+    switch (om.kind) {
+        case DQ_OP_SIZE:
+            st->u.num_matches.num_matches = cond_count;
+            present = cond_count_present;
+            break;
+        case DQ_OP_COMPLETENESS: {
+            // sum(cast(isNotNull(when(where, col)) AS int)): NULL only over zero rows.
+            const int64_t matches = om.from_bits == 1 ? sp.vt : (om.from_bits == 2 ? cond_count : c.n);
+            st->u.num_matches_and_count.num_matches = matches;
+            st->u.num_matches_and_count.count = cond_count;
+            present = (om.nrows > 0) && cond_count_present;
+            break;
+        }
+        case DQ_OP_COMPLIANCE:
+            // sum(cast(when(where, pred) AS int)): NULL when no row has where TRUE and pred non-null.
+            st->u.num_matches_and_count.num_matches = sp.pt;
+            st->u.num_matches_and_count.count = cond_count;
+            present = (sp.pnn > 0) && cond_count_present;
+            break;
+        case DQ_OP_MEAN:
+            st->u.mean.sum = om.is_float ? c.dsum : (double)c.isum / scale;
+            st->u.mean.count = c.n;
+            present = c.n > 0;
+            break;
+        case DQ_OP_SUM:
+            st->u.dbl.value = om.is_float ? c.dsum : (double)c.isum / scale;
+            present = c.n > 0;
+            break;
+        case DQ_OP_MINIMUM:
+            if (om.is_float) st->u.dbl.value = (c.nnan == c.n) ? NAN : c.dmin;
+            else st->u.dbl.value = (double)c.imin / scale;
+            present = c.n > 0;
+            break;
+        case DQ_OP_MAXIMUM:
+            if (om.is_float) st->u.dbl.value = (c.nnan > 0) ? NAN : c.dmax;
+            else st->u.dbl.value = (double)c.imax / scale;
+            present = c.n > 0;
+            break;
+        case DQ_OP_STANDARD_DEVIATION:
+            st->u.stddev.n = (double)c.n;
+            st->u.stddev.avg = c.mean / scale;
+            st->u.stddev.m2 = c.m2 / (scale * scale);
+            present = c.n > 0;
+            break;
+        case DQ_OP_CORRELATION:
+            st->u.corr.n = sp.corr.n;
+            st->u.corr.x_avg = om.colpos ? sp.corr.ya : sp.corr.xa;
+            st->u.corr.y_avg = om.colpos ? sp.corr.xa : sp.corr.ya;
+            st->u.corr.ck = sp.corr.ck;
+            st->u.corr.x_mk = om.colpos ? sp.corr.ym : sp.corr.xm;
+            st->u.corr.y_mk = om.colpos ? sp.corr.xm : sp.corr.ym;
+            present = sp.corr.n > 0.0;
+            break;
+        case DQ_OP_APPROX_COUNT_DISTINCT: {
+            // 6-bit registers, 10 per word, LSB first (C/StatefulHyperloglogPlus.scala:99-109).
+            const uint8_t* regs = hll_final + (int64_t)om.hll_slot * kHllRegs;
+            for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) {
+                uint64_t word = 0;
+                for (int k = 0; k < 10; ++k) {
+                    const int idx = w * 10 + k;
+                    if (idx < kHllRegs) word |= (uint64_t)(regs[idx] & 63u) << (6 * k);
+                }
+                st->u.hll.words[w] = (int64_t)word;
+            }
+            present = 1;  // the HLL aggregate is never null (nullable = false)
+            break;
+        }
+        default:
+            break;
+    }
+    st->present = present;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Launchers
+// ------------------------------------------------------------------------------------------------
+template <int P, int NC, bool F0, bool F1>
+static const void* values_kernel_ptr() {
+    return reinterpret_cast<const void*>(&scan_values_kernel<P, NC, F0, F1>);
+}
+
+static const void* values_kernel_for(int P, int nc, bool f0, bool f1) {
+#define DQ_VK(p, n, a, b) \
+    if (P == p && nc == n && f0 == a && f1 == b) return values_kernel_ptr<p, n, a, b>();
+    DQ_VK(2, 1, false, false) DQ_VK(2, 1, true, false) DQ_VK(4, 1, false, false) DQ_VK(4, 1, true, false)
+    DQ_VK(8, 1, false, false) DQ_VK(8, 1, true, false)
+    DQ_VK(2, 2, false, false) DQ_VK(2, 2, false, true) DQ_VK(2, 2, true, false) DQ_VK(2, 2, true, true)
+    DQ_VK(4, 2, false, false) DQ_VK(4, 2, false, true) DQ_VK(4, 2, true, false) DQ_VK(4, 2, true, true)
+    DQ_VK(8, 2, false, false) DQ_VK(8, 2, false, true) DQ_VK(8, 2, true, false) DQ_VK(8, 2, true, true)
+#undef DQ_VK
+    return nullptr;
+}
+
+int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1) {
+    const void* k = kind == SK_BITS ? reinterpret_cast<const void*>(&scan_bits_kernel) : values_kernel_for(P, nc, f0, f1);
+    if (!k) return 0;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, 0) != hipSuccess || n <= 0) n = 1;
+    return n;
+}
+
+int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, const SlotDesc* slots, const int32_t* group,
+                      int ngroup, int64_t nrows, int64_t ntiles, int gstride, int grid, SlotPartial* partials,
+                      uint8_t* hll_partials, hipStream_t s) {
+    if (kind == SK_BITS) {
+        hipLaunchKernelGGL(scan_bits_kernel, dim3(grid), dim3(kBlock), 0, s, slots, group, ngroup, nrows, ntiles,
+                           gstride, partials);
+        return 0;
+    }
+    const void* k = values_kernel_for(P, nc, f0, f1);
+    if (!k) return -1;
+    void* args[] = {(void*)&slots, (void*)&group, (void*)&ngroup, (void*)&nrows, (void*)&ntiles,
+                    (void*)&gstride, (void*)&partials, (void*)&hll_partials};
+    return hipLaunchKernel(k, dim3(grid), dim3(kBlock), args, 0, s) == hipSuccess ? 0 : -1;
+}
+
+void launch_reduce_partials(const SlotPartial* partials, const int32_t* nblocks_of, int nslots, int gstride,
+                            SlotPartial* finals, hipStream_t s) {
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(nslots), dim3(kBlock), 0, s, partials, nblocks_of, gstride, finals);
+}
+
+void launch_reduce_hll(const uint8_t* hll_partials, const int32_t* nblocks_of, int nhll, int gstride,
+                       uint8_t* hll_final, hipStream_t s) {
+    if (nhll == 0) return;
+    hipLaunchKernelGGL(reduce_hll_kernel, dim3(nhll), dim3(kHllRegs), 0, s, hll_partials, nblocks_of, gstride,
+                       hll_final);
+}
+
+void launch_finalize(const OpMap* ops, int nops, const SlotPartial* finals, const uint8_t* hll_final,
+                     dq_state* out, hipStream_t s) {
+    const int tb = 64;
+    hipLaunchKernelGGL(finalize_kernel, dim3((nops + tb - 1) / tb), dim3(tb), 0, s, ops, nops, finals, hll_final,
+                       out);
+}
+
+}  // namespace dq

@@ -1,0 +1,93 @@
+"""Device selection and the frequency-table handle (the GPU side of computeFrequencies)."""
+import ctypes
+import os
+
+import numpy as np
+
+from . import native as N
+
+_device = None
+
+
+def set_device(device):
+    global _device
+    _device = int(device)
+
+
+def device():
+    if _device is not None:
+        return _device
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def ctx():
+    return N.context(device())
+
+
+class FrequencyTable:
+    """Device-resident (key -> count) table built by dq_frequencies over `key_columns` of `source`."""
+
+    def __init__(self, context, handle, source, key_columns, include_nulls):
+        self.ctx = context
+        self.handle = handle
+        self.source = source
+        self.key_columns = [source[c] for c in key_columns]
+        self.names = list(key_columns)
+        self.include_nulls = include_nulls
+        s = self.summary(None)
+        self.num_rows = s["num_rows"]
+        self.num_groups = s["num_groups"]
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self.ctx.lib.dq_freq_free(self.ctx.handle, self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+    def summary(self, entropy_rows=None):
+        out = N.DqFreqSummary()
+        rc = self.ctx.lib.dq_freq_summarize(self.ctx.handle, self.handle, int(entropy_rows or 0), ctypes.byref(out))
+        self.ctx.check(rc, "dq_freq_summarize")
+        return {"num_rows": out.num_rows, "num_groups": out.num_groups, "num_unique": out.num_unique,
+                "entropy": out.entropy, "entropy_rows": out.entropy_rows, "max_count": out.max_count}
+
+    def _key_of_row(self, r):
+        key = []
+        for c in self.key_columns:
+            valid = c.validity is None or bool((c.validity[r >> 3] >> (r & 7)) & 1)
+            key.append(c.value_at(int(r)) if valid else None)
+        return tuple(key)
+
+    def top(self, k):
+        """[(key tuple, count)] of the k largest groups (ties: smallest representative row)."""
+        k = int(min(k, self.num_groups))
+        rows = np.zeros(max(k, 1), dtype=np.int64)
+        counts = np.zeros(max(k, 1), dtype=np.int64)
+        n = self.ctx.lib.dq_freq_top(self.ctx.handle, self.handle, k, rows.ctypes.data, counts.ctypes.data)
+        if n < 0:
+            raise N.NativeError(int(n), "dq_freq_top: %s" % self.ctx.last_error())
+        return [(self._key_of_row(int(rows[i])), int(counts[i])) for i in range(n)]
+
+    def to_dict(self):
+        n = self.num_groups
+        rows = np.zeros(max(n, 1), dtype=np.int64)
+        counts = np.zeros(max(n, 1), dtype=np.int64)
+        got = self.ctx.lib.dq_freq_export(self.ctx.handle, self.handle, n, rows.ctypes.data, counts.ctypes.data)
+        if got < 0:
+            raise N.NativeError(int(got), "dq_freq_export: %s" % self.ctx.last_error())
+        return {self._key_of_row(int(rows[i])): int(counts[i]) for i in range(got)}
+
+
+def frequencies(table, key_columns, include_nulls=False):
+    context = ctx()
+    names = list(table.columns)
+    cols = [table[c].native() for c in names]
+    keys = np.array([names.index(c) for c in key_columns], dtype=np.int32)
+    arr = (N.DqColumn * max(len(cols), 1))(*cols)
+    handle = ctypes.c_void_p()
+    rc = context.lib.dq_frequencies(context.handle, arr, len(cols), table.nrows, keys.ctypes.data, len(keys),
+                                    N.FREQ_INCLUDE_NULLS if include_nulls else 0, ctypes.byref(handle))
+    context.check(rc, "dq_frequencies")
+    return FrequencyTable(context, handle, table, key_columns, include_nulls)

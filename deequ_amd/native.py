@@ -1,0 +1,281 @@
+"""ctypes binding of libdq.so (include/dq.h) — the same C-ABI a JVM host binds over JNI.
+
+The library is loaded from the package directory (built in-tree by __graft_entry__.build()).
+There is no CPU fallback: if the library or a GPU is missing, operations raise.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdq.so")
+
+# ---- constants mirrored from include/dq.h -------------------------------------------------------
+DQ_OK = 0
+STATUS_NAMES = {0: "DQ_OK", -1: "DQ_ERR_INVALID_ARGUMENT", -2: "DQ_ERR_UNSUPPORTED", -3: "DQ_ERR_DEVICE",
+                -4: "DQ_ERR_OUT_OF_MEMORY", -5: "DQ_ERR_NO_DEVICE", -6: "DQ_ERR_PREDICATE",
+                -7: "DQ_ERR_ALIGNMENT"}
+
+TYPE_BOOLEAN, TYPE_BYTE, TYPE_SHORT, TYPE_INT, TYPE_LONG, TYPE_FLOAT, TYPE_DOUBLE, TYPE_STRING, \
+    TYPE_DATE, TYPE_TIMESTAMP, TYPE_DECIMAL = range(1, 12)
+
+COL_DEVICE = 0x1
+SCAN_OUT_DEVICE = 0x1
+FREQ_INCLUDE_NULLS = 0x1
+
+OP_SIZE, OP_COMPLETENESS, OP_COMPLIANCE, OP_MEAN, OP_SUM, OP_MINIMUM, OP_MAXIMUM, OP_STANDARD_DEVIATION, \
+    OP_CORRELATION, OP_APPROX_COUNT_DISTINCT, OP_MIN_LENGTH, OP_MAX_LENGTH, OP_DATATYPE = range(1, 14)
+
+# predicate opcodes
+P_COL, P_CONST, P_NULL = 1, 2, 3
+P_EQ, P_NE, P_LT, P_LE, P_GT, P_GE, P_EQ_NULLSAFE = 10, 11, 12, 13, 14, 15, 16
+P_AND, P_OR, P_NOT, P_IS_NULL, P_IS_NOT_NULL, P_IN, P_COALESCE = 20, 21, 22, 23, 24, 25, 26
+P_ADD, P_SUB, P_MUL, P_DIV, P_MOD, P_NEG = 30, 31, 32, 33, 34, 35
+P_LIKE, P_LENGTH, P_CAST_DOUBLE, P_CAST_LONG = 40, 41, 42, 43
+V_BOOL, V_LONG, V_DOUBLE, V_STRING = 1, 2, 3, 4
+
+SYNTH_DYADIC, SYNTH_UNIFORM, SYNTH_NORMAL, SYNTH_INT32R, SYNTH_KEY30, SYNTH_GAUSS01 = range(1, 7)
+
+HLL_NUM_WORDS = 52
+
+# Every symbol include/dq.h declares (checked by tests/test_native_abi.py).
+EXPORTED_SYMBOLS = (
+    "dq_abi_version", "dq_open", "dq_close", "dq_last_error", "dq_set_stream", "dq_synchronize", "dq_scan",
+    "dq_scan_launch_count", "dq_state_merge", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
+    "dq_freq_summarize", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_synth_column", "dq_synth_validity",
+)
+
+
+class DqColumn(ctypes.Structure):
+    _fields_ = [("spark_type", ctypes.c_int32), ("flags", ctypes.c_uint32), ("length", ctypes.c_int64),
+                ("values", ctypes.c_void_p), ("validity", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("decimal_precision", ctypes.c_int32), ("decimal_scale", ctypes.c_int32)]
+
+
+class DqConst(ctypes.Structure):
+    _fields_ = [("tag", ctypes.c_int32), ("str_len", ctypes.c_int32), ("i64", ctypes.c_int64),
+                ("f64", ctypes.c_double), ("str_offset", ctypes.c_int64)]
+
+
+class DqPredicate(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_void_p), ("code_len", ctypes.c_int32), ("n_consts", ctypes.c_int32),
+                ("consts", ctypes.c_void_p), ("strings", ctypes.c_void_p), ("strings_len", ctypes.c_int64)]
+
+
+class DqOp(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("column", ctypes.c_int32 * 2), ("where", ctypes.c_int32),
+                ("predicate", ctypes.c_int32)]
+
+
+class _NumMatches(ctypes.Structure):
+    _fields_ = [("num_matches", ctypes.c_int64)]
+
+
+class _NumMatchesAndCount(ctypes.Structure):
+    _fields_ = [("num_matches", ctypes.c_int64), ("count", ctypes.c_int64)]
+
+
+class _Mean(ctypes.Structure):
+    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64)]
+
+
+class _Dbl(ctypes.Structure):
+    _fields_ = [("value", ctypes.c_double)]
+
+
+class _StdDev(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_double), ("avg", ctypes.c_double), ("m2", ctypes.c_double)]
+
+
+class _Corr(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_double), ("x_avg", ctypes.c_double), ("y_avg", ctypes.c_double),
+                ("ck", ctypes.c_double), ("x_mk", ctypes.c_double), ("y_mk", ctypes.c_double)]
+
+
+class _Hll(ctypes.Structure):
+    _fields_ = [("words", ctypes.c_int64 * HLL_NUM_WORDS)]
+
+
+class _DataType(ctypes.Structure):
+    _fields_ = [("num_null", ctypes.c_int64), ("num_fractional", ctypes.c_int64), ("num_integral", ctypes.c_int64),
+                ("num_boolean", ctypes.c_int64), ("num_string", ctypes.c_int64)]
+
+
+class _StateUnion(ctypes.Union):
+    _fields_ = [("num_matches", _NumMatches), ("num_matches_and_count", _NumMatchesAndCount), ("mean", _Mean),
+                ("dbl", _Dbl), ("stddev", _StdDev), ("corr", _Corr), ("hll", _Hll), ("datatype", _DataType)]
+
+
+class DqState(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("present", ctypes.c_int32), ("u", _StateUnion)]
+
+
+class DqFreqSummary(ctypes.Structure):
+    _fields_ = [("num_rows", ctypes.c_int64), ("num_groups", ctypes.c_int64), ("num_unique", ctypes.c_int64),
+                ("entropy", ctypes.c_double), ("entropy_rows", ctypes.c_int64), ("max_count", ctypes.c_int64)]
+
+
+STATE_SIZE = ctypes.sizeof(DqState)
+
+
+class NativeError(RuntimeError):
+    """A failed libdq call (status code + dq_last_error message)."""
+
+    def __init__(self, status, message):
+        self.status = status
+        super().__init__("%s: %s" % (STATUS_NAMES.get(status, status), message))
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path=None):
+    """Load libdq.so and declare its prototypes. Raises if the library was not built."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise NativeError(-5, "libdq.so not found at %s: run __graft_entry__.build() (no CPU fallback exists)" % p)
+        lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+        c_void_p, c_int, c_int64, c_uint32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32
+        sig = {
+            "dq_abi_version": (c_int, []),
+            "dq_open": (c_void_p, [c_int, ctypes.POINTER(c_int)]),
+            "dq_close": (None, [c_void_p]),
+            "dq_last_error": (ctypes.c_char_p, [c_void_p]),
+            "dq_set_stream": (c_int, [c_void_p, c_void_p]),
+            "dq_synchronize": (c_int, [c_void_p]),
+            "dq_scan": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                c_uint32]),
+            "dq_scan_launch_count": (c_int64, [c_void_p]),
+            "dq_state_merge": (c_int, [c_void_p, c_void_p, c_void_p]),
+            "dq_hll_count": (ctypes.c_double, [c_void_p]),
+            "dq_spark_hash64": (c_int64, [ctypes.c_int32, c_void_p, c_int64]),
+            "dq_frequencies": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_uint32, c_void_p]),
+            "dq_freq_summarize": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+            "dq_freq_top": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+            "dq_freq_export": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+            "dq_freq_free": (None, [c_void_p, c_void_p]),
+            "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
+            "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def hll_count(words):
+    """DeequHyperLogLogPlusPlusUtils.count over 52 packed register words (host-side, C-ABI)."""
+    lib = load_library()
+    arr = (ctypes.c_int64 * HLL_NUM_WORDS)(*[int(np.int64(np.uint64(w & 0xFFFFFFFFFFFFFFFF))) for w in words])
+    return lib.dq_hll_count(arr)
+
+
+def spark_hash64(spark_type, value):
+    """Spark XxHash64Function.hash(value, type, 42) as a signed 64-bit int (test hook)."""
+    lib = load_library()
+    if spark_type == TYPE_STRING:
+        b = value.encode("utf-8") if isinstance(value, str) else bytes(value)
+        buf = ctypes.create_string_buffer(b, len(b))
+        return lib.dq_spark_hash64(spark_type, buf, len(b))
+    dtype = {TYPE_BOOLEAN: np.uint8, TYPE_BYTE: np.int8, TYPE_SHORT: np.int16, TYPE_INT: np.int32,
+             TYPE_DATE: np.int32, TYPE_LONG: np.int64, TYPE_TIMESTAMP: np.int64, TYPE_DECIMAL: np.int64,
+             TYPE_FLOAT: np.float32, TYPE_DOUBLE: np.float64}[spark_type]
+    a = np.array([value], dtype=dtype)
+    return lib.dq_spark_hash64(spark_type, a.ctypes.data, a.nbytes)
+
+
+def merge_states(a, b):
+    """State.sum through the C-ABI (dq_state_merge)."""
+    lib = load_library()
+    out = DqState()
+    rc = lib.dq_state_merge(ctypes.byref(a), ctypes.byref(b), ctypes.byref(out))
+    if rc != DQ_OK:
+        raise NativeError(rc, "dq_state_merge")
+    return out
+
+
+class Context:
+    """One dq_ctx bound to one GPU (one per process / rank)."""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        status = ctypes.c_int(0)
+        self.handle = self.lib.dq_open(int(device), ctypes.byref(status))
+        if not self.handle:
+            raise NativeError(status.value, "dq_open(%d) failed: a MI355X GPU is required" % device)
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self.lib.dq_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_error(self):
+        msg = self.lib.dq_last_error(self.handle)
+        return msg.decode() if msg else ""
+
+    def check(self, rc, what):
+        if rc != DQ_OK:
+            raise NativeError(rc, "%s: %s" % (what, self.last_error()))
+
+    def set_stream(self, stream_ptr):
+        self.check(self.lib.dq_set_stream(self.handle, ctypes.c_void_p(stream_ptr or 0)), "dq_set_stream")
+
+    def synchronize(self):
+        self.check(self.lib.dq_synchronize(self.handle), "dq_synchronize")
+
+    def scan_launch_count(self):
+        return self.lib.dq_scan_launch_count(self.handle)
+
+    def scan(self, columns, nrows, ops, preds, out_device_ptr=None):
+        """Run dq_scan. `columns`: list of DqColumn, `ops`: list of DqOp, `preds`: list of DqPredicate.
+        Returns a list of DqState (host) or None when writing to a device buffer."""
+        ncol = len(columns)
+        col_arr = (DqColumn * max(ncol, 1))(*columns)
+        op_arr = (DqOp * max(len(ops), 1))(*ops)
+        pred_arr = (DqPredicate * max(len(preds), 1))(*preds)
+        if out_device_ptr is not None:
+            rc = self.lib.dq_scan(self.handle, col_arr, ncol, int(nrows), op_arr, len(ops), pred_arr, len(preds),
+                                  ctypes.c_void_p(out_device_ptr), SCAN_OUT_DEVICE)
+            self.check(rc, "dq_scan")
+            return None
+        out = (DqState * max(len(ops), 1))()
+        rc = self.lib.dq_scan(self.handle, col_arr, ncol, int(nrows), op_arr, len(ops), pred_arr, len(preds), out, 0)
+        self.check(rc, "dq_scan")
+        return [out[i] for i in range(len(ops))]
+
+    def synth_column(self, kind, seed, row0, nrows, dev_ptr):
+        self.check(self.lib.dq_synth_column(self.handle, kind, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows,
+                                            ctypes.c_void_p(dev_ptr)), "dq_synth_column")
+
+    def synth_validity(self, seed, row0, nrows, null_permille, dev_ptr):
+        self.check(self.lib.dq_synth_validity(self.handle, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows, null_permille,
+                                              ctypes.c_void_p(dev_ptr)), "dq_synth_validity")
+
+
+_contexts = {}
+
+
+def context(device=0):
+    """Process-wide cached context for a device."""
+    ctx = _contexts.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _contexts[device] = ctx
+    return ctx

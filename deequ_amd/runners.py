@@ -1,0 +1,274 @@
+"""AnalysisRunner / AnalysisRunBuilder / AnalyzerContext / state providers — the deequ runner API
+(R/AnalysisRunner.scala, R/AnalysisRunBuilder.scala, R/AnalyzerContext.scala, A/StateProvider.scala)
+driving the MI355X engine. The scan-shareable analyzers of a run become ONE dq_scan call (one fused
+pass over HBM), exactly where the reference issues one `data.agg(...)` Spark job."""
+import json
+
+from . import native as N
+from . import engine
+from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer,
+                        FrequencyBasedAnalyzer, Preconditions, Size, computeFrequencies)
+from .expr import compile_predicate
+from .metrics import DoubleMetric, Success
+
+
+class ScanBatch:
+    """The dq_op list of one fused scan: deduplicated ops, predicates compiled once per string."""
+
+    def __init__(self, data):
+        self.data = data
+        self.names = list(data.columns)
+        self.col_index = {n: i for i, n in enumerate(self.names)}
+        self.preds = []
+        self.pred_index = {}
+        self.ops = []
+        self.op_index = {}
+
+    def predicate(self, text):
+        if text not in self.pred_index:
+            self.preds.append(compile_predicate(text, self.col_index))
+            self.pred_index[text] = len(self.preds) - 1
+        return self.pred_index[text]
+
+    def add_op(self, kind, columns=(), where=None, predicate=None):
+        cols = [self.col_index[c] if c in self.col_index else -1 for c in columns]
+        for c, name in zip(cols, columns):
+            if c < 0:
+                from .metrics import NoSuchColumnException
+                raise NoSuchColumnException("Input data does not include column %s!" % name)
+        w = self.predicate(where) if where is not None else -1
+        p = self.predicate(predicate) if predicate is not None else -1
+        key = (kind, tuple(cols), w, p)
+        if key not in self.op_index:
+            op = N.DqOp()
+            op.kind = kind
+            op.column[0] = cols[0] if len(cols) > 0 else -1
+            op.column[1] = cols[1] if len(cols) > 1 else -1
+            op.where = w
+            op.predicate = p
+            self.ops.append(op)
+            self.op_index[key] = len(self.ops) - 1
+        return self.op_index[key]
+
+    def native_columns(self):
+        return [self.data[n].native() for n in self.names]
+
+    def run(self, out_device_ptr=None):
+        if not self.ops:
+            return []
+        return engine.ctx().scan(self.native_columns(), self.data.nrows, self.ops,
+                                 [p.to_native() for p in self.preds], out_device_ptr=out_device_ptr)
+
+
+class AnalyzerContext:
+    """R/AnalyzerContext.scala:29-105."""
+
+    def __init__(self, metricMap=None):
+        self.metricMap = dict(metricMap or {})
+
+    @staticmethod
+    def empty():
+        return AnalyzerContext()
+
+    @property
+    def allMetrics(self):
+        return list(self.metricMap.values())
+
+    def metric(self, analyzer):
+        return self.metricMap.get(analyzer)
+
+    def __add__(self, other):  # `++`: right-hand side wins
+        m = dict(self.metricMap)
+        m.update(other.metricMap)
+        return AnalyzerContext(m)
+
+    @staticmethod
+    def successMetricsAsJson(analyzerContext, forAnalyzers=()):
+        rows = []
+        for a, m in analyzerContext.metricMap.items():
+            if forAnalyzers and a not in forAnalyzers:
+                continue
+            if not m.value.isSuccess:
+                continue
+            for dm in m.flatten():
+                rows.append({"entity": str(dm.entity), "instance": dm.instance, "name": dm.name,
+                             "value": dm.value.get()})
+        return json.dumps(rows)
+
+
+class InMemoryStateProvider:
+    """A/StateProvider.scala:47-69."""
+
+    def __init__(self):
+        self.states = {}
+
+    def load(self, analyzer):
+        return self.states.get(analyzer)
+
+    def persist(self, analyzer, state):
+        self.states[analyzer] = state
+
+
+class Analysis:
+    """A/Analysis.scala: a list of analyzers (deprecated entry point kept for the reference tests)."""
+
+    def __init__(self, analyzers=None):
+        self.analyzers = list(analyzers or [])
+
+    def addAnalyzer(self, analyzer):
+        return Analysis(self.analyzers + [analyzer])
+
+    def addAnalyzers(self, analyzers):
+        return Analysis(self.analyzers + list(analyzers))
+
+    def run(self, data, aggregateWith=None, saveStatesWith=None):
+        return AnalysisRunner.doAnalysisRun(data, self.analyzers, aggregateWith, saveStatesWith)
+
+
+class AnalysisRunBuilder:
+    """R/AnalysisRunBuilder.scala:27-116."""
+
+    def __init__(self, data):
+        self.data = data
+        self.analyzers = []
+        self._aggregateWith = None
+        self._saveStatesWith = None
+
+    def addAnalyzer(self, analyzer):
+        self.analyzers.append(analyzer)
+        return self
+
+    def addAnalyzers(self, analyzers):
+        self.analyzers.extend(analyzers)
+        return self
+
+    def aggregateWith(self, stateLoader):
+        self._aggregateWith = stateLoader
+        return self
+
+    def saveStatesWith(self, statePersister):
+        self._saveStatesWith = statePersister
+        return self
+
+    def run(self):
+        return AnalysisRunner.doAnalysisRun(self.data, self.analyzers, self._aggregateWith, self._saveStatesWith)
+
+
+class AnalysisRunner:
+    """R/AnalysisRunner.scala:46-548."""
+
+    @staticmethod
+    def onData(data):
+        return AnalysisRunBuilder(data)
+
+    @staticmethod
+    def run(data, analysis, aggregateWith=None, saveStatesWith=None):
+        return AnalysisRunner.doAnalysisRun(data, analysis.analyzers, aggregateWith, saveStatesWith)
+
+    @staticmethod
+    def doAnalysisRun(data, analyzers, aggregateWith=None, saveStatesWith=None):
+        """R/AnalysisRunner.scala:97-203 (repository reuse and file output are out of scope)."""
+        if not analyzers:
+            return AnalyzerContext.empty()
+        allAnalyzers = []
+        for a in analyzers:  # VerificationSuite does not dedupe; the result map does
+            if a not in allAnalyzers:
+                allAnalyzers.append(a)
+        passed = [a for a in allAnalyzers if Preconditions.findFirstFailing(data.schema, a.preconditions()) is None]
+        failed = [a for a in allAnalyzers if a not in passed]
+        preconditionFailures = AnalyzerContext(
+            {a: a.toFailureMetric(Preconditions.findFirstFailing(data.schema, a.preconditions())) for a in failed})
+        grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
+        scanning = [a for a in passed if not isinstance(a, GroupingAnalyzer)]
+        nonGrouped = AnalysisRunner._runScanningAnalyzers(data, scanning, aggregateWith, saveStatesWith)
+        grouped = AnalyzerContext.empty()
+        by_cols = {}
+        for a in grouping:
+            by_cols.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
+        for cols, group in by_cols.items():
+            _, metrics = AnalysisRunner._runGroupingAnalyzers(data, list(cols), group, aggregateWith, saveStatesWith)
+            grouped = grouped + metrics
+        return preconditionFailures + nonGrouped + grouped
+
+    @staticmethod
+    def _runScanningAnalyzers(data, analyzers, aggregateWith=None, saveStatesTo=None):
+        """R/AnalysisRunner.scala:289-336: one fused dq_scan for all shareable analyzers."""
+        shareable = [a for a in analyzers if isinstance(a, ScanShareableAnalyzer)]
+        others = [a for a in analyzers if not isinstance(a, ScanShareableAnalyzer)]
+        results = {}
+        if shareable:
+            try:
+                batch = ScanBatch(data)
+                offsets = [a.addOps(batch) for a in shareable]
+                states = batch.run()
+                for a, ops in zip(shareable, offsets):
+                    try:
+                        results[a] = a.metricFromAggregationResult(states, ops, aggregateWith, saveStatesTo)
+                    except Exception as e:  # successOrFailureMetricFrom (:340-353)
+                        results[a] = a.toFailureMetric(e)
+            except Exception as e:  # any failure of the shared aggregation fails every analyzer (:320-323)
+                for a in shareable:
+                    results[a] = a.toFailureMetric(e)
+        for a in others:
+            results[a] = a.calculate(data, aggregateWith, saveStatesTo)
+        return AnalyzerContext(results)
+
+    @staticmethod
+    def _runGroupingAnalyzers(data, groupingColumns, analyzers, aggregateWith=None, saveStatesTo=None):
+        """R/AnalysisRunner.scala:259-287 (+ runAnalyzersForParticularGrouping :480-548)."""
+        try:
+            freq = computeFrequencies(data, groupingColumns)
+        except Exception as e:
+            return 0, AnalyzerContext({a: a.toFailureMetric(e) for a in analyzers})
+        if aggregateWith is not None:
+            prev = aggregateWith.load(analyzers[0])
+            if prev is not None:
+                freq = freq.sum(prev)
+        ctx = AnalysisRunner._runAnalyzersForParticularGrouping(freq, analyzers, saveStatesTo)
+        return freq.numRows, ctx
+
+    @staticmethod
+    def _runAnalyzersForParticularGrouping(freq, analyzers, saveStatesTo=None):
+        results = {}
+        for a in analyzers:
+            try:
+                results[a] = a.computeMetricFrom(freq)
+            except Exception as e:
+                results[a] = a.toFailureMetric(e)
+        if saveStatesTo is not None:
+            saveStatesTo.persist(analyzers[0], freq)
+        return AnalyzerContext(results)
+
+    @staticmethod
+    def runOnAggregatedStates(schema, analysis, stateLoaders, saveStatesWith=None):
+        """R/AnalysisRunner.scala:385-460: metrics from merged persisted states, no data scan."""
+        if not analysis.analyzers or not stateLoaders:
+            return AnalyzerContext.empty()
+        analyzers = analysis.analyzers
+        passed = [a for a in analyzers if Preconditions.findFirstFailing(schema, a.preconditions()) is None]
+        failed = [a for a in analyzers if a not in passed]
+        pre = AnalyzerContext({a: a.toFailureMetric(Preconditions.findFirstFailing(schema, a.preconditions()))
+                               for a in failed})
+        agg = InMemoryStateProvider()
+        for a in passed:
+            for loader in stateLoaders:
+                a.aggregateStateTo(agg, loader, agg)
+        grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
+        scanning = [a for a in passed if not isinstance(a, GroupingAnalyzer)]
+        res = {}
+        for a in scanning:
+            m = a.loadStateAndComputeMetric(agg)
+            if saveStatesWith is not None:
+                a.copyStateTo(agg, saveStatesWith)
+            if m is not None:
+                res[a] = m
+        by_cols = {}
+        for a in grouping:
+            by_cols.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
+        out = pre + AnalyzerContext(res)
+        for cols, group in by_cols.items():
+            states = [agg.load(a) for a in group if agg.load(a) is not None]
+            if not states:
+                raise ValueError("requirement failed")
+            out = out + AnalysisRunner._runAnalyzersForParticularGrouping(states[0], group, saveStatesWith)
+        return out

@@ -1,0 +1,285 @@
+"""deequ's states: commutative semigroups of sufficient statistics (A/Analyzer.scala:29-48), with
+conversion from the C-ABI dq_state records. Each `sum` follows the reference state's own file."""
+import math
+
+import numpy as np
+
+from . import native as N
+
+
+class State:
+    def sum(self, other):
+        raise NotImplementedError
+
+    def __add__(self, other):
+        return self.sum(other)
+
+
+class DoubleValuedState(State):
+    def metricValue(self):
+        raise NotImplementedError
+
+
+class NumMatches(DoubleValuedState):
+    """A/Size.scala:23-31."""
+
+    def __init__(self, numMatches):
+        self.numMatches = int(numMatches)
+
+    def sum(self, other):
+        return NumMatches(self.numMatches + other.numMatches)
+
+    def metricValue(self):
+        return float(self.numMatches)
+
+    def __eq__(self, o):
+        return isinstance(o, NumMatches) and o.numMatches == self.numMatches
+
+    def __repr__(self):
+        return "NumMatches(%d)" % self.numMatches
+
+
+class NumMatchesAndCount(DoubleValuedState):
+    """A/Analyzer.scala:230-244."""
+
+    def __init__(self, numMatches, count):
+        self.numMatches, self.count = int(numMatches), int(count)
+
+    def sum(self, other):
+        return NumMatchesAndCount(self.numMatches + other.numMatches, self.count + other.count)
+
+    def metricValue(self):
+        return float("nan") if self.count == 0 else self.numMatches / self.count
+
+    def __eq__(self, o):
+        return isinstance(o, NumMatchesAndCount) and (o.numMatches, o.count) == (self.numMatches, self.count)
+
+    def __repr__(self):
+        return "NumMatchesAndCount(%d,%d)" % (self.numMatches, self.count)
+
+
+class MeanState(DoubleValuedState):
+    """A/Mean.scala:25-34."""
+
+    def __init__(self, sum_, count):
+        self.sum_, self.count = float(sum_), int(count)
+
+    def sum(self, other):
+        return MeanState(self.sum_ + other.sum_, self.count + other.count)
+
+    def metricValue(self):
+        return float("nan") if self.count == 0 else self.sum_ / self.count
+
+    def __eq__(self, o):
+        return isinstance(o, MeanState) and (o.sum_, o.count) == (self.sum_, self.count)
+
+    def __repr__(self):
+        return "MeanState(%r,%d)" % (self.sum_, self.count)
+
+
+class SumState(DoubleValuedState):
+    """A/Sum.scala:25-33."""
+
+    def __init__(self, sum_):
+        self.sum_ = float(sum_)
+
+    def sum(self, other):
+        return SumState(self.sum_ + other.sum_)
+
+    def metricValue(self):
+        return self.sum_
+
+    def __eq__(self, o):
+        return isinstance(o, SumState) and o.sum_ == self.sum_
+
+    def __repr__(self):
+        return "SumState(%r)" % self.sum_
+
+
+def _java_min(a, b):
+    if math.isnan(a) or math.isnan(b):
+        return float("nan")
+    if a == 0.0 and b == 0.0:
+        return a if math.copysign(1, a) < 0 else b
+    return a if a <= b else b
+
+
+def _java_max(a, b):
+    if math.isnan(a) or math.isnan(b):
+        return float("nan")
+    if a == 0.0 and b == 0.0:
+        return b if math.copysign(1, a) < 0 else a
+    return a if a >= b else b
+
+
+class MinState(DoubleValuedState):
+    """A/Minimum.scala:25-33 (merge = math.min)."""
+
+    def __init__(self, minValue):
+        self.minValue = float(minValue)
+
+    def sum(self, other):
+        return MinState(_java_min(self.minValue, other.minValue))
+
+    def metricValue(self):
+        return self.minValue
+
+    def __eq__(self, o):
+        return isinstance(o, MinState) and o.minValue == self.minValue
+
+    def __repr__(self):
+        return "MinState(%r)" % self.minValue
+
+
+class MaxState(DoubleValuedState):
+    """A/Maximum.scala:25-33 (merge = math.max)."""
+
+    def __init__(self, maxValue):
+        self.maxValue = float(maxValue)
+
+    def sum(self, other):
+        return MaxState(_java_max(self.maxValue, other.maxValue))
+
+    def metricValue(self):
+        return self.maxValue
+
+    def __eq__(self, o):
+        return isinstance(o, MaxState) and o.maxValue == self.maxValue
+
+    def __repr__(self):
+        return "MaxState(%r)" % self.maxValue
+
+
+class StandardDeviationState(DoubleValuedState):
+    """A/StandardDeviation.scala:25-45 (Chan merge)."""
+
+    def __init__(self, n, avg, m2):
+        if not n > 0.0:
+            raise ValueError("requirement failed: Standard deviation is undefined for n = 0.")
+        self.n, self.avg, self.m2 = float(n), float(avg), float(m2)
+
+    def metricValue(self):
+        return math.sqrt(self.m2 / self.n)
+
+    def sum(self, other):
+        newN = self.n + other.n
+        delta = other.avg - self.avg
+        deltaN = 0.0 if newN == 0.0 else delta / newN
+        return StandardDeviationState(newN, self.avg + deltaN * other.n,
+                                      self.m2 + other.m2 + delta * deltaN * self.n * other.n)
+
+    def __eq__(self, o):
+        return isinstance(o, StandardDeviationState) and (o.n, o.avg, o.m2) == (self.n, self.avg, self.m2)
+
+    def __repr__(self):
+        return "StandardDeviationState(%r,%r,%r)" % (self.n, self.avg, self.m2)
+
+
+class CorrelationState(DoubleValuedState):
+    """A/Correlation.scala:26-57."""
+
+    def __init__(self, n, xAvg, yAvg, ck, xMk, yMk):
+        if not n > 0.0:
+            raise ValueError("requirement failed: Correlation undefined for n = 0.")
+        self.n, self.xAvg, self.yAvg, self.ck, self.xMk, self.yMk = map(float, (n, xAvg, yAvg, ck, xMk, yMk))
+
+    def sum(self, other):
+        n1, n2 = self.n, other.n
+        newN = n1 + n2
+        dx = other.xAvg - self.xAvg
+        dxN = 0.0 if newN == 0.0 else dx / newN
+        dy = other.yAvg - self.yAvg
+        dyN = 0.0 if newN == 0.0 else dy / newN
+        return CorrelationState(newN, self.xAvg + dxN * n2, self.yAvg + dyN * n2,
+                                self.ck + other.ck + dx * dyN * n1 * n2,
+                                self.xMk + other.xMk + dx * dxN * n1 * n2,
+                                self.yMk + other.yMk + dy * dyN * n1 * n2)
+
+    def metricValue(self):
+        d = math.sqrt(self.xMk * self.yMk)
+        if d == 0.0:
+            return float("nan") if self.ck == 0.0 else math.copysign(float("inf"), self.ck)
+        return self.ck / d
+
+    def __eq__(self, o):
+        return isinstance(o, CorrelationState) and \
+            (o.n, o.xAvg, o.yAvg, o.ck, o.xMk, o.yMk) == (self.n, self.xAvg, self.yAvg, self.ck, self.xMk, self.yMk)
+
+    def __repr__(self):
+        return "CorrelationState(%r,%r,%r,%r,%r,%r)" % (self.n, self.xAvg, self.yAvg, self.ck, self.xMk, self.yMk)
+
+
+def hll_merge(w1, w2):
+    """DeequHyperLogLogPlusPlusUtils.merge (C/StatefulHyperloglogPlus.scala:188-208)."""
+    out = []
+    idx = 0
+    for a, b in zip(w1, w2):
+        a &= 0xFFFFFFFFFFFFFFFF
+        b &= 0xFFFFFFFFFFFFFFFF
+        word, mask = 0, 63
+        i = 0
+        while idx < 512 and i < 10:
+            word |= max(a & mask, b & mask)
+            mask <<= 6
+            i += 1
+            idx += 1
+        out.append(word)
+    return out
+
+
+class ApproxCountDistinctState(DoubleValuedState):
+    """A/ApproxCountDistinct.scala:26-41: 52 words of 6-bit HLL++ registers (P = 9)."""
+
+    def __init__(self, words):
+        self.words = [int(w) & 0xFFFFFFFFFFFFFFFF for w in words]
+
+    def sum(self, other):
+        return ApproxCountDistinctState(hll_merge(self.words, other.words))
+
+    def metricValue(self):
+        return N.hll_count(self.words)
+
+    def registers(self):
+        regs = []
+        for w in self.words:
+            for k in range(10):
+                if len(regs) < 512:
+                    regs.append((w >> (6 * k)) & 63)
+        return regs
+
+    def __eq__(self, o):
+        return isinstance(o, ApproxCountDistinctState) and o.words == self.words
+
+    def __repr__(self):
+        return "ApproxCountDistinctState(%s)" % ",".join(str(np.int64(np.uint64(w))) for w in self.words)
+
+
+def state_from_native(st):
+    """dq_state -> reference State (None for an absent state, i.e. ifNoNullsIn failed)."""
+    if not st.present:
+        return None
+    k = st.kind
+    u = st.u
+    if k == N.OP_SIZE:
+        return NumMatches(u.num_matches.num_matches)
+    if k in (N.OP_COMPLETENESS, N.OP_COMPLIANCE):
+        return NumMatchesAndCount(u.num_matches_and_count.num_matches, u.num_matches_and_count.count)
+    if k == N.OP_MEAN:
+        return MeanState(u.mean.sum, u.mean.count)
+    if k == N.OP_SUM:
+        return SumState(u.dbl.value)
+    if k in (N.OP_MINIMUM, N.OP_MIN_LENGTH):
+        return MinState(u.dbl.value)
+    if k in (N.OP_MAXIMUM, N.OP_MAX_LENGTH):
+        return MaxState(u.dbl.value)
+    if k == N.OP_STANDARD_DEVIATION:
+        if u.stddev.n == 0.0:
+            return None
+        return StandardDeviationState(u.stddev.n, u.stddev.avg, u.stddev.m2)
+    if k == N.OP_CORRELATION:
+        if not u.corr.n > 0.0:
+            return None
+        return CorrelationState(u.corr.n, u.corr.x_avg, u.corr.y_avg, u.corr.ck, u.corr.x_mk, u.corr.y_mk)
+    if k == N.OP_APPROX_COUNT_DISTINCT:
+        return ApproxCountDistinctState(list(u.hll.words))
+    raise ValueError("unknown state kind %d" % k)

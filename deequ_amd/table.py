@@ -1,0 +1,336 @@
+"""Columnar batches in the layout the C-ABI takes (Arrow-style buffers + the Spark physical type).
+
+This stands where deequ takes a Spark DataFrame (`AnalysisRunner.onData(df)`,
+R/AnalysisRunner.scala:51-53). A Table holds named columns; each column is a values buffer,
+an LSB-first validity bitmap (None = no nulls) and, for strings, int32 offsets into UTF-8 data.
+`Table.to_device()` moves the buffers into HBM (torch is used only as the device allocator) so
+repeated runs read device-resident data, as the benchmark does.
+"""
+import csv
+import math
+import re
+from collections import OrderedDict
+
+import numpy as np
+
+from . import native as N
+
+SPARK_TYPE_NAMES = {
+    N.TYPE_BOOLEAN: "BooleanType", N.TYPE_BYTE: "ByteType", N.TYPE_SHORT: "ShortType",
+    N.TYPE_INT: "IntegerType", N.TYPE_LONG: "LongType", N.TYPE_FLOAT: "FloatType",
+    N.TYPE_DOUBLE: "DoubleType", N.TYPE_STRING: "StringType", N.TYPE_DATE: "DateType",
+    N.TYPE_TIMESTAMP: "TimestampType", N.TYPE_DECIMAL: "DecimalType",
+}
+_NAME_TO_TYPE = {v.lower().replace("type", ""): k for k, v in SPARK_TYPE_NAMES.items()}
+_NAME_TO_TYPE.update({"int": N.TYPE_INT, "bigint": N.TYPE_LONG, "bool": N.TYPE_BOOLEAN, "str": N.TYPE_STRING,
+                      "float64": N.TYPE_DOUBLE, "float32": N.TYPE_FLOAT, "int64": N.TYPE_LONG,
+                      "int32": N.TYPE_INT, "int16": N.TYPE_SHORT, "int8": N.TYPE_BYTE})
+
+NUMPY_OF = {N.TYPE_BOOLEAN: np.uint8, N.TYPE_BYTE: np.int8, N.TYPE_SHORT: np.int16, N.TYPE_INT: np.int32,
+            N.TYPE_LONG: np.int64, N.TYPE_FLOAT: np.float32, N.TYPE_DOUBLE: np.float64, N.TYPE_DATE: np.int32,
+            N.TYPE_TIMESTAMP: np.int64, N.TYPE_DECIMAL: np.int64}
+
+NUMERIC_TYPES = (N.TYPE_BYTE, N.TYPE_SHORT, N.TYPE_INT, N.TYPE_LONG, N.TYPE_FLOAT, N.TYPE_DOUBLE, N.TYPE_DECIMAL)
+
+
+def spark_type_of(name_or_code):
+    if isinstance(name_or_code, int):
+        return name_or_code
+    key = str(name_or_code).lower().replace("type", "")
+    key = re.sub(r"\(.*\)", "", key)
+    if key not in _NAME_TO_TYPE:
+        raise ValueError("unknown Spark type %r" % name_or_code)
+    return _NAME_TO_TYPE[key]
+
+
+def pack_validity(mask):
+    """bool mask (True = non-null) -> Arrow LSB-first bitmap (uint8), padded to 8-byte multiples."""
+    mask = np.asarray(mask, dtype=bool)
+    bits = np.packbits(mask, bitorder="little")
+    pad = (-len(bits)) % 8
+    if pad:
+        bits = np.concatenate([bits, np.zeros(pad, dtype=np.uint8)])
+    return bits
+
+
+def unpack_validity(bitmap, n):
+    if bitmap is None:
+        return np.ones(n, dtype=bool)
+    return np.unpackbits(np.asarray(bitmap, dtype=np.uint8), bitorder="little", count=n).astype(bool)
+
+
+class Column:
+    """One column: Spark type, values, optional validity bitmap, optional string offsets."""
+
+    def __init__(self, name, spark_type, values, validity=None, offsets=None, decimal_precision=0,
+                 decimal_scale=0, length=None):
+        self.name = name
+        self.spark_type = spark_type_of(spark_type)
+        self.values = values
+        self.validity = validity
+        self.offsets = offsets
+        self.decimal_precision = decimal_precision
+        self.decimal_scale = decimal_scale
+        if length is None:
+            length = len(offsets) - 1 if self.spark_type == N.TYPE_STRING else len(values)
+        self.length = int(length)
+        self.device = None  # dict of torch tensors once resident in HBM
+
+    @property
+    def type_name(self):
+        n = SPARK_TYPE_NAMES[self.spark_type]
+        if self.spark_type == N.TYPE_DECIMAL:
+            return "DecimalType(%d,%d)" % (self.decimal_precision, self.decimal_scale)
+        return n
+
+    def is_numeric(self):
+        return self.spark_type in NUMERIC_TYPES
+
+    def null_mask(self):
+        return ~unpack_validity(self.validity, self.length)
+
+    def to_pylist(self):
+        """Python values with None for nulls (host-side formatting only, e.g. Histogram keys)."""
+        valid = unpack_validity(self.validity, self.length)
+        out = []
+        for i in range(self.length):
+            out.append(self.value_at(i) if valid[i] else None)
+        return out
+
+    def value_at(self, i):
+        if self.spark_type == N.TYPE_STRING:
+            o = self.offsets
+            return bytes(self.values[o[i]:o[i + 1]]).decode("utf-8")
+        v = self.values[i]
+        if self.spark_type == N.TYPE_BOOLEAN:
+            return bool(v)
+        if self.spark_type in (N.TYPE_FLOAT, N.TYPE_DOUBLE):
+            return float(v)
+        if self.spark_type == N.TYPE_DECIMAL:
+            return int(v) / (10 ** self.decimal_scale)
+        return int(v)
+
+    def native(self):
+        """DqColumn for the C-ABI (device pointers when resident in HBM)."""
+        c = N.DqColumn()
+        c.spark_type = self.spark_type
+        c.length = self.length
+        c.decimal_precision = self.decimal_precision
+        c.decimal_scale = self.decimal_scale
+        if self.device is not None:
+            c.flags = N.COL_DEVICE
+            c.values = self.device["values"].data_ptr() if self.device.get("values") is not None else None
+            c.validity = self.device["validity"].data_ptr() if self.device.get("validity") is not None else None
+            c.offsets = self.device["offsets"].data_ptr() if self.device.get("offsets") is not None else None
+        else:
+            c.flags = 0
+            c.values = self.values.ctypes.data if self.values is not None and len(self.values) else None
+            c.validity = self.validity.ctypes.data if self.validity is not None else None
+            c.offsets = self.offsets.ctypes.data if self.offsets is not None else None
+        return c
+
+
+def _column_from_pylist(name, spark_type, items):
+    t = spark_type_of(spark_type)
+    n = len(items)
+    mask = np.array([x is not None and not (isinstance(x, float) and math.isnan(x) and t == N.TYPE_STRING)
+                     for x in items], dtype=bool)
+    validity = None if mask.all() else pack_validity(mask)
+    if t == N.TYPE_STRING:
+        enc = [("" if x is None else str(x)).encode("utf-8") for x in items]
+        offsets = np.zeros(n + 1, dtype=np.int32)
+        if n:
+            offsets[1:] = np.cumsum([len(b) for b in enc])
+        data = np.frombuffer(b"".join(enc), dtype=np.uint8).copy() if n else np.zeros(0, dtype=np.uint8)
+        return Column(name, t, data, validity, offsets, length=n)
+    if t == N.TYPE_DECIMAL:
+        from decimal import Decimal
+        vals = [Decimal(str(x)) if x is not None else Decimal(0) for x in items]
+        scale = max([max(0, -v.as_tuple().exponent) for v in vals] + [0])
+        unscaled = np.array([int(v.scaleb(scale)) for v in vals], dtype=np.int64)
+        prec = max([len(str(abs(int(u)))) for u in unscaled] + [1])
+        return Column(name, t, unscaled, validity, decimal_precision=max(prec, scale + 1), decimal_scale=scale)
+    dtype = NUMPY_OF[t]
+    fill = 0
+    vals = np.array([fill if x is None else x for x in items], dtype=dtype)
+    return Column(name, t, vals, validity)
+
+
+class Table:
+    """Named columns of equal length (the DataFrame stand-in of the drop-in API)."""
+
+    def __init__(self, columns):
+        self.columns = OrderedDict()
+        n = None
+        for c in columns:
+            if n is not None and c.length != n:
+                raise ValueError("column %s has %d rows, expected %d" % (c.name, c.length, n))
+            n = c.length
+            self.columns[c.name] = c
+        self.nrows = n or 0
+
+    # ---- constructors ---------------------------------------------------------------------------
+    @classmethod
+    def from_rows(cls, rows, names, types=None):
+        """Like Spark's `Seq((..),(..)).toDF(names...)`: None is null; types default from values."""
+        cols = []
+        for j, name in enumerate(names):
+            items = [r[j] for r in rows]
+            t = types[j] if types else _infer_py_type(items)
+            cols.append(_column_from_pylist(name, t, items))
+        return cls(cols)
+
+    @classmethod
+    def from_pydict(cls, data, types=None):
+        cols = []
+        for name, items in data.items():
+            t = (types or {}).get(name) or _infer_py_type(list(items))
+            cols.append(_column_from_pylist(name, t, list(items)))
+        return cls(cols)
+
+    @classmethod
+    def from_arrays(cls, arrays, types=None, validity=None):
+        """numpy arrays (fixed width) -> columns; `validity`: name -> bool mask."""
+        cols = []
+        for name, arr in arrays.items():
+            arr = np.ascontiguousarray(arr)
+            t = (types or {}).get(name)
+            if t is None:
+                t = {np.dtype(np.float64): N.TYPE_DOUBLE, np.dtype(np.float32): N.TYPE_FLOAT,
+                     np.dtype(np.int64): N.TYPE_LONG, np.dtype(np.int32): N.TYPE_INT,
+                     np.dtype(np.int16): N.TYPE_SHORT, np.dtype(np.int8): N.TYPE_BYTE,
+                     np.dtype(np.bool_): N.TYPE_BOOLEAN}[arr.dtype]
+            t = spark_type_of(t)
+            vals = arr.astype(NUMPY_OF[t]) if t != N.TYPE_BOOLEAN else arr.astype(np.uint8)
+            vm = (validity or {}).get(name)
+            cols.append(Column(name, t, vals, pack_validity(vm) if vm is not None else None))
+        return cls(cols)
+
+    @classmethod
+    def from_csv(cls, path, header=True, infer_schema=True):
+        """CSV -> Table with Spark 2.2 CSV `inferSchema` typing (empty field = null)."""
+        with open(path, newline="") as f:
+            rows = list(csv.reader(f))
+        names = rows[0] if header else ["_c%d" % i for i in range(len(rows[0]))]
+        body = rows[1:] if header else rows
+        cols = []
+        for j, name in enumerate(names):
+            raw = [(r[j] if j < len(r) else "") for r in body]
+            items = [None if x == "" else x for x in raw]
+            t = _csv_infer(items) if infer_schema else N.TYPE_STRING
+            if t == N.TYPE_STRING:
+                cols.append(_column_from_pylist(name, t, items))
+            elif t == N.TYPE_DOUBLE:
+                cols.append(_column_from_pylist(name, t, [None if x is None else float(x) for x in items]))
+            elif t == N.TYPE_BOOLEAN:
+                cols.append(_column_from_pylist(name, t, [None if x is None else x.lower() == "true" for x in items]))
+            else:
+                cols.append(_column_from_pylist(name, t, [None if x is None else int(x) for x in items]))
+        return cls(cols)
+
+    # ---- schema / access ------------------------------------------------------------------------
+    @property
+    def schema(self):
+        return OrderedDict((n, c.type_name) for n, c in self.columns.items())
+
+    @property
+    def fieldNames(self):
+        return list(self.columns)
+
+    def __getitem__(self, name):
+        return self.columns[name]
+
+    def __contains__(self, name):
+        return name in self.columns
+
+    def count(self):
+        return self.nrows
+
+    def select_rows(self, mask):
+        """Host-side row subset (test helper: builds partitions like parallelize(rows, numSlices))."""
+        mask = np.asarray(mask, dtype=bool)
+        out = []
+        for c in self.columns.values():
+            valid = unpack_validity(c.validity, c.length)[mask]
+            if c.spark_type == N.TYPE_STRING:
+                items = [c.value_at(i) for i in np.nonzero(mask)[0]]
+                items = [x if v else None for x, v in zip(items, valid)]
+                out.append(_column_from_pylist(c.name, c.spark_type, items))
+            else:
+                vals = c.values[mask]
+                nc = Column(c.name, c.spark_type, np.ascontiguousarray(vals),
+                            None if valid.all() else pack_validity(valid), decimal_precision=c.decimal_precision,
+                            decimal_scale=c.decimal_scale)
+                out.append(nc)
+        return Table(out)
+
+    def to_device(self, device=0):
+        """Copy every buffer into HBM (torch tensors as the allocator); runs then read device memory."""
+        import torch
+        dev = torch.device("cuda", device)
+        for c in self.columns.values():
+            d = {}
+            if c.spark_type == N.TYPE_STRING:
+                d["values"] = torch.from_numpy(np.concatenate([c.values, np.zeros(16, np.uint8)])).to(dev)
+                d["offsets"] = torch.from_numpy(c.offsets.astype(np.int32)).to(dev)
+            else:
+                d["values"] = torch.from_numpy(np.ascontiguousarray(c.values).view(np.uint8).copy()).to(dev)
+            if c.validity is not None:
+                d["validity"] = torch.from_numpy(pack_validity(unpack_validity(c.validity, c.length))).to(dev)
+            c.device = d
+        return self
+
+
+def _infer_py_type(items):
+    nn = [x for x in items if x is not None]
+    if not nn:
+        return N.TYPE_STRING
+    if all(isinstance(x, bool) for x in nn):
+        return N.TYPE_BOOLEAN
+    if all(isinstance(x, (int, np.integer)) and not isinstance(x, bool) for x in nn):
+        return N.TYPE_INT if all(-2 ** 31 <= int(x) < 2 ** 31 for x in nn) else N.TYPE_LONG
+    if all(isinstance(x, (int, float, np.integer, np.floating)) for x in nn):
+        return N.TYPE_DOUBLE
+    return N.TYPE_STRING
+
+
+_INT_RE = re.compile(r"^[+-]?\d+$")
+
+
+def _csv_infer(items):
+    """Spark 2.2 CSVInferSchema per column: Integer -> Long -> Decimal(p,0) -> Double -> Boolean -> String."""
+    rank = {None: 0, N.TYPE_INT: 1, N.TYPE_LONG: 2, N.TYPE_DOUBLE: 4, N.TYPE_BOOLEAN: 5, N.TYPE_STRING: 6}
+    cur = None
+    for x in items:
+        if x is None:
+            continue
+        t = _csv_field_type(x)
+        if cur is None:
+            cur = t
+        elif t != cur:
+            if {t, cur} <= {N.TYPE_INT, N.TYPE_LONG, N.TYPE_DOUBLE}:
+                cur = max(t, cur, key=lambda k: rank[k])
+            else:
+                cur = N.TYPE_STRING
+        if cur == N.TYPE_STRING:
+            break
+    return cur if cur is not None else N.TYPE_STRING
+
+
+def _csv_field_type(x):
+    if _INT_RE.match(x):
+        v = int(x)
+        if -2 ** 31 <= v < 2 ** 31:
+            return N.TYPE_INT
+        if -2 ** 63 <= v < 2 ** 63:
+            return N.TYPE_LONG
+        return N.TYPE_DOUBLE
+    try:
+        float(x)
+        if re.match(r"^[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?[dDfF]?$", x) or x in ("NaN", "Infinity", "-Infinity"):
+            return N.TYPE_DOUBLE
+    except ValueError:
+        pass
+    if x.lower() in ("true", "false"):
+        return N.TYPE_BOOLEAN
+    return N.TYPE_STRING

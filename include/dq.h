@@ -1,0 +1,256 @@
+/*
+ * dq.h — C-ABI of the MI355X-native deequ metrics engine (libdq.so).
+ *
+ * This is the drop-in boundary for deequ's AnalysisRunner hot path. The reference has no native
+ * code: the seams replaced here are Scala methods, cited per entry point. A JVM host binds these
+ * symbols over JNI; this repository's host mirror binds them over ctypes
+ * (deequ_amd/native.py).
+ *
+ * Conventions
+ *   - Plain C types only; no torch / HIP types cross this boundary (streams are `void*`).
+ *   - Every call returns 0 (DQ_OK) on success or a negative dq_status; dq_last_error(ctx) then
+ *     holds a message. A failed dq_scan fails EVERY op of the batch, mirroring the catch-all in
+ *     runScanningAnalyzers (R/AnalysisRunner.scala:320-323).
+ *   - A dq_ctx is bound to one GPU and is not re-entrant; use one ctx per process/rank.
+ *   - States are returned in native byte order (little-endian on x86/MI355X hosts) with the
+ *     field order of the reference's HdfsStateProvider layouts (A/StateProvider.scala:187-262).
+ *
+ * Path abbreviations: A/ = src/main/scala/com/amazon/deequ/analyzers/,
+ * R/ = A/runners/, C/ = A/catalyst/ (all under /root/reference).
+ */
+#ifndef DEEQU_AMD_DQ_H
+#define DEEQU_AMD_DQ_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQ_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------------------------------
+ * Status codes
+ * ------------------------------------------------------------------------------------------- */
+typedef enum dq_status {
+    DQ_OK = 0,
+    DQ_ERR_INVALID_ARGUMENT = -1,  /* bad op / column index / length mismatch          */
+    DQ_ERR_UNSUPPORTED = -2,       /* op not defined for this Spark type               */
+    DQ_ERR_DEVICE = -3,            /* HIP runtime error (message in dq_last_error)     */
+    DQ_ERR_OUT_OF_MEMORY = -4,
+    DQ_ERR_NO_DEVICE = -5,         /* no MI355X visible: the engine never falls back   */
+    DQ_ERR_PREDICATE = -6,         /* malformed predicate program                      */
+    DQ_ERR_ALIGNMENT = -7          /* device column not 16-B (values) / 8-B (bitmap) aligned */
+} dq_status;
+
+/* ---------------------------------------------------------------------------------------------
+ * Columns: Arrow-style buffers carrying the *Spark* physical type. The type is mandatory because
+ * HLL hashing (C/StatefulHyperloglogPlus.scala:93) and Sum/Min/Max result rules depend on it.
+ * ------------------------------------------------------------------------------------------- */
+typedef enum dq_spark_type {
+    DQ_TYPE_BOOLEAN = 1,    /* uint8 0/1                                 */
+    DQ_TYPE_BYTE = 2,       /* int8                                      */
+    DQ_TYPE_SHORT = 3,      /* int16                                     */
+    DQ_TYPE_INT = 4,        /* int32                                     */
+    DQ_TYPE_LONG = 5,       /* int64                                     */
+    DQ_TYPE_FLOAT = 6,      /* float32                                   */
+    DQ_TYPE_DOUBLE = 7,     /* float64                                   */
+    DQ_TYPE_STRING = 8,     /* UTF-8 bytes in `values`, int32 `offsets`  */
+    DQ_TYPE_DATE = 9,       /* int32 days since epoch                    */
+    DQ_TYPE_TIMESTAMP = 10, /* int64 microseconds since epoch            */
+    DQ_TYPE_DECIMAL = 11    /* int64 unscaled value, precision <= 18     */
+} dq_spark_type;
+
+#define DQ_COL_DEVICE 0x1u /* values/validity/offsets are device pointers on the ctx's GPU */
+
+typedef struct dq_column {
+    int32_t spark_type;        /* dq_spark_type                                               */
+    uint32_t flags;            /* DQ_COL_*                                                    */
+    int64_t length;            /* rows                                                        */
+    const void* values;        /* fixed width: `length` elements; STRING: UTF-8 data bytes    */
+    const uint8_t* validity;   /* Arrow LSB-first bitmap (bit i set = row i non-null), or NULL */
+    const int32_t* offsets;    /* STRING only: length + 1 offsets into `values`                */
+    int32_t decimal_precision; /* DECIMAL only                                                 */
+    int32_t decimal_scale;     /* DECIMAL only                                                 */
+} dq_column;
+
+/* ---------------------------------------------------------------------------------------------
+ * Predicates (`where` filters and Compliance predicates). deequ accepts Spark SQL strings
+ * (A/Analyzer.scala:409-432, A/Compliance.scala:49-52); the host compiles them to this postfix
+ * program, evaluated per row on the GPU with SQL three-valued logic.
+ * ------------------------------------------------------------------------------------------- */
+typedef enum dq_pred_opcode {
+    DQ_P_COL = 1,        /* arg: column index          -> push column value (NULL if invalid) */
+    DQ_P_CONST = 2,      /* arg: constant index        -> push constant                       */
+    DQ_P_NULL = 3,       /*                            -> push NULL                           */
+    DQ_P_EQ = 10, DQ_P_NE = 11, DQ_P_LT = 12, DQ_P_LE = 13, DQ_P_GT = 14, DQ_P_GE = 15,
+    DQ_P_EQ_NULLSAFE = 16, /* <=>                                                              */
+    DQ_P_AND = 20, DQ_P_OR = 21, DQ_P_NOT = 22,
+    DQ_P_IS_NULL = 23, DQ_P_IS_NOT_NULL = 24,
+    DQ_P_IN = 25,        /* arg: n                     -> x IN (v1..vn); n+1 operands          */
+    DQ_P_COALESCE = 26,  /* arg: n operands                                                    */
+    DQ_P_ADD = 30, DQ_P_SUB = 31, DQ_P_MUL = 32, DQ_P_DIV = 33, DQ_P_MOD = 34, DQ_P_NEG = 35,
+    DQ_P_LIKE = 40,      /* arg: constant index of the pattern; 1 operand                      */
+    DQ_P_LENGTH = 41,    /* UTF-8 character count                                             */
+    DQ_P_CAST_DOUBLE = 42, DQ_P_CAST_LONG = 43, DQ_P_CAST_STRING_NUM = 44
+} dq_pred_opcode;
+
+typedef enum dq_value_tag { DQ_V_BOOL = 1, DQ_V_LONG = 2, DQ_V_DOUBLE = 3, DQ_V_STRING = 4 } dq_value_tag;
+
+typedef struct dq_const {
+    int32_t tag;           /* dq_value_tag                                         */
+    int32_t str_len;       /* STRING: byte length                                  */
+    int64_t i64;           /* BOOL / LONG                                          */
+    double f64;            /* DOUBLE                                               */
+    int64_t str_offset;    /* STRING: offset into dq_predicate.strings             */
+} dq_const;
+
+typedef struct dq_predicate {
+    const int32_t* code;   /* pairs (opcode, arg)                                  */
+    int32_t code_len;      /* number of int32 words (2 per instruction)            */
+    int32_t n_consts;
+    const dq_const* consts;
+    const uint8_t* strings;/* string constant pool                                 */
+    int64_t strings_len;
+} dq_predicate;
+
+/* ---------------------------------------------------------------------------------------------
+ * Scan-shareable ops. One dq_op per deduplicated analyzer (VerificationSuite does not dedupe,
+ * M/VerificationSuite.scala:119; the host does).
+ * ------------------------------------------------------------------------------------------- */
+typedef enum dq_op_kind {
+    DQ_OP_SIZE = 1,                 /* A/Size.scala:33-47                    -> num_matches            */
+    DQ_OP_COMPLETENESS = 2,         /* A/Completeness.scala:26-46            -> num_matches_and_count  */
+    DQ_OP_COMPLIANCE = 3,           /* A/Compliance.scala:37-53              -> num_matches_and_count  */
+    DQ_OP_MEAN = 4,                 /* A/Mean.scala:25-54                    -> mean                   */
+    DQ_OP_SUM = 5,                  /* A/Sum.scala:25-52                     -> dbl                    */
+    DQ_OP_MINIMUM = 6,              /* A/Minimum.scala:25-53                 -> dbl                    */
+    DQ_OP_MAXIMUM = 7,              /* A/Maximum.scala:25-53                 -> dbl                    */
+    DQ_OP_STANDARD_DEVIATION = 8,   /* A/StandardDeviation.scala:25-73       -> stddev                 */
+    DQ_OP_CORRELATION = 9,          /* A/Correlation.scala:26-105            -> corr                   */
+    DQ_OP_APPROX_COUNT_DISTINCT = 10,/* A/ApproxCountDistinct.scala:26-64    -> hll                    */
+    DQ_OP_MIN_LENGTH = 11,          /* A/MinLength.scala:25-41               -> dbl                    */
+    DQ_OP_MAX_LENGTH = 12,          /* A/MaxLength.scala:25-41               -> dbl                    */
+    DQ_OP_DATATYPE = 13             /* A/DataType.scala:32-183               -> datatype               */
+} dq_op_kind;
+
+typedef struct dq_op {
+    int32_t kind;       /* dq_op_kind                                         */
+    int32_t column[2];  /* column indices; column[1] only for CORRELATION     */
+    int32_t where;      /* predicate index of the `where` filter, -1 = none   */
+    int32_t predicate;  /* COMPLIANCE: predicate index; otherwise -1          */
+} dq_op;
+
+#define DQ_HLL_NUM_WORDS 52 /* DeequHyperLogLogPlusPlusUtils.NUM_WORDS, C/StatefulHyperloglogPlus.scala:154 */
+#define DQ_HLL_REGISTERS 512
+
+/* One state per op. present == 0 encodes `None` (ifNoNullsIn, A/Analyzer.scala:389-403), which
+ * the host turns into EmptyStateException (A/Analyzer.scala:444-455). */
+typedef struct dq_state {
+    int32_t kind;
+    int32_t present;
+    union {
+        struct { int64_t num_matches; } num_matches;                        /* NumMatches          */
+        struct { int64_t num_matches; int64_t count; } num_matches_and_count;/* NumMatchesAndCount  */
+        struct { double sum; int64_t count; } mean;                         /* MeanState           */
+        struct { double value; } dbl;                                       /* Sum/Min/Max State   */
+        struct { double n, avg, m2; } stddev;                               /* StandardDeviationState */
+        struct { double n, x_avg, y_avg, ck, x_mk, y_mk; } corr;            /* CorrelationState    */
+        struct { int64_t words[DQ_HLL_NUM_WORDS]; } hll;                    /* ApproxCountDistinctState */
+        struct { int64_t num_null, num_fractional, num_integral, num_boolean, num_string; } datatype;
+    } u;
+} dq_state;
+
+#define DQ_SCAN_OUT_DEVICE 0x1u /* `out` is a device pointer: dq_scan returns without syncing */
+
+/* ---------------------------------------------------------------------------------------------
+ * Frequency tables (grouping analyzers). Replaces FrequencyBasedAnalyzer.computeFrequencies
+ * (A/GroupingAnalyzers.scala:53-79) and the fused aggregation over the table in
+ * runAnalyzersForParticularGrouping (R/AnalysisRunner.scala:480-548).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct dq_freq_table dq_freq_table; /* device-resident (key -> count) table */
+
+#define DQ_FREQ_INCLUDE_NULLS 0x1u /* Histogram semantics: null is a key ("NullValue"), all rows count */
+
+typedef struct dq_freq_summary {
+    int64_t num_rows;      /* rows with >= 1 non-null grouping column (A/GroupingAnalyzers.scala:73-76) */
+    int64_t num_groups;    /* count(*) over the table  (CountDistinct, Distinctness numerator)         */
+    int64_t num_unique;    /* sum[count == 1]          (Uniqueness, UniqueValueRatio numerator)        */
+    double entropy;        /* sum over groups of -(c/N) ln(c/N), N = entropy_rows                     */
+    int64_t entropy_rows;  /* the N used for `entropy`                                                 */
+    int64_t max_count;
+} dq_freq_summary;
+
+/* ---------------------------------------------------------------------------------------------
+ * Entry points
+ * ------------------------------------------------------------------------------------------- */
+typedef struct dq_ctx dq_ctx;
+
+int dq_abi_version(void);
+
+/* Bind a context to HIP device `device`. Fails with DQ_ERR_NO_DEVICE when no GPU is visible. */
+dq_ctx* dq_open(int device, int* status);
+void dq_close(dq_ctx* ctx);
+const char* dq_last_error(const dq_ctx* ctx);
+
+/* Run kernels on this HIP stream (hipStream_t as void*); NULL = the context's own stream. */
+int dq_set_stream(dq_ctx* ctx, void* stream);
+int dq_synchronize(dq_ctx* ctx);
+
+/* The fused scan: replaces runScanningAnalyzers (R/AnalysisRunner.scala:289-336), i.e. the single
+ * `data.agg(...).collect()` of all ScanShareableAnalyzer.aggregationFunctions() (:306-313) plus
+ * fromAggregationResult (A/Analyzer.scala:172-175). Every column is read once from HBM.
+ * `out` receives nops dq_state records (host memory unless DQ_SCAN_OUT_DEVICE). */
+int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows,
+            const dq_op* ops, int nops, const dq_predicate* preds, int npreds,
+            dq_state* out, uint32_t flags);
+
+/* Number of fused-scan kernel launches issued so far (the analogue of the SparkMonitor job count
+ * asserted in T/analyzers/runners/AnalysisRunnerTests.scala:50-74). */
+int64_t dq_scan_launch_count(const dq_ctx* ctx);
+
+/* Semigroup merge of two states of the same op kind (State.sum, per analyzer file);
+ * also used for the rank-ordered fold after the RCCL all-gather. */
+int dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out);
+
+/* DeequHyperLogLogPlusPlusUtils.count (C/StatefulHyperloglogPlus.scala:210-257), including the
+ * Java int-shift quirk `1 << Midx` and precision-9 bias correction; returns the rounded estimate. */
+double dq_hll_count(const int64_t words[DQ_HLL_NUM_WORDS]);
+
+/* Spark XxHash64Function.hash(value, type, 42) for one fixed-width value (test hook). */
+int64_t dq_spark_hash64(int32_t spark_type, const void* value, int64_t len);
+
+/* Build the (key -> count) table of the given key columns (computeFrequencies). */
+int dq_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows,
+                   const int32_t* key_columns, int nkeys, uint32_t flags, dq_freq_table** table);
+/* Fused aggregation over the table (Uniqueness/Distinctness/UniqueValueRatio/Entropy/CountDistinct);
+ * entropy_rows <= 0 means "use this table's num_rows". */
+int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* table, int64_t entropy_rows, dq_freq_summary* out);
+/* Export up to k (key-row, count) pairs with the largest counts (Histogram top-N,
+ * A/Histogram.scala:76-78). Ties are broken by smallest representative row. Returns the number written. */
+int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* table, int64_t k, int64_t* rep_rows, int64_t* counts);
+/* Export the whole table: group representative row index and count for every group. */
+int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* table, int64_t capacity, int64_t* rep_rows, int64_t* counts);
+void dq_freq_free(dq_ctx* ctx, dq_freq_table* table);
+
+/* Synthetic input generators for benches/tests (counter-based splitmix64). */
+typedef enum dq_synth_kind {
+    DQ_SYNTH_DYADIC = 1,   /* f64: k * 2^-8, k uniform in [-256, 256]                */
+    DQ_SYNTH_UNIFORM = 2,  /* f64: U[0,1) on a 2^-53 grid                            */
+    DQ_SYNTH_NORMAL = 3,   /* f64: 100 + 15 * (sum of 12 U[0,1) on a 2^-48 grid - 6)   */
+    DQ_SYNTH_INT32R = 4,   /* i64: U[-2^31, 2^31)                                    */
+    DQ_SYNTH_KEY30 = 5,    /* i64: splitmix64(row) mod 2^30                          */
+    DQ_SYNTH_GAUSS01 = 6   /* f64: sum of 12 U[0,1) on a 2^-48 grid - 6              */
+} dq_synth_kind;
+
+int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int64_t nrows,
+                    void* values_dev);
+/* Validity bitmap (ceil(nrows/64) words) with P(null) = null_permille / 1000. */
+int dq_synth_validity(dq_ctx* ctx, uint64_t seed, int64_t row0, int64_t nrows, int32_t null_permille,
+                      uint8_t* validity_dev);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DEEQU_AMD_DQ_H */

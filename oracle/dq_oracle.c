@@ -1,0 +1,395 @@
+/*
+ * dq_oracle.c — CPU restatement of deequ's scan-shareable aggregations (TEST INFRASTRUCTURE).
+ *
+ * This file is the parity oracle for the MI355X engine. Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it; the product (deequ_amd/) never does.
+ *
+ * It restates, row by row and in Spark's sequential per-partition order, the aggregates deequ
+ * builds (paths under /root/reference/src/main/scala/com/amazon/deequ/analyzers/):
+ *   count / sum / min / max        Size.scala:33-47, Completeness.scala:38-41, Mean.scala:36-40,
+ *                                  Sum.scala:34-37, Minimum.scala:34-37, Maximum.scala:34-37
+ *                                  (Spark 2.2 Sum: Long accumulator for integral inputs, Double for
+ *                                  fractional; Min/Max order NaN above every number)
+ *   stddev (n, avg, m2)            catalyst/StatefulStdDevPop.scala:24-34 — Spark CentralMomentAgg
+ *                                  update: n' = n+1; d = x-avg; dN = d/n'; avg += dN; m2 += d*(d-dN)
+ *   correlation                    catalyst/StatefulCorrelation.scala:24-49 — Spark Corr update
+ *   HLL++ registers + estimate     catalyst/StatefulHyperloglogPlus.scala:89-298 (P = 9, XXH64 seed 42)
+ * plus an "exact" two-pass long-double mean/m2 used to judge fp64 tolerances, and the synthetic
+ * splitmix64 generators of SURVEY.md §8d (same formulas as deequ_amd/csrc/synth.hip).
+ *
+ * Spark-side pieces (CentralMomentAgg, Corr, XXH64) are third-party (spark-catalyst_2.11:2.2.2,
+ * pom.xml:73-83) and absent from /root/reference; XXH64 is pinned against the python `xxhash`
+ * package, the rest against the reference's known-answer tests (tests/golden/).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "hll_bias_p9.h"
+
+/* ---- XXH64 (standard; Spark's XXH64.hashInt / hashLong / hashUnsafeBytes) --------------------- */
+static const uint64_t XP1 = 0x9E3779B185EBCA87ULL, XP2 = 0xC2B2AE3D27D4EB4FULL, XP3 = 0x165667B19E3779F9ULL,
+                      XP4 = 0x85EBCA77C2B2AE63ULL, XP5 = 0x27D4EB2F165667C5ULL;
+
+static uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static uint64_t avalanche(uint64_t h) {
+    h ^= h >> 33; h *= XP2; h ^= h >> 29; h *= XP3; h ^= h >> 32;
+    return h;
+}
+static uint64_t rd64(const uint8_t* p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static uint32_t rd32(const uint8_t* p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static uint64_t xround(uint64_t acc, uint64_t in) { acc += in * XP2; acc = rotl(acc, 31); return acc * XP1; }
+
+uint64_t oracle_xxh64(const uint8_t* p, int64_t len, uint64_t seed) {
+    const uint8_t* end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+        while (p + 32 <= end) {
+            v1 = xround(v1, rd64(p)); v2 = xround(v2, rd64(p + 8));
+            v3 = xround(v3, rd64(p + 16)); v4 = xround(v4, rd64(p + 24));
+            p += 32;
+        }
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        uint64_t vs[4] = {v1, v2, v3, v4};
+        for (int i = 0; i < 4; ++i) { h ^= xround(0, vs[i]); h = h * XP1 + XP4; }
+    } else {
+        h = seed + XP5;
+    }
+    h += (uint64_t)len;
+    for (; p + 8 <= end; p += 8) { h ^= xround(0, rd64(p)); h = rotl(h, 27) * XP1 + XP4; }
+    if (p + 4 <= end) { h ^= (uint64_t)rd32(p) * XP1; h = rotl(h, 23) * XP2 + XP3; p += 4; }
+    for (; p < end; ++p) { h ^= (uint64_t)(*p) * XP5; h = rotl(h, 11) * XP1; }
+    return avalanche(h);
+}
+
+/* Spark type codes (include/dq.h dq_spark_type). */
+enum { T_BOOLEAN = 1, T_BYTE, T_SHORT, T_INT, T_LONG, T_FLOAT, T_DOUBLE, T_STRING, T_DATE, T_TIMESTAMP, T_DECIMAL };
+
+/* XxHash64Function.hash(value, type, 42) for a fixed-width value given as raw bytes. */
+uint64_t oracle_spark_hash(int spark_type, const void* v) {
+    uint8_t b[8];
+    switch (spark_type) {
+        case T_BOOLEAN: { int32_t x = *(const uint8_t*)v ? 1 : 0; memcpy(b, &x, 4); return oracle_xxh64(b, 4, 42); }
+        case T_BYTE: { int32_t x = *(const int8_t*)v; memcpy(b, &x, 4); return oracle_xxh64(b, 4, 42); }
+        case T_SHORT: { int32_t x = *(const int16_t*)v; memcpy(b, &x, 4); return oracle_xxh64(b, 4, 42); }
+        case T_INT: case T_DATE: return oracle_xxh64((const uint8_t*)v, 4, 42);
+        case T_FLOAT: {
+            float f = *(const float*)v;
+            uint32_t u = 0x7fc00000u;          /* Float.floatToIntBits canonical NaN */
+            if (f == f) memcpy(&u, &f, 4);
+            memcpy(b, &u, 4);
+            return oracle_xxh64(b, 4, 42);
+        }
+        case T_DOUBLE: {
+            double d = *(const double*)v;
+            uint64_t u = 0x7ff8000000000000ULL; /* Double.doubleToLongBits canonical NaN */
+            if (d == d) memcpy(&u, &d, 8);
+            memcpy(b, &u, 8);
+            return oracle_xxh64(b, 8, 42);
+        }
+        default: return oracle_xxh64((const uint8_t*)v, 8, 42); /* LONG, TIMESTAMP, DECIMAL unscaled */
+    }
+}
+
+/* ---- one column, Spark order ---------------------------------------------------------------- */
+typedef struct {
+    int64_t n;          /* rows counted (valid and where-true) */
+    int64_t isum;       /* integral: Long sum with wrap-around */
+    double dsum;        /* fractional: Double sum in row order */
+    int64_t imin, imax;
+    double dmin, dmax;  /* Spark ordering: NaN greatest */
+    double w_n, w_avg, w_m2;          /* CentralMomentAgg, row order */
+    double ex_mean, ex_m2;            /* exact two-pass in long double */
+} oracle_col;
+
+static int elem_size(int t) {
+    switch (t) {
+        case T_BOOLEAN: case T_BYTE: return 1;
+        case T_SHORT: return 2;
+        case T_INT: case T_DATE: case T_FLOAT: return 4;
+        default: return 8;
+    }
+}
+static int is_frac(int t) { return t == T_FLOAT || t == T_DOUBLE; }
+static int64_t as_i64(int t, const uint8_t* p) {
+    switch (t) {
+        case T_BOOLEAN: return *p ? 1 : 0;
+        case T_BYTE: return *(const int8_t*)p;
+        case T_SHORT: { int16_t x; memcpy(&x, p, 2); return x; }
+        case T_INT: case T_DATE: { int32_t x; memcpy(&x, p, 4); return x; }
+        default: { int64_t x; memcpy(&x, p, 8); return x; }
+    }
+}
+static double as_f64(int t, const uint8_t* p, int scale) {
+    if (t == T_FLOAT) { float f; memcpy(&f, p, 4); return (double)f; }
+    if (t == T_DOUBLE) { double d; memcpy(&d, p, 8); return d; }
+    if (t == T_DECIMAL) {
+        double s = 1.0;
+        for (int i = 0; i < scale; ++i) s *= 10.0;
+        return (double)as_i64(t, p) / s;
+    }
+    return (double)as_i64(t, p);
+}
+/* Spark's NaN-aware "a > b" for doubles (Utils.nanSafeCompareDoubles). */
+static int nan_gt(double a, double b) {
+    if (a != a) return b == b;
+    if (b != b) return 0;
+    return a > b;
+}
+
+/* mask[i] != 0: row i is non-null and its `where` is TRUE. */
+void oracle_column(int spark_type, int decimal_scale, const void* values, const uint8_t* mask, int64_t nrows,
+                   oracle_col* out) {
+    const uint8_t* v = (const uint8_t*)values;
+    const int es = elem_size(spark_type);
+    oracle_col r;
+    memset(&r, 0, sizeof(r));
+    r.imin = INT64_MAX;
+    r.imax = INT64_MIN;
+    r.dmin = NAN;
+    r.dmax = NAN;
+    int first = 1;
+    long double s = 0.0L;
+    for (int64_t i = 0; i < nrows; ++i) {
+        if (!mask[i]) continue;
+        const uint8_t* p = v + i * es;
+        const double x = as_f64(spark_type, p, decimal_scale);
+        r.n++;
+        if (is_frac(spark_type)) {
+            r.dsum += x;
+            if (first || nan_gt(r.dmin, x)) r.dmin = x;
+            if (first || nan_gt(x, r.dmax)) r.dmax = x;
+        } else {
+            const int64_t xi = as_i64(spark_type, p);
+            r.isum = (int64_t)((uint64_t)r.isum + (uint64_t)xi);
+            if (xi < r.imin) r.imin = xi;
+            if (xi > r.imax) r.imax = xi;
+        }
+        first = 0;
+        /* CentralMomentAgg update (input cast to Double) */
+        const double n1 = r.w_n + 1.0;
+        const double delta = x - r.w_avg;
+        const double deltaN = delta / n1;
+        r.w_avg += deltaN;
+        r.w_m2 += delta * (delta - deltaN);
+        r.w_n = n1;
+        s += (long double)x;
+    }
+    if (r.n > 0) {
+        const long double mean = s / (long double)r.n;
+        long double m2 = 0.0L;
+        for (int64_t i = 0; i < nrows; ++i) {
+            if (!mask[i]) continue;
+            const long double d = (long double)as_f64(spark_type, v + i * es, decimal_scale) - mean;
+            m2 += d * d;
+        }
+        r.ex_mean = (double)mean;
+        r.ex_m2 = (double)m2;
+    }
+    *out = r;
+}
+
+typedef struct {
+    double n, x_avg, y_avg, ck, x_mk, y_mk;   /* Spark Corr update, row order */
+    double ex_ck, ex_x_mk, ex_y_mk;           /* exact two-pass */
+} oracle_corr;
+
+void oracle_correlation(int tx, int sx, const void* xv, int ty, int sy, const void* yv, const uint8_t* mask,
+                        int64_t nrows, oracle_corr* out) {
+    const uint8_t* xp = (const uint8_t*)xv;
+    const uint8_t* yp = (const uint8_t*)yv;
+    const int ex = elem_size(tx), ey = elem_size(ty);
+    oracle_corr r;
+    memset(&r, 0, sizeof(r));
+    long double sxl = 0.0L, syl = 0.0L;
+    for (int64_t i = 0; i < nrows; ++i) {
+        if (!mask[i]) continue;
+        const double x = as_f64(tx, xp + i * ex, sx), y = as_f64(ty, yp + i * ey, sy);
+        const double n1 = r.n + 1.0;
+        const double dx = x - r.x_avg;
+        const double dy = y - r.y_avg;
+        r.x_avg += dx / n1;
+        r.y_avg += dy / n1;
+        r.ck += dx * (y - r.y_avg);
+        r.x_mk += dx * (x - r.x_avg);
+        r.y_mk += dy * (y - r.y_avg);
+        r.n = n1;
+        sxl += x;
+        syl += y;
+    }
+    if (r.n > 0) {
+        const long double mx = sxl / (long double)r.n, my = syl / (long double)r.n;
+        long double ck = 0, xm = 0, ym = 0;
+        for (int64_t i = 0; i < nrows; ++i) {
+            if (!mask[i]) continue;
+            const long double dx = (long double)as_f64(tx, xp + i * ex, sx) - mx;
+            const long double dy = (long double)as_f64(ty, yp + i * ey, sy) - my;
+            ck += dx * dy;
+            xm += dx * dx;
+            ym += dy * dy;
+        }
+        r.ex_ck = (double)ck;
+        r.ex_x_mk = (double)xm;
+        r.ex_y_mk = (double)ym;
+    }
+    *out = r;
+}
+
+/* ---- HLL++ (StatefulHyperloglogPlus.update, P = 9) ------------------------------------------- */
+static void hll_add(uint8_t* regs, uint64_t x) {
+    const uint32_t idx = (uint32_t)(x >> 55);
+    const uint64_t w = (x << 9) | (1ULL << 8);
+    const uint8_t pw = (uint8_t)(__builtin_clzll(w) + 1);
+    if (pw > regs[idx]) regs[idx] = pw;
+}
+
+void oracle_hll_fixed(int spark_type, const void* values, const uint8_t* mask, int64_t nrows, uint8_t* regs512) {
+    const uint8_t* v = (const uint8_t*)values;
+    const int es = elem_size(spark_type);
+    for (int64_t i = 0; i < nrows; ++i)
+        if (mask[i]) hll_add(regs512, oracle_spark_hash(spark_type, v + i * es));
+}
+
+void oracle_hll_strings(const uint8_t* data, const int32_t* offsets, const uint8_t* mask, int64_t nrows,
+                        uint8_t* regs512) {
+    for (int64_t i = 0; i < nrows; ++i)
+        if (mask[i]) hll_add(regs512, oracle_xxh64(data + offsets[i], offsets[i + 1] - offsets[i], 42));
+}
+
+/* 6-bit registers, 10 per 64-bit word (StatefulHyperloglogPlus.update word layout). */
+void oracle_hll_pack(const uint8_t* regs512, int64_t* words52) {
+    for (int w = 0; w < 52; ++w) {
+        uint64_t word = 0;
+        for (int k = 0; k < 10; ++k) {
+            const int idx = w * 10 + k;
+            if (idx < 512) word |= (uint64_t)(regs512[idx] & 63) << (6 * k);
+        }
+        words52[w] = (int64_t)word;
+    }
+}
+
+static double estimate_bias(double e) {
+    int lo = 0, hi = DQ_HLL_P9_N - 1, nearest = -1;
+    while (lo <= hi) {            /* java.util.Arrays.binarySearch */
+        const int mid = (lo + hi) >> 1;
+        if (DQ_HLL_P9_RAW[mid] < e) lo = mid + 1;
+        else if (DQ_HLL_P9_RAW[mid] > e) hi = mid - 1;
+        else { nearest = mid; break; }
+    }
+    if (nearest < 0) nearest = lo;
+    int low = nearest - 6 + 1;
+    if (low < 0) low = 0;
+    int high = low + 6;
+    if (high > DQ_HLL_P9_N) high = DQ_HLL_P9_N;
+    while (high < DQ_HLL_P9_N) {
+        const double dh = e - DQ_HLL_P9_RAW[high], dl = e - DQ_HLL_P9_RAW[low];
+        if (!(dh * dh < dl * dl)) break;
+        ++low;
+        ++high;
+    }
+    double s = 0.0;
+    for (int i = low; i < high; ++i) s += DQ_HLL_P9_BIAS[i];
+    return s / (high - low);
+}
+
+/* DeequHyperLogLogPlusPlusUtils.count, with Scala's Int shift `1 << Midx` (distance mod 32). */
+double oracle_hll_count(const int64_t* words52) {
+    const double M = 512.0;
+    const double alphaM2 = (0.7213 / (1.0 + 1.079 / M)) * M * M;
+    double zInverse = 0.0, V = 0.0;
+    int idx = 0;
+    for (int w = 0; w < 52; ++w) {
+        for (int k = 0; k < 10 && idx < 512; ++k, ++idx) {
+            const int m = (int)(((uint64_t)words52[w] >> (6 * k)) & 63);
+            const int32_t p2 = (int32_t)(1u << (m & 31));
+            zInverse += 1.0 / (double)p2;
+            if (m == 0) V += 1.0;
+        }
+    }
+    double est;
+    const double e = alphaM2 / zInverse;
+    const double corrected = e < 5.0 * M ? e - estimate_bias(e) : e;
+    if (V > 0) {
+        const double H = M * log(M / V);
+        est = H <= DQ_HLL_P9_THRESHOLD ? H : corrected;
+    } else {
+        est = corrected;
+    }
+    return floor(est + 0.5);
+}
+
+/* ---- synthetic inputs (identical to deequ_amd/csrc/synth.hip) ------------------ */
+uint64_t oracle_splitmix64(uint64_t seed, uint64_t i) {
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static double sum12(uint64_t seed, uint64_t row) {
+    double s = 0.0;
+    for (int j = 0; j < 12; ++j) {
+        const uint64_t h = oracle_splitmix64(seed ^ (0xA5A5A5A5ULL * (uint64_t)(j + 1)), row);
+        s = s + (double)(h >> 16) * 0x1.0p-48;
+    }
+    return s;
+}
+
+void oracle_synth_column(int kind, uint64_t seed, int64_t row0, int64_t n, void* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        const uint64_t row = (uint64_t)(row0 + i);
+        const uint64_t h = oracle_splitmix64(seed, row);
+        switch (kind) {
+            case 1: ((double*)out)[i] = (double)((int64_t)(h % 513ULL) - 256) * 0x1.0p-8; break;
+            case 2: ((double*)out)[i] = (double)(h >> 11) * 0x1.0p-53; break;
+            case 3: { volatile double t = sum12(seed, row) - 6.0; volatile double u = 15.0 * t;
+                      ((double*)out)[i] = 100.0 + u; break; }
+            case 4: ((int64_t*)out)[i] = (int64_t)(int32_t)(uint32_t)(h >> 32); break;
+            case 5: ((int64_t*)out)[i] = (int64_t)(h & ((1ULL << 30) - 1)); break;
+            case 6: ((double*)out)[i] = sum12(seed, row) - 6.0; break;
+            default: break;
+        }
+    }
+}
+
+void oracle_synth_validity(uint64_t seed, int64_t row0, int64_t n, int permille, uint8_t* mask) {
+    for (int64_t i = 0; i < n; ++i)
+        mask[i] = (int)(oracle_splitmix64(seed, (uint64_t)(row0 + i)) % 1000ULL) >= permille;
+}
+
+/* ---- CPU baseline leg: the Spark-order per-row work only (count, sum, min, max, CentralMomentAgg)
+ * over a fixed-width column with a validity mask; returns rows visited. Used by bench.py. -------- */
+int64_t oracle_scan_spark(int spark_type, const void* values, const uint8_t* valid, int64_t nrows, double* out5) {
+    const uint8_t* v = (const uint8_t*)values;
+    const int es = elem_size(spark_type);
+    const int frac = is_frac(spark_type);
+    int64_t n = 0, isum = 0, imin = INT64_MAX, imax = INT64_MIN;
+    double dsum = 0.0, dmin = NAN, dmax = NAN, wn = 0.0, wavg = 0.0, wm2 = 0.0;
+    for (int64_t i = 0; i < nrows; ++i) {
+        if (!valid[i]) continue;
+        const uint8_t* p = v + i * es;
+        const double x = as_f64(spark_type, p, 0);
+        if (frac) {
+            dsum += x;
+            if (n == 0 || nan_gt(dmin, x)) dmin = x;
+            if (n == 0 || nan_gt(x, dmax)) dmax = x;
+        } else {
+            const int64_t xi = as_i64(spark_type, p);
+            isum = (int64_t)((uint64_t)isum + (uint64_t)xi);
+            if (xi < imin) imin = xi;
+            if (xi > imax) imax = xi;
+        }
+        ++n;
+        const double n1 = wn + 1.0, delta = x - wavg, deltaN = delta / n1;
+        wavg += deltaN;
+        wm2 += delta * (delta - deltaN);
+        wn = n1;
+    }
+    out5[0] = (double)n;
+    out5[1] = frac ? dsum : (double)isum;
+    out5[2] = frac ? dmin : (double)imin;
+    out5[3] = frac ? dmax : (double)imax;
+    out5[4] = wn > 0 ? sqrt(wm2 / wn) : NAN;
+    return nrows;
+}

@@ -1,0 +1,387 @@
+"""Parity oracle (TEST INFRASTRUCTURE — never imported by deequ_amd/).
+
+Expected deequ states for a Table, restated from the reference's semantics:
+  - per-row aggregates through the C restatement in oracle/dq_oracle.c (liboracle.so),
+  - `where` / Compliance predicates by a pure-Python three-valued-logic evaluator of the parsed
+    expression tree (small inputs only),
+  - frequency tables (computeFrequencies, A/GroupingAnalyzers.scala:53-79) with Python dicts / numpy,
+    entropy with math.fsum (exact summation).
+Citations per function; SURVEY.md §8a restates every rule used here.
+"""
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+T_BOOLEAN, T_BYTE, T_SHORT, T_INT, T_LONG, T_FLOAT, T_DOUBLE, T_STRING, T_DATE, T_TIMESTAMP, T_DECIMAL = range(1, 12)
+
+
+class OracleCol(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("isum", ctypes.c_int64), ("dsum", ctypes.c_double),
+                ("imin", ctypes.c_int64), ("imax", ctypes.c_int64), ("dmin", ctypes.c_double),
+                ("dmax", ctypes.c_double), ("w_n", ctypes.c_double), ("w_avg", ctypes.c_double),
+                ("w_m2", ctypes.c_double), ("ex_mean", ctypes.c_double), ("ex_m2", ctypes.c_double)]
+
+
+class OracleCorr(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_double), ("x_avg", ctypes.c_double), ("y_avg", ctypes.c_double),
+                ("ck", ctypes.c_double), ("x_mk", ctypes.c_double), ("y_mk", ctypes.c_double),
+                ("ex_ck", ctypes.c_double), ("ex_x_mk", ctypes.c_double), ("ex_y_mk", ctypes.c_double)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = ctypes.CDLL(LIB)
+        L.oracle_xxh64.restype = ctypes.c_uint64
+        L.oracle_xxh64.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64]
+        L.oracle_spark_hash.restype = ctypes.c_uint64
+        L.oracle_spark_hash.argtypes = [ctypes.c_int, ctypes.c_void_p]
+        L.oracle_column.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                    ctypes.POINTER(OracleCol)]
+        L.oracle_correlation.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(OracleCorr)]
+        L.oracle_hll_fixed.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+        L.oracle_hll_strings.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                         ctypes.c_void_p]
+        L.oracle_hll_pack.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_hll_count.restype = ctypes.c_double
+        L.oracle_hll_count.argtypes = [ctypes.c_void_p]
+        L.oracle_splitmix64.restype = ctypes.c_uint64
+        L.oracle_splitmix64.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_synth_column.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_void_p]
+        L.oracle_synth_validity.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                            ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+# ---- raw helpers ---------------------------------------------------------------------------------
+def xxh64(data, seed=42):
+    b = bytes(data)
+    buf = ctypes.create_string_buffer(b, max(len(b), 1))
+    return lib().oracle_xxh64(buf, len(b), seed)
+
+
+def spark_hash(spark_type, value):
+    dtype = {T_BOOLEAN: np.uint8, T_BYTE: np.int8, T_SHORT: np.int16, T_INT: np.int32, T_DATE: np.int32,
+             T_LONG: np.int64, T_TIMESTAMP: np.int64, T_DECIMAL: np.int64, T_FLOAT: np.float32,
+             T_DOUBLE: np.float64}[spark_type]
+    a = np.array([value], dtype=dtype)
+    return lib().oracle_spark_hash(spark_type, a.ctypes.data)
+
+
+def hll_count(words):
+    w = np.array([int(np.int64(np.uint64(x & 0xFFFFFFFFFFFFFFFF))) for x in words], dtype=np.int64)
+    return lib().oracle_hll_count(w.ctypes.data)
+
+
+def synth_column(kind, seed, row0, n):
+    dt = np.int64 if kind in (4, 5) else np.float64
+    out = np.zeros(n, dtype=dt)
+    lib().oracle_synth_column(kind, seed, row0, n, out.ctypes.data)
+    return out
+
+
+def synth_validity(seed, row0, n, permille):
+    m = np.zeros(n, dtype=np.uint8)
+    lib().oracle_synth_validity(seed, row0, n, permille, m.ctypes.data)
+    return m.astype(bool)
+
+
+# ---- predicate evaluation (3VL) ------------------------------------------------------------------
+def _cmp_vals(a, b):
+    """Spark comparison after PromoteStrings (string vs number -> double). None = NULL result."""
+    if isinstance(a, str) and isinstance(b, str):
+        ab, bb = a.encode(), b.encode()
+        return (ab > bb) - (ab < bb)
+    if isinstance(a, str) or isinstance(b, str):
+        try:
+            a = float(a) if isinstance(a, str) else float(a)
+            b = float(b) if isinstance(b, str) else float(b)
+        except ValueError:
+            return None
+    if isinstance(a, bool):
+        a = int(a)
+    if isinstance(b, bool):
+        b = int(b)
+    an = isinstance(a, float) and math.isnan(a)
+    bn = isinstance(b, float) and math.isnan(b)
+    if an or bn:
+        return 0 if an and bn else (1 if an else -1)
+    return (a > b) - (a < b)
+
+
+def _like(s, pat):
+    import re
+    rx, i = "", 0
+    while i < len(pat):
+        c = pat[i]
+        if c == "\\" and i + 1 < len(pat):
+            rx += re.escape(pat[i + 1])
+            i += 2
+            continue
+        rx += ".*" if c == "%" else ("." if c == "_" else re.escape(c))
+        i += 1
+    return re.fullmatch(rx, s, flags=re.S) is not None
+
+
+def _eval(node, row):
+    k = node.kind
+    if k == "col":
+        return row[node.value]
+    if k == "const":
+        kind, v = node.value
+        return v
+    if k == "null":
+        return None
+    if k == "cmp":
+        a, b = _eval(node.children[0], row), _eval(node.children[1], row)
+        if node.value == "<=>":
+            if a is None or b is None:
+                return a is None and b is None
+            return _cmp_vals(a, b) == 0
+        if a is None or b is None:
+            return None
+        c = _cmp_vals(a, b)
+        if c is None:
+            return None
+        return {"=": c == 0, "!=": c != 0, "<": c < 0, "<=": c <= 0, ">": c > 0, ">=": c >= 0}[node.value]
+    if k == "and":
+        a, b = _eval(node.children[0], row), _eval(node.children[1], row)
+        if a is False or b is False:
+            return False
+        if a is None or b is None:
+            return None
+        return True
+    if k == "or":
+        a, b = _eval(node.children[0], row), _eval(node.children[1], row)
+        if a is True or b is True:
+            return True
+        if a is None or b is None:
+            return None
+        return False
+    if k == "not":
+        a = _eval(node.children[0], row)
+        return None if a is None else (not a)
+    if k == "isnull":
+        return _eval(node.children[0], row) is None
+    if k == "isnotnull":
+        return _eval(node.children[0], row) is not None
+    if k == "in":
+        x = _eval(node.children[0], row)
+        if x is None:
+            return None
+        any_null = False
+        for ch in node.children[1:]:
+            e = _eval(ch, row)
+            if e is None:
+                any_null = True
+            elif _cmp_vals(x, e) == 0:
+                return True
+        return None if any_null else False
+    if k == "like":
+        x = _eval(node.children[0], row)
+        return None if x is None else _like(x, node.value)
+    if k == "arith":
+        a, b = _eval(node.children[0], row), _eval(node.children[1], row)
+        if a is None or b is None:
+            return None
+        a = float(a) if isinstance(a, str) else a
+        b = float(b) if isinstance(b, str) else b
+        op = node.value
+        if op == "/":
+            return None if b == 0 else float(a) / float(b)
+        if op == "%":
+            if b == 0:
+                return None
+            return math.fmod(a, b) if isinstance(a, float) or isinstance(b, float) else int(math.fmod(a, b))
+        return {"+": a + b, "-": a - b, "*": a * b}[op]
+    if k == "neg":
+        a = _eval(node.children[0], row)
+        return None if a is None else -a
+    if k == "coalesce":
+        for ch in node.children:
+            v = _eval(ch, row)
+            if v is not None:
+                return v
+        return None
+    if k == "length":
+        a = _eval(node.children[0], row)
+        return None if a is None else len(a)
+    if k == "cast_double":
+        a = _eval(node.children[0], row)
+        if a is None:
+            return None
+        try:
+            return float(a)
+        except ValueError:
+            return None
+    if k == "cast_long":
+        a = _eval(node.children[0], row)
+        if a is None:
+            return None
+        try:
+            return int(float(a)) if isinstance(a, str) else int(a)
+        except ValueError:
+            return None
+    raise ValueError(k)
+
+
+def predicate_masks(table, text):
+    """(TRUE mask, NOT-NULL mask) of a SQL predicate over every row."""
+    from deequ_amd.expr import _Parser  # the parse tree only; evaluation is independent
+    tree = _Parser(text).parse()
+    cols = {n: table[n].to_pylist() for n in table.columns}
+    t = np.zeros(table.nrows, dtype=bool)
+    nn = np.zeros(table.nrows, dtype=bool)
+    for i in range(table.nrows):
+        v = _eval(tree, {n: cols[n][i] for n in cols})
+        nn[i] = v is not None
+        t[i] = v is True or (v is not None and not isinstance(v, bool) and v != 0)
+    return t, nn
+
+
+# ---- expected states per analyzer ---------------------------------------------------------------
+def _valid(col):
+    from deequ_amd.table import unpack_validity
+    return unpack_validity(col.validity, col.length)
+
+
+def _where(table, where):
+    if where is None:
+        return np.ones(table.nrows, dtype=bool), np.ones(table.nrows, dtype=bool)
+    return predicate_masks(table, where)
+
+
+def _cond_count(table, where):
+    """conditionalCount (A/Analyzer.scala:426-432): (value, present)."""
+    if where is None:
+        return table.nrows, True
+    t, nn = _where(table, where)
+    return int(t.sum()), bool(nn.any())
+
+
+def column_stats(table, column, where=None):
+    c = table[column]
+    wt, _ = _where(table, where)
+    mask = (_valid(c) & wt).astype(np.uint8)
+    out = OracleCol()
+    vals = np.ascontiguousarray(c.values)
+    lib().oracle_column(c.spark_type, c.decimal_scale, vals.ctypes.data, mask.ctypes.data, c.length,
+                        ctypes.byref(out))
+    return out
+
+
+def expected_state(table, analyzer, exact=True):
+    """The reference State for `analyzer` on `table` (None = empty state), oracle semantics."""
+    import deequ_amd as D
+    from deequ_amd import states as S
+    name = type(analyzer).__name__
+    if name == "Size":
+        v, present = _cond_count(table, analyzer.where)
+        return S.NumMatches(v) if present else None
+    if name == "Completeness":
+        c = table[analyzer.column]
+        wt, _ = _where(table, analyzer.where)
+        cnt, present = _cond_count(table, analyzer.where)
+        if table.nrows == 0 or not present:
+            return None
+        return S.NumMatchesAndCount(int((_valid(c) & wt).sum()), cnt)
+    if name == "Compliance":
+        wt, _ = _where(table, analyzer.where)
+        pt, pnn = predicate_masks(table, analyzer.predicate)
+        cnt, present = _cond_count(table, analyzer.where)
+        if not (wt & pnn).any() or not present:
+            return None
+        return S.NumMatchesAndCount(int((wt & pt).sum()), cnt)
+    if name in ("Mean", "Sum", "Minimum", "Maximum", "StandardDeviation"):
+        c = table[analyzer.column]
+        st = column_stats(table, analyzer.column, analyzer.where)
+        if st.n == 0:
+            return None
+        frac = c.spark_type in (T_FLOAT, T_DOUBLE)
+        scale = 10.0 ** c.decimal_scale if c.spark_type == T_DECIMAL else 1.0
+        total = st.dsum if frac else st.isum / scale
+        if name == "Mean":
+            return S.MeanState(total, st.n)
+        if name == "Sum":
+            return S.SumState(total)
+        if name == "Minimum":
+            return S.MinState(st.dmin if frac else st.imin / scale)
+        if name == "Maximum":
+            return S.MaxState(st.dmax if frac else st.imax / scale)
+        if exact:
+            return S.StandardDeviationState(float(st.n), st.ex_mean, st.ex_m2)
+        return S.StandardDeviationState(st.w_n, st.w_avg, st.w_m2)
+    if name == "Correlation":
+        x, y = table[analyzer.firstColumn], table[analyzer.secondColumn]
+        wt, _ = _where(table, analyzer.where)
+        mask = (_valid(x) & _valid(y) & wt).astype(np.uint8)
+        out = OracleCorr()
+        xv, yv = np.ascontiguousarray(x.values), np.ascontiguousarray(y.values)
+        lib().oracle_correlation(x.spark_type, x.decimal_scale, xv.ctypes.data, y.spark_type, y.decimal_scale,
+                                 yv.ctypes.data, mask.ctypes.data, x.length, ctypes.byref(out))
+        if out.n == 0:
+            return None
+        if exact:
+            return S.CorrelationState(out.n, out.x_avg, out.y_avg, out.ex_ck, out.ex_x_mk, out.ex_y_mk)
+        return S.CorrelationState(out.n, out.x_avg, out.y_avg, out.ck, out.x_mk, out.y_mk)
+    if name == "ApproxCountDistinct":
+        c = table[analyzer.column]
+        wt, _ = _where(table, analyzer.where)
+        mask = (_valid(c) & wt).astype(np.uint8)
+        regs = np.zeros(512, dtype=np.uint8)
+        if c.spark_type == T_STRING:
+            lib().oracle_hll_strings(c.values.ctypes.data if len(c.values) else None, c.offsets.ctypes.data,
+                                     mask.ctypes.data, c.length, regs.ctypes.data)
+        else:
+            vals = np.ascontiguousarray(c.values)
+            lib().oracle_hll_fixed(c.spark_type, vals.ctypes.data, mask.ctypes.data, c.length, regs.ctypes.data)
+        words = np.zeros(52, dtype=np.int64)
+        lib().oracle_hll_pack(regs.ctypes.data, words.ctypes.data)
+        return S.ApproxCountDistinctState([int(w) for w in words])
+    raise ValueError("no oracle for %s" % name)
+
+
+def frequencies(table, columns, include_nulls=False):
+    """computeFrequencies: {key tuple: count} over rows with >= 1 non-null key (all rows if
+    include_nulls, Histogram semantics), plus numRows."""
+    cols = [table[c].to_pylist() for c in columns]
+    freq = {}
+    nrows = 0
+    for i in range(table.nrows):
+        key = tuple(_group_key(c[i]) for c in cols)
+        if not include_nulls and all(k is None for k in key):
+            continue
+        nrows += 1
+        freq[key] = freq.get(key, 0) + 1
+    return freq, nrows
+
+
+def _group_key(v):
+    """Spark groups on binary equality: NaN canonical, -0.0 != 0.0."""
+    if isinstance(v, float):
+        if math.isnan(v):
+            return ("nan",)
+        if v == 0.0 and math.copysign(1.0, v) < 0:
+            return ("-0.0",)
+    return v
+
+
+def grouping_summary(freq, num_rows):
+    counts = list(freq.values())
+    ent = math.fsum(-(c / num_rows) * math.log(c / num_rows) for c in counts) if counts else 0.0
+    return {"num_groups": len(counts), "num_unique": sum(1 for c in counts if c == 1), "entropy": ent,
+            "num_rows": num_rows}
