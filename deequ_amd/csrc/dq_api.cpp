@@ -149,6 +149,12 @@ double java_math_max(double a, double b) {
 
 }  // namespace
 
+namespace dq {
+hipStream_t ctx_stream(dq_ctx* ctx) { return ctx->stream; }
+int ctx_device(dq_ctx* ctx) { return ctx->device; }
+int ctx_fail(dq_ctx* ctx, int code, const char* msg) { return fail(ctx, code, "%s", msg); }
+}  // namespace dq
+
 // =================================================================================================
 // C-ABI
 // =================================================================================================
@@ -841,6 +847,17 @@ int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int6
     if (nrows == 0) return DQ_OK;
     DQ_HIP(ctx, hipSetDevice(ctx->device));
     launch_synth_column(kind, seed, row0, nrows, values_dev, ctx->stream);
+    DQ_HIP(ctx, hipGetLastError());
+    return DQ_OK;
+}
+
+int dq_synth_freq_keys(dq_ctx* ctx, int64_t total_rows, int64_t distinct, int64_t row0, int64_t nrows, int64_t* keys_dev) {
+    if (!ctx || total_rows <= 0 || distinct <= 0 || distinct > total_rows || nrows < 0 || row0 < 0 ||
+        row0 + nrows > total_rows || (!keys_dev && nrows > 0))
+        return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_synth_freq_keys: invalid arguments");
+    if (nrows == 0) return DQ_OK;
+    DQ_HIP(ctx, hipSetDevice(ctx->device));
+    launch_synth_freq_keys(total_rows, distinct, row0, nrows, keys_dev, ctx->stream);
     DQ_HIP(ctx, hipGetLastError());
     return DQ_OK;
 }

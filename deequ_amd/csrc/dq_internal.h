@@ -167,6 +167,7 @@ void launch_finalize(const OpMap* ops, int nops, const SlotPartial* finals, cons
 void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
                       int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s);
 void launch_synth_column(int kind, uint64_t seed, int64_t row0, int64_t nrows, void* out, hipStream_t s);
+void launch_synth_freq_keys(int64_t total, int64_t distinct, int64_t row0, int64_t nrows, int64_t* out, hipStream_t s);
 void launch_synth_validity(uint64_t seed, int64_t row0, int64_t nrows, int permille, uint8_t* out,
                            hipStream_t s);
 

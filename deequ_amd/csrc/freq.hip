@@ -1,15 +1,787 @@
-// freq.hip — frequency tables for the grouping analyzers (placeholder until the HBM hash lands).
+// freq.hip — HBM-resident frequency tables for the grouping analyzers (gfx950).
+//
+// Replaces FrequencyBasedAnalyzer.computeFrequencies (A/GroupingAnalyzers.scala:53-79):
+//   SELECT cols, COUNT(*) WHERE c1 IS NOT NULL OR ... GROUP BY cols     (+ numRows = that WHERE's count)
+// and the fused aggregation over the table (runAnalyzersForParticularGrouping,
+// R/AnalysisRunner.scala:480-548): #groups, #(count == 1), sum -(c/N) ln(c/N), plus Histogram's
+// variant (A/Histogram.scala:54-70: every row counts, NULL is the "NullValue" group) and top-N.
+//
+// Table: open addressing with linear probing over 16-byte slots {u64 key, u32 count, u32 pad} so a
+// probe touches one cache line. Keys:
+//   * fast path (one fixed-width key column): key = mix(canonical 64-bit value), mix = the bijective
+//     splitmix64 finalizer, so distinct values never collide; the one value that maps to the EMPTY
+//     marker is counted in a side counter. Spark groups on binary row equality: NaN is
+//     canonicalised (UnsafeRow.setDouble), -0.0 and 0.0 stay distinct.
+//   * general path (several key columns or strings): a 64-bit fingerprint over (null flag, value)
+//     of every key column, plus the group's smallest row index; a verification pass compares every
+//     row with its group's representative row and the build is redone with a new seed if two
+//     distinct keys ever shared a fingerprint, so results are exact.
+// Capacity comes from a 4096-register HLL estimate of the distinct keys (pass 1); inserts are
+// global 64-bit CAS + 32-bit atomic adds (pass 2). Summaries, radix-select top-N and exports are
+// table scans with per-workgroup partials folded in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "dq_common.h"
 #include "dq_internal.h"
 
+using namespace dq;
+
+namespace {
+
+constexpr int kMaxKeys = 16;
+constexpr uint64_t kEmpty = ~0ull;
+constexpr int kSizingRegs = 4096;  // HLL registers used only to size the table
+constexpr int kFreqBlock = 256;
+constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (fixed: deterministic partials)
+
+struct KeyCol {
+    const void* values;
+    const uint8_t* validity;
+    const int32_t* offsets;
+    int32_t spark_type;
+    int32_t elem;
+};
+
+struct KeySpec {
+    KeyCol cols[kMaxKeys];
+    int32_t ncols;
+    int32_t fast;          // single fixed-width key column
+    int32_t include_nulls; // Histogram semantics
+    int32_t string_null_is_value;  // Histogram on a string column: NULL == "NullValue"
+    uint64_t seed;         // fingerprint seed (general path)
+};
+
+struct Slot {
+    unsigned long long key;
+    unsigned int count;
+    unsigned int pad;
+};
+
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ bool is_valid(const KeyCol& c, int64_t r) {
+    return c.validity == nullptr || ((c.validity[r >> 3] >> (r & 7)) & 1);
+}
+
+// Canonical 64-bit value of a fixed-width cell (the grouping equality of Spark's UnsafeRow bytes).
+__device__ __forceinline__ uint64_t canonical(const KeyCol& c, int64_t r) {
+    switch (c.elem) {
+        case ET_U8: return static_cast<const uint8_t*>(c.values)[r] ? 1ull : 0ull;
+        case ET_I8: return (uint64_t)(int64_t) static_cast<const int8_t*>(c.values)[r];
+        case ET_I16: return (uint64_t)(int64_t) static_cast<const int16_t*>(c.values)[r];
+        case ET_I32: return (uint64_t)(int64_t) static_cast<const int32_t*>(c.values)[r];
+        case ET_F32: return (uint64_t)float_to_int_bits(static_cast<const float*>(c.values)[r]);
+        case ET_F64: return double_to_long_bits(static_cast<const double*>(c.values)[r]);
+        default: return static_cast<const uint64_t*>(c.values)[r];
+    }
+}
+
+__device__ __constant__ const uint8_t kNullValue[9] = {'N', 'u', 'l', 'l', 'V', 'a', 'l', 'u', 'e'};
+
+// Key of row r: returns false when the row does not take part (all key columns NULL, grouping
+// semantics); `null_group` = the row belongs to the fast path's NULL group (Histogram semantics).
+__device__ __forceinline__ bool row_key(const KeySpec& ks, int64_t r, uint64_t& h, bool& null_group) {
+    null_group = false;
+    if (ks.fast) {
+        const KeyCol& c = ks.cols[0];
+        if (!is_valid(c, r)) {
+            if (!ks.include_nulls) return false;
+            null_group = true;
+            return true;
+        }
+        h = mix64(canonical(c, r));
+        return true;
+    }
+    bool any = false;
+    uint64_t acc = ks.seed;
+    for (int i = 0; i < ks.ncols; ++i) {
+        const KeyCol& c = ks.cols[i];
+        uint64_t ch;
+        if (is_valid(c, r)) {
+            any = true;
+            if (c.spark_type == DQ_TYPE_STRING) {
+                const int32_t o0 = c.offsets[r], o1 = c.offsets[r + 1];
+                ch = xxh_bytes(static_cast<const uint8_t*>(c.values) + o0, o1 - o0, ks.seed);
+            } else {
+                ch = xxh_long(canonical(c, r), ks.seed);
+            }
+        } else if (ks.string_null_is_value) {
+            any = true;
+            ch = xxh_bytes(kNullValue, 9, ks.seed);
+        } else {
+            ch = 0x6A09E667F3BCC909ULL;  // NULL component
+        }
+        acc = mix64(acc + P64_1 * (uint64_t)(i + 1) + ch);
+    }
+    if (!any && !ks.include_nulls) return false;
+    h = acc == kEmpty ? kEmpty - 1 : acc;
+    return true;
+}
+
+// Exact equality of two rows' keys (null-safe, A/GroupingAnalyzers.scala:149-151).
+__device__ bool rows_equal(const KeySpec& ks, int64_t a, int64_t b) {
+    for (int i = 0; i < ks.ncols; ++i) {
+        const KeyCol& c = ks.cols[i];
+        bool va = is_valid(c, a), vb = is_valid(c, b);
+        if (c.spark_type == DQ_TYPE_STRING) {
+            const uint8_t* pa;
+            const uint8_t* pb;
+            int la, lb;
+            if (va) { pa = static_cast<const uint8_t*>(c.values) + c.offsets[a]; la = c.offsets[a + 1] - c.offsets[a]; }
+            else if (ks.string_null_is_value) { pa = kNullValue; la = 9; va = true; }
+            else { pa = nullptr; la = 0; }
+            if (vb) { pb = static_cast<const uint8_t*>(c.values) + c.offsets[b]; lb = c.offsets[b + 1] - c.offsets[b]; }
+            else if (ks.string_null_is_value) { pb = kNullValue; lb = 9; vb = true; }
+            else { pb = nullptr; lb = 0; }
+            if (va != vb) return false;
+            if (!va) continue;
+            if (la != lb) return false;
+            for (int k = 0; k < la; ++k)
+                if (pa[k] != pb[k]) return false;
+        } else {
+            if (va != vb) return false;
+            if (va && canonical(c, a) != canonical(c, b)) return false;
+        }
+    }
+    return true;
+}
+
+// ---- pass 1: distinct-count estimate for sizing ------------------------------------------------
+__global__ void __launch_bounds__(kFreqBlock)
+sizing_hll_kernel(KeySpec ks, int64_t nrows, unsigned int* __restrict__ regs) {
+    __shared__ unsigned int lds[kSizingRegs];
+    for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock) lds[i] = 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * kFreqBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < nrows; r += stride) {
+        uint64_t h;
+        bool ng;
+        if (!row_key(ks, r, h, ng) || ng) continue;
+        const uint64_t x = xxh_long(h, 7);  // fresh bits for the register index
+        const unsigned int idx = (unsigned int)(x >> 52);
+        const unsigned int rank = (unsigned int)__clzll((long long)((x << 12) | (1ull << 11))) + 1u;
+        if (rank > lds[idx]) atomicMax(&lds[idx], rank);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock)
+        if (lds[i]) atomicMax(&regs[i], lds[i]);
+}
+
+// ---- pass 2: insert ----------------------------------------------------------------------------
+struct Counters {
+    unsigned long long num_rows;   // rows taking part (numRows)
+    unsigned long long sentinel;   // fast path: rows whose mixed key equals kEmpty
+    unsigned long long nulls;      // fast path + include_nulls: NULL rows
+    unsigned long long overflow;   // probe limit hit: rebuild bigger
+    unsigned long long mismatch;   // general path verification: fingerprint collisions
+    unsigned long long pad[3];
+};
+
+__device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, unsigned long long* lds4) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if ((threadIdx.x & 63) == 0) lds4[threadIdx.x >> 6] = v;
+    __syncthreads();
+    unsigned long long s = 0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < kFreqBlock / 64; ++w) s += lds4[w];
+    __syncthreads();
+    return s;
+}
+
+__global__ void __launch_bounds__(kFreqBlock)
+insert_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
+              uint64_t mask, Counters* __restrict__ ctr) {
+    __shared__ unsigned long long red[kFreqBlock / 64];
+    unsigned long long taken = 0, sent = 0, nulls = 0, ovf = 0;
+    const int64_t stride = (int64_t)gridDim.x * kFreqBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < nrows; r += stride) {
+        uint64_t h;
+        bool ng;
+        if (!row_key(ks, r, h, ng)) continue;
+        ++taken;
+        if (ng) { ++nulls; continue; }
+        if (h == kEmpty) { ++sent; continue; }
+        uint64_t pos = h & mask;
+        for (uint64_t probe = 0;; ++probe) {
+            if (probe > 4096 || probe > mask) { ++ovf; break; }
+            Slot* s = slots + pos;
+            unsigned long long k = __hip_atomic_load(&s->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == kEmpty) {
+                const unsigned long long prev = atomicCAS(&s->key, kEmpty, (unsigned long long)h);
+                k = prev == kEmpty ? (unsigned long long)h : prev;
+            }
+            if (k == h) {
+                atomicAdd(&s->count, 1u);
+                if (reps) atomicMin(&reps[pos], (unsigned long long)r);
+                break;
+            }
+            pos = (pos + 1) & mask;
+        }
+    }
+    taken = block_sum_u64(taken, red);
+    sent = block_sum_u64(sent, red);
+    nulls = block_sum_u64(nulls, red);
+    ovf = block_sum_u64(ovf, red);
+    if (threadIdx.x == 0) {
+        if (taken) atomicAdd(&ctr->num_rows, taken);
+        if (sent) atomicAdd(&ctr->sentinel, sent);
+        if (nulls) atomicAdd(&ctr->nulls, nulls);
+        if (ovf) atomicAdd(&ctr->overflow, ovf);
+    }
+}
+
+// General path: every row must equal its group's representative row.
+__global__ void __launch_bounds__(kFreqBlock)
+verify_kernel(KeySpec ks, int64_t nrows, const Slot* __restrict__ slots, const unsigned long long* __restrict__ reps,
+              uint64_t mask, Counters* __restrict__ ctr) {
+    __shared__ unsigned long long red[kFreqBlock / 64];
+    unsigned long long bad = 0;
+    const int64_t stride = (int64_t)gridDim.x * kFreqBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < nrows; r += stride) {
+        uint64_t h;
+        bool ng;
+        if (!row_key(ks, r, h, ng)) continue;
+        uint64_t pos = h & mask;
+        for (uint64_t probe = 0; probe <= mask; ++probe) {
+            if (slots[pos].key == h) {
+                if (!rows_equal(ks, r, (int64_t)reps[pos])) ++bad;
+                break;
+            }
+            if (slots[pos].key == kEmpty) { ++bad; break; }
+            pos = (pos + 1) & mask;
+        }
+    }
+    bad = block_sum_u64(bad, red);
+    if (threadIdx.x == 0 && bad) atomicAdd(&ctr->mismatch, bad);
+}
+
+__global__ void fill_kernel(Slot* __restrict__ slots, unsigned long long* __restrict__ reps, uint64_t cap) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+        slots[i].key = kEmpty;
+        slots[i].count = 0;
+        slots[i].pad = 0;
+        if (reps) reps[i] = ~0ull;
+    }
+}
+
+// ---- table scans ---------------------------------------------------------------------------------
+struct SummaryPartial {
+    unsigned long long groups, unique, maxc, pad;
+    double ent, comp;
+};
+
+__global__ void __launch_bounds__(kFreqBlock)
+summary_kernel(const Slot* __restrict__ slots, uint64_t cap, double n, SummaryPartial* __restrict__ out) {
+    __shared__ SummaryPartial red[kFreqBlock];
+    const uint64_t chunk = (cap + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t b1 = b0 + chunk < cap ? b0 + chunk : cap;
+    SummaryPartial p = {0, 0, 0, 0, 0.0, 0.0};
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += kFreqBlock) {
+        const unsigned int c = slots[i].count;
+        if (c == 0) continue;
+        p.groups++;
+        p.unique += c == 1;
+        p.maxc = c > p.maxc ? c : p.maxc;
+        if (n > 0) {
+            const double q = (double)c / n;
+            const double term = -q * log(q);
+            const double y = term - p.comp;  // Kahan
+            const double t = p.ent + y;
+            p.comp = (t - p.ent) - y;
+            p.ent = t;
+        }
+    }
+    red[threadIdx.x] = p;
+    __syncthreads();
+    for (int s = kFreqBlock / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            SummaryPartial& a = red[threadIdx.x];
+            const SummaryPartial& b = red[threadIdx.x + s];
+            a.groups += b.groups;
+            a.unique += b.unique;
+            a.maxc = b.maxc > a.maxc ? b.maxc : a.maxc;
+            const double y = b.ent - (a.comp + b.comp);
+            const double t = a.ent + y;
+            a.comp = (t - a.ent) - y;
+            a.ent = t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+// Radix-select step: histogram of 11-bit digit `shift` of counts whose higher bits equal `prefix`.
+__global__ void __launch_bounds__(kFreqBlock)
+digit_hist_kernel(const Slot* __restrict__ slots, uint64_t cap, int shift, unsigned int prefix_mask,
+                  unsigned int prefix, unsigned long long* __restrict__ hist) {
+    __shared__ unsigned int lds[2048];
+    for (int i = threadIdx.x; i < 2048; i += kFreqBlock) lds[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * kFreqBlock;
+    for (uint64_t i = (uint64_t)blockIdx.x * kFreqBlock + threadIdx.x; i < cap; i += stride) {
+        const unsigned int c = slots[i].count;
+        if (c == 0 || (c & prefix_mask) != prefix) continue;
+        atomicAdd(&lds[(c >> shift) & 2047u], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2048; i += kFreqBlock)
+        if (lds[i]) atomicAdd(&hist[i], (unsigned long long)lds[i]);
+}
+
+// Selection predicate of the compaction kernels: mode 0 = count > t, 1 = count == t, 2 = count > 0.
+__device__ __forceinline__ bool selected(unsigned int c, int mode, unsigned int t) {
+    return mode == 0 ? c > t : (mode == 1 ? c == t : c > 0);
+}
+
+__global__ void __launch_bounds__(kFreqBlock)
+count_selected_kernel(const Slot* __restrict__ slots, uint64_t cap, int mode, unsigned int t,
+                      unsigned long long* __restrict__ per_block) {
+    __shared__ unsigned long long red[kFreqBlock / 64];
+    const uint64_t chunk = (cap + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t b1 = b0 + chunk < cap ? b0 + chunk : cap;
+    unsigned long long n = 0;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += kFreqBlock) n += selected(slots[i].count, mode, t);
+    n = block_sum_u64(n, red);
+    if (threadIdx.x == 0) per_block[blockIdx.x] = n;
+}
+
+// Writes the selected slots of each workgroup's chunk in slot order at out[offset[b] + rank],
+// skipping ranks >= limit. key_out gets the slot key (fast) or the representative row (general).
+__global__ void __launch_bounds__(kFreqBlock)
+compact_kernel(const Slot* __restrict__ slots, const unsigned long long* __restrict__ reps, uint64_t cap, int mode,
+               unsigned int t, const unsigned long long* __restrict__ offsets, unsigned long long limit,
+               unsigned long long* __restrict__ key_out, unsigned long long* __restrict__ count_out) {
+    __shared__ unsigned int wave_counts[kFreqBlock / 64];
+    const uint64_t chunk = (cap + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t b1 = b0 + chunk < cap ? b0 + chunk : cap;
+    unsigned long long base = offsets[blockIdx.x];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint64_t i0 = b0; i0 < b1; i0 += kFreqBlock) {
+        const uint64_t i = i0 + threadIdx.x;
+        const bool sel = i < b1 && selected(slots[i].count, mode, t);
+        const unsigned long long bal = __ballot(sel);
+        const unsigned int before = __popcll(bal & ((1ull << lane) - 1ull));
+        if (lane == 0) wave_counts[wave] = __popcll(bal);
+        __syncthreads();
+        unsigned int wave_off = 0, tile_total = 0;
+        for (int w = 0; w < kFreqBlock / 64; ++w) {
+            if (w < wave) wave_off += wave_counts[w];
+            tile_total += wave_counts[w];
+        }
+        if (sel) {
+            const unsigned long long rank = base + wave_off + before;
+            if (rank < limit) {
+                key_out[rank] = reps ? reps[i] : slots[i].key;
+                count_out[rank] = slots[i].count;
+            }
+        }
+        base += tile_total;
+        __syncthreads();
+    }
+}
+
+uint64_t mul_inverse(uint64_t a) {  // a^-1 mod 2^64 for odd a (Newton)
+    uint64_t x = a;
+    for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+    return x;
+}
+
+uint64_t unxorshift(uint64_t z, int s) {
+    uint64_t x = z;
+    for (int i = 0; i < 64 / s + 1; ++i) x = z ^ (x >> s);
+    return x;
+}
+
+// Inverse of mix64: the canonical value behind a fast-path key.
+uint64_t unmix64(uint64_t z) {
+    z = unxorshift(z, 31);
+    z *= mul_inverse(0x94D049BB133111EBULL);
+    z = unxorshift(z, 27);
+    z *= mul_inverse(0xBF58476D1CE4E5B9ULL);
+    z = unxorshift(z, 30);
+    return z;
+}
+
+}  // namespace
+
+struct dq_ctx;  // defined in dq_api.cpp; only its device/stream are needed here
+extern "C" int dq_set_stream(dq_ctx* ctx, void* stream);
+namespace dq {
+hipStream_t ctx_stream(dq_ctx* ctx);
+int ctx_device(dq_ctx* ctx);
+int ctx_fail(dq_ctx* ctx, int code, const char* msg);
+}
+
+struct dq_freq_table {
+    int device = 0;
+    KeySpec ks;
+    Slot* slots = nullptr;
+    unsigned long long* reps = nullptr;
+    Counters* ctr = nullptr;  // device
+    Counters host_ctr;
+    uint64_t cap = 0;
+    int fast = 1;
+    void* scratch = nullptr;  // device scratch for scans
+    size_t scratch_bytes = 0;
+    std::vector<void*> staged;  // host key columns copied to HBM (rows are re-read by verify/export)
+};
+
+namespace {
+
+void free_table_buffers(dq_freq_table* t) {
+    if (t->slots) (void)hipFree(t->slots);
+    if (t->reps) (void)hipFree(t->reps);
+    if (t->ctr) (void)hipFree(t->ctr);
+    if (t->scratch) (void)hipFree(t->scratch);
+    t->slots = nullptr;
+    t->reps = nullptr;
+    t->ctr = nullptr;
+    t->scratch = nullptr;
+    for (void* p : t->staged) (void)hipFree(p);
+    t->staged.clear();
+}
+
+double hll_raw_estimate(const std::vector<unsigned int>& regs) {
+    const double m = (double)regs.size();
+    double z = 0.0, zeros = 0.0;
+    for (unsigned int r : regs) {
+        z += ldexp(1.0, -(int)r);
+        zeros += r == 0;
+    }
+    const double alpha = 0.7213 / (1.0 + 1.079 / m);
+    double e = alpha * m * m / z;
+    if (e <= 2.5 * m && zeros > 0) e = m * log(m / zeros);
+    return e;
+}
+
+int scan_grid(uint64_t n) {
+    uint64_t g = (n + kFreqBlock - 1) / kFreqBlock;
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(g, 2048));
+}
+
+}  // namespace
+
+#define FQ_HIP(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return dq::ctx_fail((ctx), DQ_ERR_DEVICE, hipGetErrorString(e_));   \
+    } while (0)
+
 extern "C" {
-int dq_frequencies(dq_ctx*, const dq_column*, int, int64_t, const int32_t*, int, uint32_t, dq_freq_table** t) {
-    if (t) *t = nullptr;
-    return DQ_ERR_UNSUPPORTED;
+
+int dq_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
+                   int nkeys, uint32_t flags, dq_freq_table** out) {
+    if (!ctx || !out || nkeys <= 0 || nkeys > kMaxKeys || nrows < 0)
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_frequencies: invalid arguments");
+    *out = nullptr;
+    const int dev = dq::ctx_device(ctx);
+    FQ_HIP(ctx, hipSetDevice(dev));
+    hipStream_t s = dq::ctx_stream(ctx);
+    dq_freq_table* t = new dq_freq_table();
+    t->device = dev;
+    memset(&t->ks, 0, sizeof(t->ks));
+    std::vector<void*> staged;
+    auto cleanup = [&]() {
+        for (void* p : staged) (void)hipFree(p);
+    };
+    for (int i = 0; i < nkeys; ++i) {
+        const int c = key_columns[i];
+        if (c < 0 || c >= ncols || columns[c].length != nrows) {
+            delete t;
+            return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_frequencies: bad key column");
+        }
+        const dq_column& col = columns[c];
+        KeyCol& kc = t->ks.cols[i];
+        kc.spark_type = col.spark_type;
+        kc.elem = elem_of(col.spark_type);
+        if (col.flags & DQ_COL_DEVICE) {
+            kc.values = col.values;
+            kc.validity = col.validity;
+            kc.offsets = col.offsets;
+        } else {
+            // stage host buffers (kept alive with the table: rows are re-read by verify / export)
+            size_t vbytes = col.spark_type == DQ_TYPE_STRING ? (nrows ? (size_t)col.offsets[nrows] : 0)
+                                                              : (size_t)nrows * std::max(1, elem_size(kc.elem));
+            void* v = nullptr;
+            FQ_HIP(ctx, hipMalloc(&v, vbytes + 16));
+            staged.push_back(v);
+            if (vbytes) FQ_HIP(ctx, hipMemcpyAsync(v, col.values, vbytes, hipMemcpyHostToDevice, s));
+            kc.values = v;
+            if (col.validity) {
+                void* vd = nullptr;
+                const size_t nb = (size_t)(nrows + 7) / 8;
+                FQ_HIP(ctx, hipMalloc(&vd, nb + 8));
+                staged.push_back(vd);
+                if (nb) FQ_HIP(ctx, hipMemcpyAsync(vd, col.validity, nb, hipMemcpyHostToDevice, s));
+                kc.validity = (const uint8_t*)vd;
+            }
+            if (col.spark_type == DQ_TYPE_STRING) {
+                void* od = nullptr;
+                FQ_HIP(ctx, hipMalloc(&od, ((size_t)nrows + 1) * 4));
+                staged.push_back(od);
+                FQ_HIP(ctx, hipMemcpyAsync(od, col.offsets, ((size_t)nrows + 1) * 4, hipMemcpyHostToDevice, s));
+                kc.offsets = (const int32_t*)od;
+            }
+        }
+        if (kc.elem == ET_NONE && kc.spark_type != DQ_TYPE_STRING) {
+            cleanup();
+            delete t;
+            return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_frequencies: unsupported key type");
+        }
+    }
+    t->ks.ncols = nkeys;
+    t->ks.include_nulls = (flags & DQ_FREQ_INCLUDE_NULLS) ? 1 : 0;
+    t->ks.fast = (nkeys == 1 && t->ks.cols[0].spark_type != DQ_TYPE_STRING) ? 1 : 0;
+    t->ks.string_null_is_value = (t->ks.include_nulls && nkeys == 1 && t->ks.cols[0].spark_type == DQ_TYPE_STRING);
+    t->fast = t->ks.fast;
+    t->ks.seed = 0x243F6A8885A308D3ULL;
+
+    // pass 1: size the table from an HLL estimate of the distinct keys
+    unsigned int* regs = nullptr;
+    FQ_HIP(ctx, hipMalloc(&regs, kSizingRegs * sizeof(unsigned int)));
+    FQ_HIP(ctx, hipMemsetAsync(regs, 0, kSizingRegs * sizeof(unsigned int), s));
+    if (nrows > 0) hipLaunchKernelGGL(sizing_hll_kernel, dim3(scan_grid((uint64_t)nrows)), dim3(kFreqBlock), 0, s, t->ks, nrows, regs);
+    std::vector<unsigned int> hregs(kSizingRegs);
+    FQ_HIP(ctx, hipMemcpyAsync(hregs.data(), regs, kSizingRegs * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    (void)hipFree(regs);
+    const double est = hll_raw_estimate(hregs);
+    uint64_t cap = 1024;
+    while ((double)cap < 2.2 * est && cap < (1ull << 40)) cap <<= 1;
+    FQ_HIP(ctx, hipMalloc(&t->ctr, sizeof(Counters)));
+
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        if (t->slots) (void)hipFree(t->slots);
+        if (t->reps) (void)hipFree(t->reps);
+        t->slots = nullptr;
+        t->reps = nullptr;
+        if (hipMalloc(&t->slots, cap * sizeof(Slot)) != hipSuccess ||
+            (!t->fast && hipMalloc(&t->reps, cap * sizeof(unsigned long long)) != hipSuccess)) {
+            cleanup();
+            free_table_buffers(t);
+            delete t;
+            return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
+        }
+        t->cap = cap;
+        FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
+        hipLaunchKernelGGL(fill_kernel, dim3(scan_grid(cap)), dim3(kFreqBlock), 0, s, t->slots, t->reps, cap);
+        if (nrows > 0) {
+            const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
+            hipLaunchKernelGGL(insert_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots, t->reps,
+                               cap - 1, t->ctr);
+            if (!t->fast)
+                hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots,
+                                   t->reps, cap - 1, t->ctr);
+        }
+        FQ_HIP(ctx, hipGetLastError());
+        FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+        FQ_HIP(ctx, hipStreamSynchronize(s));
+        if (t->host_ctr.overflow) {
+            cap <<= 2;
+            continue;
+        }
+        if (t->host_ctr.mismatch) {  // 64-bit fingerprint collision: new seed
+            t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
+            continue;
+        }
+        break;
+    }
+    if (t->host_ctr.overflow || t->host_ctr.mismatch) {
+        cleanup();
+        free_table_buffers(t);
+        delete t;
+        return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
+    }
+    t->scratch_bytes = kScanBlocks * (sizeof(SummaryPartial) + 3 * sizeof(unsigned long long)) + 2048 * 8 + 256;
+    FQ_HIP(ctx, hipMalloc(&t->scratch, t->scratch_bytes));
+    t->staged = staged;
+    *out = t;
+    return DQ_OK;
 }
-int dq_freq_summarize(dq_ctx*, const dq_freq_table*, int64_t, dq_freq_summary*) { return DQ_ERR_UNSUPPORTED; }
-int64_t dq_freq_top(dq_ctx*, const dq_freq_table*, int64_t, int64_t*, int64_t*) { return -1; }
-int64_t dq_freq_export(dq_ctx*, const dq_freq_table*, int64_t, int64_t*, int64_t*) { return -1; }
-void dq_freq_free(dq_ctx*, dq_freq_table*) {}
+
+int dq_freq_key_kind(const dq_freq_table* t) { return !t ? -1 : (t->fast ? DQ_FREQ_KEYS_VALUES : DQ_FREQ_KEYS_ROWS); }
+
+int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows, dq_freq_summary* out) {
+    if (!ctx || !t || !out) return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_summarize: invalid arguments");
+    FQ_HIP(ctx, hipSetDevice(t->device));
+    hipStream_t s = dq::ctx_stream(ctx);
+    const int64_t n = entropy_rows > 0 ? entropy_rows : (int64_t)t->host_ctr.num_rows;
+    SummaryPartial* parts = (SummaryPartial*)t->scratch;
+    hipLaunchKernelGGL(summary_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->cap, (double)n, parts);
+    FQ_HIP(ctx, hipGetLastError());
+    std::vector<SummaryPartial> hp(kScanBlocks);
+    FQ_HIP(ctx, hipMemcpyAsync(hp.data(), parts, sizeof(SummaryPartial) * kScanBlocks, hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    unsigned long long groups = 0, unique = 0, maxc = 0;
+    double ent = 0.0, comp = 0.0;
+    auto add_term = [&](double term) {
+        const double y = term - comp;
+        const double tt = ent + y;
+        comp = (tt - ent) - y;
+        ent = tt;
+    };
+    for (const SummaryPartial& p : hp) {
+        groups += p.groups;
+        unique += p.unique;
+        maxc = std::max(maxc, p.maxc);
+        add_term(p.ent - p.comp);
+    }
+    // side groups: the fast path's EMPTY-colliding value and (Histogram) the NULL group
+    for (unsigned long long extra : {t->host_ctr.sentinel, t->host_ctr.nulls}) {
+        if (!extra) continue;
+        groups += 1;
+        unique += extra == 1;
+        maxc = std::max(maxc, extra);
+        if (n > 0) {
+            const double q = (double)extra / (double)n;
+            add_term(-q * log(q));
+        }
+    }
+    out->num_rows = (int64_t)t->host_ctr.num_rows;
+    out->num_groups = (int64_t)groups;
+    out->num_unique = (int64_t)unique;
+    out->entropy = ent;
+    out->entropy_rows = n;
+    out->max_count = (int64_t)maxc;
+    out->null_count = (int64_t)t->host_ctr.nulls;
+    return DQ_OK;
 }
+
+static int64_t compact(dq_ctx* ctx, const dq_freq_table* t, int mode, unsigned int thr, uint64_t limit,
+                       std::vector<unsigned long long>& keys, std::vector<unsigned long long>& counts) {
+    hipStream_t s = dq::ctx_stream(ctx);
+    unsigned long long* per_block = (unsigned long long*)((char*)t->scratch + kScanBlocks * sizeof(SummaryPartial));
+    unsigned long long* offsets = per_block + kScanBlocks;
+    hipLaunchKernelGGL(count_selected_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->cap, mode, thr,
+                       per_block);
+    std::vector<unsigned long long> pb(kScanBlocks), off(kScanBlocks);
+    if (hipMemcpyAsync(pb.data(), per_block, kScanBlocks * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    unsigned long long total = 0;
+    for (int b = 0; b < kScanBlocks; ++b) {
+        off[b] = total;
+        total += pb[b];
+    }
+    const uint64_t n = std::min<uint64_t>(total, limit);
+    keys.assign(n, 0);
+    counts.assign(n, 0);
+    if (n == 0) return 0;
+    unsigned long long* dk = nullptr;
+    unsigned long long* dc = nullptr;
+    if (hipMalloc(&dk, n * 8) != hipSuccess || hipMalloc(&dc, n * 8) != hipSuccess) return -1;
+    if (hipMemcpyAsync(offsets, off.data(), kScanBlocks * 8, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
+    hipLaunchKernelGGL(compact_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->reps, t->cap, mode, thr,
+                       offsets, (unsigned long long)n, dk, dc);
+    bool ok = hipMemcpyAsync(keys.data(), dk, n * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+              hipMemcpyAsync(counts.data(), dc, n * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+              hipStreamSynchronize(s) == hipSuccess;
+    (void)hipFree(dk);
+    (void)hipFree(dc);
+    return ok ? (int64_t)n : -1;
+}
+
+static void decode_keys(const dq_freq_table* t, std::vector<unsigned long long>& keys) {
+    if (t->fast)
+        for (auto& k : keys) k = unmix64(k);
+}
+
+int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* t, int64_t capacity, int64_t* keys, int64_t* counts) {
+    if (!ctx || !t || capacity < 0 || (capacity > 0 && (!keys || !counts))) return DQ_ERR_INVALID_ARGUMENT;
+    if (hipSetDevice(t->device) != hipSuccess) return DQ_ERR_DEVICE;
+    std::vector<unsigned long long> k, c;
+    if (compact(ctx, t, 2, 0, (uint64_t)capacity, k, c) < 0) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "export failed");
+    decode_keys(t, k);
+    int64_t n = (int64_t)k.size();
+    for (int64_t i = 0; i < n; ++i) {
+        keys[i] = (int64_t)k[i];
+        counts[i] = (int64_t)c[i];
+    }
+    if (t->host_ctr.sentinel && n < capacity) {
+        keys[n] = (int64_t)unmix64(kEmpty);
+        counts[n] = (int64_t)t->host_ctr.sentinel;
+        ++n;
+    }
+    return n;
+}
+
+int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* t, int64_t k, int64_t* keys, int64_t* counts) {
+    if (!ctx || !t || k < 0 || (k > 0 && (!keys || !counts))) return DQ_ERR_INVALID_ARGUMENT;
+    if (k == 0) return 0;
+    if (hipSetDevice(t->device) != hipSuccess) return DQ_ERR_DEVICE;
+    hipStream_t s = dq::ctx_stream(ctx);
+    // Radix select of the k-th largest count over three 11-bit digits.
+    unsigned long long* hist = (unsigned long long*)((char*)t->scratch + kScanBlocks * sizeof(SummaryPartial) +
+                                                     2 * kScanBlocks * 8);
+    unsigned int prefix = 0, prefix_mask = 0;
+    uint64_t remaining = (uint64_t)k;
+    std::vector<unsigned long long> h(2048);
+    bool exhausted = false;
+    for (int shift : {22, 11, 0}) {
+        if (hipMemsetAsync(hist, 0, 2048 * 8, s) != hipSuccess) return DQ_ERR_DEVICE;
+        hipLaunchKernelGGL(digit_hist_kernel, dim3(scan_grid(t->cap)), dim3(kFreqBlock), 0, s, t->slots, t->cap, shift,
+                           prefix_mask, prefix, hist);
+        if (hipMemcpyAsync(h.data(), hist, 2048 * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return DQ_ERR_DEVICE;
+        int d = 2047;
+        uint64_t acc = 0;
+        for (; d >= 0; --d) {
+            if (acc + h[d] >= remaining) break;
+            acc += h[d];
+        }
+        if (d < 0) {  // fewer groups than k: take all of them
+            exhausted = true;
+            break;
+        }
+
+        remaining -= acc;
+        prefix |= (unsigned int)d << shift;
+        prefix_mask |= 2047u << shift;
+    }
+    std::vector<unsigned long long> gk, gc, tk, tc;
+    if (exhausted) {
+        if (compact(ctx, t, 2, 0, UINT64_MAX, gk, gc) < 0) return DQ_ERR_DEVICE;
+    } else {
+        if (compact(ctx, t, 0, prefix, UINT64_MAX, gk, gc) < 0) return DQ_ERR_DEVICE;
+        if (compact(ctx, t, 1, prefix, remaining, tk, tc) < 0) return DQ_ERR_DEVICE;
+    }
+    decode_keys(t, gk);
+    decode_keys(t, tk);
+    std::vector<std::pair<unsigned long long, unsigned long long>> all;  // (count, key)
+    for (size_t i = 0; i < gk.size(); ++i) all.push_back({gc[i], gk[i]});
+    for (size_t i = 0; i < tk.size(); ++i) all.push_back({tc[i], tk[i]});
+    if (t->host_ctr.sentinel) all.push_back({t->host_ctr.sentinel, unmix64(kEmpty)});
+    std::stable_sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    const int64_t n = std::min<int64_t>(k, (int64_t)all.size());
+    for (int64_t i = 0; i < n; ++i) {
+        keys[i] = (int64_t)all[i].second;
+        counts[i] = (int64_t)all[i].first;
+    }
+    return n;
+}
+
+void dq_freq_free(dq_ctx* ctx, dq_freq_table* t) {
+    (void)ctx;
+    if (!t) return;
+    (void)hipSetDevice(t->device);
+    (void)hipDeviceSynchronize();
+    free_table_buffers(t);
+    delete t;
+}
+
+}  // extern "C"

@@ -72,6 +72,27 @@ __global__ void synth_validity_kernel(uint64_t seed, int64_t row0, int64_t nrows
     }
 }
 
+__global__ void synth_freq_keys_kernel(int64_t total, int64_t distinct, int64_t row0, int64_t nrows, int64_t* out) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const uint64_t half = (uint64_t)(distinct / 2 > 0 ? distinct / 2 : 1);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nrows; i += stride) {
+        const uint64_t r = (uint64_t)(row0 + i);
+        const uint64_t j = (uint64_t)(((unsigned __int128)r * 0x9E3779B1ULL) % (uint64_t)total);
+        const uint64_t k = j < (uint64_t)distinct ? j : (j - (uint64_t)distinct) % half;
+        uint64_t z = k;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        out[i] = (int64_t)(z ^ (z >> 31));
+    }
+}
+
+void launch_synth_freq_keys(int64_t total, int64_t distinct, int64_t row0, int64_t nrows, int64_t* out, hipStream_t s) {
+    int64_t blocks = (nrows + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(synth_freq_keys_kernel, dim3((unsigned)blocks), dim3(256), 0, s, total, distinct, row0, nrows, out);
+}
+
 void launch_synth_column(int kind, uint64_t seed, int64_t row0, int64_t nrows, void* out, hipStream_t s) {
     int64_t blocks = (nrows + 255) / 256;
     if (blocks > 65536) blocks = 65536;

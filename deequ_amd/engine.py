@@ -51,7 +51,11 @@ class FrequencyTable:
         rc = self.ctx.lib.dq_freq_summarize(self.ctx.handle, self.handle, int(entropy_rows or 0), ctypes.byref(out))
         self.ctx.check(rc, "dq_freq_summarize")
         return {"num_rows": out.num_rows, "num_groups": out.num_groups, "num_unique": out.num_unique,
-                "entropy": out.entropy, "entropy_rows": out.entropy_rows, "max_count": out.max_count}
+                "entropy": out.entropy, "entropy_rows": out.entropy_rows, "max_count": out.max_count,
+                "null_count": out.null_count}
+
+    def key_kind(self):
+        return self.ctx.lib.dq_freq_key_kind(self.handle)
 
     def _key_of_row(self, r):
         key = []
@@ -60,24 +64,55 @@ class FrequencyTable:
             key.append(c.value_at(int(r)) if valid else None)
         return tuple(key)
 
+    def _decode_value(self, k):
+        """Canonical 64-bit key of the single fixed-width key column -> Python value."""
+        c = self.key_columns[0]
+        u = np.uint64(k & 0xFFFFFFFFFFFFFFFF)
+        if c.spark_type == N.TYPE_DOUBLE:
+            return float(u.view(np.float64))
+        if c.spark_type == N.TYPE_FLOAT:
+            return float(np.uint32(int(u) & 0xFFFFFFFF).view(np.float32))
+        i = int(u.view(np.int64))
+        if c.spark_type == N.TYPE_BOOLEAN:
+            return bool(i)
+        if c.spark_type == N.TYPE_DECIMAL:
+            from decimal import Decimal
+            return Decimal(i).scaleb(-c.decimal_scale)
+        return i
+
+    def _decode(self, k):
+        if self.key_kind() == N.FREQ_KEYS_VALUES:
+            return (self._decode_value(int(k)),)
+        return self._key_of_row(int(k))
+
     def top(self, k):
-        """[(key tuple, count)] of the k largest groups (ties: smallest representative row)."""
+        """[(key tuple, count)] of the k largest groups (NULL group included for Histogram)."""
         k = int(min(k, self.num_groups))
-        rows = np.zeros(max(k, 1), dtype=np.int64)
+        keys = np.zeros(max(k, 1), dtype=np.int64)
         counts = np.zeros(max(k, 1), dtype=np.int64)
-        n = self.ctx.lib.dq_freq_top(self.ctx.handle, self.handle, k, rows.ctypes.data, counts.ctypes.data)
+        n = self.ctx.lib.dq_freq_top(self.ctx.handle, self.handle, k, keys.ctypes.data, counts.ctypes.data)
         if n < 0:
             raise N.NativeError(int(n), "dq_freq_top: %s" % self.ctx.last_error())
-        return [(self._key_of_row(int(rows[i])), int(counts[i])) for i in range(n)]
+        out = [(self._decode(keys[i]), int(counts[i])) for i in range(n)]
+        nulls = self.summary(None)["null_count"]
+        if nulls:
+            out.append(((None,) * len(self.key_columns), int(nulls)))
+            out.sort(key=lambda kv: -kv[1])
+            out = out[:k]
+        return out
 
     def to_dict(self):
         n = self.num_groups
-        rows = np.zeros(max(n, 1), dtype=np.int64)
+        keys = np.zeros(max(n, 1), dtype=np.int64)
         counts = np.zeros(max(n, 1), dtype=np.int64)
-        got = self.ctx.lib.dq_freq_export(self.ctx.handle, self.handle, n, rows.ctypes.data, counts.ctypes.data)
+        got = self.ctx.lib.dq_freq_export(self.ctx.handle, self.handle, n, keys.ctypes.data, counts.ctypes.data)
         if got < 0:
             raise N.NativeError(int(got), "dq_freq_export: %s" % self.ctx.last_error())
-        return {self._key_of_row(int(rows[i])): int(counts[i]) for i in range(got)}
+        out = {self._decode(keys[i]): int(counts[i]) for i in range(got)}
+        nulls = self.summary(None)["null_count"]
+        if nulls:
+            out[(None,) * len(self.key_columns)] = int(nulls)
+        return out
 
 
 def frequencies(table, key_columns, include_nulls=False):

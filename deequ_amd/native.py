@@ -24,6 +24,7 @@ TYPE_BOOLEAN, TYPE_BYTE, TYPE_SHORT, TYPE_INT, TYPE_LONG, TYPE_FLOAT, TYPE_DOUBL
 COL_DEVICE = 0x1
 SCAN_OUT_DEVICE = 0x1
 FREQ_INCLUDE_NULLS = 0x1
+FREQ_KEYS_VALUES, FREQ_KEYS_ROWS = 0, 1
 
 OP_SIZE, OP_COMPLETENESS, OP_COMPLIANCE, OP_MEAN, OP_SUM, OP_MINIMUM, OP_MAXIMUM, OP_STANDARD_DEVIATION, \
     OP_CORRELATION, OP_APPROX_COUNT_DISTINCT, OP_MIN_LENGTH, OP_MAX_LENGTH, OP_DATATYPE = range(1, 14)
@@ -44,7 +45,8 @@ HLL_NUM_WORDS = 52
 EXPORTED_SYMBOLS = (
     "dq_abi_version", "dq_open", "dq_close", "dq_last_error", "dq_set_stream", "dq_synchronize", "dq_scan",
     "dq_scan_launch_count", "dq_state_merge", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
-    "dq_freq_summarize", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_synth_column", "dq_synth_validity",
+    "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_synth_column", "dq_synth_freq_keys",
+    "dq_synth_validity",
 )
 
 
@@ -114,7 +116,8 @@ class DqState(ctypes.Structure):
 
 class DqFreqSummary(ctypes.Structure):
     _fields_ = [("num_rows", ctypes.c_int64), ("num_groups", ctypes.c_int64), ("num_unique", ctypes.c_int64),
-                ("entropy", ctypes.c_double), ("entropy_rows", ctypes.c_int64), ("max_count", ctypes.c_int64)]
+                ("entropy", ctypes.c_double), ("entropy_rows", ctypes.c_int64), ("max_count", ctypes.c_int64),
+                ("null_count", ctypes.c_int64)]
 
 
 STATE_SIZE = ctypes.sizeof(DqState)
@@ -158,10 +161,12 @@ def load_library(path=None):
             "dq_spark_hash64": (c_int64, [ctypes.c_int32, c_void_p, c_int64]),
             "dq_frequencies": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_uint32, c_void_p]),
             "dq_freq_summarize": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+            "dq_freq_key_kind": (c_int, [c_void_p]),
             "dq_freq_top": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
             "dq_freq_export": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
             "dq_freq_free": (None, [c_void_p, c_void_p]),
             "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
+            "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
             "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),
         }
         for name, (res, args) in sig.items():
@@ -263,6 +268,10 @@ class Context:
     def synth_column(self, kind, seed, row0, nrows, dev_ptr):
         self.check(self.lib.dq_synth_column(self.handle, kind, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows,
                                             ctypes.c_void_p(dev_ptr)), "dq_synth_column")
+
+    def synth_freq_keys(self, total_rows, distinct, row0, nrows, dev_ptr):
+        self.check(self.lib.dq_synth_freq_keys(self.handle, int(total_rows), int(distinct), int(row0), int(nrows),
+                                               ctypes.c_void_p(dev_ptr)), "dq_synth_freq_keys")
 
     def synth_validity(self, seed, row0, nrows, null_permille, dev_ptr):
         self.check(self.lib.dq_synth_validity(self.handle, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows, null_permille,

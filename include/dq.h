@@ -179,6 +179,7 @@ typedef struct dq_freq_summary {
     double entropy;        /* sum over groups of -(c/N) ln(c/N), N = entropy_rows                     */
     int64_t entropy_rows;  /* the N used for `entropy`                                                 */
     int64_t max_count;
+    int64_t null_count;    /* DQ_FREQ_INCLUDE_NULLS: rows whose keys are all NULL (one extra group)  */
 } dq_freq_summary;
 
 /* ---------------------------------------------------------------------------------------------
@@ -226,11 +227,17 @@ int dq_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nro
 /* Fused aggregation over the table (Uniqueness/Distinctness/UniqueValueRatio/Entropy/CountDistinct);
  * entropy_rows <= 0 means "use this table's num_rows". */
 int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* table, int64_t entropy_rows, dq_freq_summary* out);
-/* Export up to k (key-row, count) pairs with the largest counts (Histogram top-N,
- * A/Histogram.scala:76-78). Ties are broken by smallest representative row. Returns the number written. */
-int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* table, int64_t k, int64_t* rep_rows, int64_t* counts);
-/* Export the whole table: group representative row index and count for every group. */
-int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* table, int64_t capacity, int64_t* rep_rows, int64_t* counts);
+/* How exported groups are identified: DQ_FREQ_KEYS_VALUES = the canonical 64-bit key of the single
+ * fixed-width key column (integers sign-extended, FLOAT/DOUBLE bit patterns with NaN canonical),
+ * DQ_FREQ_KEYS_ROWS = the smallest row index of the group (multi-column or string keys). */
+#define DQ_FREQ_KEYS_VALUES 0
+#define DQ_FREQ_KEYS_ROWS 1
+int dq_freq_key_kind(const dq_freq_table* table);
+/* Export up to k (key, count) pairs with the largest counts (Histogram top-N, A/Histogram.scala:76-78).
+ * Ties are broken by slot order (deterministic). Returns the number written, < 0 on error. */
+int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* table, int64_t k, int64_t* keys, int64_t* counts);
+/* Export the whole table (every group's key and count). Returns the number written, < 0 on error. */
+int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* table, int64_t capacity, int64_t* keys, int64_t* counts);
 void dq_freq_free(dq_ctx* ctx, dq_freq_table* table);
 
 /* Synthetic input generators for benches/tests (counter-based splitmix64). */
@@ -245,6 +252,11 @@ typedef enum dq_synth_kind {
 
 int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int64_t nrows,
                     void* values_dev);
+/* Config-C4 frequency keys: row r of a `total_rows` table gets key
+ * mix64(j < distinct ? j : (j - distinct) mod (distinct / 2)) with j = (r * 0x9E3779B1) mod total_rows,
+ * so exactly `distinct` keys exist when (total_rows - distinct) is a multiple of distinct / 2. */
+int dq_synth_freq_keys(dq_ctx* ctx, int64_t total_rows, int64_t distinct, int64_t row0, int64_t nrows,
+                       int64_t* keys_dev);
 /* Validity bitmap (ceil(nrows/64) words) with P(null) = null_permille / 1000. */
 int dq_synth_validity(dq_ctx* ctx, uint64_t seed, int64_t row0, int64_t nrows, int32_t null_permille,
                       uint8_t* validity_dev);

@@ -393,3 +393,17 @@ int64_t oracle_scan_spark(int spark_type, const void* values, const uint8_t* val
     out5[4] = wn > 0 ? sqrt(wm2 / wn) : NAN;
     return nrows;
 }
+
+/* Config-C4 frequency keys (same formula as deequ_amd/csrc/synth.hip). */
+void oracle_synth_freq_keys(int64_t total, int64_t distinct, int64_t row0, int64_t n, int64_t* out) {
+    const uint64_t half = (uint64_t)(distinct / 2 > 0 ? distinct / 2 : 1);
+    for (int64_t i = 0; i < n; ++i) {
+        const uint64_t r = (uint64_t)(row0 + i);
+        const uint64_t j = (uint64_t)(((unsigned __int128)r * 0x9E3779B1ULL) % (uint64_t)total);
+        const uint64_t k = j < (uint64_t)distinct ? j : (j - (uint64_t)distinct) % half;
+        uint64_t z = k;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        out[i] = (int64_t)(z ^ (z >> 31));
+    }
+}

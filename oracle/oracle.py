@@ -63,6 +63,8 @@ def lib():
                                           ctypes.c_void_p]
         L.oracle_synth_validity.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
                                             ctypes.c_void_p]
+        L.oracle_synth_freq_keys.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -91,6 +93,12 @@ def synth_column(kind, seed, row0, n):
     dt = np.int64 if kind in (4, 5) else np.float64
     out = np.zeros(n, dtype=dt)
     lib().oracle_synth_column(kind, seed, row0, n, out.ctypes.data)
+    return out
+
+
+def synth_freq_keys(total, distinct, row0, n):
+    out = np.zeros(n, dtype=np.int64)
+    lib().oracle_synth_freq_keys(total, distinct, row0, n, out.ctypes.data)
     return out
 
 

@@ -1,0 +1,170 @@
+"""GPU parity of the frequency tables (grouping analyzers + Histogram) against the oracle and the
+reference KATs. Bars: bit-exact group counts / numRows / distinct counts / histograms; entropy within
+1e-12 relative of the exact (fsum) oracle."""
+import math
+
+import numpy as np
+import pytest
+
+import deequ_amd as D
+import deequ_amd.native as N
+from deequ_amd import engine
+from deequ_amd.table import Table, Column, pack_validity
+import oracle as O
+from helpers import analyzer_from_spec, check_metric, table_from_fixture
+
+pytestmark = pytest.mark.gpu
+
+GROUPING = {"Uniqueness", "Distinctness", "UniqueValueRatio", "Entropy", "CountDistinct", "MutualInformation",
+            "Histogram"}
+
+
+def test_grouping_kats(kats):
+    for k in kats["kats"]:
+        if k["analyzer"][0] not in GROUPING:
+            continue
+        t = table_from_fixture(kats["fixtures"][k["fixture"]])
+        a = analyzer_from_spec(k["analyzer"])
+        check_metric(a.calculate(t), k["expected"], rel=1e-15)
+
+
+def test_grouping_kats_through_runner(kats):
+    # several grouping analyzers on the same columns share one frequency table
+    t = table_from_fixture(kats["fixtures"]["dfFull"])
+    analyzers = [D.Uniqueness(["att1"]), D.Distinctness(["att1"]), D.Entropy("att1"), D.CountDistinct(["att1"]),
+                 D.UniqueValueRatio(["att1"]), D.Size()]
+    ctx = D.AnalysisRunner.onData(t).addAnalyzers(analyzers).run()
+    assert ctx.metric(D.Uniqueness(["att1"])).value.get() == 0.25
+    assert ctx.metric(D.Distinctness(["att1"])).value.get() == 0.5
+    ent = -(0.75 * math.log(0.75) + 0.25 * math.log(0.25))
+    assert abs(ctx.metric(D.Entropy("att1")).value.get() - ent) < 1e-15
+    assert ctx.metric(D.CountDistinct(["att1"])).value.get() == 2.0
+    assert ctx.metric(D.UniqueValueRatio(["att1"])).value.get() == 0.5
+    assert ctx.metric(D.Size()).value.get() == 4.0
+
+
+def test_incremental_grouping_merges(kats):
+    inc = kats["incremental"]
+    a, b = table_from_fixture(inc["initial"]), table_from_fixture(inc["delta"])
+    for spec, va, vb, vm, src in inc["cases"]:
+        an = analyzer_from_spec(spec)
+        if type(an).__name__ not in GROUPING:
+            continue
+        sa, sb = an.computeStateFrom(a), an.computeStateFrom(b)
+        assert an.computeMetricFrom(sa).value.get() == va, src
+        assert an.computeMetricFrom(sb).value.get() == vb, src
+        assert an.computeMetricFrom(sa.sum(sb)).value.get() == vm, src
+
+
+def _summary_vs_oracle(table, cols, include_nulls=False):
+    ft = engine.frequencies(table, cols, include_nulls=include_nulls)
+    s = ft.summary(None)
+    freq, n = O.frequencies(table, cols, include_nulls=include_nulls)
+    exp = O.grouping_summary(freq, n)
+    assert s["num_rows"] == n
+    assert s["num_groups"] == exp["num_groups"]
+    assert s["num_unique"] == exp["num_unique"]
+    assert abs(s["entropy"] - exp["entropy"]) <= 1e-12 * max(1.0, exp["entropy"])
+    got = ft.to_dict()
+    norm = {tuple(O._group_key(v) for v in k): c for k, c in got.items()}
+    assert norm == freq
+    return ft, freq
+
+
+@pytest.mark.parametrize("n", [0, 1, 1000, 65537])
+def test_fixed_width_keys_parity(n):
+    rng = np.random.default_rng(n)
+    valid = rng.random(n) > 0.1
+    cols = {
+        "l": rng.integers(-50, 50, n).astype(np.int64),
+        "i": rng.integers(-3, 3, n).astype(np.int32),
+        "d": np.where(rng.random(n) < 0.05, np.nan, rng.integers(0, 20, n) / 4.0),
+        "f": (rng.integers(0, 7, n) / 2.0).astype(np.float32),
+        "b": rng.integers(0, 2, n).astype(np.bool_),
+        "u": rng.permutation(n).astype(np.int64),
+    }
+    t = Table.from_arrays(cols, validity={"l": valid, "d": valid})
+    for c in cols:
+        _summary_vs_oracle(t, [c])
+        _summary_vs_oracle(t, [c], include_nulls=True)
+
+
+def test_signed_zero_and_nan_grouping():
+    x = np.array([0.0, -0.0, np.nan, float(np.frombuffer(np.uint64(0x7ff8000000000001).tobytes(), np.float64)[0]),
+                  1.0, 1.0])
+    t = Table.from_arrays({"x": x})
+    ft, freq = _summary_vs_oracle(t, ["x"])
+    assert ft.summary()["num_groups"] == 4  # 0.0, -0.0, NaN (canonical), 1.0
+
+
+def test_all_ones_key_is_counted():
+    # int64 -1 has every bit set: the fast path must not confuse it with an empty slot
+    t = Table.from_arrays({"k": np.array([-1, -1, 5, -1, 0], dtype=np.int64)})
+    _summary_vs_oracle(t, ["k"])
+
+
+def test_string_and_multicolumn_keys_parity():
+    rng = np.random.default_rng(3)
+    n = 20000
+    words = ["", "a", "bb", "ccc", "ü", "NullValue", "x" * 40, "long string " * 5]
+    s1 = [None if rng.random() < 0.1 else words[rng.integers(0, len(words))] for _ in range(n)]
+    s2 = [None if rng.random() < 0.3 else str(rng.integers(0, 30)) for _ in range(n)]
+    i1 = [None if rng.random() < 0.2 else int(rng.integers(0, 4)) for _ in range(n)]
+    t = Table.from_pydict({"s1": s1, "s2": s2, "i1": i1}, types={"s1": "string", "s2": "string", "i1": "int"})
+    _summary_vs_oracle(t, ["s1"])
+    _summary_vs_oracle(t, ["s1", "s2"])
+    _summary_vs_oracle(t, ["s2", "i1"])
+    _summary_vs_oracle(t, ["s1", "s2", "i1"])
+
+
+def test_histogram_string_null_merges_with_literal_nullvalue():
+    # Histogram casts to string and fills NULL with "NullValue" (A/Histogram.scala:60-63)
+    t = Table.from_pydict({"s": ["NullValue", None, "a", None]}, types={"s": "string"})
+    m = D.Histogram("s").calculate(t)
+    dist = m.value.get()
+    assert dist.numberOfBins == 2
+    assert dist["NullValue"].absolute == 3 and dist["a"].absolute == 1
+
+
+def test_histogram_topn_and_ratios():
+    rng = np.random.default_rng(8)
+    n = 50000
+    vals = rng.zipf(1.6, n) % 3000
+    valid = rng.random(n) > 0.02
+    t = Table.from_arrays({"v": vals.astype(np.int64)}, validity={"v": valid})
+    m = D.Histogram("v", None, 100).calculate(t)
+    dist = m.value.get()
+    freq, _ = O.frequencies(t, ["v"], include_nulls=True)
+    assert dist.numberOfBins == len(freq)
+    top = sorted(freq.values(), reverse=True)[:100]
+    assert sorted((v.absolute for v in dist.values.values()), reverse=True) == top
+    for key, v in dist.values.items():
+        okey = None if key == "NullValue" else int(key)
+        assert freq[(okey,)] == v.absolute
+        assert v.ratio == v.absolute / n
+
+
+def test_c4_closed_form_at_reduced_scale():
+    # exactly D distinct keys, D/2 of them 19 times and D/2 once.
+    total, distinct = 10_000_000, 1_000_000
+    import torch
+    keys = torch.empty(total, dtype=torch.int64, device="cuda")
+    engine.ctx().synth_freq_keys(total, distinct, 0, total, keys.data_ptr())
+    engine.ctx().synchronize()
+    col = Column("k", N.TYPE_LONG, None, None, length=total)
+    col.device = {"values": keys}
+    t = Table([col])
+    analyzers = [D.Uniqueness(["k"]), D.Distinctness(["k"]), D.UniqueValueRatio(["k"]), D.CountDistinct(["k"]),
+                 D.Entropy("k")]
+    ctx = D.AnalysisRunner.onData(t).addAnalyzers(analyzers).run()
+    half = distinct // 2
+    assert ctx.metric(analyzers[0]).value.get() == half / total
+    assert ctx.metric(analyzers[1]).value.get() == distinct / total
+    assert ctx.metric(analyzers[2]).value.get() == 0.5
+    assert ctx.metric(analyzers[3]).value.get() == float(distinct)
+    big = (total - half) / half  # occurrences of the repeated keys
+    exact = math.fsum([-half * (big / total) * math.log(big / total), -half * (1 / total) * math.log(1 / total)])
+    assert abs(ctx.metric(analyzers[4]).value.get() - exact) <= 1e-12 * exact
+    # device generator == oracle generator on a slice
+    sl = keys[123456:123456 + 4096].cpu().numpy()
+    assert np.array_equal(sl, O.synth_freq_keys(total, distinct, 123456, 4096))
