@@ -518,13 +518,15 @@ class MutualInformation(FrequencyBasedAnalyzer):
         for (a, b), c in joint.items():
             px[a] = px.get(a, 0) + c
             py[b] = py.get(b, 0) + c
-        mi = 0.0
+        terms = []
         for (a, b), c in joint.items():
             if a is None or b is None:
                 continue  # Spark's equi-join on the marginals drops NULL keys
             pxy = c / total
-            mi += pxy * math.log(pxy / ((px[a] / total) * (py[b] / total)))
-        return metricFromValue(mi, self.name, inst, Entity.Mutlicolumn)
+            terms.append(pxy * math.log(pxy / ((px[a] / total) * (py[b] / total))))
+        if not terms:  # sum over zero joined rows is NULL (A/MutualInformation.scala:82-86)
+            return metricFromEmpty(self, self.name, inst, Entity.Mutlicolumn)
+        return metricFromValue(math.fsum(terms), self.name, inst, Entity.Mutlicolumn)
 
     def toFailureMetric(self, exception):
         return metricFromFailure(exception, self.name, ",".join(self.columns), Entity.Mutlicolumn)

@@ -24,6 +24,29 @@ def ctx():
     return N.context(device())
 
 
+class GroupFloat(float):
+    """A float group key with Spark's grouping equality: bitwise, NaN canonical (so NaN == NaN and
+    -0.0 != 0.0, unlike Python floats). Formats like a float."""
+
+    def _bits(self):
+        v = float(self)
+        if v != v:
+            return 0x7FF8000000000000
+        return int(np.array([v], dtype=np.float64).view(np.uint64)[0])
+
+    def __eq__(self, other):
+        if isinstance(other, float):
+            return self._bits() == GroupFloat(other)._bits()
+        return NotImplemented
+
+    def __ne__(self, other):
+        r = self.__eq__(other)
+        return r if r is NotImplemented else not r
+
+    def __hash__(self):
+        return hash(("GroupFloat", self._bits()))
+
+
 class FrequencyTable:
     """Device-resident (key -> count) table built by dq_frequencies over `key_columns` of `source`."""
 
@@ -61,7 +84,8 @@ class FrequencyTable:
         key = []
         for c in self.key_columns:
             valid = c.validity is None or bool((c.validity[r >> 3] >> (r & 7)) & 1)
-            key.append(c.value_at(int(r)) if valid else None)
+            v = c.value_at(int(r)) if valid else None
+            key.append(GroupFloat(v) if isinstance(v, float) else v)
         return tuple(key)
 
     def _decode_value(self, k):
@@ -69,9 +93,9 @@ class FrequencyTable:
         c = self.key_columns[0]
         u = np.uint64(k & 0xFFFFFFFFFFFFFFFF)
         if c.spark_type == N.TYPE_DOUBLE:
-            return float(u.view(np.float64))
+            return GroupFloat(u.view(np.float64))
         if c.spark_type == N.TYPE_FLOAT:
-            return float(np.uint32(int(u) & 0xFFFFFFFF).view(np.float32))
+            return GroupFloat(np.uint32(int(u) & 0xFFFFFFFF).view(np.float32))
         i = int(u.view(np.int64))
         if c.spark_type == N.TYPE_BOOLEAN:
             return bool(i)

@@ -381,10 +381,12 @@ def frequencies(table, columns, include_nulls=False):
 def _group_key(v):
     """Spark groups on binary equality: NaN canonical, -0.0 != 0.0."""
     if isinstance(v, float):
-        if math.isnan(v):
+        fv = float(v)
+        if math.isnan(fv):
             return ("nan",)
-        if v == 0.0 and math.copysign(1.0, v) < 0:
+        if fv == 0.0 and math.copysign(1.0, fv) < 0:
             return ("-0.0",)
+        return fv
     return v
 
 
