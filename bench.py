@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample-rows", type=int, default=8_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
+    ap.add_argument("--device-override", type=int, default=None, help="run every rank on this GPU (rehearsal)")
     args = ap.parse_args()
 
     import torch
@@ -97,7 +99,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
+    if args.device_override is not None:
+        local = args.device_override
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -123,7 +127,8 @@ def main():
     offsets = [a.addOps(batch) for a in analyzers]
     nops = len(batch.ops)
     out = torch.empty(nops * N.STATE_SIZE, dtype=torch.uint8, device=dev)
-    gathered = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, device=dev)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    gathered = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, device=coll_dev)
     host = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, pin_memory=True)
     cols = batch.native_columns()
     preds = [p.to_native() for p in batch.preds]
@@ -136,7 +141,7 @@ def main():
         if i is not None:
             ev[i][1].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out)  # RCCL over xGMI
+            dist.all_gather_into_tensor(gathered, out if args.dist_backend == "nccl" else out.cpu())  # RCCL over xGMI
             src = gathered
         else:
             src = out
@@ -166,7 +171,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     scan_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))

@@ -15,5 +15,6 @@ from .analyzers import (Size, Completeness, Compliance, Mean, Sum, Minimum, Maxi
 from .runners import (AnalysisRunner, AnalysisRunBuilder, AnalyzerContext, Analysis, InMemoryStateProvider,
                       ScanBatch)
 from .table import Table, Column
+from . import distributed
 
 __all__ = [n for n in dir() if not n.startswith("_")]

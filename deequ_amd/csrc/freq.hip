@@ -785,3 +785,101 @@ void dq_freq_free(dq_ctx* ctx, dq_freq_table* t) {
 }
 
 }  // extern "C"
+
+// ---- multi-GPU key partitioning --------------------------------------------------------------------
+namespace {
+
+constexpr int kMaxParts = 64;
+
+__device__ __forceinline__ int owner_of(uint64_t canon, int nparts) {
+    return (int)((mix64(canon) >> 32) % (uint64_t)nparts);
+}
+
+__global__ void __launch_bounds__(kFreqBlock)
+part_count_kernel(KeyCol c, int64_t nrows, int nparts, unsigned long long* __restrict__ counts) {
+    __shared__ unsigned int lds[kMaxParts + 1];
+    for (int i = threadIdx.x; i <= kMaxParts; i += kFreqBlock) lds[i] = 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * kFreqBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < nrows; r += stride) {
+        if (!is_valid(c, r)) {
+            atomicAdd(&lds[kMaxParts], 1u);
+            continue;
+        }
+        atomicAdd(&lds[owner_of(canonical(c, r), nparts)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i <= kMaxParts; i += kFreqBlock)
+        if (lds[i]) atomicAdd(&counts[i], (unsigned long long)lds[i]);
+}
+
+// Each workgroup reserves its slice of every bucket with one atomic per bucket, then scatters.
+__global__ void __launch_bounds__(kFreqBlock)
+part_scatter_kernel(KeyCol c, int64_t nrows, int nparts, unsigned long long* __restrict__ cursors,
+                    unsigned long long* __restrict__ out) {
+    __shared__ unsigned int cnt[kMaxParts];
+    __shared__ unsigned long long base[kMaxParts];
+    const int64_t per_block = (nrows + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = (int64_t)blockIdx.x * per_block;
+    const int64_t r1 = r0 + per_block < nrows ? r0 + per_block : nrows;
+    for (int i = threadIdx.x; i < kMaxParts; i += kFreqBlock) cnt[i] = 0;
+    __syncthreads();
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kFreqBlock)
+        if (is_valid(c, r)) atomicAdd(&cnt[owner_of(canonical(c, r), nparts)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nparts; i += kFreqBlock) {
+        base[i] = cnt[i] ? atomicAdd(&cursors[i], (unsigned long long)cnt[i]) : 0ull;
+        cnt[i] = 0;
+    }
+    __syncthreads();
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kFreqBlock) {
+        if (!is_valid(c, r)) continue;
+        const uint64_t k = canonical(c, r);
+        const int p = owner_of(k, nparts);
+        const unsigned int slot = atomicAdd(&cnt[p], 1u);
+        out[base[p] + slot] = k;
+    }
+}
+
+}  // namespace
+
+extern "C" int dq_partition_keys(dq_ctx* ctx, const dq_column* column, int64_t nrows, int nparts, int64_t* keys_dev,
+                                 int64_t* part_counts, int64_t* null_rows) {
+    if (!ctx || !column || nparts < 1 || nparts > kMaxParts || nrows < 0 || !part_counts ||
+        column->length != nrows || elem_of(column->spark_type) == ET_NONE || !(column->flags & DQ_COL_DEVICE) ||
+        (nrows > 0 && !keys_dev))
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_partition_keys: invalid arguments (device fixed-width column)");
+    FQ_HIP(ctx, hipSetDevice(dq::ctx_device(ctx)));
+    hipStream_t s = dq::ctx_stream(ctx);
+    KeyCol c;
+    c.values = column->values;
+    c.validity = column->validity;
+    c.offsets = nullptr;
+    c.spark_type = column->spark_type;
+    c.elem = elem_of(column->spark_type);
+    unsigned long long* dev = nullptr;
+    FQ_HIP(ctx, hipMalloc(&dev, sizeof(unsigned long long) * 2 * (kMaxParts + 1)));
+    FQ_HIP(ctx, hipMemsetAsync(dev, 0, sizeof(unsigned long long) * 2 * (kMaxParts + 1), s));
+    const int grid = scan_grid((uint64_t)std::max<int64_t>(nrows, 1));
+    if (nrows > 0) hipLaunchKernelGGL(part_count_kernel, dim3(grid), dim3(kFreqBlock), 0, s, c, nrows, nparts, dev);
+    unsigned long long h[kMaxParts + 1];
+    FQ_HIP(ctx, hipMemcpyAsync(h, dev, sizeof(h), hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    unsigned long long cur[kMaxParts + 1] = {0};
+    unsigned long long off = 0;
+    for (int p = 0; p < nparts; ++p) {
+        cur[p] = off;
+        part_counts[p] = (int64_t)h[p];
+        off += h[p];
+    }
+    if (null_rows) *null_rows = (int64_t)h[kMaxParts];
+    unsigned long long* cursors = dev + kMaxParts + 1;
+    FQ_HIP(ctx, hipMemcpyAsync(cursors, cur, sizeof(unsigned long long) * kMaxParts, hipMemcpyHostToDevice, s));
+    if (nrows > 0)
+        hipLaunchKernelGGL(part_scatter_kernel, dim3(grid), dim3(kFreqBlock), 0, s, c, nrows, nparts, cursors,
+                           (unsigned long long*)keys_dev);
+    FQ_HIP(ctx, hipGetLastError());
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    (void)hipFree(dev);
+    return DQ_OK;
+}

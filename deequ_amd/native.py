@@ -45,7 +45,7 @@ HLL_NUM_WORDS = 52
 EXPORTED_SYMBOLS = (
     "dq_abi_version", "dq_open", "dq_close", "dq_last_error", "dq_set_stream", "dq_synchronize", "dq_scan",
     "dq_scan_launch_count", "dq_state_merge", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
-    "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_synth_column", "dq_synth_freq_keys",
+    "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity",
 )
 
@@ -165,6 +165,7 @@ def load_library(path=None):
             "dq_freq_top": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
             "dq_freq_export": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
             "dq_freq_free": (None, [c_void_p, c_void_p]),
+            "dq_partition_keys": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
             "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
             "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
             "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),

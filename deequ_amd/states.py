@@ -254,6 +254,40 @@ class ApproxCountDistinctState(DoubleValuedState):
         return "ApproxCountDistinctState(%s)" % ",".join(str(np.int64(np.uint64(w))) for w in self.words)
 
 
+def state_to_native(kind, state):
+    """Reference State (or None) -> dq_state record of op `kind` (persisted / exchanged states)."""
+    st = N.DqState()
+    st.kind = kind
+    st.present = 0 if state is None else 1
+    if state is None:
+        return st
+    u = st.u
+    if isinstance(state, NumMatches):
+        u.num_matches.num_matches = state.numMatches
+    elif isinstance(state, NumMatchesAndCount):
+        u.num_matches_and_count.num_matches = state.numMatches
+        u.num_matches_and_count.count = state.count
+    elif isinstance(state, MeanState):
+        u.mean.sum, u.mean.count = state.sum_, state.count
+    elif isinstance(state, SumState):
+        u.dbl.value = state.sum_
+    elif isinstance(state, MinState):
+        u.dbl.value = state.minValue
+    elif isinstance(state, MaxState):
+        u.dbl.value = state.maxValue
+    elif isinstance(state, StandardDeviationState):
+        u.stddev.n, u.stddev.avg, u.stddev.m2 = state.n, state.avg, state.m2
+    elif isinstance(state, CorrelationState):
+        c = u.corr
+        c.n, c.x_avg, c.y_avg, c.ck, c.x_mk, c.y_mk = state.n, state.xAvg, state.yAvg, state.ck, state.xMk, state.yMk
+    elif isinstance(state, ApproxCountDistinctState):
+        for i, w in enumerate(state.words):
+            u.hll.words[i] = int(np.int64(np.uint64(w)))
+    else:
+        raise ValueError("cannot encode %r" % (state,))
+    return st
+
+
 def state_from_native(st):
     """dq_state -> reference State (None for an absent state, i.e. ifNoNullsIn failed)."""
     if not st.present:

@@ -240,6 +240,15 @@ int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* table, int64_t k, int64_t*
 int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* table, int64_t capacity, int64_t* keys, int64_t* counts);
 void dq_freq_free(dq_ctx* ctx, dq_freq_table* table);
 
+/* Multi-GPU grouping: the canonical 64-bit keys (see DQ_FREQ_KEYS_VALUES) of one
+ * fixed-width column's non-NULL rows, bucketed by owner rank = (mix64(key) >> 32) % nparts, written
+ * contiguously per rank into keys_dev (capacity nrows, device memory) for an RCCL all-to-all; the
+ * owner of a key builds its table from the keys it receives, so every group lives on exactly one
+ * rank. part_counts (host, nparts entries) receives the bucket sizes; *null_rows the NULL rows.
+ * Returns DQ_OK or an error. */
+int dq_partition_keys(dq_ctx* ctx, const dq_column* column, int64_t nrows, int nparts, int64_t* keys_dev,
+                      int64_t* part_counts, int64_t* null_rows);
+
 /* Synthetic input generators for benches/tests (counter-based splitmix64). */
 typedef enum dq_synth_kind {
     DQ_SYNTH_DYADIC = 1,   /* f64: k * 2^-8, k uniform in [-256, 256]                */

@@ -1,0 +1,117 @@
+"""Secondary measurements for the other BASELINE.json configs (one JSON line each, single GPU):
+
+  c3     ApproxCountDistinct(k) + Correlation(x, y) + Completeness over 1e9 rows (k = splitmix64 mod 2^30,
+         x, y ~ sum-of-uniforms normals, 1 % nulls)                                  24.4 B/row
+  c4     Uniqueness / Distinctness / UniqueValueRatio / CountDistinct / Entropy on 1e9 int64 keys with
+         exactly 1e8 distinct (5e7 x 19 + 5e7 x 1), checked against the closed forms   8 B/row (+ table)
+  suite10  the north-star "10-analyzer" fused scan: C2 columns + Compliance(c_i > 0), ApproxCountDistinct(c_i),
+         Correlation(c_2k, c_2k+1)                                                    65 B/row
+
+    python tools/bench_configs.py --config c4 [--rows 1e9] [--steps 5]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PEAK = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", required=True, choices=["c3", "c4", "suite10"])
+    ap.add_argument("--rows", type=float, default=1e9)
+    ap.add_argument("--distinct", type=float, default=1e8)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+    import deequ_amd as D
+    import deequ_amd.native as N
+    from deequ_amd import engine
+    from deequ_amd.table import Table, Column
+    import bench
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    ctx = engine.ctx()
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    R = int(args.rows)
+
+    def col(name, kind, seed, spark_type, nulls=True):
+        dt = torch.float64 if spark_type == N.TYPE_DOUBLE else torch.int64
+        v = torch.empty(R, dtype=dt, device=dev)
+        ctx.synth_column(kind, seed, 0, R, v.data_ptr())
+        c = Column(name, spark_type, None, None, length=R)
+        c.device = {"values": v}
+        if nulls:
+            m = torch.zeros((R + 63) // 64 * 8, dtype=torch.uint8, device=dev)
+            ctx.synth_validity(seed + 0x100, 0, R, 10, m.data_ptr())
+            c.device["validity"] = m
+        return c
+
+    if args.config == "c3":
+        t = Table([col("k", 5, 0xC3000001, N.TYPE_LONG), col("x", 6, 0xC3000002, N.TYPE_DOUBLE),
+                   col("y", 6, 0xC3000003, N.TYPE_DOUBLE)])
+        analyzers = [D.ApproxCountDistinct("k"), D.Correlation("x", "y"), D.Completeness("k")]
+        bytes_per_row = 3 * (8 + 1 / 8)
+    elif args.config == "suite10":
+        t = bench.build_shard(torch, N, ctx, 0, R, dev)
+        names = list(t.columns)
+        analyzers = bench.c2_analyzers(D, names)
+        analyzers += [D.Compliance("pos_%s" % c, "%s > 0" % c) for c in names]
+        analyzers += [D.ApproxCountDistinct(c) for c in names]
+        analyzers += [D.Correlation(names[2 * i], names[2 * i + 1]) for i in range(4)]
+        bytes_per_row = 8 * (8 + 1 / 8)
+    else:
+        keys = torch.empty(R, dtype=torch.int64, device=dev)
+        ctx.synth_freq_keys(R, int(args.distinct), 0, R, keys.data_ptr())
+        c = Column("k", N.TYPE_LONG, None, None, length=R)
+        c.device = {"values": keys}
+        t = Table([c])
+        analyzers = [D.Uniqueness(["k"]), D.Distinctness(["k"]), D.UniqueValueRatio(["k"]), D.CountDistinct(["k"]),
+                     D.Entropy("k")]
+        bytes_per_row = 8.0
+    ctx.synchronize()
+
+    def run():
+        return D.AnalysisRunner.onData(t).addAnalyzers(analyzers).run()
+
+    for _ in range(args.warmup):
+        res = run()
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        res = run()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    sec = float(np.median(times))
+    out = {"config": args.config, "rows": R, "analyzers": len(analyzers), "ms": sec * 1e3, "rows_per_s": R / sec,
+           "algorithmic_GBps": bytes_per_row * R / sec / 1e9, "frac_of_peak": bytes_per_row * R / sec / 1e9 / PEAK,
+           "note": "end-to-end AnalysisRunner.run() wall time (plan + kernels + host metrics), median of %d"
+                   % args.steps}
+    if args.config == "c4":
+        Dn = int(args.distinct)
+        half = Dn // 2
+        big = (R - half) / half
+        exact_ent = math.fsum([-half * (big / R) * math.log(big / R), -half * (1 / R) * math.log(1 / R)])
+        got = {type(a).__name__: res.metric(a).value.get() for a in analyzers}
+        out["check"] = {"Uniqueness": got["Uniqueness"] == half / R, "Distinctness": got["Distinctness"] == Dn / R,
+                        "UniqueValueRatio": got["UniqueValueRatio"] == 0.5, "CountDistinct": got["CountDistinct"] == Dn,
+                        "Entropy_rel_err": abs(got["Entropy"] - exact_ent) / exact_ent}
+    else:
+        out["sample_metrics"] = {repr(a): res.metric(a).value.get() for a in analyzers[:3]}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
