@@ -111,7 +111,10 @@ def main():
     from deequ_amd.states import state_from_native
     engine.set_device(local)
     ctx = engine.ctx()
-    stream = torch.cuda.current_stream(dev)
+    # One explicit stream for the scan, the collectives and the copies (torch's default stream
+    # reports handle 0, which dq_set_stream would map to the context's own stream).
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
     total = int(args.rows)

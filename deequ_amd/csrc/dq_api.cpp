@@ -320,8 +320,15 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     }
 
     // ---- plan: column uses -> slots -----------------------------------------------------------
-    struct Use { uint32_t flags = 0; int slot = -1; int pos = 0; int hll = -1; };
+    struct Use {
+        uint32_t flags = 0;
+        int slot = -1, pos = 0, hll = -1;
+        int pred_op = 0, pred_kind = FP_NONE, pred_src = -1;  // fused `col <op> const` Compliance predicate
+        int64_t pred_i = 0;
+        double pred_d = 0.0;
+    };
     std::map<std::pair<int, int>, Use> uses;  // (column, where) -> use
+    std::vector<int> fused_col(nops, -1);     // Compliance ops answered inside a value slot
     for (int i = 0; i < nops; ++i) {
         const dq_op& op = ops[i];
         const auto key = std::make_pair(op.column[0], op.where);
@@ -329,6 +336,37 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             case DQ_OP_MEAN: case DQ_OP_SUM: case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM: uses[key].flags |= CF_STATS; break;
             case DQ_OP_STANDARD_DEVIATION: uses[key].flags |= CF_MOMENTS; break;
             case DQ_OP_APPROX_COUNT_DISTINCT: uses[key].flags |= CF_HLL; break;
+            case DQ_OP_COMPLIANCE: {
+                // `col <op> const` on a non-decimal numeric column: evaluate inside that column's scan.
+                const dq_predicate& pr = preds[op.predicate];
+                if (pr.code_len != 6) break;
+                int a = pr.code[0], aa = pr.code[1], b = pr.code[2], ba = pr.code[3], cmp = pr.code[4];
+                if (cmp < DQ_P_EQ || cmp > DQ_P_GE) break;
+                if (a == DQ_P_CONST && b == DQ_P_COL) {  // const <op> col  ->  col <op'> const
+                    std::swap(a, b);
+                    std::swap(aa, ba);
+                    if (cmp == DQ_P_LT) cmp = DQ_P_GT;
+                    else if (cmp == DQ_P_GT) cmp = DQ_P_LT;
+                    else if (cmp == DQ_P_LE) cmp = DQ_P_GE;
+                    else if (cmp == DQ_P_GE) cmp = DQ_P_LE;
+                }
+                if (a != DQ_P_COL || b != DQ_P_CONST || ba < 0 || ba >= pr.n_consts) break;
+                const dq_const& k = pr.consts[ba];
+                const int t = columns[aa].spark_type;
+                if (!(t >= DQ_TYPE_BYTE && t <= DQ_TYPE_DOUBLE) || (k.tag != DQ_V_LONG && k.tag != DQ_V_DOUBLE)) break;
+                Use& u = uses[std::make_pair(aa, op.where)];
+                const int kind = k.tag == DQ_V_LONG ? FP_LONG : FP_DOUBLE;
+                if (u.pred_kind != FP_NONE &&
+                    !(u.pred_op == cmp && u.pred_kind == kind && u.pred_i == k.i64 &&
+                      (kind == FP_LONG || u.pred_d == k.f64)))
+                    break;  // one fused predicate per column scan; others use the predicate VM
+                u.pred_op = cmp;
+                u.pred_kind = kind;
+                u.pred_i = k.i64;
+                u.pred_d = k.f64;
+                fused_col[i] = aa;
+                break;
+            }
             default: break;
         }
     }
@@ -389,6 +427,10 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     for (auto& kv : uses) {
         SlotDesc& sd = slots[kv.second.slot];
         sd.col[kv.second.pos].flags |= kv.second.flags;
+        sd.col[kv.second.pos].pred_op = kv.second.pred_op;
+        sd.col[kv.second.pos].pred_kind = kv.second.pred_kind;
+        sd.col[kv.second.pos].pred_i = kv.second.pred_i;
+        sd.col[kv.second.pos].pred_d = kv.second.pred_d;
         if (kv.second.flags & CF_HLL) {
             kv.second.hll = nhll++;
             sd.col[kv.second.pos].hll_slot = kv.second.hll;
@@ -428,7 +470,14 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 if (op.where >= 0) m.slot = bits_slot(0, -1, op.where);
                 break;
             case DQ_OP_COMPLIANCE:
-                m.slot = bits_slot(2, op.predicate, op.where);
+                if (fused_col[i] >= 0) {
+                    const Use& u = uses.at({fused_col[i], op.where});
+                    m.slot = u.slot;
+                    m.colpos = u.pos;
+                    m.from_bits = 3;  // fused predicate: matches = c.pt, non-null rows = c.n
+                } else {
+                    m.slot = bits_slot(2, op.predicate, op.where);
+                }
                 break;
             case DQ_OP_COMPLETENESS: {
                 auto it = uses.find({c, op.where});
@@ -459,13 +508,22 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     }
     const int nslots = (int)slots.size();
     if (nslots > kMaxSlots) return fail(ctx, DQ_ERR_UNSUPPORTED, "too many slots (%d)", nslots);
+    // Predicates evaluated by the VM pass: `where` filters and Compliance predicates not fused into
+    // a value scan.
+    std::fill(pred_used.begin(), pred_used.end(), 0);
+    for (int i = 0; i < nops; ++i) {
+        if (ops[i].where >= 0) pred_used[ops[i].where] = 1;
+        if (ops[i].kind == DQ_OP_COMPLIANCE && fused_col[i] < 0) pred_used[ops[i].predicate] = 1;
+    }
 
     // ---- device memory layout -----------------------------------------------------------------
     // Launch groups: one kernel launch per slot shape; each gets a grid sized to fill the chip once.
     const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
-    struct Group { int kind, P, nc; bool f0, f1; int grid; std::vector<int32_t> slots; };
+    struct Group { int kind, P, nc; bool f0, f1, heavy; int grid; std::vector<int32_t> slots; };
     std::vector<Group> groups;
-    auto shape_key = [](int kind, int P, int nc, bool f0, bool f1) { return ((((kind * 16 + P) * 4 + nc) * 2 + f0) * 2 + f1); };
+    auto shape_key = [](int kind, int P, int nc, bool f0, bool f1, bool heavy) {
+        return (((((kind * 16 + P) * 4 + nc) * 2 + f0) * 2 + f1) * 2 + heavy);
+    };
     std::map<int, int> group_of;
     for (int s = 0; s < (int)slots.size(); ++s) {
         const SlotDesc& sd = slots[s];
@@ -473,15 +531,19 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         const bool f1 = sd.kind == SK_VALUES && sd.ncols > 1 && (sd.col[1].elem == ET_F32 || sd.col[1].elem == ET_F64);
         const int P = sd.kind == SK_VALUES ? sd.rows_per_load : 8;
         const int nc = sd.kind == SK_VALUES ? sd.ncols : 1;
-        const int key = shape_key(sd.kind, P, nc, f0, f1);
+        // HLL registers or a fused predicate need the larger (HEAVY) kernel instantiation.
+        bool heavy = false;
+        for (int k = 0; sd.kind == SK_VALUES && k < sd.ncols; ++k)
+            heavy |= (sd.col[k].flags & CF_HLL) || sd.col[k].pred_kind != FP_NONE;
+        const int key = shape_key(sd.kind, P, nc, f0, f1, heavy);
         auto it = group_of.find(key);
         if (it == group_of.end()) {
             int occ;
             auto oc = ctx->occupancy.find(key);
             if (oc != ctx->occupancy.end()) occ = oc->second;
-            else occ = ctx->occupancy[key] = std::max(1, scan_group_blocks_per_cu(sd.kind, P, nc, f0, f1));
+            else occ = ctx->occupancy[key] = std::max(1, scan_group_blocks_per_cu(sd.kind, P, nc, f0, f1, heavy));
             const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(ntiles, 1), (int64_t)ctx->cus * occ));
-            groups.push_back(Group{sd.kind, P, nc, f0, f1, (int)grid, {}});
+            groups.push_back(Group{sd.kind, P, nc, f0, f1, heavy, (int)grid, {}});
             it = group_of.emplace(key, (int)groups.size() - 1).first;
         }
         groups[it->second].slots.push_back(s);
@@ -658,7 +720,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             if (rc) return rc;
             size_t off = 0;
             for (const Group& g : groups) {
-                if (launch_scan_group(g.kind, g.P, g.nc, g.f0, g.f1, dslots, dgroups + off, (int)g.slots.size(), nrows,
+                if (launch_scan_group(g.kind, g.P, g.nc, g.f0, g.f1, g.heavy, dslots, dgroups + off, (int)g.slots.size(), nrows,
                                       ntiles, gstride, g.grid, partials, hllp, ctx->stream) != 0)
                     return fail(ctx, DQ_ERR_DEVICE, "scan launch failed for shape (%d,%d,%d)", g.kind, g.P, g.nc);
                 DQ_HIP(ctx, hipGetLastError());

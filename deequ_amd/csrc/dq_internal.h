@@ -39,6 +39,9 @@ enum ColFlags : uint32_t {
 
 // Row mapping inside a 2048-row tile: L loads of P consecutive rows per thread, L * P = 8.
 // Striped (coalesced) for a single element size; pairs of different sizes use P = 8.
+// A Compliance predicate `column <op> constant` evaluated inside the value scan (no extra pass).
+enum FusedPredKind : int32_t { FP_NONE = 0, FP_LONG = 1, FP_DOUBLE = 2 };
+
 struct ColDesc {
     const void* values;
     const uint64_t* validity;  // nullptr = all valid
@@ -46,6 +49,10 @@ struct ColDesc {
     int32_t elem;              // ElemType
     uint32_t flags;            // ColFlags
     int32_t hll_slot;          // index into the HLL partial arrays, -1 = none
+    int32_t pred_op;           // dq_pred_opcode DQ_P_EQ..DQ_P_GE of the fused predicate
+    int32_t pred_kind;         // FusedPredKind
+    int64_t pred_i;            // constant (FP_LONG)
+    double pred_d;             // constant (FP_DOUBLE)
 };
 
 enum SlotKind : int32_t { SK_VALUES = 0, SK_BITS = 1 };
@@ -71,6 +78,8 @@ struct ColPartial {
     double dsum;
     double dmin, dmax;  // NaN-free min/max (NaN handled through nnan, Spark orders NaN largest)
     double mean, m2;    // Welford/Chan state over the same rows (n)
+    int64_t pt;         // rows of n where the fused predicate is TRUE
+    int64_t pad;
 };
 
 struct CorrPartial {
@@ -154,10 +163,10 @@ inline int rows_per_load_of(int e) {
 // Kernel launchers (defined in the .hip files).
 // One launch per slot shape (kind, P, column count, float/integral storage); each launch walks its
 // slots with tiles interleaved over `grid` workgroups and writes partials[slot * gstride + block].
-int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, const SlotDesc* slots, const int32_t* group,
-                      int ngroup, int64_t nrows, int64_t ntiles, int gstride, int grid, SlotPartial* partials,
-                      uint8_t* hll_partials, hipStream_t s);
-int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1);
+int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, bool heavy, const SlotDesc* slots,
+                      const int32_t* group, int ngroup, int64_t nrows, int64_t ntiles, int gstride, int grid,
+                      SlotPartial* partials, uint8_t* hll_partials, hipStream_t s);
+int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1, bool heavy);
 void launch_reduce_partials(const SlotPartial* partials, const int32_t* nblocks_of, int nslots, int gstride,
                             SlotPartial* finals, hipStream_t s);
 void launch_reduce_hll(const uint8_t* hll_partials, const int32_t* nblocks_of, int nhll, int gstride,

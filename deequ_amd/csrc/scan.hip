@@ -59,6 +59,8 @@ __device__ __forceinline__ void col_init(ColPartial& a) {
     a.dmax = -INFINITY;
     a.mean = 0.0;
     a.m2 = 0.0;
+    a.pt = 0;
+    a.pad = 0;
 }
 
 // StandardDeviationState.sum (A/StandardDeviation.scala:37-44) with an explicit empty side.
@@ -82,6 +84,7 @@ __device__ __forceinline__ void col_merge(ColPartial& a, const ColPartial& b) {
     moments_merge(a.n, a.mean, a.m2, b.n, b.mean, b.m2);
     a.n += b.n;
     a.nnan += b.nnan;
+    a.pt += b.pt;
     a.isum = (int64_t)((uint64_t)a.isum + (uint64_t)b.isum);
     a.imin = b.imin < a.imin ? b.imin : a.imin;
     a.imax = b.imax > a.imax ? b.imax : a.imax;
@@ -140,6 +143,8 @@ __device__ __forceinline__ void col_shfl(ColPartial& o, const ColPartial& a, int
     o.dmax = shfl_down_f64(a.dmax, off);
     o.mean = shfl_down_f64(a.mean, off);
     o.m2 = shfl_down_f64(a.m2, off);
+    o.pt = shfl_down_i64(a.pt, off);
+    o.pad = 0;
 }
 
 __device__ __forceinline__ void slot_shfl(SlotPartial& o, const SlotPartial& a, int off, int ncols,
@@ -361,25 +366,25 @@ __device__ __forceinline__ uint64_t spark_hash(uint64_t v, int spark_type) {
 // Per-lane accumulators, specialised by storage class so only live state occupies VGPRs.
 // ------------------------------------------------------------------------------------------------
 struct FAcc {  // FLOAT / DOUBLE column
-    int64_t n, nnan;
+    int64_t n, nnan, pt;
     double sum, mn, mx, mean, m2;
 };
 struct IAcc {  // integral column (Long sum with wrap-around, integer min/max)
-    int64_t n, sum, mn, mx;
+    int64_t n, sum, mn, mx, pt;
     double mean, m2;
 };
 template <bool F> struct AccOf { using type = IAcc; };
 template <> struct AccOf<true> { using type = FAcc; };
 
 __device__ __forceinline__ void acc_init(FAcc& a) {
-    a.n = a.nnan = 0;
+    a.n = a.nnan = a.pt = 0;
     a.sum = 0.0;
     a.mn = INFINITY;
     a.mx = -INFINITY;
     a.mean = a.m2 = 0.0;
 }
 __device__ __forceinline__ void acc_init(IAcc& a) {
-    a.n = a.sum = 0;
+    a.n = a.sum = a.pt = 0;
     a.mn = INT64_MAX;
     a.mx = INT64_MIN;
     a.mean = a.m2 = 0.0;
@@ -389,6 +394,7 @@ __device__ __forceinline__ void acc_merge(FAcc& a, const FAcc& b) {
     moments_merge(a.n, a.mean, a.m2, b.n, b.mean, b.m2);
     a.n += b.n;
     a.nnan += b.nnan;
+    a.pt += b.pt;
     a.sum += b.sum;
     a.mn = fmin(a.mn, b.mn);
     a.mx = fmax(a.mx, b.mx);
@@ -396,6 +402,7 @@ __device__ __forceinline__ void acc_merge(FAcc& a, const FAcc& b) {
 __device__ __forceinline__ void acc_merge(IAcc& a, const IAcc& b) {
     moments_merge(a.n, a.mean, a.m2, b.n, b.mean, b.m2);
     a.n += b.n;
+    a.pt += b.pt;
     a.sum = (int64_t)((uint64_t)a.sum + (uint64_t)b.sum);
     a.mn = b.mn < a.mn ? b.mn : a.mn;
     a.mx = b.mx > a.mx ? b.mx : a.mx;
@@ -404,6 +411,7 @@ __device__ __forceinline__ void acc_merge(IAcc& a, const IAcc& b) {
 __device__ __forceinline__ void acc_shfl(FAcc& o, const FAcc& a, int off) {
     o.n = shfl_down_i64(a.n, off);
     o.nnan = shfl_down_i64(a.nnan, off);
+    o.pt = shfl_down_i64(a.pt, off);
     o.sum = shfl_down_f64(a.sum, off);
     o.mn = shfl_down_f64(a.mn, off);
     o.mx = shfl_down_f64(a.mx, off);
@@ -413,6 +421,7 @@ __device__ __forceinline__ void acc_shfl(FAcc& o, const FAcc& a, int off) {
 __device__ __forceinline__ void acc_shfl(IAcc& o, const IAcc& a, int off) {
     o.n = shfl_down_i64(a.n, off);
     o.sum = shfl_down_i64(a.sum, off);
+    o.pt = shfl_down_i64(a.pt, off);
     o.mn = shfl_down_i64(a.mn, off);
     o.mx = shfl_down_i64(a.mx, off);
     o.mean = shfl_down_f64(a.mean, off);
@@ -435,9 +444,11 @@ __device__ __forceinline__ void store_empty(ColPartial& p) {
     p.dmin = INFINITY;
     p.dmax = -INFINITY;
     p.mean = p.m2 = 0.0;
+    p.pt = p.pad = 0;
 }
 __device__ __forceinline__ void store_partial(ColPartial& p, const FAcc& a) {
     store_empty(p);
+    p.pt = a.pt;
     p.n = a.n;
     p.nnan = a.nnan;
     p.dsum = a.sum;
@@ -448,6 +459,7 @@ __device__ __forceinline__ void store_partial(ColPartial& p, const FAcc& a) {
 }
 __device__ __forceinline__ void store_partial(ColPartial& p, const IAcc& a) {
     store_empty(p);
+    p.pt = a.pt;
     p.n = a.n;
     p.isum = a.sum;
     p.imin = a.mn;
@@ -545,6 +557,50 @@ __device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint
     a.n += cnt;
 }
 
+// Rows of mask m where `value <op> constant` holds (Spark comparison semantics: integral vs long
+// constant compares as long; otherwise as double with NaN above every number and NaN = NaN).
+template <bool F>
+__device__ __forceinline__ int fused_pred_count(const ColDesc& c, const uint64_t (&v)[8], uint32_t m) {
+    uint32_t hit = 0;
+    if (!F && c.pred_kind == FP_LONG) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t x = (int64_t)v[k];
+            const int cmp = x < c.pred_i ? -1 : (x > c.pred_i ? 1 : 0);
+            bool r;
+            switch (c.pred_op) {
+                case DQ_P_EQ: r = cmp == 0; break;
+                case DQ_P_NE: r = cmp != 0; break;
+                case DQ_P_LT: r = cmp < 0; break;
+                case DQ_P_LE: r = cmp <= 0; break;
+                case DQ_P_GT: r = cmp > 0; break;
+                default: r = cmp >= 0; break;
+            }
+            hit |= r ? (1u << k) : 0u;
+        }
+    } else {
+        const double y = c.pred_kind == FP_LONG ? (double)c.pred_i : c.pred_d;
+        const bool yn = y != y;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double x = to_double(v[k], F);
+            const bool xn = x != x;
+            const int cmp = (xn || yn) ? ((xn && yn) ? 0 : (xn ? 1 : -1)) : (x < y ? -1 : (x > y ? 1 : 0));
+            bool r;
+            switch (c.pred_op) {
+                case DQ_P_EQ: r = cmp == 0; break;
+                case DQ_P_NE: r = cmp != 0; break;
+                case DQ_P_LT: r = cmp < 0; break;
+                case DQ_P_LE: r = cmp <= 0; break;
+                case DQ_P_GT: r = cmp > 0; break;
+                default: r = cmp >= 0; break;
+            }
+            hit |= r ? (1u << k) : 0u;
+        }
+    }
+    return __popc(hit & m);
+}
+
 template <bool FX, bool FY>
 __device__ __forceinline__ void accumulate_corr(CorrPartial& c, const uint64_t (&x)[8], const uint64_t (&y)[8],
                                                 uint32_t m) {
@@ -600,7 +656,7 @@ struct BlockRed {
     int64_t wt[kBlock / 64], wnn[kBlock / 64];
 };
 
-template <int P, int NC, bool F0, bool F1>
+template <int P, int NC, bool F0, bool F1, bool HEAVY>
 __global__ void __launch_bounds__(kBlock)
 scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__ group, int ngroup,
                    int64_t nrows, int64_t ntiles, int gstride, SlotPartial* __restrict__ partials,
@@ -618,8 +674,9 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
         const ColDesc c0 = sd.col[0];
         const ColDesc c1 = sd.col[1];
         const bool has_where = sd.where_t != nullptr;
-        const bool hll0 = (c0.flags & CF_HLL) != 0;
-        const bool hll1 = NC > 1 && (c1.flags & CF_HLL) != 0;
+        // HLL and fused predicates only exist in the HEAVY instantiations (register budget).
+        const bool hll0 = HEAVY && (c0.flags & CF_HLL) != 0;
+        const bool hll1 = HEAVY && NC > 1 && (c1.flags & CF_HLL) != 0;
         A0 a0;
         A1 a1;
         acc_init(a0);
@@ -643,9 +700,11 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                 my &= w;
             }
             accumulate(a0, xv, mx, c0.flags);
+            if (HEAVY && c0.pred_kind) a0.pt += fused_pred_count<F0>(c0, xv, mx);
             if (hll0) hll_update(hll_lds[0], xv, mx, c0.spark_type);
             if (NC > 1) {
                 accumulate(a1, yv, my, c1.flags);
+                if (HEAVY && c1.pred_kind) a1.pt += fused_pred_count<F1>(c1, yv, my);
                 if (hll1) hll_update(hll_lds[NC - 1], yv, my, c1.spark_type);
                 accumulate_corr<F0, F1>(cp, xv, yv, mx & my);
             }
@@ -861,9 +920,10 @@ __global__ void finalize_kernel(const OpMap* __restrict__ ops, int nops, const S
         }
         case DQ_OP_COMPLIANCE:
             // sum(cast(when(where, pred) AS int)): NULL when no row has where TRUE and pred non-null.
-            st->u.num_matches_and_count.num_matches = sp.pt;
+            // Fused `col <op> const` (from_bits == 3): pred is non-null exactly where col is.
+            st->u.num_matches_and_count.num_matches = om.from_bits == 3 ? c.pt : sp.pt;
             st->u.num_matches_and_count.count = cond_count;
-            present = (sp.pnn > 0) && cond_count_present;
+            present = (om.from_bits == 3 ? c.n > 0 : sp.pnn > 0) && cond_count_present;
             break;
         case DQ_OP_MEAN:
             st->u.mean.sum = om.is_float ? c.dsum : (double)c.isum / scale;
@@ -923,13 +983,14 @@ __global__ void finalize_kernel(const OpMap* __restrict__ ops, int nops, const S
 // Launchers
 // ------------------------------------------------------------------------------------------------
 template <int P, int NC, bool F0, bool F1>
-static const void* values_kernel_ptr() {
-    return reinterpret_cast<const void*>(&scan_values_kernel<P, NC, F0, F1>);
+static const void* values_kernel_ptr(bool heavy) {
+    return heavy ? reinterpret_cast<const void*>(&scan_values_kernel<P, NC, F0, F1, true>)
+                 : reinterpret_cast<const void*>(&scan_values_kernel<P, NC, F0, F1, false>);
 }
 
-static const void* values_kernel_for(int P, int nc, bool f0, bool f1) {
+static const void* values_kernel_for(int P, int nc, bool f0, bool f1, bool heavy) {
 #define DQ_VK(p, n, a, b) \
-    if (P == p && nc == n && f0 == a && f1 == b) return values_kernel_ptr<p, n, a, b>();
+    if (P == p && nc == n && f0 == a && f1 == b) return values_kernel_ptr<p, n, a, b>(heavy);
     DQ_VK(2, 1, false, false) DQ_VK(2, 1, true, false) DQ_VK(4, 1, false, false) DQ_VK(4, 1, true, false)
     DQ_VK(8, 1, false, false) DQ_VK(8, 1, true, false)
     DQ_VK(2, 2, false, false) DQ_VK(2, 2, false, true) DQ_VK(2, 2, true, false) DQ_VK(2, 2, true, true)
@@ -939,15 +1000,15 @@ static const void* values_kernel_for(int P, int nc, bool f0, bool f1) {
     return nullptr;
 }
 
-int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1) {
-    const void* k = kind == SK_BITS ? reinterpret_cast<const void*>(&scan_bits_kernel) : values_kernel_for(P, nc, f0, f1);
+int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1, bool heavy) {
+    const void* k = kind == SK_BITS ? reinterpret_cast<const void*>(&scan_bits_kernel) : values_kernel_for(P, nc, f0, f1, heavy);
     if (!k) return 0;
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, 0) != hipSuccess || n <= 0) n = 1;
     return n;
 }
 
-int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, const SlotDesc* slots, const int32_t* group,
+int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, bool heavy, const SlotDesc* slots, const int32_t* group,
                       int ngroup, int64_t nrows, int64_t ntiles, int gstride, int grid, SlotPartial* partials,
                       uint8_t* hll_partials, hipStream_t s) {
     if (kind == SK_BITS) {
@@ -955,7 +1016,7 @@ int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, const SlotDesc*
                            gstride, partials);
         return 0;
     }
-    const void* k = values_kernel_for(P, nc, f0, f1);
+    const void* k = values_kernel_for(P, nc, f0, f1, heavy);
     if (!k) return -1;
     void* args[] = {(void*)&slots, (void*)&group, (void*)&ngroup, (void*)&nrows, (void*)&ntiles,
                     (void*)&gstride, (void*)&partials, (void*)&hll_partials};

@@ -120,9 +120,10 @@ class GpuLocal:
         import torch
         nops = len(batch.ops)
         out = torch.empty(max(nops, 1) * N.STATE_SIZE, dtype=torch.uint8, device="cuda")
+        torch.cuda.current_stream().synchronize()  # `out` allocated on torch's stream
         ctx = engine.ctx()
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
         batch.run(out_device_ptr=out.data_ptr())
+        ctx.synchronize()  # the scan runs on the context's stream; order it before torch reads `out`
         return out[:nops * N.STATE_SIZE]
 
     def partition(self, column, world):

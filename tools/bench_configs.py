@@ -42,7 +42,8 @@ def main():
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     ctx = engine.ctx()
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     R = int(args.rows)
 
