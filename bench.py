@@ -79,6 +79,22 @@ def cpu_baseline(seconds, sample_rows):
                       % (sample_rows, rows // sample_rows, el)}
 
 
+def measured_traffic(rows_per_gpu):
+    """HBM bytes per dq_scan call of this workload from the committed rocprofv3 PMC passes
+    (tools/gpu_pmc.sh -> tools/pmc_traffic.py -> profiles/<round>/c2_traffic_*.json), in GB, or None
+    when no PMC measurement of this exact shard size is committed."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "c2_traffic_*.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if int(d.get("rows", -1)) == rows_per_gpu:
+            best = (d["traffic_bytes_per_call"] / 1e9, os.path.relpath(path, ROOT))
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,6 +204,7 @@ def main():
     achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
     ms_per_step = elapsed / args.steps * 1e3
     value = total / (elapsed / args.steps)
+    traffic = measured_traffic(nrows)
     result = {
         "metric": "rows/sec + HBM GB/s (% peak) for fused analyzer suite, 1B rows, 1/2/4/8 GPUs",
         "value": value,
@@ -206,7 +223,9 @@ def main():
                    "rows": total, "rows_per_gpu": nrows, "columns": len(names), "ops": nops,
                    "parallelism": "rows sharded dp%d + RCCL all-gather of states" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBPS, "traffic": None,
+                     "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic[0] if traffic else None,
+                     "traffic_unit": "GB per dq_scan call (HBM FETCH+WRITE from rocprofv3 PMC, %s)"
+                                     % (traffic[1] if traffic else "not measured for this shard size"),
                      "kernel": "dq_scan fused pass (scan_values_kernel launches + partial folds), HIP events "
                                "on the scan stream, avg %.3f ms over %d steps; algorithmic bytes %.1f B/row x %d rows"
                                % (scan_ms, args.steps, bytes_per_row, nrows)},

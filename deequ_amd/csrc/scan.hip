@@ -630,16 +630,44 @@ __device__ __forceinline__ void accumulate_corr(CorrPartial& c, const uint64_t (
     corr_merge(c, b);
 }
 
-__device__ __forceinline__ void hll_update(uint32_t* regs, const uint64_t (&v)[8], uint32_t m, int spark_type) {
-#pragma unroll 1
+// Hash class of a Spark type for XxHash64Function: 0 = hashInt of the int value, 1 = hashInt of the
+// float bits, 2 = hashLong of the double bits, 3 = hashLong of the long value.
+__device__ __forceinline__ int hash_class(int spark_type) {
+    switch (spark_type) {
+        case DQ_TYPE_BOOLEAN: case DQ_TYPE_BYTE: case DQ_TYPE_SHORT: case DQ_TYPE_INT: case DQ_TYPE_DATE: return 0;
+        case DQ_TYPE_FLOAT: return 1;
+        case DQ_TYPE_DOUBLE: return 2;
+        default: return 3;
+    }
+}
+
+// All 8 lane values are hashed unconditionally (independent multiply chains the scheduler can
+// interleave; no divergence), then the valid ones are max-merged into the LDS registers with
+// no-return ds_max atomics (fire-and-forget: no LDS latency on the critical path).
+template <int HC>
+__device__ __forceinline__ void hll_update8(uint32_t* regs, const uint64_t (&v)[8], uint32_t m) {
+    uint32_t packed[8];
+#pragma unroll
     for (int k = 0; k < 8; ++k) {
-        if ((m >> k) & 1u) {
-            const uint64_t x = spark_hash(v[k], spark_type);
-            const uint32_t idx = hll_index(x);
-            const uint32_t pw = hll_rank(x);
-            // Registers only grow: skip the LDS atomic when it cannot raise the register.
-            if (pw > regs[idx]) atomicMax(&regs[idx], pw);
-        }
+        uint64_t x;
+        if (HC == 0) x = xxh_int((uint32_t)(int32_t)(int64_t)v[k], SPARK_HLL_SEED);
+        else if (HC == 1) x = xxh_int(float_to_int_bits((float)as_f64(v[k])), SPARK_HLL_SEED);
+        else if (HC == 2) x = xxh_long(double_to_long_bits(as_f64(v[k])), SPARK_HLL_SEED);
+        else x = xxh_long(v[k], SPARK_HLL_SEED);
+        packed[k] = hll_index(x) | (hll_rank(x) << 16);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if ((m >> k) & 1u) atomicMax(&regs[packed[k] & 0xffffu], packed[k] >> 16);
+}
+
+__device__ __forceinline__ void hll_update(uint32_t* regs, const uint64_t (&v)[8], uint32_t m, int spark_type) {
+    if (m == 0u) return;
+    switch (hash_class(spark_type)) {  // wave-uniform
+        case 0: hll_update8<0>(regs, v, m); break;
+        case 1: hll_update8<1>(regs, v, m); break;
+        case 2: hll_update8<2>(regs, v, m); break;
+        default: hll_update8<3>(regs, v, m); break;
     }
 }
 
@@ -699,13 +727,20 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                 mx &= w;
                 my &= w;
             }
+            // Phases are fenced from each other (sched_barrier) so the scheduler cannot interleave
+            // them: only one phase's temporaries are live at a time, which keeps the 2-column
+            // HEAVY kernels out of AGPR/SGPR spilling.
             accumulate(a0, xv, mx, c0.flags);
+            if (HEAVY) __builtin_amdgcn_sched_barrier(0);
             if (HEAVY && c0.pred_kind) a0.pt += fused_pred_count<F0>(c0, xv, mx);
             if (hll0) hll_update(hll_lds[0], xv, mx, c0.spark_type);
             if (NC > 1) {
+                if (HEAVY) __builtin_amdgcn_sched_barrier(0);
                 accumulate(a1, yv, my, c1.flags);
+                if (HEAVY) __builtin_amdgcn_sched_barrier(0);
                 if (HEAVY && c1.pred_kind) a1.pt += fused_pred_count<F1>(c1, yv, my);
                 if (hll1) hll_update(hll_lds[NC - 1], yv, my, c1.spark_type);
+                if (HEAVY) __builtin_amdgcn_sched_barrier(0);
                 accumulate_corr<F0, F1>(cp, xv, yv, mx & my);
             }
         };
@@ -713,12 +748,21 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
         const int64_t nfull = nrows / kTileRows;
         int64_t t = blockIdx.x;
         uint64_t x[8], y[8], xn[8], yn[8];
-        if (t < nfull) {
+        constexpr bool kDoubleBuffer = !(HEAVY && NC > 1);
+        if (kDoubleBuffer && t < nfull) {
             load_values<P, F0>(c0, t * kTileRows, tid, true, nrows, x);
             if (NC > 1) load_values<P, F1>(c1, t * kTileRows, tid, true, nrows, y);
         }
         for (; t < nfull; t += G) {
             const int64_t tn = t + G;
+            if (!kDoubleBuffer) {
+                // Two-column HEAVY kernels: no register double buffer (it costs 32 VGPRs and pushes
+                // them to 1 wave/SIMD); a second resident wave hides the load latency instead.
+                load_values<P, F0>(c0, t * kTileRows, tid, true, nrows, x);
+                if (NC > 1) load_values<P, F1>(c1, t * kTileRows, tid, true, nrows, y);
+                fold(t * kTileRows, true, x, y);
+                continue;
+            }
             if (tn < nfull) {
                 load_values<P, F0>(c0, tn * kTileRows, tid, true, nrows, xn);
                 if (NC > 1) load_values<P, F1>(c1, tn * kTileRows, tid, true, nrows, yn);

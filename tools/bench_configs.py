@@ -26,7 +26,7 @@ PEAK = 8000.0
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", required=True, choices=["c3", "c4", "suite10"])
+    ap.add_argument("--config", required=True, choices=["c3", "c4", "suite10", "s10_nocorr", "corr4", "hll8", "c2"])
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--distinct", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=5)
@@ -64,6 +64,20 @@ def main():
                    col("y", 6, 0xC3000003, N.TYPE_DOUBLE)])
         analyzers = [D.ApproxCountDistinct("k"), D.Correlation("x", "y"), D.Completeness("k")]
         bytes_per_row = 3 * (8 + 1 / 8)
+    elif args.config in ("s10_nocorr", "corr4", "hll8", "c2"):
+        # cost breakdown of suite10 (diagnostics)
+        t = bench.build_shard(torch, N, ctx, 0, R, dev)
+        names = list(t.columns)
+        analyzers = []
+        if args.config in ("s10_nocorr", "c2"):
+            analyzers += bench.c2_analyzers(D, names)
+        if args.config == "s10_nocorr":
+            analyzers += [D.Compliance("pos_%s" % c, "%s > 0" % c) for c in names]
+        if args.config in ("s10_nocorr", "hll8"):
+            analyzers += [D.ApproxCountDistinct(c) for c in names]
+        if args.config == "corr4":
+            analyzers += [D.Correlation(names[2 * i], names[2 * i + 1]) for i in range(4)]
+        bytes_per_row = 8 * (8 + 1 / 8)
     elif args.config == "suite10":
         t = bench.build_shard(torch, N, ctx, 0, R, dev)
         names = list(t.columns)
