@@ -152,6 +152,7 @@ double java_math_max(double a, double b) {
 namespace dq {
 hipStream_t ctx_stream(dq_ctx* ctx) { return ctx->stream; }
 int ctx_device(dq_ctx* ctx) { return ctx->device; }
+int ctx_cus(dq_ctx* ctx) { return ctx->cus; }
 int ctx_fail(dq_ctx* ctx, int code, const char* msg) { return fail(ctx, code, "%s", msg); }
 }  // namespace dq
 

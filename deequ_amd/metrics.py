@@ -141,6 +141,29 @@ class DoubleMetric(Metric):
         return "DoubleMetric(%s,%s,%s,%r)" % (self.entity, self.name, self.instance, self.value)
 
 
+class KeyedDoubleMetric(Metric):
+    """M/metrics/Metric.scala:51-68 (ApproxQuantiles): a map of quantile string -> value."""
+
+    def __init__(self, entity, name, instance, value):
+        self.entity, self.name, self.instance, self.value = entity, name, instance, value
+
+    def flatten(self):
+        if self.value.isSuccess:
+            return [DoubleMetric(self.entity, "%s-%s" % (self.name, k), self.instance, Success(v))
+                    for k, v in self.value.get().items()]
+        return [DoubleMetric(self.entity, self.name, self.instance, Failure(self.value.failed))]
+
+    def __eq__(self, other):
+        return isinstance(other, KeyedDoubleMetric) and (self.entity, self.name, self.instance) == \
+            (other.entity, other.name, other.instance) and self.value == other.value
+
+    def __hash__(self):
+        return hash((self.entity, self.name, self.instance))
+
+    def __repr__(self):
+        return "KeyedDoubleMetric(%s,%s,%s,%r)" % (self.entity, self.name, self.instance, self.value)
+
+
 class DistributionValue:
     def __init__(self, absolute, ratio):
         self.absolute, self.ratio = absolute, ratio

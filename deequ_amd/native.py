@@ -45,7 +45,8 @@ HLL_NUM_WORDS = 52
 EXPORTED_SYMBOLS = (
     "dq_abi_version", "dq_open", "dq_close", "dq_last_error", "dq_set_stream", "dq_synchronize", "dq_scan",
     "dq_scan_launch_count", "dq_state_merge", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
-    "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys", "dq_synth_column", "dq_synth_freq_keys",
+    "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
+    "dq_quantile_summary", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity",
 )
 
@@ -166,6 +167,8 @@ def load_library(path=None):
             "dq_freq_export": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
             "dq_freq_free": (None, [c_void_p, c_void_p]),
             "dq_partition_keys": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
+            "dq_quantile_summary": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_double, c_int64, c_void_p,
+                                              c_void_p, c_void_p]),
             "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
             "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
             "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),
@@ -265,6 +268,20 @@ class Context:
         rc = self.lib.dq_scan(self.handle, col_arr, ncol, int(nrows), op_arr, len(ops), pred_arr, len(preds), out, 0)
         self.check(rc, "dq_scan")
         return [out[i] for i in range(len(ops))]
+
+    def quantile_summary(self, column, nrows, relative_error):
+        """dq_quantile_summary: exact (value, rank) samples of a zero-uncertainty GK summary of the
+        column's non-NULL values, and their count n."""
+        cap = int(nrows) if relative_error <= 0.0 else min(int(nrows), int(2.0 / relative_error) + 8)
+        cap = max(cap, 2)
+        vals = np.empty(cap, dtype=np.float64)
+        ranks = np.empty(cap, dtype=np.int64)
+        count = ctypes.c_int64(0)
+        ns = self.lib.dq_quantile_summary(self.handle, ctypes.byref(column), int(nrows), float(relative_error), cap,
+                                          vals.ctypes.data, ranks.ctypes.data, ctypes.byref(count))
+        if ns < 0:
+            self.check(int(ns), "dq_quantile_summary")
+        return vals[:ns].copy(), ranks[:ns].copy(), int(count.value)
 
     def synth_column(self, kind, seed, row0, nrows, dev_ptr):
         self.check(self.lib.dq_synth_column(self.handle, kind, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows,

@@ -12,8 +12,15 @@ from .expr import compile_predicate
 from .metrics import DoubleMetric, Success
 
 
+class ScanResult(list):
+    """dq_state per op, plus the PercentileDigest of each quantile request."""
+    quantiles = ()
+
+
 class ScanBatch:
-    """The dq_op list of one fused scan: deduplicated ops, predicates compiled once per string."""
+    """The dq_op list of one fused scan: deduplicated ops, predicates compiled once per string.
+    ApproxQuantile(s) register quantile requests, one dq_quantile_summary per (column, relativeError)
+    after the fused pass (they share one digest, as Spark computes identical digests)."""
 
     def __init__(self, data):
         self.data = data
@@ -23,6 +30,8 @@ class ScanBatch:
         self.pred_index = {}
         self.ops = []
         self.op_index = {}
+        self.quantile_reqs = []
+        self.quantile_index = {}
 
     def predicate(self, text):
         if text not in self.pred_index:
@@ -50,14 +59,40 @@ class ScanBatch:
             self.op_index[key] = len(self.ops) - 1
         return self.op_index[key]
 
+    def add_quantile(self, column, relativeError):
+        if column not in self.col_index:
+            from .metrics import NoSuchColumnException
+            raise NoSuchColumnException("Input data does not include column %s!" % column)
+        key = (column, float(relativeError))
+        if key not in self.quantile_index:
+            self.quantile_reqs.append(key)
+            self.quantile_index[key] = len(self.quantile_reqs) - 1
+        return self.quantile_index[key]
+
     def native_columns(self):
         return [self.data[n].native() for n in self.names]
 
     def run(self, out_device_ptr=None):
-        if not self.ops:
-            return []
-        return engine.ctx().scan(self.native_columns(), self.data.nrows, self.ops,
-                                 [p.to_native() for p in self.preds], out_device_ptr=out_device_ptr)
+        res = ScanResult()
+        if self.ops:
+            got = engine.ctx().scan(self.native_columns(), self.data.nrows, self.ops,
+                                    [p.to_native() for p in self.preds], out_device_ptr=out_device_ptr)
+            if got is not None:
+                res.extend(got)
+        if self.quantile_reqs:
+            from .quantiles import PercentileDigest, DEFAULT_HEAD_SIZE
+            res.quantiles = []
+            small = self.data.nrows < DEFAULT_HEAD_SIZE
+            for column, rel in self.quantile_reqs:
+                # below the head-buffer size Spark's digest is a function of the sorted values: get all
+                # of them (rank spacing 1) and rebuild Spark's own summary; above it, a bounded summary
+                vals, ranks, n = engine.ctx().quantile_summary(self.data[column].native(), self.data.nrows,
+                                                               0.0 if small else rel)
+                if small:
+                    res.quantiles.append(PercentileDigest.spark_single_partition(rel, vals))
+                else:
+                    res.quantiles.append(PercentileDigest.from_order_statistics(rel, vals, ranks, n))
+        return res
 
 
 class AnalyzerContext:

@@ -254,6 +254,20 @@ class ApproxCountDistinctState(DoubleValuedState):
         return "ApproxCountDistinctState(%s)" % ",".join(str(np.int64(np.uint64(w))) for w in self.words)
 
 
+class ApproxQuantileState(State):
+    """A/ApproxQuantile.scala:28-36: wraps a PercentileDigest; sum = PercentileDigest.merge."""
+
+    def __init__(self, percentileDigest):
+        self.percentileDigest = percentileDigest
+
+    def sum(self, other):
+        return ApproxQuantileState(self.percentileDigest.merge(other.percentileDigest))
+
+    def __repr__(self):
+        s = self.percentileDigest.quantileSummaries
+        return "ApproxQuantileState(count=%d, samples=%d)" % (s.count, len(s.sampled))
+
+
 def state_to_native(kind, state):
     """Reference State (or None) -> dq_state record of op `kind` (persisted / exchanged states)."""
     st = N.DqState()

@@ -240,6 +240,18 @@ int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* table, int64_t k, int64_t*
 int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* table, int64_t capacity, int64_t* keys, int64_t* counts);
 void dq_freq_free(dq_ctx* ctx, dq_freq_table* table);
 
+/* ApproxQuantile / ApproxQuantiles (A/ApproxQuantile.scala:28-103, A/ApproxQuantiles.scala:39-101): replaces the
+ * per-row PercentileDigest.add of StatefulApproxQuantile.update (C/StatefulApproxQuantile.scala:65-72). Computes
+ * EXACT order statistics of the column's non-NULL values cast to double, in java.lang.Double.compare order
+ * (-0.0 < 0.0, NaN largest), at 1-based ranks 1, n and every max(1, floor(relative_error * n))-th rank in between:
+ * the samples (value, g = rank gap, delta = 0) of a Greenwald-Khanna summary with no rank uncertainty, from which
+ * the host builds Spark's QuantileSummaries / PercentileDigest (relative_error = 0 returns all n sorted values).
+ * Numeric columns only (Preconditions.isNumeric). values_out / ranks_out hold max_samples entries (2/relative_error
+ * + 2 always suffices when relative_error * n >= 1; n otherwise). *count receives n. Returns the number of samples
+ * written (0 for an empty or all-NULL column), or a negative dq_status. */
+int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows, double relative_error,
+                            int64_t max_samples, double* values_out, int64_t* ranks_out, int64_t* count_out);
+
 /* Multi-GPU grouping: the canonical 64-bit keys (see DQ_FREQ_KEYS_VALUES) of one
  * fixed-width column's non-NULL rows, bucketed by owner rank = (mix64(key) >> 32) % nparts, written
  * contiguously per rank into keys_dev (capacity nrows, device memory) for an RCCL all-to-all; the

@@ -395,3 +395,54 @@ def grouping_summary(freq, num_rows):
     ent = math.fsum(-(c / num_rows) * math.log(c / num_rows) for c in counts) if counts else 0.0
     return {"num_groups": len(counts), "num_unique": sum(1 for c in counts if c == 1), "entropy": ent,
             "num_rows": num_rows}
+
+
+# ---- ApproxQuantile(s): exact order statistics (A/ApproxQuantile.scala:28-103) ----------------------
+def java_sorted_doubles(table, column):
+    """The column's non-NULL values cast to double (Spark's implicit DoubleType cast of the child,
+    C/StatefulApproxQuantile.scala:50-52; Decimal.toDouble = unscaled / 10^scale for compact
+    decimals), sorted in java.lang.Double.compare order (-0.0 < 0.0, NaN largest), which is the order
+    of QuantileSummaries' `sortBy(_.value)`."""
+    col = table[column]
+    valid = _valid(col)
+    v = np.asarray(col.values)[: col.length][valid]
+    if col.spark_type == T_DECIMAL:
+        d = v.astype(np.float64) / (10.0 ** col.decimal_scale) if col.decimal_scale else v.astype(np.float64)
+    else:
+        d = v.astype(np.float64)
+    bits = d.view(np.uint64).copy()
+    bits[np.isnan(d)] = np.uint64(0x7FF8000000000000)
+    neg = (bits >> np.uint64(63)) == 1
+    keys = np.where(neg, ~bits, bits | np.uint64(1 << 63))
+    keys.sort()
+    neg = (keys >> np.uint64(63)) == 0
+    out = np.where(neg, ~keys, keys & np.uint64(0x7FFFFFFFFFFFFFFF))
+    return out.view(np.float64)
+
+
+def summary_ranks(n, relative_error):
+    """Ranks of the zero-uncertainty summary dq_quantile_summary returns: 1, n and every
+    max(1, floor(relativeError * n))-th rank in between."""
+    if n == 0:
+        return np.zeros(0, dtype=np.int64)
+    s = max(1, int(math.floor(relative_error * n)))
+    r = list(range(1, n + 1, s))
+    if r[-1] != n:
+        r.append(n)
+    return np.array(r, dtype=np.int64)
+
+
+def rank_interval(sorted_values, value):
+    """1-based [lowest, highest] rank `value` occupies in the sorted (Java-ordered) values."""
+    keys = _java_keys(sorted_values)
+    k = _java_keys(np.array([value], dtype=np.float64))[0]
+    lo = int(np.searchsorted(keys, k, side="left")) + 1
+    hi = int(np.searchsorted(keys, k, side="right"))
+    return lo, hi
+
+
+def _java_keys(d):
+    bits = np.asarray(d, dtype=np.float64).view(np.uint64).copy()
+    bits[np.isnan(np.asarray(d, dtype=np.float64))] = np.uint64(0x7FF8000000000000)
+    neg = (bits >> np.uint64(63)) == 1
+    return np.where(neg, ~bits, bits | np.uint64(1 << 63))
