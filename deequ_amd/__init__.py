@@ -9,9 +9,10 @@ from .metrics import (Entity, DoubleMetric, HistogramMetric, KeyedDoubleMetric, 
                       NumberOfSpecifiedColumnsException, IllegalAnalyzerParameterException)
 from .states import (NumMatches, NumMatchesAndCount, MeanState, SumState, MinState, MaxState,
                      StandardDeviationState, CorrelationState, ApproxCountDistinctState,
-                     ApproxQuantileState)
+                     ApproxQuantileState, DataTypeHistogram)
 from .analyzers import (Size, Completeness, Compliance, Mean, Sum, Minimum, Maximum, StandardDeviation, Correlation,
-                        ApproxCountDistinct, ApproxQuantile, ApproxQuantiles, Uniqueness, Distinctness, UniqueValueRatio, Entropy, CountDistinct,
+                        ApproxCountDistinct, ApproxQuantile, ApproxQuantiles, MinLength, MaxLength, DataType,
+                        Uniqueness, Distinctness, UniqueValueRatio, Entropy, CountDistinct,
                         MutualInformation, Histogram, FrequenciesAndNumRows, Preconditions, computeFrequencies)
 from .runners import (AnalysisRunner, AnalysisRunBuilder, AnalyzerContext, Analysis, InMemoryStateProvider,
                       ScanBatch)

@@ -17,7 +17,7 @@ from .metrics import (DoubleMetric, Entity, Failure, Success, EmptyStateExceptio
                       IllegalAnalyzerParameterException, HistogramMetric, Distribution, DistributionValue,
                       MetricCalculationRuntimeException, KeyedDoubleMetric, wrap_if_necessary)
 from .states import (NumMatches, NumMatchesAndCount, MeanState, SumState, MinState, MaxState, ApproxQuantileState,
-                     state_from_native)
+                     DataTypeHistogram, state_from_native)
 from . import engine
 
 COL_PREFIX = "com_amazon_deequ_dq_metrics_"
@@ -355,6 +355,57 @@ class ApproxCountDistinct(StandardScanShareableAnalyzer):
 
     def addOps(self, batch):
         return [batch.add_op(N.OP_APPROX_COUNT_DISTINCT, (self.column,), where=self.where)]
+
+
+class _StringLengthAnalyzer(StandardScanShareableAnalyzer):
+    _fields = ("column", "where")
+    op_kind = None
+
+    def __init__(self, column, where=None):
+        self.column, self.where = column, where
+
+    instance = property(lambda self: self.column)
+
+    def additionalPreconditions(self):
+        return [Preconditions.hasColumn(self.column), Preconditions.isString(self.column)]
+
+    def addOps(self, batch):
+        return [batch.add_op(self.op_kind, (self.column,), where=self.where)]
+
+
+class MinLength(_StringLengthAnalyzer):
+    """A/MinLength.scala:25-41: min(length(when(where, col))) as Double."""
+    name, op_kind = "MinLength", N.OP_MIN_LENGTH
+
+
+class MaxLength(_StringLengthAnalyzer):
+    """A/MaxLength.scala:25-41: max(length(when(where, col))) as Double."""
+    name, op_kind = "MaxLength", N.OP_MAX_LENGTH
+
+
+class DataType(ScanShareableAnalyzer):
+    """A/DataType.scala:138-183: StatefulDataType histogram of the value cast to string."""
+    _fields = ("column", "where")
+
+    def __init__(self, column, where=None):
+        self.column, self.where = column, where
+
+    def preconditions(self):
+        return [Preconditions.hasColumn(self.column)]
+
+    def addOps(self, batch):
+        return [batch.add_op(N.OP_DATATYPE, (self.column,), where=self.where)]
+
+    def fromAggregationResult(self, states, ops):
+        return state_from_native(states[ops[0]])
+
+    def computeMetricFrom(self, state):
+        if state is None:
+            return self.toFailureMetric(emptyStateException(self))
+        return HistogramMetric(self.column, Success(state.toDistribution()))
+
+    def toFailureMetric(self, exception):
+        return HistogramMetric(self.column, Failure(wrap_if_necessary(exception)))
 
 
 def _quantile_param_checks(quantiles, relativeError):

@@ -242,7 +242,8 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             return fail(ctx, DQ_ERR_UNSUPPORTED, "column %d: decimal precision > 18 unsupported", c);
         if ((col.flags & DQ_COL_DEVICE) && nrows > 0) {
             const int e = elem_of(col.spark_type);
-            const size_t va = e == ET_NONE ? 1 : (elem_size(e) == 1 ? 8 : 16);
+            // strings: 4-byte aligned UTF-8 (read as dwords), padded by 16 bytes past offsets[length]
+            const size_t va = e == ET_NONE ? 4 : (elem_size(e) == 1 ? 8 : 16);
             if (((uintptr_t)col.values % va) != 0 || ((uintptr_t)col.validity % 8) != 0)
                 return fail(ctx, DQ_ERR_ALIGNMENT, "device column %d: values must be %zu-byte and validity 8-byte aligned", c, va);
         }
@@ -279,9 +280,14 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 col_used[op.column[0]] = col_used[op.column[1]] = 1;
                 break;
             case DQ_OP_APPROX_COUNT_DISTINCT:
+            case DQ_OP_DATATYPE:
                 if (!col_ok(op.column[0])) return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "op %d: bad column", i);
-                if (!is_fixed_width(columns[op.column[0]].spark_type))
-                    return fail(ctx, DQ_ERR_UNSUPPORTED, "op %d: ApproxCountDistinct on this type is not implemented", i);
+                col_used[op.column[0]] = 1;
+                break;
+            case DQ_OP_MIN_LENGTH: case DQ_OP_MAX_LENGTH:
+                if (!col_ok(op.column[0])) return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "op %d: bad column", i);
+                if (columns[op.column[0]].spark_type != DQ_TYPE_STRING)
+                    return fail(ctx, DQ_ERR_UNSUPPORTED, "op %d: MinLength/MaxLength need a string column", i);
                 col_used[op.column[0]] = 1;
                 break;
             default:
@@ -336,7 +342,9 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         switch (op.kind) {
             case DQ_OP_MEAN: case DQ_OP_SUM: case DQ_OP_MINIMUM: case DQ_OP_MAXIMUM: uses[key].flags |= CF_STATS; break;
             case DQ_OP_STANDARD_DEVIATION: uses[key].flags |= CF_MOMENTS; break;
-            case DQ_OP_APPROX_COUNT_DISTINCT: uses[key].flags |= CF_HLL; break;
+            case DQ_OP_APPROX_COUNT_DISTINCT:
+                if (columns[op.column[0]].spark_type != DQ_TYPE_STRING) uses[key].flags |= CF_HLL;
+                break;
             case DQ_OP_COMPLIANCE: {
                 // `col <op> const` on a non-decimal numeric column: evaluate inside that column's scan.
                 const dq_predicate& pr = preds[op.predicate];
@@ -437,6 +445,47 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             sd.col[kv.second.pos].hll_slot = kv.second.hll;
         }
     }
+    // String-shaped ops -> string slots (column, where): MinLength/MaxLength, DataType, string HLL.
+    std::vector<StrSlot> sslots;
+    std::map<std::pair<int, int>, int> sslot_of;
+    std::vector<int> op_sslot(nops, -1);
+    for (int i = 0; i < nops; ++i) {
+        const dq_op& op = ops[i];
+        const bool str_hll = op.kind == DQ_OP_APPROX_COUNT_DISTINCT && columns[op.column[0]].spark_type == DQ_TYPE_STRING;
+        if (!(op.kind == DQ_OP_MIN_LENGTH || op.kind == DQ_OP_MAX_LENGTH || op.kind == DQ_OP_DATATYPE || str_hll)) continue;
+        const auto key = std::make_pair(op.column[0], op.where);
+        auto it = sslot_of.find(key);
+        if (it == sslot_of.end()) {
+            StrSlot ss;
+            memset(&ss, 0, sizeof(ss));
+            ss.spark_type = columns[op.column[0]].spark_type;
+            ss.decimal_scale = columns[op.column[0]].decimal_scale;
+            ss.hll_slot = -1;
+            ss.values = (const void*)(intptr_t)op.column[0];  // column index until pointers are known
+            ss.where_t = (const uint64_t*)(intptr_t)(op.where + 1);
+            sslots.push_back(ss);
+            it = sslot_of.emplace(key, (int)sslots.size() - 1).first;
+        }
+        StrSlot& ss = sslots[it->second];
+        if (op.kind == DQ_OP_DATATYPE) ss.flags |= SF_DTYPE;
+        else if (str_hll) {
+            ss.flags |= SF_HLL;
+            if (ss.hll_slot < 0) ss.hll_slot = nhll++;
+        } else ss.flags |= SF_LEN;
+        op_sslot[i] = it->second;
+    }
+    const int nsslots = (int)sslots.size();
+    std::vector<StrOpMap> sopmap;
+    for (int i = 0; i < nops; ++i) {
+        if (op_sslot[i] < 0 || ops[i].kind == DQ_OP_APPROX_COUNT_DISTINCT) continue;
+        StrOpMap m;
+        m.op = i;
+        m.kind = ops[i].kind;
+        m.slot = op_sslot[i];
+        m.pad = 0;
+        sopmap.push_back(m);
+    }
+
     // Ops -> OpMap; bits-only slots for Size(where), Completeness of unread columns, Compliance.
     std::vector<OpMap> opmap(nops);
     std::map<std::tuple<int, int, int>, int> bits_slots;  // (kind, col/pred, where) -> slot
@@ -498,7 +547,13 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 m.slot = op_slot[i].first;
                 m.colpos = op_slot[i].second;
                 break;
+            case DQ_OP_MIN_LENGTH: case DQ_OP_MAX_LENGTH: case DQ_OP_DATATYPE:
+                break;  // written by finalize_strings_kernel
             default: {
+                if (op_sslot[i] >= 0) {  // ApproxCountDistinct of a string column
+                    m.hll_slot = sslots[op_sslot[i]].hll_slot;
+                    break;
+                }
                 const Use& u = uses.at({c, op.where});
                 m.slot = u.slot;
                 m.colpos = u.pos;
@@ -551,12 +606,16 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     }
     int gstride = 1;
     for (const Group& g : groups) gstride = std::max(gstride, g.grid);
+    const int sgrid = nsslots ? string_scan_grid(ctx->cus, nrows) : 0;
+    gstride = std::max(gstride, sgrid);
     std::vector<int32_t> slot_nblocks(std::max<size_t>(slots.size(), 1), 1);
     for (const Group& g : groups)
         for (int32_t s : g.slots) slot_nblocks[s] = g.grid;
     std::vector<int32_t> hll_nblocks(std::max(nhll, 1), 1);
     for (const auto& kv : uses)
         if (kv.second.hll >= 0) hll_nblocks[kv.second.hll] = slot_nblocks[kv.second.slot];
+    for (const StrSlot& ss : sslots)
+        if (ss.hll_slot >= 0) hll_nblocks[ss.hll_slot] = sgrid;
     const int64_t pwords = padded_words_for(nrows);
     const size_t bitmap_bytes = (size_t)(nrows + 7) / 8;
 
@@ -618,12 +677,16 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         uint8_t* hllp = (uint8_t*)b.take((size_t)std::max(nhll, 1) * gstride * kHllRegs);
         uint8_t* hllf = (uint8_t*)b.take((size_t)std::max(nhll, 1) * kHllRegs);
         dq_state* dout = (flags & DQ_SCAN_OUT_DEVICE) ? out : (dq_state*)b.take(sizeof(dq_state) * nops);
+        StrSlot* dsslots = (StrSlot*)b.take(sizeof(StrSlot) * std::max(nsslots, 1));
+        StrPartial* spartials = (StrPartial*)b.take(sizeof(StrPartial) * (size_t)std::max(nsslots, 1) * gstride);
+        StrOpMap* dsops = (StrOpMap*)b.take(sizeof(StrOpMap) * std::max<size_t>(sopmap.size(), 1));
         if (!pass) {
             arena_need = b.off;
             int rc = ensure_arena(ctx, arena_need);
             if (rc) return rc;
             // plan bytes uploaded through pinned staging
-            size_t pin = sizeof(PredColumn) * std::max(ncols, 1) + sizeof(SlotDesc) * std::max(nslots, 1) +
+            size_t pin = sizeof(StrSlot) * std::max(nsslots, 1) + sizeof(StrOpMap) * std::max<size_t>(sopmap.size(), 1) +
+                         sizeof(PredColumn) * std::max(ncols, 1) + sizeof(SlotDesc) * std::max(nslots, 1) +
                          sizeof(OpMap) * nops + sizeof(dq_state) * nops + 4 * (slot_nblocks.size() + hll_nblocks.size() + nslots) + 8192;
             for (int p = 0; p < npreds; ++p)
                 if (pred_used[p])
@@ -717,8 +780,6 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             if (rc) return rc;
             rc = upload(dslot_nb, slot_nblocks.data(), sizeof(int32_t) * slot_nblocks.size());
             if (rc) return rc;
-            rc = upload(dhll_nb, hll_nblocks.data(), sizeof(int32_t) * hll_nblocks.size());
-            if (rc) return rc;
             size_t off = 0;
             for (const Group& g : groups) {
                 if (launch_scan_group(g.kind, g.P, g.nc, g.f0, g.f1, g.heavy, dslots, dgroups + off, (int)g.slots.size(), nrows,
@@ -727,14 +788,39 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 DQ_HIP(ctx, hipGetLastError());
                 off += g.slots.size();
             }
-            ctx->scan_launches++;
             launch_reduce_partials(partials, dslot_nb, nslots, gstride, finals, ctx->stream);
             DQ_HIP(ctx, hipGetLastError());
+        }
+        if (nsslots) {
+            for (StrSlot& ss : sslots) {
+                const int c = (int)(intptr_t)ss.values;
+                const int w = (int)(intptr_t)ss.where_t - 1;
+                ss.values = dval[c];
+                ss.data = (const uint8_t*)dval[c];
+                ss.offsets = (const int32_t*)doffs[c];
+                ss.validity = (const uint64_t*)dvalid[c];
+                ss.where_t = w >= 0 ? pt[w] : nullptr;
+            }
+            rc = upload(dsslots, sslots.data(), sizeof(StrSlot) * nsslots);
+            if (rc) return rc;
+            launch_string_scan(dsslots, nsslots, nrows, sgrid, gstride, spartials, hllp, ctx->stream);
+            DQ_HIP(ctx, hipGetLastError());
+        }
+        if (nslots || nsslots) ctx->scan_launches++;
+        if (nhll) {
+            rc = upload(dhll_nb, hll_nblocks.data(), sizeof(int32_t) * hll_nblocks.size());
+            if (rc) return rc;
             launch_reduce_hll(hllp, dhll_nb, nhll, gstride, hllf, ctx->stream);
             DQ_HIP(ctx, hipGetLastError());
         }
         launch_finalize(dops, nops, finals, hllf, dout, ctx->stream);
         DQ_HIP(ctx, hipGetLastError());
+        if (!sopmap.empty()) {
+            rc = upload(dsops, sopmap.data(), sizeof(StrOpMap) * sopmap.size());
+            if (rc) return rc;
+            launch_finalize_strings(dsops, (int)sopmap.size(), spartials, sgrid, gstride, nrows, dout, ctx->stream);
+            DQ_HIP(ctx, hipGetLastError());
+        }
         if (!(flags & DQ_SCAN_OUT_DEVICE)) {
             void* h = hb.take(sizeof(dq_state) * nops, 16);
             DQ_HIP(ctx, hipMemcpyAsync(h, dout, sizeof(dq_state) * nops, hipMemcpyDeviceToHost, ctx->stream));

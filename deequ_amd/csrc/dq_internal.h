@@ -110,6 +110,38 @@ struct OpMap {
     int64_t nrows;       // count(*) of the batch
 };
 
+// String-shaped ops (strings.hip): one slot per (column, where).
+enum StrFlags : uint32_t {
+    SF_LEN = 1u,    // MinLength / MaxLength (UTF-8 characters)
+    SF_DTYPE = 2u,  // DataType histogram
+    SF_HLL = 4u,    // ApproxCountDistinct over UTF-8 bytes
+};
+
+struct StrSlot {
+    const uint8_t* data;       // STRING: UTF-8 bytes (4-byte aligned, >= 16 readable bytes past the end)
+    const int32_t* offsets;    // STRING: nrows + 1 offsets
+    const void* values;        // fixed width (DataType of a non-string column)
+    const uint64_t* validity;  // nullptr = all valid
+    const uint64_t* where_t;   // where TRUE (padded bitmap) or nullptr
+    int32_t spark_type;
+    int32_t decimal_scale;
+    uint32_t flags;            // StrFlags
+    int32_t hll_slot;          // shared numbering with the fixed-width HLL partials, -1 = none
+};
+
+struct StrPartial {
+    int64_t n;                 // rows with the value non-NULL and where TRUE
+    int64_t minlen, maxlen;
+    int64_t dt[5];             // DataType classes (index 0 unused: NULLs are derived)
+};
+
+struct StrOpMap {
+    int32_t op;                // index into the dq_state output
+    int32_t kind;              // DQ_OP_MIN_LENGTH / DQ_OP_MAX_LENGTH / DQ_OP_DATATYPE
+    int32_t slot;
+    int32_t pad;
+};
+
 // Predicate VM limits.
 constexpr int kPredStack = 16;
 
@@ -175,6 +207,11 @@ void launch_finalize(const OpMap* ops, int nops, const SlotPartial* finals, cons
                      dq_state* out, hipStream_t s);
 void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
                       int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s);
+int string_scan_grid(int cus, int64_t nrows);
+void launch_string_scan(const StrSlot* slots, int nslots, int64_t nrows, int grid, int gstride, StrPartial* partials,
+                        uint8_t* hll_partials, hipStream_t s);
+void launch_finalize_strings(const StrOpMap* ops, int nops, const StrPartial* partials, int nblocks, int gstride,
+                             int64_t nrows, dq_state* out, hipStream_t s);
 void launch_synth_column(int kind, uint64_t seed, int64_t row0, int64_t nrows, void* out, hipStream_t s);
 void launch_synth_freq_keys(int64_t total, int64_t distinct, int64_t row0, int64_t nrows, int64_t* out, hipStream_t s);
 void launch_synth_validity(uint64_t seed, int64_t row0, int64_t nrows, int permille, uint8_t* out,

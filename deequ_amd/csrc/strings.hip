@@ -1,0 +1,327 @@
+// strings.hip — the string-shaped scan ops of the fused pass (gfx950 / CDNA4).
+//
+// Per (column, where) "string slot", one lane per row:
+//   MinLength / MaxLength    min/max(length(when(where, col))) — UTF-8 character count
+//                            (A/MinLength.scala:28-30, A/MaxLength.scala:28-30)
+//   DataType                 StatefulDataType.update (C/StatefulDataType.scala:58-69): the value cast to
+//                            string, classified by the full-match regexes
+//                            FRACTIONAL ^(-|\+)? ?\d*\.\d*$, INTEGRAL ^(-|\+)? ?\d*$, BOOLEAN ^(true|false)$
+//                            (:36-38), in that order; rows outside `where` count as NULL
+//                            (conditionalSelection, A/DataType.scala:146-148)
+//   ApproxCountDistinct      XxHash64(UTF-8 bytes, seed 42) into HLL++ registers (P = 9) in LDS
+//                            (C/StatefulHyperloglogPlus.scala:89-112) — the register partials share the
+//                            fixed-width HLL arrays, so reduce_hll / finalize pack them the same way.
+// Non-string columns only reach this kernel for DataType, whose string cast is decided from the value
+// (Java's Long/Double/Float/BigDecimal.toString rules, see numeric_class).
+// Byte work, no MFMA: bytes are read as aligned little-endian dwords (adjacent lanes own adjacent
+// strings, so a wave's loads share cache lines); per-block partials are folded in a fixed order.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include "dq_common.h"
+#include "dq_internal.h"
+
+namespace dq {
+
+namespace {
+
+__device__ __forceinline__ uint32_t load_word(const uint8_t* base, int64_t aligned_off) {
+    return *reinterpret_cast<const uint32_t*>(base + aligned_off);
+}
+
+__device__ __forceinline__ uint8_t byte_at(const uint8_t* base, int64_t off) { return base[off]; }
+
+// UTF-8 characters (non-continuation bytes) in [o0, o1) — UTF8String.numChars for valid UTF-8.
+__device__ int64_t utf8_length(const uint8_t* data, int64_t o0, int64_t o1) {
+    if (o1 <= o0) return 0;
+    int64_t cont = 0;
+    const int64_t w0 = o0 & ~(int64_t)3;
+    for (int64_t w = w0; w < o1; w += 4) {
+        uint32_t x = load_word(data, w);
+        uint32_t mask = 0xFFFFFFFFu;
+        if (w < o0) mask &= 0xFFFFFFFFu << (8 * (o0 - w));
+        if (w + 4 > o1) mask &= 0xFFFFFFFFu >> (8 * (w + 4 - o1));
+        // continuation byte: bit 7 set, bit 6 clear
+        const uint32_t c = x & ~(x << 1) & 0x80808080u & mask;
+        cont += __popc(c);
+    }
+    return (o1 - o0) - cont;
+}
+
+// XXH64.hashUnsafeBytes over data[o0, o1) (seed 42), reading bytes through dword loads.
+__device__ __forceinline__ uint64_t le64_at(const uint8_t* data, int64_t p) {
+    const int64_t a = p & ~(int64_t)3;
+    const int sh = (int)(p - a) * 8;
+    const uint32_t w0 = load_word(data, a), w1 = load_word(data, a + 4), w2 = load_word(data, a + 8);
+    const uint64_t lo = sh ? (((uint64_t)w1 << (32 - sh)) | (w0 >> sh)) : w0;
+    const uint64_t hi = sh ? (((uint64_t)w2 << (32 - sh)) | (w1 >> sh)) : w1;
+    return (lo & 0xFFFFFFFFull) | (hi << 32);
+}
+__device__ __forceinline__ uint32_t le32_at(const uint8_t* data, int64_t p) {
+    const int64_t a = p & ~(int64_t)3;
+    const int sh = (int)(p - a) * 8;
+    const uint32_t w0 = load_word(data, a);
+    if (!sh) return w0;
+    const uint32_t w1 = load_word(data, a + 4);
+    return (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
+}
+
+__device__ uint64_t xxh64_utf8(const uint8_t* data, int64_t o0, int64_t o1, uint64_t seed) {
+    const int64_t len = o1 - o0;
+    int64_t p = o0;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = seed + P64_1 + P64_2, v2 = seed + P64_2, v3 = seed, v4 = seed - P64_1;
+        const int64_t limit = o1 - 32;
+        do {
+            v1 = xxh_round(v1, le64_at(data, p));
+            v2 = xxh_round(v2, le64_at(data, p + 8));
+            v3 = xxh_round(v3, le64_at(data, p + 16));
+            v4 = xxh_round(v4, le64_at(data, p + 24));
+            p += 32;
+        } while (p <= limit);
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = xxh_merge_round(h, v1);
+        h = xxh_merge_round(h, v2);
+        h = xxh_merge_round(h, v3);
+        h = xxh_merge_round(h, v4);
+    } else {
+        h = seed + P64_5;
+    }
+    h += (uint64_t)len;
+    while (p + 8 <= o1) {
+        h ^= xxh_round(0, le64_at(data, p));
+        h = rotl64(h, 27) * P64_1 + P64_4;
+        p += 8;
+    }
+    if (p + 4 <= o1) {
+        h ^= (uint64_t)le32_at(data, p) * P64_1;
+        h = rotl64(h, 23) * P64_2 + P64_3;
+        p += 4;
+    }
+    while (p < o1) {
+        h ^= (uint64_t)byte_at(data, p) * P64_5;
+        h = rotl64(h, 11) * P64_1;
+        ++p;
+    }
+    return xxh_fmix(h);
+}
+
+enum DtClass : int { DT_NULL = 0, DT_FRACTIONAL = 1, DT_INTEGRAL = 2, DT_BOOLEAN = 3, DT_STRING = 4 };
+
+// StatefulDataType's three full-match regexes over the UTF-8 bytes.
+__device__ int classify_string(const uint8_t* data, int64_t o0, int64_t o1) {
+    int64_t i = o0;
+    if (i < o1) {
+        const uint8_t c = byte_at(data, i);
+        if (c == '-' || c == '+') ++i;
+    }
+    if (i < o1 && byte_at(data, i) == ' ') ++i;
+    while (i < o1) {
+        const uint8_t c = byte_at(data, i);
+        if (c < '0' || c > '9') break;
+        ++i;
+    }
+    if (i == o1) return DT_INTEGRAL;  // includes "" and a lone sign
+    if (byte_at(data, i) == '.') {
+        ++i;
+        while (i < o1) {
+            const uint8_t c = byte_at(data, i);
+            if (c < '0' || c > '9') break;
+            ++i;
+        }
+        if (i == o1) return DT_FRACTIONAL;
+    }
+    const int64_t n = o1 - o0;
+    if (n == 4 && byte_at(data, o0) == 't' && byte_at(data, o0 + 1) == 'r' && byte_at(data, o0 + 2) == 'u' &&
+        byte_at(data, o0 + 3) == 'e')
+        return DT_BOOLEAN;
+    if (n == 5 && byte_at(data, o0) == 'f' && byte_at(data, o0 + 1) == 'a' && byte_at(data, o0 + 2) == 'l' &&
+        byte_at(data, o0 + 3) == 's' && byte_at(data, o0 + 4) == 'e')
+        return DT_BOOLEAN;
+    return DT_STRING;
+}
+
+// DataType of a non-string value through Spark's cast to string:
+//   boolean -> "true"/"false"; integral -> digits; double/float -> Java toString, which is plain
+//   ("d.ddd", FRACTIONAL) exactly for 0 and 1e-3 <= |x| < 1e7 and "d.dddE±n" / "NaN" / "Infinity"
+//   (STRING) otherwise; decimal -> BigDecimal.toString: scale 0 -> digits (INTEGRAL), otherwise
+//   plain with a point (FRACTIONAL) unless the adjusted exponent is < -6 (scientific, STRING);
+//   date / timestamp -> "yyyy-MM-dd..." (STRING).
+__device__ int numeric_class(const StrSlot& s, int64_t row) {
+    switch (s.spark_type) {
+        case DQ_TYPE_BOOLEAN: return DT_BOOLEAN;
+        case DQ_TYPE_BYTE: case DQ_TYPE_SHORT: case DQ_TYPE_INT: case DQ_TYPE_LONG: return DT_INTEGRAL;
+        case DQ_TYPE_DOUBLE: {
+            const double x = static_cast<const double*>(s.values)[row];
+            const double a = fabs(x);
+            return (x == 0.0 || (a >= 1e-3 && a < 1e7)) ? DT_FRACTIONAL : DT_STRING;  // NaN/inf fail both
+        }
+        case DQ_TYPE_FLOAT: {
+            const float x = static_cast<const float*>(s.values)[row];
+            const float a = fabsf(x);
+            return (x == 0.0f || (a >= 1e-3f && a < 1e7f)) ? DT_FRACTIONAL : DT_STRING;
+        }
+        case DQ_TYPE_DECIMAL: {
+            if (s.decimal_scale == 0) return DT_INTEGRAL;
+            const int64_t v = static_cast<const int64_t*>(s.values)[row];
+            uint64_t m = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+            int digits = 1;
+            while (m >= 10) {
+                m /= 10;
+                ++digits;
+            }
+            return (digits - 1 - s.decimal_scale) < -6 ? DT_STRING : DT_FRACTIONAL;
+        }
+        default: return DT_STRING;  // DATE, TIMESTAMP
+    }
+}
+
+__device__ __forceinline__ int64_t shfl_down_i64s(int64_t x, int off) {
+    int lo = (int)(uint32_t)(uint64_t)x, hi = (int)(uint32_t)((uint64_t)x >> 32);
+    lo = __shfl_down(lo, off, 64);
+    hi = __shfl_down(hi, off, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(kBlock)
+scan_strings_kernel(const StrSlot* __restrict__ slots, int nslots, int64_t nrows, int gstride,
+                    StrPartial* __restrict__ partials, uint8_t* __restrict__ hll_partials) {
+    __shared__ uint32_t regs[kHllRegs];
+    __shared__ StrPartial red[kBlock / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int si = 0; si < nslots; ++si) {
+        const StrSlot s = slots[si];
+        const bool str = s.spark_type == DQ_TYPE_STRING;
+        const bool want_hll = (s.flags & SF_HLL) && str;
+        if (want_hll) {
+            for (int i = tid; i < kHllRegs; i += kBlock) regs[i] = 0;
+            __syncthreads();
+        }
+        int64_t n = 0, mn = INT64_MAX, mx = INT64_MIN;
+        int64_t dt[5] = {0, 0, 0, 0, 0};
+        const int64_t stride = (int64_t)gridDim.x * kBlock;
+        for (int64_t row = (int64_t)blockIdx.x * kBlock + tid; row < nrows; row += stride) {
+            bool on = s.validity == nullptr || ((s.validity[row >> 6] >> (row & 63)) & 1ull);
+            if (s.where_t) on = on && ((s.where_t[row >> 6] >> (row & 63)) & 1ull);
+            if (!on) continue;
+            ++n;
+            if (str) {
+                const int64_t o0 = s.offsets[row], o1 = s.offsets[row + 1];
+                if (s.flags & SF_LEN) {
+                    const int64_t len = utf8_length(s.data, o0, o1);
+                    mn = len < mn ? len : mn;
+                    mx = len > mx ? len : mx;
+                }
+                if (s.flags & SF_DTYPE) dt[classify_string(s.data, o0, o1)] += 1;
+                if (want_hll) {
+                    const uint64_t x = xxh64_utf8(s.data, o0, o1, SPARK_HLL_SEED);
+                    atomicMax(&regs[hll_index(x)], hll_rank(x));
+                }
+            } else if (s.flags & SF_DTYPE) {
+                dt[numeric_class(s, row)] += 1;
+            }
+        }
+        // wave64 tree, then the 4 waves in a fixed order
+#pragma unroll 1
+        for (int off = 32; off > 0; off >>= 1) {
+            const int64_t on_ = shfl_down_i64s(n, off), omn = shfl_down_i64s(mn, off), omx = shfl_down_i64s(mx, off);
+            int64_t odt[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) odt[k] = shfl_down_i64s(dt[k], off);
+            if (lane < off) {
+                n += on_;
+                mn = omn < mn ? omn : mn;
+                mx = omx > mx ? omx : mx;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) dt[k] += odt[k];
+            }
+        }
+        if (lane == 0) {
+            red[wave].n = n;
+            red[wave].minlen = mn;
+            red[wave].maxlen = mx;
+            for (int k = 0; k < 5; ++k) red[wave].dt[k] = dt[k];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            StrPartial p = red[0];
+            for (int w = 1; w < kBlock / 64; ++w) {
+                p.n += red[w].n;
+                p.minlen = red[w].minlen < p.minlen ? red[w].minlen : p.minlen;
+                p.maxlen = red[w].maxlen > p.maxlen ? red[w].maxlen : p.maxlen;
+                for (int k = 0; k < 5; ++k) p.dt[k] += red[w].dt[k];
+            }
+            partials[(int64_t)si * gstride + blockIdx.x] = p;
+        }
+        if (want_hll) {
+            __syncthreads();
+            uint8_t* dst = hll_partials + ((int64_t)s.hll_slot * gstride + blockIdx.x) * kHllRegs;
+            for (int i = tid; i < kHllRegs; i += kBlock) dst[i] = (uint8_t)regs[i];
+        }
+        __syncthreads();
+    }
+}
+
+// One thread per string op: fold its slot's block partials in block order, write the dq_state.
+__global__ void finalize_strings_kernel(const StrOpMap* __restrict__ ops, int nops, const StrPartial* __restrict__ partials,
+                                        int nblocks, int gstride, int64_t nrows, dq_state* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nops) return;
+    const StrOpMap om = ops[i];
+    int64_t n = 0, mn = INT64_MAX, mx = INT64_MIN;
+    int64_t dt[5] = {0, 0, 0, 0, 0};
+    for (int b = 0; b < nblocks; ++b) {
+        const StrPartial p = partials[(int64_t)om.slot * gstride + b];
+        n += p.n;
+        mn = p.minlen < mn ? p.minlen : mn;
+        mx = p.maxlen > mx ? p.maxlen : mx;
+        for (int k = 1; k < 5; ++k) dt[k] += p.dt[k];
+    }
+    dq_state* st = out + om.op;
+    for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) st->u.hll.words[w] = 0;
+    st->kind = om.kind;
+    switch (om.kind) {
+        case DQ_OP_MIN_LENGTH:
+            st->u.dbl.value = (double)mn;
+            st->present = n > 0;
+            break;
+        case DQ_OP_MAX_LENGTH:
+            st->u.dbl.value = (double)mx;
+            st->present = n > 0;
+            break;
+        default: {  // DQ_OP_DATATYPE: the UDAF buffer is never NULL; rows outside where / NULL are numNull
+            st->u.datatype.num_fractional = dt[DT_FRACTIONAL];
+            st->u.datatype.num_integral = dt[DT_INTEGRAL];
+            st->u.datatype.num_boolean = dt[DT_BOOLEAN];
+            st->u.datatype.num_string = dt[DT_STRING];
+            st->u.datatype.num_null = nrows - (dt[1] + dt[2] + dt[3] + dt[4]);
+            st->present = 1;
+            break;
+        }
+    }
+}
+
+int string_scan_grid(int cus, int64_t nrows) {
+    const int64_t want = (nrows + kBlock - 1) / kBlock;
+    return (int)(want < 1 ? 1 : (want < (int64_t)cus * 4 ? want : (int64_t)cus * 4));
+}
+
+void launch_string_scan(const StrSlot* slots, int nslots, int64_t nrows, int grid, int gstride, StrPartial* partials,
+                        uint8_t* hll_partials, hipStream_t s) {
+    if (nslots == 0) return;
+    hipLaunchKernelGGL(scan_strings_kernel, dim3(grid), dim3(kBlock), 0, s, slots, nslots, nrows, gstride, partials,
+                       hll_partials);
+}
+
+void launch_finalize_strings(const StrOpMap* ops, int nops, const StrPartial* partials, int nblocks, int gstride,
+                             int64_t nrows, dq_state* out, hipStream_t s) {
+    if (nops == 0) return;
+    hipLaunchKernelGGL(finalize_strings_kernel, dim3((nops + 63) / 64), dim3(64), 0, s, ops, nops, partials, nblocks,
+                       gstride, nrows, out);
+}
+
+}  // namespace dq

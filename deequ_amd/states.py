@@ -254,6 +254,68 @@ class ApproxCountDistinctState(DoubleValuedState):
         return "ApproxCountDistinctState(%s)" % ",".join(str(np.int64(np.uint64(w))) for w in self.words)
 
 
+class DataTypeHistogram(State):
+    """A/DataType.scala:81-92 (+ toBytes / toDistribution / determineType :94-183)."""
+    NULL_POS, FRACTIONAL_POS, INTEGRAL_POS, BOOLEAN_POS, STRING_POS = range(5)
+    SIZE_IN_BYTES = 40
+
+    def __init__(self, numNull, numFractional, numIntegral, numBoolean, numString):
+        self.numNull, self.numFractional, self.numIntegral = int(numNull), int(numFractional), int(numIntegral)
+        self.numBoolean, self.numString = int(numBoolean), int(numString)
+
+    def _t(self):
+        return (self.numNull, self.numFractional, self.numIntegral, self.numBoolean, self.numString)
+
+    def sum(self, other):
+        return DataTypeHistogram(*[a + b for a, b in zip(self._t(), other._t())])
+
+    def __eq__(self, o):
+        return isinstance(o, DataTypeHistogram) and o._t() == self._t()
+
+    def __repr__(self):
+        return "DataTypeHistogram(%d,%d,%d,%d,%d)" % self._t()
+
+    def toBytes(self):
+        import struct
+        return struct.pack(">5q", *self._t())
+
+    @staticmethod
+    def fromBytes(data):
+        import struct
+        if len(data) != DataTypeHistogram.SIZE_IN_BYTES:
+            raise ValueError("requirement failed")
+        return DataTypeHistogram(*struct.unpack(">5q", data))
+
+    def toDistribution(self):
+        from .metrics import Distribution, DistributionValue
+        total = sum(self._t())
+
+        def ratio(x):
+            return x / total if total else float("nan")
+        return Distribution({
+            "Unknown": DistributionValue(self.numNull, ratio(self.numNull)),
+            "Fractional": DistributionValue(self.numFractional, ratio(self.numFractional)),
+            "Integral": DistributionValue(self.numIntegral, ratio(self.numIntegral)),
+            "Boolean": DistributionValue(self.numBoolean, ratio(self.numBoolean)),
+            "String": DistributionValue(self.numString, ratio(self.numString))}, 5)
+
+    @staticmethod
+    def determineType(dist):
+        """DataTypeHistogram.determineType (A/DataType.scala:143-171)."""
+        def r(k):
+            v = dist.values.get(k)
+            return 0.0 if v is None else v.ratio
+        if r("Unknown") == 1.0:
+            return "Unknown"
+        if r("String") > 0.0 or (r("Boolean") > 0.0 and (r("Integral") > 0.0 or r("Fractional") > 0.0)):
+            return "String"
+        if r("Boolean") > 0.0:
+            return "Boolean"
+        if r("Fractional") > 0.0:
+            return "Fractional"
+        return "Integral"
+
+
 class ApproxQuantileState(State):
     """A/ApproxQuantile.scala:28-36: wraps a PercentileDigest; sum = PercentileDigest.merge."""
 
@@ -297,6 +359,9 @@ def state_to_native(kind, state):
     elif isinstance(state, ApproxCountDistinctState):
         for i, w in enumerate(state.words):
             u.hll.words[i] = int(np.int64(np.uint64(w)))
+    elif isinstance(state, DataTypeHistogram):
+        d = u.datatype
+        d.num_null, d.num_fractional, d.num_integral, d.num_boolean, d.num_string = state._t()
     else:
         raise ValueError("cannot encode %r" % (state,))
     return st
@@ -330,4 +395,7 @@ def state_from_native(st):
         return CorrelationState(u.corr.n, u.corr.x_avg, u.corr.y_avg, u.corr.ck, u.corr.x_mk, u.corr.y_mk)
     if k == N.OP_APPROX_COUNT_DISTINCT:
         return ApproxCountDistinctState(list(u.hll.words))
+    if k == N.OP_DATATYPE:
+        d = u.datatype
+        return DataTypeHistogram(d.num_null, d.num_fractional, d.num_integral, d.num_boolean, d.num_string)
     raise ValueError("unknown state kind %d" % k)

@@ -360,7 +360,116 @@ def expected_state(table, analyzer, exact=True):
         words = np.zeros(52, dtype=np.int64)
         lib().oracle_hll_pack(regs.ctypes.data, words.ctypes.data)
         return S.ApproxCountDistinctState([int(w) for w in words])
+    if name in ("MinLength", "MaxLength"):
+        # min/max(length(when(where, col))): Spark's length = characters (A/MinLength.scala:28-30)
+        c = table[analyzer.column]
+        wt, _ = _where(table, analyzer.where)
+        m = _valid(c) & wt
+        lens = [len(c.value_at(i)) for i in range(c.length) if m[i]]
+        if not lens:
+            return None
+        return S.MinState(float(min(lens))) if name == "MinLength" else S.MaxState(float(max(lens)))
+    if name == "DataType":
+        # StatefulDataType.update over the value cast to string (C/StatefulDataType.scala:58-69),
+        # NULL for rows outside `where` (conditionalSelection, A/DataType.scala:146-148)
+        c = table[analyzer.column]
+        wt, _ = _where(table, analyzer.where)
+        m = _valid(c) & wt
+        counts = [0, 0, 0, 0, 0]
+        for i in range(c.length):
+            if not m[i]:
+                counts[0] += 1
+                continue
+            counts[datatype_class(spark_cast_to_string(c, i))] += 1
+        return S.DataTypeHistogram(*counts)
     raise ValueError("no oracle for %s" % name)
+
+
+# StatefulDataType's regexes (C/StatefulDataType.scala:36-38), ASCII \d as in java.util.regex
+_FRACTIONAL = __import__("re").compile(r"^(-|\+)? ?[0-9]*\.[0-9]*$")
+_INTEGRAL = __import__("re").compile(r"^(-|\+)? ?[0-9]*$")
+_BOOLEAN = __import__("re").compile(r"^(true|false)$")
+
+
+def datatype_class(text):
+    """1 Fractional, 2 Integral, 3 Boolean, 4 String; Regex.unapplySeq is a full match (`matches`)."""
+    if _FRACTIONAL.fullmatch(text):
+        return 1
+    if _INTEGRAL.fullmatch(text):
+        return 2
+    if _BOOLEAN.fullmatch(text):
+        return 3
+    return 4
+
+
+def java_double_to_string(d, is_float=False):
+    """java.lang.Double/Float.toString: shortest round-trip digits (Python repr), plain notation for
+    1e-3 <= |d| < 1e7, otherwise d.dddE<exp>; "NaN", "Infinity"."""
+    if d != d:
+        return "NaN"
+    if d in (float("inf"), float("-inf")):
+        return "Infinity" if d > 0 else "-Infinity"
+    if d == 0.0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    r = str(np.float32(d)) if is_float else repr(float(d))  # shortest round-trip digits of the float / double
+    sign = "-" if r.startswith("-") else ""
+    r = r.lstrip("-")
+    mant, _, exp = r.partition("e")
+    digits = mant.replace(".", "")
+    point = mant.index(".") if "." in mant else len(mant)
+    e10 = (int(exp) if exp else 0) + point  # value = 0.digits * 10^e10
+    lead = len(digits) - len(digits.lstrip("0"))
+    digits = digits.strip("0") or "0"
+    e10 -= lead
+    thr = np.float32(1e-3) if is_float else 1e-3
+    if thr <= abs(d) < 1e7:
+        if e10 <= 0:
+            return sign + "0." + "0" * (-e10) + digits
+        if e10 >= len(digits):
+            return sign + digits + "0" * (e10 - len(digits)) + ".0"
+        return sign + digits[:e10] + "." + digits[e10:]
+    frac = digits[1:] or "0"
+    return "%s%s.%sE%d" % (sign, digits[0], frac, e10 - 1)
+
+
+def spark_cast_to_string(col, i):
+    """Cast(value AS STRING) for row i (Spark 2.2: Java toString of the boxed value, BigDecimal.toString)."""
+    from decimal import Decimal
+    t = col.spark_type
+    if t == T_STRING:
+        return col.value_at(i)
+    v = col.values[i]
+    if t == T_BOOLEAN:
+        return "true" if v else "false"
+    if t in (T_BYTE, T_SHORT, T_INT, T_LONG):
+        return str(int(v))
+    if t == T_DOUBLE:
+        return java_double_to_string(float(v))
+    if t == T_FLOAT:
+        return java_double_to_string(float(v), is_float=True)
+    if t == T_DECIMAL:
+        return java_bigdecimal_to_string(int(v), col.decimal_scale)
+    if t == T_DATE:
+        import datetime
+        return (datetime.date(1970, 1, 1) + datetime.timedelta(days=int(v))).isoformat()
+    return "1970-01-01 00:00:00"  # timestamps: any "yyyy-MM-dd HH:mm:ss" text classifies as String
+
+
+def java_bigdecimal_to_string(unscaled, scale):
+    """java.math.BigDecimal.toString (scientific when scale < 0 or adjusted exponent < -6)."""
+    neg = unscaled < 0
+    digits = str(abs(unscaled))
+    adjusted = len(digits) - 1 - scale
+    if scale >= 0 and adjusted >= -6:
+        if scale == 0:
+            body = digits
+        elif len(digits) > scale:
+            body = digits[:-scale] + "." + digits[-scale:]
+        else:
+            body = "0." + "0" * (scale - len(digits)) + digits
+    else:
+        body = digits[0] + ("." + digits[1:] if len(digits) > 1 else "") + "E" + ("+" if adjusted > 0 else "") + str(adjusted)
+    return ("-" if neg else "") + body
 
 
 def frequencies(table, columns, include_nulls=False):

@@ -54,9 +54,32 @@ FIXTURES = {
     # T/analyzers/NullHandlingTests.scala:40-52: all-null columns of every type, 8 rows
     "dfAllNull": {"names": ["stringCol", "numericCol", "numericCol2", "numericCol3"], "types": [S, D, D, D],
                   "rows": [[None, None, None, float(i)] for i in range(1, 9)]},
+    # FixtureSupport.scala:259-268
+    "dfWithVariableStringLengthValues": {"names": ["att1"], "types": [S], "rows": [[""], ["a"], ["bb"], ["ccc"],
+                                                                                  ["dddd"]]},
+    # FixtureSupport.scala:110-135
+    "dfFractionalIntegralTypes": {"names": ["item", "att1"], "types": [S, S], "rows": [["1", "1.0"], ["2", "1"]]},
+    "dfFractionalStringTypes": {"names": ["item", "att1"], "types": [S, S], "rows": [["1", "1.0"], ["2", "a"]]},
+    "dfIntegralStringTypes": {"names": ["item", "att1"], "types": [S, S], "rows": [["1", "1"], ["2", "a"]]},
+    # T/analyzers/AnalyzerTests.scala:320-343: att1 cast to FloatType / StringType
+    "dfWithNumericValuesCast": {"names": ["item", "att1_float", "att1_str"], "types": [S, "float", S], "rows": [
+        [str(i), float(i), str(i)] for i in range(1, 7)]},
+    "dfWithNumericFractionalValuesStr": {"names": ["item", "att1_str"], "types": [S, S], "rows": [
+        [str(i), "%d.0" % i] for i in range(1, 7)]},
+    # T/analyzers/AnalyzerTests.scala:389-420
+    "dfBoolean": {"names": ["item", "att1"], "types": [S, S], "rows": [["1", "true"], ["2", "false"]]},
+    "dfBooleanAndNull": {"names": ["item", "att1"], "types": [S, S], "rows": [
+        ["1", "true"], ["2", "false"], ["3", None], ["4", "2.0"]]},
+    # T/analyzers/AnalyzerTests.scala:568-601: sparkContext.range(-1000L, 1000L).toDF("att1")
+    "dfRange": {"names": ["att1"], "types": [L], "rows": [[i] for i in range(-1000, 1000)]},
 }
 
 ENT = -(0.75 * math.log(0.75) + 0.25 * math.log(0.25))
+
+
+def dt(**kw):
+    """distributionFrom (T/analyzers/AnalyzerTests.scala:271-291): the given classes, zeros elsewhere."""
+    return {"datatype": {k: list(v) for k, v in kw.items()}}
 
 # (fixture, analyzer spec, expected) — analyzer spec: [class, args...]; expected: number | "NaN" |
 # {"failure": ExceptionName} | {"bins": n, "keys": [...]}
@@ -132,6 +155,53 @@ KATS = [
      "T/analyzers/AnalyzerTests.scala:644-652"),
     ("dfWithConditionallyInformativeColumns", ["Correlation", "att2", "att1"], 1.0,
      "T/analyzers/AnalyzerTests.scala:653-656"),
+    # :294-420 DataType
+    ("dfFull", ["DataType", "att1"], dt(String=(4, 1.0)), "T/analyzers/AnalyzerTests.scala:294-299"),
+    ("dfWithNumericValues", ["DataType", "att1"], dt(Integral=(6, 1.0)), "T/analyzers/AnalyzerTests.scala:301-305"),
+    ("dfWithNegativeNumbers", ["DataType", "att1"], dt(Integral=(4, 1.0)), "T/analyzers/AnalyzerTests.scala:307-311"),
+    ("dfWithNegativeNumbers", ["DataType", "att2"], dt(Fractional=(4, 1.0)),
+     "T/analyzers/AnalyzerTests.scala:313-318"),
+    ("dfWithNumericValuesCast", ["DataType", "att1_float"], dt(Fractional=(6, 1.0)),
+     "T/analyzers/AnalyzerTests.scala:321-327"),
+    ("dfWithNumericValuesCast", ["DataType", "att1_str"], dt(Integral=(6, 1.0)),
+     "T/analyzers/AnalyzerTests.scala:329-334"),
+    ("dfWithNumericFractionalValuesStr", ["DataType", "att1_str"], dt(Fractional=(6, 1.0)),
+     "T/analyzers/AnalyzerTests.scala:336-343"),
+    ("dfFractionalIntegralTypes", ["DataType", "att1"], dt(Fractional=(1, 0.5), Integral=(1, 0.5)),
+     "T/analyzers/AnalyzerTests.scala:352-360"),
+    ("dfFractionalStringTypes", ["DataType", "att1"], dt(Fractional=(1, 0.5), String=(1, 0.5)),
+     "T/analyzers/AnalyzerTests.scala:362-370"),
+    ("dfIntegralStringTypes", ["DataType", "att1"], dt(Integral=(1, 0.5), String=(1, 0.5)),
+     "T/analyzers/AnalyzerTests.scala:372-380"),
+    ("dfWithUniqueColumns", ["DataType", "uniqueWithNulls"], dt(Unknown=(1, 1.0 / 6.0), Integral=(5, 5.0 / 6.0)),
+     "T/analyzers/AnalyzerTests.scala:382-390"),
+    ("dfBoolean", ["DataType", "att1"], dt(Boolean=(2, 1.0)), "T/analyzers/AnalyzerTests.scala:392-402"),
+    ("dfBooleanAndNull", ["DataType", "att1"], dt(Fractional=(1, 0.25), Unknown=(1, 0.25), Boolean=(2, 0.5)),
+     "T/analyzers/AnalyzerTests.scala:404-420"),
+    # :506-540 MinLength / MaxLength
+    ("dfWithVariableStringLengthValues", ["MinLength", "att1"], 0.0, "T/analyzers/AnalyzerTests.scala:506-510"),
+    ("dfWithVariableStringLengthValues", ["MinLength", "att1", "att1 != ''"], 1.0,
+     "T/analyzers/AnalyzerTests.scala:512-517"),
+    ("dfWithNumericValues", ["MinLength", "att1"], {"failure": "WrongColumnTypeException"},
+     "T/analyzers/AnalyzerTests.scala:519-522"),
+    ("dfWithVariableStringLengthValues", ["MaxLength", "att1"], 4.0, "T/analyzers/AnalyzerTests.scala:524-528"),
+    ("dfWithVariableStringLengthValues", ["MaxLength", "att1", "att1 != 'dddd'"], 3.0,
+     "T/analyzers/AnalyzerTests.scala:530-535"),
+    ("dfWithNumericValues", ["MaxLength", "att1"], {"failure": "WrongColumnTypeException"},
+     "T/analyzers/AnalyzerTests.scala:537-540"),
+    # :568-601 ApproxQuantile (bounds only: the reference pins no digest values)
+    ("dfRange", ["ApproxQuantile", "att1", 0.5], {"between": [-20, 20]}, "T/analyzers/AnalyzerTests.scala:568-579"),
+    ("dfRange", ["ApproxQuantile", "att1", 0.25], {"between": [-520, -480]},
+     "T/analyzers/AnalyzerTests.scala:581-590"),
+    ("dfRange", ["ApproxQuantile", "att1", 0.75], {"between": [480, 520]}, "T/analyzers/AnalyzerTests.scala:592-601"),
+    ("dfWithNumericValues", ["ApproxQuantile", "att1", 0.5, 1.1], {"failure": "IllegalAnalyzerParameterException"},
+     "T/analyzers/AnalyzerTests.scala:603-610"),
+    ("dfWithNumericValues", ["ApproxQuantile", "att1", 0.5, -0.1], {"failure": "IllegalAnalyzerParameterException"},
+     "T/analyzers/AnalyzerTests.scala:611-618"),
+    ("dfWithNumericValues", ["ApproxQuantile", "att1", -0.1], {"failure": "IllegalAnalyzerParameterException"},
+     "T/analyzers/AnalyzerTests.scala:619-627"),
+    ("dfWithNumericValues", ["ApproxQuantile", "att1", 1.1], {"failure": "IllegalAnalyzerParameterException"},
+     "T/analyzers/AnalyzerTests.scala:628-635"),
     # T/analyzers/NullHandlingTests.scala:54-141 (all-null columns)
     ("dfAllNull", ["Size"], 8.0, "T/analyzers/NullHandlingTests.scala:95"),
     ("dfAllNull", ["Completeness", "stringCol"], 0.0, "T/analyzers/NullHandlingTests.scala:96"),
@@ -157,6 +227,13 @@ KATS = [
      "T/analyzers/NullHandlingTests.scala:125"),
     ("dfAllNull", ["Correlation", "numericCol", "numericCol3"], {"failure": "EmptyStateException"},
      "T/analyzers/NullHandlingTests.scala:127"),
+    ("dfAllNull", ["ApproxQuantile", "numericCol", 0.5], {"failure": "EmptyStateException"},
+     "T/analyzers/NullHandlingTests.scala:113"),
+    ("dfAllNull", ["MinLength", "stringCol"], {"failure": "EmptyStateException"},
+     "T/analyzers/NullHandlingTests.scala:105"),
+    ("dfAllNull", ["MaxLength", "stringCol"], {"failure": "EmptyStateException"},
+     "T/analyzers/NullHandlingTests.scala:106"),
+    ("dfAllNull", ["DataType", "stringCol"], dt(Unknown=(8, 1.0)), "T/analyzers/NullHandlingTests.scala:108-109"),
 ]
 
 # T/analyzers/IncrementalAnalyzerTest.scala:31-268 — states of two partitions merged.

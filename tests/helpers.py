@@ -14,7 +14,8 @@ def analyzer_from_spec(spec):
     cls = getattr(D, name)
     if name == "Histogram" and len(args) == 2:
         return cls(args[0], None, args[1])
-    if name in ("Completeness", "Mean", "Sum", "Minimum", "Maximum", "StandardDeviation", "ApproxCountDistinct"):
+    if name in ("Completeness", "Mean", "Sum", "Minimum", "Maximum", "StandardDeviation", "ApproxCountDistinct",
+                "MinLength", "MaxLength", "DataType"):
         return cls(args[0], args[1] if len(args) > 1 else None)
     if name == "Compliance":
         return cls(args[0], args[1], args[2] if len(args) > 2 else None)
@@ -34,6 +35,17 @@ def check_metric(metric, expected, rel=0.0):
         return
     assert metric.value.isSuccess, metric
     v = metric.value.get()
+    if isinstance(expected, dict) and "between" in expected:
+        lo, hi = expected["between"]
+        assert lo < v < hi, (metric, expected)
+        return
+    if isinstance(expected, dict) and "datatype" in expected:
+        want = {k: (0, 0.0) for k in ("Unknown", "Fractional", "Integral", "Boolean", "String")}
+        want.update({k: tuple(x) for k, x in expected["datatype"].items()})
+        assert v.numberOfBins == 5, v
+        got = {k: (dv.absolute, dv.ratio) for k, dv in v.values.items()}
+        assert got == want, (got, want)
+        return
     if isinstance(expected, dict):
         assert v.numberOfBins == expected["bins"], v
         if "keys" in expected:

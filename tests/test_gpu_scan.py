@@ -18,7 +18,7 @@ from helpers import analyzer_from_spec, check_metric, table_from_fixture
 pytestmark = pytest.mark.gpu
 
 SCAN = {"Size", "Completeness", "Compliance", "Mean", "Sum", "Minimum", "Maximum", "StandardDeviation",
-        "Correlation", "ApproxCountDistinct"}
+        "Correlation", "ApproxCountDistinct", "MinLength", "MaxLength", "DataType", "ApproxQuantile"}
 REL = 1e-12
 
 
@@ -30,8 +30,6 @@ def test_scan_kats_one_by_one(kats):
     for k in scan_kats(kats):
         t = table_from_fixture(kats["fixtures"][k["fixture"]])
         a = analyzer_from_spec(k["analyzer"])
-        if k["analyzer"][0] == "ApproxCountDistinct" and t[a.column].spark_type == N.TYPE_STRING:
-            continue  # string HLL: not yet in the fused scan
         m = a.calculate(t)
         check_metric(m, k["expected"], rel=1e-15 if k["analyzer"][0] == "StandardDeviation" else 0.0)
 
@@ -46,8 +44,6 @@ def test_scan_kats_fused_in_one_run(kats):
         analyzers, exps = [], []
         for k in ks:
             a = analyzer_from_spec(k["analyzer"])
-            if k["analyzer"][0] == "ApproxCountDistinct" and a.column in t and t[a.column].spark_type == N.TYPE_STRING:
-                continue
             if isinstance(k["expected"], dict) and k["expected"].get("failure") == "*":
                 continue  # an unresolvable predicate fails the whole batch (R/AnalysisRunner.scala:320-323)
             analyzers.append(a)

@@ -47,6 +47,15 @@ def oracle_metric_value(table, analyzer):
     if name == "Histogram":
         freq, n = O.frequencies(table, [analyzer.column], include_nulls=True)
         return freq
+    if name in ("MinLength", "MaxLength"):
+        st = O.expected_state(table, analyzer)
+        return None if st is None else st.metricValue()
+    if name == "DataType":
+        st = O.expected_state(table, analyzer)
+        return st.toDistribution()
+    if name == "ApproxQuantile":
+        s = O.java_sorted_doubles(table, analyzer.column)
+        return float(s[max(1, math.ceil(analyzer.quantile * len(s))) - 1])  # the exact quantile
     raise KeyError(name)
 
 
@@ -64,6 +73,16 @@ def test_oracle_matches_reference_kats(kats):
             if isinstance(exp, dict):
                 continue
             raise
+        if isinstance(exp, dict) and "between" in exp:
+            assert exp["between"][0] < v < exp["between"][1], (k, v)
+            checked += 1
+            continue
+        if isinstance(exp, dict) and "datatype" in exp:
+            want = {kk: (0, 0.0) for kk in ("Unknown", "Fractional", "Integral", "Boolean", "String")}
+            want.update({kk: tuple(x) for kk, x in exp["datatype"].items()})
+            assert {kk: (dv.absolute, dv.ratio) for kk, dv in v.values.items()} == want, k
+            checked += 1
+            continue
         if isinstance(exp, dict):
             assert len(v) == exp["bins"], k
             continue
@@ -72,7 +91,7 @@ def test_oracle_matches_reference_kats(kats):
         else:
             assert v is not None and abs(v - exp) <= 1e-15 * max(1.0, abs(exp)), (k, v)
         checked += 1
-    assert checked >= 30
+    assert checked >= 50
 
 
 def test_oracle_stddev_spark_order_is_bit_exact(kats):
