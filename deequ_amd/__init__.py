@@ -12,6 +12,7 @@ from .states import (NumMatches, NumMatchesAndCount, MeanState, SumState, MinSta
                      ApproxQuantileState, DataTypeHistogram)
 from .analyzers import (Size, Completeness, Compliance, Mean, Sum, Minimum, Maximum, StandardDeviation, Correlation,
                         ApproxCountDistinct, ApproxQuantile, ApproxQuantiles, MinLength, MaxLength, DataType,
+                        PatternMatch, Patterns,
                         Uniqueness, Distinctness, UniqueValueRatio, Entropy, CountDistinct,
                         MutualInformation, Histogram, FrequenciesAndNumRows, Preconditions, computeFrequencies)
 from .runners import (AnalysisRunner, AnalysisRunBuilder, AnalyzerContext, Analysis, InMemoryStateProvider,

@@ -15,7 +15,7 @@ from .expr import compile_predicate
 from .metrics import (DoubleMetric, Entity, Failure, Success, EmptyStateException, NoSuchColumnException,
                       WrongColumnTypeException, NoColumnsSpecifiedException, NumberOfSpecifiedColumnsException,
                       IllegalAnalyzerParameterException, HistogramMetric, Distribution, DistributionValue,
-                      MetricCalculationRuntimeException, KeyedDoubleMetric, wrap_if_necessary)
+                      MetricCalculationRuntimeException, KeyedDoubleMetric, UnsupportedOnDevice, wrap_if_necessary)
 from .states import (NumMatches, NumMatchesAndCount, MeanState, SumState, MinState, MaxState, ApproxQuantileState,
                      DataTypeHistogram, state_from_native)
 from . import engine
@@ -406,6 +406,49 @@ class DataType(ScanShareableAnalyzer):
 
     def toFailureMetric(self, exception):
         return HistogramMetric(self.column, Failure(wrap_if_necessary(exception)))
+
+
+class PatternMatch(StandardScanShareableAnalyzer):
+    """A/PatternMatch.scala:37-55: sum(when(regexp_extract(col, pattern, 0) != "", 1).otherwise(0))
+    under `where`, plus conditionalCount. The pattern runs on the GPU's backtracking regex engine
+    (deequ_amd/regex.py, csrc/regex.hip); a NULL value counts 0."""
+    _fields = ("column", "pattern_", "where")
+    name = "PatternMatch"
+
+    def __init__(self, column, pattern, where=None):
+        self.column, self.where = column, where
+        self.pattern_ = pattern.pattern if hasattr(pattern, "pattern") else str(pattern)
+
+    instance = property(lambda self: self.column)
+
+    @property
+    def pattern(self):
+        return self.pattern_
+
+    def addOps(self, batch):
+        col = batch.data[self.column] if self.column in batch.col_index else None
+        if col is not None and col.spark_type in (N.TYPE_FLOAT, N.TYPE_DOUBLE, N.TYPE_DECIMAL, N.TYPE_DATE,
+                                                  N.TYPE_TIMESTAMP):
+            raise UnsupportedOnDevice(
+                "PatternMatch over %s: the GPU engine does not format this type as a string" % col.type_name)
+        p = batch.regex_predicate(self.column, self.pattern_)
+        return [batch.add_op(N.OP_COMPLIANCE, where=self.where, predicate_index=p)]
+
+
+class Patterns:
+    """A/PatternMatch.scala:57-72 (the reference's pattern constants)."""
+    EMAIL = (r"""(?:[a-z0-9!#$%&'*+/=?^_`{|}~-]+(?:\.[a-z0-9!#$%&'*+/=?^_`{|}~-]+)*|"(?:[\x01-\x08\x0b\x0c\x0e-\x1f"""
+             r"""\x21\x23-\x5b\x5d-\x7f]|\\[\x01-\x09\x0b\x0c\x0e-\x7f])*")@(?:(?:[a-z0-9](?:[a-z0-9-]*[a-z0-9])?\.)+"""
+             r"""[a-z0-9](?:[a-z0-9-]*[a-z0-9])?|\[(?:(?:25[0-5]|2[0-4][0-9]|[01]?[0-9][0-9]?)\.){3}(?:25[0-5]|"""
+             r"""2[0-4][0-9]|[01]?[0-9][0-9]?|[a-z0-9-]*[a-z0-9]:(?:[\x01-\x08\x0b\x0c\x0e-\x1f\x21-\x5a\x53-\x7f]|"""
+             r"""\\[\x01-\x09\x0b\x0c\x0e-\x7f])+)\])""")
+    URL = r"""(https?|ftp)://[^\s/$.?#].[^\s]*"""
+    SOCIAL_SECURITY_NUMBER_US = (
+        r"""((?!219-09-9999|078-05-1120)(?!666|000|9\d{2})\d{3}-(?!00)\d{2}-(?!0{4})\d{4})|((?!219 09 9999|078 05 1120)"""
+        r"""(?!666|000|9\d{2})\d{3} (?!00)\d{2} (?!0{4})\d{4})|((?!219099999|078051120)(?!666|000|9\d{2})\d{3}"""
+        r"""(?!00)\d{2}(?!0{4})\d{4})""")
+    CREDITCARD = (r"""\b(?:3[47]\d{2}([\ \-]?)\d{6}\1\d|(?:(?:4\d|5[1-5]|65)\d{2}|6011)([\ \-]?)\d{4}\2\d{4}\2)"""
+                  r"""\d{4}\b""")
 
 
 def _quantile_param_checks(quantiles, relativeError):

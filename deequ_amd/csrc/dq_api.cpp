@@ -299,6 +299,19 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         const dq_predicate& pr = preds[p];
         if (pr.code_len <= 0 || (pr.code_len & 1) || !pr.code)
             return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: empty or odd-length program", p);
+        if (pr.code_len == 4 && pr.code[2] == DQ_P_REGEX) {
+            const int c = pr.code[1], k = pr.code[3];
+            if (pr.code[0] != DQ_P_COL || !col_ok(c) || k < 0 || k >= pr.n_consts || pr.consts[k].tag != DQ_V_STRING ||
+                pr.consts[k].str_len < 32 || (pr.consts[k].str_offset & 3) ||
+                pr.consts[k].str_offset + pr.consts[k].str_len > pr.strings_len)
+                return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: malformed REGEX program", p);
+            const int t = columns[c].spark_type;
+            if (!(t == DQ_TYPE_STRING || t == DQ_TYPE_BOOLEAN || t == DQ_TYPE_BYTE || t == DQ_TYPE_SHORT ||
+                  t == DQ_TYPE_INT || t == DQ_TYPE_LONG))
+                return fail(ctx, DQ_ERR_UNSUPPORTED, "predicate %d: PatternMatch over this column type is not supported", p);
+            col_used[c] = 1;
+            continue;
+        }
         int depth = 0, maxd = 0;
         for (int k = 0; k < pr.code_len; k += 2) {
             const int op = pr.code[k], arg = pr.code[k + 1];
@@ -309,6 +322,8 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             } else if (op == DQ_P_CONST || op == DQ_P_NULL) {
                 if (op == DQ_P_CONST && (arg < 0 || arg >= pr.n_consts)) return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: bad constant", p);
                 ++depth;
+            } else if (op == DQ_P_REGEX) {
+                return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: REGEX is only supported as [COL, REGEX]", p);
             } else if (op == DQ_P_IN) {
                 depth -= arg;
             } else if (op == DQ_P_COALESCE) {
@@ -659,6 +674,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             pn[p] = (uint64_t*)b.take((size_t)pwords * 8);
         }
         void* pcols = b.take(sizeof(PredColumn) * std::max(ncols, 1));
+        int32_t* rx_status = (int32_t*)b.take(sizeof(int32_t) * std::max(npreds, 1));
         std::vector<void*> pprog(npreds, nullptr), pcode(npreds, nullptr), pconst(npreds, nullptr), pstr(npreds, nullptr);
         for (int p = 0; p < npreds; ++p) {
             if (!pred_used[p]) continue;
@@ -685,7 +701,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             int rc = ensure_arena(ctx, arena_need);
             if (rc) return rc;
             // plan bytes uploaded through pinned staging
-            size_t pin = sizeof(StrSlot) * std::max(nsslots, 1) + sizeof(StrOpMap) * std::max<size_t>(sopmap.size(), 1) +
+            size_t pin = sizeof(int32_t) * std::max(npreds, 1) + 32 + sizeof(StrSlot) * std::max(nsslots, 1) + sizeof(StrOpMap) * std::max<size_t>(sopmap.size(), 1) +
                          sizeof(PredColumn) * std::max(ncols, 1) + sizeof(SlotDesc) * std::max(nslots, 1) +
                          sizeof(OpMap) * nops + sizeof(dq_state) * nops + 4 * (slot_nblocks.size() + hll_nblocks.size() + nslots) + 8192;
             for (int p = 0; p < npreds; ++p)
@@ -707,7 +723,9 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             DQ_HIP(ctx, hipMemcpyAsync(dst, h, n, hipMemcpyHostToDevice, ctx->stream));
             return DQ_OK;
         };
+        bool any_regex = false;
         if (npred_used) {
+            DQ_HIP(ctx, hipMemsetAsync(rx_status, 0, sizeof(int32_t) * std::max(npreds, 1), ctx->stream));
             std::vector<PredColumn> pc(std::max(ncols, 1));
             for (int c = 0; c < ncols; ++c) {
                 memset(&pc[c], 0, sizeof(PredColumn));
@@ -741,7 +759,15 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 pg.n_consts = pr.n_consts;
                 rc = upload(pprog[p], &pg, sizeof(pg));
                 if (rc) return rc;
-                launch_predicate((const PredProgram*)pprog[p], (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p], ctx->stream);
+                if (pr.code_len == 4 && pr.code[2] == DQ_P_REGEX) {
+                    const dq_const& k = pr.consts[pr.code[3]];
+                    launch_regex(pc[pr.code[1]], (const int32_t*)((const uint8_t*)pstr[p] + k.str_offset), nrows, pwords,
+                                 pt[p], pn[p], rx_status + p, ctx->stream);
+                    any_regex = true;
+                } else {
+                    launch_predicate((const PredProgram*)pprog[p], (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p],
+                                     ctx->stream);
+                }
                 DQ_HIP(ctx, hipGetLastError());
             }
         }
@@ -820,6 +846,15 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             if (rc) return rc;
             launch_finalize_strings(dsops, (int)sopmap.size(), spartials, sgrid, gstride, nrows, dout, ctx->stream);
             DQ_HIP(ctx, hipGetLastError());
+        }
+        if (any_regex) {
+            // a row that exhausted the backtracking budget fails the batch (never a silent count)
+            int32_t* hs = (int32_t*)hb.take(sizeof(int32_t) * std::max(npreds, 1), 16);
+            DQ_HIP(ctx, hipMemcpyAsync(hs, rx_status, sizeof(int32_t) * std::max(npreds, 1), hipMemcpyDeviceToHost, ctx->stream));
+            DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            for (int p = 0; p < npreds; ++p)
+                if (pred_used[p] && hs[p])
+                    return fail(ctx, DQ_ERR_UNSUPPORTED, "predicate %d: regex backtracking limit exceeded", p);
         }
         if (!(flags & DQ_SCAN_OUT_DEVICE)) {
             void* h = hb.take(sizeof(dq_state) * nops, 16);

@@ -212,6 +212,8 @@ void launch_string_scan(const StrSlot* slots, int nslots, int64_t nrows, int gri
                         uint8_t* hll_partials, hipStream_t s);
 void launch_finalize_strings(const StrOpMap* ops, int nops, const StrPartial* partials, int nblocks, int gstride,
                              int64_t nrows, dq_state* out, hipStream_t s);
+void launch_regex(const PredColumn& col, const int32_t* image_dev, int64_t nrows, int64_t padded_words,
+                  uint64_t* out_t, uint64_t* out_nn, int32_t* status, hipStream_t s);
 void launch_synth_column(int kind, uint64_t seed, int64_t row0, int64_t nrows, void* out, hipStream_t s);
 void launch_synth_freq_keys(int64_t total, int64_t distinct, int64_t row0, int64_t nrows, int64_t* out, hipStream_t s);
 void launch_synth_validity(uint64_t seed, int64_t row0, int64_t nrows, int permille, uint8_t* out,

@@ -1,0 +1,335 @@
+// regex.hip — PatternMatch on the GPU (gfx950 / CDNA4).
+//
+// PatternMatch (A/PatternMatch.scala:37-55) sums `when(regexp_extract(col, pattern, 0) != "", 1)
+// .otherwise(0)` under `where`: a row matches when the FIRST match of java.util.regex
+// Matcher.find() is non-empty; a NULL value counts 0. The host compiles the pattern
+// (deequ_amd/regex.py) to the program of a backtracking engine with Java's leftmost-first
+// priorities; this kernel runs it with one lane per row (per-lane explicit stack of branch / undo
+// frames in private memory) and emits the predicate bitmaps the scan consumes (TRUE rows, and
+// NOT-NULL = every row: the expression is never NULL). Numbers are matched against their Spark
+// string cast (integral: decimal digits, boolean: "true"/"false").
+//
+// Program image (little-endian int32): header {magic, ninstr, nclasses, nranges, ngroups, nloops,
+// anchored, 0}, ninstr x {op, a, b}, nclasses x {first range, count}, nranges x {lo, hi}.
+#include <hip/hip_runtime.h>
+
+#include "dq_common.h"
+#include "dq_internal.h"
+
+namespace dq {
+
+namespace {
+
+enum RxOp : int32_t {
+    RX_CHAR = 1, RX_CLASS, RX_ANY, RX_SPLIT, RX_JMP, RX_SAVE, RX_ASSERT, RX_BACKREF, RX_LOOK, RX_LOOKEND, RX_MARK,
+    RX_CHECK, RX_MATCH
+};
+enum RxAssert : int32_t { AS_BOL = 0, AS_EOL, AS_WORDB, AS_NWORDB, AS_BEGIN, AS_END, AS_ENDZ };
+enum RxFrame : uint32_t { FR_BRANCH = 0, FR_CAP = 1, FR_LOOP = 2, FR_LOOK = 3 };
+
+constexpr int kRxStack = 512;       // frames per lane
+constexpr int kRxSteps = 1 << 20;   // instruction budget per row
+constexpr int kRxGroups = 10;       // group 0 unused + 9 capturing groups
+constexpr int kRxLoops = 16;
+
+struct RxProg {
+    const int32_t* ins;      // 3 words per instruction
+    const int32_t* classes;  // (first, count) pairs
+    const int32_t* ranges;   // (lo, hi) pairs
+    int32_t ninstr;
+    int32_t anchored;
+};
+
+// One code point at byte i (UTF-8); malformed bytes decode as U+FFFD of length 1.
+__device__ __forceinline__ int32_t decode(const uint8_t* s, int n, int i, int& len) {
+    const uint8_t c = s[i];
+    if (c < 0x80) {
+        len = 1;
+        return c;
+    }
+    const int need = c >= 0xF0 ? 3 : (c >= 0xE0 ? 2 : (c >= 0xC0 ? 1 : -1));
+    if (need < 0 || i + need >= n) {
+        len = 1;
+        return 0xFFFD;
+    }
+    int32_t cp = c & (0x3F >> need);
+    for (int k = 1; k <= need; ++k) {
+        const uint8_t b = s[i + k];
+        if ((b & 0xC0) != 0x80) {
+            len = 1;
+            return 0xFFFD;
+        }
+        cp = (cp << 6) | (b & 0x3F);
+    }
+    len = need + 1;
+    return cp;
+}
+
+// Start of the code point ending at byte i (exclusive), for look-behind of \b.
+__device__ __forceinline__ int32_t decode_prev(const uint8_t* s, int n, int i) {
+    int j = i - 1;
+    while (j > 0 && (s[j] & 0xC0) == 0x80 && i - j < 4) --j;
+    int len;
+    return decode(s, n, j, len);
+}
+
+__device__ __forceinline__ bool is_line_term(int32_t c) {
+    return c == '\n' || c == '\r' || c == 0x85 || c == 0x2028 || c == 0x2029;
+}
+
+// Character.isLetterOrDigit || '_' (Java's \b), exact for ASCII and Latin-1, coarse above.
+__device__ __forceinline__ bool is_word(int32_t c) {
+    if (c < 0x80) return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || c == '_';
+    if (c < 0xC0) return c == 0xAA || c == 0xB5 || c == 0xBA;
+    if (c == 0xD7 || c == 0xF7) return false;
+    if ((c >= 0x2000 && c <= 0x2BFF) || (c >= 0x3000 && c <= 0x303F) || (c >= 0xFE30 && c <= 0xFE4F) ||
+        (c >= 0xFF00 && c <= 0xFF0F) || c >= 0x1F000)
+        return false;
+    return true;
+}
+
+__device__ __forceinline__ bool in_class(const RxProg& p, int k, int32_t c) {
+    const int first = p.classes[2 * k], cnt = p.classes[2 * k + 1];
+    for (int r = 0; r < cnt; ++r) {
+        const int32_t lo = p.ranges[2 * (first + r)], hi = p.ranges[2 * (first + r) + 1];
+        if (c < lo) return false;  // ranges are sorted
+        if (c <= hi) return true;
+    }
+    return false;
+}
+
+// $ without MULTILINE: end of input, or before a final line terminator ("\r\n" counts as one).
+__device__ __forceinline__ bool at_eol(const uint8_t* s, int n, int i) {
+    if (i == n) return true;
+    int len;
+    const int32_t c = decode(s, n, i, len);
+    if (c == '\r' && i + 1 < n && s[i + 1] == '\n') return i + 2 == n;
+    return is_line_term(c) && i + len == n;
+}
+
+__device__ __forceinline__ uint64_t frame(uint32_t kind, uint32_t a, int32_t pos) {
+    return ((uint64_t)((kind << 28) | (a & 0x0FFFFFFFu)) << 32) | (uint32_t)pos;
+}
+
+// Backtracking match of the program anchored at byte `start`: end position, -1 = no match,
+// -2 = resource limit (stack / step budget).
+__device__ int rx_match_at(const RxProg& p, const uint8_t* s, int n, int start, uint64_t* stk) {
+    int32_t caps[2 * kRxGroups];
+    int32_t loops[kRxLoops];
+    for (int k = 0; k < 2 * kRxGroups; ++k) caps[k] = -1;
+    for (int k = 0; k < kRxLoops; ++k) loops[k] = -1;
+    int top = 0, pc = 0, pos = start;
+    for (int steps = 0; steps < kRxSteps; ++steps) {
+        const int op = p.ins[3 * pc], a = p.ins[3 * pc + 1], b = p.ins[3 * pc + 2];
+        bool ok = true;
+        switch (op) {
+            case RX_CHAR: {
+                int len;
+                if (pos < n && decode(s, n, pos, len) == a) { pos += len; ++pc; } else ok = false;
+                break;
+            }
+            case RX_CLASS: {
+                int len;
+                if (pos < n && in_class(p, a, decode(s, n, pos, len))) { pos += len; ++pc; } else ok = false;
+                break;
+            }
+            case RX_ANY: {
+                int len;
+                if (pos < n && !is_line_term(decode(s, n, pos, len))) { pos += len; ++pc; } else ok = false;
+                break;
+            }
+            case RX_SPLIT:
+                if (top >= kRxStack) return -2;
+                stk[top++] = frame(FR_BRANCH, (uint32_t)b, pos);
+                pc = a;
+                break;
+            case RX_JMP: pc = a; break;
+            case RX_SAVE:
+                if (top >= kRxStack) return -2;
+                stk[top++] = frame(FR_CAP, (uint32_t)a, caps[a]);
+                caps[a] = pos;
+                ++pc;
+                break;
+            case RX_ASSERT: {
+                bool r;
+                switch (a) {
+                    case AS_BOL: case AS_BEGIN: r = pos == 0; break;
+                    case AS_EOL: case AS_ENDZ: r = at_eol(s, n, pos); break;
+                    case AS_END: r = pos == n; break;
+                    default: {
+                        int len;
+                        const bool left = pos > 0 && is_word(decode_prev(s, n, pos));
+                        const bool right = pos < n && is_word(decode(s, n, pos, len));
+                        r = (left != right) == (a == AS_WORDB);
+                        break;
+                    }
+                }
+                if (r) ++pc; else ok = false;
+                break;
+            }
+            case RX_BACKREF: {
+                const int g0 = caps[2 * a], g1 = caps[2 * a + 1];
+                if (g0 < 0 || g1 < 0) { ok = false; break; }  // Java: a reference to an unset group fails
+                const int len = g1 - g0;
+                if (pos + len > n) { ok = false; break; }
+                for (int k = 0; k < len && ok; ++k) ok = s[g0 + k] == s[pos + k];
+                if (ok) { pos += len; ++pc; }
+                break;
+            }
+            case RX_LOOK:
+                if (top >= kRxStack) return -2;
+                stk[top++] = frame(FR_LOOK, (uint32_t)(a | (b << 24)), pos);  // b = 1: negative
+                ++pc;
+                break;
+            case RX_LOOKEND: {
+                // The lookahead body matched. Find its LOOK frame, drop the frames above it (for
+                // (?!X) undoing X's captures, as the whole lookahead then fails).
+                int j = top - 1;
+                while (j >= 0 && (uint32_t)(stk[j] >> 60) != FR_LOOK) --j;
+                if (j < 0) return -2;
+                const uint32_t larg = (uint32_t)(stk[j] >> 32) & 0x0FFFFFFFu;
+                const bool neg = (larg >> 24) != 0;
+                for (int k = top - 1; k > j; --k) {
+                    const uint32_t kind = (uint32_t)(stk[k] >> 60), arg = (uint32_t)(stk[k] >> 32) & 0x0FFFFFFFu;
+                    const int32_t fp = (int32_t)(uint32_t)stk[k];
+                    if (kind == FR_CAP && neg) caps[arg] = fp;
+                    if (kind == FR_LOOP) loops[arg] = fp;
+                }
+                const int32_t lpos = (int32_t)(uint32_t)stk[j];
+                top = j;
+                if (neg) ok = false;  // (?!X) and X matched
+                else {                // (?=X): continue after the group at the original position
+                    pos = lpos;
+                    pc = (int)(larg & 0xFFFFFF);
+                }
+                break;
+            }
+            case RX_MARK:
+                if (top >= kRxStack) return -2;
+                stk[top++] = frame(FR_LOOP, (uint32_t)a, loops[a]);
+                loops[a] = pos;
+                ++pc;
+                break;
+            case RX_CHECK:
+                if (pos == loops[a]) ok = false; else ++pc;  // an empty iteration does not repeat
+                break;
+            case RX_MATCH: return pos;
+            default: return -2;
+        }
+        if (ok) continue;
+        // backtrack
+        for (;;) {
+            if (top == 0) return -1;
+            const uint64_t f = stk[--top];
+            const uint32_t kind = (uint32_t)(f >> 60), arg = (uint32_t)(f >> 32) & 0x0FFFFFFFu;
+            const int32_t fp = (int32_t)(uint32_t)f;
+            if (kind == FR_BRANCH) { pc = (int)arg; pos = fp; break; }
+            if (kind == FR_CAP) { caps[arg] = fp; continue; }
+            if (kind == FR_LOOP) { loops[arg] = fp; continue; }
+            // FR_LOOK: the lookahead body failed
+            if (arg >> 24) { pos = fp; pc = (int)(arg & 0xFFFFFF); break; }  // (?!X): succeeds
+        }
+    }
+    return -2;
+}
+
+// Spark's cast of an integral value to its decimal string.
+__device__ int format_long(int64_t v, uint8_t* buf) {
+    uint8_t tmp[20];
+    uint64_t m = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
+    int k = 0;
+    do {
+        tmp[k++] = (uint8_t)('0' + m % 10);
+        m /= 10;
+    } while (m);
+    int n = 0;
+    if (v < 0) buf[n++] = '-';
+    while (k) buf[n++] = tmp[--k];
+    return n;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(256)
+regex_match_kernel(PredColumn col, const int32_t* __restrict__ image, int64_t nrows, int64_t padded_words,
+                   uint64_t* __restrict__ out_t, uint64_t* __restrict__ out_nn, int32_t* __restrict__ status) {
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    RxProg p;
+    p.ninstr = image[1];
+    p.anchored = image[6];
+    p.ins = image + 8;
+    p.classes = p.ins + 3 * p.ninstr;
+    p.ranges = p.classes + 2 * image[2];
+    bool t = false;
+    if (row < nrows) {
+        bool valid = true;
+        if (col.validity) valid = (col.validity[row >> 6] >> (row & 63)) & 1ull;
+        if (valid) {
+            uint8_t buf[24];
+            const uint8_t* s;
+            int n;
+            switch (col.spark_type) {
+                case DQ_TYPE_STRING: {
+                    const int32_t o0 = col.offsets[row], o1 = col.offsets[row + 1];
+                    s = static_cast<const uint8_t*>(col.values) + o0;
+                    n = o1 - o0;
+                    break;
+                }
+                case DQ_TYPE_BOOLEAN: {
+                    const bool b = static_cast<const uint8_t*>(col.values)[row] != 0;
+                    const char* txt = b ? "true" : "false";
+                    n = b ? 4 : 5;
+                    for (int k = 0; k < n; ++k) buf[k] = (uint8_t)txt[k];
+                    s = buf;
+                    break;
+                }
+                default: {
+                    int64_t v;
+                    switch (col.spark_type) {
+                        case DQ_TYPE_BYTE: v = static_cast<const int8_t*>(col.values)[row]; break;
+                        case DQ_TYPE_SHORT: v = static_cast<const int16_t*>(col.values)[row]; break;
+                        case DQ_TYPE_INT: v = static_cast<const int32_t*>(col.values)[row]; break;
+                        default: v = static_cast<const int64_t*>(col.values)[row]; break;
+                    }
+                    n = format_long(v, buf);
+                    s = buf;
+                    break;
+                }
+            }
+            uint64_t stk[kRxStack];
+            // Matcher.find(): the first start position (code point boundaries) with a match
+            for (int start = 0; start <= n;) {
+                const int end = rx_match_at(p, s, n, start, stk);
+                if (end == -2) {
+                    atomicOr(status, 1);
+                    break;
+                }
+                if (end >= 0) {
+                    t = end > start;  // regexp_extract(..., 0) != ""
+                    break;
+                }
+                if (p.anchored || start == n) break;
+                int len;
+                decode(s, n, start, len);
+                start += len;
+            }
+        }
+    }
+    const uint64_t bt = __ballot(t);
+    const uint64_t bn = __ballot(row < nrows);
+    const int64_t w = row >> 6;
+    if ((threadIdx.x & 63) == 0 && w < padded_words) {
+        out_t[w] = bt;
+        out_nn[w] = bn;
+    }
+}
+
+void launch_regex(const PredColumn& col, const int32_t* image_dev, int64_t nrows, int64_t padded_words,
+                  uint64_t* out_t, uint64_t* out_nn, int32_t* status, hipStream_t s) {
+    const int64_t rows = padded_words * 64;
+    const int64_t blocks = (rows + 255) / 256;
+    hipLaunchKernelGGL(regex_match_kernel, dim3((unsigned)blocks), dim3(256), 0, s, col, image_dev, nrows,
+                       padded_words, out_t, out_nn, status);
+}
+
+}  // namespace dq

@@ -105,6 +105,11 @@ class EmptyStateException(MetricCalculationRuntimeException):
     pass
 
 
+class UnsupportedOnDevice(MetricCalculationRuntimeException):
+    """An analyzer configuration this engine does not evaluate on the GPU (e.g. a regex construct
+    outside the supported java.util.regex subset). It fails that analyzer only — never a CPU path."""
+
+
 def wrap_if_necessary(exception):
     """MetricCalculationException.wrapIfNecessary (R/MetricCalculationException.scala:69-76)."""
     if isinstance(exception, MetricCalculationException):

@@ -34,7 +34,7 @@ P_COL, P_CONST, P_NULL = 1, 2, 3
 P_EQ, P_NE, P_LT, P_LE, P_GT, P_GE, P_EQ_NULLSAFE = 10, 11, 12, 13, 14, 15, 16
 P_AND, P_OR, P_NOT, P_IS_NULL, P_IS_NOT_NULL, P_IN, P_COALESCE = 20, 21, 22, 23, 24, 25, 26
 P_ADD, P_SUB, P_MUL, P_DIV, P_MOD, P_NEG = 30, 31, 32, 33, 34, 35
-P_LIKE, P_LENGTH, P_CAST_DOUBLE, P_CAST_LONG = 40, 41, 42, 43
+P_LIKE, P_LENGTH, P_CAST_DOUBLE, P_CAST_LONG, P_CAST_STRING_NUM, P_REGEX = 40, 41, 42, 43, 44, 45
 V_BOOL, V_LONG, V_DOUBLE, V_STRING = 1, 2, 3, 4
 
 SYNTH_DYADIC, SYNTH_UNIFORM, SYNTH_NORMAL, SYNTH_INT32R, SYNTH_KEY30, SYNTH_GAUSS01 = range(1, 7)

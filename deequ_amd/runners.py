@@ -9,7 +9,7 @@ from . import engine
 from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer,
                         FrequencyBasedAnalyzer, Preconditions, Size, computeFrequencies)
 from .expr import compile_predicate
-from .metrics import DoubleMetric, Success
+from .metrics import DoubleMetric, Success, UnsupportedOnDevice
 
 
 class ScanResult(list):
@@ -39,7 +39,25 @@ class ScanBatch:
             self.pred_index[text] = len(self.preds) - 1
         return self.pred_index[text]
 
-    def add_op(self, kind, columns=(), where=None, predicate=None):
+    def regex_predicate(self, column, pattern):
+        """PatternMatch's `regexp_extract(col, pattern, 0) != ""` as the [COL, REGEX] program."""
+        from .expr import CompiledPredicate
+        from .regex import compile_regex
+        key = ("\x00regex", column, pattern)
+        if key not in self.pred_index:
+            if column not in self.col_index:
+                from .metrics import NoSuchColumnException
+                raise NoSuchColumnException("Input data does not include column %s!" % column)
+            image = compile_regex(pattern).to_bytes()
+            k = N.DqConst()
+            k.tag, k.str_len, k.str_offset = N.V_STRING, len(image), 0
+            self.preds.append(CompiledPredicate("regexp_extract(%s, %r, 0) != ''" % (column, pattern),
+                                                [N.P_COL, self.col_index[column], N.P_REGEX, 0], [k], image,
+                                                [column]))
+            self.pred_index[key] = len(self.preds) - 1
+        return self.pred_index[key]
+
+    def add_op(self, kind, columns=(), where=None, predicate=None, predicate_index=None):
         cols = [self.col_index[c] if c in self.col_index else -1 for c in columns]
         for c, name in zip(cols, columns):
             if c < 0:
@@ -47,6 +65,8 @@ class ScanBatch:
                 raise NoSuchColumnException("Input data does not include column %s!" % name)
         w = self.predicate(where) if where is not None else -1
         p = self.predicate(predicate) if predicate is not None else -1
+        if predicate_index is not None:
+            p = predicate_index
         key = (kind, tuple(cols), w, p)
         if key not in self.op_index:
             op = N.DqOp()
@@ -234,9 +254,17 @@ class AnalysisRunner:
         if shareable:
             try:
                 batch = ScanBatch(data)
-                offsets = [a.addOps(batch) for a in shareable]
+                offsets = []
+                for a in shareable:
+                    try:
+                        offsets.append(a.addOps(batch))
+                    except UnsupportedOnDevice as e:  # this engine's limitation: only this analyzer fails
+                        offsets.append(None)
+                        results[a] = a.toFailureMetric(e)
                 states = batch.run()
                 for a, ops in zip(shareable, offsets):
+                    if ops is None:
+                        continue
                     try:
                         results[a] = a.metricFromAggregationResult(states, ops, aggregateWith, saveStatesTo)
                     except Exception as e:  # successOrFailureMetricFrom (:340-353)

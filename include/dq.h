@@ -92,7 +92,13 @@ typedef enum dq_pred_opcode {
     DQ_P_ADD = 30, DQ_P_SUB = 31, DQ_P_MUL = 32, DQ_P_DIV = 33, DQ_P_MOD = 34, DQ_P_NEG = 35,
     DQ_P_LIKE = 40,      /* arg: constant index of the pattern; 1 operand                      */
     DQ_P_LENGTH = 41,    /* UTF-8 character count                                             */
-    DQ_P_CAST_DOUBLE = 42, DQ_P_CAST_LONG = 43, DQ_P_CAST_STRING_NUM = 44
+    DQ_P_CAST_DOUBLE = 42, DQ_P_CAST_LONG = 43, DQ_P_CAST_STRING_NUM = 44,
+    /* PatternMatch (A/PatternMatch.scala:46-48): arg = index of a STRING constant holding a compiled
+     * java.util.regex program (deequ_amd/regex.py image, 4-byte aligned in the pool); 1 operand.
+     * TRUE when the first Matcher.find() match of the value's string form is non-empty, FALSE
+     * otherwise, also for NULL (`when(regexp_extract(..) != "", 1).otherwise(0)`). Only as the whole
+     * program [COL c, REGEX k], over STRING / integral / BOOLEAN columns. */
+    DQ_P_REGEX = 45
 } dq_pred_opcode;
 
 typedef enum dq_value_tag { DQ_V_BOOL = 1, DQ_V_LONG = 2, DQ_V_DOUBLE = 3, DQ_V_STRING = 4 } dq_value_tag;

@@ -360,6 +360,25 @@ def expected_state(table, analyzer, exact=True):
         words = np.zeros(52, dtype=np.int64)
         lib().oracle_hll_pack(regs.ctypes.data, words.ctypes.data)
         return S.ApproxCountDistinctState([int(w) for w in words])
+    if name == "PatternMatch":
+        # sum(when(regexp_extract(col, p, 0) != "", 1).otherwise(0)) under where (A/PatternMatch.scala:46-48):
+        # Python's `re` is, like java.util.regex, a leftmost-first backtracking engine; re.ASCII gives
+        # Java's default \d \s \w classes (Java's Unicode \b, `.` and `$` line terminators differ
+        # only on non-ASCII word characters / \r, \u0085, \u2028, \u2029, absent from the tests).
+        import re
+        c = table[analyzer.column]
+        rx = re.compile(java_regex_to_python(analyzer.pattern), re.ASCII)
+        wt, _ = _where(table, analyzer.where)
+        valid = _valid(c)
+        cnt, present = _cond_count(table, analyzer.where)
+        hits = 0
+        for i in range(c.length):
+            if wt[i] and valid[i]:
+                m = rx.search(spark_cast_to_string(c, i))
+                hits += 1 if (m is not None and m.group(0) != "") else 0
+        if not wt.any() or not present:
+            return None
+        return S.NumMatchesAndCount(hits, cnt)
     if name in ("MinLength", "MaxLength"):
         # min/max(length(when(where, col))): Spark's length = characters (A/MinLength.scala:28-30)
         c = table[analyzer.column]
@@ -383,6 +402,21 @@ def expected_state(table, analyzer, exact=True):
             counts[datatype_class(spark_cast_to_string(c, i))] += 1
         return S.DataTypeHistogram(*counts)
     raise ValueError("no oracle for %s" % name)
+
+
+def java_regex_to_python(p):
+    r"""The two java.util.regex anchors Python spells differently: \z (end of input) -> \Z and
+    \Z (end, or before a final line terminator) -> (?=\n?\Z)."""
+    out, i = [], 0
+    while i < len(p):
+        if p[i] == "\\" and i + 1 < len(p):
+            nxt = p[i + 1]
+            out.append("\\Z" if nxt == "z" else ("(?=\\n?\\Z)" if nxt == "Z" else p[i:i + 2]))
+            i += 2
+        else:
+            out.append(p[i])
+            i += 1
+    return "".join(out)
 
 
 # StatefulDataType's regexes (C/StatefulDataType.scala:36-38), ASCII \d as in java.util.regex

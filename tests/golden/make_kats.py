@@ -70,6 +70,23 @@ FIXTURES = {
     "dfBoolean": {"names": ["item", "att1"], "types": [S, S], "rows": [["1", "true"], ["2", "false"]]},
     "dfBooleanAndNull": {"names": ["item", "att1"], "types": [S, S], "rows": [
         ["1", "true"], ["2", "false"], ["3", None], ["4", "2.0"]]},
+    # T/analyzers/AnalyzerTests.scala:662-760 (dataFrameWithColumn("some", ...))
+    "dfPatternDoubles": {"names": ["some"], "types": [D], "rows": [[1.1], [None], [3.2], [4.4]]},
+    "dfPatternInts": {"names": ["some"], "types": [S], "rows": [["1"], ["a"]]},
+    "dfPatternEmail": {"names": ["some"], "types": [S], "rows": [["someone@somewhere.org"], ["someone@else"]]},
+    "dfPatternCreditCard": {"names": ["some"], "types": [S], "rows": [[x] for x in [
+        "378282246310005", "6011111111111117", "6011 1111 1111 1117", "6011-1111-1111-1117", "5555555555554444",
+        "5555 5555 5555 4444", "5555-5555-5555-4444", "4111111111111111", "4111 1111 1111 1111",
+        "4111-1111-1111-1111", "0000111122223333", "000011112222333", "00001111222233"]]},
+    "dfPatternURL": {"names": ["some"], "types": [S], "rows": [[x] for x in [
+        "http://foo.com/blah_blah", "http://foo.com/blah_blah_(wikipedia)",
+        "http://foo.bar/?q=Test%20URL-encoded%20stuff", "http://\u27a1.ws/\u4a39", "http://\u2318.ws/",
+        "http://\u263a.damowmow.com/", "http://\u4f8b\u5b50.\u6d4b\u8bd5", "https://foo_bar.example.com/",
+        "http://userid@example.com:8080", "http://foo.com/blah_(wikipedia)#cite-1", "http://../", "h://test",
+        "http://.www.foo.bar/"]]},
+    "dfPatternSSN": {"names": ["some"], "types": [S], "rows": [[x] for x in [
+        "111-05-1130", "111051130", "111-05-000", "111-00-000", "000-05-1130", "666-05-1130", "900-05-1130",
+        "999-05-1130"]]},
     # T/analyzers/AnalyzerTests.scala:568-601: sparkContext.range(-1000L, 1000L).toDF("att1")
     "dfRange": {"names": ["att1"], "types": [L], "rows": [[i] for i in range(-1000, 1000)]},
 }
@@ -189,6 +206,15 @@ KATS = [
      "T/analyzers/AnalyzerTests.scala:530-535"),
     ("dfWithNumericValues", ["MaxLength", "att1"], {"failure": "WrongColumnTypeException"},
      "T/analyzers/AnalyzerTests.scala:537-540"),
+    # :662-760 PatternMatch (Patterns = A/PatternMatch.scala:57-72)
+    ("dfPatternDoubles", ["PatternMatch", "some", "\\d\\.\\d"], 0.75, "T/analyzers/AnalyzerTests.scala:665-669"),
+    ("dfPatternInts", ["PatternMatch", "some", "\\d"], 0.5, "T/analyzers/AnalyzerTests.scala:671-674"),
+    ("dfPatternEmail", ["PatternMatch", "some", "@EMAIL"], 0.5, "T/analyzers/AnalyzerTests.scala:676-680"),
+    ("dfPatternCreditCard", ["PatternMatch", "some", "@CREDITCARD"], 10.0 / 13.0,
+     "T/analyzers/AnalyzerTests.scala:682-707"),
+    ("dfPatternURL", ["PatternMatch", "some", "@URL"], 10.0 / 13.0, "T/analyzers/AnalyzerTests.scala:709-736"),
+    ("dfPatternSSN", ["PatternMatch", "some", "@SOCIAL_SECURITY_NUMBER_US"], 2.0 / 8.0,
+     "T/analyzers/AnalyzerTests.scala:738-754"),
     # :568-601 ApproxQuantile (bounds only: the reference pins no digest values)
     ("dfRange", ["ApproxQuantile", "att1", 0.5], {"between": [-20, 20]}, "T/analyzers/AnalyzerTests.scala:568-579"),
     ("dfRange", ["ApproxQuantile", "att1", 0.25], {"between": [-520, -480]},

@@ -21,6 +21,11 @@ def analyzer_from_spec(spec):
         return cls(args[0], args[1], args[2] if len(args) > 2 else None)
     if name == "Correlation":
         return cls(args[0], args[1], args[2] if len(args) > 2 else None)
+    if name == "PatternMatch":
+        pat = args[1]
+        if pat.startswith("@"):
+            pat = getattr(D.Patterns, pat[1:])
+        return cls(args[0], pat, args[2] if len(args) > 2 else None)
     if name == "Size":
         return cls(args[0] if args else None)
     return cls(*args)

@@ -1,0 +1,86 @@
+"""GPU parity of PatternMatch (regex.hip backtracking engine over programs from deequ_amd/regex.py)
+against the oracle (Python's `re`, also a leftmost-first backtracking engine, with re.ASCII for
+Java's default classes). Bar: exact match counts. Inputs are ASCII without \\r so that the two
+engines' documented differences (Unicode \\b, Java's extra line terminators) do not apply."""
+import numpy as np
+import pytest
+
+import deequ_amd as D
+from deequ_amd.table import Table, Column, _column_from_pylist
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+PATTERNS = [
+    r"\d", r"\d\.\d", r"^a.*z$", r"(a|ab)(c|bcd)(d*)", r"a*?b", r"(\w)\1", r"foo(?!bar)", r"(?=.*\d)[a-z]+",
+    r"\d{2,4}-\d{2}", r"x*", r"\bfoo\b", r"o$", r"<.+?>", r"[^\s/$.?#].[^\s]*", r"(ab|a)*c", r"(?:a|b)+?c",
+    r"^$", r"\W+", r"[A-Z][a-z]{2,}\s", r"(\d+)-\1", r"q(?=u)", r"\Bo", r"(a*)*b", r"\A\d+\z",
+    D.Patterns.EMAIL, D.Patterns.URL, D.Patterns.SOCIAL_SECURITY_NUMBER_US, D.Patterns.CREDITCARD,
+]
+
+WORDS = ["foo", "bar", "foobar", "foo bar", "a1", "abz", "az", "abcd", "abd", "aab", "11-11", "123-45",
+         "1234-56", "xx", "", "<a><b>", "http://x.com/a b", "someone@somewhere.org", "someone@else", "o\n",
+         "Hello world", "12-12", "quit", "qa", "aaab", "ccc", "4111 1111 1111 1111", "6011-1111-1111-1117",
+         "378282246310005", "111-05-1130", "666-05-1130", "abbbc", "aaa", "b", "1.5", "x.y", "Zed ", "abcab"]
+
+
+def random_strings(rng, n):
+    chars = list("abcfoqruxz0123456789 -./@<>:#?\n") + ["AB", "foo", "bar"]
+    out = []
+    for _ in range(n):
+        if rng.random() < 0.4:
+            out.append(WORDS[rng.integers(len(WORDS))])
+        else:
+            out.append("".join(chars[j] for j in rng.integers(0, len(chars), int(rng.integers(0, 25)))))
+    return out
+
+
+def states(t, analyzers):
+    batch = D.ScanBatch(t)
+    offs = [a.addOps(batch) for a in analyzers]
+    res = batch.run()
+    return [a.fromAggregationResult(res, o) for a, o in zip(analyzers, offs)]
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_patterns_match_python_re(device):
+    rng = np.random.default_rng(11)
+    n = 6000
+    items = [None if rng.random() < 0.05 else s for s in random_strings(rng, n)]
+    k = [int(x) for x in rng.integers(0, 5, n)]
+    t = Table([_column_from_pylist("s", "string", items), _column_from_pylist("k", "int", k)])
+    if device:
+        t.to_device(0)
+    analyzers = [D.PatternMatch("s", p) for p in PATTERNS] + [D.PatternMatch("s", r"\d", where="k < 2")]
+    got = states(t, analyzers)
+    for a, g in zip(analyzers, got):
+        exp = O.expected_state(t, a)
+        assert g == exp, (a.pattern, g, exp)
+
+
+def test_pattern_match_over_integral_and_boolean_columns():
+    rng = np.random.default_rng(5)
+    vals = rng.integers(-2000, 2000, 5000).astype(np.int64)
+    vals[:3] = [np.iinfo(np.int64).min, np.iinfo(np.int64).max, 0]
+    t = Table([Column("i", "long", vals), Column("j", "int", vals.astype(np.int32)),
+               Column("b", "boolean", (vals > 0).astype(np.uint8))])
+    analyzers = [D.PatternMatch("i", r"^-?\d{3}$"), D.PatternMatch("j", r"9"), D.PatternMatch("b", r"^t"),
+                 D.PatternMatch("i", r"808$")]
+    got = states(t, analyzers)
+    for a, g in zip(analyzers, got):
+        assert g == O.expected_state(t, a), a
+
+
+def test_unsupported_construct_fails_only_that_analyzer():
+    t = Table([_column_from_pylist("s", "string", ["a", "b", None])])
+    bad = D.PatternMatch("s", r"(?i)a")
+    ctx = D.AnalysisRunner.onData(t).addAnalyzers([bad, D.Completeness("s"), D.PatternMatch("s", "a")]).run()
+    assert ctx.metric(bad).value.isFailure
+    assert ctx.metric(D.Completeness("s")).value.get() == 2.0 / 3.0
+    assert ctx.metric(D.PatternMatch("s", "a")).value.get() == 1.0 / 3.0
+
+
+def test_catastrophic_backtracking_fails_loudly():
+    t = Table([_column_from_pylist("s", "string", ["x" * 40])])
+    m = D.PatternMatch("s", r"(x+x+)+y").calculate(t)
+    assert m.value.isFailure  # budget exhausted: the batch fails instead of miscounting

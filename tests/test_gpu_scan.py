@@ -18,7 +18,7 @@ from helpers import analyzer_from_spec, check_metric, table_from_fixture
 pytestmark = pytest.mark.gpu
 
 SCAN = {"Size", "Completeness", "Compliance", "Mean", "Sum", "Minimum", "Maximum", "StandardDeviation",
-        "Correlation", "ApproxCountDistinct", "MinLength", "MaxLength", "DataType", "ApproxQuantile"}
+        "Correlation", "ApproxCountDistinct", "MinLength", "MaxLength", "DataType", "ApproxQuantile", "PatternMatch"}
 REL = 1e-12
 
 
@@ -31,6 +31,10 @@ def test_scan_kats_one_by_one(kats):
         t = table_from_fixture(kats["fixtures"][k["fixture"]])
         a = analyzer_from_spec(k["analyzer"])
         m = a.calculate(t)
+        if isinstance(a, D.PatternMatch) and t[a.column].spark_type == N.TYPE_DOUBLE:
+            # Java Double.toString is not restated on the GPU: this configuration fails loudly
+            assert m.value.isFailure and type(m.value.failed).__name__ == "UnsupportedOnDevice", m
+            continue
         check_metric(m, k["expected"], rel=1e-15 if k["analyzer"][0] == "StandardDeviation" else 0.0)
 
 
@@ -46,6 +50,8 @@ def test_scan_kats_fused_in_one_run(kats):
             a = analyzer_from_spec(k["analyzer"])
             if isinstance(k["expected"], dict) and k["expected"].get("failure") == "*":
                 continue  # an unresolvable predicate fails the whole batch (R/AnalysisRunner.scala:320-323)
+            if isinstance(a, D.PatternMatch) and t[a.column].spark_type == N.TYPE_DOUBLE:
+                continue
             analyzers.append(a)
             exps.append(k["expected"])
         before = engine.ctx().scan_launch_count()

@@ -12,7 +12,7 @@ import oracle as O
 from helpers import analyzer_from_spec, table_from_fixture
 
 SCAN = {"Size", "Completeness", "Compliance", "Mean", "Sum", "Minimum", "Maximum", "StandardDeviation",
-        "Correlation", "ApproxCountDistinct"}
+        "Correlation", "ApproxCountDistinct", "PatternMatch"}
 GROUPING = {"Uniqueness", "Distinctness", "UniqueValueRatio", "Entropy", "CountDistinct"}
 
 
