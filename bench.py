@@ -149,6 +149,7 @@ def main():
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     gathered = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, device=coll_dev)
     host = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, pin_memory=True)
+    host_np = host.numpy()
     cols = batch.native_columns()
     preds = [p.to_native() for p in batch.preds]
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -166,16 +167,8 @@ def main():
             src = out
         host[:src.numel()].copy_(src, non_blocking=True)
         stream.synchronize()
-        # rank-ordered fold with the reference semigroup merges (State.sum)
-        raw = host.numpy()
-        states = []
-        for op in range(nops):
-            acc = None
-            for r in range(world):
-                s = N.DqState.from_buffer_copy(raw[(r * nops + op) * N.STATE_SIZE:(r * nops + op + 1) * N.STATE_SIZE])
-                acc = s if acc is None else N.merge_states(acc, s)
-            states.append(acc)
-        return states
+        # rank-ordered fold with the reference semigroup merges (State.sum), one C-ABI call
+        return N.fold_states(host_np, world, nops)
 
     for _ in range(args.warmup):
         step()

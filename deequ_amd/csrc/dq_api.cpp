@@ -942,6 +942,23 @@ int dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out) {
     return DQ_OK;
 }
 
+int dq_state_fold(const dq_state* states, int nparts, int nops, dq_state* out) {
+    // Rank-ordered semigroup fold (Analyzers.merge per op, A/Analyzer.scala:367-386) of nparts x nops
+    // records laid out part-major, as an all-gather of per-rank dq_scan outputs delivers them.
+    if ((nparts > 0 && nops > 0 && (!states || !out)) || nparts < 0 || nops < 0) return DQ_ERR_INVALID_ARGUMENT;
+    for (int i = 0; i < nops; ++i) {
+        dq_state acc = states[i];
+        for (int r = 1; r < nparts; ++r) {
+            dq_state next;
+            const int rc = dq_state_merge(&acc, &states[(size_t)r * nops + i], &next);
+            if (rc) return rc;
+            acc = next;
+        }
+        out[i] = acc;
+    }
+    return DQ_OK;
+}
+
 // DeequHyperLogLogPlusPlusUtils.estimateBias (C/StatefulHyperloglogPlus.scala:259-297), P = 9, K = 6.
 static double hll_estimate_bias(double e) {
     const double* est = DQ_HLL_P9_RAW;

@@ -30,17 +30,10 @@ from .runners import AnalyzerContext, ScanBatch
 
 
 def fold_states(raw, world, nops):
-    """Rank-ordered semigroup fold of all-gathered dq_state records (rank-major bytes)."""
+    """Rank-ordered semigroup fold of all-gathered dq_state records (rank-major bytes), in one
+    dq_state_fold call."""
     raw = np.ascontiguousarray(np.asarray(raw, dtype=np.uint8))
-    out = []
-    for op in range(nops):
-        acc = None
-        for r in range(world):
-            off = (r * nops + op) * N.STATE_SIZE
-            s = N.DqState.from_buffer_copy(raw[off:off + N.STATE_SIZE].tobytes())
-            acc = s if acc is None else N.merge_states(acc, s)
-        out.append(acc)
-    return out
+    return N.fold_states(raw, world, nops)
 
 
 def kahan_fold(values):

@@ -44,7 +44,7 @@ HLL_NUM_WORDS = 52
 # Every symbol include/dq.h declares (checked by tests/test_native_abi.py).
 EXPORTED_SYMBOLS = (
     "dq_abi_version", "dq_open", "dq_close", "dq_last_error", "dq_set_stream", "dq_synchronize", "dq_scan",
-    "dq_scan_launch_count", "dq_state_merge", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
+    "dq_scan_launch_count", "dq_state_merge", "dq_state_fold", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
     "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
     "dq_quantile_summary", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity",
@@ -158,6 +158,7 @@ def load_library(path=None):
                                 c_uint32]),
             "dq_scan_launch_count": (c_int64, [c_void_p]),
             "dq_state_merge": (c_int, [c_void_p, c_void_p, c_void_p]),
+            "dq_state_fold": (c_int, [c_void_p, c_int, c_int, c_void_p]),
             "dq_hll_count": (ctypes.c_double, [c_void_p]),
             "dq_spark_hash64": (c_int64, [ctypes.c_int32, c_void_p, c_int64]),
             "dq_frequencies": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_uint32, c_void_p]),
@@ -211,6 +212,18 @@ def merge_states(a, b):
     if rc != DQ_OK:
         raise NativeError(rc, "dq_state_merge")
     return out
+
+
+def fold_states(buf, nparts, nops):
+    """dq_state_fold over a part-major buffer of nparts x nops dq_state records (any object exposing
+    the buffer protocol, e.g. a pinned host tensor's numpy view); returns nops DqState."""
+    lib = load_library()
+    arr = np.frombuffer(buf, dtype=np.uint8, count=nparts * nops * STATE_SIZE)
+    out = (DqState * max(nops, 1))()
+    rc = lib.dq_state_fold(arr.ctypes.data, int(nparts), int(nops), out)
+    if rc != DQ_OK:
+        raise NativeError(rc, "dq_state_fold")
+    return [out[i] for i in range(nops)]
 
 
 class Context:

@@ -220,6 +220,10 @@ int64_t dq_scan_launch_count(const dq_ctx* ctx);
  * also used for the rank-ordered fold after the RCCL all-gather. */
 int dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out);
 
+/* Rank-ordered fold of nparts x nops states (part-major, e.g. an all-gather of per-rank dq_scan outputs):
+ * out[i] = states[0][i] + states[1][i] + ... with dq_state_merge, deterministic for every rank count. */
+int dq_state_fold(const dq_state* states, int nparts, int nops, dq_state* out);
+
 /* DeequHyperLogLogPlusPlusUtils.count (C/StatefulHyperloglogPlus.scala:210-257), including the
  * Java int-shift quirk `1 << Midx` and precision-9 bias correction; returns the rounded estimate. */
 double dq_hll_count(const int64_t words[DQ_HLL_NUM_WORDS]);
