@@ -16,16 +16,31 @@
 //     of every key column, plus the group's smallest row index; a verification pass compares every
 //     row with its group's representative row and the build is redone with a new seed if two
 //     distinct keys ever shared a fingerprint, so results are exact.
-// Capacity comes from a 4096-register HLL estimate of the distinct keys (pass 1); inserts are
-// global 64-bit CAS + 32-bit atomic adds (pass 2). Summaries, radix-select top-N and exports are
-// table scans with per-workgroup partials folded in a fixed order (deterministic).
+// Build = partitioned aggregation, no global atomics on the hot path:
+//   1. extract: a count pass (side counters + a 4096-register HLL estimate of the distinct keys +
+//      per-workgroup counts), then every taking-part row's 64-bit key h (and, general path, its row
+//      index) compacted in row order into an array;
+//   2. the estimate picks b bucket bits so a bucket holds ~1024 distinct keys on average; a
+//      rocPRIM radix sort on b bits of h makes every bucket a contiguous run;
+//   3. one workgroup per bucket (heavy buckets are split into slices) aggregates its run in an LDS
+//      open-addressing table of kRegion slots and stores it as region `bucket` of the global table
+//      (a slice of a split bucket merges its LDS table into the region with global atomics).
+// The table is 2^b regions x kRegion slots; a key lives in region h & (2^b - 1) (its LOW bits: the
+// rocPRIM 4.2 radix sort of ROCm 7.2 returned unsorted output for 64-bit keys with begin_bit > 0 in
+// tools/micro/rp_bits.hip, while [0, b) sorts correctly), probing from its top 11 bits inside it.
+// Summaries, radix-select top-N and exports are table scans with per-workgroup partials folded in a
+// fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <vector>
+
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "dq_common.h"
 #include "dq_internal.h"
@@ -39,6 +54,9 @@ constexpr uint64_t kEmpty = ~0ull;
 constexpr int kSizingRegs = 4096;  // HLL registers used only to size the table
 constexpr int kFreqBlock = 256;
 constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (fixed: deterministic partials)
+constexpr int kRegion = 2048;      // slots per bucket region (the LDS table of one workgroup)
+constexpr int kRegionTarget = 1024;  // distinct keys per bucket the bucket count aims at (load 0.5)
+constexpr int64_t kSliceRows = 1 << 18;  // rows per build work item (larger buckets are split)
 
 struct KeyCol {
     const void* values;
@@ -156,28 +174,7 @@ __device__ bool rows_equal(const KeySpec& ks, int64_t a, int64_t b) {
     return true;
 }
 
-// ---- pass 1: distinct-count estimate for sizing ------------------------------------------------
-__global__ void __launch_bounds__(kFreqBlock)
-sizing_hll_kernel(KeySpec ks, int64_t nrows, unsigned int* __restrict__ regs) {
-    __shared__ unsigned int lds[kSizingRegs];
-    for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock) lds[i] = 0;
-    __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * kFreqBlock;
-    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < nrows; r += stride) {
-        uint64_t h;
-        bool ng;
-        if (!row_key(ks, r, h, ng) || ng) continue;
-        const uint64_t x = xxh_long(h, 7);  // fresh bits for the register index
-        const unsigned int idx = (unsigned int)(x >> 52);
-        const unsigned int rank = (unsigned int)__clzll((long long)((x << 12) | (1ull << 11))) + 1u;
-        if (rank > lds[idx]) atomicMax(&lds[idx], rank);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock)
-        if (lds[i]) atomicMax(&regs[i], lds[i]);
-}
-
-// ---- pass 2: insert ----------------------------------------------------------------------------
+// ---- build counters --------------------------------------------------------------------------------
 struct Counters {
     unsigned long long num_rows;   // rows taking part (numRows)
     unsigned long long sentinel;   // fast path: rows whose mixed key equals kEmpty
@@ -198,81 +195,230 @@ __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v
     return s;
 }
 
-__global__ void __launch_bounds__(kFreqBlock)
-insert_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
-              uint64_t mask, Counters* __restrict__ ctr) {
-    __shared__ unsigned long long red[kFreqBlock / 64];
-    unsigned long long taken = 0, sent = 0, nulls = 0, ovf = 0;
-    const int64_t stride = (int64_t)gridDim.x * kFreqBlock;
-    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < nrows; r += stride) {
-        uint64_t h;
-        bool ng;
-        if (!row_key(ks, r, h, ng)) continue;
-        ++taken;
-        if (ng) { ++nulls; continue; }
-        if (h == kEmpty) { ++sent; continue; }
-        uint64_t pos = h & mask;
-        for (uint64_t probe = 0;; ++probe) {
-            if (probe > 4096 || probe > mask) { ++ovf; break; }
-            Slot* s = slots + pos;
-            unsigned long long k = __hip_atomic_load(&s->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (k == kEmpty) {
-                const unsigned long long prev = atomicCAS(&s->key, kEmpty, (unsigned long long)h);
-                k = prev == kEmpty ? (unsigned long long)h : prev;
-            }
-            if (k == h) {
-                atomicAdd(&s->count, 1u);
-                if (reps) atomicMin(&reps[pos], (unsigned long long)r);
-                break;
-            }
-            pos = (pos + 1) & mask;
-        }
-    }
-    taken = block_sum_u64(taken, red);
-    sent = block_sum_u64(sent, red);
-    nulls = block_sum_u64(nulls, red);
-    ovf = block_sum_u64(ovf, red);
-    if (threadIdx.x == 0) {
-        if (taken) atomicAdd(&ctr->num_rows, taken);
-        if (sent) atomicAdd(&ctr->sentinel, sent);
-        if (nulls) atomicAdd(&ctr->nulls, nulls);
-        if (ovf) atomicAdd(&ctr->overflow, ovf);
-    }
-}
-
 // General path: every row must equal its group's representative row.
 __global__ void __launch_bounds__(kFreqBlock)
 verify_kernel(KeySpec ks, int64_t nrows, const Slot* __restrict__ slots, const unsigned long long* __restrict__ reps,
-              uint64_t mask, Counters* __restrict__ ctr) {
+              int bits, Counters* __restrict__ ctr) {
     __shared__ unsigned long long red[kFreqBlock / 64];
     unsigned long long bad = 0;
     const int64_t stride = (int64_t)gridDim.x * kFreqBlock;
     for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < nrows; r += stride) {
         uint64_t h;
         bool ng;
-        if (!row_key(ks, r, h, ng)) continue;
-        uint64_t pos = h & mask;
-        for (uint64_t probe = 0; probe <= mask; ++probe) {
+        if (!row_key(ks, r, h, ng) || ng || h == kEmpty) continue;
+        const uint64_t base = (h & ((1ull << bits) - 1)) * kRegion;
+        unsigned int p = (unsigned int)(h >> 53) & (kRegion - 1);
+        bool found = false;
+        for (int probe = 0; probe < kRegion; ++probe) {
+            const uint64_t pos = base + p;
             if (slots[pos].key == h) {
                 if (!rows_equal(ks, r, (int64_t)reps[pos])) ++bad;
+                found = true;
                 break;
             }
-            if (slots[pos].key == kEmpty) { ++bad; break; }
-            pos = (pos + 1) & mask;
+            if (slots[pos].key == kEmpty) break;
+            p = (p + 1) & (kRegion - 1);
         }
+        if (!found) ++bad;
     }
     bad = block_sum_u64(bad, red);
     if (threadIdx.x == 0 && bad) atomicAdd(&ctr->mismatch, bad);
 }
 
-__global__ void fill_kernel(Slot* __restrict__ slots, unsigned long long* __restrict__ reps, uint64_t cap) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
-        slots[i].key = kEmpty;
-        slots[i].count = 0;
-        slots[i].pad = 0;
-        if (reps) reps[i] = ~0ull;
+// ---- partitioned build ---------------------------------------------------------------------------
+// Pass 1a (count): over a contiguous chunk of rows per workgroup, the side counters, the sizing HLL
+// and the number of rows whose key goes to the table (per workgroup, for the write offsets).
+__device__ __forceinline__ void chunk_of(int64_t nrows, int64_t& r0, int64_t& r1) {
+    const int64_t per = (nrows + gridDim.x - 1) / gridDim.x;
+    r0 = (int64_t)blockIdx.x * per;
+    r1 = r0 + per < nrows ? r0 + per : nrows;
+    if (r0 > nrows) r0 = nrows;
+}
+
+__global__ void __launch_bounds__(kFreqBlock)
+extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__ block_keep,
+                     unsigned int* __restrict__ regs, Counters* __restrict__ ctr) {
+    __shared__ unsigned int lds[kSizingRegs];
+    __shared__ unsigned long long red[kFreqBlock / 64];
+    for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock) lds[i] = 0;
+    __syncthreads();
+    int64_t r0, r1;
+    chunk_of(nrows, r0, r1);
+    unsigned long long taken = 0, sent = 0, nulls = 0, kept = 0;
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kFreqBlock) {
+        uint64_t h;
+        bool ng;
+        if (!row_key(ks, r, h, ng)) continue;
+        ++taken;
+        if (ng) { ++nulls; continue; }
+        if (h == kEmpty) { ++sent; continue; }
+        ++kept;
+        const uint64_t x = xxh_long(h, 7);  // fresh bits for the sizing register index
+        const unsigned int idx = (unsigned int)(x >> 52);
+        const unsigned int rank = (unsigned int)__clzll((long long)((x << 12) | (1ull << 11))) + 1u;
+        if (rank > lds[idx]) atomicMax(&lds[idx], rank);
     }
+    taken = block_sum_u64(taken, red);
+    sent = block_sum_u64(sent, red);
+    nulls = block_sum_u64(nulls, red);
+    kept = block_sum_u64(kept, red);
+    if (threadIdx.x == 0) {
+        block_keep[blockIdx.x] = kept;
+        if (taken) atomicAdd(&ctr->num_rows, taken);
+        if (sent) atomicAdd(&ctr->sentinel, sent);
+        if (nulls) atomicAdd(&ctr->nulls, nulls);
+    }
+    for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock)
+        if (lds[i]) atomicMax(&regs[i], lds[i]);
+}
+
+// Pass 1b (write): the same chunks again; keys (and row indices) compacted in row order at the
+// workgroup's offset — no shared counter, deterministic layout.
+__global__ void __launch_bounds__(kFreqBlock)
+extract_write_kernel(KeySpec ks, int64_t nrows, const unsigned long long* __restrict__ block_off,
+                     unsigned long long* __restrict__ hs, unsigned long long* __restrict__ rows) {
+    __shared__ unsigned int wave_cnt[kFreqBlock / 64];
+    int64_t r0, r1;
+    chunk_of(nrows, r0, r1);
+    unsigned long long base = block_off[blockIdx.x];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t t0 = r0; t0 < r1; t0 += kFreqBlock) {
+        const int64_t r = t0 + threadIdx.x;
+        uint64_t h = 0;
+        bool ng = false;
+        const bool keep = r < r1 && row_key(ks, r, h, ng) && !ng && h != kEmpty;
+        const unsigned long long bal = __ballot(keep);
+        if (lane == 0) wave_cnt[wave] = (unsigned int)__popcll(bal);
+        __syncthreads();
+        unsigned long long off = base, tile = 0;
+        for (int w = 0; w < kFreqBlock / 64; ++w) {
+            if (w < wave) off += wave_cnt[w];
+            tile += wave_cnt[w];
+        }
+        if (keep) {
+            const unsigned long long at = off + __popcll(bal & ((1ull << lane) - 1ull));
+            hs[at] = h;
+            if (rows) rows[at] = (unsigned long long)r;
+        }
+        base += tile;
+        __syncthreads();
+    }
+}
+
+// bounds[b] = first index of bucket b in the keys sorted on their low `bits` bits.
+__global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ hs, uint64_t n, int bits, uint64_t nbuckets,
+                                     unsigned long long* __restrict__ bounds) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nbuckets) return;
+    if (b == nbuckets) { bounds[b] = n; return; }
+    if (bits == 0) { bounds[b] = 0; return; }
+    const uint64_t mask = nbuckets - 1;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((hs[mid] & mask) < b) lo = mid + 1; else hi = mid;
+    }
+    bounds[b] = lo;
+}
+
+// Probe start of a key inside its region: its top bits (the region is chosen by the low bits).
+__device__ __forceinline__ unsigned int region_probe(uint64_t h) { return (unsigned int)(h >> 53) & (kRegion - 1); }
+
+struct BuildItem {
+    unsigned long long begin, end;  // range of the sorted keys
+    unsigned int bucket;
+    unsigned int split;             // 1: the bucket is split over several items (merge with atomics)
+};
+
+__global__ void region_init_kernel(const BuildItem* __restrict__ items, int nitems, Slot* __restrict__ slots,
+                                   unsigned long long* __restrict__ reps) {
+    const BuildItem it = items[blockIdx.x];
+    if (!it.split) return;
+    Slot* region = slots + (uint64_t)it.bucket * kRegion;
+    for (int i = threadIdx.x; i < kRegion; i += blockDim.x) {
+        region[i].key = kEmpty;
+        region[i].count = 0;
+        region[i].pad = 0;
+        if (reps) reps[(uint64_t)it.bucket * kRegion + i] = ~0ull;
+    }
+}
+
+// One work item per workgroup: aggregate the item's keys in an LDS table, then store (whole bucket)
+// or merge (slice of a split bucket) it into the bucket's region.
+__global__ void __launch_bounds__(kFreqBlock)
+build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
+             const unsigned long long* __restrict__ rows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
+             Counters* __restrict__ ctr) {
+    __shared__ unsigned long long lkey[kRegion];
+    __shared__ unsigned int lcnt[kRegion];
+    __shared__ unsigned long long lrep[kRegion];
+    __shared__ unsigned int lovf;
+    const BuildItem it = items[blockIdx.x];
+    for (int i = threadIdx.x; i < kRegion; i += kFreqBlock) {
+        lkey[i] = kEmpty;
+        lcnt[i] = 0;
+        lrep[i] = ~0ull;
+    }
+    if (threadIdx.x == 0) lovf = 0;
+    __syncthreads();
+    for (unsigned long long j = it.begin + threadIdx.x; j < it.end; j += kFreqBlock) {
+        const unsigned long long h = hs[j];
+        unsigned int p = region_probe(h);
+        bool done = false;
+        for (int probe = 0; probe < kRegion; ++probe) {
+            unsigned long long k = lkey[p];
+            if (k == kEmpty) {
+                const unsigned long long prev = atomicCAS(&lkey[p], kEmpty, h);
+                k = prev == kEmpty ? h : prev;
+            }
+            if (k == h) {
+                atomicAdd(&lcnt[p], 1u);
+                if (rows) atomicMin(&lrep[p], rows[j]);
+                done = true;
+                break;
+            }
+            p = (p + 1) & (kRegion - 1);
+        }
+        if (!done) lovf = 1;
+    }
+    __syncthreads();
+    Slot* region = slots + (uint64_t)it.bucket * kRegion;
+    unsigned long long* rrep = reps ? reps + (uint64_t)it.bucket * kRegion : nullptr;
+    if (!it.split) {
+        for (int i = threadIdx.x; i < kRegion; i += kFreqBlock) {
+            Slot sl;
+            sl.key = lkey[i];
+            sl.count = lcnt[i];
+            sl.pad = 0;
+            region[i] = sl;
+            if (rrep) rrep[i] = lrep[i];
+        }
+    } else {
+        for (int i = threadIdx.x; i < kRegion; i += kFreqBlock) {
+            const unsigned long long h = lkey[i];
+            if (h == kEmpty) continue;
+            unsigned int p = region_probe(h);
+            bool done = false;
+            for (int probe = 0; probe < kRegion; ++probe) {
+                Slot* sl = region + p;
+                unsigned long long k = __hip_atomic_load(&sl->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (k == kEmpty) {
+                    const unsigned long long prev = atomicCAS(&sl->key, kEmpty, h);
+                    k = prev == kEmpty ? h : prev;
+                }
+                if (k == h) {
+                    atomicAdd(&sl->count, lcnt[i]);
+                    if (rrep) atomicMin(&rrep[p], lrep[i]);
+                    done = true;
+                    break;
+                }
+                p = (p + 1) & (kRegion - 1);
+            }
+            if (!done) lovf = 1;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->overflow, 1ull);
 }
 
 // ---- table scans ---------------------------------------------------------------------------------
@@ -434,7 +580,10 @@ struct dq_freq_table {
     Counters* ctr = nullptr;  // device
     Counters host_ctr;
     uint64_t cap = 0;
+    int bits = 0;           // 2^bits bucket regions of kRegion slots
     int fast = 1;
+    int64_t cached_n = -1;  // dq_freq_summarize memo (the table is immutable once built)
+    dq_freq_summary cached;
     void* scratch = nullptr;  // device scratch for scans
     size_t scratch_bytes = 0;
     std::vector<void*> staged;  // host key columns copied to HBM (rows are re-read by verify/export)
@@ -480,6 +629,170 @@ int scan_grid(uint64_t n) {
         hipError_t e_ = (expr);                                                                   \
         if (e_ != hipSuccess) return dq::ctx_fail((ctx), DQ_ERR_DEVICE, hipGetErrorString(e_));   \
     } while (0)
+
+namespace {
+
+struct DevBuf {  // scratch device buffers of one build, released on every path
+    std::vector<void*> ptrs;
+    ~DevBuf() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    hipError_t alloc(void** p, size_t bytes) {
+        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+        if (e == hipSuccess) ptrs.push_back(*p);
+        return e;
+    }
+};
+
+// extract (+ sizing) -> radix sort on `bits` bits of the keys -> per-bucket LDS aggregation.
+// A bucket whose distinct keys overflow its region (or a fingerprint collision on the general
+// path) restarts the sort/build with more bucket bits (or a new seed).
+int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
+    hipStream_t s = dq::ctx_stream(ctx);
+    DevBuf buf;
+    const bool general = !t->fast;
+    for (int seed_attempt = 0; seed_attempt < 4; ++seed_attempt) {
+        unsigned long long *hs = nullptr, *rows = nullptr, *bk = nullptr;
+        unsigned int* regs = nullptr;
+        const size_t n_alloc = (size_t)std::max<int64_t>(nrows, 1);
+        const int xgrid = scan_grid((uint64_t)std::max<int64_t>(nrows, 1));
+        FQ_HIP(ctx, buf.alloc((void**)&hs, n_alloc * 8));
+        if (general) FQ_HIP(ctx, buf.alloc((void**)&rows, n_alloc * 8));
+        FQ_HIP(ctx, buf.alloc((void**)&bk, 2 * sizeof(unsigned long long) * xgrid));
+        FQ_HIP(ctx, buf.alloc((void**)&regs, kSizingRegs * sizeof(unsigned int)));
+        FQ_HIP(ctx, hipMemsetAsync(bk, 0, 2 * sizeof(unsigned long long) * xgrid, s));
+        FQ_HIP(ctx, hipMemsetAsync(regs, 0, kSizingRegs * sizeof(unsigned int), s));
+        FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
+        if (nrows > 0)
+            hipLaunchKernelGGL(extract_count_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows, bk, regs, t->ctr);
+        FQ_HIP(ctx, hipGetLastError());
+        std::vector<unsigned int> hregs(kSizingRegs);
+        std::vector<unsigned long long> hkeep(xgrid), hoff(xgrid);
+        FQ_HIP(ctx, hipMemcpyAsync(hregs.data(), regs, kSizingRegs * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+        FQ_HIP(ctx, hipMemcpyAsync(hkeep.data(), bk, sizeof(unsigned long long) * xgrid, hipMemcpyDeviceToHost, s));
+        FQ_HIP(ctx, hipStreamSynchronize(s));
+        unsigned long long n = 0;
+        for (int g = 0; g < xgrid; ++g) {
+            hoff[g] = n;
+            n += hkeep[g];
+        }
+        if (nrows > 0) {
+            FQ_HIP(ctx, hipMemcpyAsync(bk + xgrid, hoff.data(), sizeof(unsigned long long) * xgrid, hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(extract_write_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
+                               (const unsigned long long*)(bk + xgrid), hs, rows);
+            FQ_HIP(ctx, hipGetLastError());
+        }
+        const double est = n ? hll_raw_estimate(hregs) : 0.0;
+        int bits = 0;
+        while (bits < 40 && est / (double)(1ull << bits) > (double)kRegionTarget) ++bits;
+        unsigned long long *hs2 = nullptr, *rows2 = nullptr;
+        FQ_HIP(ctx, buf.alloc((void**)&hs2, n_alloc * 8));
+        if (general) FQ_HIP(ctx, buf.alloc((void**)&rows2, n_alloc * 8));
+        bool collision = false;
+        for (int grow = 0; grow < 8; ++grow, ++bits) {
+            // ---- sort on the low `bits` bits: each bucket becomes one contiguous run ----------------
+            const unsigned long long* sorted = hs;
+            const unsigned long long* srows = rows;
+            if (bits > 0 && n > 1) {
+                size_t tmp_bytes = 0;
+                void* tmp = nullptr;
+                if (general) {
+                    FQ_HIP(ctx, rocprim::radix_sort_pairs(nullptr, tmp_bytes, hs, hs2, rows, rows2, (size_t)n, 0u,
+                                                          (unsigned)bits, s));
+                    FQ_HIP(ctx, buf.alloc(&tmp, tmp_bytes));
+                    FQ_HIP(ctx, rocprim::radix_sort_pairs(tmp, tmp_bytes, hs, hs2, rows, rows2, (size_t)n, 0u, (unsigned)bits, s));
+                    srows = rows2;
+                } else {
+                    FQ_HIP(ctx, rocprim::radix_sort_keys(nullptr, tmp_bytes, hs, hs2, (size_t)n, 0u, (unsigned)bits, s));
+                    FQ_HIP(ctx, buf.alloc(&tmp, tmp_bytes));
+                    FQ_HIP(ctx, rocprim::radix_sort_keys(tmp, tmp_bytes, hs, hs2, (size_t)n, 0u, (unsigned)bits, s));
+                }
+                sorted = hs2;
+            }
+            const uint64_t nb = 1ull << bits;
+            unsigned long long* bounds = nullptr;
+            FQ_HIP(ctx, buf.alloc((void**)&bounds, (nb + 1) * 8));
+            hipLaunchKernelGGL(bucket_bounds_kernel, dim3((unsigned)((nb + 1 + 255) / 256)), dim3(256), 0, s, sorted,
+                               (uint64_t)n, bits, nb, bounds);
+            std::vector<unsigned long long> hb(nb + 1);
+            FQ_HIP(ctx, hipMemcpyAsync(hb.data(), bounds, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
+            FQ_HIP(ctx, hipStreamSynchronize(s));
+            if (getenv("DQ_DEBUG_FREQ")) {
+                std::vector<unsigned long long> hk(n);
+                (void)hipMemcpy(hk.data(), sorted, n * 8, hipMemcpyDeviceToHost);
+                uint64_t unsorted = 0, maxb = 0, bad_range = 0;
+                for (uint64_t i = 1; i < n; ++i)
+                    if (bits && (hk[i] & (nb - 1)) < (hk[i - 1] & (nb - 1))) ++unsorted;
+                for (uint64_t bk = 0; bk < nb; ++bk) {
+                    if (hb[bk + 1] < hb[bk]) ++bad_range;
+                    else maxb = std::max<uint64_t>(maxb, hb[bk + 1] - hb[bk]);
+                }
+                fprintf(stderr, "[freq] sort check bits=%d n=%llu unsorted=%llu bad_ranges=%llu max_bucket=%llu\n", bits,
+                        (unsigned long long)n, (unsigned long long)unsorted, (unsigned long long)bad_range,
+                        (unsigned long long)maxb);
+            }
+            std::vector<BuildItem> items;
+            items.reserve(nb);
+            for (uint64_t bk = 0; bk < nb; ++bk) {
+                const unsigned long long b0 = hb[bk], b1 = hb[bk + 1];
+                const unsigned int split = (b1 - b0) > (unsigned long long)kSliceRows ? 1u : 0u;
+                if (!split) {
+                    items.push_back(BuildItem{b0, b1, (unsigned int)bk, 0u});
+                    continue;
+                }
+                for (unsigned long long x = b0; x < b1; x += kSliceRows)
+                    items.push_back(BuildItem{x, std::min<unsigned long long>(b1, x + kSliceRows), (unsigned int)bk, 1u});
+            }
+            // ---- table ---------------------------------------------------------------------------
+            const uint64_t cap = nb * kRegion;
+            if (t->slots) (void)hipFree(t->slots);
+            if (t->reps) (void)hipFree(t->reps);
+            t->slots = nullptr;
+            t->reps = nullptr;
+            if (hipMalloc(&t->slots, cap * sizeof(Slot)) != hipSuccess ||
+                (general && hipMalloc(&t->reps, cap * sizeof(unsigned long long)) != hipSuccess))
+                return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
+            t->cap = cap;
+            t->bits = bits;
+            BuildItem* ditems = nullptr;
+            FQ_HIP(ctx, buf.alloc((void**)&ditems, items.size() * sizeof(BuildItem)));
+            FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), items.size() * sizeof(BuildItem), hipMemcpyHostToDevice, s));
+            const int nitems = (int)items.size();
+            hipLaunchKernelGGL(region_init_kernel, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, nitems, t->slots, t->reps);
+            hipLaunchKernelGGL(build_kernel, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, sorted, srows, t->slots,
+                               t->reps, t->ctr);
+            FQ_HIP(ctx, hipGetLastError());
+            if (general && nrows > 0) {
+                const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
+                hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots, t->reps,
+                                   bits, t->ctr);
+            }
+            FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+            FQ_HIP(ctx, hipStreamSynchronize(s));
+            if (getenv("DQ_DEBUG_FREQ"))
+                fprintf(stderr, "[freq] rows=%lld n=%llu est=%.1f bits=%d items=%zu rows_taken=%llu ovf=%llu mis=%llu\n",
+                        (long long)nrows, n, est, bits, items.size(), t->host_ctr.num_rows, t->host_ctr.overflow,
+                        t->host_ctr.mismatch);
+            if (t->host_ctr.overflow) {  // a bucket held more distinct keys than its region: more buckets
+                Counters c = t->host_ctr;
+                c.overflow = 0;
+                c.mismatch = 0;
+                FQ_HIP(ctx, hipMemcpyAsync(t->ctr, &c, sizeof(Counters), hipMemcpyHostToDevice, s));
+                FQ_HIP(ctx, hipStreamSynchronize(s));  // `c` lives on this stack frame
+                continue;
+            }
+            collision = t->host_ctr.mismatch != 0;
+            break;
+        }
+        if (t->host_ctr.overflow) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
+        if (!collision) return DQ_OK;
+        // 64-bit fingerprint collision on the general path: new seed, rebuild from scratch
+        t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
+    }
+    return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -550,61 +863,13 @@ int dq_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nro
     t->fast = t->ks.fast;
     t->ks.seed = 0x243F6A8885A308D3ULL;
 
-    // pass 1: size the table from an HLL estimate of the distinct keys
-    unsigned int* regs = nullptr;
-    FQ_HIP(ctx, hipMalloc(&regs, kSizingRegs * sizeof(unsigned int)));
-    FQ_HIP(ctx, hipMemsetAsync(regs, 0, kSizingRegs * sizeof(unsigned int), s));
-    if (nrows > 0) hipLaunchKernelGGL(sizing_hll_kernel, dim3(scan_grid((uint64_t)nrows)), dim3(kFreqBlock), 0, s, t->ks, nrows, regs);
-    std::vector<unsigned int> hregs(kSizingRegs);
-    FQ_HIP(ctx, hipMemcpyAsync(hregs.data(), regs, kSizingRegs * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-    FQ_HIP(ctx, hipStreamSynchronize(s));
-    (void)hipFree(regs);
-    const double est = hll_raw_estimate(hregs);
-    uint64_t cap = 1024;
-    while ((double)cap < 2.2 * est && cap < (1ull << 40)) cap <<= 1;
     FQ_HIP(ctx, hipMalloc(&t->ctr, sizeof(Counters)));
-
-    for (int attempt = 0; attempt < 8; ++attempt) {
-        if (t->slots) (void)hipFree(t->slots);
-        if (t->reps) (void)hipFree(t->reps);
-        t->slots = nullptr;
-        t->reps = nullptr;
-        if (hipMalloc(&t->slots, cap * sizeof(Slot)) != hipSuccess ||
-            (!t->fast && hipMalloc(&t->reps, cap * sizeof(unsigned long long)) != hipSuccess)) {
-            cleanup();
-            free_table_buffers(t);
-            delete t;
-            return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
-        }
-        t->cap = cap;
-        FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
-        hipLaunchKernelGGL(fill_kernel, dim3(scan_grid(cap)), dim3(kFreqBlock), 0, s, t->slots, t->reps, cap);
-        if (nrows > 0) {
-            const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
-            hipLaunchKernelGGL(insert_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots, t->reps,
-                               cap - 1, t->ctr);
-            if (!t->fast)
-                hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots,
-                                   t->reps, cap - 1, t->ctr);
-        }
-        FQ_HIP(ctx, hipGetLastError());
-        FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-        FQ_HIP(ctx, hipStreamSynchronize(s));
-        if (t->host_ctr.overflow) {
-            cap <<= 2;
-            continue;
-        }
-        if (t->host_ctr.mismatch) {  // 64-bit fingerprint collision: new seed
-            t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
-            continue;
-        }
-        break;
-    }
-    if (t->host_ctr.overflow || t->host_ctr.mismatch) {
+    int rc = build_table(ctx, t, nrows);
+    if (rc) {
         cleanup();
         free_table_buffers(t);
         delete t;
-        return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
+        return rc;
     }
     t->scratch_bytes = kScanBlocks * (sizeof(SummaryPartial) + 3 * sizeof(unsigned long long)) + 2048 * 8 + 256;
     FQ_HIP(ctx, hipMalloc(&t->scratch, t->scratch_bytes));
@@ -620,6 +885,10 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
     FQ_HIP(ctx, hipSetDevice(t->device));
     hipStream_t s = dq::ctx_stream(ctx);
     const int64_t n = entropy_rows > 0 ? entropy_rows : (int64_t)t->host_ctr.num_rows;
+    if (t->cached_n == n) {  // one table scan serves every analyzer of the grouping
+        *out = t->cached;
+        return DQ_OK;
+    }
     SummaryPartial* parts = (SummaryPartial*)t->scratch;
     hipLaunchKernelGGL(summary_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->cap, (double)n, parts);
     FQ_HIP(ctx, hipGetLastError());
@@ -658,6 +927,9 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
     out->entropy_rows = n;
     out->max_count = (int64_t)maxc;
     out->null_count = (int64_t)t->host_ctr.nulls;
+    dq_freq_table* mt = const_cast<dq_freq_table*>(t);
+    mt->cached = *out;
+    mt->cached_n = n;
     return DQ_OK;
 }
 
