@@ -17,6 +17,8 @@ from .analyzers import (Size, Completeness, Compliance, Mean, Sum, Minimum, Maxi
                         MutualInformation, Histogram, FrequenciesAndNumRows, Preconditions, computeFrequencies)
 from .runners import (AnalysisRunner, AnalysisRunBuilder, AnalyzerContext, Analysis, InMemoryStateProvider,
                       ScanBatch)
+from .checks import (Check, CheckLevel, CheckStatus, ConstraintStatus, ConstrainableDataTypes, VerificationSuite,
+                     VerificationResult)
 from .table import Table, Column
 from . import distributed
 
