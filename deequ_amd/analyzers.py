@@ -129,7 +129,7 @@ class Analyzer:
         for f in self._fields:
             v = getattr(self, f)
             if isinstance(v, list):
-                v = "List(%s)" % ", ".join(v)
+                v = "List(%s)" % ", ".join(_java_double_to_string(x) if isinstance(x, float) else str(x) for x in v)
             elif v is None:
                 v = "None"
             elif f == "where":

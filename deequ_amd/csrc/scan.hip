@@ -661,8 +661,20 @@ __device__ __forceinline__ void hll_update8(uint32_t* regs, const uint64_t (&v)[
         if ((m >> k) & 1u) atomicMax(&regs[packed[k] & 0xffffu], packed[k] >> 16);
 }
 
+// The hash class follows from the storage shape except for mixed-width pairs (P = 8): 8-byte
+// storage is DOUBLE (2) or LONG / TIMESTAMP / DECIMAL (3), 4-byte FLOAT (1) or INT / DATE (0).
+// Resolving it at compile time keeps one hash variant per kernel (instruction-cache footprint).
+template <int P, bool F>
 __device__ __forceinline__ void hll_update(uint32_t* regs, const uint64_t (&v)[8], uint32_t m, int spark_type) {
     if (m == 0u) return;
+    if (P == 2) {
+        hll_update8<F ? 2 : 3>(regs, v, m);
+        return;
+    }
+    if (P == 4) {
+        hll_update8<F ? 1 : 0>(regs, v, m);
+        return;
+    }
     switch (hash_class(spark_type)) {  // wave-uniform
         case 0: hll_update8<0>(regs, v, m); break;
         case 1: hll_update8<1>(regs, v, m); break;
@@ -733,13 +745,13 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
             accumulate(a0, xv, mx, c0.flags);
             if (HEAVY) __builtin_amdgcn_sched_barrier(0);
             if (HEAVY && c0.pred_kind) a0.pt += fused_pred_count<F0>(c0, xv, mx);
-            if (hll0) hll_update(hll_lds[0], xv, mx, c0.spark_type);
+            if (hll0) hll_update<P, F0>(hll_lds[0], xv, mx, c0.spark_type);
             if (NC > 1) {
                 if (HEAVY) __builtin_amdgcn_sched_barrier(0);
                 accumulate(a1, yv, my, c1.flags);
                 if (HEAVY) __builtin_amdgcn_sched_barrier(0);
                 if (HEAVY && c1.pred_kind) a1.pt += fused_pred_count<F1>(c1, yv, my);
-                if (hll1) hll_update(hll_lds[NC - 1], yv, my, c1.spark_type);
+                if (hll1) hll_update<P, F1>(hll_lds[NC - 1], yv, my, c1.spark_type);
                 if (HEAVY) __builtin_amdgcn_sched_barrier(0);
                 accumulate_corr<F0, F1>(cp, xv, yv, mx & my);
             }

@@ -26,7 +26,7 @@ from .analyzers import (ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFr
                         FrequenciesAndNumRows, Preconditions, metricFromFailure)
 from .metrics import (HistogramMetric, Distribution, DistributionValue, Success, Failure, wrap_if_necessary,
                       MetricCalculationRuntimeException)
-from .runners import AnalyzerContext, ScanBatch
+from .runners import AnalyzerContext, ScanBatch, ScanResult
 
 
 def fold_states(raw, world, nops):
@@ -62,6 +62,22 @@ class Exchange:
         out = self.torch.empty(self.world * t.numel(), dtype=self.torch.uint8, device=self.device)
         self.dist.all_gather_into_tensor(out, t.to(self.device), group=self.group)
         return out
+
+    def all_gather_blobs(self, blob):
+        """Variable-size byte strings of every rank, in rank order (sizes first, then padded bytes)."""
+        torch = self.torch
+        n = torch.tensor([len(blob)], dtype=torch.int64, device=self.device)
+        sizes = torch.empty(self.world, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(sizes, n, group=self.group)
+        sizes = [int(v) for v in sizes.cpu().tolist()]
+        width = max(max(sizes), 1)
+        buf = torch.zeros(width, dtype=torch.uint8)
+        if blob:
+            buf[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+        out = torch.empty(self.world * width, dtype=torch.uint8, device=self.device)
+        self.dist.all_gather_into_tensor(out, buf.to(self.device), group=self.group)
+        raw = out.cpu().numpy().tobytes()
+        return [raw[r * width:r * width + sizes[r]] for r in range(self.world)]
 
     def all_reduce_i64(self, values):
         t = self.torch.tensor(values, dtype=self.torch.int64, device=self.device)
@@ -110,14 +126,15 @@ class GpuLocal:
     """Per-rank compute on this process's GPU through libdq.so."""
 
     def scan_states(self, batch):
+        """This shard's dq_state records (device bytes) and its quantile digests."""
         import torch
         nops = len(batch.ops)
         out = torch.empty(max(nops, 1) * N.STATE_SIZE, dtype=torch.uint8, device="cuda")
         torch.cuda.current_stream().synchronize()  # `out` allocated on torch's stream
         ctx = engine.ctx()
-        batch.run(out_device_ptr=out.data_ptr())
+        res = batch.run(out_device_ptr=out.data_ptr())
         ctx.synchronize()  # the scan runs on the context's stream; order it before torch reads `out`
-        return out[:nops * N.STATE_SIZE]
+        return out[:nops * N.STATE_SIZE], list(res.quantiles)
 
     def partition(self, column, world):
         import torch
@@ -218,9 +235,21 @@ class DistributedAnalysisRunner:
             try:
                 batch = ScanBatch(shard)
                 offsets = [a.addOps(batch) for a in shareable]
-                local_states = self.local.scan_states(batch)
+                local_states, local_q = self.local.scan_states(batch)
                 gathered = self.ex.all_gather_bytes(local_states)
-                states = fold_states(gathered.cpu().numpy(), self.ex.world, len(batch.ops))
+                states = ScanResult(fold_states(gathered.cpu().numpy(), self.ex.world, len(batch.ops)))
+                if batch.quantile_reqs:
+                    # ApproxQuantile digests: every rank's PercentileDigest (serialized), merged in rank
+                    # order with QuantileSummaries.merge — as Spark merges per-partition digests
+                    from .quantiles import PercentileDigest
+                    merged = []
+                    for dg in local_q:
+                        acc = None
+                        for blob in self.ex.all_gather_blobs(dg.serialize()):
+                            d = PercentileDigest.deserialize(blob)
+                            acc = d if acc is None else acc.merge(d)
+                        merged.append(acc)
+                    states.quantiles = merged
                 for a, ops in zip(shareable, offsets):
                     try:
                         results[a] = a.metricFromAggregationResult(states, ops)

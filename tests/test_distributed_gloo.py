@@ -61,7 +61,16 @@ class OracleLocal:
             a = op_to_analyzer(batch, op)
             st = O.expected_state(batch.data, a, exact=False)
             raw += bytes(state_to_native(op.kind, st))
-        return torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        digests = []
+        for column, rel in batch.quantile_reqs:  # the runner's digest policy over oracle order statistics
+            from deequ_amd.quantiles import PercentileDigest, DEFAULT_HEAD_SIZE
+            s = O.java_sorted_doubles(batch.data, column)
+            if batch.data.nrows < DEFAULT_HEAD_SIZE:
+                digests.append(PercentileDigest.spark_single_partition(rel, s))
+            else:
+                r = O.summary_ranks(len(s), rel)
+                digests.append(PercentileDigest.from_order_statistics(rel, s[r - 1], r, len(s)))
+        return torch.frombuffer(bytearray(raw or b"\0"), dtype=torch.uint8)[:len(raw)], digests
 
     def partition(self, column, world):
         valid = unpack_validity(column.validity, column.length)
@@ -110,7 +119,8 @@ def analyzers():
             D.StandardDeviation("x"), D.Correlation("x", "y"), D.ApproxCountDistinct("k"),
             D.Compliance("big", "x > 5", "k < 150"), D.Mean("y", "k > 20"),
             D.Uniqueness(["k"]), D.Distinctness(["k"]), D.Entropy("k"), D.CountDistinct(["k"]),
-            D.UniqueValueRatio(["k"]), D.Histogram("d", None, 10), D.Uniqueness(["d"])]
+            D.UniqueValueRatio(["k"]), D.Histogram("d", None, 10), D.Uniqueness(["d"]),
+            D.ApproxQuantile("x", 0.5), D.ApproxQuantile("y", 0.9, 0.05), D.ApproxQuantiles("y", [0.1, 0.5])]
 
 
 def _worker(rank, world, port, q):
@@ -132,6 +142,8 @@ def _worker(rank, world, port, q):
             if isinstance(a, D.Histogram):
                 d = m.value.get()
                 out[repr(a)] = (d.numberOfBins, sorted((k, v.absolute) for k, v in d.values.items()))
+            elif isinstance(a, D.ApproxQuantiles):
+                out[repr(a)] = dict(m.value.get())
             else:
                 out[repr(a)] = m.value.get()
         q.put((rank, out))
@@ -176,6 +188,17 @@ def test_distributed_runner_matches_single_table_oracle(world):
             assert g[0] == len(freq)
             top = sorted(freq.values(), reverse=True)[:10]
             assert sorted((c for _, c in g[1]), reverse=True) == top
+            continue
+        if name in ("ApproxQuantile", "ApproxQuantiles"):
+            # per-rank Spark digests merged in rank order: within the merged summary's rank bound
+            srt = O.java_sorted_doubles(t, a.column)
+            n = len(srt)
+            qs = [a.quantile] if name == "ApproxQuantile" else a.quantiles
+            vals = [g] if name == "ApproxQuantile" else [g[repr(q)] for q in qs]
+            for q, v in zip(qs, vals):
+                lo, hi = O.rank_interval(srt, v)
+                slack = 2 * math.ceil(a.relativeError * n) + world
+                assert lo - slack <= math.ceil(q * n) <= hi + slack, (a, q, v)
             continue
         if name in ("Uniqueness", "Distinctness", "Entropy", "CountDistinct", "UniqueValueRatio"):
             freq, nrows = O.frequencies(t, a.columns)
