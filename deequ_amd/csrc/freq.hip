@@ -27,7 +27,7 @@
 //      (a slice of a split bucket merges its LDS table into the region with global atomics).
 // The table is 2^b regions x kRegion slots; a key lives in region h & (2^b - 1) (its LOW bits: the
 // rocPRIM 4.2 radix sort of ROCm 7.2 returned unsorted output for 64-bit keys with begin_bit > 0 in
-// tools/micro/rp_bits.hip, while [0, b) sorts correctly), probing from its top 11 bits inside it.
+// tools/micro/rp_bits.hip, while [0, b) sorts correctly), probing from its top 12 bits inside it.
 // Summaries, radix-select top-N and exports are table scans with per-workgroup partials folded in a
 // fixed order (deterministic).
 #include <hip/hip_runtime.h>
@@ -54,8 +54,10 @@ constexpr uint64_t kEmpty = ~0ull;
 constexpr int kSizingRegs = 4096;  // HLL registers used only to size the table
 constexpr int kFreqBlock = 256;
 constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (fixed: deterministic partials)
-constexpr int kRegion = 2048;      // slots per bucket region (the LDS table of one workgroup)
-constexpr int kRegionTarget = 1024;  // distinct keys per bucket the bucket count aims at (load 0.5)
+constexpr int kRegion = 4096;      // slots per bucket region (the LDS table of one workgroup)
+// Distinct keys per bucket the bucket count aims at (load <= ~0.63). rocPRIM sorts 8 bits per pass
+// on gfx950, so 1e8 distinct keys take b = 16 (2 passes) rather than 17 (3 passes).
+constexpr int kRegionTarget = 2600;
 constexpr int64_t kSliceRows = 1 << 18;  // rows per build work item (larger buckets are split)
 
 struct KeyCol {
@@ -86,6 +88,9 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
+
+// Probe start of a key inside its region: its top bits (the region is chosen by the low bits).
+__device__ __forceinline__ unsigned int region_probe(uint64_t h) { return (unsigned int)(h >> 52) & (kRegion - 1); }
 
 __device__ __forceinline__ bool is_valid(const KeyCol& c, int64_t r) {
     return c.validity == nullptr || ((c.validity[r >> 3] >> (r & 7)) & 1);
@@ -207,7 +212,7 @@ verify_kernel(KeySpec ks, int64_t nrows, const Slot* __restrict__ slots, const u
         bool ng;
         if (!row_key(ks, r, h, ng) || ng || h == kEmpty) continue;
         const uint64_t base = (h & ((1ull << bits) - 1)) * kRegion;
-        unsigned int p = (unsigned int)(h >> 53) & (kRegion - 1);
+        unsigned int p = region_probe(h);
         bool found = false;
         for (int probe = 0; probe < kRegion; ++probe) {
             const uint64_t pos = base + p;
@@ -253,9 +258,9 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
         if (ng) { ++nulls; continue; }
         if (h == kEmpty) { ++sent; continue; }
         ++kept;
-        const uint64_t x = xxh_long(h, 7);  // fresh bits for the sizing register index
-        const unsigned int idx = (unsigned int)(x >> 52);
-        const unsigned int rank = (unsigned int)__clzll((long long)((x << 12) | (1ull << 11))) + 1u;
+        // h is already a mixed 64-bit key (splitmix64 finalizer / fingerprint): use its bits directly
+        const unsigned int idx = (unsigned int)(h >> 52);
+        const unsigned int rank = (unsigned int)__clzll((long long)((h << 12) | (1ull << 11))) + 1u;
         if (rank > lds[idx]) atomicMax(&lds[idx], rank);
     }
     taken = block_sum_u64(taken, red);
@@ -321,8 +326,6 @@ __global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ hs, 
     bounds[b] = lo;
 }
 
-// Probe start of a key inside its region: its top bits (the region is chosen by the low bits).
-__device__ __forceinline__ unsigned int region_probe(uint64_t h) { return (unsigned int)(h >> 53) & (kRegion - 1); }
 
 struct BuildItem {
     unsigned long long begin, end;  // range of the sorted keys
@@ -344,78 +347,92 @@ __global__ void region_init_kernel(const BuildItem* __restrict__ items, int nite
 }
 
 // One work item per workgroup: aggregate the item's keys in an LDS table, then store (whole bucket)
-// or merge (slice of a split bucket) it into the bucket's region.
-__global__ void __launch_bounds__(kFreqBlock)
+// or merge (slice of a split bucket) it into the bucket's region. Keys are loaded kBuildUnroll at a
+// time per lane (independent global loads in flight), and each probe is a single LDS compare-and-
+// swap EMPTY -> h whose returned value says inserted / found / occupied.
+constexpr int kBuildBlock = 512;
+constexpr int kBuildUnroll = 4;
+
+__device__ __forceinline__ bool lds_insert(unsigned long long* lkey, unsigned int* lcnt, unsigned long long* lrep,
+                                           unsigned long long h, unsigned long long row, bool general) {
+    unsigned int p = region_probe(h);
+    for (int probe = 0; probe < kRegion; ++probe) {
+        const unsigned long long prev = atomicCAS(&lkey[p], kEmpty, h);
+        if (prev == kEmpty || prev == h) {
+            atomicAdd(&lcnt[p], 1u);
+            if (general) atomicMin(&lrep[p], row);
+            return true;
+        }
+        p = (p + 1) & (kRegion - 1);
+    }
+    return false;
+}
+
+template <bool GENERAL>
+__global__ void __launch_bounds__(kBuildBlock)
 build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
              const unsigned long long* __restrict__ rows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
              Counters* __restrict__ ctr) {
     __shared__ unsigned long long lkey[kRegion];
     __shared__ unsigned int lcnt[kRegion];
-    __shared__ unsigned long long lrep[kRegion];
+    __shared__ unsigned long long lrep[GENERAL ? kRegion : 1];
     __shared__ unsigned int lovf;
     const BuildItem it = items[blockIdx.x];
-    for (int i = threadIdx.x; i < kRegion; i += kFreqBlock) {
+    for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
         lkey[i] = kEmpty;
         lcnt[i] = 0;
-        lrep[i] = ~0ull;
+        if (GENERAL) lrep[i] = ~0ull;
     }
     if (threadIdx.x == 0) lovf = 0;
     __syncthreads();
-    for (unsigned long long j = it.begin + threadIdx.x; j < it.end; j += kFreqBlock) {
-        const unsigned long long h = hs[j];
-        unsigned int p = region_probe(h);
-        bool done = false;
-        for (int probe = 0; probe < kRegion; ++probe) {
-            unsigned long long k = lkey[p];
-            if (k == kEmpty) {
-                const unsigned long long prev = atomicCAS(&lkey[p], kEmpty, h);
-                k = prev == kEmpty ? h : prev;
-            }
-            if (k == h) {
-                atomicAdd(&lcnt[p], 1u);
-                if (rows) atomicMin(&lrep[p], rows[j]);
-                done = true;
-                break;
-            }
-            p = (p + 1) & (kRegion - 1);
+    bool ok = true;
+    constexpr unsigned long long kStep = (unsigned long long)kBuildBlock * kBuildUnroll;
+    for (unsigned long long j0 = it.begin + threadIdx.x; j0 < it.end; j0 += kStep) {
+        unsigned long long h[kBuildUnroll], rw[kBuildUnroll];
+#pragma unroll
+        for (int u = 0; u < kBuildUnroll; ++u) {
+            const unsigned long long j = j0 + (unsigned long long)u * kBuildBlock;
+            h[u] = j < it.end ? hs[j] : kEmpty;
+            rw[u] = (GENERAL && j < it.end) ? rows[j] : 0ull;
         }
-        if (!done) lovf = 1;
+#pragma unroll
+        for (int u = 0; u < kBuildUnroll; ++u)
+            if (h[u] != kEmpty) ok &= lds_insert(lkey, lcnt, lrep, h[u], rw[u], GENERAL);
     }
+    if (!ok) lovf = 1;
     __syncthreads();
     Slot* region = slots + (uint64_t)it.bucket * kRegion;
-    unsigned long long* rrep = reps ? reps + (uint64_t)it.bucket * kRegion : nullptr;
+    unsigned long long* rrep = GENERAL ? reps + (uint64_t)it.bucket * kRegion : nullptr;
     if (!it.split) {
-        for (int i = threadIdx.x; i < kRegion; i += kFreqBlock) {
+        for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
             Slot sl;
             sl.key = lkey[i];
             sl.count = lcnt[i];
             sl.pad = 0;
             region[i] = sl;
-            if (rrep) rrep[i] = lrep[i];
+            if (GENERAL) rrep[i] = lrep[i];
         }
     } else {
-        for (int i = threadIdx.x; i < kRegion; i += kFreqBlock) {
+        bool mok = true;
+        for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
             const unsigned long long h = lkey[i];
             if (h == kEmpty) continue;
             unsigned int p = region_probe(h);
             bool done = false;
             for (int probe = 0; probe < kRegion; ++probe) {
                 Slot* sl = region + p;
-                unsigned long long k = __hip_atomic_load(&sl->key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (k == kEmpty) {
-                    const unsigned long long prev = atomicCAS(&sl->key, kEmpty, h);
-                    k = prev == kEmpty ? h : prev;
-                }
-                if (k == h) {
+                const unsigned long long prev = atomicCAS(&sl->key, kEmpty, h);
+                if (prev == kEmpty || prev == h) {
                     atomicAdd(&sl->count, lcnt[i]);
-                    if (rrep) atomicMin(&rrep[p], lrep[i]);
+                    if (GENERAL) atomicMin(&rrep[p], lrep[i]);
                     done = true;
                     break;
                 }
                 p = (p + 1) & (kRegion - 1);
             }
-            if (!done) lovf = 1;
+            mok &= done;
         }
+        if (!mok) lovf = 1;
         __syncthreads();
     }
     if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->overflow, 1ull);
@@ -759,8 +776,12 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
             FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), items.size() * sizeof(BuildItem), hipMemcpyHostToDevice, s));
             const int nitems = (int)items.size();
             hipLaunchKernelGGL(region_init_kernel, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, nitems, t->slots, t->reps);
-            hipLaunchKernelGGL(build_kernel, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, sorted, srows, t->slots,
-                               t->reps, t->ctr);
+            if (general)
+                hipLaunchKernelGGL(build_kernel<true>, dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows,
+                                   t->slots, t->reps, t->ctr);
+            else
+                hipLaunchKernelGGL(build_kernel<false>, dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows,
+                                   t->slots, t->reps, t->ctr);
             FQ_HIP(ctx, hipGetLastError());
             if (general && nrows > 0) {
                 const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
