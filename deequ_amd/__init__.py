@@ -12,10 +12,11 @@ from .states import (NumMatches, NumMatchesAndCount, MeanState, SumState, MinSta
                      ApproxQuantileState, DataTypeHistogram)
 from .analyzers import (Size, Completeness, Compliance, Mean, Sum, Minimum, Maximum, StandardDeviation, Correlation,
                         ApproxCountDistinct, ApproxQuantile, ApproxQuantiles, MinLength, MaxLength, DataType,
-                        PatternMatch, Patterns,
+                        PatternMatch, Patterns, KLLSketch,
                         Uniqueness, Distinctness, UniqueValueRatio, Entropy, CountDistinct,
                         MutualInformation, Histogram, FrequenciesAndNumRows, Preconditions, computeFrequencies)
-from .runners import (AnalysisRunner, AnalysisRunBuilder, AnalyzerContext, Analysis, InMemoryStateProvider,
+from .kll import (KLLParameters, KLLState, KLLMetric, BucketDistribution, BucketValue, QuantileNonSample)
+from .runners import (AnalysisRunner, KLLRunner, AnalysisRunBuilder, AnalyzerContext, Analysis, InMemoryStateProvider,
                       ScanBatch)
 from .checks import (Check, CheckLevel, CheckStatus, ConstraintStatus, ConstrainableDataTypes, VerificationSuite,
                      VerificationResult)

@@ -531,6 +531,54 @@ class ApproxQuantiles(ScanShareableAnalyzer):
         return KeyedDoubleMetric(Entity.Column, "ApproxQuantiles", self.column, Failure(wrap_if_necessary(exception)))
 
 
+class KLLSketch(ScanShareableAnalyzer):
+    """A/KLLSketch.scala:82-176. AnalysisRunner routes it to KLLRunner (one extra pass per column,
+    deequ_amd/runners.py); the sketching itself is dq_kll_sketch on the GPU. No `where` (commented out in
+    the reference)."""
+    _fields = ("column", "kllParameters")
+
+    def __init__(self, column, kllParameters=None):
+        from .kll import DEFAULT_SKETCH_SIZE, DEFAULT_SHRINKING_FACTOR, MAXIMUM_ALLOWED_DETAIL_BINS
+        self.column, self.kllParameters = column, kllParameters
+        self.sketchSize = DEFAULT_SKETCH_SIZE
+        self.shrinkingFactor = DEFAULT_SHRINKING_FACTOR
+        self.numberOfBuckets = MAXIMUM_ALLOWED_DETAIL_BINS
+        if kllParameters is not None:
+            self.sketchSize = kllParameters.sketchSize
+            self.shrinkingFactor = kllParameters.shrinkingFactor
+            self.numberOfBuckets = kllParameters.numberOfBuckets
+
+    def __repr__(self):
+        p = "None" if self.kllParameters is None else "Some(%r)" % (self.kllParameters,)
+        return "KLLSketch(%s,%s)" % (self.column, p)
+
+    def preconditions(self):
+        from .kll import MAXIMUM_ALLOWED_DETAIL_BINS
+
+        def param_check(_):
+            if self.numberOfBuckets > MAXIMUM_ALLOWED_DETAIL_BINS:
+                raise IllegalAnalyzerParameterException(
+                    "Cannot return KLL Sketch related values for more than %d values" % MAXIMUM_ALLOWED_DETAIL_BINS)
+        return [param_check, Preconditions.hasColumn(self.column), Preconditions.isNumeric(self.column)]
+
+    def computeStateFrom(self, data):
+        from .runners import KLLRunner
+        return KLLRunner.sketch_column(data, self.column, self.sketchSize, self.shrinkingFactor)
+
+    def computeMetricFrom(self, state):
+        from .kll import KLLMetric, bucket_distribution
+        if state is None:
+            return KLLMetric(self.column, Failure(emptyStateException(self)))
+        try:
+            return KLLMetric(self.column, Success(bucket_distribution(state, self.numberOfBuckets)))
+        except Exception as e:
+            return KLLMetric(self.column, Failure(e))
+
+    def toFailureMetric(self, exception):
+        from .kll import KLLMetric
+        return KLLMetric(self.column, Failure(wrap_if_necessary(exception)))
+
+
 # ---- grouping analyzers (A/GroupingAnalyzers.scala) ----------------------------------------------
 class FrequenciesAndNumRows:
     """A/GroupingAnalyzers.scala:123-156. `frequencies` is a device (key -> count) table produced by

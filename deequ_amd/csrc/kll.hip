@@ -1,0 +1,479 @@
+// kll.hip — KLLSketch (deequ's deterministic KLL, QuantileNonSample) on gfx950 / CDNA4.
+//
+// Replaces the per-row `sketch.updateUntyped(row.get(index))` loop of KLLRunner.sketchPartitions
+// (R/KLLRunner.scala:148-179) for one partition whose non-NULL values arrive in row order, and
+// produces the KLLState bytes the reference reads (A/KLLSketch.scala:56-66: min, max, then the
+// KLLSketchSerializer layout, A/catalyst/KLLSketchSerializer.scala:60-80), bit for bit.
+//
+// Why this parallelises: QuantileNonSample.update / condense (A/QuantileNonSample.scala:80-121)
+// decide WHEN and WHICH level compacts from buffer LENGTHS only, never from values, and the
+// compactor offset flips on a count-only rule (A/NonSampleCompactor.scala:40-47; the Random offset
+// is commented out in the reference). So the whole compaction schedule is a function of n:
+//   1. the host replays the count automaton event by event (one event per compaction, ~n/1000),
+//      recording for every level h the compactions as (start, L, offset) over that level's
+//      arrival stream: a compaction sorts the first L = items - items%2 buffered items (an odd
+//      leftover is the newest arrival and stays), keeps every other one from `offset`, and appends
+//      them to level h+1's stream. Consecutive compactions of a level therefore sort consecutive,
+//      non-overlapping ranges of its stream;
+//   2. the GPU runs one launch per level: one workgroup per compaction sorts its range in LDS
+//      (bitonic network over java.lang.Double.compare order keys — Scala's `.sorted` with
+//      Ordering.Double) and writes the alternate picks into the next level's stream at the
+//      position the schedule assigned. All compactions of a level are independent;
+//   3. what no compaction consumed is each level's final buffer, copied back in arrival order.
+// min/max (UntypedQuantileNonSample.updateUntyped, math.min/max from Int.MaxValue/Int.MinValue) come
+// from each level-0 range's sorted ends (+ the final level-0 buffer on the host).
+//
+// Work: level 0 reads 8 B and writes 4 B per value; each level above handles about half of the
+// previous one's items — ~2n sorted items and ~24 B of HBM traffic per value in total.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "dq_common.h"
+#include "dq_internal.h"
+
+namespace dq {
+
+constexpr int kKllBlock = 256;
+constexpr int kKllMaxPad = 16384;  // 128 KiB of LDS keys: the largest compaction handled
+constexpr int kKllStageBlock = 256;
+constexpr int kKllStageRows = 2048;  // rows per workgroup tile of the NULL-compaction pass
+
+__device__ __forceinline__ uint64_t kll_key(double d) {
+    uint64_t u = d != d ? 0x7ff8000000000000ULL : (uint64_t)__double_as_longlong(d);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double kll_value(uint64_t k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffULL) : ~k));
+}
+
+struct KllColumn {
+    const void* values;
+    const uint64_t* validity;
+    int32_t elem;
+};
+
+__device__ __forceinline__ double kll_load(const KllColumn& c, int64_t r) {
+    switch (c.elem) {
+        case ET_F64: return static_cast<const double*>(c.values)[r];
+        case ET_F32: return (double)static_cast<const float*>(c.values)[r];
+        case ET_I64: return (double)static_cast<const int64_t*>(c.values)[r];
+        case ET_I32: return (double)static_cast<const int32_t*>(c.values)[r];
+        case ET_I16: return (double)static_cast<const int16_t*>(c.values)[r];
+        default: return (double)static_cast<const int8_t*>(c.values)[r];
+    }
+}
+
+__device__ __forceinline__ bool kll_valid(const KllColumn& c, int64_t r) {
+    return c.validity == nullptr || ((c.validity[r >> 6] >> (r & 63)) & 1ull);
+}
+
+// NULL compaction, pass 1: non-NULL rows per 2048-row tile.
+__global__ void __launch_bounds__(kKllStageBlock)
+kll_count_kernel(KllColumn c, int64_t nrows, unsigned int* __restrict__ tile_counts) {
+    __shared__ unsigned int red[kKllStageBlock / 64];
+    const int64_t t = blockIdx.x;
+    const int64_t r0 = t * kKllStageRows;
+    unsigned int cnt = 0;
+    for (int64_t r = r0 + threadIdx.x; r < r0 + kKllStageRows && r < nrows; r += kKllStageBlock) cnt += kll_valid(c, r);
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned int s = 0;
+        for (int w = 0; w < kKllStageBlock / 64; ++w) s += red[w];
+        tile_counts[t] = s;
+    }
+}
+
+// NULL compaction, pass 2: non-NULL values as doubles, in row order, from each tile's offset.
+__global__ void __launch_bounds__(kKllStageBlock)
+kll_write_kernel(KllColumn c, int64_t nrows, const unsigned long long* __restrict__ tile_offsets,
+                 double* __restrict__ out) {
+    __shared__ unsigned int wsum[kKllStageBlock / 64];
+    const int64_t r0 = (int64_t)blockIdx.x * kKllStageRows;
+    unsigned long long base = tile_offsets[blockIdx.x];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t rb = r0; rb < r0 + kKllStageRows && rb < nrows; rb += kKllStageBlock) {
+        const int64_t r = rb + threadIdx.x;
+        const bool v = r < nrows && kll_valid(c, r);
+        const unsigned long long ball = __ballot(v);
+        const unsigned int before = (unsigned int)__popcll(ball & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = (unsigned int)__popcll(ball);
+        __syncthreads();
+        unsigned int wbase = 0, total = 0;
+        for (int w = 0; w < kKllStageBlock / 64; ++w) {
+            if (w < wave) wbase += wsum[w];
+            total += wsum[w];
+        }
+        if (v) out[base + wbase + before] = kll_load(c, r);
+        base += total;
+        __syncthreads();
+    }
+}
+
+struct KllSeg {
+    unsigned long long start;   // first item of the compacted range in this level's stream
+    unsigned long long outpos;  // first slot of its picks in the next level's stream
+    unsigned int len;           // L (even)
+    unsigned int offset;        // NonSampleCompactor.offset at this compaction
+};
+
+// One workgroup per compaction of one level: sort the range in LDS, keep every other item.
+// Level 0 also folds the range's sorted ends into the running min / max keys.
+template <int PAD>
+__global__ void __launch_bounds__(kKllBlock)
+kll_compact_kernel(const double* __restrict__ src, const KllSeg* __restrict__ segs, double* __restrict__ dst,
+                   unsigned long long* __restrict__ minmax) {
+    __shared__ uint64_t k[PAD];
+    const KllSeg sg = segs[blockIdx.x];
+    const int len = (int)sg.len;
+    const double* in = src + sg.start;
+    for (int i = threadIdx.x; i < PAD; i += kKllBlock) k[i] = i < len ? kll_key(in[i]) : ~0ull;
+    __syncthreads();
+    for (int size = 2; size <= PAD; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < PAD / 2; t += kKllBlock) {
+                const int lo = 2 * t - (t & (stride - 1));
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const uint64_t a = k[lo], b = k[hi];
+                if ((a > b) == up) {
+                    k[lo] = b;
+                    k[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const int half = len >> 1;
+    double* out = dst + sg.outpos;
+    for (int j = threadIdx.x; j < half; j += kKllBlock) out[j] = kll_value(k[(int)sg.offset + 2 * j]);
+    if (minmax && threadIdx.x == 0 && len > 0) {
+        const uint64_t lo = k[0], hi = k[len - 1];
+        if (lo < *(volatile unsigned long long*)&minmax[0]) atomicMin(&minmax[0], (unsigned long long)lo);
+        if (hi > *(volatile unsigned long long*)&minmax[1]) atomicMax(&minmax[1], (unsigned long long)hi);
+    }
+}
+
+int launch_kll_compact(int pad, const double* src, const KllSeg* segs, int nseg, double* dst,
+                       unsigned long long* minmax, hipStream_t s) {
+    if (nseg <= 0) return 0;
+    switch (pad) {
+#define KLL_CASE(P) \
+    case P: hipLaunchKernelGGL(kll_compact_kernel<P>, dim3(nseg), dim3(kKllBlock), 0, s, src, segs, dst, minmax); break;
+        KLL_CASE(256)
+        KLL_CASE(512)
+        KLL_CASE(1024)
+        KLL_CASE(2048)
+        KLL_CASE(4096)
+        KLL_CASE(8192)
+        KLL_CASE(16384)
+#undef KLL_CASE
+        default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+hipStream_t ctx_stream(dq_ctx* ctx);
+int ctx_device(dq_ctx* ctx);
+int ctx_fail(dq_ctx* ctx, int code, const char* msg);
+
+}  // namespace dq
+
+namespace {
+
+using namespace dq;
+
+struct KBuffers {
+    std::vector<void*> ptrs;
+    ~KBuffers() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    hipError_t alloc(void** p, size_t bytes) {
+        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+        if (e == hipSuccess) ptrs.push_back(*p);
+        return e;
+    }
+};
+
+uint64_t host_key(double d) {
+    uint64_t u;
+    if (d != d) {
+        u = 0x7ff8000000000000ULL;
+    } else {
+        memcpy(&u, &d, 8);
+    }
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ULL);
+}
+double host_value(uint64_t k) {
+    uint64_t u = (k >> 63) ? (k & 0x7fffffffffffffffULL) : ~k;
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+
+// QuantileNonSample.capacity (A/QuantileNonSample.scala:87-89).
+int kll_capacity(int sketch_size, double f, int h) {
+    return 2 * ((int)ceil((double)sketch_size * pow(f, (double)h) / 2.0) + 1);
+}
+
+// The count automaton of QuantileNonSample.update/condense/expand for n updates.
+struct KllLevel {
+    int64_t len = 0;       // buffered items
+    int32_t ncomp = 0;     // NonSampleCompactor.numOfCompress
+    int32_t offset = 0;    // NonSampleCompactor.offset
+    int64_t pos = 0;       // first unconsumed item of this level's stream
+    int64_t arrived = 0;   // items appended to this level's stream
+    int maxlen = 0;        // largest compaction range
+    std::vector<KllSeg> segs;
+};
+
+struct KllSchedule {
+    std::vector<KllLevel> levels;
+    int64_t actual = 0;
+    int64_t total = 0;
+};
+
+bool kll_schedule(int64_t n, int sketch_size, double f, KllSchedule& sc) {
+    std::vector<int> caps;
+    auto cap = [&](int h) {
+        while ((int)caps.size() <= h) caps.push_back(kll_capacity(sketch_size, f, (int)caps.size()));
+        return (int64_t)caps[h];
+    };
+    sc.levels.assign(1, KllLevel());
+    sc.total = cap(0);
+    sc.actual = 0;
+    int64_t rem = n;
+    while (rem > 0) {
+        const int64_t k = std::min<int64_t>(rem, std::max<int64_t>(1, sc.total - sc.actual + 1));
+        sc.levels[0].len += k;
+        sc.levels[0].arrived += k;
+        sc.actual += k;
+        rem -= k;
+        if (sc.actual <= sc.total) continue;
+        for (size_t h = 0; h < sc.levels.size(); ++h) {
+            if (sc.levels[h].len < cap((int)h)) continue;
+            if (h + 1 >= sc.levels.size()) {
+                if (sc.levels.size() >= 120) return false;
+                sc.levels.push_back(KllLevel());
+                sc.total = 0;
+                for (size_t i = 0; i < sc.levels.size(); ++i) sc.total += cap((int)i);
+            }
+            KllLevel& lv = sc.levels[h];
+            const int64_t items = lv.len;
+            const int64_t L = items - items % 2;
+            if (L > kKllMaxPad) return false;
+            if (lv.ncomp % 2 == 1) lv.offset = 1 - lv.offset;
+            KllLevel& up = sc.levels[h + 1];
+            KllSeg sg;
+            sg.start = (unsigned long long)lv.pos;
+            sg.outpos = (unsigned long long)up.arrived;
+            sg.len = (unsigned int)L;
+            sg.offset = (unsigned int)lv.offset;
+            lv.segs.push_back(sg);
+            lv.maxlen = std::max<int>(lv.maxlen, (int)L);
+            lv.pos += L;
+            lv.len = items % 2;
+            up.len += L / 2;
+            up.arrived += L / 2;
+            lv.ncomp += 1;
+            sc.actual -= L / 2;  // = the sum of buffer lengths, as getCompactorItemsCount recomputes it
+            break;
+        }
+    }
+    return true;
+}
+
+void put_be32(std::vector<uint8_t>& o, int32_t v) {
+    for (int i = 3; i >= 0; --i) o.push_back((uint8_t)((uint32_t)v >> (8 * i)));
+}
+void put_be64(std::vector<uint8_t>& o, uint64_t v) {
+    for (int i = 7; i >= 0; --i) o.push_back((uint8_t)(v >> (8 * i)));
+}
+void put_f64(std::vector<uint8_t>& o, double d) {
+    uint64_t u;
+    memcpy(&u, &d, 8);
+    put_be64(o, u);
+}
+
+}  // namespace
+
+#define KL_HIP(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return dq::ctx_fail((ctx), DQ_ERR_DEVICE, hipGetErrorString(e_));   \
+    } while (0)
+
+extern "C" {
+
+int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t sketch_size,
+                      double shrinking_factor, uint8_t* state_out, int64_t capacity) {
+    if (!ctx || !column || nrows < 0 || column->length != nrows || capacity < 0 || (capacity > 0 && !state_out))
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_kll_sketch: invalid arguments");
+    if (!(shrinking_factor == shrinking_factor))
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_kll_sketch: shrinking factor is NaN");
+    const int t = column->spark_type;
+    // KLLRunner.emptySketches (R/KLLRunner.scala:118-145): Byte/Short/Int/Long/Float/Double only.
+    if (!(t == DQ_TYPE_BYTE || t == DQ_TYPE_SHORT || t == DQ_TYPE_INT || t == DQ_TYPE_LONG || t == DQ_TYPE_FLOAT ||
+          t == DQ_TYPE_DOUBLE))
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_kll_sketch: Cannot handle column type");
+    const int dev = dq::ctx_device(ctx);
+    KL_HIP(ctx, hipSetDevice(dev));
+    hipStream_t s = dq::ctx_stream(ctx);
+    KBuffers buf;
+
+    KllColumn kc;
+    kc.elem = elem_of(t);
+    const size_t vbytes = (size_t)nrows * elem_size(kc.elem);
+    const size_t bbytes = (size_t)(nrows + 63) / 64 * 8;
+    if (column->flags & DQ_COL_DEVICE) {
+        kc.values = column->values;
+        kc.validity = (const uint64_t*)column->validity;
+    } else {
+        void *v = nullptr, *m = nullptr;
+        KL_HIP(ctx, buf.alloc(&v, vbytes));
+        if (nrows) KL_HIP(ctx, hipMemcpyAsync(v, column->values, vbytes, hipMemcpyHostToDevice, s));
+        if (column->validity) {
+            KL_HIP(ctx, buf.alloc(&m, bbytes));
+            KL_HIP(ctx, hipMemsetAsync(m, 0, bbytes, s));
+            if (nrows)
+                KL_HIP(ctx, hipMemcpyAsync(m, column->validity, (size_t)(nrows + 7) / 8, hipMemcpyHostToDevice, s));
+        }
+        kc.values = v;
+        kc.validity = (const uint64_t*)m;
+    }
+
+    // ---- level-0 stream: the non-NULL values as doubles in row order -----------------------------
+    const double* stream0 = nullptr;
+    int64_t n = nrows;
+    if (kc.elem == ET_F64 && kc.validity == nullptr) {
+        stream0 = static_cast<const double*>(kc.values);
+    } else if (nrows > 0) {
+        const int64_t ntiles = (nrows + kKllStageRows - 1) / kKllStageRows;
+        unsigned int* dcounts = nullptr;
+        unsigned long long* doffs = nullptr;
+        KL_HIP(ctx, buf.alloc((void**)&dcounts, sizeof(unsigned int) * ntiles));
+        KL_HIP(ctx, buf.alloc((void**)&doffs, sizeof(unsigned long long) * ntiles));
+        hipLaunchKernelGGL(kll_count_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows, dcounts);
+        KL_HIP(ctx, hipGetLastError());
+        std::vector<unsigned int> counts(ntiles);
+        KL_HIP(ctx, hipMemcpyAsync(counts.data(), dcounts, sizeof(unsigned int) * ntiles, hipMemcpyDeviceToHost, s));
+        KL_HIP(ctx, hipStreamSynchronize(s));
+        std::vector<unsigned long long> offs(ntiles);
+        unsigned long long acc = 0;
+        for (int64_t i = 0; i < ntiles; ++i) {
+            offs[i] = acc;
+            acc += counts[i];
+        }
+        n = (int64_t)acc;
+        double* dense = nullptr;
+        KL_HIP(ctx, buf.alloc((void**)&dense, sizeof(double) * (size_t)std::max<int64_t>(n, 1)));
+        KL_HIP(ctx, hipMemcpyAsync(doffs, offs.data(), sizeof(unsigned long long) * ntiles, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows,
+                           (const unsigned long long*)doffs, dense);
+        KL_HIP(ctx, hipGetLastError());
+        stream0 = dense;
+    } else {
+        n = 0;
+    }
+
+    // ---- the compaction schedule (count-only) ------------------------------------------------------
+    KllSchedule sc;
+    if (!kll_schedule(n, sketch_size, shrinking_factor, sc))
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_kll_sketch: sketch parameters need a compaction larger than 16384 items");
+    const size_t nlev = sc.levels.size();
+
+    // ---- streams of levels >= 1, one device buffer ------------------------------------------------
+    std::vector<int64_t> lbase(nlev, 0);
+    int64_t upper = 0;
+    for (size_t h = 1; h < nlev; ++h) {
+        lbase[h] = upper;
+        upper += sc.levels[h].arrived;
+    }
+    double* dup = nullptr;
+    KL_HIP(ctx, buf.alloc((void**)&dup, sizeof(double) * (size_t)std::max<int64_t>(upper, 1)));
+    size_t nseg_all = 0;
+    for (const KllLevel& l : sc.levels) nseg_all += l.segs.size();
+    KllSeg* dsegs = nullptr;
+    KL_HIP(ctx, buf.alloc((void**)&dsegs, sizeof(KllSeg) * std::max<size_t>(nseg_all, 1)));
+    std::vector<KllSeg> hsegs;
+    hsegs.reserve(nseg_all);
+    for (const KllLevel& l : sc.levels) hsegs.insert(hsegs.end(), l.segs.begin(), l.segs.end());
+    if (nseg_all)
+        KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs.data(), sizeof(KllSeg) * nseg_all, hipMemcpyHostToDevice, s));
+    unsigned long long* dminmax = nullptr;
+    KL_HIP(ctx, buf.alloc((void**)&dminmax, sizeof(unsigned long long) * 2));
+    const unsigned long long mm_init[2] = {~0ull, 0ull};
+    KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, s));
+
+    size_t segoff = 0;
+    for (size_t h = 0; h < nlev; ++h) {  // a level that compacted always has a level above it
+        const KllLevel& l = sc.levels[h];
+        if (l.segs.empty()) continue;
+        int pad = 256;
+        while (pad < l.maxlen) pad <<= 1;
+        const double* src = h == 0 ? stream0 : dup + lbase[h];
+        double* dst = dup + lbase[h + 1];
+        if (launch_kll_compact(pad, src, dsegs + segoff, (int)l.segs.size(), dst, h == 0 ? dminmax : nullptr, s) != 0)
+            return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
+        segoff += l.segs.size();
+    }
+
+    // ---- final buffers --------------------------------------------------------------------------
+    std::vector<std::vector<double>> fin(nlev);
+    for (size_t h = 0; h < nlev; ++h) {
+        const KllLevel& l = sc.levels[h];
+        fin[h].resize((size_t)l.len);
+        if (l.len == 0) continue;
+        const double* src = (h == 0 ? stream0 : dup + lbase[h]) + l.pos;
+        KL_HIP(ctx, hipMemcpyAsync(fin[h].data(), src, sizeof(double) * (size_t)l.len, hipMemcpyDeviceToHost, s));
+    }
+    unsigned long long mm[2];
+    KL_HIP(ctx, hipMemcpyAsync(mm, dminmax, sizeof(mm), hipMemcpyDeviceToHost, s));
+    KL_HIP(ctx, hipStreamSynchronize(s));
+
+    // UntypedQuantileNonSample.updateUntyped: math.min / math.max folds from Int.MaxValue.toDouble /
+    // Int.MinValue.toDouble (java.lang.Math: NaN-propagating, -0.0 < 0.0) = the order-key extremes
+    // of every item, NaN if any item is NaN.
+    uint64_t kmin = mm[0], kmax = mm[1];
+    for (double d : fin[0]) {
+        kmin = std::min<uint64_t>(kmin, host_key(d));
+        kmax = std::max<uint64_t>(kmax, host_key(d));
+    }
+    double vmin = 2147483647.0, vmax = -2147483648.0;
+    if (n > 0) {
+        const double lo = host_value(kmin), hi = host_value(kmax);
+        if (hi != hi) {
+            vmin = vmax = NAN;
+        } else {
+            vmin = host_key(lo) < host_key(vmin) ? lo : vmin;
+            vmax = host_key(hi) > host_key(vmax) ? hi : vmax;
+        }
+    }
+
+    // ---- KLLState bytes (big-endian ByteBuffer) ---------------------------------------------------
+    std::vector<uint8_t> o;
+    put_f64(o, vmin);
+    put_f64(o, vmax);
+    put_be32(o, sketch_size);
+    put_f64(o, shrinking_factor);
+    put_be32(o, (int32_t)nlev);              // curNumOfCompactors
+    put_be32(o, (int32_t)sc.actual);         // compactorActualSize
+    put_be32(o, (int32_t)sc.total);          // compactorTotalSize
+    put_be32(o, (int32_t)nlev);              // compactors.length
+    for (size_t h = 0; h < nlev; ++h) {
+        put_be32(o, sc.levels[h].ncomp);
+        put_be32(o, sc.levels[h].offset);
+        put_be32(o, (int32_t)fin[h].size());
+        for (double d : fin[h]) put_f64(o, d);
+    }
+    if ((int64_t)o.size() <= capacity) memcpy(state_out, o.data(), o.size());
+    return (int64_t)o.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,344 @@
+"""KLLSketch: deequ's deterministic KLL quantile sketch (A/KLLSketch.scala, A/QuantileNonSample.scala,
+A/NonSampleCompactor.scala, R/KLLRunner.scala, M/metrics/KLLMetric.scala).
+
+The per-row sketching (KLLRunner.sketchPartitions' `updateUntyped` loop) runs on the GPU
+(dq_kll_sketch, deequ_amd/csrc/kll.hip), which returns the KLLState bytes of one partition holding
+the column in row order. This module is the host side the reference runs on the driver: the state
+(de)serialization (KLLState.fromBytes, KLLSketchSerializer), the sketch merge (QuantileNonSample.merge,
+used by KLLState.sum and KLLRunner's treeReduce over partitions), rank and quantile queries, and the
+metric (KLLSketch.computeMetricFrom -> BucketDistribution / KLLMetric). All of it works on a few
+thousand sketch items, never on rows.
+"""
+import math
+import struct
+
+from .metrics import DoubleMetric, Entity, Failure, Success
+
+DEFAULT_SKETCH_SIZE = 2048  # KLLSketch.DEFAULT_SKETCH_SIZE
+DEFAULT_SHRINKING_FACTOR = 0.64  # KLLSketch.DEFAULT_SHRINKING_FACTOR
+MAXIMUM_ALLOWED_DETAIL_BINS = 100  # KLLSketch.MAXIMUM_ALLOWED_DETAIL_BINS
+
+
+def _order_key(v):
+    """Ordering.Double.compare (java.lang.Double.compare): -0.0 < 0.0, NaN largest — what `.sorted`
+    and `sortBy` use."""
+    if v != v:
+        return (2, 0.0)
+    if v == 0.0:
+        return (0, -0.5 if math.copysign(1.0, v) < 0 else 0.0)
+    return (0, v)
+
+
+def _capacity(sketch_size, shrinking_factor, height):
+    """QuantileNonSample.capacity (A/QuantileNonSample.scala:87-89)."""
+    return 2 * (int(math.ceil(sketch_size * math.pow(shrinking_factor, height) / 2)) + 1)
+
+
+class NonSampleCompactor:
+    """A/NonSampleCompactor.scala:29-69 (the Random offset is commented out in the reference)."""
+
+    __slots__ = ("numOfCompress", "offset", "buffer")
+
+    def __init__(self, numOfCompress=0, offset=0, buffer=None):
+        self.numOfCompress, self.offset = int(numOfCompress), int(offset)
+        self.buffer = list(buffer or [])
+
+    def copy(self):
+        return NonSampleCompactor(self.numOfCompress, self.offset, self.buffer)
+
+    def compact(self):
+        items = len(self.buffer)
+        ln = items - items % 2
+        if self.numOfCompress % 2 == 1:
+            self.offset = 1 - self.offset
+        srt = sorted(self.buffer[:ln], key=_order_key)
+        output = srt[self.offset:ln:2]
+        self.buffer = [self.buffer[items - 1]] if items % 2 == 1 else []
+        self.numOfCompress += 1
+        return output
+
+
+class QuantileNonSample:
+    """A/QuantileNonSample.scala:24-306 over doubles (the only instantiation deequ uses)."""
+
+    def __init__(self, sketchSize=DEFAULT_SKETCH_SIZE, shrinkingFactor=DEFAULT_SHRINKING_FACTOR, compactors=None,
+                 curNumOfCompactors=None, compactorActualSize=None, compactorTotalSize=None):
+        self.sketchSize = int(sketchSize)
+        self.shrinkingFactor = float(shrinkingFactor)
+        if compactors is None:  # the constructor calls expand() once
+            self.compactors = []
+            self.curNumOfCompactors = 0
+            self.compactorActualSize = 0
+            self.compactorTotalSize = 0
+            self.expand()
+        else:
+            self.compactors = compactors
+            self.curNumOfCompactors = int(curNumOfCompactors)
+            self.compactorActualSize = int(compactorActualSize)
+            self.compactorTotalSize = int(compactorTotalSize)
+
+    def copy(self):
+        return QuantileNonSample(self.sketchSize, self.shrinkingFactor, [c.copy() for c in self.compactors],
+                                 self.curNumOfCompactors, self.compactorActualSize, self.compactorTotalSize)
+
+    def capacity(self, height):
+        return _capacity(self.sketchSize, self.shrinkingFactor, height)
+
+    def expand(self):
+        self.compactors.append(NonSampleCompactor())
+        self.curNumOfCompactors = len(self.compactors)
+        self.compactorTotalSize = self.getCompactorCapacityCount()
+
+    def reconstruct(self, sketchSize, shrinkingFactor, data):
+        self.sketchSize, self.shrinkingFactor = int(sketchSize), float(shrinkingFactor)
+        self.compactors = [NonSampleCompactor(buffer=list(d)) for d in data]
+        self.curNumOfCompactors = len(data)
+        self.compactorActualSize = self.getCompactorItemsCount()
+        self.compactorTotalSize = self.getCompactorCapacityCount()
+
+    def getCompactorItems(self):
+        return [list(c.buffer) for c in self.compactors]
+
+    def update(self, item):
+        """QuantileNonSample.update (host-side restatement; the GPU runs this loop for real data)."""
+        self.compactors[0].buffer.append(float(item))
+        self.compactorActualSize += 1
+        if self.compactorActualSize > self.compactorTotalSize:
+            self.condense()
+
+    def condense(self):
+        for height in range(len(self.compactors)):
+            if len(self.compactors[height].buffer) >= self.capacity(height):
+                if height + 1 >= self.curNumOfCompactors:
+                    self.expand()
+                output = self.compactors[height].compact()
+                self.compactors[height + 1].buffer.extend(output)
+                self.compactorActualSize = self.getCompactorItemsCount()
+                break
+
+    def merge(self, that):
+        """QuantileNonSample.merge (A/QuantileNonSample.scala:218-234); returns a new sketch (the
+        Scala version mutates and returns `this`)."""
+        out = self.copy()
+        while out.curNumOfCompactors < that.curNumOfCompactors:
+            out.expand()
+        for i in range(that.curNumOfCompactors):
+            out.compactors[i].buffer = out.compactors[i].buffer + list(that.compactors[i].buffer)
+        out.compactorActualSize = out.getCompactorItemsCount()
+        while out.compactorActualSize >= out.compactorTotalSize:
+            out.condense()
+        return out
+
+    def _output(self):
+        out = []
+        for i, c in enumerate(self.compactors[:self.curNumOfCompactors]):
+            w = 1 << i
+            out.extend((v, w) for v in c.buffer)
+        return out
+
+    def getRank(self, item):
+        """Inclusive rank: Ordering.Double.gt is IEEE `>` in Scala 2.11, so NaN targets count."""
+        return sum(w for t, w in self._output() if not (t > item))
+
+    def getRankExclusive(self, item):
+        return sum(w for t, w in self._output() if t < item)
+
+    def quantiles(self, q):
+        """QuantileNonSample.quantiles (A/QuantileNonSample.scala:249-281)."""
+        output = self._output()
+        if not output:
+            return []
+        items = sorted(output, key=lambda p: _order_key(p[0]))
+        total = sum(w for _, w in items)
+        next_thresh = total // q
+        curq, i, so_far = 1, 0, 0
+        res = [items[0][0]] * (q - 1)
+        while i < len(items) and curq < q:
+            while so_far < next_thresh:
+                so_far += items[i][1]
+                i += 1
+            res[curq - 1] = items[min(i, len(items) - 1)][0]
+            curq += 1
+            next_thresh = curq * total // q
+        return res
+
+    def getCompactorItemsCount(self):
+        return sum(len(c.buffer) for c in self.compactors[:self.curNumOfCompactors])
+
+    def getCompactorCapacityCount(self):
+        return sum(self.capacity(h) for h in range(self.curNumOfCompactors))
+
+    # KLLSketchSerializer (A/catalyst/KLLSketchSerializer.scala:60-118), big-endian ByteBuffer
+    def serialize(self):
+        out = [struct.pack(">idiiii", self.sketchSize, self.shrinkingFactor, self.curNumOfCompactors,
+                           self.compactorActualSize, self.compactorTotalSize, len(self.compactors))]
+        for c in self.compactors:
+            out.append(struct.pack(">iii", c.numOfCompress, c.offset, len(c.buffer)))
+            out.append(struct.pack(">%dd" % len(c.buffer), *c.buffer))
+        return b"".join(out)
+
+    @staticmethod
+    def deserialize(data, off=0):
+        size, f, cur, actual, total, ncomp = struct.unpack_from(">idiiii", data, off)
+        off += 28
+        comps = []
+        for _ in range(ncomp):
+            nc, o, ln = struct.unpack_from(">iii", data, off)
+            off += 12
+            buf = list(struct.unpack_from(">%dd" % ln, data, off))
+            off += 8 * ln
+            comps.append(NonSampleCompactor(nc, o, buf))
+        return QuantileNonSample(size, f, comps, cur, actual, total)
+
+
+def _java_min(a, b):
+    """java.lang.Math.min on doubles (NaN-propagating, -0.0 < 0.0)."""
+    if a != a or b != b:
+        return float("nan")
+    return a if _order_key(a) <= _order_key(b) else b
+
+
+def _java_max(a, b):
+    if a != a or b != b:
+        return float("nan")
+    return a if _order_key(a) >= _order_key(b) else b
+
+
+class KLLState:
+    """A/KLLSketch.scala:32-67."""
+
+    def __init__(self, qSketch, globalMax, globalMin):
+        self.qSketch, self.globalMax, self.globalMin = qSketch, float(globalMax), float(globalMin)
+
+    def sum(self, other):
+        return KLLState(self.qSketch.merge(other.qSketch), _java_max(self.globalMax, other.globalMax),
+                        _java_min(self.globalMin, other.globalMin))
+
+    @staticmethod
+    def fromBytes(data):
+        mn, mx = struct.unpack_from(">dd", data, 0)
+        return KLLState(QuantileNonSample.deserialize(data, 16), mx, mn)
+
+    def toBytes(self):
+        """StatefulKLLSketch.toBytes layout (C/StatefulKLLSketch.scala:86-92): min, max, sketch."""
+        return struct.pack(">dd", self.globalMin, self.globalMax) + self.qSketch.serialize()
+
+    def __eq__(self, other):
+        return isinstance(other, KLLState) and self.toBytes() == other.toBytes()
+
+
+class KLLParameters:
+    """A/KLLSketch.scala:75-80."""
+
+    def __init__(self, sketchSize, shrinkingFactor, numberOfBuckets):
+        self.sketchSize, self.shrinkingFactor, self.numberOfBuckets = int(sketchSize), float(shrinkingFactor), \
+            int(numberOfBuckets)
+
+    def _key(self):
+        return (self.sketchSize, self.shrinkingFactor, self.numberOfBuckets)
+
+    def __eq__(self, other):
+        return isinstance(other, KLLParameters) and self._key() == other._key()
+
+    def __hash__(self):
+        return hash(self._key())
+
+    def __repr__(self):
+        return "KLLParameters(%d,%r,%d)" % self._key()
+
+
+class BucketValue:
+    """M/metrics/KLLMetric.scala:24."""
+
+    def __init__(self, lowValue, highValue, count):
+        self.lowValue, self.highValue, self.count = float(lowValue), float(highValue), int(count)
+
+    def __eq__(self, other):
+        return isinstance(other, BucketValue) and (self.lowValue, self.highValue, self.count) == \
+            (other.lowValue, other.highValue, other.count)
+
+    def __repr__(self):
+        return "BucketValue(%r,%r,%d)" % (self.lowValue, self.highValue, self.count)
+
+
+class BucketDistribution:
+    """M/metrics/KLLMetric.scala:26-96."""
+
+    def __init__(self, buckets, parameters, data):
+        self.buckets, self.parameters, self.data = list(buckets), [float(p) for p in parameters], \
+            [list(d) for d in data]
+
+    def computePercentiles(self):
+        # parameters = (shrinkingFactor, sketchSize) but are read back as (sketchSize, shrinkingFactor); the
+        # quantiles depend only on `data`, so the swap (kept from the reference) is harmless.
+        q = QuantileNonSample(int(self.parameters[0]), self.parameters[1])
+        q.reconstruct(int(self.parameters[0]), self.parameters[1], self.data)
+        return q.quantiles(100)
+
+    def __getitem__(self, key):
+        return self.buckets[key]
+
+    def argmax(self):
+        current, best = 0, 0
+        for i, b in enumerate(self.buckets):
+            if b.count > current:
+                current, best = b.count, i
+        return best
+
+    def __eq__(self, other):
+        if not isinstance(other, BucketDistribution):
+            return False
+        if self.buckets != other.buckets or self.parameters != other.parameters or \
+                len(self.data) != len(other.data):
+            return False
+        return all(list(a) == list(b) for a, b in zip(self.data, other.data))
+
+    def __repr__(self):
+        return "BucketDistribution(%r,%r,%r)" % (self.buckets, self.parameters, self.data)
+
+
+class KLLMetric:
+    """M/metrics/KLLMetric.scala:98-126."""
+    name = "KLL"
+
+    def __init__(self, column, value):
+        self.column, self.value = column, value
+        self.entity = Entity.Column
+        self.instance = column
+
+    def flatten(self):
+        if self.value.isFailure:
+            return [DoubleMetric(self.entity, "%s.buckets" % self.name, self.instance, Failure(self.value.failed))]
+        dist = self.value.get()
+        out = [DoubleMetric(self.entity, "%s.buckets" % self.name, self.instance,
+                            Success(float(len(dist.buckets))))]
+        for b in dist.buckets:
+            out.append(DoubleMetric(self.entity, "%s.low" % self.name, self.instance, Success(b.lowValue)))
+            out.append(DoubleMetric(self.entity, "%s.high" % self.name, self.instance, Success(b.highValue)))
+            out.append(DoubleMetric(self.entity, "%s.count" % self.name, self.instance, Success(float(b.count))))
+        return out
+
+    def __eq__(self, other):
+        return isinstance(other, KLLMetric) and self.column == other.column and self.value == other.value
+
+    def __hash__(self):
+        return hash(("KLL", self.column))
+
+    def __repr__(self):
+        return "KLLMetric(%s,%r)" % (self.column, self.value)
+
+
+def bucket_distribution(state, numberOfBuckets):
+    """KLLSketch.computeMetricFrom's body (A/KLLSketch.scala:121-146)."""
+    sk = state.qSketch
+    start, end = state.globalMin, state.globalMax
+    buckets = []
+    for i in range(numberOfBuckets):
+        low = start + (end - start) * i / float(numberOfBuckets)
+        high = start + (end - start) * (i + 1) / float(numberOfBuckets)
+        if i == numberOfBuckets - 1:
+            cnt = sk.getRank(high) - sk.getRankExclusive(low)
+        else:
+            cnt = sk.getRankExclusive(high) - sk.getRankExclusive(low)
+        buckets.append(BucketValue(low, high, cnt))
+    return BucketDistribution(buckets, [sk.shrinkingFactor, float(sk.sketchSize)], sk.getCompactorItems())

@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "dq_abi_version", "dq_open", "dq_close", "dq_last_error", "dq_set_stream", "dq_synchronize", "dq_scan",
     "dq_scan_launch_count", "dq_state_merge", "dq_state_fold", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
     "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
-    "dq_quantile_summary", "dq_synth_column", "dq_synth_freq_keys",
+    "dq_quantile_summary", "dq_kll_sketch", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity",
 )
 
@@ -170,6 +170,8 @@ def load_library(path=None):
             "dq_partition_keys": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
             "dq_quantile_summary": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_double, c_int64, c_void_p,
                                               c_void_p, c_void_p]),
+            "dq_kll_sketch": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_int32, ctypes.c_double, c_void_p,
+                                        c_int64]),
             "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
             "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
             "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),
@@ -295,6 +297,19 @@ class Context:
         if ns < 0:
             self.check(int(ns), "dq_quantile_summary")
         return vals[:ns].copy(), ranks[:ns].copy(), int(count.value)
+
+    def kll_sketch(self, column, nrows, sketch_size, shrinking_factor):
+        """dq_kll_sketch: the KLLState bytes of one partition holding the column's rows in order."""
+        cap = 1 << 16
+        while True:
+            buf = np.empty(cap, dtype=np.uint8)
+            n = self.lib.dq_kll_sketch(self.handle, ctypes.byref(column), int(nrows), int(sketch_size),
+                                       float(shrinking_factor), buf.ctypes.data, cap)
+            if n < 0:
+                self.check(int(n), "dq_kll_sketch")
+            if n <= cap:
+                return buf[:n].tobytes()
+            cap = int(n)
 
     def synth_column(self, kind, seed, row0, nrows, dev_ptr):
         self.check(self.lib.dq_synth_column(self.handle, kind, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows,

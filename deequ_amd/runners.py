@@ -7,7 +7,7 @@ import json
 from . import native as N
 from . import engine
 from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer,
-                        FrequencyBasedAnalyzer, Preconditions, Size, computeFrequencies)
+                        FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies)
 from .expr import compile_predicate
 from .metrics import DoubleMetric, Success, UnsupportedOnDevice
 
@@ -209,6 +209,40 @@ class AnalysisRunBuilder:
         return AnalysisRunner.doAnalysisRun(self.data, self.analyzers, self._aggregateWith, self._saveStatesWith)
 
 
+class KLLRunner:
+    """R/KLLRunner.scala:91-179: KLL sketches in an extra pass. Each column's sketch is built by
+    dq_kll_sketch on the GPU as ONE partition holding the rows in order (KLLRunner.sketchPartitions over a
+    single-partition DataFrame); partition sketches of a sharded table merge with KLLState.sum, as the
+    reference's treeReduce does."""
+
+    _SUPPORTED = ("DoubleType", "FloatType", "ByteType", "ShortType", "IntegerType", "LongType")
+
+    @staticmethod
+    def sketch_column(data, column, sketchSize, shrinkingFactor):
+        from .kll import KLLState
+        t = data.schema[column]
+        if t not in KLLRunner._SUPPORTED:  # KLLRunner.emptySketches (:118-145)
+            raise ValueError("Cannot handle %s" % t)
+        raw = engine.ctx().kll_sketch(data[column].native(), data.nrows, sketchSize, shrinkingFactor)
+        return KLLState.fromBytes(raw)
+
+    @staticmethod
+    def computeKLLSketchesInExtraPass(data, analyzers, aggregateWith=None, saveStatesTo=None):
+        from .kll import DEFAULT_SKETCH_SIZE, DEFAULT_SHRINKING_FACTOR
+        params = {}
+        for a in analyzers:  # columnsAndParameters: `.toMap`, the last analyzer of a column wins
+            params[a.column] = a.kllParameters
+        sketches = {}
+        for column, p in params.items():
+            size, f = (p.sketchSize, p.shrinkingFactor) if p is not None else \
+                (DEFAULT_SKETCH_SIZE, DEFAULT_SHRINKING_FACTOR)
+            sketches[column] = KLLRunner.sketch_column(data, column, size, f)
+        results = {}
+        for a in analyzers:
+            results[a] = a.calculateMetric(sketches[a.column], aggregateWith, saveStatesTo)
+        return AnalyzerContext(results)
+
+
 class AnalysisRunner:
     """R/AnalysisRunner.scala:46-548."""
 
@@ -234,7 +268,12 @@ class AnalysisRunner:
         preconditionFailures = AnalyzerContext(
             {a: a.toFailureMetric(Preconditions.findFirstFailing(data.schema, a.preconditions())) for a in failed})
         grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
-        scanning = [a for a in passed if not isinstance(a, GroupingAnalyzer)]
+        allScanning = [a for a in passed if not isinstance(a, GroupingAnalyzer)]
+        kllAnalyzers = [a for a in allScanning if isinstance(a, KLLSketch)]
+        scanning = [a for a in allScanning if not isinstance(a, KLLSketch)]
+        kllMetrics = AnalyzerContext.empty()
+        if kllAnalyzers:
+            kllMetrics = KLLRunner.computeKLLSketchesInExtraPass(data, kllAnalyzers, aggregateWith, saveStatesWith)
         nonGrouped = AnalysisRunner._runScanningAnalyzers(data, scanning, aggregateWith, saveStatesWith)
         grouped = AnalyzerContext.empty()
         by_cols = {}
@@ -243,7 +282,7 @@ class AnalysisRunner:
         for cols, group in by_cols.items():
             _, metrics = AnalysisRunner._runGroupingAnalyzers(data, list(cols), group, aggregateWith, saveStatesWith)
             grouped = grouped + metrics
-        return preconditionFailures + nonGrouped + grouped
+        return preconditionFailures + nonGrouped + grouped + kllMetrics
 
     @staticmethod
     def _runScanningAnalyzers(data, analyzers, aggregateWith=None, saveStatesTo=None):

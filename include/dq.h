@@ -262,6 +262,17 @@ void dq_freq_free(dq_ctx* ctx, dq_freq_table* table);
 int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows, double relative_error,
                             int64_t max_samples, double* values_out, int64_t* ranks_out, int64_t* count_out);
 
+/* KLLSketch (A/KLLSketch.scala:82-176) as KLLRunner.computeKLLSketchesInExtraPass builds it
+ * (R/KLLRunner.scala:91-179): replaces the per-row QuantileNonSample.update loop of sketchPartitions for ONE
+ * partition whose non-NULL values (cast to double) arrive in row order. Writes the KLLState bytes
+ * (A/KLLSketch.scala:56-66: min f64, max f64, then the KLLSketchSerializer layout,
+ * A/catalyst/KLLSketchSerializer.scala:60-80; all big-endian) to state_out when they fit in `capacity`, and
+ * returns their length (call again with a larger buffer when the return value exceeds capacity), or a negative
+ * dq_status. BYTE/SHORT/INT/LONG/FLOAT/DOUBLE columns only (other types: DQ_ERR_UNSUPPORTED, as
+ * KLLRunner.emptySketches throws). NaN items are stored canonical. */
+int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t sketch_size,
+                      double shrinking_factor, uint8_t* state_out, int64_t capacity);
+
 /* Multi-GPU grouping: the canonical 64-bit keys (see DQ_FREQ_KEYS_VALUES) of one
  * fixed-width column's non-NULL rows, bucketed by owner rank = (mix64(key) >> 32) % nparts, written
  * contiguously per rank into keys_dev (capacity nrows, device memory) for an RCCL all-to-all; the

@@ -589,3 +589,86 @@ def _java_keys(d):
     bits[np.isnan(np.asarray(d, dtype=np.float64))] = np.uint64(0x7FF8000000000000)
     neg = (bits >> np.uint64(63)) == 1
     return np.where(neg, ~bits, bits | np.uint64(1 << 63))
+
+
+# ---- KLLSketch (A/KLLSketch.scala, A/QuantileNonSample.scala, A/NonSampleCompactor.scala,
+#      R/KLLRunner.scala) ---------------------------------------------------------------------------
+
+def _java_total_order(a):
+    """uint64 keys ordering float64 like java.lang.Double.compare (-0.0 < 0.0, NaN largest)."""
+    a = np.asarray(a, dtype=np.float64).copy()
+    a[np.isnan(a)] = np.nan  # canonical NaN
+    b = a.view(np.uint64)
+    neg = (b >> np.uint64(63)).astype(bool)
+    return np.where(neg, ~b, b | np.uint64(1 << 63))
+
+
+def _kll_capacity(sketch_size, shrinking_factor, height):
+    """QuantileNonSample.capacity (A/QuantileNonSample.scala:87-89)."""
+    return 2 * (int(math.ceil(sketch_size * math.pow(shrinking_factor, height) / 2)) + 1)
+
+
+def kll_sketch_sequential(values, sketch_size=2048, shrinking_factor=0.64):
+    """The sketch of one partition whose items arrive in `values` order: QuantileNonSample.update /
+    condense / expand (A/QuantileNonSample.scala:80-121) with NonSampleCompactor.compact
+    (A/NonSampleCompactor.scala:40-66; the Random offset is commented out in the reference, so the
+    offset flips deterministically after every odd-numbered compaction). Returns a dict with the
+    serializer fields (A/catalyst/KLLSketchSerializer.scala:60-80)."""
+    cap = lambda h: _kll_capacity(sketch_size, shrinking_factor, h)
+    bufs, ncomp, offs = [[]], [0], [0]
+    total = cap(0)
+    actual = 0
+    for v in values:
+        bufs[0].append(float(v))
+        actual += 1
+        if actual > total:
+            for h in range(len(bufs)):
+                if len(bufs[h]) >= cap(h):
+                    if h + 1 >= len(bufs):
+                        bufs.append([]); ncomp.append(0); offs.append(0)
+                        total = sum(cap(i) for i in range(len(bufs)))
+                    items = len(bufs[h])
+                    ln = items - items % 2
+                    if ncomp[h] % 2 == 1:
+                        offs[h] = 1 - offs[h]
+                    part = np.asarray(bufs[h][:ln], dtype=np.float64)
+                    srt = part[np.argsort(_java_total_order(part), kind="stable")]
+                    bufs[h + 1].extend(srt[offs[h]:ln:2].tolist())
+                    bufs[h] = [bufs[h][items - 1]] if items % 2 else []
+                    ncomp[h] += 1
+                    actual = sum(len(b) for b in bufs)
+                    break
+    return {"sketchSize": sketch_size, "shrinkingFactor": shrinking_factor, "curNumOfCompactors": len(bufs),
+            "compactorActualSize": actual, "compactorTotalSize": total,
+            "compactors": [(ncomp[h], offs[h], bufs[h]) for h in range(len(bufs))]}
+
+
+def kll_runner_min_max(values):
+    """UntypedQuantileNonSample min/max (R/KLLRunner.scala:27-36): math.min / math.max folds starting
+    from Int.MaxValue.toDouble / Int.MinValue.toDouble (NaN-propagating, -0.0 < 0.0)."""
+    lo, hi = 2147483647.0, -2147483648.0
+    for v in values:
+        v = float(v)
+        if v != v or lo != lo:
+            lo = float("nan")
+        elif v < lo or (v == lo == 0.0 and math.copysign(1.0, v) < 0):
+            lo = v
+        if v != v or hi != hi:
+            hi = float("nan")
+        elif v > hi or (v == hi == 0.0 and math.copysign(1.0, v) > 0):
+            hi = v
+    return lo, hi
+
+
+def kll_state_bytes(values, sketch_size=2048, shrinking_factor=0.64):
+    """KLLState bytes for one partition (A/KLLSketch.scala:56-66 read order: min, max, sketch)."""
+    import struct
+    sk = kll_sketch_sequential(values, sketch_size, shrinking_factor)
+    lo, hi = kll_runner_min_max(values)
+    out = [struct.pack(">dd", lo, hi),
+           struct.pack(">idiiii", sk["sketchSize"], sk["shrinkingFactor"], sk["curNumOfCompactors"],
+                       sk["compactorActualSize"], sk["compactorTotalSize"], len(sk["compactors"]))]
+    for nc, off, buf in sk["compactors"]:
+        out.append(struct.pack(">iii", nc, off, len(buf)))
+        out.append(struct.pack(">%dd" % len(buf), *buf))
+    return b"".join(out)
