@@ -154,6 +154,14 @@ hipStream_t ctx_stream(dq_ctx* ctx) { return ctx->stream; }
 int ctx_device(dq_ctx* ctx) { return ctx->device; }
 int ctx_cus(dq_ctx* ctx) { return ctx->cus; }
 int ctx_fail(dq_ctx* ctx, int code, const char* msg) { return fail(ctx, code, "%s", msg); }
+// The context's device arena / pinned staging buffer, grown to `bytes` (NULL + error set on failure).
+// Used by one call at a time (a ctx is not re-entrant); work queued on the ctx stream stays ordered.
+void* ctx_scratch(dq_ctx* ctx, size_t bytes) { return ensure_arena(ctx, bytes) == DQ_OK ? ctx->arena : nullptr; }
+void* ctx_pinned_buf(dq_ctx* ctx, size_t bytes) {
+    if (ensure_pinned(ctx, bytes) != DQ_OK) return nullptr;
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return nullptr;  // earlier copies from it are done
+    return ctx->pinned;
+}
 }  // namespace dq
 
 // =================================================================================================

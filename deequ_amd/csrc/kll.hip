@@ -30,7 +30,11 @@
 #include <math.h>
 #include <string.h>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "dq_common.h"
@@ -38,7 +42,6 @@
 
 namespace dq {
 
-constexpr int kKllBlock = 256;
 constexpr int kKllMaxPad = 16384;  // 128 KiB of LDS keys: the largest compaction handled
 constexpr int kKllStageBlock = 256;
 constexpr int kKllStageRows = 2048;  // rows per workgroup tile of the NULL-compaction pass
@@ -116,63 +119,150 @@ kll_write_kernel(KllColumn c, int64_t nrows, const unsigned long long* __restric
     }
 }
 
-struct KllSeg {
-    unsigned long long start;   // first item of the compacted range in this level's stream
-    unsigned long long outpos;  // first slot of its picks in the next level's stream
-    unsigned int len;           // L (even)
-    unsigned int offset;        // NonSampleCompactor.offset at this compaction
-};
+// One compaction, packed in 8 bytes: start of the compacted range in its level's stream (bits 0-39),
+// L (bits 40-54, <= 16384) and the compactor offset (bit 63). Compactions consume a level's stream
+// contiguously from 0 and every L is even, so the picks go to next-level slot start / 2.
+__host__ __device__ inline uint64_t kll_desc(uint64_t start, uint32_t len, uint32_t offset) {
+    return start | ((uint64_t)len << 40) | ((uint64_t)offset << 63);
+}
 
-// One workgroup per compaction of one level: sort the range in LDS, keep every other item.
-// Level 0 also folds the range's sorted ends into the running min / max keys.
-template <int PAD>
-__global__ void __launch_bounds__(kKllBlock)
-kll_compact_kernel(const double* __restrict__ src, const KllSeg* __restrict__ segs, double* __restrict__ dst,
-                   unsigned long long* __restrict__ minmax) {
-    __shared__ uint64_t k[PAD];
-    const KllSeg sg = segs[blockIdx.x];
-    const int len = (int)sg.len;
-    const double* in = src + sg.start;
-    for (int i = threadIdx.x; i < PAD; i += kKllBlock) k[i] = i < len ? kll_key(in[i]) : ~0ull;
-    __syncthreads();
-    for (int size = 2; size <= PAD; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < PAD / 2; t += kKllBlock) {
-                const int lo = 2 * t - (t & (stride - 1));
-                const int hi = lo + stride;
-                const bool up = (lo & size) == 0;
-                const uint64_t a = k[lo], b = k[hi];
-                if ((a > b) == up) {
-                    k[lo] = b;
-                    k[hi] = a;
+// One workgroup of T threads per compaction of one level; the range (<= T*E items, padded with +inf
+// keys) is sorted as a merge sort: every thread sorts E consecutive keys in registers (bitonic network,
+// compile-time indices), then log2(T) rounds merge pairs of sorted runs through LDS, each thread
+// producing E outputs of its merged pair from a merge-path split (binary search on the diagonal) — far
+// fewer LDS accesses and barriers than a bitonic network over LDS. The LDS image is padded by one key per
+// thread (physical index i + i/E) so thread-contiguous accesses are bank-conflict free. The picks
+// sorted[offset + 2j] go straight from registers to the next level's stream; level 0 also folds the
+// range's sorted ends into the running min / max keys.
+template <int E>
+__device__ __forceinline__ void kll_reg_sort(uint64_t (&v)[E]) {
+    constexpr int P = E <= 4 ? 4 : (E <= 8 ? 8 : 16);
+    uint64_t w[P];
+#pragma unroll
+    for (int r = 0; r < P; ++r) w[r] = r < E ? v[r] : ~0ull;
+#pragma unroll
+    for (int size = 2; size <= P; size <<= 1)
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+            for (int r = 0; r < P; ++r) {
+                const int q = r ^ stride;
+                if (q > r) {
+                    const bool asc = (r & size) == 0;
+                    const uint64_t a = w[r], b = w[q];
+                    const bool sw = (a > b) == asc;
+                    w[r] = sw ? b : a;
+                    w[q] = sw ? a : b;
                 }
             }
-            __syncthreads();
-        }
+#pragma unroll
+    for (int r = 0; r < E; ++r) v[r] = w[r];
+}
+
+template <int T, int E>
+__global__ void __launch_bounds__(T)
+kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
+                   unsigned long long* __restrict__ minmax) {
+    constexpr int PAD = T * E;
+    __shared__ uint64_t k[PAD + T];
+    auto at = [](int i) { return i + i / E; };
+    const uint64_t sg = segs[blockIdx.x];
+    const uint64_t start = sg & ((1ull << 40) - 1);
+    const int len = (int)((sg >> 40) & 0x7FFF);
+    const int t = threadIdx.x;
+    const double* in = src + start;
+    uint64_t v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = t * E + r;
+        v[r] = i < len ? kll_key(in[i]) : ~0ull;
     }
+    kll_reg_sort<E>(v);
+    for (int w = E; w < PAD; w <<= 1) {
+#pragma unroll
+        for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
+        __syncthreads();
+        const int diag = E * (t & (2 * (w / E) - 1));  // offset inside the merged pair (w / E is a power of 2)
+        const int A = (t * E) - diag, B = A + w;
+        int lo = diag > w ? diag - w : 0, hi = diag < w ? diag : w;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (k[at(A + mid)] <= k[at(B + diag - 1 - mid)]) lo = mid + 1;
+            else hi = mid;
+        }
+        int ai = A + lo, bi = B + diag - lo;
+        const int aend = A + w, bend = B + w;
+        uint64_t ah = ai < aend ? k[at(ai)] : ~0ull, bh = bi < bend ? k[at(bi)] : ~0ull;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const bool takeA = bi >= bend || (ai < aend && ah <= bh);
+            if (takeA) {
+                v[r] = ah;
+                ++ai;
+                ah = ai < aend ? k[at(ai)] : ~0ull;
+            } else {
+                v[r] = bh;
+                ++bi;
+                bh = bi < bend ? k[at(bi)] : ~0ull;
+            }
+        }
+        __syncthreads();
+    }
+    // picks: sorted index i = t*E + r with i = offset + 2j, j < len/2
     const int half = len >> 1;
-    double* out = dst + sg.outpos;
-    for (int j = threadIdx.x; j < half; j += kKllBlock) out[j] = kll_value(k[(int)sg.offset + 2 * j]);
-    if (minmax && threadIdx.x == 0 && len > 0) {
-        const uint64_t lo = k[0], hi = k[len - 1];
-        if (lo < *(volatile unsigned long long*)&minmax[0]) atomicMin(&minmax[0], (unsigned long long)lo);
-        if (hi > *(volatile unsigned long long*)&minmax[1]) atomicMax(&minmax[1], (unsigned long long)hi);
+    const int off = (int)(sg >> 63);
+    double* out = dst + (start >> 1);
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = t * E + r;
+        const int d = i - off;
+        if (d >= 0 && (d & 1) == 0 && (d >> 1) < half) out[d >> 1] = kll_value(v[r]);
+    }
+    if (minmax && len > 0) {
+        if (t == 0 && v[0] < *(volatile unsigned long long*)&minmax[0]) atomicMin(&minmax[0], (unsigned long long)v[0]);
+        const int last = len - 1;
+        if (t == last / E) {
+            uint64_t hi = 0;
+#pragma unroll
+            for (int r = 0; r < E; ++r)
+                if (r == last % E) hi = v[r];
+            if (hi > *(volatile unsigned long long*)&minmax[1]) atomicMax(&minmax[1], (unsigned long long)hi);
+        }
     }
 }
 
-int launch_kll_compact(int pad, const double* src, const KllSeg* segs, int nseg, double* dst,
+// Compaction classes: (threads, keys per thread), capacity T*E.
+struct KllClass {
+    int t, e;
+};
+constexpr KllClass kKllClasses[] = {{64, 4},   {64, 8},   {64, 12},   {64, 16},   {128, 12},  {128, 16},
+                                    {256, 12}, {256, 16}, {512, 12},  {512, 16},  {1024, 12}, {1024, 16}};
+constexpr int kKllNumClasses = sizeof(kKllClasses) / sizeof(kKllClasses[0]);
+
+int kll_class_of(int len) {
+    for (int c = 0; c < kKllNumClasses; ++c)
+        if (kKllClasses[c].t * kKllClasses[c].e >= len) return c;
+    return -1;
+}
+
+int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nseg, double* dst,
                        unsigned long long* minmax, hipStream_t s) {
     if (nseg <= 0) return 0;
-    switch (pad) {
-#define KLL_CASE(P) \
-    case P: hipLaunchKernelGGL(kll_compact_kernel<P>, dim3(nseg), dim3(kKllBlock), 0, s, src, segs, dst, minmax); break;
-        KLL_CASE(256)
-        KLL_CASE(512)
-        KLL_CASE(1024)
-        KLL_CASE(2048)
-        KLL_CASE(4096)
-        KLL_CASE(8192)
-        KLL_CASE(16384)
+    switch (cls) {
+#define KLL_CASE(C, T, E) \
+    case C: hipLaunchKernelGGL((kll_compact_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax); break;
+        KLL_CASE(0, 64, 4)
+        KLL_CASE(1, 64, 8)
+        KLL_CASE(2, 64, 12)
+        KLL_CASE(3, 64, 16)
+        KLL_CASE(4, 128, 12)
+        KLL_CASE(5, 128, 16)
+        KLL_CASE(6, 256, 12)
+        KLL_CASE(7, 256, 16)
+        KLL_CASE(8, 512, 12)
+        KLL_CASE(9, 512, 16)
+        KLL_CASE(10, 1024, 12)
+        KLL_CASE(11, 1024, 16)
 #undef KLL_CASE
         default: return -1;
     }
@@ -182,6 +272,8 @@ int launch_kll_compact(int pad, const double* src, const KllSeg* segs, int nseg,
 hipStream_t ctx_stream(dq_ctx* ctx);
 int ctx_device(dq_ctx* ctx);
 int ctx_fail(dq_ctx* ctx, int code, const char* msg);
+void* ctx_scratch(dq_ctx* ctx, size_t bytes);
+void* ctx_pinned_buf(dq_ctx* ctx, size_t bytes);
 
 }  // namespace dq
 
@@ -229,8 +321,8 @@ struct KllLevel {
     int32_t offset = 0;    // NonSampleCompactor.offset
     int64_t pos = 0;       // first unconsumed item of this level's stream
     int64_t arrived = 0;   // items appended to this level's stream
-    int maxlen = 0;        // largest compaction range
-    std::vector<KllSeg> segs;
+    std::vector<uint64_t> segs;                   // compactions, in order
+    int64_t per_class[16] = {0};                  // compactions per kernel class
 };
 
 struct KllSchedule {
@@ -270,13 +362,8 @@ bool kll_schedule(int64_t n, int sketch_size, double f, KllSchedule& sc) {
             if (L > kKllMaxPad) return false;
             if (lv.ncomp % 2 == 1) lv.offset = 1 - lv.offset;
             KllLevel& up = sc.levels[h + 1];
-            KllSeg sg;
-            sg.start = (unsigned long long)lv.pos;
-            sg.outpos = (unsigned long long)up.arrived;
-            sg.len = (unsigned int)L;
-            sg.offset = (unsigned int)lv.offset;
-            lv.segs.push_back(sg);
-            lv.maxlen = std::max<int>(lv.maxlen, (int)L);
+            lv.segs.push_back(kll_desc((uint64_t)lv.pos, (uint32_t)L, (uint32_t)lv.offset));
+            ++lv.per_class[kll_class_of((int)L)];
             lv.pos += L;
             lv.len = items % 2;
             up.len += L / 2;
@@ -349,14 +436,17 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     }
 
     // ---- level-0 stream: the non-NULL values as doubles in row order -----------------------------
+    const auto t0 = std::chrono::steady_clock::now();
     const double* stream0 = nullptr;
     int64_t n = nrows;
-    if (kc.elem == ET_F64 && kc.validity == nullptr) {
+    const bool zero_copy = kc.elem == ET_F64 && kc.validity == nullptr;
+    const int64_t ntiles = (nrows + kKllStageRows - 1) / kKllStageRows;
+    unsigned long long* doffs = nullptr;
+    std::vector<unsigned long long> offs;
+    if (zero_copy) {
         stream0 = static_cast<const double*>(kc.values);
     } else if (nrows > 0) {
-        const int64_t ntiles = (nrows + kKllStageRows - 1) / kKllStageRows;
         unsigned int* dcounts = nullptr;
-        unsigned long long* doffs = nullptr;
         KL_HIP(ctx, buf.alloc((void**)&dcounts, sizeof(unsigned int) * ntiles));
         KL_HIP(ctx, buf.alloc((void**)&doffs, sizeof(unsigned long long) * ntiles));
         hipLaunchKernelGGL(kll_count_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows, dcounts);
@@ -364,20 +454,13 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
         std::vector<unsigned int> counts(ntiles);
         KL_HIP(ctx, hipMemcpyAsync(counts.data(), dcounts, sizeof(unsigned int) * ntiles, hipMemcpyDeviceToHost, s));
         KL_HIP(ctx, hipStreamSynchronize(s));
-        std::vector<unsigned long long> offs(ntiles);
+        offs.resize(ntiles);
         unsigned long long acc = 0;
         for (int64_t i = 0; i < ntiles; ++i) {
             offs[i] = acc;
             acc += counts[i];
         }
         n = (int64_t)acc;
-        double* dense = nullptr;
-        KL_HIP(ctx, buf.alloc((void**)&dense, sizeof(double) * (size_t)std::max<int64_t>(n, 1)));
-        KL_HIP(ctx, hipMemcpyAsync(doffs, offs.data(), sizeof(unsigned long long) * ntiles, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows,
-                           (const unsigned long long*)doffs, dense);
-        KL_HIP(ctx, hipGetLastError());
-        stream0 = dense;
     } else {
         n = 0;
     }
@@ -387,41 +470,73 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     if (!kll_schedule(n, sketch_size, shrinking_factor, sc))
         return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_kll_sketch: sketch parameters need a compaction larger than 16384 items");
     const size_t nlev = sc.levels.size();
+    const auto t1 = std::chrono::steady_clock::now();
 
-    // ---- streams of levels >= 1, one device buffer ------------------------------------------------
+    // ---- device scratch (the context arena): [dense level-0 stream][levels >= 1][descriptors][min/max]
     std::vector<int64_t> lbase(nlev, 0);
     int64_t upper = 0;
     for (size_t h = 1; h < nlev; ++h) {
         lbase[h] = upper;
         upper += sc.levels[h].arrived;
     }
-    double* dup = nullptr;
-    KL_HIP(ctx, buf.alloc((void**)&dup, sizeof(double) * (size_t)std::max<int64_t>(upper, 1)));
     size_t nseg_all = 0;
     for (const KllLevel& l : sc.levels) nseg_all += l.segs.size();
-    KllSeg* dsegs = nullptr;
-    KL_HIP(ctx, buf.alloc((void**)&dsegs, sizeof(KllSeg) * std::max<size_t>(nseg_all, 1)));
-    std::vector<KllSeg> hsegs;
-    hsegs.reserve(nseg_all);
-    for (const KllLevel& l : sc.levels) hsegs.insert(hsegs.end(), l.segs.begin(), l.segs.end());
-    if (nseg_all)
-        KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs.data(), sizeof(KllSeg) * nseg_all, hipMemcpyHostToDevice, s));
-    unsigned long long* dminmax = nullptr;
-    KL_HIP(ctx, buf.alloc((void**)&dminmax, sizeof(unsigned long long) * 2));
+    const size_t dense_bytes = zero_copy ? 0 : (size_t)n * 8;
+    const size_t up_off = (dense_bytes + 255) / 256 * 256;
+    const size_t seg_off = up_off + ((size_t)upper * 8 + 255) / 256 * 256;
+    const size_t mm_off = seg_off + (nseg_all * 8 + 255) / 256 * 256;
+    uint8_t* scratch = static_cast<uint8_t*>(dq::ctx_scratch(ctx, mm_off + 256));
+    if (!scratch) return DQ_ERR_OUT_OF_MEMORY;
+    double* dup = reinterpret_cast<double*>(scratch + up_off);
+    uint64_t* dsegs = reinterpret_cast<uint64_t*>(scratch + seg_off);
+    unsigned long long* dminmax = reinterpret_cast<unsigned long long*>(scratch + mm_off);
+    if (!zero_copy && n > 0) {
+        double* dense = reinterpret_cast<double*>(scratch);
+        KL_HIP(ctx, hipMemcpyAsync(doffs, offs.data(), sizeof(unsigned long long) * ntiles, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows,
+                           (const unsigned long long*)doffs, dense);
+        KL_HIP(ctx, hipGetLastError());
+        stream0 = dense;
+    }
+
+    // compactions grouped per (level, kernel class), staged in pinned memory: one launch per group; the
+    // order inside a level is free because every compaction's input range and output slot are explicit
+    struct Launch {
+        size_t level, first, count;
+        int cls;
+    };
+    std::vector<Launch> launches;
+    uint64_t* hsegs = nseg_all ? static_cast<uint64_t*>(dq::ctx_pinned_buf(ctx, nseg_all * 8)) : nullptr;
+    if (nseg_all && !hsegs) return DQ_ERR_OUT_OF_MEMORY;
+    size_t pos = 0;
+    for (size_t h = 0; h < nlev; ++h) {
+        const KllLevel& l = sc.levels[h];
+        size_t cursor[kKllNumClasses];
+        for (int c = 0; c < kKllNumClasses; ++c) {
+            cursor[c] = pos;
+            if (l.per_class[c]) launches.push_back({h, pos, (size_t)l.per_class[c], c});
+            pos += (size_t)l.per_class[c];
+        }
+        for (const uint64_t d : l.segs) hsegs[cursor[kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
+    }
+    if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, s));
     const unsigned long long mm_init[2] = {~0ull, 0ull};
     KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, s));
+    const auto t2 = std::chrono::steady_clock::now();
 
-    size_t segoff = 0;
-    for (size_t h = 0; h < nlev; ++h) {  // a level that compacted always has a level above it
-        const KllLevel& l = sc.levels[h];
-        if (l.segs.empty()) continue;
-        int pad = 256;
-        while (pad < l.maxlen) pad <<= 1;
+    for (const Launch& L : launches) {  // a level that compacted always has a level above it
+        const size_t h = L.level;
         const double* src = h == 0 ? stream0 : dup + lbase[h];
         double* dst = dup + lbase[h + 1];
-        if (launch_kll_compact(pad, src, dsegs + segoff, (int)l.segs.size(), dst, h == 0 ? dminmax : nullptr, s) != 0)
+        if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, s) != 0)
             return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
-        segoff += l.segs.size();
+    }
+    if (getenv("DQ_KLL_TIMING")) {
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        fprintf(stderr, "[dq_kll_sketch] n=%lld levels=%zu compactions=%zu count+schedule %.2f ms, staging %.2f ms\n",
+                (long long)n, nlev, nseg_all, ms(t0, t1), ms(t1, t2));
     }
 
     // ---- final buffers --------------------------------------------------------------------------

@@ -12,6 +12,7 @@
 
 #include "dq_common.h"
 #include "dq_internal.h"
+#include "dq_parse.h"
 
 namespace dq {
 
@@ -62,31 +63,28 @@ __device__ __forceinline__ bool is_ws(uint8_t c) { return c == ' ' || c == '\t' 
 __device__ const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                       1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
-// Spark Cast(string -> double): trimmed decimal literal, NULL when it does not parse.
-__device__ bool parse_double(const uint8_t* s, int n, double& out) {
+// Spark Cast(string -> double) = java.lang.Double.parseDouble, correctly rounded (dq_parse.h). The
+// rare literal it cannot round on the device (hexadecimal, or > 19 significant digits on a rounding
+// boundary) falls back to a plain decimal scale here: predicates have no per-row error channel.
+__device__ bool parse_double_approx(const uint8_t* s, int n, double& out) {
     int i = 0;
-    while (i < n && is_ws(s[i])) ++i;
-    while (n > i && is_ws(s[n - 1])) --n;
+    while (i < n && s[i] <= ' ') ++i;
+    while (n > i && s[n - 1] <= ' ') --n;
     if (i >= n) return false;
     bool neg = false;
     if (s[i] == '+' || s[i] == '-') {
         neg = s[i] == '-';
         ++i;
     }
-    uint64_t mant = 0;
-    int digits = 0, exp10 = 0, nd = 0;
+    double v = 0.0;
+    int exp10 = 0, nd = 0;
     bool seen_dot = false;
     for (; i < n; ++i) {
         const uint8_t c = s[i];
         if (c >= '0' && c <= '9') {
             ++nd;
-            if (digits < 19) {
-                mant = mant * 10 + (c - '0');
-                if (mant) ++digits;
-                if (seen_dot) --exp10;
-            } else if (!seen_dot) {
-                ++exp10;
-            }
+            v = v * 10.0 + (c - '0');
+            if (seen_dot) --exp10;
         } else if (c == '.' && !seen_dot) {
             seen_dot = true;
         } else {
@@ -101,55 +99,25 @@ __device__ bool parse_double(const uint8_t* s, int n, double& out) {
             eneg = s[i] == '-';
             ++i;
         }
-        int e = 0, ed = 0;
-        for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i, ++ed) e = e < 10000 ? e * 10 + (s[i] - '0') : e;
-        if (ed == 0) return false;
+        int e = 0;
+        for (; i < n && s[i] >= '0' && s[i] <= '9'; ++i) e = e < 10000 ? e * 10 + (s[i] - '0') : e;
         exp10 += eneg ? -e : e;
     }
-    if (i < n) {
-        // Java's parser accepts a trailing type suffix such as 'd' / 'f'.
-        if (i + 1 == n && (s[i] == 'd' || s[i] == 'D' || s[i] == 'f' || s[i] == 'F')) {
-        } else {
-            return false;
-        }
-    }
-    double v = (double)mant;
-    if (exp10 >= 0) {
-        while (exp10 > 22) { v *= 1e22; exp10 -= 22; }
-        v *= kPow10[exp10];
-    } else {
-        while (exp10 < -22) { v /= 1e22; exp10 += 22; }
-        v /= kPow10[-exp10];
-    }
+    while (exp10 > 22) { v *= 1e22; exp10 -= 22; }
+    while (exp10 < -22) { v /= 1e22; exp10 += 22; }
+    v = exp10 >= 0 ? v * kPow10[exp10] : v / kPow10[-exp10];
     out = neg ? -v : v;
     return true;
 }
 
-__device__ bool parse_long(const uint8_t* s, int n, int64_t& out) {
-    int i = 0;
-    while (i < n && is_ws(s[i])) ++i;
-    while (n > i && is_ws(s[n - 1])) --n;
-    if (i >= n) return false;
-    bool neg = false;
-    if (s[i] == '+' || s[i] == '-') {
-        neg = s[i] == '-';
-        ++i;
-    }
-    if (i >= n) return false;
-    uint64_t v = 0;
-    for (; i < n; ++i) {
-        if (s[i] < '0' || s[i] > '9') break;
-        v = v * 10 + (s[i] - '0');
-    }
-    if (i < n) {
-        // Spark truncates a fractional part when casting "1.5" to long.
-        if (s[i] != '.') return false;
-        for (++i; i < n; ++i)
-            if (s[i] < '0' || s[i] > '9') return false;
-    }
-    out = neg ? -(int64_t)v : (int64_t)v;
-    return true;
+__device__ bool parse_double(const uint8_t* s, int n, double& out) {
+    bool slow = false;
+    if (java_parse_double(s, n, out, slow)) return true;
+    return slow ? parse_double_approx(s, n, out) : false;
 }
+
+// Spark 2.2 Cast(string -> long) = UTF8String.toLong (dq_parse.h).
+__device__ bool parse_long(const uint8_t* s, int n, int64_t& out) { return spark_string_to_long(s, n, out); }
 
 __device__ __forceinline__ bool numeric(const Val& v) { return v.tag == DQ_V_LONG || v.tag == DQ_V_DOUBLE || v.tag == DQ_V_BOOL; }
 __device__ __forceinline__ double as_double(const Val& v) { return v.tag == DQ_V_DOUBLE ? v.d : (double)v.i; }

@@ -136,12 +136,30 @@ class QuantileNonSample:
             out.extend((v, w) for v in c.buffer)
         return out
 
+    def _output_arrays(self):
+        import numpy as np
+        items = np.concatenate([np.asarray(c.buffer, dtype=np.float64)
+                                for c in self.compactors[:self.curNumOfCompactors]] or [np.zeros(0)])
+        weights = np.concatenate([np.full(len(c.buffer), 1 << i, dtype=np.int64)
+                                  for i, c in enumerate(self.compactors[:self.curNumOfCompactors])] or
+                                 [np.zeros(0, dtype=np.int64)])
+        return items, weights
+
     def getRank(self, item):
         """Inclusive rank: Ordering.Double.gt is IEEE `>` in Scala 2.11, so NaN targets count."""
-        return sum(w for t, w in self._output() if not (t > item))
+        return int(self.getRanks([item], exclusive=False)[0])
 
     def getRankExclusive(self, item):
-        return sum(w for t, w in self._output() if t < item)
+        return int(self.getRanks([item], exclusive=True)[0])
+
+    def getRanks(self, items, exclusive):
+        """getRank / getRankExclusive for many query items at once (same IEEE comparisons)."""
+        import numpy as np
+        t, w = self._output_arrays()
+        q = np.asarray(items, dtype=np.float64)[:, None]
+        with np.errstate(invalid="ignore"):
+            hit = (t[None, :] < q) if exclusive else ~(t[None, :] > q)
+        return (hit * w[None, :]).sum(axis=1)
 
     def quantiles(self, q):
         """QuantileNonSample.quantiles (A/QuantileNonSample.scala:249-281)."""
@@ -332,13 +350,15 @@ def bucket_distribution(state, numberOfBuckets):
     """KLLSketch.computeMetricFrom's body (A/KLLSketch.scala:121-146)."""
     sk = state.qSketch
     start, end = state.globalMin, state.globalMax
+    lows = [start + (end - start) * i / float(numberOfBuckets) for i in range(numberOfBuckets)]
+    highs = [start + (end - start) * (i + 1) / float(numberOfBuckets) for i in range(numberOfBuckets)]
+    ex_low = sk.getRanks(lows, exclusive=True) if numberOfBuckets else []
+    ex_high = sk.getRanks(highs, exclusive=True) if numberOfBuckets else []
     buckets = []
     for i in range(numberOfBuckets):
-        low = start + (end - start) * i / float(numberOfBuckets)
-        high = start + (end - start) * (i + 1) / float(numberOfBuckets)
         if i == numberOfBuckets - 1:
-            cnt = sk.getRank(high) - sk.getRankExclusive(low)
+            cnt = sk.getRank(highs[i]) - int(ex_low[i])
         else:
-            cnt = sk.getRankExclusive(high) - sk.getRankExclusive(low)
-        buckets.append(BucketValue(low, high, cnt))
+            cnt = int(ex_high[i]) - int(ex_low[i])
+        buckets.append(BucketValue(lows[i], highs[i], cnt))
     return BucketDistribution(buckets, [sk.shrinkingFactor, float(sk.sketchSize)], sk.getCompactorItems())

@@ -672,3 +672,64 @@ def kll_state_bytes(values, sketch_size=2048, shrinking_factor=0.64):
         out.append(struct.pack(">iii", nc, off, len(buf)))
         out.append(struct.pack(">%dd" % len(buf), *buf))
     return b"".join(out)
+
+
+# ---- Spark 2.2 string -> number casts (ColumnProfiler.castColumn, M/profiles/ColumnProfiler.scala:346-355) --
+
+def spark_string_to_long(s):
+    """UTF8String.toLong (spark-unsafe 2.2.2, third-party): no trimming, optional sign, digits, an optional
+    '.' followed by digits only (truncated), overflow -> None."""
+    b = s.encode("utf-8")
+    if not b:
+        return None
+    neg = b[0:1] == b"-"
+    i = 1 if b[0:1] in (b"-", b"+") else 0
+    if i == 1 and len(b) == 1:
+        return None
+    digits = []
+    while i < len(b):
+        c = b[i]
+        i += 1
+        if c == ord("."):
+            break
+        if not 48 <= c <= 57:
+            return None
+        digits.append(c - 48)
+    while i < len(b):
+        if not 48 <= b[i] <= 57:
+            return None
+        i += 1
+    v = 0
+    for d in digits:
+        v = v * 10 + d
+    v = -v if neg else v
+    if not -(1 << 63) <= v < (1 << 63):
+        return None
+    return v
+
+
+_JAVA_DOUBLE = None
+
+
+def java_parse_double(s):
+    """java.lang.Double.parseDouble for decimal literals (String.trim of chars <= ' ', optional sign,
+    NaN / Infinity, digits with an optional point, optional exponent, optional f/F/d/D suffix); the value
+    is Python's correctly rounded float() of the same digits. Returns None where Java throws."""
+    import re
+    global _JAVA_DOUBLE
+    if _JAVA_DOUBLE is None:
+        _JAVA_DOUBLE = re.compile(r"([+-]?)(NaN|Infinity|(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?)[fFdD]?\Z")
+    t = s
+    i, j = 0, len(t)
+    while i < j and ord(t[i]) <= 32:
+        i += 1
+    while j > i and ord(t[j - 1]) <= 32:
+        j -= 1
+    m = _JAVA_DOUBLE.match(t[i:j])
+    if not m:
+        return None
+    body = m.group(2)
+    if body == "NaN":
+        return float("nan")
+    v = float("inf") if body == "Infinity" else float(body)
+    return -v if m.group(1) == "-" else v

@@ -4,6 +4,7 @@
          x, y ~ sum-of-uniforms normals, 1 % nulls)                                  24.4 B/row
   c4     Uniqueness / Distinctness / UniqueValueRatio / CountDistinct / Entropy on 1e9 int64 keys with
          exactly 1e8 distinct (5e7 x 19 + 5e7 x 1), checked against the closed forms   8 B/row (+ table)
+  kll    KLLSketch(x) (sketch 2048, shrinking 0.64) over 1e9 fp64 rows [kll_nulls: 1 % nulls]  8 B/row
   suite10  the north-star "10-analyzer" fused scan: C2 columns + Compliance(c_i > 0), ApproxCountDistinct(c_i),
          Correlation(c_2k, c_2k+1)                                                    65 B/row
 
@@ -26,7 +27,7 @@ PEAK = 8000.0
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", required=True, choices=["c3", "c4", "suite10", "s10_nocorr", "corr4", "hll8", "c2"])
+    ap.add_argument("--config", required=True, choices=["c3", "c4", "suite10", "s10_nocorr", "corr4", "hll8", "c2", "kll", "kll_nulls"])
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--distinct", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=5)
@@ -78,6 +79,11 @@ def main():
         if args.config == "corr4":
             analyzers += [D.Correlation(names[2 * i], names[2 * i + 1]) for i in range(4)]
         bytes_per_row = 8 * (8 + 1 / 8)
+    elif args.config in ("kll", "kll_nulls"):
+        # KLLSketch (default sketch 2048 / 0.64) over one fp64 column, N(100, 15^2)
+        t = Table([col("x", 3, 0x5EED0003, N.TYPE_DOUBLE, nulls=args.config == "kll_nulls")])
+        analyzers = [D.KLLSketch("x")]
+        bytes_per_row = 8 + (1 / 8 if args.config == "kll_nulls" else 0)
     elif args.config == "suite10":
         t = bench.build_shard(torch, N, ctx, 0, R, dev)
         names = list(t.columns)
@@ -124,7 +130,7 @@ def main():
                         "UniqueValueRatio": got["UniqueValueRatio"] == 0.5, "CountDistinct": got["CountDistinct"] == Dn,
                         "Entropy_rel_err": abs(got["Entropy"] - exact_ent) / exact_ent}
     else:
-        out["sample_metrics"] = {repr(a): res.metric(a).value.get() for a in analyzers[:3]}
+        out["sample_metrics"] = {repr(a): repr(res.metric(a).value.get())[:200] for a in analyzers[:3]}
     print(json.dumps(out), flush=True)
 
 
