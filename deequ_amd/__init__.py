@@ -21,6 +21,8 @@ from .runners import (AnalysisRunner, KLLRunner, AnalysisRunBuilder, AnalyzerCon
 from .checks import (Check, CheckLevel, CheckStatus, ConstraintStatus, ConstrainableDataTypes, VerificationSuite,
                      VerificationResult)
 from .table import Table, Column
+from .profiles import (ColumnProfiler, ColumnProfilerRunner, ColumnProfilerRunBuilder, ColumnProfiles,
+                       StandardColumnProfile, NumericColumnProfile, DataTypeInstances)
 from . import distributed
 
 __all__ = [n for n in dir() if not n.startswith("_")]

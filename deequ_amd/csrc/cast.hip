@@ -1,4 +1,4 @@
-// cast.hip — Spark Cast of a STRING column to LONG / DOUBLE on gfx950 (one lane per row).
+// cast.hip — Spark Cast of a column to LONG / DOUBLE on gfx950 (one lane per row).
 //
 // Replaces ColumnProfiler.castColumn (M/profiles/ColumnProfiler.scala:346-355, called from
 // castNumericStringColumns :427-445 for columns whose DataType pass inferred Integral / Fractional):
@@ -21,32 +21,73 @@ namespace dq {
 
 constexpr int kCastBlock = 256;
 
+// Numeric sources: element kind + decimal scale (Spark Decimal, compact form: value = unscaled / 10^scale).
+struct CastSource {
+    const void* values;
+    const uint8_t* bytes;      // STRING
+    const int32_t* offsets;    // STRING
+    const uint64_t* validity;
+    int32_t elem;              // ET_* (ET_NONE for STRING)
+    int32_t decimal_scale;
+    int64_t pow10;             // 10^scale
+};
+
+// java (long) of a double: NaN -> 0, saturating (Scala Double.toLong, Spark 2.2 Cast double -> long).
+__device__ __forceinline__ int64_t java_d2l(double d) {
+    if (d != d) return 0;
+    if (d >= 9223372036854775807.0) return INT64_MAX;
+    if (d <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)d;
+}
+
+template <bool STRING>
 __global__ void __launch_bounds__(kCastBlock)
-cast_strings_kernel(const uint8_t* __restrict__ bytes, const int32_t* __restrict__ offsets,
-                    const uint64_t* __restrict__ validity, int64_t nrows, int to_double, void* __restrict__ values_out,
-                    uint64_t* __restrict__ validity_out, unsigned int* __restrict__ slow_flag) {
+cast_kernel(CastSource c, int64_t nrows, int to_double, void* __restrict__ values_out,
+            uint64_t* __restrict__ validity_out, unsigned int* __restrict__ slow_flag) {
     const int64_t stride = (int64_t)gridDim.x * kCastBlock;
     for (int64_t base = (int64_t)blockIdx.x * kCastBlock; base < nrows; base += stride) {
         const int64_t r = base + threadIdx.x;
         bool ok = false;
-        if (r < nrows && (validity == nullptr || ((validity[r >> 6] >> (r & 63)) & 1ull))) {
-            const int32_t o = offsets[r];
-            const int len = offsets[r + 1] - o;
-            const uint8_t* s = bytes + o;
-            if (to_double) {
-                double d = 0.0;
-                bool slow = false;
-                ok = java_parse_double(s, len, d, slow);
-                if (slow) atomicOr(slow_flag, 1u);
-                static_cast<double*>(values_out)[r] = ok ? d : 0.0;
+        double d = 0.0;
+        int64_t v = 0;
+        if (r < nrows && (c.validity == nullptr || ((c.validity[r >> 6] >> (r & 63)) & 1ull))) {
+            if (STRING) {
+                const int32_t o = c.offsets[r];
+                const int len = c.offsets[r + 1] - o;
+                const uint8_t* s = c.bytes + o;
+                if (to_double) {
+                    bool slow = false;
+                    ok = java_parse_double(s, len, d, slow);
+                    if (slow) atomicOr(slow_flag, 1u);
+                } else {
+                    ok = spark_string_to_long(s, len, v);
+                }
             } else {
-                int64_t v = 0;
-                ok = spark_string_to_long(s, len, v);
-                static_cast<int64_t*>(values_out)[r] = ok ? v : 0;
+                ok = true;
+                switch (c.elem) {
+                    case ET_F64: d = static_cast<const double*>(c.values)[r]; v = java_d2l(d); break;
+                    case ET_F32: d = (double)static_cast<const float*>(c.values)[r]; v = java_d2l(d); break;
+                    case ET_I64: {
+                        const int64_t x = static_cast<const int64_t*>(c.values)[r];
+                        if (c.decimal_scale) {  // Decimal.toDouble / Decimal.toLong (truncating)
+                            d = (double)x / (double)c.pow10;
+                            v = x / c.pow10;
+                        } else {
+                            d = (double)x;
+                            v = x;
+                        }
+                        break;
+                    }
+                    case ET_I32: v = static_cast<const int32_t*>(c.values)[r]; d = (double)v; break;
+                    case ET_I16: v = static_cast<const int16_t*>(c.values)[r]; d = (double)v; break;
+                    case ET_I8: v = static_cast<const int8_t*>(c.values)[r]; d = (double)v; break;
+                    default: v = static_cast<const uint8_t*>(c.values)[r] ? 1 : 0; d = (double)v; break;
+                }
             }
-        } else if (r < nrows) {
-            if (to_double) static_cast<double*>(values_out)[r] = 0.0;
-            else static_cast<int64_t*>(values_out)[r] = 0;
+        }
+        if (r < nrows) {
+            if (to_double) static_cast<double*>(values_out)[r] = ok ? d : 0.0;
+            else static_cast<int64_t*>(values_out)[r] = ok ? v : 0;
         }
         const unsigned long long ball = __ballot(ok);
         if ((threadIdx.x & 63) == 0 && r < nrows) validity_out[r >> 6] = ball;
@@ -82,54 +123,81 @@ struct CBuffers {
 
 extern "C" {
 
-int dq_cast_strings(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_dev,
-                    uint8_t* validity_dev) {
+int dq_cast_column(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_dev,
+                   uint8_t* validity_dev) {
     if (!ctx || !column || nrows < 0 || column->length != nrows || (nrows > 0 && (!values_dev || !validity_dev)))
-        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_cast_strings: invalid arguments");
-    if (column->spark_type != DQ_TYPE_STRING || !column->offsets)
-        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_cast_strings: column is not a string column");
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_cast_column: invalid arguments");
+    const int t = column->spark_type;
+    const bool is_string = t == DQ_TYPE_STRING;
+    if (is_string && !column->offsets)
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_cast_column: string column without offsets");
+    if (!is_string && !(t == DQ_TYPE_BOOLEAN || t == DQ_TYPE_BYTE || t == DQ_TYPE_SHORT || t == DQ_TYPE_INT ||
+                        t == DQ_TYPE_LONG || t == DQ_TYPE_FLOAT || t == DQ_TYPE_DOUBLE || t == DQ_TYPE_DECIMAL))
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_cast_column: source type cannot be cast to a number here");
+    if (t == DQ_TYPE_DECIMAL && (column->decimal_precision > 18 || column->decimal_scale < 0 || column->decimal_scale > 18))
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_cast_column: decimal precision > 18 unsupported");
     if (to_type != DQ_TYPE_LONG && to_type != DQ_TYPE_DOUBLE)
-        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_cast_strings: target type must be LONG or DOUBLE");
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_cast_column: target type must be LONG or DOUBLE");
     if (((uintptr_t)values_dev & 7) || ((uintptr_t)validity_dev & 7))
-        return dq::ctx_fail(ctx, DQ_ERR_ALIGNMENT, "dq_cast_strings: output buffers must be 8-B aligned");
+        return dq::ctx_fail(ctx, DQ_ERR_ALIGNMENT, "dq_cast_column: output buffers must be 8-B aligned");
     if (nrows == 0) return DQ_OK;
     CA_HIP(ctx, hipSetDevice(dq::ctx_device(ctx)));
     hipStream_t s = dq::ctx_stream(ctx);
     CBuffers buf;
-    const uint8_t* bytes = (const uint8_t*)column->values;
-    const int32_t* offs = column->offsets;
-    const uint64_t* valid = (const uint64_t*)column->validity;
-    if (!(column->flags & DQ_COL_DEVICE)) {
-        const int32_t total = column->offsets[nrows];
+    dq::CastSource c;
+    memset(&c, 0, sizeof(c));
+    c.elem = is_string ? dq::ET_NONE : dq::elem_of(t);
+    c.decimal_scale = t == DQ_TYPE_DECIMAL ? column->decimal_scale : 0;
+    c.pow10 = 1;
+    for (int i = 0; i < c.decimal_scale; ++i) c.pow10 *= 10;
+    if (column->flags & DQ_COL_DEVICE) {
+        c.values = column->values;
+        c.bytes = (const uint8_t*)column->values;
+        c.offsets = column->offsets;
+        c.validity = (const uint64_t*)column->validity;
+    } else {
         void *b = nullptr, *o = nullptr, *m = nullptr;
-        CA_HIP(ctx, buf.alloc(&b, (size_t)total + 16));
-        CA_HIP(ctx, buf.alloc(&o, sizeof(int32_t) * (size_t)(nrows + 1)));
-        if (total > 0) CA_HIP(ctx, hipMemcpyAsync(b, column->values, (size_t)total, hipMemcpyHostToDevice, s));
-        CA_HIP(ctx, hipMemcpyAsync(o, column->offsets, sizeof(int32_t) * (size_t)(nrows + 1), hipMemcpyHostToDevice, s));
+        if (is_string) {
+            const int32_t total = column->offsets[nrows];
+            CA_HIP(ctx, buf.alloc(&b, (size_t)total + 16));
+            CA_HIP(ctx, buf.alloc(&o, sizeof(int32_t) * (size_t)(nrows + 1)));
+            if (total > 0) CA_HIP(ctx, hipMemcpyAsync(b, column->values, (size_t)total, hipMemcpyHostToDevice, s));
+            CA_HIP(ctx, hipMemcpyAsync(o, column->offsets, sizeof(int32_t) * (size_t)(nrows + 1), hipMemcpyHostToDevice, s));
+        } else {
+            const size_t vb = (size_t)nrows * dq::elem_size(c.elem);
+            CA_HIP(ctx, buf.alloc(&b, vb));
+            CA_HIP(ctx, hipMemcpyAsync(b, column->values, vb, hipMemcpyHostToDevice, s));
+        }
         if (column->validity) {
             const size_t bb = (size_t)(nrows + 63) / 64 * 8;
             CA_HIP(ctx, buf.alloc(&m, bb));
             CA_HIP(ctx, hipMemsetAsync(m, 0, bb, s));
             CA_HIP(ctx, hipMemcpyAsync(m, column->validity, (size_t)(nrows + 7) / 8, hipMemcpyHostToDevice, s));
         }
-        bytes = (const uint8_t*)b;
-        offs = (const int32_t*)o;
-        valid = (const uint64_t*)m;
+        c.values = b;
+        c.bytes = (const uint8_t*)b;
+        c.offsets = (const int32_t*)o;
+        c.validity = (const uint64_t*)m;
     }
     unsigned int* dslow = nullptr;
     CA_HIP(ctx, buf.alloc((void**)&dslow, sizeof(unsigned int)));
     CA_HIP(ctx, hipMemsetAsync(dslow, 0, sizeof(unsigned int), s));
     const int64_t blocks = (nrows + dq::kCastBlock - 1) / dq::kCastBlock;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)dq::ctx_cus(ctx) * 16));
-    hipLaunchKernelGGL(dq::cast_strings_kernel, dim3(grid), dim3(dq::kCastBlock), 0, s, bytes, offs, valid, nrows,
-                       to_type == DQ_TYPE_DOUBLE ? 1 : 0, values_dev, (uint64_t*)validity_dev, dslow);
+    const int to_double = to_type == DQ_TYPE_DOUBLE ? 1 : 0;
+    if (is_string)
+        hipLaunchKernelGGL(dq::cast_kernel<true>, dim3(grid), dim3(dq::kCastBlock), 0, s, c, nrows, to_double, values_dev,
+                           (uint64_t*)validity_dev, dslow);
+    else
+        hipLaunchKernelGGL(dq::cast_kernel<false>, dim3(grid), dim3(dq::kCastBlock), 0, s, c, nrows, to_double,
+                           values_dev, (uint64_t*)validity_dev, dslow);
     CA_HIP(ctx, hipGetLastError());
     unsigned int slow = 0;
     CA_HIP(ctx, hipMemcpyAsync(&slow, dslow, sizeof(slow), hipMemcpyDeviceToHost, s));
     CA_HIP(ctx, hipStreamSynchronize(s));
     if (slow)
         return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED,
-                            "dq_cast_strings: a value needs the arbitrary-precision path of Double.parseDouble "
+                            "dq_cast_column: a value needs the arbitrary-precision path of Double.parseDouble "
                             "(hexadecimal literal, or > 19 significant digits on a rounding boundary)");
     return DQ_OK;
 }

@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "dq_abi_version", "dq_open", "dq_close", "dq_last_error", "dq_set_stream", "dq_synchronize", "dq_scan",
     "dq_scan_launch_count", "dq_state_merge", "dq_state_fold", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
     "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
-    "dq_quantile_summary", "dq_kll_sketch", "dq_cast_strings", "dq_synth_column", "dq_synth_freq_keys",
+    "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity",
 )
 
@@ -172,7 +172,7 @@ def load_library(path=None):
                                               c_void_p, c_void_p]),
             "dq_kll_sketch": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_int32, ctypes.c_double, c_void_p,
                                         c_int64]),
-            "dq_cast_strings": (c_int, [c_void_p, c_void_p, c_int64, ctypes.c_int32, c_void_p, c_void_p]),
+            "dq_cast_column": (c_int, [c_void_p, c_void_p, c_int64, ctypes.c_int32, c_void_p, c_void_p]),
             "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
             "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
             "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),
@@ -312,11 +312,11 @@ class Context:
                 return buf[:n].tobytes()
             cap = int(n)
 
-    def cast_strings(self, column, nrows, to_type, values_dev_ptr, validity_dev_ptr):
-        """dq_cast_strings: Spark Cast(string -> long | double) into caller-owned device buffers."""
-        self.check(self.lib.dq_cast_strings(self.handle, ctypes.byref(column), int(nrows), int(to_type),
+    def cast_column(self, column, nrows, to_type, values_dev_ptr, validity_dev_ptr):
+        """dq_cast_column: Spark Cast(column -> long | double) into caller-owned device buffers."""
+        self.check(self.lib.dq_cast_column(self.handle, ctypes.byref(column), int(nrows), int(to_type),
                                             ctypes.c_void_p(values_dev_ptr), ctypes.c_void_p(validity_dev_ptr)),
-                   "dq_cast_strings")
+                   "dq_cast_column")
 
     def synth_column(self, kind, seed, row0, nrows, dev_ptr):
         self.check(self.lib.dq_synth_column(self.handle, kind, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows,

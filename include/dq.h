@@ -273,14 +273,16 @@ int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows,
 int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t sketch_size,
                       double shrinking_factor, uint8_t* state_out, int64_t capacity);
 
-/* ColumnProfiler.castColumn (M/profiles/ColumnProfiler.scala:346-355): Spark 2.2 Cast of a STRING column to
- * LONG (UTF8String.toLong: no trimming, optional sign, digits, optional '.' + digits truncated, overflow NULL) or
- * DOUBLE (java.lang.Double.parseDouble, correctly rounded); NULL rows and strings that do not parse become NULL.
- * values_dev receives nrows x 8 B, validity_dev ceil(nrows / 64) x 8 B (LSB-first bitmap); both device memory,
- * 8-B aligned. Returns DQ_OK, or DQ_ERR_UNSUPPORTED when a string needs Double.parseDouble's arbitrary-precision
- * path (hexadecimal literal, or more than 19 significant digits on a rounding boundary) — never a silent guess. */
-int dq_cast_strings(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_dev,
-                    uint8_t* validity_dev);
+/* ColumnProfiler.castColumn (M/profiles/ColumnProfiler.scala:346-355): Spark 2.2 Cast of a column to LONG or
+ * DOUBLE. STRING sources: UTF8String.toLong (no trimming, optional sign, digits, optional '.' + digits truncated,
+ * overflow NULL) / java.lang.Double.parseDouble (correctly rounded); strings that do not parse become NULL.
+ * Numeric sources: integers sign-extend / convert, FLOAT/DOUBLE -> LONG as Java's (long) (NaN 0, saturating),
+ * DECIMAL(p <= 18) -> Decimal.toLong (truncating) / Decimal.toDouble, BOOLEAN -> 0/1. values_dev receives nrows x 8 B,
+ * validity_dev ceil(nrows / 64) x 8 B (LSB-first bitmap); both device memory, 8-B aligned. Returns DQ_OK, or
+ * DQ_ERR_UNSUPPORTED when a string needs Double.parseDouble's arbitrary-precision path (hexadecimal literal, or
+ * more than 19 significant digits on a rounding boundary) — never a silent guess. */
+int dq_cast_column(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_dev,
+                   uint8_t* validity_dev);
 
 /* Multi-GPU grouping: the canonical 64-bit keys (see DQ_FREQ_KEYS_VALUES) of one
  * fixed-width column's non-NULL rows, bucketed by owner rank = (mix64(key) >> 32) % nparts, written

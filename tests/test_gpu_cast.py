@@ -1,4 +1,4 @@
-"""GPU parity of dq_cast_strings (cast.hip + dq_parse.h) against the oracle's restatements of Spark 2.2's
+"""GPU parity of dq_cast_column (cast.hip + dq_parse.h) against the oracle's restatements of Spark 2.2's
 Cast(string -> long) (UTF8String.toLong) and Cast(string -> double) (java.lang.Double.parseDouble, whose
 correctly rounded value is Python's float() of the same digits). Bar: bit-exact values and identical
 NULLs. Strings with more than 19 significant digits either match or fail loudly (DQ_ERR_UNSUPPORTED)."""
@@ -23,7 +23,7 @@ def gpu_cast(strings, to_type, device=False):
     n = len(strings)
     vals = torch.empty(max(n, 1), dtype=torch.float64 if to_type == N.TYPE_DOUBLE else torch.int64, device="cuda")
     mask = torch.zeros(max((n + 63) // 64, 1) * 8, dtype=torch.uint8, device="cuda")
-    engine.ctx().cast_strings(t["s"].native(), n, to_type, vals.data_ptr(), mask.data_ptr())
+    engine.ctx().cast_column(t["s"].native(), n, to_type, vals.data_ptr(), mask.data_ptr())
     ok = unpack_validity(mask.cpu().numpy(), n)
     return vals.cpu().numpy()[:n], ok, valid
 
