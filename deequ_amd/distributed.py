@@ -136,6 +136,11 @@ class GpuLocal:
         ctx.synchronize()  # the scan runs on the context's stream; order it before torch reads `out`
         return out[:nops * N.STATE_SIZE], list(res.quantiles)
 
+    def kll_state(self, shard, column, sketch_size, shrinking_factor):
+        """This shard's KLLState bytes (one partition, rows in order)."""
+        from .runners import KLLRunner
+        return KLLRunner.sketch_column(shard, column, sketch_size, shrinking_factor).toBytes()
+
     def partition(self, column, world):
         import torch
         ctx = engine.ctx()
@@ -230,7 +235,11 @@ class DistributedAnalysisRunner:
                 results[a] = a.toFailureMetric(e)
             else:
                 passed.append(a)
-        shareable = [a for a in passed if isinstance(a, ScanShareableAnalyzer)]
+        from .analyzers import KLLSketch
+        kll = [a for a in passed if isinstance(a, KLLSketch)]
+        shareable = [a for a in passed if isinstance(a, ScanShareableAnalyzer) and not isinstance(a, KLLSketch)]
+        if kll:
+            self._kll_metrics(shard, kll, results)
         if shareable:
             try:
                 batch = ScanBatch(shard)
@@ -273,6 +282,31 @@ class DistributedAnalysisRunner:
             for a in group:
                 results[a] = self._grouping_metric(a, freq)
         return AnalyzerContext(results)
+
+    def _kll_metrics(self, shard, analyzers, results):
+        """KLLRunner.computeKLLSketchesInExtraPass (R/KLLRunner.scala:91-116) over row shards: each rank
+        sketches its shard as one partition (dq_kll_sketch), the KLLState bytes are all-gathered and merged
+        in rank order with KLLState.sum — the reference's treeReduce over partition sketches."""
+        from .kll import KLLState, DEFAULT_SKETCH_SIZE, DEFAULT_SHRINKING_FACTOR
+        params = {}
+        for a in analyzers:
+            params[a.column] = a.kllParameters
+        merged = {}
+        for column, p in params.items():
+            size, f = (p.sketchSize, p.shrinkingFactor) if p is not None else \
+                (DEFAULT_SKETCH_SIZE, DEFAULT_SHRINKING_FACTOR)
+            try:
+                blob = self.local.kll_state(shard, column, size, f)
+                acc = None
+                for b in self.ex.all_gather_blobs(blob):
+                    st = KLLState.fromBytes(b)
+                    acc = st if acc is None else acc.sum(st)
+                merged[column] = acc
+            except Exception as e:
+                merged[column] = e
+        for a in analyzers:
+            st = merged[a.column]
+            results[a] = a.toFailureMetric(st) if isinstance(st, Exception) else a.calculateMetric(st)
 
     def _frequencies(self, shard, cols):
         if len(cols) != 1 or shard[cols[0]].spark_type == N.TYPE_STRING:

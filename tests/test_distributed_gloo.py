@@ -72,6 +72,12 @@ class OracleLocal:
                 digests.append(PercentileDigest.from_order_statistics(rel, s[r - 1], r, len(s)))
         return torch.frombuffer(bytearray(raw or b"\0"), dtype=torch.uint8)[:len(raw)], digests
 
+    def kll_state(self, shard, column, sketch_size, shrinking_factor):
+        import oracle as O
+        c = shard[column]
+        vals = np.asarray(c.values, dtype=np.float64)[unpack_validity(c.validity, c.length)]
+        return O.kll_state_bytes(vals, sketch_size, shrinking_factor)
+
     def partition(self, column, world):
         valid = unpack_validity(column.validity, column.length)
         keys = canonical_keys(column)[valid]
@@ -120,7 +126,8 @@ def analyzers():
             D.Compliance("big", "x > 5", "k < 150"), D.Mean("y", "k > 20"),
             D.Uniqueness(["k"]), D.Distinctness(["k"]), D.Entropy("k"), D.CountDistinct(["k"]),
             D.UniqueValueRatio(["k"]), D.Histogram("d", None, 10), D.Uniqueness(["d"]),
-            D.ApproxQuantile("x", 0.5), D.ApproxQuantile("y", 0.9, 0.05), D.ApproxQuantiles("y", [0.1, 0.5])]
+            D.ApproxQuantile("x", 0.5), D.ApproxQuantile("y", 0.9, 0.05), D.ApproxQuantiles("y", [0.1, 0.5]),
+            D.KLLSketch("x", D.KLLParameters(64, 0.64, 10)), D.KLLSketch("k")]
 
 
 def _worker(rank, world, port, q):
@@ -144,6 +151,9 @@ def _worker(rank, world, port, q):
                 out[repr(a)] = (d.numberOfBins, sorted((k, v.absolute) for k, v in d.values.items()))
             elif isinstance(a, D.ApproxQuantiles):
                 out[repr(a)] = dict(m.value.get())
+            elif isinstance(a, D.KLLSketch):
+                bd = m.value.get()
+                out[repr(a)] = ([(b.lowValue, b.highValue, b.count) for b in bd.buckets], bd.data)
             else:
                 out[repr(a)] = m.value.get()
         q.put((rank, out))
@@ -207,6 +217,21 @@ def test_distributed_runner_matches_single_table_oracle(world):
                    "Entropy": s["entropy"], "CountDistinct": float(s["num_groups"]),
                    "UniqueValueRatio": s["num_unique"] / s["num_groups"]}[name]
             assert abs(g - exp) <= 1e-12 * max(1.0, abs(exp)), (a, g, exp)
+            continue
+        if name == "KLLSketch":
+            # partition sketches (the sequential oracle per rank shard) merged in rank order
+            from deequ_amd.kll import KLLState, bucket_distribution
+            c = t[a.column]
+            valid = unpack_validity(c.validity, c.length)
+            per = (t.nrows + world - 1) // world
+            acc = None
+            for r in range(world):
+                seg = np.asarray(c.values, dtype=np.float64)[r * per:(r + 1) * per][valid[r * per:(r + 1) * per]]
+                st = KLLState.fromBytes(O.kll_state_bytes(seg, a.sketchSize, a.shrinkingFactor))
+                acc = st if acc is None else acc.sum(st)
+            bd = bucket_distribution(acc, a.numberOfBuckets)
+            assert g[0] == [(b.lowValue, b.highValue, b.count) for b in bd.buckets], a
+            assert g[1] == bd.data and sum(b[2] for b in g[0]) == int(valid.sum()), a
             continue
         st = O.expected_state(t, a, exact=True)
         exp = O.hll_count(st.words) if name == "ApproxCountDistinct" else st.metricValue()

@@ -26,7 +26,7 @@ def _analyzers():
     return [D.Size(), D.Completeness("x"), D.Mean("x"), D.Sum("k"), D.Minimum("y"), D.Maximum("k"),
             D.StandardDeviation("x"), D.Correlation("x", "y"), D.ApproxCountDistinct("k"),
             D.Compliance("big", "x > 5", "k < 150"), D.Uniqueness(["k"]), D.Distinctness(["k"]), D.Entropy("k"),
-            D.CountDistinct(["k"]), D.UniqueValueRatio(["k"]), D.Histogram("d", None, 10)]
+            D.CountDistinct(["k"]), D.UniqueValueRatio(["k"]), D.Histogram("d", None, 10), D.KLLSketch("x")]
 
 
 def _worker(rank, world, port, q):
@@ -49,6 +49,9 @@ def _worker(rank, world, port, q):
             if isinstance(a, D.Histogram):
                 d = m.value.get()
                 out[repr(a)] = (d.numberOfBins, sorted((k, v.absolute) for k, v in d.values.items()))
+            elif isinstance(a, D.KLLSketch):
+                bd = m.value.get()
+                out[repr(a)] = ([(b.lowValue, b.highValue, b.count) for b in bd.buckets], bd.data)
             else:
                 out[repr(a)] = m.value.get()
         q.put((rank, out))
@@ -76,6 +79,20 @@ def test_two_ranks_on_one_gpu_match_single_gpu_run():
         g = res[0][repr(a)]
         assert g == res[1][repr(a)], a
         m = single.metric(a).value.get()
+        if isinstance(a, D.KLLSketch):
+            # two partition sketches merged in rank order (KLLRunner's treeReduce)
+            from deequ_amd.kll import bucket_distribution
+            t = _table()
+            per = (t.nrows + 1) // 2
+            halves = []
+            for r in range(2):
+                mask = np.zeros(t.nrows, dtype=bool)
+                mask[r * per:(r + 1) * per] = True
+                halves.append(D.runners.KLLRunner.sketch_column(t.select_rows(mask), "x", 2048, 0.64))
+            bd = bucket_distribution(halves[0].sum(halves[1]), 100)
+            assert g[0] == [(b.lowValue, b.highValue, b.count) for b in bd.buckets] and g[1] == bd.data
+            assert sum(b[2] for b in g[0]) == sum(b.count for b in m.buckets)
+            continue
         if isinstance(a, D.Histogram):
             assert g[0] == m.numberOfBins
             assert sorted(c for _, c in g[1]) == sorted(v.absolute for v in m.values.values())
