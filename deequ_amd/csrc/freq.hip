@@ -53,6 +53,9 @@ constexpr int kMaxKeys = 16;
 constexpr uint64_t kEmpty = ~0ull;
 constexpr int kSizingRegs = 4096;  // HLL registers used only to size the table
 constexpr int kFreqBlock = 256;
+constexpr int kDigitBins = 256;    // radix partition: first pass on the low 8 bits of the key
+constexpr int kPartTile = 4096;    // keys per workgroup tile of the partition scatters (16 per lane)
+constexpr int kPass2Item = 65536;  // keys per work item of the second partition pass
 constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (fixed: deterministic partials)
 constexpr int kRegion = 4096;      // slots per bucket region (the LDS table of one workgroup)
 // Distinct keys per bucket the bucket count aims at (load <= ~0.63). rocPRIM sorts 8 bits per pass
@@ -242,26 +245,44 @@ __device__ __forceinline__ void chunk_of(int64_t nrows, int64_t& r0, int64_t& r1
 
 __global__ void __launch_bounds__(kFreqBlock)
 extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__ block_keep,
-                     unsigned int* __restrict__ regs, Counters* __restrict__ ctr) {
+                     uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, unsigned int* __restrict__ hist1) {
     __shared__ unsigned int lds[kSizingRegs];
+    __shared__ unsigned int dh[kDigitBins];
     __shared__ unsigned long long red[kFreqBlock / 64];
     for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock) lds[i] = 0;
+    for (int i = threadIdx.x; i < kDigitBins; i += kFreqBlock) dh[i] = 0;
     __syncthreads();
-    int64_t r0, r1;
-    chunk_of(nrows, r0, r1);
     unsigned long long taken = 0, sent = 0, nulls = 0, kept = 0;
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += kFreqBlock) {
-        uint64_t h;
-        bool ng;
-        if (!row_key(ks, r, h, ng)) continue;
-        ++taken;
-        if (ng) { ++nulls; continue; }
-        if (h == kEmpty) { ++sent; continue; }
-        ++kept;
-        // h is already a mixed 64-bit key (splitmix64 finalizer / fingerprint): use its bits directly
-        const unsigned int idx = (unsigned int)(h >> 52);
-        const unsigned int rank = (unsigned int)__clzll((long long)((h << 12) | (1ull << 11))) + 1u;
-        if (rank > lds[idx]) atomicMax(&lds[idx], rank);
+    constexpr int U = 4;  // rows in flight per lane
+    // tiles of kPartTile rows interleaved over the workgroups (tile g, g + G, ...): all workgroups stream
+    // through one narrow address window, as the partition scatter that replays the same tiles does
+    const int64_t ntiles = (nrows + kPartTile - 1) / kPartTile;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
+    for (int64_t rb = tile * kPartTile + threadIdx.x, r1 = min((tile + 1) * (int64_t)kPartTile, nrows); rb < r1;
+         rb += (int64_t)kFreqBlock * U) {
+        uint64_t hv[U];
+        bool ok[U], ngv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = rb + (int64_t)u * kFreqBlock;
+            ngv[u] = false;
+            hv[u] = 0;
+            ok[u] = r < r1 && row_key(ks, r, hv[u], ngv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            ++taken;
+            if (ngv[u]) { ++nulls; continue; }
+            const uint64_t h = hv[u];
+            if (h == kEmpty) { ++sent; continue; }
+            ++kept;
+            // h is already a mixed 64-bit key (splitmix64 finalizer / fingerprint): use its bits directly
+            const unsigned int idx = (unsigned int)(h >> 52);
+            const unsigned int rank = (unsigned int)__clzll((long long)((h << 12) | (1ull << 11))) + 1u;
+            if (rank > lds[idx]) atomicMax(&lds[idx], rank);
+            if (hist1) atomicAdd(&dh[(unsigned int)h & (kDigitBins - 1)], 1u);
+        }
     }
     taken = block_sum_u64(taken, red);
     sent = block_sum_u64(sent, red);
@@ -273,21 +294,39 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
         if (sent) atomicAdd(&ctr->sentinel, sent);
         if (nulls) atomicAdd(&ctr->nulls, nulls);
     }
-    for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock)
-        if (lds[i]) atomicMax(&regs[i], lds[i]);
+    // this workgroup's sizing registers, one byte each; sizing_reduce_kernel takes the max over workgroups
+    // (a global atomicMax per register per workgroup contends on 4096 addresses)
+    for (int i = threadIdx.x; i < kSizingRegs / 4; i += kFreqBlock) {
+        const unsigned int w = lds[4 * i] | (lds[4 * i + 1] << 8) | (lds[4 * i + 2] << 16) | (lds[4 * i + 3] << 24);
+        reinterpret_cast<unsigned int*>(regs_part + (uint64_t)blockIdx.x * kSizingRegs)[i] = w;
+    }
+    if (hist1)
+        for (int i = threadIdx.x; i < kDigitBins; i += kFreqBlock) hist1[(uint64_t)blockIdx.x * kDigitBins + i] = dh[i];
 }
 
-// Pass 1b (write): the same chunks again; keys (and row indices) compacted in row order at the
+// Max over workgroups of the per-workgroup sizing registers: grid (kSizingRegs / 256, G), each thread
+// folds a run of workgroups for one register.
+__global__ void __launch_bounds__(256)
+sizing_reduce_kernel(const uint8_t* __restrict__ regs_part, int ngroups, unsigned int* __restrict__ regs) {
+    const int reg = blockIdx.x * 256 + threadIdx.x;
+    const int per = (ngroups + gridDim.y - 1) / gridDim.y;
+    const int g0 = blockIdx.y * per, g1 = min(ngroups, g0 + per);
+    unsigned int m = 0;
+    for (int g = g0; g < g1; ++g) m = max(m, (unsigned int)regs_part[(uint64_t)g * kSizingRegs + reg]);
+    if (m) atomicMax(&regs[reg], m);
+}
+
+// Pass 1b (write): the same tiles again; keys (and row indices) compacted in tile order at the
 // workgroup's offset — no shared counter, deterministic layout.
 __global__ void __launch_bounds__(kFreqBlock)
 extract_write_kernel(KeySpec ks, int64_t nrows, const unsigned long long* __restrict__ block_off,
                      unsigned long long* __restrict__ hs, unsigned long long* __restrict__ rows) {
     __shared__ unsigned int wave_cnt[kFreqBlock / 64];
-    int64_t r0, r1;
-    chunk_of(nrows, r0, r1);
     unsigned long long base = block_off[blockIdx.x];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t t0 = r0; t0 < r1; t0 += kFreqBlock) {
+    const int64_t ntiles = (nrows + kPartTile - 1) / kPartTile;  // the count pass's tiles
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
+    for (int64_t t0 = tile * kPartTile, r1 = min(t0 + (int64_t)kPartTile, nrows); t0 < r1; t0 += kFreqBlock) {
         const int64_t r = t0 + threadIdx.x;
         uint64_t h = 0;
         bool ng = false;
@@ -326,6 +365,247 @@ __global__ void bucket_bounds_kernel(const unsigned long long* __restrict__ hs, 
     bounds[b] = lo;
 }
 
+
+// ---- radix partition (replaces extract-write + a device radix sort) -------------------------------
+// Pass 1 scatters every kept key into one of 256 partitions by its low 8 bits, straight from the rows
+// (the count pass above already produced each workgroup's per-digit counts). Pass 2 splits each
+// partition by the next (bits - 8) bits. Both scatters stage a 4096-key tile in LDS ordered by digit, so
+// the global writes are runs per digit rather than single scattered words. Within a digit the order is
+// the arrival order through LDS atomics — irrelevant to the per-bucket aggregation that follows.
+
+// Per digit d: exclusive prefix over workgroups of hist[g][d] -> off[g][d], and the digit total.
+__global__ void __launch_bounds__(256)
+digit_scan_kernel(const unsigned int* __restrict__ hist, int ngroups, int nbins, unsigned long long* __restrict__ off,
+                  unsigned long long* __restrict__ totals) {
+    __shared__ unsigned long long part[256];
+    const int d = blockIdx.x;
+    // each thread owns a contiguous run of groups
+    const int per = (ngroups + 255) / 256;
+    const int g0 = threadIdx.x * per, g1 = min(ngroups, g0 + per);
+    unsigned long long sum = 0;
+    for (int g = g0; g < g1; ++g) sum += hist[(uint64_t)g * nbins + d];
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // inclusive Hillis-Steele scan over the 256 thread sums
+        const unsigned long long v = threadIdx.x >= o ? part[threadIdx.x - o] : 0ull;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned long long run = threadIdx.x ? part[threadIdx.x - 1] : 0ull;
+    for (int g = g0; g < g1; ++g) {
+        off[(uint64_t)g * nbins + d] = run;
+        run += hist[(uint64_t)g * nbins + d];
+    }
+    if (threadIdx.x == 255) totals[d] = part[255];
+}
+
+// One tile (<= kPartTile keys in registers, digit per key) -> LDS staging ordered by digit -> global
+// runs at cursor[digit]. `bins` <= BINS. Returns after the cursors advanced.
+template <int BINS, bool GENERAL>
+__device__ __forceinline__ void scatter_tile(const uint64_t (&h)[kPartTile / kFreqBlock],
+                                             const uint64_t (&rw)[kPartTile / kFreqBlock], const bool (&keep)[kPartTile / kFreqBlock],
+                                             int shift, unsigned int mask, unsigned int* hist, unsigned int* start,
+                                             unsigned long long* cursor, unsigned long long* sh, unsigned long long* sr,
+                                             unsigned long long* __restrict__ out_h, unsigned long long* __restrict__ out_r) {
+    constexpr int PER = kPartTile / kFreqBlock;
+    unsigned int rank[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+        rank[j] = keep[j] ? atomicAdd(&hist[(unsigned int)(h[j] >> shift) & mask], 1u) : 0u;
+    __syncthreads();
+    // exclusive scan of hist -> start: each thread sums a run of BINS / 256 bins, wave-level inclusive
+    // scan of the run sums (shuffles), then the 4 wave totals
+    constexpr int RUN = BINS / kFreqBlock > 0 ? BINS / kFreqBlock : 1;
+    __shared__ unsigned int wsum[kFreqBlock / 64];
+    unsigned int total;
+    {
+        const int b0 = threadIdx.x * RUN;
+        unsigned int acc = 0;
+#pragma unroll
+        for (int b = 0; b < RUN; ++b) acc += hist[b0 + b];
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        unsigned int inc = acc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int v = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        unsigned int run = inc - acc;
+        total = 0;
+#pragma unroll
+        for (int w = 0; w < kFreqBlock / 64; ++w) {
+            if (w < wave) run += wsum[w];
+            total += wsum[w];
+        }
+#pragma unroll
+        for (int b = 0; b < RUN; ++b) {
+            start[b0 + b] = run;
+            run += hist[b0 + b];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (!keep[j]) continue;
+        const unsigned int at = start[(unsigned int)(h[j] >> shift) & mask] + rank[j];
+        sh[at] = h[j];
+        if (GENERAL) sr[at] = rw[j];
+    }
+    __syncthreads();
+    for (unsigned int i = threadIdx.x; i < total; i += kFreqBlock) {
+        const unsigned long long hv = sh[i];
+        const unsigned int d = (unsigned int)(hv >> shift) & mask;
+        const unsigned long long pos = cursor[d] + (i - start[d]);
+        out_h[pos] = hv;
+        if (GENERAL) out_r[pos] = sr[i];
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < BINS; b += kFreqBlock) {
+        cursor[b] += hist[b];
+        hist[b] = 0;
+    }
+    __syncthreads();
+}
+
+// Pass 1: rows -> 256 partitions (same workgroup chunks as extract_count_kernel).
+template <bool GENERAL>
+__global__ void __launch_bounds__(kFreqBlock)
+partition1_kernel(KeySpec ks, int64_t nrows, const unsigned long long* __restrict__ off1,
+                  const unsigned long long* __restrict__ totals, unsigned long long* __restrict__ out_h,
+                  unsigned long long* __restrict__ out_r) {
+    constexpr int PER = kPartTile / kFreqBlock;
+    __shared__ unsigned int hist[kDigitBins], start[kDigitBins];
+    __shared__ unsigned long long cursor[kDigitBins];
+    __shared__ unsigned long long sh[kPartTile];
+    __shared__ unsigned long long sr[GENERAL ? kPartTile : 1];
+    {
+        // cursor[d] = (exclusive scan of the digit totals)[d] + this workgroup's offset inside digit d
+        __shared__ unsigned long long tot[kDigitBins];
+        tot[threadIdx.x] = totals[threadIdx.x];
+        hist[threadIdx.x] = 0;
+        __syncthreads();
+        for (int o = 1; o < kDigitBins; o <<= 1) {
+            const unsigned long long v = threadIdx.x >= o ? tot[threadIdx.x - o] : 0ull;
+            __syncthreads();
+            tot[threadIdx.x] += v;
+            __syncthreads();
+        }
+        cursor[threadIdx.x] = (threadIdx.x ? tot[threadIdx.x - 1] : 0ull) + off1[(uint64_t)blockIdx.x * kDigitBins + threadIdx.x];
+        __syncthreads();
+    }
+    const int64_t ntiles = (nrows + kPartTile - 1) / kPartTile;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * kPartTile, r1 = min(t0 + (int64_t)kPartTile, nrows);
+        uint64_t h[PER], rw[PER];
+        bool keep[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int64_t r = t0 + (int64_t)j * kFreqBlock + threadIdx.x;
+            bool ng = false;
+            h[j] = 0;
+            keep[j] = r < r1 && row_key(ks, r, h[j], ng) && !ng && h[j] != kEmpty;
+            rw[j] = (unsigned long long)r;
+        }
+        scatter_tile<kDigitBins, GENERAL>(h, rw, keep, 0, kDigitBins - 1, hist, start, cursor, sh, sr, out_h, out_r);
+    }
+}
+
+struct Pass2Item {
+    unsigned long long begin, end;  // range in the pass-1 output (inside one partition)
+};
+
+// Pass 2 count: per work item, histogram of the second digit.
+template <int BINS>
+__global__ void __launch_bounds__(kFreqBlock)
+count2_kernel(const Pass2Item* __restrict__ items, const unsigned long long* __restrict__ hs, int shift, unsigned int mask,
+              unsigned int* __restrict__ cnt) {
+    __shared__ unsigned int hist[BINS];
+    for (int b = threadIdx.x; b < BINS; b += kFreqBlock) hist[b] = 0;
+    __syncthreads();
+    const Pass2Item it = items[blockIdx.x];
+    for (unsigned long long i = it.begin + threadIdx.x; i < it.end; i += kFreqBlock)
+        atomicAdd(&hist[(unsigned int)(hs[i] >> shift) & mask], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < BINS; b += kFreqBlock) cnt[(uint64_t)blockIdx.x * BINS + b] = hist[b];
+}
+
+// Pass 2 offsets, one workgroup per partition: for each bin, exclusive prefix over the partition's items;
+// bins laid out in order inside the partition. Writes off[item][bin] (absolute) and each bucket's range
+// (bucket = partition + 256 * bin, i.e. the low `bits` bits of its keys).
+template <int BINS>
+__global__ void __launch_bounds__(kFreqBlock)
+scan2_kernel(const unsigned int* __restrict__ cnt, const int* __restrict__ part_items, const unsigned long long* __restrict__ part_begin,
+             int nbins, unsigned long long* __restrict__ off, unsigned long long* __restrict__ bstart,
+             unsigned long long* __restrict__ bcount) {
+    __shared__ unsigned long long tot[BINS];
+    __shared__ unsigned long long runsum[kFreqBlock];
+    const int p = blockIdx.x;
+    const int i0 = part_items[p], i1 = part_items[p + 1];
+    for (int b = threadIdx.x; b < nbins; b += kFreqBlock) {
+        unsigned long long run = 0;
+        for (int i = i0; i < i1; ++i) {
+            const unsigned int c = cnt[(uint64_t)i * BINS + b];
+            off[(uint64_t)i * BINS + b] = run;
+            run += c;
+        }
+        tot[b] = run;
+    }
+    __syncthreads();
+    constexpr int RUN = BINS / kFreqBlock > 0 ? BINS / kFreqBlock : 1;
+    const int b0 = threadIdx.x * RUN;
+    unsigned long long acc = 0;
+    for (int b = b0; b < b0 + RUN && b < nbins; ++b) acc += tot[b];
+    runsum[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 1; o < kFreqBlock; o <<= 1) {
+        const unsigned long long v = threadIdx.x >= o ? runsum[threadIdx.x - o] : 0ull;
+        __syncthreads();
+        runsum[threadIdx.x] += v;
+        __syncthreads();
+    }
+    unsigned long long base = part_begin[p] + (threadIdx.x ? runsum[threadIdx.x - 1] : 0ull);
+    for (int b = b0; b < b0 + RUN && b < nbins; ++b) {
+        const uint64_t bucket = (uint64_t)p + (uint64_t)kDigitBins * b;
+        bstart[bucket] = base;
+        bcount[bucket] = tot[b];
+        for (int i = i0; i < i1; ++i) off[(uint64_t)i * BINS + b] += base;
+        base += tot[b];
+    }
+}
+
+// Pass 2 scatter: per work item, keys (and rows) -> their bucket's range.
+template <int BINS, bool GENERAL>
+__global__ void __launch_bounds__(kFreqBlock)
+scatter2_kernel(const Pass2Item* __restrict__ items, const unsigned long long* __restrict__ off, const unsigned long long* __restrict__ in_h,
+                const unsigned long long* __restrict__ in_r, int shift, unsigned int mask, unsigned long long* __restrict__ out_h,
+                unsigned long long* __restrict__ out_r) {
+    constexpr int PER = kPartTile / kFreqBlock;
+    __shared__ unsigned int hist[BINS], start[BINS];
+    __shared__ unsigned long long cursor[BINS];
+    __shared__ unsigned long long sh[kPartTile];
+    __shared__ unsigned long long sr[GENERAL ? kPartTile : 1];
+    const Pass2Item it = items[blockIdx.x];
+    for (int b = threadIdx.x; b < BINS; b += kFreqBlock) {
+        hist[b] = 0;
+        cursor[b] = off[(uint64_t)blockIdx.x * BINS + b];
+    }
+    __syncthreads();
+    for (unsigned long long t0 = it.begin; t0 < it.end; t0 += kPartTile) {
+        uint64_t h[PER], rw[PER];
+        bool keep[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const unsigned long long i = t0 + (unsigned long long)j * kFreqBlock + threadIdx.x;
+            keep[j] = i < it.end;
+            h[j] = keep[j] ? __builtin_nontemporal_load(&in_h[i]) : 0ull;
+            rw[j] = (GENERAL && keep[j]) ? in_r[i] : 0ull;
+        }
+        scatter_tile<BINS, GENERAL>(h, rw, keep, shift, mask, hist, start, cursor, sh, sr, out_h, out_r);
+    }
+}
 
 struct BuildItem {
     unsigned long long begin, end;  // range of the sorted keys
@@ -664,24 +944,203 @@ struct DevBuf {  // scratch device buffers of one build, released on every path
 // extract (+ sizing) -> radix sort on `bits` bits of the keys -> per-bucket LDS aggregation.
 // A bucket whose distinct keys overflow its region (or a fingerprint collision on the general
 // path) restarts the sort/build with more bucket bits (or a new seed).
+// Aggregates the bucketed keys (bucket b = keys[bstart[b], bstart[b] + bcount[b])) into one region per
+// bucket. Returns DQ_OK with *overflow / *collision set from the device counters.
+int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, const unsigned long long* sorted,
+                  const unsigned long long* srows, const std::vector<unsigned long long>& bstart,
+                  const std::vector<unsigned long long>& bcount, int bits, bool* overflow, bool* collision) {
+    hipStream_t s = dq::ctx_stream(ctx);
+    const bool general = !t->fast;
+    const uint64_t nb = 1ull << bits;
+    std::vector<BuildItem> items;
+    items.reserve(nb);
+    for (uint64_t bk = 0; bk < nb; ++bk) {
+        const unsigned long long b0 = bstart[bk], b1 = b0 + bcount[bk];
+        if (b1 - b0 <= (unsigned long long)kSliceRows) {
+            items.push_back(BuildItem{b0, b1, (unsigned int)bk, 0u});
+            continue;
+        }
+        for (unsigned long long x = b0; x < b1; x += kSliceRows)
+            items.push_back(BuildItem{x, std::min<unsigned long long>(b1, x + kSliceRows), (unsigned int)bk, 1u});
+    }
+    const uint64_t cap = nb * kRegion;
+    if (t->slots) (void)hipFree(t->slots);
+    if (t->reps) (void)hipFree(t->reps);
+    t->slots = nullptr;
+    t->reps = nullptr;
+    if (hipMalloc(&t->slots, cap * sizeof(Slot)) != hipSuccess ||
+        (general && hipMalloc(&t->reps, cap * sizeof(unsigned long long)) != hipSuccess))
+        return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
+    t->cap = cap;
+    t->bits = bits;
+    BuildItem* ditems = nullptr;
+    FQ_HIP(ctx, buf.alloc((void**)&ditems, items.size() * sizeof(BuildItem)));
+    FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), items.size() * sizeof(BuildItem), hipMemcpyHostToDevice, s));
+    const int nitems = (int)items.size();
+    hipLaunchKernelGGL(region_init_kernel, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, nitems, t->slots, t->reps);
+    if (general)
+        hipLaunchKernelGGL(build_kernel<true>, dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, t->slots,
+                           t->reps, t->ctr);
+    else
+        hipLaunchKernelGGL(build_kernel<false>, dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, t->slots,
+                           t->reps, t->ctr);
+    FQ_HIP(ctx, hipGetLastError());
+    if (general && nrows > 0) {
+        const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
+        hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots, t->reps, bits,
+                           t->ctr);
+    }
+    FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    if (getenv("DQ_DEBUG_FREQ"))
+        fprintf(stderr, "[freq] rows=%lld bits=%d items=%zu rows_taken=%llu ovf=%llu mis=%llu\n", (long long)nrows, bits,
+                items.size(), t->host_ctr.num_rows, t->host_ctr.overflow, t->host_ctr.mismatch);
+    *overflow = t->host_ctr.overflow != 0;
+    *collision = t->host_ctr.mismatch != 0;
+    if (*overflow) {  // reset for the retry with more buckets
+        Counters c = t->host_ctr;
+        c.overflow = 0;
+        c.mismatch = 0;
+        FQ_HIP(ctx, hipMemcpyAsync(t->ctr, &c, sizeof(Counters), hipMemcpyHostToDevice, s));
+        FQ_HIP(ctx, hipStreamSynchronize(s));  // `c` lives on this stack frame
+    }
+    return DQ_OK;
+}
+
+// Radix-partition path (8 <= bits <= kMaxPartBits): rows -> 256 partitions (pass 1, fed by the count pass's
+// per-workgroup digit histograms) -> buckets (pass 2 on the next bits - 8 bits) -> regions.
+constexpr int kMaxPartBits = 20;
+
+int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, int xgrid, const unsigned int* hist1,
+                      unsigned long long n, int bits, bool* collision) {
+    hipStream_t s = dq::ctx_stream(ctx);
+    const bool general = !t->fast;
+    const size_t n_alloc = (size_t)std::max<unsigned long long>(n, 1);
+    unsigned long long *off1 = nullptr, *totals = nullptr, *h1 = nullptr, *r1 = nullptr;
+    FQ_HIP(ctx, buf.alloc((void**)&off1, sizeof(unsigned long long) * (size_t)xgrid * kDigitBins));
+    FQ_HIP(ctx, buf.alloc((void**)&totals, sizeof(unsigned long long) * kDigitBins));
+    FQ_HIP(ctx, buf.alloc((void**)&h1, n_alloc * 8));
+    if (general) FQ_HIP(ctx, buf.alloc((void**)&r1, n_alloc * 8));
+    hipLaunchKernelGGL(digit_scan_kernel, dim3(kDigitBins), dim3(256), 0, s, hist1, xgrid, kDigitBins, off1, totals);
+    if (general)
+        hipLaunchKernelGGL(partition1_kernel<true>, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
+                           (const unsigned long long*)off1, (const unsigned long long*)totals, h1, r1);
+    else
+        hipLaunchKernelGGL(partition1_kernel<false>, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
+                           (const unsigned long long*)off1, (const unsigned long long*)totals, h1, r1);
+    FQ_HIP(ctx, hipGetLastError());
+    std::vector<unsigned long long> tot(kDigitBins), pbegin(kDigitBins + 1, 0);
+    FQ_HIP(ctx, hipMemcpyAsync(tot.data(), totals, sizeof(unsigned long long) * kDigitBins, hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    for (int d = 0; d < kDigitBins; ++d) pbegin[d + 1] = pbegin[d] + tot[d];
+    unsigned long long *h2 = nullptr, *r2 = nullptr;
+    for (int grow = 0; grow < 8 && bits <= kMaxPartBits; ++grow, ++bits) {
+        std::vector<unsigned long long> bstart, bcount;
+        const unsigned long long *sorted = h1, *srows = r1;
+        if (bits == 8) {
+            bstart.assign(pbegin.begin(), pbegin.begin() + kDigitBins);
+            bcount = tot;
+        } else {
+            const int d2 = bits - 8;
+            const int bins = 1 << d2;
+            const bool big = bins > kDigitBins;
+            const int BINS = big ? 4096 : kDigitBins;
+            std::vector<Pass2Item> items;
+            std::vector<int> pitems(kDigitBins + 1, 0);
+            for (int p = 0; p < kDigitBins; ++p) {
+                pitems[p] = (int)items.size();
+                for (unsigned long long x = pbegin[p]; x < pbegin[p + 1]; x += kPass2Item)
+                    items.push_back(Pass2Item{x, std::min<unsigned long long>(pbegin[p + 1], x + kPass2Item)});
+            }
+            pitems[kDigitBins] = (int)items.size();
+            const int nitems = (int)items.size();
+            Pass2Item* ditems = nullptr;
+            int* dpitems = nullptr;
+            unsigned long long *dpbegin = nullptr, *off2 = nullptr, *dbstart = nullptr, *dbcount = nullptr;
+            unsigned int* cnt2 = nullptr;
+            const uint64_t nb = 1ull << bits;
+            FQ_HIP(ctx, buf.alloc((void**)&ditems, sizeof(Pass2Item) * std::max(nitems, 1)));
+            FQ_HIP(ctx, buf.alloc((void**)&dpitems, sizeof(int) * (kDigitBins + 1)));
+            FQ_HIP(ctx, buf.alloc((void**)&dpbegin, sizeof(unsigned long long) * kDigitBins));
+            FQ_HIP(ctx, buf.alloc((void**)&cnt2, sizeof(unsigned int) * (size_t)std::max(nitems, 1) * BINS));
+            FQ_HIP(ctx, buf.alloc((void**)&off2, sizeof(unsigned long long) * (size_t)std::max(nitems, 1) * BINS));
+            FQ_HIP(ctx, buf.alloc((void**)&dbstart, sizeof(unsigned long long) * nb));
+            FQ_HIP(ctx, buf.alloc((void**)&dbcount, sizeof(unsigned long long) * nb));
+            if (nitems)
+                FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), sizeof(Pass2Item) * nitems, hipMemcpyHostToDevice, s));
+            FQ_HIP(ctx, hipMemcpyAsync(dpitems, pitems.data(), sizeof(int) * (kDigitBins + 1), hipMemcpyHostToDevice, s));
+            FQ_HIP(ctx, hipMemcpyAsync(dpbegin, pbegin.data(), sizeof(unsigned long long) * kDigitBins, hipMemcpyHostToDevice, s));
+            if (!h2) {
+                FQ_HIP(ctx, buf.alloc((void**)&h2, n_alloc * 8));
+                if (general) FQ_HIP(ctx, buf.alloc((void**)&r2, n_alloc * 8));
+            }
+            const unsigned int mask = (unsigned int)bins - 1;
+            if (big) {
+                if (nitems) hipLaunchKernelGGL(count2_kernel<4096>, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, h1, 8, mask, cnt2);
+                hipLaunchKernelGGL(scan2_kernel<4096>, dim3(kDigitBins), dim3(kFreqBlock), 0, s, cnt2, dpitems, dpbegin, bins, off2,
+                                   dbstart, dbcount);
+                if (nitems && general)
+                    hipLaunchKernelGGL((scatter2_kernel<4096, true>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1, 8,
+                                       mask, h2, r2);
+                else if (nitems)
+                    hipLaunchKernelGGL((scatter2_kernel<4096, false>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1, 8,
+                                       mask, h2, r2);
+            } else {
+                if (nitems) hipLaunchKernelGGL(count2_kernel<kDigitBins>, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, h1, 8, mask, cnt2);
+                hipLaunchKernelGGL(scan2_kernel<kDigitBins>, dim3(kDigitBins), dim3(kFreqBlock), 0, s, cnt2, dpitems, dpbegin, bins,
+                                   off2, dbstart, dbcount);
+                if (nitems && general)
+                    hipLaunchKernelGGL((scatter2_kernel<kDigitBins, true>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1,
+                                       8, mask, h2, r2);
+                else if (nitems)
+                    hipLaunchKernelGGL((scatter2_kernel<kDigitBins, false>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1,
+                                       8, mask, h2, r2);
+            }
+            FQ_HIP(ctx, hipGetLastError());
+            bstart.resize(nb);
+            bcount.resize(nb);
+            FQ_HIP(ctx, hipMemcpyAsync(bstart.data(), dbstart, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, s));
+            FQ_HIP(ctx, hipMemcpyAsync(bcount.data(), dbcount, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, s));
+            FQ_HIP(ctx, hipStreamSynchronize(s));
+            sorted = h2;
+            srows = r2;
+        }
+        bool overflow = false;
+        const int rc = build_regions(ctx, t, nrows, buf, sorted, srows, bstart, bcount, bits, &overflow, collision);
+        if (rc != DQ_OK) return rc;
+        if (!overflow) return DQ_OK;
+    }
+    return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
+}
+
+// extract (+ sizing) -> bucketing on the low `bits` bits of the keys -> per-bucket LDS aggregation. Tables of
+// 8..20 bucket bits take the radix-partition path; the others compact the keys and sort them on the bucket
+// bits with rocPRIM. A bucket whose distinct keys overflow its region (or a fingerprint collision on the
+// general path) restarts with more bucket bits (or a new seed).
 int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
     hipStream_t s = dq::ctx_stream(ctx);
     DevBuf buf;
     const bool general = !t->fast;
+    const bool no_partition = getenv("DQ_FREQ_NO_PARTITION") != nullptr;
     for (int seed_attempt = 0; seed_attempt < 4; ++seed_attempt) {
         unsigned long long *hs = nullptr, *rows = nullptr, *bk = nullptr;
-        unsigned int* regs = nullptr;
+        unsigned int *regs = nullptr, *hist1 = nullptr;
+        uint8_t* regs_part = nullptr;
         const size_t n_alloc = (size_t)std::max<int64_t>(nrows, 1);
         const int xgrid = scan_grid((uint64_t)std::max<int64_t>(nrows, 1));
-        FQ_HIP(ctx, buf.alloc((void**)&hs, n_alloc * 8));
-        if (general) FQ_HIP(ctx, buf.alloc((void**)&rows, n_alloc * 8));
         FQ_HIP(ctx, buf.alloc((void**)&bk, 2 * sizeof(unsigned long long) * xgrid));
         FQ_HIP(ctx, buf.alloc((void**)&regs, kSizingRegs * sizeof(unsigned int)));
+        FQ_HIP(ctx, buf.alloc((void**)&regs_part, (size_t)kSizingRegs * xgrid));
+        FQ_HIP(ctx, buf.alloc((void**)&hist1, sizeof(unsigned int) * (size_t)xgrid * kDigitBins));
         FQ_HIP(ctx, hipMemsetAsync(bk, 0, 2 * sizeof(unsigned long long) * xgrid, s));
         FQ_HIP(ctx, hipMemsetAsync(regs, 0, kSizingRegs * sizeof(unsigned int), s));
         FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
-        if (nrows > 0)
-            hipLaunchKernelGGL(extract_count_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows, bk, regs, t->ctr);
+        if (nrows > 0) {
+            hipLaunchKernelGGL(extract_count_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows, bk, regs_part,
+                               t->ctr, hist1);
+            hipLaunchKernelGGL(sizing_reduce_kernel, dim3(kSizingRegs / 256, std::min(xgrid, 64)), dim3(256), 0, s,
+                               (const uint8_t*)regs_part, xgrid, regs);
+        }
         FQ_HIP(ctx, hipGetLastError());
         std::vector<unsigned int> hregs(kSizingRegs);
         std::vector<unsigned long long> hkeep(xgrid), hoff(xgrid);
@@ -693,20 +1152,32 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
             hoff[g] = n;
             n += hkeep[g];
         }
+        const double est = n ? hll_raw_estimate(hregs) : 0.0;
+        int bits = 0;
+        while (bits < 40 && est / (double)(1ull << bits) > (double)kRegionTarget) ++bits;
+        if (getenv("DQ_DEBUG_FREQ"))
+            fprintf(stderr, "[freq] rows=%lld n=%llu est=%.1f bits=%d\n", (long long)nrows, n, est, bits);
+        bool collision = false;
+        if (!no_partition && n > 0 && bits >= 8 && bits <= kMaxPartBits) {
+            const int rc = build_partitioned(ctx, t, nrows, buf, xgrid, hist1, n, bits, &collision);
+            if (rc != DQ_OK) return rc;
+            if (!collision) return DQ_OK;
+            t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
+            continue;
+        }
+        FQ_HIP(ctx, buf.alloc((void**)&hs, n_alloc * 8));
+        if (general) FQ_HIP(ctx, buf.alloc((void**)&rows, n_alloc * 8));
         if (nrows > 0) {
             FQ_HIP(ctx, hipMemcpyAsync(bk + xgrid, hoff.data(), sizeof(unsigned long long) * xgrid, hipMemcpyHostToDevice, s));
             hipLaunchKernelGGL(extract_write_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
                                (const unsigned long long*)(bk + xgrid), hs, rows);
             FQ_HIP(ctx, hipGetLastError());
         }
-        const double est = n ? hll_raw_estimate(hregs) : 0.0;
-        int bits = 0;
-        while (bits < 40 && est / (double)(1ull << bits) > (double)kRegionTarget) ++bits;
         unsigned long long *hs2 = nullptr, *rows2 = nullptr;
         FQ_HIP(ctx, buf.alloc((void**)&hs2, n_alloc * 8));
         if (general) FQ_HIP(ctx, buf.alloc((void**)&rows2, n_alloc * 8));
-        bool collision = false;
-        for (int grow = 0; grow < 8; ++grow, ++bits) {
+        bool overflow = true;
+        for (int grow = 0; grow < 8 && overflow; ++grow, ++bits) {
             // ---- sort on the low `bits` bits: each bucket becomes one contiguous run ----------------
             const unsigned long long* sorted = hs;
             const unsigned long long* srows = rows;
@@ -731,81 +1202,17 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
             FQ_HIP(ctx, buf.alloc((void**)&bounds, (nb + 1) * 8));
             hipLaunchKernelGGL(bucket_bounds_kernel, dim3((unsigned)((nb + 1 + 255) / 256)), dim3(256), 0, s, sorted,
                                (uint64_t)n, bits, nb, bounds);
-            std::vector<unsigned long long> hb(nb + 1);
+            std::vector<unsigned long long> hb(nb + 1), bstart(nb), bcount(nb);
             FQ_HIP(ctx, hipMemcpyAsync(hb.data(), bounds, (nb + 1) * 8, hipMemcpyDeviceToHost, s));
             FQ_HIP(ctx, hipStreamSynchronize(s));
-            if (getenv("DQ_DEBUG_FREQ")) {
-                std::vector<unsigned long long> hk(n);
-                (void)hipMemcpy(hk.data(), sorted, n * 8, hipMemcpyDeviceToHost);
-                uint64_t unsorted = 0, maxb = 0, bad_range = 0;
-                for (uint64_t i = 1; i < n; ++i)
-                    if (bits && (hk[i] & (nb - 1)) < (hk[i - 1] & (nb - 1))) ++unsorted;
-                for (uint64_t bk = 0; bk < nb; ++bk) {
-                    if (hb[bk + 1] < hb[bk]) ++bad_range;
-                    else maxb = std::max<uint64_t>(maxb, hb[bk + 1] - hb[bk]);
-                }
-                fprintf(stderr, "[freq] sort check bits=%d n=%llu unsorted=%llu bad_ranges=%llu max_bucket=%llu\n", bits,
-                        (unsigned long long)n, (unsigned long long)unsorted, (unsigned long long)bad_range,
-                        (unsigned long long)maxb);
+            for (uint64_t b = 0; b < nb; ++b) {
+                bstart[b] = hb[b];
+                bcount[b] = hb[b + 1] - hb[b];
             }
-            std::vector<BuildItem> items;
-            items.reserve(nb);
-            for (uint64_t bk = 0; bk < nb; ++bk) {
-                const unsigned long long b0 = hb[bk], b1 = hb[bk + 1];
-                const unsigned int split = (b1 - b0) > (unsigned long long)kSliceRows ? 1u : 0u;
-                if (!split) {
-                    items.push_back(BuildItem{b0, b1, (unsigned int)bk, 0u});
-                    continue;
-                }
-                for (unsigned long long x = b0; x < b1; x += kSliceRows)
-                    items.push_back(BuildItem{x, std::min<unsigned long long>(b1, x + kSliceRows), (unsigned int)bk, 1u});
-            }
-            // ---- table ---------------------------------------------------------------------------
-            const uint64_t cap = nb * kRegion;
-            if (t->slots) (void)hipFree(t->slots);
-            if (t->reps) (void)hipFree(t->reps);
-            t->slots = nullptr;
-            t->reps = nullptr;
-            if (hipMalloc(&t->slots, cap * sizeof(Slot)) != hipSuccess ||
-                (general && hipMalloc(&t->reps, cap * sizeof(unsigned long long)) != hipSuccess))
-                return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
-            t->cap = cap;
-            t->bits = bits;
-            BuildItem* ditems = nullptr;
-            FQ_HIP(ctx, buf.alloc((void**)&ditems, items.size() * sizeof(BuildItem)));
-            FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), items.size() * sizeof(BuildItem), hipMemcpyHostToDevice, s));
-            const int nitems = (int)items.size();
-            hipLaunchKernelGGL(region_init_kernel, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, nitems, t->slots, t->reps);
-            if (general)
-                hipLaunchKernelGGL(build_kernel<true>, dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows,
-                                   t->slots, t->reps, t->ctr);
-            else
-                hipLaunchKernelGGL(build_kernel<false>, dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows,
-                                   t->slots, t->reps, t->ctr);
-            FQ_HIP(ctx, hipGetLastError());
-            if (general && nrows > 0) {
-                const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
-                hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots, t->reps,
-                                   bits, t->ctr);
-            }
-            FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-            FQ_HIP(ctx, hipStreamSynchronize(s));
-            if (getenv("DQ_DEBUG_FREQ"))
-                fprintf(stderr, "[freq] rows=%lld n=%llu est=%.1f bits=%d items=%zu rows_taken=%llu ovf=%llu mis=%llu\n",
-                        (long long)nrows, n, est, bits, items.size(), t->host_ctr.num_rows, t->host_ctr.overflow,
-                        t->host_ctr.mismatch);
-            if (t->host_ctr.overflow) {  // a bucket held more distinct keys than its region: more buckets
-                Counters c = t->host_ctr;
-                c.overflow = 0;
-                c.mismatch = 0;
-                FQ_HIP(ctx, hipMemcpyAsync(t->ctr, &c, sizeof(Counters), hipMemcpyHostToDevice, s));
-                FQ_HIP(ctx, hipStreamSynchronize(s));  // `c` lives on this stack frame
-                continue;
-            }
-            collision = t->host_ctr.mismatch != 0;
-            break;
+            const int rc = build_regions(ctx, t, nrows, buf, sorted, srows, bstart, bcount, bits, &overflow, &collision);
+            if (rc != DQ_OK) return rc;
         }
-        if (t->host_ctr.overflow) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
+        if (overflow) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
         if (!collision) return DQ_OK;
         // 64-bit fingerprint collision on the general path: new seed, rebuild from scratch
         t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
