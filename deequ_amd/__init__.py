@@ -23,6 +23,7 @@ from .checks import (Check, CheckLevel, CheckStatus, ConstraintStatus, Constrain
 from .table import Table, Column
 from .profiles import (ColumnProfiler, ColumnProfilerRunner, ColumnProfilerRunBuilder, ColumnProfiles,
                        StandardColumnProfile, NumericColumnProfile, DataTypeInstances)
+from .state_provider import HdfsStateProvider, FileSystemStateProvider
 from . import distributed
 
 __all__ = [n for n in dir() if not n.startswith("_")]

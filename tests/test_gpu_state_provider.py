@@ -1,0 +1,71 @@
+"""T/analyzers/StateProviderTest.scala and StateAggregationIntegrationTest.scala on the GPU engine:
+states computed by the HIP kernels, persisted through HdfsStateProvider / InMemoryStateProvider,
+loaded back equal, and partition states merged with aggregateWith equal to a full-data run."""
+import pytest
+
+import deequ_amd as D
+from deequ_amd.runners import AnalysisRunner, Analysis
+from deequ_amd.table import Table
+
+pytestmark = pytest.mark.gpu
+
+
+def some_data():
+    # StateProviderTest.scala:226-238
+    rows = [("1", "a", 17, 1.3), ("2", None, 12, 76.0), ("3", "b", 15, 89.0), ("4", "b", 12, 12.7),
+            ("5", None, 1, 1.0), ("6", "a", 21, 78.0), ("7", None, 12, 0.0)]
+    return Table.from_rows(rows, ["item", "att1", "count", "price"], ["string", "string", "int", "double"])
+
+
+SCAN = [D.Size(), D.Completeness("att1"), D.Compliance("att1", "att1 = 'b'"), D.PatternMatch("att1", D.Patterns.EMAIL),
+        D.Sum("price"), D.Mean("price"), D.Minimum("price"), D.Maximum("price"), D.StandardDeviation("price"),
+        D.MaxLength("att1"), D.MinLength("att1"), D.DataType("item"), D.ApproxCountDistinct("att1"),
+        D.Correlation("count", "price")]
+FREQ = [D.Uniqueness("att1"), D.Uniqueness(["att1", "count"]), D.Entropy("att1")]
+
+
+@pytest.mark.parametrize("kind", ["memory", "filesystem"])
+def test_states_restore(kind, tmp_path):
+    data = some_data()
+    provider = D.InMemoryStateProvider() if kind == "memory" else D.HdfsStateProvider(None, str(tmp_path / "st"))
+    for a in SCAN:
+        state = a.computeStateFrom(data)
+        assert state is not None, a
+        provider.persist(a, state)
+        assert provider.load(a) == state, a
+    for a in FREQ:
+        state = a.computeStateFrom(data)
+        provider.persist(a, state)
+        back = provider.load(a)
+        assert back.numRows == state.numRows
+        assert set(back.as_dict().items()) == set(state.as_dict().items())
+    aq = D.ApproxQuantile("price", 0.5)
+    state = aq.computeStateFrom(data)
+    provider.persist(aq, state)
+    got, want = provider.load(aq).percentileDigest.quantileSummaries, state.percentileDigest.quantileSummaries
+    assert (got.compressThreshold, got.relativeError, got.count) == (want.compressThreshold, want.relativeError,
+                                                                     want.count)
+    assert got.sampled == want.sampled
+
+
+def test_partition_states_on_disk_aggregate_to_full_run(tmp_path):
+    """StateAggregationIntegrationTest: states of two partitions saved to disk; aggregateWith over
+    the second partition and runOnAggregatedStates both give the full-data metrics."""
+    data = some_data()
+    first = data.select_rows([True, True, True, False, False, False, False])
+    second = data.select_rows([False, False, False, True, True, True, True])
+    analyzers = [D.Size(), D.Completeness("att1"), D.Mean("price"), D.StandardDeviation("price"),
+                 D.Maximum("price"), D.ApproxCountDistinct("att1"), D.Uniqueness("att1"), D.Entropy("count")]
+    # one grouping analyzer per column set: a run persists only the head analyzer's frequency table
+    # (AnalysisRunner.scala:543) and HdfsStateProvider.load of any other one fails, as in the reference
+    p1 = D.HdfsStateProvider(None, str(tmp_path / "p1"))
+    p2 = D.HdfsStateProvider(None, str(tmp_path / "p2"))
+    AnalysisRunner.onData(first).addAnalyzers(analyzers).saveStatesWith(p1).run()
+    AnalysisRunner.onData(second).addAnalyzers(analyzers).saveStatesWith(p2).run()
+    full = AnalysisRunner.onData(data).addAnalyzers(analyzers).run()
+    incremental = AnalysisRunner.onData(second).addAnalyzers(analyzers).aggregateWith(p1).run()
+    merged = AnalysisRunner.runOnAggregatedStates(data.schema, Analysis(analyzers), [p1, p2])
+    for a in analyzers:
+        want = full.metric(a).value.get()
+        assert incremental.metric(a).value.get() == pytest.approx(want, rel=1e-12), a
+        assert merged.metric(a).value.get() == pytest.approx(want, rel=1e-12), a
