@@ -80,6 +80,33 @@ __device__ __forceinline__ void moments_merge(int64_t na, double& mean, double& 
     m2 = m2 + m2b + delta * deltaN * n1 * n2;
 }
 
+// Batch-path reciprocal: v_rcp_f64 plus two Newton steps (within 1 ulp) for 1/cnt and 1/n, since
+// the per-8-row fold would otherwise spend two full IEEE divisions (div_scale/rcp/fma/div_fmas/
+// div_fixup) per batch per column. The moments stay within the 1e-12 relative bound of the Spark per-row Welford order either way.
+__device__ __forceinline__ double rcp_refined(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-d, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+// moments_merge for the per-lane batch fold (nb >= 1 guaranteed by the caller).
+__device__ __forceinline__ void moments_merge_batch(int64_t na, double& mean, double& m2, int nb,
+                                                    double meanb, double m2b) {
+    if (na == 0) {
+        mean = meanb;
+        m2 = m2b;
+        return;
+    }
+    const double n1 = (double)na, n2 = (double)nb;
+    const double newN = n1 + n2;
+    const double delta = meanb - mean;
+    const double deltaN = delta * rcp_refined(newN);
+    mean = mean + deltaN * n2;
+    m2 = m2 + m2b + delta * deltaN * n1 * n2;
+}
+
 __device__ __forceinline__ void col_merge(ColPartial& a, const ColPartial& b) {
     moments_merge(a.n, a.mean, a.m2, b.n, b.mean, b.m2);
     a.n += b.n;
@@ -510,14 +537,14 @@ __device__ __forceinline__ void accumulate(FAcc& a, const uint64_t (&v)[8], uint
         a.mn = fmin(a.mn, mn);
         a.mx = fmax(a.mx, mx);
         if (flags & CF_MOMENTS) {
-            const double mb = s / (double)cnt;
+            const double mb = s * rcp_refined((double)cnt);
             double m2b = 0.0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const double d = as_f64(v[k]) - mb;
                 m2b += ((m >> k) & 1u) ? d * d : 0.0;
             }
-            moments_merge(a.n, a.mean, a.m2, cnt, mb, m2b);
+            moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
         }
     }
     a.n += cnt;
@@ -545,14 +572,14 @@ __device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) s += ((m >> k) & 1u) ? (double)(int64_t)v[k] : 0.0;
-        const double mb = s / (double)cnt;
+        const double mb = s * rcp_refined((double)cnt);
         double m2b = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const double d = (double)(int64_t)v[k] - mb;
             m2b += ((m >> k) & 1u) ? d * d : 0.0;
         }
-        moments_merge(a.n, a.mean, a.m2, cnt, mb, m2b);
+        moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
     }
     a.n += cnt;
 }
