@@ -156,6 +156,51 @@ def _column_from_pylist(name, spark_type, items):
     return Column(name, t, vals, validity)
 
 
+def _arrow_validity(arr, n):
+    if arr.null_count == 0:
+        return None
+    bits = np.frombuffer(arr.buffers()[0], dtype=np.uint8)
+    mask = np.unpackbits(bits, bitorder="little", count=arr.offset + n)[arr.offset:].astype(bool)
+    return pack_validity(mask)
+
+
+def _column_from_arrow(name, arr, pa):
+    t, n = arr.type, len(arr)
+    validity = _arrow_validity(arr, n)
+    if pa.types.is_dictionary(t):
+        return _column_from_arrow(name, arr.dictionary_decode(), pa)
+    if pa.types.is_large_string(t):
+        arr, t = arr.cast(pa.string()), pa.string()
+    if pa.types.is_string(t):
+        bufs = arr.buffers()
+        offs = np.frombuffer(bufs[1], dtype=np.int32)[arr.offset:arr.offset + n + 1]
+        data = np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None else np.zeros(0, np.uint8)
+        base = int(offs[0]) if n else 0
+        end = int(offs[-1]) if n else 0
+        return Column(name, N.TYPE_STRING, data[base:end], validity, (offs - base).astype(np.int32), length=n)
+    if pa.types.is_boolean(t):
+        bits = np.frombuffer(arr.buffers()[1], dtype=np.uint8)
+        vals = np.unpackbits(bits, bitorder="little", count=arr.offset + n)[arr.offset:].astype(np.uint8)
+        return Column(name, N.TYPE_BOOLEAN, vals, validity)
+    if pa.types.is_decimal(t):
+        if t.precision > 18:
+            raise ValueError("column %s: DecimalType(%d,%d) exceeds the 64-bit unscaled range"
+                             % (name, t.precision, t.scale))
+        unscaled = np.array([0 if v is None else int(v.scaleb(t.scale)) for v in arr.to_pylist()], dtype=np.int64)
+        return Column(name, N.TYPE_DECIMAL, unscaled, validity, decimal_precision=t.precision,
+                      decimal_scale=t.scale)
+    if pa.types.is_timestamp(t):
+        us = arr.cast(pa.timestamp("us", tz=t.tz), safe=False) if t.unit != "us" else arr
+        vals = np.frombuffer(us.buffers()[1], dtype=np.int64)[us.offset:us.offset + n]
+        return Column(name, N.TYPE_TIMESTAMP, vals, validity)
+    spark = {pa.int8(): N.TYPE_BYTE, pa.int16(): N.TYPE_SHORT, pa.int32(): N.TYPE_INT, pa.int64(): N.TYPE_LONG,
+             pa.float32(): N.TYPE_FLOAT, pa.float64(): N.TYPE_DOUBLE, pa.date32(): N.TYPE_DATE}.get(t)
+    if spark is None:
+        raise ValueError("column %s: Arrow type %s has no Spark counterpart here" % (name, t))
+    vals = np.frombuffer(arr.buffers()[1], dtype=NUMPY_OF[spark])[arr.offset:arr.offset + n]
+    return Column(name, spark, vals, validity)
+
+
 class Table:
     """Named columns of equal length (the DataFrame stand-in of the drop-in API)."""
 
@@ -227,6 +272,26 @@ class Table:
             else:
                 cols.append(_column_from_pylist(name, t, [None if x is None else int(x) for x in items]))
         return cls(cols)
+
+    @classmethod
+    def from_arrow(cls, table):
+        """pyarrow.Table (a Spark DataFrame collected through Arrow, or a parquet read) -> Table.
+        Fixed-width values and UTF-8 offsets/data are taken from the Arrow buffers without a
+        per-row pass; validity bitmaps are realigned to bit 0 and padded; booleans are widened to one
+        byte per row, timestamps normalised to Spark's microseconds, decimals (precision <= 18) to
+        unscaled longs."""
+        import pyarrow as pa
+        cols = []
+        for name, chunked in zip(table.column_names, table.columns):
+            arr = chunked.combine_chunks() if chunked.num_chunks != 1 else chunked.chunk(0)
+            cols.append(_column_from_arrow(name, arr, pa))
+        return cls(cols)
+
+    @classmethod
+    def from_parquet(cls, path, columns=None):
+        """Parquet file or directory -> Table (through pyarrow, then `from_arrow`)."""
+        import pyarrow.parquet as pq
+        return cls.from_arrow(pq.read_table(path, columns=columns))
 
     # ---- schema / access ------------------------------------------------------------------------
     @property
