@@ -51,32 +51,55 @@ def build_shard(torch, N, ctx, row0, nrows, dev):
     return Table(cols)
 
 
-def cpu_baseline(seconds, sample_rows):
-    """The oracle's Spark-order restatement (oracle/dq_oracle.c oracle_scan_spark), one thread, over a
-    bounded sample of the same synthetic columns; rows/s of the 8-column suite."""
+def cpu_baseline(seconds, sample_rows, threads=None):
+    """The oracle's Spark-order restatement (oracle/dq_oracle.c oracle_scan_spark) over a bounded
+    sample of the same synthetic columns, split into `threads` contiguous row partitions scanned
+    concurrently (Spark local[N]'s one-task-per-partition shape; ctypes releases the GIL). Rows/s of
+    the 8-column suite; the O(threads) state merge is not timed."""
+    import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     L = O.lib()
     L.oracle_scan_spark.restype = ctypes.c_int64
     L.oracle_scan_spark.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    if threads is None:
+        threads = min(16, int(os.environ.get("OMP_NUM_THREADS", 0)) or os.cpu_count() or 1)
+    threads = max(1, min(int(threads), sample_rows))
     cols = []
     for c, kind in enumerate(C2_KINDS):
         v = O.synth_column(kind, SEED + c, 0, sample_rows)
         m = O.synth_validity(SEED + 0x100 + c, 0, sample_rows, 10).astype(np.uint8)
         cols.append((7 if kind in (1, 2, 3) else 5, v, m))
-    out = np.zeros(5)
-    rows, t0 = 0, time.perf_counter()
-    while True:
-        for st, v, m in cols:
-            L.oracle_scan_spark(st, v.ctypes.data, m.ctypes.data, sample_rows, out.ctypes.data)
-        rows += sample_rows
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": rows / el, "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": "oracle_scan_spark over %d-row x 8-col sample of the C2 columns, %d passes in %.1f s "
-                      "(Spark-order count/sum/min/max/Welford; not deequ/Spark itself)"
-                      % (sample_rows, rows // sample_rows, el)}
+    bounds = [sample_rows * i // threads for i in range(threads + 1)]
+    done = [0] * threads
+    start = threading.Barrier(threads + 1)
+    deadline = [0.0]
+
+    def worker(i):
+        lo, hi = bounds[i], bounds[i + 1]
+        out = np.zeros(5)
+        start.wait()
+        while True:
+            for st, v, m in cols:
+                L.oracle_scan_spark(st, v[lo:].ctypes.data, m[lo:].ctypes.data, hi - lo, out.ctypes.data)
+            done[i] += hi - lo
+            if time.perf_counter() >= deadline[0]:
+                break
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    t0 = time.perf_counter()
+    deadline[0] = t0 + seconds
+    start.wait()
+    for t in ts:
+        t.join()
+    el = time.perf_counter() - t0
+    rows = sum(done)
+    return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": "oracle_scan_spark over a %d-row x 8-col sample of the C2 columns in %d row partitions "
+                      "(one host thread each), %.1f sample passes in %.1f s (Spark-order count/sum/min/max/"
+                      "Welford; not deequ/Spark itself)" % (sample_rows, threads, rows / sample_rows, el)}
 
 
 def measured_traffic(rows_per_gpu):
