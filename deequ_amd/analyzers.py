@@ -132,8 +132,10 @@ class Analyzer:
                 v = "List(%s)" % ", ".join(_java_double_to_string(x) if isinstance(x, float) else str(x) for x in v)
             elif v is None:
                 v = "None"
-            elif f == "where":
+            elif f in ("where", "binningUdf"):
                 v = "Some(%s)" % v
+            elif isinstance(v, float):
+                v = _java_double_to_string(v)  # Scala's Double.toString inside the case-class toString
             args.append(str(v))
         return "%s(%s)" % (type(self).__name__, ",".join(args))
 
@@ -580,6 +582,17 @@ class KLLSketch(ScanShareableAnalyzer):
 
 
 # ---- grouping analyzers (A/GroupingAnalyzers.scala) ----------------------------------------------
+def _canonical_group_key(key):
+    """A group key tuple with every float wrapped as engine.GroupFloat (bitwise equality, NaN canonical,
+    -0.0 != 0.0), so keys from device tables, persisted states and host dicts join exactly."""
+    if not isinstance(key, tuple):
+        key = (key,)
+    if any(isinstance(v, float) and not isinstance(v, engine.GroupFloat) for v in key):
+        return tuple(engine.GroupFloat(v) if isinstance(v, float) and not isinstance(v, engine.GroupFloat) else v
+                     for v in key)
+    return key
+
+
 class FrequenciesAndNumRows:
     """A/GroupingAnalyzers.scala:123-156. `frequencies` is a device (key -> count) table produced by
     dq_frequencies, or a host dict after a state merge (outer join with counts added)."""
@@ -595,10 +608,13 @@ class FrequenciesAndNumRows:
         return self.frequencies.to_dict()
 
     def sum(self, other):
-        """Null-safe full outer join on the keys, counts added (A/GroupingAnalyzers.scala:127-147)."""
-        merged = dict(self.as_dict())
-        for k, v in other.as_dict().items():
-            merged[k] = merged.get(k, 0) + v
+        """Null-safe full outer join on the keys, counts added (A/GroupingAnalyzers.scala:127-147). Keys are
+        compared with Spark's grouping equality (floating values bitwise, NaN canonical: GroupFloat)."""
+        merged = {}
+        for src in (self.as_dict(), other.as_dict()):
+            for k, v in src.items():
+                k = _canonical_group_key(k)
+                merged[k] = merged.get(k, 0) + v
         return FrequenciesAndNumRows(merged, self.numRows + other.numRows, self.columns)
 
     def summary(self, entropy_rows=None):
@@ -759,7 +775,13 @@ class Histogram(Analyzer):
     """A/Histogram.scala:41-117: counts per value (nulls as "NullValue"), top-N details."""
     NullFieldReplacement = "NullValue"
     MaximumAllowedDetailBins = 1000
-    _fields = ("column", "maxDetailBins")
+    # case class Histogram(column, binningUdf: Option[UserDefinedFunction], maxDetailBins): the UDF takes
+    # part in equality (by identity, as Scala compares the wrapped function object) and in toString
+    _fields = ("column", "binningUdf", "maxDetailBins")
+
+    def _key(self):
+        udf = None if self.binningUdf is None else ("udf", id(self.binningUdf))
+        return (type(self).__name__, self.column, udf, self.maxDetailBins)
 
     def __init__(self, column, binningUdf=None, maxDetailBins=MaximumAllowedDetailBins):
         self.column, self.binningUdf, self.maxDetailBins = column, binningUdf, maxDetailBins

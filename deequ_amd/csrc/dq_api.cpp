@@ -1051,7 +1051,7 @@ int64_t dq_spark_hash64(int32_t spark_type, const void* value, int64_t len) {
 }
 
 int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int64_t nrows, void* values_dev) {
-    if (!ctx || nrows < 0 || (!values_dev && nrows > 0) || kind < DQ_SYNTH_DYADIC || kind > DQ_SYNTH_GAUSS01)
+    if (!ctx || nrows < 0 || (!values_dev && nrows > 0) || kind < DQ_SYNTH_DYADIC || kind > DQ_SYNTH_GAUSS_CORR)
         return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_synth_column: invalid arguments");
     if (nrows == 0) return DQ_OK;
     DQ_HIP(ctx, hipSetDevice(ctx->device));

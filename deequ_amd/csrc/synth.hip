@@ -10,6 +10,8 @@
 
 namespace dq {
 
+constexpr uint64_t kSynthCorrNoise = 0x5A5A5A5A5A5A5A5AULL;
+
 __device__ __forceinline__ double sum12_u48(uint64_t seed, uint64_t row) {
     double s = 0.0;
 #pragma unroll
@@ -42,6 +44,13 @@ __global__ void synth_column_kernel(int kind, uint64_t seed, int64_t row0, int64
             case DQ_SYNTH_GAUSS01:
                 static_cast<double*>(out)[i] = __dsub_rn(sum12_u48(seed, row), 6.0);
                 break;
+            case DQ_SYNTH_GAUSS_CORR: {
+                // y = 0.6 x + 0.8 e: x = GAUSS01(seed), e = GAUSS01(seed ^ kCorrNoise) -> corr(x, y) ~ 0.6
+                const double x = __dsub_rn(sum12_u48(seed, row), 6.0);
+                const double e = __dsub_rn(sum12_u48(seed ^ kSynthCorrNoise, row), 6.0);
+                static_cast<double*>(out)[i] = __dadd_rn(__dmul_rn(0.6, x), __dmul_rn(0.8, e));
+                break;
+            }
             case DQ_SYNTH_INT32R:
                 static_cast<int64_t*>(out)[i] = (int64_t)(int32_t)(uint32_t)(h >> 32);
                 break;

@@ -37,7 +37,7 @@ P_ADD, P_SUB, P_MUL, P_DIV, P_MOD, P_NEG = 30, 31, 32, 33, 34, 35
 P_LIKE, P_LENGTH, P_CAST_DOUBLE, P_CAST_LONG, P_CAST_STRING_NUM, P_REGEX = 40, 41, 42, 43, 44, 45
 V_BOOL, V_LONG, V_DOUBLE, V_STRING = 1, 2, 3, 4
 
-SYNTH_DYADIC, SYNTH_UNIFORM, SYNTH_NORMAL, SYNTH_INT32R, SYNTH_KEY30, SYNTH_GAUSS01 = range(1, 7)
+SYNTH_DYADIC, SYNTH_UNIFORM, SYNTH_NORMAL, SYNTH_INT32R, SYNTH_KEY30, SYNTH_GAUSS01, SYNTH_GAUSS_CORR = range(1, 8)
 
 HLL_NUM_WORDS = 52
 

@@ -224,6 +224,7 @@ class HdfsStateProvider:
             columns = [n for n in names if n != COUNT_COL]
             cols = [t.column(n).to_pylist() for n in columns]
             for key, c in zip(zip(*cols), t.column(COUNT_COL).to_pylist()):
+                key = A._canonical_group_key(key)  # floating keys join bitwise (GroupFloat), as in device tables
                 freq[key] = freq.get(key, 0) + int(c)
         (num_rows,) = struct.unpack(">q", self._read(self._bin(ident, "-num_rows"))[:8])
         return A.FrequenciesAndNumRows(freq, num_rows, columns)

@@ -300,7 +300,9 @@ typedef enum dq_synth_kind {
     DQ_SYNTH_NORMAL = 3,   /* f64: 100 + 15 * (sum of 12 U[0,1) on a 2^-48 grid - 6)   */
     DQ_SYNTH_INT32R = 4,   /* i64: U[-2^31, 2^31)                                    */
     DQ_SYNTH_KEY30 = 5,    /* i64: splitmix64(row) mod 2^30                          */
-    DQ_SYNTH_GAUSS01 = 6   /* f64: sum of 12 U[0,1) on a 2^-48 grid - 6              */
+    DQ_SYNTH_GAUSS01 = 6,  /* f64: sum of 12 U[0,1) on a 2^-48 grid - 6              */
+    DQ_SYNTH_GAUSS_CORR = 7/* f64: 0.6 * GAUSS01(seed) + 0.8 * GAUSS01(seed ^ 0x5A5A5A5A5A5A5A5A):
+                            *      correlated (rho ~ 0.6) with the GAUSS01 column of the same seed */
 } dq_synth_kind;
 
 int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int64_t nrows,

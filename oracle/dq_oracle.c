@@ -23,6 +23,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "hll_bias_p9.h"
@@ -348,6 +349,10 @@ void oracle_synth_column(int kind, uint64_t seed, int64_t row0, int64_t n, void*
             case 4: ((int64_t*)out)[i] = (int64_t)(int32_t)(uint32_t)(h >> 32); break;
             case 5: ((int64_t*)out)[i] = (int64_t)(h & ((1ULL << 30) - 1)); break;
             case 6: ((double*)out)[i] = sum12(seed, row) - 6.0; break;
+            case 7: { volatile double x = sum12(seed, row) - 6.0;
+                      volatile double e = sum12(seed ^ 0x5A5A5A5A5A5A5A5AULL, row) - 6.0;
+                      volatile double a = 0.6 * x; volatile double b = 0.8 * e;
+                      ((double*)out)[i] = a + b; break; }
             default: break;
         }
     }
@@ -406,4 +411,228 @@ void oracle_synth_freq_keys(int64_t total, int64_t distinct, int64_t row0, int64
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
         out[i] = (int64_t)(z ^ (z >> 31));
     }
+}
+
+/* ---- streamed parity of the generated BASELINE workloads (C2 / suite10 / C3) -------------------
+ * The columns are regenerated row by row from the counter-based generators above (never held in
+ * memory), so 1e9-row configurations are checked in one pass over OpenMP threads. Everything the
+ * reference computes exactly is exact here: counts, Long sums (wrap-around), min/max, Compliance
+ * counts, HLL registers (XXH64 hashLong/hashInt, StatefulHyperloglogPlus.scala:89-112). Moments and
+ * correlation are the EXACT values (shifted sums in long double with Kahan-Babuska compensation),
+ * the yardstick the north star's 1e-12 tolerance is applied to; they restate what
+ * CentralMomentAgg / Corr converge to (StandardDeviation.scala:37-44, Correlation.scala:37-52). */
+typedef struct {
+    int32_t kind;        /* synth kind (1..7) */
+    int32_t spark_type;  /* T_DOUBLE or T_LONG */
+    uint64_t seed;
+    uint64_t vseed;      /* validity seed */
+    int32_t permille;    /* P(null) in 1/1000; < 0: no validity bitmap */
+    int32_t hll;         /* 1: HLL++ registers */
+    int32_t pred_gt0;    /* 1: Compliance(col > 0) count */
+    int32_t pad;
+} oracle_gen_spec;
+
+typedef struct {
+    int64_t n, nnan, isum, imin, imax, pred_true;
+    double dmin, dmax;
+    double ex_sum, ex_mean, ex_m2;
+    uint8_t regs[512];
+} oracle_gen_col;
+
+typedef struct {
+    double n, x_avg, y_avg, ck, x_mk, y_mk;
+} oracle_gen_corr;
+
+typedef struct { long double s, c; } kbn;
+static void kbn_add(kbn* a, long double x) {
+    const long double t = a->s + x;
+    if (fabsl(a->s) >= fabsl(x)) a->c += (a->s - t) + x;
+    else a->c += (x - t) + a->s;
+    a->s = t;
+}
+static long double kbn_val(const kbn* a) { return a->s + a->c; }
+
+/* One generated value: its raw 8 bytes, and its value cast to (long) double as Spark casts it. */
+static uint64_t synth_raw(int kind, uint64_t seed, uint64_t row) {
+    uint64_t v;
+    oracle_synth_column(kind, seed, (int64_t)row, 1, &v);
+    return v;
+}
+static long double raw_value(int spark_type, uint64_t raw) {
+    if (spark_type == T_DOUBLE) { double d; memcpy(&d, &raw, 8); return (long double)d; }
+    return (long double)(double)(int64_t)raw;
+}
+
+/* XXH64.hashLong / hashInt of the canonical value (C/StatefulHyperloglogPlus.scala:93). */
+static uint64_t hash_long(uint64_t v) {
+    uint64_t h = 42 + XP5 + 8;
+    h ^= rotl(v * XP2, 31) * XP1;
+    h = rotl(h, 27) * XP1 + XP4;
+    return avalanche(h);
+}
+
+typedef struct {
+    int64_t n, nnan, isum, imin, imax, pred_true;
+    double dmin, dmax;
+    int first;
+    kbn s1, s2, sum;
+    uint8_t regs[512];
+} gen_acc;
+
+typedef struct { int64_t n; kbn sx, sy, sxx, syy, sxy; } corr_acc;
+
+int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0, int64_t nrows, int npairs,
+                           const int32_t* pairs, int threads, oracle_gen_col* out, oracle_gen_corr* corr_out) {
+    if (ncols <= 0 || ncols > 64 || nrows <= 0) return -1;
+    long double shift[64];
+    for (int c = 0; c < ncols; ++c) shift[c] = raw_value(specs[c].spark_type, synth_raw(specs[c].kind, specs[c].seed, (uint64_t)row0));
+    gen_acc* acc = (gen_acc*)calloc((size_t)ncols, sizeof(gen_acc));
+    corr_acc* cacc = (corr_acc*)calloc((size_t)(npairs > 0 ? npairs : 1), sizeof(corr_acc));
+    if (!acc || !cacc) return -2;
+    for (int c = 0; c < ncols; ++c) {
+        acc[c].imin = INT64_MAX;
+        acc[c].imax = INT64_MIN;
+        acc[c].first = 1;
+    }
+    const int64_t chunk = 1 << 16;
+    const int64_t nchunks = (nrows + chunk - 1) / chunk;
+    if (threads <= 0) threads = 1;
+#pragma omp parallel num_threads(threads)
+    {
+        gen_acc* la = (gen_acc*)calloc((size_t)ncols, sizeof(gen_acc));
+        corr_acc* lc = (corr_acc*)calloc((size_t)(npairs > 0 ? npairs : 1), sizeof(corr_acc));
+        for (int c = 0; c < ncols; ++c) {
+            la[c].imin = INT64_MAX;
+            la[c].imax = INT64_MIN;
+            la[c].first = 1;
+        }
+        double* x = (double*)malloc(sizeof(double) * (size_t)ncols);
+        int* ok = (int*)malloc(sizeof(int) * (size_t)ncols);
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t k = 0; k < nchunks; ++k) {
+            const int64_t lo = row0 + k * chunk;
+            int64_t hi = lo + chunk;
+            if (hi > row0 + nrows) hi = row0 + nrows;
+            for (int64_t r = lo; r < hi; ++r) {
+                for (int c = 0; c < ncols; ++c) {
+                    const oracle_gen_spec* sp = &specs[c];
+                    ok[c] = sp->permille < 0 || (int)(oracle_splitmix64(sp->vseed, (uint64_t)r) % 1000ULL) >= sp->permille;
+                    if (!ok[c]) continue;
+                    const uint64_t raw = synth_raw(sp->kind, sp->seed, (uint64_t)r);
+                    double v;
+                    memcpy(&v, &raw, 8);
+                    gen_acc* a = &la[c];
+                    a->n++;
+                    if (sp->spark_type == T_DOUBLE) {
+                        if (v != v) a->nnan++;
+                        if (a->first || nan_gt(a->dmin, v)) a->dmin = v;
+                        if (a->first || nan_gt(v, a->dmax)) a->dmax = v;
+                        kbn_add(&a->sum, (long double)v);
+                        if (sp->pred_gt0 && (v > 0.0 || v != v)) a->pred_true++;
+                        if (sp->hll) hll_add(a->regs, hash_long(v == v ? raw : 0x7ff8000000000000ULL));
+                        x[c] = v;
+                    } else {
+                        const int64_t iv = (int64_t)raw;
+                        a->isum = (int64_t)((uint64_t)a->isum + (uint64_t)iv);
+                        if (iv < a->imin) a->imin = iv;
+                        if (iv > a->imax) a->imax = iv;
+                        if (sp->pred_gt0 && iv > 0) a->pred_true++;
+                        if (sp->hll) hll_add(a->regs, hash_long((uint64_t)iv));
+                        x[c] = (double)iv;
+                    }
+                    a->first = 0;
+                    const long double d = (long double)x[c] - shift[c];
+                    kbn_add(&a->s1, d);
+                    kbn_add(&a->s2, d * d);
+                }
+                for (int p = 0; p < npairs; ++p) {
+                    const int cx = pairs[2 * p], cy = pairs[2 * p + 1];
+                    if (!ok[cx] || !ok[cy]) continue;
+                    const long double kx = shift[cx], ky = shift[cy];
+                    const long double dx = (long double)x[cx] - kx, dy = (long double)x[cy] - ky;
+                    corr_acc* q = &lc[p];
+                    q->n++;
+                    kbn_add(&q->sx, dx);
+                    kbn_add(&q->sy, dy);
+                    kbn_add(&q->sxx, dx * dx);
+                    kbn_add(&q->syy, dy * dy);
+                    kbn_add(&q->sxy, dx * dy);
+                }
+            }
+        }
+#pragma omp critical
+        {
+            for (int c = 0; c < ncols; ++c) {
+                gen_acc* a = &acc[c];
+                const gen_acc* b = &la[c];
+                if (b->n == 0) continue;
+                a->n += b->n;
+                a->nnan += b->nnan;
+                a->pred_true += b->pred_true;
+                a->isum = (int64_t)((uint64_t)a->isum + (uint64_t)b->isum);
+                if (b->imin < a->imin) a->imin = b->imin;
+                if (b->imax > a->imax) a->imax = b->imax;
+                if (a->first || nan_gt(a->dmin, b->dmin)) a->dmin = b->dmin;
+                if (a->first || nan_gt(b->dmax, a->dmax)) a->dmax = b->dmax;
+                a->first = 0;
+                kbn_add(&a->s1, kbn_val(&b->s1));
+                kbn_add(&a->s2, kbn_val(&b->s2));
+                kbn_add(&a->sum, kbn_val(&b->sum));
+                for (int i = 0; i < 512; ++i)
+                    if (b->regs[i] > a->regs[i]) a->regs[i] = b->regs[i];
+            }
+            for (int p = 0; p < npairs; ++p) {
+                cacc[p].n += lc[p].n;
+                kbn_add(&cacc[p].sx, kbn_val(&lc[p].sx));
+                kbn_add(&cacc[p].sy, kbn_val(&lc[p].sy));
+                kbn_add(&cacc[p].sxx, kbn_val(&lc[p].sxx));
+                kbn_add(&cacc[p].syy, kbn_val(&lc[p].syy));
+                kbn_add(&cacc[p].sxy, kbn_val(&lc[p].sxy));
+            }
+        }
+        free(la);
+        free(lc);
+        free(x);
+        free(ok);
+    }
+    for (int c = 0; c < ncols; ++c) {
+        const gen_acc* a = &acc[c];
+        oracle_gen_col* o = &out[c];
+        memset(o, 0, sizeof(*o));
+        o->n = a->n;
+        o->nnan = a->nnan;
+        o->isum = a->isum;
+        o->imin = a->imin;
+        o->imax = a->imax;
+        o->pred_true = a->pred_true;
+        o->dmin = a->n ? a->dmin : NAN;
+        o->dmax = a->n ? a->dmax : NAN;
+        memcpy(o->regs, a->regs, 512);
+        if (a->n > 0) {
+            const long double k = shift[c];
+            const long double n = (long double)a->n, s1 = kbn_val(&a->s1), s2 = kbn_val(&a->s2);
+            o->ex_sum = specs[c].spark_type == T_DOUBLE ? (double)kbn_val(&a->sum) : (double)(k * n + s1);
+            o->ex_mean = (double)(k + s1 / n);
+            o->ex_m2 = (double)(s2 - s1 * s1 / n);
+        }
+    }
+    for (int p = 0; p < npairs; ++p) {
+        const corr_acc* q = &cacc[p];
+        oracle_gen_corr* o = &corr_out[p];
+        memset(o, 0, sizeof(*o));
+        o->n = (double)q->n;
+        if (q->n == 0) continue;
+        const int cx = pairs[2 * p], cy = pairs[2 * p + 1];
+        const long double kx = shift[cx], ky = shift[cy];
+        const long double n = (long double)q->n;
+        const long double sx = kbn_val(&q->sx), sy = kbn_val(&q->sy);
+        o->x_avg = (double)(kx + sx / n);
+        o->y_avg = (double)(ky + sy / n);
+        o->ck = (double)(kbn_val(&q->sxy) - sx * sy / n);
+        o->x_mk = (double)(kbn_val(&q->sxx) - sx * sx / n);
+        o->y_mk = (double)(kbn_val(&q->syy) - sy * sy / n);
+    }
+    free(acc);
+    free(cacc);
+    return 0;
 }

@@ -34,6 +34,24 @@ class OracleCorr(ctypes.Structure):
                 ("ex_ck", ctypes.c_double), ("ex_x_mk", ctypes.c_double), ("ex_y_mk", ctypes.c_double)]
 
 
+class OracleGenSpec(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("spark_type", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("vseed", ctypes.c_uint64), ("permille", ctypes.c_int32), ("hll", ctypes.c_int32),
+                ("pred_gt0", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class OracleGenCol(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int64), ("nnan", ctypes.c_int64), ("isum", ctypes.c_int64), ("imin", ctypes.c_int64),
+                ("imax", ctypes.c_int64), ("pred_true", ctypes.c_int64), ("dmin", ctypes.c_double),
+                ("dmax", ctypes.c_double), ("ex_sum", ctypes.c_double), ("ex_mean", ctypes.c_double),
+                ("ex_m2", ctypes.c_double), ("regs", ctypes.c_uint8 * 512)]
+
+
+class OracleGenCorr(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_double), ("x_avg", ctypes.c_double), ("y_avg", ctypes.c_double),
+                ("ck", ctypes.c_double), ("x_mk", ctypes.c_double), ("y_mk", ctypes.c_double)]
+
+
 _lib = None
 
 
@@ -65,6 +83,10 @@ def lib():
                                             ctypes.c_void_p]
         L.oracle_synth_freq_keys.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                              ctypes.c_void_p]
+        L.oracle_generated_suite.restype = ctypes.c_int
+        L.oracle_generated_suite.argtypes = [ctypes.c_int, ctypes.POINTER(OracleGenSpec), ctypes.c_int64,
+                                             ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                             ctypes.POINTER(OracleGenCol), ctypes.POINTER(OracleGenCorr)]
         _lib = L
     return _lib
 
@@ -106,6 +128,37 @@ def synth_validity(seed, row0, n, permille):
     m = np.zeros(n, dtype=np.uint8)
     lib().oracle_synth_validity(seed, row0, n, permille, m.ctypes.data)
     return m.astype(bool)
+
+
+def generated_suite(specs, row0, nrows, pairs=(), threads=None):
+    """Streamed oracle over generated columns (dq_oracle.c oracle_generated_suite): `specs` are dicts
+    with kind, spark_type, seed, vseed, permille (< 0 = no nulls), hll, pred_gt0. Returns (per-column
+    dicts, per-pair correlation dicts). Exact counts / Long sums / min / max / Compliance counts / HLL
+    registers; exact (compensated long double) sums, moments and co-moments."""
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1
+        threads = max(1, min(threads, 16))
+    arr = (OracleGenSpec * len(specs))()
+    for i, sp in enumerate(specs):
+        arr[i] = OracleGenSpec(sp["kind"], sp["spark_type"], sp["seed"], sp.get("vseed", 0), sp.get("permille", -1),
+                               int(sp.get("hll", 0)), int(sp.get("pred_gt0", 0)), 0)
+    outc = (OracleGenCol * len(specs))()
+    npairs = len(pairs)
+    pa = np.array([c for p in pairs for c in p] or [0], dtype=np.int32)
+    outp = (OracleGenCorr * max(npairs, 1))()
+    rc = lib().oracle_generated_suite(len(specs), arr, row0, nrows, npairs, pa.ctypes.data, threads, outc, outp)
+    if rc != 0:
+        raise RuntimeError("oracle_generated_suite failed: %d" % rc)
+    cols = []
+    for o in outc:
+        d = {f: getattr(o, f) for f, _ in OracleGenCol._fields_ if f != "regs"}
+        d["regs"] = np.frombuffer(bytes(o.regs), dtype=np.uint8).copy()
+        words = np.zeros(52, dtype=np.int64)
+        lib().oracle_hll_pack(d["regs"].ctypes.data, words.ctypes.data)
+        d["words"] = [int(w) for w in words]
+        cols.append(d)
+    corrs = [{f: getattr(outp[i], f) for f, _ in OracleGenCorr._fields_} for i in range(npairs)]
+    return cols, corrs
 
 
 # ---- predicate evaluation (3VL) ------------------------------------------------------------------

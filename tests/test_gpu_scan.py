@@ -150,7 +150,16 @@ def assert_state_parity(table, analyzer, got):
     elif name == "StandardDeviation":
         assert got.n == exp.n and _close(got.avg, exp.avg) and _close(got.m2, exp.m2), (analyzer, got, exp)
     elif name == "Correlation":
-        assert got.n == exp.n and _close(got.metricValue(), exp.metricValue(), 1e-11), (analyzer, got, exp)
+        # all six CorrelationState fields within 1e-12 of the exact oracle: xMk / yMk relative, the averages
+        # relative to max(|avg|, standard deviation) and ck relative to sqrt(xMk * yMk); the metric to 1e-12
+        assert got.n == exp.n, analyzer
+        sx, sy = math.sqrt(abs(exp.xMk) / exp.n), math.sqrt(abs(exp.yMk) / exp.n)
+        scale_ck = math.sqrt(abs(exp.xMk * exp.yMk))
+        for g, e, sc in [(got.xAvg, exp.xAvg, max(abs(exp.xAvg), sx)), (got.yAvg, exp.yAvg, max(abs(exp.yAvg), sy)),
+                         (got.ck, exp.ck, scale_ck), (got.xMk, exp.xMk, abs(exp.xMk)), (got.yMk, exp.yMk, abs(exp.yMk))]:
+            assert (math.isnan(g) and math.isnan(e)) or g == e or abs(g - e) <= REL * sc, (analyzer, got, exp)
+        gm, em = got.metricValue(), exp.metricValue()
+        assert (math.isnan(gm) and math.isnan(em)) or abs(gm - em) <= REL, (analyzer, gm, em)
     elif name == "ApproxCountDistinct":
         assert got.words == exp.words, analyzer
     else:

@@ -214,3 +214,48 @@ def test_synth_generators_are_deterministic_and_shaped():
     assert 0.985 < v.mean() < 0.995
     # counter-based: a shard regenerates the same rows
     assert np.array_equal(O.synth_column(4, 7, 500, 100), O.synth_column(4, 7, 0, 600)[500:])
+
+
+def test_generated_suite_oracle_matches_column_oracle():
+    """The streamed generator oracle (used at 1e9 rows by tests/test_gpu_configs.py) against the
+    materialised per-column oracle on the same generated rows: counts, Long sums, min/max, Compliance
+    counts and HLL registers identical; exact moments and co-moments equal to a long-double two-pass."""
+    import numpy as np
+    n, row0 = 150_001, 12_345
+    specs = [dict(kind=k, spark_type=7 if k in (1, 2, 3, 6, 7) else 5, seed=0x5EED0000 + k, vseed=0x5EED0100 + k,
+                  permille=10, hll=1, pred_gt0=1) for k in (1, 2, 3, 4, 5, 6, 7)]
+    specs[6]["seed"] = specs[5]["seed"]  # GAUSS_CORR shares GAUSS01's seed -> correlated pair (5, 6)
+    cols, corrs = O.generated_suite(specs, row0, n, [(5, 6), (0, 3)], threads=4)
+    vals, masks = [], []
+    for sp, o in zip(specs, cols):
+        v = O.synth_column(sp["kind"], sp["seed"], row0, n)
+        m = O.synth_validity(sp["vseed"], row0, n, sp["permille"])
+        vals.append(v)
+        masks.append(m)
+        vv = v[m]
+        assert o["n"] == int(m.sum())
+        assert o["pred_true"] == int((vv > 0).sum())
+        if sp["spark_type"] == 5:
+            assert o["isum"] == int(vv.astype(np.int64).sum())
+            assert (o["imin"], o["imax"]) == (int(vv.min()), int(vv.max()))
+        else:
+            assert (o["dmin"], o["dmax"]) == (float(vv.min()), float(vv.max()))
+        ld = vv.astype(np.longdouble)
+        mean = ld.mean()
+        assert abs(o["ex_mean"] - float(mean)) <= 1e-15 * max(1.0, abs(float(mean)))
+        m2 = float(((ld - mean) ** 2).sum())
+        assert abs(o["ex_m2"] - m2) <= 1e-14 * m2
+        regs = np.zeros(512, dtype=np.uint8)
+        O.lib().oracle_hll_fixed(sp["spark_type"], np.ascontiguousarray(v).ctypes.data,
+                                 m.astype(np.uint8).ctypes.data, n, regs.ctypes.data)
+        assert (regs == o["regs"]).all()
+    for (x, y), o in zip([(5, 6), (0, 3)], corrs):
+        m = masks[x] & masks[y]
+        xv, yv = vals[x][m].astype(np.longdouble), vals[y][m].astype(np.longdouble)
+        dx, dy = xv - xv.mean(), yv - yv.mean()
+        assert o["n"] == float(m.sum())
+        ck, xm, ym = float((dx * dy).sum()), float((dx * dx).sum()), float((dy * dy).sum())
+        assert abs(o["ck"] - ck) <= 1e-14 * math.sqrt(xm * ym)
+        assert abs(o["x_mk"] - xm) <= 1e-14 * xm and abs(o["y_mk"] - ym) <= 1e-14 * ym
+    r = corrs[0]["ck"] / math.sqrt(corrs[0]["x_mk"] * corrs[0]["y_mk"])
+    assert 0.55 < r < 0.65

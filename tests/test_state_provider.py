@@ -137,3 +137,40 @@ def test_run_on_aggregated_states_from_two_persisted_partitions(tmp_path):
     assert ctx.metric(comp).value.get() == 0.8
     assert ctx.metric(mean).value.get() == 2.0
     assert ctx.metric(uniq).value.get() == 2.0 / 5.0  # b and c occur once in the merged table
+
+
+def test_float_grouping_keys_merge_bitwise_across_persisted_states(tmp_path):
+    """Frequencies of a double grouping column loaded from disk join the in-memory state with Spark's
+    grouping equality (bitwise, NaN canonical, -0.0 != 0.0): repeated values merge, -0.0 and 0.0 stay
+    apart, NaNs merge (plain float keys never equalled GroupFloat keys)."""
+    from deequ_amd.engine import GroupFloat
+    nan = float("nan")
+    a = D.FrequenciesAndNumRows({(GroupFloat(1.5),): 2, (GroupFloat(-0.0),): 1, (GroupFloat(nan),): 1}, 4, ["x"])
+    provider = D.HdfsStateProvider(None, str(tmp_path / "st"))
+    an = D.CountDistinct(["x"])
+    provider.persist(an, D.FrequenciesAndNumRows({(1.5,): 3, (0.0,): 1, (float("nan"),): 2}, 6, ["x"]))
+    loaded = provider.load(an)
+    for merged in (a.sum(loaded), loaded.sum(a)):
+        d = merged.as_dict()
+        assert merged.numRows == 10
+        assert d[(GroupFloat(1.5),)] == 5
+        assert d[(GroupFloat(nan),)] == 3
+        assert d[(GroupFloat(-0.0),)] == 1 and d[(GroupFloat(0.0),)] == 1
+        assert len(d) == 4
+    # two loaded states (runOnAggregatedStates): NaN keys merge, signed zeros do not
+    provider2 = D.HdfsStateProvider(None, str(tmp_path / "st2"))
+    provider2.persist(an, D.FrequenciesAndNumRows({(-0.0,): 1, (float("nan"),): 1}, 2, ["x"]))
+    d = loaded.sum(provider2.load(an)).as_dict()
+    assert d[(GroupFloat(nan),)] == 3 and d[(GroupFloat(-0.0),)] == 1 and d[(GroupFloat(0.0),)] == 1
+
+
+def test_histogram_identity_and_tostring():
+    """case class Histogram(column, binningUdf, maxDetailBins): the UDF takes part in equality and toString
+    (the HdfsStateProvider file id hashes that string); Scala renders Double fields with Double.toString."""
+    f, g = (lambda s: s), (lambda s: s)
+    assert repr(D.Histogram("c")) == "Histogram(c,None,1000)"
+    assert D.Histogram("c", f) != D.Histogram("c", g) and D.Histogram("c", f) == D.Histogram("c", f)
+    assert D.Histogram("c", f) != D.Histogram("c") and len({D.Histogram("c", f), D.Histogram("c", g)}) == 2
+    assert repr(D.ApproxQuantile("c", 0.5, 1e-4)) == "ApproxQuantile(c,0.5,1.0E-4)"
+    ctx_keys = {D.Histogram("c", f): 1, D.Histogram("c", g): 2}
+    assert ctx_keys[D.Histogram("c", g)] == 2
