@@ -26,7 +26,7 @@ class UnresolvedColumnError(ValueError):
 
 _TOKEN = re.compile(r"""
     (?P<ws>\s+)
-  | (?P<num>\d+\.\d*(?:[eE][+-]?\d+)?|\.\d+(?:[eE][+-]?\d+)?|\d+(?:[eE][+-]?\d+)?[dDlL]?)
+  | (?P<num>\d+\.\d*(?:[eE][+-]?\d+)?[dD]?|\.\d+(?:[eE][+-]?\d+)?[dD]?|\d+(?:[eE][+-]?\d+)?[dDlL]?)
   | (?P<str>'(?:[^'\\]|\\.|'')*'|"(?:[^"\\]|\\.)*")
   | (?P<bq>`[^`]+`)
   | (?P<op><=>|<=|>=|<>|!=|==|=|<|>|\+|-|\*|/|%|\(|\)|,)

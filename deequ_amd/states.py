@@ -33,7 +33,9 @@ class NumMatches(DoubleValuedState):
         return float(self.numMatches)
 
     def __eq__(self, o):
-        return isinstance(o, NumMatches) and o.numMatches == self.numMatches
+        if not isinstance(o, NumMatches):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return o.numMatches == self.numMatches
 
     def __repr__(self):
         return "NumMatches(%d)" % self.numMatches
@@ -52,7 +54,9 @@ class NumMatchesAndCount(DoubleValuedState):
         return float("nan") if self.count == 0 else self.numMatches / self.count
 
     def __eq__(self, o):
-        return isinstance(o, NumMatchesAndCount) and (o.numMatches, o.count) == (self.numMatches, self.count)
+        if not isinstance(o, NumMatchesAndCount):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return (o.numMatches, o.count) == (self.numMatches, self.count)
 
     def __repr__(self):
         return "NumMatchesAndCount(%d,%d)" % (self.numMatches, self.count)
@@ -71,7 +75,9 @@ class MeanState(DoubleValuedState):
         return float("nan") if self.count == 0 else self.sum_ / self.count
 
     def __eq__(self, o):
-        return isinstance(o, MeanState) and (o.sum_, o.count) == (self.sum_, self.count)
+        if not isinstance(o, MeanState):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return (o.sum_, o.count) == (self.sum_, self.count)
 
     def __repr__(self):
         return "MeanState(%r,%d)" % (self.sum_, self.count)
@@ -90,7 +96,9 @@ class SumState(DoubleValuedState):
         return self.sum_
 
     def __eq__(self, o):
-        return isinstance(o, SumState) and o.sum_ == self.sum_
+        if not isinstance(o, SumState):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return o.sum_ == self.sum_
 
     def __repr__(self):
         return "SumState(%r)" % self.sum_
@@ -125,7 +133,9 @@ class MinState(DoubleValuedState):
         return self.minValue
 
     def __eq__(self, o):
-        return isinstance(o, MinState) and o.minValue == self.minValue
+        if not isinstance(o, MinState):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return o.minValue == self.minValue
 
     def __repr__(self):
         return "MinState(%r)" % self.minValue
@@ -144,7 +154,9 @@ class MaxState(DoubleValuedState):
         return self.maxValue
 
     def __eq__(self, o):
-        return isinstance(o, MaxState) and o.maxValue == self.maxValue
+        if not isinstance(o, MaxState):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return o.maxValue == self.maxValue
 
     def __repr__(self):
         return "MaxState(%r)" % self.maxValue
@@ -169,7 +181,9 @@ class StandardDeviationState(DoubleValuedState):
                                       self.m2 + other.m2 + delta * deltaN * self.n * other.n)
 
     def __eq__(self, o):
-        return isinstance(o, StandardDeviationState) and (o.n, o.avg, o.m2) == (self.n, self.avg, self.m2)
+        if not isinstance(o, StandardDeviationState):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return (o.n, o.avg, o.m2) == (self.n, self.avg, self.m2)
 
     def __repr__(self):
         return "StandardDeviationState(%r,%r,%r)" % (self.n, self.avg, self.m2)
@@ -202,7 +216,9 @@ class CorrelationState(DoubleValuedState):
         return self.ck / d
 
     def __eq__(self, o):
-        return isinstance(o, CorrelationState) and \
+        if not isinstance(o, CorrelationState):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return \
             (o.n, o.xAvg, o.yAvg, o.ck, o.xMk, o.yMk) == (self.n, self.xAvg, self.yAvg, self.ck, self.xMk, self.yMk)
 
     def __repr__(self):
@@ -248,7 +264,9 @@ class ApproxCountDistinctState(DoubleValuedState):
         return regs
 
     def __eq__(self, o):
-        return isinstance(o, ApproxCountDistinctState) and o.words == self.words
+        if not isinstance(o, ApproxCountDistinctState):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return o.words == self.words
 
     def __repr__(self):
         return "ApproxCountDistinctState(%s)" % ",".join(str(np.int64(np.uint64(w))) for w in self.words)
@@ -270,7 +288,9 @@ class DataTypeHistogram(State):
         return DataTypeHistogram(*[a + b for a, b in zip(self._t(), other._t())])
 
     def __eq__(self, o):
-        return isinstance(o, DataTypeHistogram) and o._t() == self._t()
+        if not isinstance(o, DataTypeHistogram):
+            return NotImplemented  # let a foreign state (e.g. a test oracle's) compare
+        return o._t() == self._t()
 
     def __repr__(self):
         return "DataTypeHistogram(%d,%d,%d,%d,%d)" % self._t()

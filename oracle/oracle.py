@@ -12,6 +12,7 @@ import ctypes
 import math
 import os
 import subprocess
+import sys
 
 import numpy as np
 
@@ -161,6 +162,490 @@ def generated_suite(specs, row0, nrows, pairs=(), threads=None):
     return cols, corrs
 
 
+
+# ---- the oracle's own State algebra and metric formulas -----------------------------------------------
+# Restated from the reference state files, independent of deequ_amd/states.py: field names match the
+# reference case classes (so tests compare field by field, and `==` against a product state compares
+# the fields), metricValue / sum follow each file.
+class OState:
+    fields = ()
+
+    def key(self):
+        return tuple(getattr(self, f) for f in self.fields)
+
+    def __eq__(self, other):
+        if type(other).__name__ != type(self).__name__:
+            return NotImplemented
+        return self.key() == tuple(getattr(other, f) for f in self.fields)
+
+    def __ne__(self, other):
+        r = self.__eq__(other)
+        return r if r is NotImplemented else not r
+
+    __hash__ = None
+
+    def __repr__(self):
+        return "oracle.%s%r" % (type(self).__name__, self.key())
+
+
+def _java_div(a, b):
+    """Java double division (x / 0.0 = +-Infinity, 0.0 / 0.0 = NaN)."""
+    if b == 0.0:
+        if a == 0.0 or a != a:
+            return float("nan")
+        return math.copysign(float("inf"), a) * math.copysign(1.0, b)
+    return a / b
+
+
+class NumMatches(OState):  # A/Size.scala:23-31
+    fields = ("numMatches",)
+
+    def __init__(self, numMatches):
+        self.numMatches = int(numMatches)
+
+    def sum(self, o):
+        return NumMatches(self.numMatches + o.numMatches)
+
+    def metricValue(self):
+        return float(self.numMatches)
+
+
+class NumMatchesAndCount(OState):  # A/Analyzer.scala:230-244
+    fields = ("numMatches", "count")
+
+    def __init__(self, numMatches, count):
+        self.numMatches, self.count = int(numMatches), int(count)
+
+    def sum(self, o):
+        return NumMatchesAndCount(self.numMatches + o.numMatches, self.count + o.count)
+
+    def metricValue(self):
+        return float("nan") if self.count == 0 else self.numMatches / self.count
+
+
+class MeanState(OState):  # A/Mean.scala:25-35
+    fields = ("sum_", "count")
+
+    def __init__(self, sum_, count):
+        self.sum_, self.count = float(sum_), int(count)
+
+    def sum(self, o):
+        return MeanState(self.sum_ + o.sum_, self.count + o.count)
+
+    def metricValue(self):
+        return float("nan") if self.count == 0 else self.sum_ / self.count
+
+
+class SumState(OState):  # A/Sum.scala:25-32
+    fields = ("sum_",)
+
+    def __init__(self, sum_):
+        self.sum_ = float(sum_)
+
+    def sum(self, o):
+        return SumState(self.sum_ + o.sum_)
+
+    def metricValue(self):
+        return self.sum_
+
+
+def _java_min(a, b):  # math.min: NaN wins, -0.0 < 0.0
+    if a != a or b != b:
+        return float("nan")
+    if a == b == 0.0:
+        return a if math.copysign(1.0, a) < 0 else b
+    return a if a < b else b
+
+
+def _java_max(a, b):
+    if a != a or b != b:
+        return float("nan")
+    if a == b == 0.0:
+        return b if math.copysign(1.0, a) < 0 else a
+    return a if a > b else b
+
+
+class MinState(OState):  # A/Minimum.scala:25-32
+    fields = ("minValue",)
+
+    def __init__(self, minValue):
+        self.minValue = float(minValue)
+
+    def sum(self, o):
+        return MinState(_java_min(self.minValue, o.minValue))
+
+    def metricValue(self):
+        return self.minValue
+
+
+class MaxState(OState):  # A/Maximum.scala:25-32
+    fields = ("maxValue",)
+
+    def __init__(self, maxValue):
+        self.maxValue = float(maxValue)
+
+    def sum(self, o):
+        return MaxState(_java_max(self.maxValue, o.maxValue))
+
+    def metricValue(self):
+        return self.maxValue
+
+
+class StandardDeviationState(OState):  # A/StandardDeviation.scala:25-50
+    fields = ("n", "avg", "m2")
+
+    def __init__(self, n, avg, m2):
+        self.n, self.avg, self.m2 = float(n), float(avg), float(m2)
+
+    def sum(self, o):
+        newN = self.n + o.n
+        delta = o.avg - self.avg
+        deltaN = 0.0 if newN == 0.0 else delta / newN
+        return StandardDeviationState(newN, self.avg + deltaN * o.n, self.m2 + o.m2 + delta * deltaN * self.n * o.n)
+
+    def metricValue(self):
+        return math.sqrt(_java_div(self.m2, self.n))
+
+
+class CorrelationState(OState):  # A/Correlation.scala:26-60
+    fields = ("n", "xAvg", "yAvg", "ck", "xMk", "yMk")
+
+    def __init__(self, n, xAvg, yAvg, ck, xMk, yMk):
+        self.n, self.xAvg, self.yAvg = float(n), float(xAvg), float(yAvg)
+        self.ck, self.xMk, self.yMk = float(ck), float(xMk), float(yMk)
+
+    def sum(self, o):
+        n1, n2 = self.n, o.n
+        newN = n1 + n2
+        dx, dy = o.xAvg - self.xAvg, o.yAvg - self.yAvg
+        dxN = 0.0 if newN == 0.0 else dx / newN
+        dyN = 0.0 if newN == 0.0 else dy / newN
+        return CorrelationState(newN, self.xAvg + dxN * n2, self.yAvg + dyN * n2,
+                                self.ck + o.ck + dx * dyN * n1 * n2, self.xMk + o.xMk + dx * dxN * n1 * n2,
+                                self.yMk + o.yMk + dy * dyN * n1 * n2)
+
+    def metricValue(self):
+        return _java_div(self.ck, math.sqrt(self.xMk * self.yMk))
+
+
+class ApproxCountDistinctState(OState):  # A/ApproxCountDistinct.scala:26-40
+    fields = ("words",)
+
+    def __init__(self, words):
+        self.words = [int(w) for w in words]
+
+    def sum(self, o):
+        ra, rb = _unpack_regs(self.words), _unpack_regs(o.words)
+        return ApproxCountDistinctState(_pack_regs(np.maximum(ra, rb)))
+
+    def metricValue(self):
+        return hll_count(self.words)
+
+
+def _unpack_regs(words):
+    regs = np.zeros(512, dtype=np.uint8)
+    for i in range(512):
+        regs[i] = (int(words[i // 10]) >> (6 * (i % 10))) & 63
+    return regs
+
+
+def _pack_regs(regs):
+    words = np.zeros(52, dtype=np.int64)
+    lib().oracle_hll_pack(np.ascontiguousarray(regs, dtype=np.uint8).ctypes.data, words.ctypes.data)
+    return [int(w) for w in words]
+
+
+class OracleDistValue:
+    def __init__(self, absolute, ratio):
+        self.absolute, self.ratio = absolute, ratio
+
+
+class OracleDistribution:
+    def __init__(self, values, numberOfBins):
+        self.values, self.numberOfBins = values, numberOfBins
+
+
+class DataTypeHistogram(OState):  # A/DataType.scala:32-110
+    fields = ("numNull", "numFractional", "numIntegral", "numBoolean", "numString")
+
+    def __init__(self, numNull, numFractional, numIntegral, numBoolean, numString):
+        self.numNull, self.numFractional, self.numIntegral = int(numNull), int(numFractional), int(numIntegral)
+        self.numBoolean, self.numString = int(numBoolean), int(numString)
+
+    def sum(self, o):
+        return DataTypeHistogram(*[a + b for a, b in zip(self.key(), o.key())])
+
+    def toDistribution(self):
+        total = sum(self.key())
+        names = ("Unknown", "Fractional", "Integral", "Boolean", "String")
+        return OracleDistribution({n: OracleDistValue(c, c / total if total else 0.0)
+                                   for n, c in zip(names, self.key())}, 5)
+
+
+# ---- the oracle's own SQL predicate parser ------------------------------------------------------------
+# Spark SQL expression strings as deequ passes them (where filters, Compliance predicates, the checks'
+# generated constraints M/checks/Check.scala:594-943), parsed by precedence climbing — independent of
+# deequ_amd/expr.py — into the nodes _eval below evaluates with three-valued logic.
+class PNode:
+    def __init__(self, kind, *children, value=None):
+        self.kind, self.children, self.value = kind, list(children), value
+
+
+def _lex(text):
+    out, i, n = [], 0, len(text)
+    ops3 = ("<=>",)
+    ops2 = ("<=", ">=", "<>", "!=", "==")
+    while i < n:
+        ch = text[i]
+        if ch.isspace():
+            i += 1
+            continue
+        if ch.isdigit() or (ch == "." and i + 1 < n and text[i + 1].isdigit()):
+            j = i
+            while j < n and text[j].isdigit():
+                j += 1
+            is_float = False
+            if j < n and text[j] == ".":
+                is_float = True
+                j += 1
+                while j < n and text[j].isdigit():
+                    j += 1
+            if j < n and text[j] in "eE" and j + 1 < n and (text[j + 1].isdigit() or text[j + 1] in "+-"):
+                is_float = True
+                j += 2
+                while j < n and text[j].isdigit():
+                    j += 1
+            lit = text[i:j]
+            if j < n and text[j] in "dD":
+                is_float, j = True, j + 1
+            elif j < n and text[j] in "lL":
+                j += 1
+            out.append(("num", float(lit) if is_float else int(lit)))
+            i = j
+            continue
+        if ch in "'\"":
+            j, buf = i + 1, []
+            while j < n:
+                c = text[j]
+                if c == "\\" and j + 1 < n:
+                    buf.append({"n": "\n", "t": "\t"}.get(text[j + 1], text[j + 1]))
+                    j += 2
+                    continue
+                if c == ch:
+                    if ch == "'" and j + 1 < n and text[j + 1] == "'":
+                        buf.append("'")
+                        j += 2
+                        continue
+                    break
+                buf.append(c)
+                j += 1
+            out.append(("str", "".join(buf)))
+            i = j + 1
+            continue
+        if ch == "`":
+            j = text.index("`", i + 1)
+            out.append(("name", text[i + 1:j]))
+            i = j + 1
+            continue
+        if ch.isalpha() or ch == "_":
+            j = i
+            while j < n and (text[j].isalnum() or text[j] in "_."):
+                j += 1
+            out.append(("word", text[i:j]))
+            i = j
+            continue
+        if text[i:i + 3] in ops3:
+            out.append(("op", text[i:i + 3]))
+            i += 3
+            continue
+        if text[i:i + 2] in ops2:
+            out.append(("op", text[i:i + 2]))
+            i += 2
+            continue
+        if ch in "=<>+-*/%(),":
+            out.append(("op", ch))
+            i += 1
+            continue
+        raise ValueError("oracle parser: bad character %r in %r" % (ch, text))
+    out.append(("end", None))
+    return out
+
+
+class OracleParser:
+    _CMP = {"=": "=", "==": "=", "!=": "!=", "<>": "!=", "<": "<", "<=": "<=", ">": ">", ">=": ">=", "<=>": "<=>"}
+
+    def __init__(self, text):
+        self.t, self.i, self.text = _lex(text), 0, text
+
+    def _peek(self, k=0):
+        return self.t[self.i + k]
+
+    def _word(self, k=0):
+        tok = self._peek(k)
+        return tok[1].upper() if tok[0] == "word" else None
+
+    def _next(self):
+        tok = self.t[self.i]
+        self.i += 1
+        return tok
+
+    def _expect_op(self, op):
+        tok = self._next()
+        if tok != ("op", op):
+            raise ValueError("oracle parser: expected %r in %r" % (op, self.text))
+
+    def parse(self):
+        node = self._expr(0)
+        if self._peek()[0] != "end":
+            raise ValueError("oracle parser: trailing input in %r" % self.text)
+        return node
+
+    # binding powers: OR 1, AND 2, NOT 3 (prefix), predicates 4, + - 5, * / % 6, unary 7
+    def _expr(self, min_bp):
+        if self._word() == "NOT":
+            self._next()
+            left = PNode("not", self._expr(3))
+        else:
+            left = self._arith(0)
+        while True:
+            w = self._word()
+            if w == "OR" and min_bp < 1:
+                self._next()
+                left = PNode("or", left, self._expr(1))
+            elif w == "AND" and min_bp < 2:
+                self._next()
+                left = PNode("and", left, self._expr(2))
+            elif min_bp < 4 and self._postfix_predicate_ahead():
+                left = self._predicate(left)
+            else:
+                return left
+
+    def _postfix_predicate_ahead(self):
+        tok = self._peek()
+        if tok[0] == "op" and tok[1] in self._CMP:
+            return True
+        w = self._word()
+        return w in ("IS", "IN", "LIKE", "BETWEEN") or (w == "NOT" and self._word(1) in ("IN", "LIKE", "BETWEEN"))
+
+    def _predicate(self, left):
+        tok = self._peek()
+        if tok[0] == "op":
+            self._next()
+            return PNode("cmp", left, self._arith(0), value=self._CMP[tok[1]])
+        negate = False
+        if self._word() == "NOT":
+            self._next()
+            negate = True
+        w = self._word()
+        self._next()
+        if w == "IS":
+            neg = self._word() == "NOT"
+            if neg:
+                self._next()
+            if self._word() != "NULL":
+                raise ValueError("oracle parser: IS [NOT] NULL expected in %r" % self.text)
+            self._next()
+            return PNode("isnotnull" if neg else "isnull", left)
+        if w == "IN":
+            self._expect_op("(")
+            items = [self._arith(0)]
+            while self._peek() == ("op", ","):
+                self._next()
+                items.append(self._arith(0))
+            self._expect_op(")")
+            node = PNode("in", left, *items)
+        elif w == "LIKE":
+            pat = self._next()
+            if pat[0] != "str":
+                raise ValueError("oracle parser: LIKE pattern must be a string literal")
+            node = PNode("like", left, value=pat[1])
+        else:  # BETWEEN lo AND hi
+            lo = self._arith(0)
+            if self._word() != "AND":
+                raise ValueError("oracle parser: BETWEEN without AND in %r" % self.text)
+            self._next()
+            hi = self._arith(0)
+            node = PNode("and", PNode("cmp", left, lo, value=">="), PNode("cmp", left, hi, value="<="))
+        return PNode("not", node) if negate else node
+
+    def _arith(self, min_bp):
+        tok = self._peek()
+        if tok == ("op", "-"):
+            self._next()
+            left = PNode("neg", self._arith(7))
+        elif tok == ("op", "+"):
+            self._next()
+            left = self._arith(7)
+        else:
+            left = self._primary()
+        while True:
+            tok = self._peek()
+            if tok[0] != "op" or tok[1] not in "+-*/%" or len(tok[1]) != 1:
+                return left
+            bp = 5 if tok[1] in "+-" else 6
+            if bp <= min_bp:
+                return left
+            self._next()
+            left = PNode("arith", left, self._arith(bp), value=tok[1])
+
+    def _primary(self):
+        kind, val = self._next()
+        if kind == "op" and val == "(":
+            node = self._expr(0)
+            self._expect_op(")")
+            return node
+        if kind == "num":
+            return PNode("const", value=("double" if isinstance(val, float) else "long", val))
+        if kind == "str":
+            return PNode("const", value=("string", val))
+        if kind == "name":
+            return PNode("col", value=val)
+        if kind != "word":
+            raise ValueError("oracle parser: unexpected %r in %r" % (val, self.text))
+        up = val.upper()
+        if up in ("TRUE", "FALSE"):
+            return PNode("const", value=("bool", up == "TRUE"))
+        if up == "NULL":
+            return PNode("null")
+        if up == "CAST":
+            self._expect_op("(")
+            inner = self._expr(0)
+            if self._word() != "AS":
+                raise ValueError("oracle parser: CAST without AS")
+            self._next()
+            target = self._next()[1].lower()
+            if self._peek() == ("op", "("):
+                while self._next() != ("op", ")"):
+                    pass
+            self._expect_op(")")
+            if target in ("double", "float", "decimal"):
+                return PNode("cast_double", inner)
+            if target in ("int", "integer", "long", "bigint", "short", "smallint", "tinyint", "byte"):
+                return PNode("cast_long", inner)
+            if target == "string":
+                return inner
+            raise ValueError("oracle parser: CAST target %s" % target)
+        if self._peek() == ("op", "("):
+            self._next()
+            args = []
+            if self._peek() != ("op", ")"):
+                args.append(self._expr(0))
+                while self._peek() == ("op", ","):
+                    self._next()
+                    args.append(self._expr(0))
+            self._expect_op(")")
+            f = val.lower()
+            if f == "coalesce":
+                return PNode("coalesce", *args)
+            if f in ("length", "char_length", "character_length"):
+                return PNode("length", args[0])
+            if f == "isnull":
+                return PNode("isnull", args[0])
+            if f == "isnotnull":
+                return PNode("isnotnull", args[0])
+            raise ValueError("oracle parser: function %s" % f)
+        return PNode("col", value=val)
+
 # ---- predicate evaluation (3VL) ------------------------------------------------------------------
 def _cmp_vals(a, b):
     """Spark comparison after PromoteStrings (string vs number -> double). None = NULL result."""
@@ -302,8 +787,7 @@ def _eval(node, row):
 
 def predicate_masks(table, text):
     """(TRUE mask, NOT-NULL mask) of a SQL predicate over every row."""
-    from deequ_amd.expr import _Parser  # the parse tree only; evaluation is independent
-    tree = _Parser(text).parse()
+    tree = OracleParser(text).parse()
     cols = {n: table[n].to_pylist() for n in table.columns}
     t = np.zeros(table.nrows, dtype=bool)
     nn = np.zeros(table.nrows, dtype=bool)
@@ -347,8 +831,7 @@ def column_stats(table, column, where=None):
 
 def expected_state(table, analyzer, exact=True):
     """The reference State for `analyzer` on `table` (None = empty state), oracle semantics."""
-    import deequ_amd as D
-    from deequ_amd import states as S
+    S = sys.modules[__name__]  # this module's own State classes (not deequ_amd's)
     name = type(analyzer).__name__
     if name == "Size":
         v, present = _cond_count(table, analyzer.where)
@@ -786,3 +1269,131 @@ def java_parse_double(s):
         return float("nan")
     v = float("inf") if body == "Infinity" else float(body)
     return -v if m.group(1) == "-" else v
+
+
+# ---- ColumnProfiler passes 1-3 (M/profiles/ColumnProfiler.scala:91-208, 357-606) --------------------
+def determine_type(counts):
+    """DataTypeHistogram.determineType (A/DataType.scala:116-143) over class counts
+    {Unknown, Fractional, Integral, Boolean, String}."""
+    total = sum(counts.values())
+    ratio = {k: (v / total if total else 0.0) for k, v in counts.items()}
+    if ratio["Unknown"] == 1.0:
+        return "Unknown"
+    if ratio["String"] > 0.0 or (ratio["Boolean"] > 0.0 and (ratio["Integral"] > 0.0 or ratio["Fractional"] > 0.0)):
+        return "String"
+    if ratio["Boolean"] > 0.0:
+        return "Boolean"
+    if ratio["Fractional"] > 0.0:
+        return "Fractional"
+    return "Integral"
+
+
+_KNOWN = {T_SHORT: "Integral", T_INT: "Integral", T_LONG: "Integral", T_FLOAT: "Fractional", T_DOUBLE: "Fractional",
+          T_DECIMAL: "Fractional", T_BOOLEAN: "Boolean", T_TIMESTAMP: "String"}
+_HIST_TYPES = (T_STRING, T_BOOLEAN, T_DOUBLE, T_FLOAT, T_INT, T_LONG, T_SHORT)
+
+
+def _hll_words_of(table, name):
+    c = table[name]
+    mask = _valid(c).astype(np.uint8)
+    regs = np.zeros(512, dtype=np.uint8)
+    if c.spark_type == T_STRING:
+        lib().oracle_hll_strings(c.values.ctypes.data if len(c.values) else None, c.offsets.ctypes.data,
+                                 mask.ctypes.data, c.length, regs.ctypes.data)
+    else:
+        vals = np.ascontiguousarray(c.values)
+        lib().oracle_hll_fixed(c.spark_type, vals.ctypes.data, mask.ctypes.data, c.length, regs.ctypes.data)
+    words = np.zeros(52, dtype=np.int64)
+    lib().oracle_hll_pack(regs.ctypes.data, words.ctypes.data)
+    return words
+
+
+def _exact_stats(values):
+    """count, sum, min, max, mean, population stddev of a 1-D float array; sums in long double."""
+    n = len(values)
+    if n == 0:
+        return None
+    ld = values.astype(np.longdouble)
+    s = ld.sum()
+    mean = s / n
+    m2 = ((ld - mean) ** 2).sum()
+    return {"n": n, "sum": float(s), "min": float(values.min()), "max": float(values.max()), "mean": float(mean),
+            "stdDev": float(np.sqrt(m2 / n))}
+
+
+def expected_profile(table, threshold=120):
+    """Per column: completeness, approximateNumDistinctValues (HLL++ of the C oracle), dataType,
+    isDataTypeInferred, typeCounts (StatefulDataType classes of Cast(x AS STRING)), pass-2 numeric
+    statistics over the column cast as ColumnProfiler.castColumn does (Spark string -> long / double
+    casts, non-parsing strings NULL), and the exact pass-3 histogram (counts; NULL as "NullValue") of
+    columns whose approximate distinct count is <= threshold."""
+    n = table.nrows
+    out = {}
+    for name in table.columns:
+        c = table[name]
+        valid = _valid(c)
+        p = {"completeness": int(valid.sum()) / n}
+        p["approx_distinct"] = int(hll_count([int(w) for w in _hll_words_of(table, name)]))
+        if c.spark_type == T_STRING:
+            py = c.to_pylist()
+            cache, counts = {}, {"Unknown": 0, "Fractional": 0, "Integral": 0, "Boolean": 0, "String": 0}
+            names = {1: "Fractional", 2: "Integral", 3: "Boolean", 4: "String"}
+            for v in py:
+                if v is None:
+                    counts["Unknown"] += 1
+                    continue
+                k = cache.get(v)
+                if k is None:
+                    k = cache[v] = names[datatype_class(v)]
+                counts[k] += 1
+            p["typeCounts"] = counts
+            p["dataType"] = determine_type(counts)
+            p["inferred"] = True
+        else:
+            p["typeCounts"] = {}
+            p["dataType"] = _KNOWN.get(c.spark_type, "Unknown")
+            p["inferred"] = False
+        if p["dataType"] in ("Integral", "Fractional"):
+            if c.spark_type == T_STRING:
+                conv = spark_string_to_long if p["dataType"] == "Integral" else java_parse_double
+                cache, vals = {}, []
+                for v in c.to_pylist():
+                    if v is None:
+                        continue
+                    if v not in cache:
+                        cache[v] = conv(v)
+                    if cache[v] is not None:
+                        vals.append(cache[v])
+                arr = np.array(vals, dtype=np.int64 if p["dataType"] == "Integral" else np.float64)
+            else:
+                arr = np.asarray(c.values)[: c.length][valid]
+            st = _exact_stats(arr.astype(np.float64))
+            if st is not None and p["dataType"] == "Integral":
+                # Spark's Long sum wraps around, then is cast to Double (A/Sum.scala:34-37, A/Mean.scala:36-40)
+                with np.errstate(over="ignore"):
+                    st["sum"] = float(int(arr.astype(np.int64).sum(dtype=np.int64)))
+                st["mean"] = st["sum"] / st["n"]
+                st["min"], st["max"] = float(int(arr.min())), float(int(arr.max()))
+            p["numeric"] = st
+        if c.spark_type in _HIST_TYPES and p["dataType"] in ("String", "Boolean", "Integral", "Fractional") and \
+                p["approx_distinct"] <= threshold:
+            freq, _ = frequencies(table, [name], include_nulls=True)
+            hist = {}
+            for (k,), cnt in freq.items():
+                if k is None:
+                    key = "NullValue"
+                elif c.spark_type == T_STRING:
+                    key = k
+                elif c.spark_type == T_BOOLEAN:
+                    key = "true" if k else "false"
+                elif c.spark_type in (T_DOUBLE, T_FLOAT):
+                    key = java_double_to_string(float("nan") if isinstance(k, tuple) and k[0] == "nan" else
+                                                (-0.0 if isinstance(k, tuple) else k), c.spark_type == T_FLOAT)
+                else:
+                    key = str(int(k))
+                hist[key] = cnt
+            p["histogram"] = hist
+        else:
+            p["histogram"] = None
+        out[name] = p
+    return out

@@ -53,3 +53,52 @@ def test_string_constants_pool():
     p = compile_predicate("item = 'héllo' OR item = 'it''s'", COLS)
     pool = bytes(p._strings[:p._strings_len])
     assert "héllo".encode() in pool and b"it's" in pool
+
+
+# The oracle parses predicates with its own precedence-climbing parser (oracle.OracleParser): the
+# product parse trees are pinned by evaluating both over a grid of rows with NULLs, and by the truth
+# tables of the reference's own predicates on the reference fixtures.
+CORPUS = ["item IN ('1', '2')", "att1 > 3", "att2 = 0", "att1 < 4", "item != '6'", "att1 != 2",
+          "att1 IS NULL OR att2 IS NOT NULL", "NOT (att1 >= 2 AND att2 <= 5)", "att1 BETWEEN 1 AND 3",
+          "coalesce(att1, 0) > 1", "item LIKE '%1%'", "length(item) >= 2", "att1 + att2 * 2 > 3", "`att1` <=> NULL",
+          "att1 NOT IN (1, 2)", "CAST(item AS DOUBLE) > 1.5", "att1 == 3", "att1 <> 3", "-att1 < -2 OR att2 % 2 = 1",
+          "att1 - att2 - 1 > 0", "att1 / 2 >= 1.5", "NOT att1 > 1 AND att2 IS NULL", "att1 NOT BETWEEN 2 AND 4",
+          "item NOT LIKE '_'", "att1 IN (1, NULL)", "att1 = 1 OR att1 = 2 AND att2 = 3", "(att1 = 1 OR att1 = 2) AND att2 = 3",
+          "att2 >= 0 AND att2 < 6 OR att1 IS NULL", "CAST(att1 AS BIGINT) * 2 = 4", "isnull(att2) OR att1 > 5",
+          "`att1` IS NULL OR `att1` >= 0", "1.5e0 < att1", "att1 > 2.0d", "item = 'it''s'"]
+
+
+def _rows():
+    import itertools
+    items = ["1", "2", "11", None, "it's", "2.5"]
+    vals = [None, 0, 1, 2, 3, 4, 5, 6, 7]
+    return [{"item": i, "att1": a, "att2": b} for i, a, b in itertools.product(items, vals, vals)]
+
+
+def test_oracle_parser_agrees_with_product_parser():
+    import oracle as O
+    from deequ_amd.expr import _Parser
+    rows = _rows()
+    for text in CORPUS:
+        mine, theirs = O.OracleParser(text).parse(), _Parser(text).parse()
+        for r in rows:
+            assert O._eval(mine, r) == O._eval(theirs, r), (text, r)
+
+
+def test_oracle_parser_reference_truth_tables(kats):
+    """Compliance KATs of the reference (tests/golden/kats.json) re-evaluated through the oracle parser."""
+    import oracle as O
+    from helpers import table_from_fixture
+    seen = 0
+    for k in kats["kats"]:
+        if k["analyzer"][0] != "Compliance" or not isinstance(k["expected"], (int, float)):
+            continue
+        t = table_from_fixture(kats["fixtures"][k["fixture"]])
+        truth, _ = O.predicate_masks(t, k["analyzer"][2])
+        where = k["analyzer"][3] if len(k["analyzer"]) > 3 else None
+        wt = O.predicate_masks(t, where)[0] if where else [True] * t.nrows
+        den = sum(1 for w in wt if w) if where else t.nrows
+        got = sum(1 for a, w in zip(truth, wt) if a and w) / den
+        assert got == k["expected"], k
+        seen += 1
+    assert seen >= 3

@@ -1,0 +1,115 @@
+"""Reduced BASELINE config C5: the full 3-pass ColumnProfiler over a 20-column mixed
+numeric / string table (5 fp64 + 5 int64 + 10 UTF-8 strings: 3 low-cardinality, 3 numeric-looking,
+4 free text 1-20 characters; 5 % nulls) at 1e6 rows, checked against the oracle's own restatement of
+the profiler (oracle.expected_profile: M/profiles/ColumnProfiler.scala:91-208, 357-606):
+  pass 1  completeness exact, approximateNumDistinctValues = HLL++ estimate of the oracle registers
+          (bit-exact), DataType class counts + determineType exact;
+  pass 2  string columns inferred Integral / Fractional cast with Spark's casts; minimum / maximum /
+          Long sums exact, mean / fp64 sum / stdDev within 1e-12 relative of the exact values;
+  pass 3  exact histograms of the columns with <= 120 approximate distinct values (keys formatted as
+          Spark's Cast to string, NULL as "NullValue", ratio = count / rows).
+DQ_C5_ROWS overrides the row count."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import deequ_amd as D
+from deequ_amd.table import Table
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ROWS = int(float(os.environ.get("DQ_C5_ROWS", "1e6")))
+
+
+def c5_table(n, seed=5):
+    import pyarrow as pa
+    rng = np.random.default_rng(seed)
+
+    def nulls():
+        return rng.random(n) < 0.05
+
+    arrays, names = [], []
+
+    def add(name, values, mask):
+        arrays.append(pa.array(values, mask=mask))
+        names.append(name)
+
+    add("d_norm", rng.normal(0.0, 1.0, n), nulls())
+    add("d_unif", rng.random(n), nulls())
+    add("d_dyad", rng.integers(-256, 257, n) / 256.0, nulls())
+    add("d_n100", 100.0 + 15.0 * rng.normal(0.0, 1.0, n), nulls())
+    add("d_lowc", rng.integers(0, 30, n) * 0.5 - 3.0, nulls())                  # 30 values -> pass-3 histogram
+    add("l_wide", rng.integers(-2 ** 40, 2 ** 40, n, dtype=np.int64), nulls())
+    add("l_lowc", rng.integers(0, 61, n, dtype=np.int64), nulls())             # 61 values -> histogram
+    add("l_i32", rng.integers(-2 ** 31, 2 ** 31, n, dtype=np.int64), nulls())
+    add("l_small", rng.integers(0, 1000, n, dtype=np.int64), nulls())
+    add("l_neg", -rng.integers(0, 2 ** 62, n, dtype=np.int64), nulls())
+
+    def strings(vals, mask):
+        return [None if m else v for v, m in zip(vals, mask)]
+
+    cats = np.array(["cat_%d" % i for i in range(50)], dtype=object)
+    add("s_cat50", strings(cats[rng.integers(0, 50, n)], nulls()), None)
+    add("s_bool", strings(np.array(["true", "false"], dtype=object)[rng.integers(0, 2, n)], nulls()), None)
+    v100 = np.array(["v%02d" % i for i in range(100)], dtype=object)
+    add("s_cat100", strings(v100[rng.integers(0, 100, n)], nulls()), None)
+    add("s_int", strings([str(int(x)) for x in rng.integers(-10 ** 6, 10 ** 6, n)], nulls()), None)
+    add("s_dec", strings(["%.2f" % x for x in rng.random(n) * 1000.0], nulls()), None)
+    mix = [str(int(x)) if r < 0.7 else "%.3f" % (x / 7.0) for x, r in zip(rng.integers(-5000, 5000, n), rng.random(n))]
+    add("s_mixnum", strings(mix, nulls()), None)
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789 ", dtype=np.uint8)
+    for k in range(4):
+        lens = rng.integers(1, 21, n)
+        pool = letters[rng.integers(0, len(letters), int(lens.sum()))].tobytes().decode()
+        offs = np.concatenate([[0], np.cumsum(lens)])
+        txt = [pool[offs[i]:offs[i + 1]] for i in range(n)]
+        if k == 3:  # some multi-byte UTF-8 (characters, not bytes, count for lengths; HLL hashes the bytes)
+            txt = [t + "é" if i % 17 == 0 else t for i, t in enumerate(txt)]
+        add("s_text%d" % k, strings(txt, nulls()), None)
+    return Table.from_arrow(pa.Table.from_arrays(arrays, names=names))
+
+
+def _close(a, b, rel=1e-12):
+    return a == b or abs(a - b) <= rel * max(abs(a), abs(b))
+
+
+def test_c5_reduced_column_profile_against_oracle():
+    t = c5_table(ROWS)
+    assert len(t.columns) == 20
+    exp = O.expected_profile(t)
+    t.to_device()
+    prof = D.ColumnProfiler.profile(t)
+    assert prof.numRecords == ROWS
+    seen_hist = seen_numeric_string = 0
+    for name, e in exp.items():
+        p = prof.profiles[name]
+        assert p.completeness == e["completeness"], name
+        assert p.approximateNumDistinctValues == e["approx_distinct"], name
+        assert p.dataType == e["dataType"], (name, p.dataType, e["dataType"])
+        assert p.isDataTypeInferred == e["inferred"], name
+        assert p.typeCounts == e["typeCounts"], (name, p.typeCounts, e["typeCounts"])
+        if e["dataType"] in ("Integral", "Fractional"):
+            assert isinstance(p, D.NumericColumnProfile), name
+            st = e["numeric"]
+            assert (p.minimum, p.maximum) == (st["min"], st["max"]), name
+            if e["dataType"] == "Integral":
+                assert p.sum == st["sum"], name
+            else:
+                assert _close(p.sum, st["sum"]), (name, p.sum, st["sum"])
+            assert _close(p.mean, st["mean"]), (name, p.mean, st["mean"])
+            assert _close(p.stdDev, st["stdDev"]), (name, p.stdDev, st["stdDev"])
+            assert sum(b.count for b in p.kll.buckets) == st["n"], name
+            seen_numeric_string += t[name].spark_type == O.T_STRING
+        if e["histogram"] is None:
+            assert p.histogram is None, name
+        else:
+            seen_hist += 1
+            got = {k: v.absolute for k, v in p.histogram.values.items()}
+            assert got == e["histogram"], name
+            assert p.histogram.numberOfBins == len(e["histogram"])
+            for k, v in p.histogram.values.items():
+                assert v.ratio == e["histogram"][k] / ROWS
+    assert seen_hist >= 5 and seen_numeric_string == 3
