@@ -607,9 +607,33 @@ class FrequenciesAndNumRows:
             return self.frequencies
         return self.frequencies.to_dict()
 
+    def _values_side(self):
+        """This state as a single fixed-width-key table (device FrequencyTable or host PairFrequencies), or None."""
+        f = self.frequencies
+        if isinstance(f, engine.PairFrequencies):
+            return f
+        if isinstance(f, engine.FrequencyTable) and f.key_kind() == N.FREQ_KEYS_VALUES:
+            return f
+        return None
+
     def sum(self, other):
         """Null-safe full outer join on the keys, counts added (A/GroupingAnalyzers.scala:127-147). Keys are
-        compared with Spark's grouping equality (floating values bitwise, NaN canonical: GroupFloat)."""
+        compared with Spark's grouping equality (floating values bitwise, NaN canonical). Single fixed-width
+        keys merge on the GPU (dq_freq_merge) when either side is a device table, as canonical 64-bit
+        pairs otherwise; other key shapes join as host dicts."""
+        a, b = self._values_side(), other._values_side()
+        if a is not None and b is not None and a.key_type == b.key_type:
+            rows = self.numRows + other.numRows
+            if isinstance(a, engine.PairFrequencies) and isinstance(b, engine.PairFrequencies):
+                keys, inv = np.unique(np.concatenate([a.keys, b.keys]), return_inverse=True)
+                counts = np.bincount(inv, weights=np.concatenate([a.counts, b.counts]).astype(np.float64),
+                                     minlength=len(keys)).astype(np.int64)
+                return FrequenciesAndNumRows(engine.PairFrequencies(a.key_type, keys, counts, rows,
+                                                                    a.null_count + b.null_count, a.decimal_scale,
+                                                                    a.names), rows, self.columns)
+            ta = a.to_device() if isinstance(a, engine.PairFrequencies) else a
+            tb = b.to_device() if isinstance(b, engine.PairFrequencies) else b
+            return FrequenciesAndNumRows(ta.merge(tb), rows, self.columns)
         merged = {}
         for src in (self.as_dict(), other.as_dict()):
             for k, v in src.items():
@@ -619,8 +643,14 @@ class FrequenciesAndNumRows:
 
     def summary(self, entropy_rows=None):
         n = self.numRows if entropy_rows is None else entropy_rows
-        if isinstance(self.frequencies, dict):
-            counts = np.fromiter(self.frequencies.values(), dtype=np.float64, count=len(self.frequencies))
+        if isinstance(self.frequencies, (dict, engine.PairFrequencies)):
+            if isinstance(self.frequencies, engine.PairFrequencies):
+                pf = self.frequencies
+                counts = pf.counts.astype(np.float64)
+                if pf.null_count:
+                    counts = np.append(counts, float(pf.null_count))
+            else:
+                counts = np.fromiter(self.frequencies.values(), dtype=np.float64, count=len(self.frequencies))
             ent = 0.0
             if len(counts):
                 p = counts / n
@@ -749,6 +779,16 @@ class MutualInformation(FrequencyBasedAnalyzer):
         inst = ",".join(self.columns)
         if state is None:
             return metricFromEmpty(self, self.name, inst, Entity.Mutlicolumn)
+        f = state.frequencies
+        if isinstance(f, engine.FrequencyTable) and f.source is not None and len(f.names) == 2 and \
+                state.numRows == f.num_rows:
+            # on the GPU: the joint table plus the two marginal tables of the same rows (dq_freq_mutual_information)
+            x = engine.frequencies(f.source, [f.names[0]])
+            y = engine.frequencies(f.source, [f.names[1]])
+            value, present = f.mutual_information(x, y)
+            if not present:
+                return metricFromEmpty(self, self.name, inst, Entity.Mutlicolumn)
+            return metricFromValue(value, self.name, inst, Entity.Mutlicolumn)
         joint = state.as_dict()
         if not joint:
             return metricFromEmpty(self, self.name, inst, Entity.Mutlicolumn)

@@ -11,6 +11,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -614,15 +615,16 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         bool heavy = false;
         for (int k = 0; sd.kind == SK_VALUES && k < sd.ncols; ++k)
             heavy |= (sd.col[k].flags & CF_HLL) || sd.col[k].pred_kind != FP_NONE;
-        const int key = shape_key(sd.kind, P, nc, f0, f1, heavy);
+        const int kind = sd.kind;
+        const int key = shape_key(kind, P, nc, f0, f1, heavy);
         auto it = group_of.find(key);
         if (it == group_of.end()) {
             int occ;
             auto oc = ctx->occupancy.find(key);
             if (oc != ctx->occupancy.end()) occ = oc->second;
-            else occ = ctx->occupancy[key] = std::max(1, scan_group_blocks_per_cu(sd.kind, P, nc, f0, f1, heavy));
+            else occ = ctx->occupancy[key] = std::max(1, scan_group_blocks_per_cu(kind, P, nc, f0, f1, heavy));
             const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(ntiles, 1), (int64_t)ctx->cus * occ));
-            groups.push_back(Group{sd.kind, P, nc, f0, f1, heavy, (int)grid, {}});
+            groups.push_back(Group{kind, P, nc, f0, f1, heavy, (int)grid, {}});
             it = group_of.emplace(key, (int)groups.size() - 1).first;
         }
         groups[it->second].slots.push_back(s);

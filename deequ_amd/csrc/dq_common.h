@@ -20,7 +20,18 @@ constexpr uint64_t P64_4 = 0x85EBCA77C2B2AE63ULL;
 constexpr uint64_t P64_5 = 0x27D4EB2F165667C5ULL;
 constexpr uint64_t SPARK_HLL_SEED = 42;  // C/StatefulHyperloglogPlus.scala:93
 
-DQ_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+DQ_HD uint64_t rotl64(uint64_t x, int r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // two v_alignbit_b32 (funnel shifts of the 32-bit halves) instead of the shift/shift/or sequence
+    // the compiler emits for a 64-bit rotate: 1 < r < 32 at every call site (XXH64 uses 1..31)
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t nh = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+    const uint32_t nl = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
+    return ((uint64_t)nh << 32) | nl;
+#else
+    return (x << r) | (x >> (64 - r));
+#endif
+}
 
 DQ_HD uint64_t xxh_fmix(uint64_t h) {
     h ^= h >> 33;

@@ -38,6 +38,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -78,18 +79,46 @@ struct KeySpec {
     int32_t include_nulls; // Histogram semantics
     int32_t string_null_is_value;  // Histogram on a string column: NULL == "NullValue"
     uint64_t seed;         // fingerprint seed (general path)
+    const long long* weights;  // per-row counts (pre-aggregated (key, count) input), nullptr = 1 per row
 };
 
+// A group: 64-bit key and its 64-bit count (Spark counts with Long: a key seen >= 2^32 times is exact).
 struct Slot {
     unsigned long long key;
-    unsigned int count;
-    unsigned int pad;
+    unsigned long long count;
 };
+
+__device__ __forceinline__ unsigned long long row_weight(const KeySpec& ks, int64_t r) {
+    return ks.weights ? (unsigned long long)ks.weights[r] : 1ull;
+}
 
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
+}
+
+__host__ __device__ constexpr uint64_t mul_inverse(uint64_t a) {  // a^-1 mod 2^64 for odd a (Newton)
+    uint64_t x = a;
+    for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+    return x;
+}
+
+__host__ __device__ __forceinline__ uint64_t unxorshift(uint64_t z, int s) {
+    uint64_t x = z;
+    for (int i = 0; i < 64 / s + 1; ++i) x = z ^ (x >> s);
+    return x;
+}
+
+// Inverse of mix64: the canonical value behind a fast-path key.
+__host__ __device__ __forceinline__ uint64_t unmix64(uint64_t z) {
+    constexpr uint64_t i2 = mul_inverse(0x94D049BB133111EBULL), i1 = mul_inverse(0xBF58476D1CE4E5B9ULL);
+    z = unxorshift(z, 31);
+    z *= i2;
+    z = unxorshift(z, 27);
+    z *= i1;
+    z = unxorshift(z, 30);
+    return z;
 }
 
 // Probe start of a key inside its region: its top bits (the region is chosen by the low bits).
@@ -272,10 +301,11 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (!ok[u]) continue;
-            ++taken;
-            if (ngv[u]) { ++nulls; continue; }
+            const unsigned long long w = row_weight(ks, rb + (int64_t)u * kFreqBlock);
+            taken += w;
+            if (ngv[u]) { nulls += w; continue; }
             const uint64_t h = hv[u];
-            if (h == kEmpty) { ++sent; continue; }
+            if (h == kEmpty) { sent += w; continue; }
             ++kept;
             // h is already a mixed 64-bit key (splitmix64 finalizer / fingerprint): use its bits directly
             const unsigned int idx = (unsigned int)(h >> 52);
@@ -621,7 +651,6 @@ __global__ void region_init_kernel(const BuildItem* __restrict__ items, int nite
     for (int i = threadIdx.x; i < kRegion; i += blockDim.x) {
         region[i].key = kEmpty;
         region[i].count = 0;
-        region[i].pad = 0;
         if (reps) reps[(uint64_t)it.bucket * kRegion + i] = ~0ull;
     }
 }
@@ -633,13 +662,15 @@ __global__ void region_init_kernel(const BuildItem* __restrict__ items, int nite
 constexpr int kBuildBlock = 512;
 constexpr int kBuildUnroll = 4;
 
-__device__ __forceinline__ bool lds_insert(unsigned long long* lkey, unsigned int* lcnt, unsigned long long* lrep,
-                                           unsigned long long h, unsigned long long row, bool general) {
+// LDS counts: 32-bit for row counting (a work item holds <= kSliceRows rows), 64-bit for weighted input.
+template <typename C>
+__device__ __forceinline__ bool lds_insert(unsigned long long* lkey, C* lcnt, unsigned long long* lrep,
+                                           unsigned long long h, unsigned long long row, C w, bool general) {
     unsigned int p = region_probe(h);
     for (int probe = 0; probe < kRegion; ++probe) {
         const unsigned long long prev = atomicCAS(&lkey[p], kEmpty, h);
         if (prev == kEmpty || prev == h) {
-            atomicAdd(&lcnt[p], 1u);
+            atomicAdd(&lcnt[p], w);
             if (general) atomicMin(&lrep[p], row);
             return true;
         }
@@ -648,13 +679,14 @@ __device__ __forceinline__ bool lds_insert(unsigned long long* lkey, unsigned in
     return false;
 }
 
-template <bool GENERAL>
+template <bool GENERAL, bool WEIGHTED>
 __global__ void __launch_bounds__(kBuildBlock)
 build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
-             const unsigned long long* __restrict__ rows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
-             Counters* __restrict__ ctr) {
+             const unsigned long long* __restrict__ rows, const long long* __restrict__ weights,
+             Slot* __restrict__ slots, unsigned long long* __restrict__ reps, Counters* __restrict__ ctr) {
+    using C = typename std::conditional<WEIGHTED, unsigned long long, unsigned int>::type;
     __shared__ unsigned long long lkey[kRegion];
-    __shared__ unsigned int lcnt[kRegion];
+    __shared__ C lcnt[kRegion];
     __shared__ unsigned long long lrep[GENERAL ? kRegion : 1];
     __shared__ unsigned int lovf;
     const BuildItem it = items[blockIdx.x];
@@ -673,11 +705,12 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
         for (int u = 0; u < kBuildUnroll; ++u) {
             const unsigned long long j = j0 + (unsigned long long)u * kBuildBlock;
             h[u] = j < it.end ? hs[j] : kEmpty;
-            rw[u] = (GENERAL && j < it.end) ? rows[j] : 0ull;
+            rw[u] = ((GENERAL || WEIGHTED) && j < it.end) ? rows[j] : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u)
-            if (h[u] != kEmpty) ok &= lds_insert(lkey, lcnt, lrep, h[u], rw[u], GENERAL);
+            if (h[u] != kEmpty)
+                ok &= lds_insert<C>(lkey, lcnt, lrep, h[u], rw[u], WEIGHTED ? (C)weights[rw[u]] : (C)1, GENERAL);
     }
     if (!ok) lovf = 1;
     __syncthreads();
@@ -687,8 +720,7 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
         for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
             Slot sl;
             sl.key = lkey[i];
-            sl.count = lcnt[i];
-            sl.pad = 0;
+            sl.count = (unsigned long long)lcnt[i];
             region[i] = sl;
             if (GENERAL) rrep[i] = lrep[i];
         }
@@ -703,7 +735,7 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
                 Slot* sl = region + p;
                 const unsigned long long prev = atomicCAS(&sl->key, kEmpty, h);
                 if (prev == kEmpty || prev == h) {
-                    atomicAdd(&sl->count, lcnt[i]);
+                    atomicAdd(&sl->count, (unsigned long long)lcnt[i]);
                     if (GENERAL) atomicMin(&rrep[p], lrep[i]);
                     done = true;
                     break;
@@ -732,7 +764,7 @@ summary_kernel(const Slot* __restrict__ slots, uint64_t cap, double n, SummaryPa
     const uint64_t b1 = b0 + chunk < cap ? b0 + chunk : cap;
     SummaryPartial p = {0, 0, 0, 0, 0.0, 0.0};
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += kFreqBlock) {
-        const unsigned int c = slots[i].count;
+        const unsigned long long c = slots[i].count;
         if (c == 0) continue;
         p.groups++;
         p.unique += c == 1;
@@ -767,16 +799,16 @@ summary_kernel(const Slot* __restrict__ slots, uint64_t cap, double n, SummaryPa
 
 // Radix-select step: histogram of 11-bit digit `shift` of counts whose higher bits equal `prefix`.
 __global__ void __launch_bounds__(kFreqBlock)
-digit_hist_kernel(const Slot* __restrict__ slots, uint64_t cap, int shift, unsigned int prefix_mask,
-                  unsigned int prefix, unsigned long long* __restrict__ hist) {
+digit_hist_kernel(const Slot* __restrict__ slots, uint64_t cap, int shift, unsigned long long prefix_mask,
+                  unsigned long long prefix, unsigned long long* __restrict__ hist) {
     __shared__ unsigned int lds[2048];
     for (int i = threadIdx.x; i < 2048; i += kFreqBlock) lds[i] = 0;
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * kFreqBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kFreqBlock + threadIdx.x; i < cap; i += stride) {
-        const unsigned int c = slots[i].count;
+        const unsigned long long c = slots[i].count;
         if (c == 0 || (c & prefix_mask) != prefix) continue;
-        atomicAdd(&lds[(c >> shift) & 2047u], 1u);
+        atomicAdd(&lds[(unsigned int)(c >> shift) & 2047u], 1u);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 2048; i += kFreqBlock)
@@ -784,12 +816,12 @@ digit_hist_kernel(const Slot* __restrict__ slots, uint64_t cap, int shift, unsig
 }
 
 // Selection predicate of the compaction kernels: mode 0 = count > t, 1 = count == t, 2 = count > 0.
-__device__ __forceinline__ bool selected(unsigned int c, int mode, unsigned int t) {
+__device__ __forceinline__ bool selected(unsigned long long c, int mode, unsigned long long t) {
     return mode == 0 ? c > t : (mode == 1 ? c == t : c > 0);
 }
 
 __global__ void __launch_bounds__(kFreqBlock)
-count_selected_kernel(const Slot* __restrict__ slots, uint64_t cap, int mode, unsigned int t,
+count_selected_kernel(const Slot* __restrict__ slots, uint64_t cap, int mode, unsigned long long t,
                       unsigned long long* __restrict__ per_block) {
     __shared__ unsigned long long red[kFreqBlock / 64];
     const uint64_t chunk = (cap + gridDim.x - 1) / gridDim.x;
@@ -805,8 +837,8 @@ count_selected_kernel(const Slot* __restrict__ slots, uint64_t cap, int mode, un
 // skipping ranks >= limit. key_out gets the slot key (fast) or the representative row (general).
 __global__ void __launch_bounds__(kFreqBlock)
 compact_kernel(const Slot* __restrict__ slots, const unsigned long long* __restrict__ reps, uint64_t cap, int mode,
-               unsigned int t, const unsigned long long* __restrict__ offsets, unsigned long long limit,
-               unsigned long long* __restrict__ key_out, unsigned long long* __restrict__ count_out) {
+               unsigned long long t, const unsigned long long* __restrict__ offsets, unsigned long long limit,
+               unsigned long long* __restrict__ key_out, unsigned long long* __restrict__ count_out, int decode) {
     __shared__ unsigned int wave_counts[kFreqBlock / 64];
     const uint64_t chunk = (cap + gridDim.x - 1) / gridDim.x;
     const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
@@ -828,7 +860,7 @@ compact_kernel(const Slot* __restrict__ slots, const unsigned long long* __restr
         if (sel) {
             const unsigned long long rank = base + wave_off + before;
             if (rank < limit) {
-                key_out[rank] = reps ? reps[i] : slots[i].key;
+                key_out[rank] = reps ? reps[i] : (decode ? unmix64(slots[i].key) : slots[i].key);
                 count_out[rank] = slots[i].count;
             }
         }
@@ -837,27 +869,73 @@ compact_kernel(const Slot* __restrict__ slots, const unsigned long long* __restr
     }
 }
 
-uint64_t mul_inverse(uint64_t a) {  // a^-1 mod 2^64 for odd a (Newton)
-    uint64_t x = a;
-    for (int i = 0; i < 6; ++i) x *= 2 - a * x;
-    return x;
+
+// ---- MutualInformation over a joint (x, y) table and the two marginal tables (A/MutualInformation.scala:35-97) --
+struct LookupTable {
+    const Slot* slots;
+    KeySpec ks;
+    unsigned long long sentinel;  // fast path: the value whose mixed key is the EMPTY marker
+    int bits;
+};
+
+// Count of row r's key in table T (0 when r's key is NULL: Spark's equi-join on the marginals drops it).
+__device__ __forceinline__ unsigned long long lookup_count(const LookupTable& T, int64_t r) {
+    uint64_t h;
+    bool ng;
+    if (!row_key(T.ks, r, h, ng) || ng) return 0;
+    if (h == kEmpty) return T.sentinel;
+    const uint64_t base = (h & ((1ull << T.bits) - 1)) * kRegion;
+    unsigned int p = region_probe(h);
+    for (int probe = 0; probe < kRegion; ++probe) {
+        const Slot& sl = T.slots[base + p];
+        if (sl.key == h) return sl.count;
+        if (sl.key == kEmpty) return 0;
+        p = (p + 1) & (kRegion - 1);
+    }
+    return 0;
 }
 
-uint64_t unxorshift(uint64_t z, int s) {
-    uint64_t x = z;
-    for (int i = 0; i < 64 / s + 1; ++i) x = z ^ (x >> s);
-    return x;
+// sum over joint groups with both keys non-NULL of (pxy/N) ln((pxy/N) / ((px/N)(py/N))), per-workgroup Kahan
+// partials over fixed slot chunks (folded in order on the host: deterministic)
+__global__ void __launch_bounds__(kFreqBlock)
+mi_kernel(const Slot* __restrict__ slots, const unsigned long long* __restrict__ reps, uint64_t cap, KeySpec jks,
+          LookupTable X, LookupTable Y, double n, SummaryPartial* __restrict__ out) {
+    __shared__ SummaryPartial red[kFreqBlock];
+    const uint64_t chunk = (cap + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t b1 = b0 + chunk < cap ? b0 + chunk : cap;
+    SummaryPartial p = {0, 0, 0, 0, 0.0, 0.0};
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += kFreqBlock) {
+        const unsigned long long c = slots[i].count;
+        if (c == 0) continue;
+        const int64_t r = (int64_t)reps[i];
+        if (!is_valid(jks.cols[0], r) || !is_valid(jks.cols[1], r)) continue;
+        const double px = (double)lookup_count(X, r), py = (double)lookup_count(Y, r);
+        const double pxy = (double)c / n;
+        const double term = pxy * log(pxy / ((px / n) * (py / n)));
+        p.groups++;
+        const double yk = term - p.comp;
+        const double t = p.ent + yk;
+        p.comp = (t - p.ent) - yk;
+        p.ent = t;
+    }
+    red[threadIdx.x] = p;
+    __syncthreads();
+    for (int st = kFreqBlock / 2; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            SummaryPartial& a = red[threadIdx.x];
+            const SummaryPartial& b = red[threadIdx.x + st];
+            a.groups += b.groups;
+            const double yk = b.ent - (a.comp + b.comp);
+            const double t = a.ent + yk;
+            a.comp = (t - a.ent) - yk;
+            a.ent = t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
 }
 
-// Inverse of mix64: the canonical value behind a fast-path key.
-uint64_t unmix64(uint64_t z) {
-    z = unxorshift(z, 31);
-    z *= mul_inverse(0x94D049BB133111EBULL);
-    z = unxorshift(z, 27);
-    z *= mul_inverse(0xBF58476D1CE4E5B9ULL);
-    z = unxorshift(z, 30);
-    return z;
-}
 
 }  // namespace
 
@@ -879,6 +957,8 @@ struct dq_freq_table {
     uint64_t cap = 0;
     int bits = 0;           // 2^bits bucket regions of kRegion slots
     int fast = 1;
+    int32_t key_type = 0;   // Spark type of the (single) key column, or of the canonical keys of a pair-built table
+    int64_t num_rows_override = -1;  // tables built from (key, count) pairs carry the caller's numRows
     int64_t cached_n = -1;  // dq_freq_summarize memo (the table is immutable once built)
     dq_freq_summary cached;
     void* scratch = nullptr;  // device scratch for scans
@@ -951,6 +1031,7 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
                   const std::vector<unsigned long long>& bcount, int bits, bool* overflow, bool* collision) {
     hipStream_t s = dq::ctx_stream(ctx);
     const bool general = !t->fast;
+    const bool weighted = t->ks.weights != nullptr;
     const uint64_t nb = 1ull << bits;
     std::vector<BuildItem> items;
     items.reserve(nb);
@@ -978,12 +1059,19 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), items.size() * sizeof(BuildItem), hipMemcpyHostToDevice, s));
     const int nitems = (int)items.size();
     hipLaunchKernelGGL(region_init_kernel, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, nitems, t->slots, t->reps);
-    if (general)
-        hipLaunchKernelGGL(build_kernel<true>, dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, t->slots,
-                           t->reps, t->ctr);
+    const long long* w = t->ks.weights;
+    if (general && weighted)
+        hipLaunchKernelGGL((build_kernel<true, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
+                           t->slots, t->reps, t->ctr);
+    else if (general)
+        hipLaunchKernelGGL((build_kernel<true, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
+                           t->slots, t->reps, t->ctr);
+    else if (weighted)
+        hipLaunchKernelGGL((build_kernel<false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
+                           t->slots, t->reps, t->ctr);
     else
-        hipLaunchKernelGGL(build_kernel<false>, dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, t->slots,
-                           t->reps, t->ctr);
+        hipLaunchKernelGGL((build_kernel<false, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
+                           t->slots, t->reps, t->ctr);
     FQ_HIP(ctx, hipGetLastError());
     if (general && nrows > 0) {
         const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
@@ -1014,7 +1102,7 @@ constexpr int kMaxPartBits = 20;
 int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, int xgrid, const unsigned int* hist1,
                       unsigned long long n, int bits, bool* collision) {
     hipStream_t s = dq::ctx_stream(ctx);
-    const bool general = !t->fast;
+    const bool general = !t->fast || t->ks.weights != nullptr;  // carry row indices (representatives / weights)
     const size_t n_alloc = (size_t)std::max<unsigned long long>(n, 1);
     unsigned long long *off1 = nullptr, *totals = nullptr, *h1 = nullptr, *r1 = nullptr;
     FQ_HIP(ctx, buf.alloc((void**)&off1, sizeof(unsigned long long) * (size_t)xgrid * kDigitBins));
@@ -1120,7 +1208,7 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
 int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
     hipStream_t s = dq::ctx_stream(ctx);
     DevBuf buf;
-    const bool general = !t->fast;
+    const bool general = !t->fast || t->ks.weights != nullptr;  // carry row indices (representatives / weights)
     const bool no_partition = getenv("DQ_FREQ_NO_PARTITION") != nullptr;
     for (int seed_attempt = 0; seed_attempt < 4; ++seed_attempt) {
         unsigned long long *hs = nullptr, *rows = nullptr, *bk = nullptr;
@@ -1226,8 +1314,17 @@ extern "C" {
 
 int dq_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
                    int nkeys, uint32_t flags, dq_freq_table** out) {
-    if (!ctx || !out || nkeys <= 0 || nkeys > kMaxKeys || nrows < 0)
+    dq_freq_options o;
+    memset(&o, 0, sizeof(o));
+    o.flags = flags;
+    return dq_frequencies_ex(ctx, columns, ncols, nrows, key_columns, nkeys, &o, out);
+}
+
+int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
+                      int nkeys, const dq_freq_options* opt, dq_freq_table** out) {
+    if (!ctx || !out || !opt || nkeys <= 0 || nkeys > kMaxKeys || nrows < 0)
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_frequencies: invalid arguments");
+    const uint32_t flags = opt->flags;
     *out = nullptr;
     const int dev = dq::ctx_device(ctx);
     FQ_HIP(ctx, hipSetDevice(dev));
@@ -1284,6 +1381,18 @@ int dq_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nro
             return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_frequencies: unsupported key type");
         }
     }
+    if (opt->weights && nrows > 0) {
+        if (opt->weights_device) {
+            t->ks.weights = reinterpret_cast<const long long*>(opt->weights);
+        } else {
+            void* w = nullptr;
+            FQ_HIP(ctx, hipMalloc(&w, (size_t)nrows * 8));
+            staged.push_back(w);
+            FQ_HIP(ctx, hipMemcpyAsync(w, opt->weights, (size_t)nrows * 8, hipMemcpyHostToDevice, s));
+            t->ks.weights = reinterpret_cast<const long long*>(w);
+        }
+    }
+    t->key_type = opt->key_type ? opt->key_type : t->ks.cols[0].spark_type;
     t->ks.ncols = nkeys;
     t->ks.include_nulls = (flags & DQ_FREQ_INCLUDE_NULLS) ? 1 : 0;
     t->ks.fast = (nkeys == 1 && t->ks.cols[0].spark_type != DQ_TYPE_STRING) ? 1 : 0;
@@ -1312,7 +1421,8 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
     if (!ctx || !t || !out) return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_summarize: invalid arguments");
     FQ_HIP(ctx, hipSetDevice(t->device));
     hipStream_t s = dq::ctx_stream(ctx);
-    const int64_t n = entropy_rows > 0 ? entropy_rows : (int64_t)t->host_ctr.num_rows;
+    const int64_t table_rows = t->num_rows_override >= 0 ? t->num_rows_override : (int64_t)t->host_ctr.num_rows;
+    const int64_t n = entropy_rows > 0 ? entropy_rows : table_rows;
     if (t->cached_n == n) {  // one table scan serves every analyzer of the grouping
         *out = t->cached;
         return DQ_OK;
@@ -1348,7 +1458,7 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
             add_term(-q * log(q));
         }
     }
-    out->num_rows = (int64_t)t->host_ctr.num_rows;
+    out->num_rows = table_rows;
     out->num_groups = (int64_t)groups;
     out->num_unique = (int64_t)unique;
     out->entropy = ent;
@@ -1361,7 +1471,7 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
     return DQ_OK;
 }
 
-static int64_t compact(dq_ctx* ctx, const dq_freq_table* t, int mode, unsigned int thr, uint64_t limit,
+static int64_t compact(dq_ctx* ctx, const dq_freq_table* t, int mode, unsigned long long thr, uint64_t limit,
                        std::vector<unsigned long long>& keys, std::vector<unsigned long long>& counts) {
     hipStream_t s = dq::ctx_stream(ctx);
     unsigned long long* per_block = (unsigned long long*)((char*)t->scratch + kScanBlocks * sizeof(SummaryPartial));
@@ -1386,7 +1496,7 @@ static int64_t compact(dq_ctx* ctx, const dq_freq_table* t, int mode, unsigned i
     if (hipMalloc(&dk, n * 8) != hipSuccess || hipMalloc(&dc, n * 8) != hipSuccess) return -1;
     if (hipMemcpyAsync(offsets, off.data(), kScanBlocks * 8, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
     hipLaunchKernelGGL(compact_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->reps, t->cap, mode, thr,
-                       offsets, (unsigned long long)n, dk, dc);
+                       offsets, (unsigned long long)n, dk, dc, 0);
     bool ok = hipMemcpyAsync(keys.data(), dk, n * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
               hipMemcpyAsync(counts.data(), dc, n * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
               hipStreamSynchronize(s) == hipSuccess;
@@ -1427,11 +1537,11 @@ int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* t, int64_t k, int64_t* key
     // Radix select of the k-th largest count over three 11-bit digits.
     unsigned long long* hist = (unsigned long long*)((char*)t->scratch + kScanBlocks * sizeof(SummaryPartial) +
                                                      2 * kScanBlocks * 8);
-    unsigned int prefix = 0, prefix_mask = 0;
+    unsigned long long prefix = 0, prefix_mask = 0;
     uint64_t remaining = (uint64_t)k;
     std::vector<unsigned long long> h(2048);
     bool exhausted = false;
-    for (int shift : {22, 11, 0}) {
+    for (int shift : {33, 22, 11, 0}) {  // 44-bit counts (>> any row count)
         if (hipMemsetAsync(hist, 0, 2048 * 8, s) != hipSuccess) return DQ_ERR_DEVICE;
         hipLaunchKernelGGL(digit_hist_kernel, dim3(scan_grid(t->cap)), dim3(kFreqBlock), 0, s, t->slots, t->cap, shift,
                            prefix_mask, prefix, hist);
@@ -1450,8 +1560,8 @@ int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* t, int64_t k, int64_t* key
         }
 
         remaining -= acc;
-        prefix |= (unsigned int)d << shift;
-        prefix_mask |= 2047u << shift;
+        prefix |= (unsigned long long)d << shift;
+        prefix_mask |= 2047ull << shift;
     }
     std::vector<unsigned long long> gk, gc, tk, tc;
     if (exhausted) {
@@ -1473,6 +1583,143 @@ int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* t, int64_t k, int64_t* key
         counts[i] = (int64_t)all[i].first;
     }
     return n;
+}
+
+
+int64_t dq_freq_export_device(dq_ctx* ctx, const dq_freq_table* t, int64_t capacity, int64_t* keys_dev,
+                              int64_t* counts_dev) {
+    if (!ctx || !t || capacity < 0 || (capacity > 0 && (!keys_dev || !counts_dev)))
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_export_device: invalid arguments");
+    if (!t->fast) return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_freq_export_device: table keys are row references");
+    FQ_HIP(ctx, hipSetDevice(t->device));
+    hipStream_t s = dq::ctx_stream(ctx);
+    unsigned long long* per_block = (unsigned long long*)((char*)t->scratch + kScanBlocks * sizeof(SummaryPartial));
+    unsigned long long* offsets = per_block + kScanBlocks;
+    hipLaunchKernelGGL(count_selected_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->cap, 2, 0ull,
+                       per_block);
+    std::vector<unsigned long long> pb(kScanBlocks), off(kScanBlocks);
+    FQ_HIP(ctx, hipMemcpyAsync(pb.data(), per_block, kScanBlocks * 8, hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    unsigned long long total = 0;
+    for (int b = 0; b < kScanBlocks; ++b) {
+        off[b] = total;
+        total += pb[b];
+    }
+    const uint64_t n = std::min<uint64_t>(total, (uint64_t)capacity);
+    if (n) {
+        FQ_HIP(ctx, hipMemcpyAsync(offsets, off.data(), kScanBlocks * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(compact_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, (const unsigned long long*)nullptr,
+                           t->cap, 2, 0ull, offsets, (unsigned long long)n, (unsigned long long*)keys_dev,
+                           (unsigned long long*)counts_dev, 1);
+        FQ_HIP(ctx, hipGetLastError());
+    }
+    int64_t written = (int64_t)n;
+    if (t->host_ctr.sentinel && written < capacity) {
+        const int64_t kv[2] = {(int64_t)unmix64(kEmpty), (int64_t)t->host_ctr.sentinel};
+        FQ_HIP(ctx, hipMemcpyAsync(keys_dev + written, &kv[0], 8, hipMemcpyHostToDevice, s));
+        FQ_HIP(ctx, hipMemcpyAsync(counts_dev + written, &kv[1], 8, hipMemcpyHostToDevice, s));
+        ++written;
+    }
+    FQ_HIP(ctx, hipStreamSynchronize(s));  // kv lives on this stack frame
+    return written;
+}
+
+int dq_freq_from_pairs(dq_ctx* ctx, int32_t key_spark_type, const int64_t* keys, const int64_t* counts, int64_t n,
+                       uint32_t flags, int64_t num_rows, int64_t null_count, dq_freq_table** out) {
+    if (!ctx || !out || n < 0 || (n > 0 && (!keys || !counts)) || num_rows < 0 || null_count < 0 ||
+        elem_of(key_spark_type) == ET_NONE)
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_from_pairs: invalid arguments");
+    dq_column col;
+    memset(&col, 0, sizeof(col));
+    col.spark_type = DQ_TYPE_LONG;  // canonical 64-bit keys (their LONG canonical form is the identity)
+    col.length = n;
+    col.values = keys;
+    col.flags = (flags & DQ_FREQ_PAIRS_DEVICE) ? DQ_COL_DEVICE : 0u;
+    dq_freq_options o;
+    memset(&o, 0, sizeof(o));
+    o.weights = counts;
+    o.weights_device = (flags & DQ_FREQ_PAIRS_DEVICE) ? 1u : 0u;
+    o.key_type = key_spark_type;
+    const int32_t key0 = 0;
+    const int rc = dq_frequencies_ex(ctx, &col, 1, n, &key0, 1, &o, out);
+    if (rc) return rc;
+    (*out)->num_rows_override = num_rows;
+    (*out)->host_ctr.nulls = (unsigned long long)null_count;
+    (*out)->cached_n = -1;
+    return DQ_OK;
+}
+
+int dq_freq_merge(dq_ctx* ctx, const dq_freq_table* a, const dq_freq_table* b, dq_freq_table** out) {
+    if (!ctx || !a || !b || !out) return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_merge: invalid arguments");
+    if (!a->fast || !b->fast)
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_freq_merge: both tables must have one fixed-width key column");
+    if (elem_of(a->key_type) != elem_of(b->key_type) || (a->key_type == DQ_TYPE_DOUBLE) != (b->key_type == DQ_TYPE_DOUBLE))
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_merge: key types differ");
+    FQ_HIP(ctx, hipSetDevice(a->device));
+    dq_freq_summary sa, sb;
+    int rc = dq_freq_summarize(ctx, a, 0, &sa);
+    if (rc) return rc;
+    rc = dq_freq_summarize(ctx, b, 0, &sb);
+    if (rc) return rc;
+    const int64_t ca = sa.num_groups - (sa.null_count ? 1 : 0), cb = sb.num_groups - (sb.null_count ? 1 : 0);
+    DevBuf buf;
+    int64_t *k = nullptr, *c = nullptr;
+    FQ_HIP(ctx, buf.alloc((void**)&k, (size_t)std::max<int64_t>(ca + cb, 1) * 8));
+    FQ_HIP(ctx, buf.alloc((void**)&c, (size_t)std::max<int64_t>(ca + cb, 1) * 8));
+    const int64_t na = dq_freq_export_device(ctx, a, ca, k, c);
+    if (na < 0) return (int)na;
+    const int64_t nb = dq_freq_export_device(ctx, b, cb, k + na, c + na);
+    if (nb < 0) return (int)nb;
+    rc = dq_freq_from_pairs(ctx, a->key_type, k, c, na + nb, DQ_FREQ_PAIRS_DEVICE, sa.num_rows + sb.num_rows,
+                            sa.null_count + sb.null_count, out);
+    if (rc == DQ_OK) {
+        // the pair arrays are this call's scratch: the merged table only keeps its slots
+        FQ_HIP(ctx, hipStreamSynchronize(dq::ctx_stream(ctx)));
+        (*out)->ks.weights = nullptr;
+        (*out)->ks.cols[0].values = nullptr;
+    }
+    return rc;
+}
+
+int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq_freq_table* x,
+                               const dq_freq_table* y, double* mi, int32_t* present) {
+    if (!ctx || !joint || !x || !y || !mi || !present)
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_mutual_information: invalid arguments");
+    if (joint->fast || joint->ks.ncols != 2 || !joint->reps || x->ks.ncols != 1 || y->ks.ncols != 1 ||
+        x->ks.weights || y->ks.weights || joint->ks.weights)
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT,
+                            "dq_freq_mutual_information: needs the (x, y) table and the x / y tables of the same rows");
+    FQ_HIP(ctx, hipSetDevice(joint->device));
+    hipStream_t s = dq::ctx_stream(ctx);
+    LookupTable X, Y;
+    X.slots = x->slots;
+    X.ks = x->ks;
+    X.sentinel = x->host_ctr.sentinel;
+    X.bits = x->bits;
+    Y.slots = y->slots;
+    Y.ks = y->ks;
+    Y.sentinel = y->host_ctr.sentinel;
+    Y.bits = y->bits;
+    const int64_t n = joint->num_rows_override >= 0 ? joint->num_rows_override : (int64_t)joint->host_ctr.num_rows;
+    SummaryPartial* parts = (SummaryPartial*)joint->scratch;
+    hipLaunchKernelGGL(mi_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, joint->slots, joint->reps, joint->cap,
+                       joint->ks, X, Y, (double)n, parts);
+    FQ_HIP(ctx, hipGetLastError());
+    std::vector<SummaryPartial> hp(kScanBlocks);
+    FQ_HIP(ctx, hipMemcpyAsync(hp.data(), parts, sizeof(SummaryPartial) * kScanBlocks, hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    unsigned long long groups = 0;
+    double sum = 0.0, comp = 0.0;
+    for (const SummaryPartial& p : hp) {
+        groups += p.groups;
+        const double yk = (p.ent - p.comp) - comp;
+        const double tt = sum + yk;
+        comp = (tt - sum) - yk;
+        sum = tt;
+    }
+    *mi = sum;
+    *present = groups > 0 ? 1 : 0;  // sum over zero joined rows is NULL (A/MutualInformation.scala:82-86)
+    return DQ_OK;
 }
 
 void dq_freq_free(dq_ctx* ctx, dq_freq_table* t) {

@@ -515,24 +515,36 @@ __device__ __forceinline__ void to_partial(ColPartial& p, const IAcc& a) {
 }
 
 // Per-lane fold of one 8-row batch (Spark's per-row updates restated as a batch + Chan merge).
+// Masked rows are sanitised once: to 0.0 for the sum and the moments, to NaN for min / max (v_min_f64 /
+// v_max_f64 return the non-NaN operand, so a NaN stand-in drops out exactly like a skipped row; the two
+// stand-ins share their low word). NaN values that are valid rows make the batch sum NaN, so they are
+// counted only in that (rare, divergent) case: Spark orders NaN above every double, which the finaliser
+// applies through nnan (max = NaN if nnan > 0, min = NaN if nnan == n). An inf - inf batch sum also lands
+// in that branch and counts zero NaNs.
 __device__ __forceinline__ void accumulate(FAcc& a, const uint64_t (&v)[8], uint32_t m, uint32_t flags) {
     const int cnt = __popc(m);
     if (cnt == 0) return;
     if (flags & (CF_STATS | CF_MOMENTS)) {
-        uint32_t nanm = 0;
-        double s = 0.0, mn = INFINITY, mx = -INFINITY;
+        double xz[8];
+        double s = 0.0, mn = __builtin_nan(""), mx = __builtin_nan("");
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const double x = as_f64(v[k]);
             const bool on = (m >> k) & 1u;
-            const bool nan = x != x;
-            nanm |= (on && nan) ? (1u << k) : 0u;
-            const bool use = on && !nan;
-            s += on ? x : 0.0;
-            mn = fmin(mn, use ? x : INFINITY);
-            mx = fmax(mx, use ? x : -INFINITY);
+            const uint32_t lo = on ? (uint32_t)v[k] : 0u;
+            const uint32_t hz = on ? (uint32_t)(v[k] >> 32) : 0u;
+            const uint32_t hn = on ? (uint32_t)(v[k] >> 32) : 0x7FF80000u;
+            xz[k] = as_f64(((uint64_t)hz << 32) | lo);
+            const double xn = as_f64(((uint64_t)hn << 32) | lo);
+            s += xz[k];
+            mn = fmin(mn, xn);
+            mx = fmax(mx, xn);
         }
-        a.nnan += __popc(nanm);
+        if (s != s) {  // a NaN among the valid rows (or inf - inf): count the NaNs exactly
+            int nn = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) nn += (((m >> k) & 1u) && as_f64(v[k]) != as_f64(v[k])) ? 1 : 0;
+            a.nnan += nn;
+        }
         a.sum += s;
         a.mn = fmin(a.mn, mn);
         a.mx = fmax(a.mx, mx);
@@ -541,8 +553,8 @@ __device__ __forceinline__ void accumulate(FAcc& a, const uint64_t (&v)[8], uint
             double m2b = 0.0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const double d = as_f64(v[k]) - mb;
-                m2b += ((m >> k) & 1u) ? d * d : 0.0;
+                const double d = ((m >> k) & 1u) ? xz[k] - mb : 0.0;
+                m2b = __builtin_fma(d, d, m2b);
             }
             moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
         }
@@ -569,15 +581,19 @@ __device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint
     }
     if (flags & CF_MOMENTS) {
         // Spark casts each value to Double before the moment update (C/StatefulStdDevPop.scala:24).
+        double xd[8];
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s += ((m >> k) & 1u) ? (double)(int64_t)v[k] : 0.0;
+        for (int k = 0; k < 8; ++k) {
+            xd[k] = (double)(int64_t)v[k];
+            s += ((m >> k) & 1u) ? xd[k] : 0.0;
+        }
         const double mb = s * rcp_refined((double)cnt);
         double m2b = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const double d = (double)(int64_t)v[k] - mb;
-            m2b += ((m >> k) & 1u) ? d * d : 0.0;
+            const double d = ((m >> k) & 1u) ? xd[k] - mb : 0.0;
+            m2b = __builtin_fma(d, d, m2b);
         }
         moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
     }
@@ -585,25 +601,29 @@ __device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint
 }
 
 // Rows of mask m where `value <op> constant` holds (Spark comparison semantics: integral vs long
-// constant compares as long; otherwise as double with NaN above every number and NaN = NaN).
+// constant compares as long; otherwise as double with NaN above every number and NaN = NaN). Branch-free:
+// the comparison's sign selects a bit of the operator's 3-bit truth mask (bit 0: <, bit 1: =, bit 2: >).
+__device__ __forceinline__ uint32_t cmp_truth_mask(int op) {
+    switch (op) {
+        case DQ_P_EQ: return 2u;
+        case DQ_P_NE: return 5u;
+        case DQ_P_LT: return 1u;
+        case DQ_P_LE: return 3u;
+        case DQ_P_GT: return 4u;
+        default: return 6u;  // GE
+    }
+}
+
 template <bool F>
 __device__ __forceinline__ int fused_pred_count(const ColDesc& c, const uint64_t (&v)[8], uint32_t m) {
+    const uint32_t truth = cmp_truth_mask(c.pred_op);  // wave-uniform
     uint32_t hit = 0;
     if (!F && c.pred_kind == FP_LONG) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int64_t x = (int64_t)v[k];
-            const int cmp = x < c.pred_i ? -1 : (x > c.pred_i ? 1 : 0);
-            bool r;
-            switch (c.pred_op) {
-                case DQ_P_EQ: r = cmp == 0; break;
-                case DQ_P_NE: r = cmp != 0; break;
-                case DQ_P_LT: r = cmp < 0; break;
-                case DQ_P_LE: r = cmp <= 0; break;
-                case DQ_P_GT: r = cmp > 0; break;
-                default: r = cmp >= 0; break;
-            }
-            hit |= r ? (1u << k) : 0u;
+            const uint32_t sel = x < c.pred_i ? 0u : (x > c.pred_i ? 2u : 1u);
+            hit |= ((truth >> sel) & 1u) << k;
         }
     } else {
         const double y = c.pred_kind == FP_LONG ? (double)c.pred_i : c.pred_d;
@@ -612,17 +632,8 @@ __device__ __forceinline__ int fused_pred_count(const ColDesc& c, const uint64_t
         for (int k = 0; k < 8; ++k) {
             const double x = to_double(v[k], F);
             const bool xn = x != x;
-            const int cmp = (xn || yn) ? ((xn && yn) ? 0 : (xn ? 1 : -1)) : (x < y ? -1 : (x > y ? 1 : 0));
-            bool r;
-            switch (c.pred_op) {
-                case DQ_P_EQ: r = cmp == 0; break;
-                case DQ_P_NE: r = cmp != 0; break;
-                case DQ_P_LT: r = cmp < 0; break;
-                case DQ_P_LE: r = cmp <= 0; break;
-                case DQ_P_GT: r = cmp > 0; break;
-                default: r = cmp >= 0; break;
-            }
-            hit |= r ? (1u << k) : 0u;
+            const uint32_t sel = (xn || yn) ? ((xn && yn) ? 1u : (xn ? 2u : 0u)) : (x < y ? 0u : (x > y ? 2u : 1u));
+            hit |= ((truth >> sel) & 1u) << k;
         }
     }
     return __popc(hit & m);
@@ -673,19 +684,25 @@ __device__ __forceinline__ int hash_class(int spark_type) {
 // no-return ds_max atomics (fire-and-forget: no LDS latency on the critical path).
 template <int HC>
 __device__ __forceinline__ void hll_update8(uint32_t* regs, const uint64_t (&v)[8], uint32_t m) {
-    uint32_t packed[8];
+    // two groups of 4 independent hash chains: enough ILP for the VALU, half the live temporaries
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        uint64_t x;
-        if (HC == 0) x = xxh_int((uint32_t)(int32_t)(int64_t)v[k], SPARK_HLL_SEED);
-        else if (HC == 1) x = xxh_int(float_to_int_bits((float)as_f64(v[k])), SPARK_HLL_SEED);
-        else if (HC == 2) x = xxh_long(double_to_long_bits(as_f64(v[k])), SPARK_HLL_SEED);
-        else x = xxh_long(v[k], SPARK_HLL_SEED);
-        packed[k] = hll_index(x) | (hll_rank(x) << 16);
+    for (int g = 0; g < 8; g += 4) {
+        uint32_t packed[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t vk = v[g + k];
+            uint64_t x;
+            if (HC == 0) x = xxh_int((uint32_t)(int32_t)(int64_t)vk, SPARK_HLL_SEED);
+            else if (HC == 1) x = xxh_int(float_to_int_bits((float)as_f64(vk)), SPARK_HLL_SEED);
+            else if (HC == 2) x = xxh_long(double_to_long_bits(as_f64(vk)), SPARK_HLL_SEED);
+            else x = xxh_long(vk, SPARK_HLL_SEED);
+            packed[k] = hll_index(x) | (hll_rank(x) << 16);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if ((m >> (g + k)) & 1u) atomicMax(&regs[packed[k] & 0xffffu], packed[k] >> 16);
+        __builtin_amdgcn_sched_barrier(0);
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if ((m >> k) & 1u) atomicMax(&regs[packed[k] & 0xffffu], packed[k] >> 16);
 }
 
 // The hash class follows from the storage shape except for mixed-width pairs (P = 8): 8-byte
@@ -723,8 +740,11 @@ struct BlockRed {
     int64_t wt[kBlock / 64], wnn[kBlock / 64];
 };
 
+#ifndef DQ_HEAVY_PAIR_MINB
+#define DQ_HEAVY_PAIR_MINB 1
+#endif
 template <int P, int NC, bool F0, bool F1, bool HEAVY>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock, (HEAVY && NC > 1) ? DQ_HEAVY_PAIR_MINB : 1)
 scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__ group, int ngroup,
                    int64_t nrows, int64_t ntiles, int gstride, SlotPartial* __restrict__ partials,
                    uint8_t* __restrict__ hll_partials) {
@@ -792,14 +812,41 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
             load_values<P, F0>(c0, t * kTileRows, tid, true, nrows, x);
             if (NC > 1) load_values<P, F1>(c1, t * kTileRows, tid, true, nrows, y);
         }
+        if (!kDoubleBuffer && t < nfull) {
+            load_values<P, F0>(c0, t * kTileRows, tid, true, nrows, x);
+            load_values<P, F1>(c1, t * kTileRows, tid, true, nrows, y);
+        }
         for (; t < nfull; t += G) {
             const int64_t tn = t + G;
             if (!kDoubleBuffer) {
-                // Two-column HEAVY kernels: no register double buffer (it costs 32 VGPRs and pushes
-                // them to 1 wave/SIMD); a second resident wave hides the load latency instead.
-                load_values<P, F0>(c0, t * kTileRows, tid, true, nrows, x);
-                if (NC > 1) load_values<P, F1>(c1, t * kTileRows, tid, true, nrows, y);
-                fold(t * kTileRows, true, x, y);
+                // Two-column HEAVY kernels: no second register set (it costs 32 VGPRs and drops them to
+                // 1 wave/SIMD). Instead the phases run in the order corr(x, y) -> x -> y, and each column's
+                // registers are refilled with the next tile's values as soon as that column is done, so the
+                // loads of x overlap the work on y and the loads of y the next tile's corr + x work.
+                const int64_t tb = t * kTileRows;
+                uint32_t mx = bits_valid<P>(c0.validity, tb, tid, true, nrows);
+                uint32_t my = bits_valid<P>(c1.validity, tb, tid, true, nrows);
+                if (has_where) {
+                    const uint32_t w = bits_padded<P>(sd.where_t, tb, tid);
+                    wt += __popc(w);
+                    wnn += __popc(bits_padded<P>(sd.where_nn, tb, tid));
+                    mx &= w;
+                    my &= w;
+                }
+                accumulate_corr<F0, F1>(cp, x, y, mx & my);
+                __builtin_amdgcn_sched_barrier(0);
+                accumulate(a0, x, mx, c0.flags);
+                __builtin_amdgcn_sched_barrier(0);
+                if (c0.pred_kind) a0.pt += fused_pred_count<F0>(c0, x, mx);
+                if (hll0) hll_update<P, F0>(hll_lds[0], x, mx, c0.spark_type);
+                __builtin_amdgcn_sched_barrier(0);
+                if (tn < nfull) load_values<P, F0>(c0, tn * kTileRows, tid, true, nrows, x);
+                accumulate(a1, y, my, c1.flags);
+                __builtin_amdgcn_sched_barrier(0);
+                if (c1.pred_kind) a1.pt += fused_pred_count<F1>(c1, y, my);
+                if (hll1) hll_update<P, F1>(hll_lds[NC - 1], y, my, c1.spark_type);
+                __builtin_amdgcn_sched_barrier(0);
+                if (tn < nfull) load_values<P, F1>(c1, tn * kTileRows, tid, true, nrows, y);
                 continue;
             }
             if (tn < nfull) {
@@ -887,6 +934,7 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
         __syncthreads();
     }
 }
+
 
 // Bits-only slots (Size(where), Completeness of an unread column, Compliance): one 64-row bitmap
 // word per lane per step, tiles interleaved over workgroups like the value kernels.

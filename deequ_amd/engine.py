@@ -47,19 +47,126 @@ class GroupFloat(float):
         return hash(("GroupFloat", self._bits()))
 
 
-class FrequencyTable:
-    """Device-resident (key -> count) table built by dq_frequencies over `key_columns` of `source`."""
+def decode_canonical(spark_type, decimal_scale, k):
+    """Canonical 64-bit key (DQ_FREQ_KEYS_VALUES) of a fixed-width column -> its Python group value."""
+    u = np.uint64(int(k) & 0xFFFFFFFFFFFFFFFF)
+    if spark_type == N.TYPE_DOUBLE:
+        return GroupFloat(u.view(np.float64))
+    if spark_type == N.TYPE_FLOAT:
+        return GroupFloat(np.uint32(int(u) & 0xFFFFFFFF).view(np.float32))
+    i = int(u.view(np.int64))
+    if spark_type == N.TYPE_BOOLEAN:
+        return bool(i)
+    if spark_type == N.TYPE_DECIMAL:
+        from decimal import Decimal
+        return Decimal(i).scaleb(-decimal_scale)
+    return i
 
-    def __init__(self, context, handle, source, key_columns, include_nulls):
+
+def canonical_keys(spark_type, values):
+    """numpy values of a fixed-width key column -> canonical 64-bit keys (int64 view): integers sign-extended,
+    FLOAT / DOUBLE bit patterns with NaN canonical (Spark's binary grouping equality)."""
+    v = np.asarray(values)
+    if spark_type == N.TYPE_DOUBLE:
+        b = v.astype(np.float64).view(np.uint64).copy()
+        b[np.isnan(v)] = np.uint64(0x7FF8000000000000)
+        return b.view(np.int64)
+    if spark_type == N.TYPE_FLOAT:
+        f = v.astype(np.float32)
+        b = f.view(np.uint32).astype(np.uint64)
+        b[np.isnan(f)] = np.uint64(0x7FC00000)
+        return b.view(np.int64)
+    return v.astype(np.int64)
+
+
+class PairFrequencies:
+    """A frequency state held as (canonical key, count) arrays on the host — a persisted state read back by
+    HdfsStateProvider — for one fixed-width key column. Merges with a device table on the GPU
+    (dq_freq_from_pairs + dq_freq_merge); as_dict() decodes it for host-side consumers."""
+
+    def __init__(self, key_type, keys, counts, num_rows, null_count=0, decimal_scale=0, names=None):
+        self.key_type, self.decimal_scale = key_type, decimal_scale
+        self.keys = np.ascontiguousarray(keys, dtype=np.int64)
+        self.counts = np.ascontiguousarray(counts, dtype=np.int64)
+        self.num_rows, self.null_count = int(num_rows), int(null_count)
+        self.names = names
+
+    def to_dict(self):
+        out = {}
+        for k, c in zip(self.keys.tolist(), self.counts.tolist()):
+            key = (decode_canonical(self.key_type, self.decimal_scale, k),)
+            out[key] = out.get(key, 0) + int(c)
+        if self.null_count:
+            out[(None,)] = self.null_count
+        return out
+
+    def to_device(self):
+        return FrequencyTable.from_pairs(self.key_type, self.keys, self.counts, self.num_rows, self.null_count,
+                                         self.decimal_scale, self.names)
+
+
+class FrequencyTable:
+    """Device-resident (key -> count) table built by dq_frequencies over `key_columns` of `source` (or from
+    (key, count) pairs: source None, `key_type` the canonical keys' Spark type)."""
+
+    def __init__(self, context, handle, source, key_columns, include_nulls, key_type=None, decimal_scale=0):
         self.ctx = context
         self.handle = handle
         self.source = source
-        self.key_columns = [source[c] for c in key_columns]
+        self.key_columns = [source[c] for c in key_columns] if source is not None else []
         self.names = list(key_columns)
         self.include_nulls = include_nulls
+        if key_type is None and self.key_columns:
+            key_type, decimal_scale = self.key_columns[0].spark_type, self.key_columns[0].decimal_scale
+        self.key_type, self.decimal_scale = key_type, decimal_scale
         s = self.summary(None)
         self.num_rows = s["num_rows"]
         self.num_groups = s["num_groups"]
+
+    @classmethod
+    def from_pairs(cls, key_type, keys, counts, num_rows, null_count=0, decimal_scale=0, names=None,
+                   device_ptrs=False):
+        """dq_freq_from_pairs: the table of (canonical key, count) pairs (numpy arrays, or device pointers)."""
+        context = ctx()
+        handle = ctypes.c_void_p()
+        if device_ptrs:
+            kp, cp, n = keys[0], counts[0], keys[1]
+        else:
+            keys = np.ascontiguousarray(keys, dtype=np.int64)
+            counts = np.ascontiguousarray(counts, dtype=np.int64)
+            kp, cp, n = keys.ctypes.data, counts.ctypes.data, len(keys)
+        rc = context.lib.dq_freq_from_pairs(context.handle, int(key_type), ctypes.c_void_p(kp), ctypes.c_void_p(cp),
+                                            int(n), N.FREQ_PAIRS_DEVICE if device_ptrs else 0, int(num_rows),
+                                            int(null_count), ctypes.byref(handle))
+        context.check(rc, "dq_freq_from_pairs")
+        return cls(context, handle, None, list(names or ["k"]), bool(null_count), key_type, decimal_scale)
+
+    def merge(self, other):
+        """FrequenciesAndNumRows.sum on the GPU (dq_freq_merge)."""
+        handle = ctypes.c_void_p()
+        rc = self.ctx.lib.dq_freq_merge(self.ctx.handle, self.handle, other.handle, ctypes.byref(handle))
+        self.ctx.check(rc, "dq_freq_merge")
+        return FrequencyTable(self.ctx, handle, None, self.names, self.include_nulls or other.include_nulls,
+                              self.key_type, self.decimal_scale)
+
+    def export_pairs(self):
+        """(canonical keys, counts) numpy arrays of a DQ_FREQ_KEYS_VALUES table (NULL group excluded)."""
+        n = self.num_groups
+        keys = np.zeros(max(n, 1), dtype=np.int64)
+        counts = np.zeros(max(n, 1), dtype=np.int64)
+        got = self.ctx.lib.dq_freq_export(self.ctx.handle, self.handle, n, keys.ctypes.data, counts.ctypes.data)
+        if got < 0:
+            raise N.NativeError(int(got), "dq_freq_export: %s" % self.ctx.last_error())
+        return keys[:got], counts[:got]
+
+    def mutual_information(self, x_table, y_table):
+        """dq_freq_mutual_information over this (x, y) table and the x / y tables: (value, present)."""
+        mi = ctypes.c_double(0.0)
+        present = ctypes.c_int32(0)
+        rc = self.ctx.lib.dq_freq_mutual_information(self.ctx.handle, self.handle, x_table.handle, y_table.handle,
+                                                     ctypes.byref(mi), ctypes.byref(present))
+        self.ctx.check(rc, "dq_freq_mutual_information")
+        return mi.value, bool(present.value)
 
     def __del__(self):
         try:
@@ -90,19 +197,7 @@ class FrequencyTable:
 
     def _decode_value(self, k):
         """Canonical 64-bit key of the single fixed-width key column -> Python value."""
-        c = self.key_columns[0]
-        u = np.uint64(k & 0xFFFFFFFFFFFFFFFF)
-        if c.spark_type == N.TYPE_DOUBLE:
-            return GroupFloat(u.view(np.float64))
-        if c.spark_type == N.TYPE_FLOAT:
-            return GroupFloat(np.uint32(int(u) & 0xFFFFFFFF).view(np.float32))
-        i = int(u.view(np.int64))
-        if c.spark_type == N.TYPE_BOOLEAN:
-            return bool(i)
-        if c.spark_type == N.TYPE_DECIMAL:
-            from decimal import Decimal
-            return Decimal(i).scaleb(-c.decimal_scale)
-        return i
+        return decode_canonical(self.key_type, self.decimal_scale, k)
 
     def _decode(self, k):
         if self.key_kind() == N.FREQ_KEYS_VALUES:
@@ -120,7 +215,7 @@ class FrequencyTable:
         out = [(self._decode(keys[i]), int(counts[i])) for i in range(n)]
         nulls = self.summary(None)["null_count"]
         if nulls:
-            out.append(((None,) * len(self.key_columns), int(nulls)))
+            out.append(((None,) * max(len(self.names), 1), int(nulls)))
             out.sort(key=lambda kv: -kv[1])
             out = out[:k]
         return out
@@ -135,7 +230,7 @@ class FrequencyTable:
         out = {self._decode(keys[i]): int(counts[i]) for i in range(got)}
         nulls = self.summary(None)["null_count"]
         if nulls:
-            out[(None,) * len(self.key_columns)] = int(nulls)
+            out[(None,) * max(len(self.names), 1)] = int(nulls)
         return out
 
 

@@ -10,7 +10,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdq.so")
+LIB_PATH = os.environ.get("DQ_LIBRARY") or os.path.join(_HERE, "libdq.so")
 
 # ---- constants mirrored from include/dq.h -------------------------------------------------------
 DQ_OK = 0
@@ -25,6 +25,7 @@ COL_DEVICE = 0x1
 SCAN_OUT_DEVICE = 0x1
 FREQ_INCLUDE_NULLS = 0x1
 FREQ_KEYS_VALUES, FREQ_KEYS_ROWS = 0, 1
+FREQ_PAIRS_DEVICE = 0x1
 
 OP_SIZE, OP_COMPLETENESS, OP_COMPLIANCE, OP_MEAN, OP_SUM, OP_MINIMUM, OP_MAXIMUM, OP_STANDARD_DEVIATION, \
     OP_CORRELATION, OP_APPROX_COUNT_DISTINCT, OP_MIN_LENGTH, OP_MAX_LENGTH, OP_DATATYPE = range(1, 14)
@@ -47,7 +48,8 @@ EXPORTED_SYMBOLS = (
     "dq_scan_launch_count", "dq_state_merge", "dq_state_fold", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
     "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
     "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
-    "dq_synth_validity",
+    "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge",
+    "dq_freq_mutual_information",
 )
 
 
@@ -121,6 +123,11 @@ class DqFreqSummary(ctypes.Structure):
                 ("null_count", ctypes.c_int64)]
 
 
+class DqFreqOptions(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint32), ("weights_device", ctypes.c_uint32), ("weights", ctypes.c_void_p),
+                ("key_type", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
 STATE_SIZE = ctypes.sizeof(DqState)
 
 
@@ -176,6 +183,12 @@ def load_library(path=None):
             "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
             "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
             "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),
+            "dq_frequencies_ex": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
+            "dq_freq_export_device": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+            "dq_freq_from_pairs": (c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_int64, c_uint32, c_int64,
+                                           c_int64, c_void_p]),
+            "dq_freq_merge": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+            "dq_freq_mutual_information": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)

@@ -18,6 +18,8 @@ import os
 import struct
 
 from . import analyzers as A
+from . import engine
+from . import native as N
 from .states import (NumMatches, NumMatchesAndCount, SumState, MeanState, MinState, MaxState,
                      StandardDeviationState, CorrelationState, ApproxCountDistinctState, DataTypeHistogram,
                      ApproxQuantileState)
@@ -196,13 +198,16 @@ class HdfsStateProvider:
             if not self.allowOverwrite:
                 raise StateAlreadyExistsError("path %s already exists." % path)
             shutil.rmtree(path) if os.path.isdir(path) else os.remove(path)
-        freq = state.as_dict()
-        columns = list(state.columns) if state.columns else \
-            ["c%d" % i for i in range(len(next(iter(freq))) if freq else 1)]
-        keys = list(freq.keys())
-        counts = [freq[k] for k in keys]
-        arrays = [pa.array([k[i] for k in keys]) for i in range(len(columns))]
-        tbl = pa.Table.from_arrays(arrays + [pa.array(counts, type=pa.int64())], names=columns + [COUNT_COL])
+        tbl = _pairs_table(state)
+        if tbl is None:
+            freq = state.as_dict()
+            columns = list(state.columns) if state.columns else \
+                ["c%d" % i for i in range(len(next(iter(freq))) if freq else 1)]
+            keys = list(freq.keys())
+            counts = [freq[k] for k in keys]
+            arrays = [pa.array([k[i] for k in keys]) for i in range(len(columns))]
+            tbl = pa.Table.from_arrays(arrays + [pa.array(counts, type=pa.int64())], names=columns + [COUNT_COL])
+        keys = range(tbl.num_rows)
         os.makedirs(path)
         parts = max(1, min(self.numPartitionsForHistogram, len(keys)))
         step = -(-len(keys) // parts) if keys else 0
@@ -216,6 +221,10 @@ class HdfsStateProvider:
         import pyarrow.parquet as pq
         path = self._freq_dir(ident)
         files = sorted(f for f in os.listdir(path) if f.endswith(".parquet"))
+        (num_rows,) = struct.unpack(">q", self._read(self._bin(ident, "-num_rows"))[:8])
+        pairs = _load_pairs(path, files, num_rows)
+        if pairs is not None:
+            return pairs
         freq = {}
         columns = None
         for f in files:
@@ -226,8 +235,77 @@ class HdfsStateProvider:
             for key, c in zip(zip(*cols), t.column(COUNT_COL).to_pylist()):
                 key = A._canonical_group_key(key)  # floating keys join bitwise (GroupFloat), as in device tables
                 freq[key] = freq.get(key, 0) + int(c)
-        (num_rows,) = struct.unpack(">q", self._read(self._bin(ident, "-num_rows"))[:8])
         return A.FrequenciesAndNumRows(freq, num_rows, columns)
 
 
 FileSystemStateProvider = HdfsStateProvider
+
+
+# ---- columnar (key, count) persistence of single fixed-width-key frequency states --------------------
+def _arrow_of(spark_type):
+    import pyarrow as pa
+    return {N.TYPE_BYTE: pa.int8(), N.TYPE_SHORT: pa.int16(), N.TYPE_INT: pa.int32(), N.TYPE_LONG: pa.int64(),
+            N.TYPE_FLOAT: pa.float32(), N.TYPE_DOUBLE: pa.float64(), N.TYPE_BOOLEAN: pa.bool_(),
+            N.TYPE_DATE: pa.date32()}.get(spark_type)
+
+
+def _pairs_table(state):
+    """The parquet table of a single fixed-width-key state straight from its canonical (key, count) arrays
+    (no per-group Python objects), or None for other key shapes."""
+    import numpy as np
+    import pyarrow as pa
+    side = state._values_side()
+    if side is None or _arrow_of(side.key_type) is None:
+        return None
+    if isinstance(side, engine.PairFrequencies):
+        keys, counts, nulls = side.keys, side.counts, side.null_count
+    else:
+        keys, counts = side.export_pairs()
+        nulls = side.summary(None)["null_count"]
+    t = side.key_type
+    if t == N.TYPE_DOUBLE:
+        vals = pa.array(keys.view(np.float64))
+    elif t == N.TYPE_FLOAT:
+        vals = pa.array((keys.view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32))
+    elif t == N.TYPE_BOOLEAN:
+        vals = pa.array(keys != 0)
+    else:
+        vals = pa.array(keys).cast(_arrow_of(t))
+    counts = np.asarray(counts, dtype=np.int64)
+    if nulls:
+        vals = pa.concat_arrays([vals, pa.nulls(1, type=vals.type)])
+        counts = np.append(counts, np.int64(nulls))
+    name = (list(state.columns) or ["c0"])[0]
+    return pa.Table.from_arrays([vals, pa.array(counts, type=pa.int64())], names=[name, COUNT_COL])
+
+
+def _load_pairs(path, files, num_rows):
+    """A persisted single fixed-width-key frequency state as canonical (key, count) arrays
+    (engine.PairFrequencies), or None when the key columns are of another shape."""
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    if not files:
+        return None
+    t = pa.concat_tables([pq.read_table(os.path.join(path, f)) for f in files])
+    keys = [n for n in t.column_names if n != COUNT_COL]
+    if len(keys) != 1:
+        return None
+    arr = t.column(keys[0]).combine_chunks()
+    spark = {pa.int8(): N.TYPE_BYTE, pa.int16(): N.TYPE_SHORT, pa.int32(): N.TYPE_INT, pa.int64(): N.TYPE_LONG,
+             pa.float32(): N.TYPE_FLOAT, pa.float64(): N.TYPE_DOUBLE, pa.bool_(): N.TYPE_BOOLEAN,
+             pa.date32(): N.TYPE_DATE}.get(arr.type)
+    if spark is None:
+        return None
+    counts = np.asarray(t.column(COUNT_COL).combine_chunks().to_numpy(zero_copy_only=False), dtype=np.int64)
+    valid = ~np.asarray(arr.is_null().to_numpy(zero_copy_only=False), dtype=bool)
+    if spark == N.TYPE_BOOLEAN:
+        vals = np.asarray(arr.fill_null(False).to_numpy(zero_copy_only=False), dtype=np.int64)
+    elif spark == N.TYPE_DATE:
+        vals = np.asarray(arr.cast(pa.int32()).fill_null(0).to_numpy(zero_copy_only=False), dtype=np.int64)
+    else:
+        vals = np.asarray(arr.fill_null(0).to_numpy(zero_copy_only=False))
+    canon = engine.canonical_keys(spark, vals)[valid]
+    nulls = int(counts[~valid].sum())
+    return A.FrequenciesAndNumRows(engine.PairFrequencies(spark, canon, counts[valid], num_rows, nulls, 0, keys),
+                                   num_rows, keys)

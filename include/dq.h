@@ -250,6 +250,41 @@ int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* table, int64_t k, int64_t*
 int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* table, int64_t capacity, int64_t* keys, int64_t* counts);
 void dq_freq_free(dq_ctx* ctx, dq_freq_table* table);
 
+/* Build options: Histogram semantics, and pre-aggregated input (each row stands for weights[row] rows: the
+ * partial tables of a sharded computeFrequencies, or persisted (key, count) states). */
+typedef struct dq_freq_options {
+    uint32_t flags;          /* DQ_FREQ_INCLUDE_NULLS                                                  */
+    uint32_t weights_device; /* 1: `weights` is a device pointer on the ctx's GPU                       */
+    const int64_t* weights;  /* nrows counts (>= 0), NULL = every row counts once                       */
+    int32_t key_type;        /* declared Spark type of the single key column's canonical values, 0 = its own */
+    int32_t pad;
+} dq_freq_options;
+int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
+                      int nkeys, const dq_freq_options* options, dq_freq_table** table);
+
+/* Every group of a DQ_FREQ_KEYS_VALUES table as (canonical key, count) into device arrays (the NULL group of a
+ * DQ_FREQ_INCLUDE_NULLS table is summary.null_count, not exported). Returns the number written or < 0. */
+int64_t dq_freq_export_device(dq_ctx* ctx, const dq_freq_table* table, int64_t capacity, int64_t* keys_dev,
+                              int64_t* counts_dev);
+
+#define DQ_FREQ_PAIRS_DEVICE 0x1u /* keys / counts of dq_freq_from_pairs are device pointers */
+/* A DQ_FREQ_KEYS_VALUES table from (canonical key, count) pairs — duplicates are added — with the state's numRows
+ * and NULL-group count: the persisted frequency states of HdfsStateProvider (A/StateProvider.scala:137-160) and
+ * the groups exchanged between shards. */
+int dq_freq_from_pairs(dq_ctx* ctx, int32_t key_spark_type, const int64_t* keys, const int64_t* counts, int64_t n,
+                       uint32_t flags, int64_t num_rows, int64_t null_count, dq_freq_table** table);
+
+/* FrequenciesAndNumRows.sum (A/GroupingAnalyzers.scala:127-147): null-safe full outer join on the key, counts
+ * added, numRows added — on the GPU, for two DQ_FREQ_KEYS_VALUES tables of the same key type. */
+int dq_freq_merge(dq_ctx* ctx, const dq_freq_table* a, const dq_freq_table* b, dq_freq_table** out);
+
+/* MutualInformation.computeMetricFrom (A/MutualInformation.scala:35-97): joint = the (x, y) table, x / y = the
+ * single-column tables of the same rows (their counts are the marginals of the joint table's non-NULL keys).
+ * *mi = sum over joint groups with both keys non-NULL of (pxy/N) ln((pxy/N) / ((px/N)(py/N))), N = joint numRows;
+ * *present = 0 when no group joins (the reference's NULL sum -> empty state). */
+int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq_freq_table* x,
+                               const dq_freq_table* y, double* mi, int32_t* present);
+
 /* ApproxQuantile / ApproxQuantiles (A/ApproxQuantile.scala:28-103, A/ApproxQuantiles.scala:39-101): replaces the
  * per-row PercentileDigest.add of StatefulApproxQuantile.update (C/StatefulApproxQuantile.scala:65-72). Computes
  * EXACT order statistics of the column's non-NULL values cast to double, in java.lang.Double.compare order
