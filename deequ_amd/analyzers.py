@@ -849,22 +849,32 @@ class Histogram(Analyzer):
         if state is None:
             return HistogramMetric(self.column, Failure(emptyStateException(self)))
         try:
-            if isinstance(state.frequencies, dict):
-                items = sorted(state.frequencies.items(), key=lambda kv: -kv[1])[:self.maxDetailBins]
-                nbins = len(state.frequencies)
+            f = state.frequencies
+            if isinstance(f, engine.PairFrequencies):  # a persisted state read back: top-N on the device
+                f = f.to_device()
+            if isinstance(f, dict):
+                items = sorted(f.items(), key=lambda kv: -kv[1])[:self.maxDetailBins]
+                nbins = len(f)
                 details = {(_hist_key(k[0])): DistributionValue(c, c / state.numRows) for k, c in items}
             else:
-                nbins = state.frequencies.num_groups
+                nbins = f.num_groups
+                col = f.key_columns[0] if f.key_columns else _KeyTypeOnly(f.key_type)
                 details = {}
-                for key, c in state.frequencies.top(self.maxDetailBins):
-                    details[_hist_key(key[0], state.frequencies.key_columns[0])] = \
-                        DistributionValue(int(c), int(c) / state.numRows)
+                for key, c in f.top(self.maxDetailBins):
+                    details[_hist_key(key[0], col)] = DistributionValue(int(c), int(c) / state.numRows)
             return HistogramMetric(self.column, Success(Distribution(details, nbins)))
         except Exception as e:
             return HistogramMetric(self.column, Failure(wrap_if_necessary(e)))
 
     def toFailureMetric(self, exception):
         return HistogramMetric(self.column, Failure(wrap_if_necessary(exception)))
+
+
+class _KeyTypeOnly:
+    """The Spark type of a table's key column when the table has no source column (merged / loaded states)."""
+
+    def __init__(self, spark_type, decimal_scale=0):
+        self.spark_type, self.decimal_scale = spark_type, decimal_scale
 
 
 def _spark_string(v, column=None):

@@ -679,6 +679,45 @@ __device__ __forceinline__ int hash_class(int spark_type) {
     }
 }
 
+// XXH64 (hashInt / hashLong, seed 42) of a lane value up to the last multiply of the avalanche, then the
+// HLL++ register index and rank (C/StatefulHyperloglogPlus.scala:96-100) from the final hash's high word
+// alone: with g = h * P3 and x = g ^ (g >> 32), idx = x >>> 55 = g_hi >>> 23 and, whenever g_hi << 9 != 0
+// (all but 2^-23 of the values), rank = nlz((x << 9) | 1 << 8) + 1 = nlz32(g_hi << 9) + 1 — so the low half of
+// the last 64-bit multiply and the final xor are only computed on that rare path. Bit-identical to
+// hll_index(xxh_*(v)) / hll_rank(xxh_*(v)).
+template <int HC>
+__device__ __forceinline__ uint32_t hll_idx_rank(uint64_t v) {
+    uint64_t h;
+    if (HC <= 1) {
+        const uint32_t iv = HC == 0 ? (uint32_t)(int32_t)(int64_t)v : float_to_int_bits((float)as_f64(v));
+        h = SPARK_HLL_SEED + P64_5 + 4ULL;
+        h ^= (uint64_t)iv * P64_1;
+        h = rotl64(h, 23) * P64_2 + P64_3;
+    } else {
+        const uint64_t lv = HC == 2 ? double_to_long_bits(as_f64(v)) : v;
+        h = SPARK_HLL_SEED + P64_5 + 8ULL;
+        h ^= rotl64(lv * P64_2, 31) * P64_1;
+        h = rotl64(h, 27) * P64_1 + P64_4;
+    }
+    h ^= h >> 33;
+    h *= P64_2;
+    h ^= h >> 29;
+    const uint32_t hl = (uint32_t)h, hh = (uint32_t)(h >> 32);
+    constexpr uint32_t p3l = (uint32_t)P64_3, p3h = (uint32_t)(P64_3 >> 32);
+    const uint32_t ghi = __umulhi(hl, p3l) + hl * p3h + hh * p3l;
+    const uint32_t idx = ghi >> 23;
+    const uint32_t t = ghi << 9;
+    uint32_t rank;
+    if (__builtin_expect(t != 0u, 1)) {
+        rank = (uint32_t)__clz((int)t) + 1u;
+    } else {
+        const uint32_t xlo = (hl * p3l) ^ ghi;
+        const uint32_t whi = xlo >> 23;
+        rank = whi ? (uint32_t)__clz((int)whi) + 1u : 32u + (uint32_t)__clz((int)((xlo << 9) | 256u)) + 1u;
+    }
+    return idx | (rank << 16);
+}
+
 // All 8 lane values are hashed unconditionally (independent multiply chains the scheduler can
 // interleave; no divergence), then the valid ones are max-merged into the LDS registers with
 // no-return ds_max atomics (fire-and-forget: no LDS latency on the critical path).
@@ -689,15 +728,7 @@ __device__ __forceinline__ void hll_update8(uint32_t* regs, const uint64_t (&v)[
     for (int g = 0; g < 8; g += 4) {
         uint32_t packed[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint64_t vk = v[g + k];
-            uint64_t x;
-            if (HC == 0) x = xxh_int((uint32_t)(int32_t)(int64_t)vk, SPARK_HLL_SEED);
-            else if (HC == 1) x = xxh_int(float_to_int_bits((float)as_f64(vk)), SPARK_HLL_SEED);
-            else if (HC == 2) x = xxh_long(double_to_long_bits(as_f64(vk)), SPARK_HLL_SEED);
-            else x = xxh_long(vk, SPARK_HLL_SEED);
-            packed[k] = hll_index(x) | (hll_rank(x) << 16);
-        }
+        for (int k = 0; k < 4; ++k) packed[k] = hll_idx_rank<HC>(v[g + k]);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if ((m >> (g + k)) & 1u) atomicMax(&regs[packed[k] & 0xffffu], packed[k] >> 16);
