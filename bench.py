@@ -7,7 +7,15 @@ semigroup fold of those states on the host. Rows are sharded contiguously across
 scaling over the 1e9-row table). Inputs are generated in HBM by the counter-based splitmix64
 generators before timing.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R]
+The same JSON line carries `secondary` measurements of the other BASELINE workloads, each timed the
+same way (its own steps, HIP events on the scan stream, its own roofline):
+  suite10  the north-star 10-analyzer suite over the same 8 columns (C2 ops + Compliance(c > 0) +
+           ApproxCountDistinct + Correlation(c_2k, c_2k+1): 73 ops), every rank count;
+  c3       ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 1e9 rows (N = 1);
+  c4       the grouping analyzers' frequency table (computeFrequencies + the fused table aggregation) on
+           1e9 int64 keys with exactly 1e8 distinct, closed forms checked (N = 1).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--no-secondary]
 """
 import argparse
 import ctypes
@@ -34,6 +42,78 @@ def c2_analyzers(D, names):
     return out
 
 
+def suite10_analyzers(D, names):
+    """The north star's 10 analyzer kinds over the C2 columns."""
+    out = c2_analyzers(D, names)
+    out += [D.Compliance("pos_%s" % c, "%s > 0" % c) for c in names]
+    out += [D.ApproxCountDistinct(c) for c in names]
+    out += [D.Correlation(names[2 * i], names[2 * i + 1]) for i in range(len(names) // 2)]
+    return out
+
+
+class ScanWorkload:
+    """One fused dq_scan step over `table` for `analyzers` (+ the RCCL all-gather and rank-ordered fold when
+    world > 1), timed with HIP events on `stream`."""
+
+    def __init__(self, torch, N, D, ctx, table, analyzers, stream, dev, world, backend):
+        import torch.distributed as dist
+        self.torch, self.N, self.ctx, self.stream, self.world, self.dist = torch, N, ctx, stream, world, dist
+        self.backend = backend
+        self.batch = D.ScanBatch(table)
+        self.offsets = [a.addOps(self.batch) for a in analyzers]
+        self.nops = len(self.batch.ops)
+        self.out = torch.empty(self.nops * N.STATE_SIZE, dtype=torch.uint8, device=dev)
+        coll_dev = dev if backend == "nccl" else torch.device("cpu")
+        self.gathered = torch.empty(world * self.nops * N.STATE_SIZE, dtype=torch.uint8, device=coll_dev)
+        self.host = torch.empty(world * self.nops * N.STATE_SIZE, dtype=torch.uint8, pin_memory=True)
+        self.host_np = self.host.numpy()
+        self.cols = self.batch.native_columns()
+        self.preds = [p.to_native() for p in self.batch.preds]
+        self.nrows = table.nrows
+
+    def step(self, ev=None):
+        if ev is not None:
+            ev[0].record(self.stream)
+        self.ctx.scan(self.cols, self.nrows, self.batch.ops, self.preds, out_device_ptr=self.out.data_ptr())
+        if ev is not None:
+            ev[1].record(self.stream)
+        if self.world > 1:
+            src_t = self.out if self.backend == "nccl" else self.out.cpu()
+            self.dist.all_gather_into_tensor(self.gathered, src_t)  # RCCL over xGMI
+            src = self.gathered
+        else:
+            src = self.out
+        self.host[:src.numel()].copy_(src, non_blocking=True)
+        self.stream.synchronize()
+        # rank-ordered fold with the reference semigroup merges (State.sum), one C-ABI call
+        return self.N.fold_states(self.host_np, self.world, self.nops)
+
+
+def timed(torch, dist, world, steps, warmup, stream, step):
+    """W untimed steps, then K steps bracketed by barrier + synchronize; max wall time over ranks and the
+    mean HIP-event time of the kernels each step brackets."""
+    for _ in range(warmup):
+        step(None)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    res = None
+    for i in range(steps):
+        res = step(ev[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return elapsed, kernel_ms, res
+
+
 def build_shard(torch, N, ctx, row0, nrows, dev):
     from deequ_amd.table import Table, Column
     cols = []
@@ -49,6 +129,80 @@ def build_shard(torch, N, ctx, row0, nrows, dev):
         cols.append(col)
     ctx.synchronize()
     return Table(cols)
+
+
+def bench_c3(torch, N, D, ctx, stream, dev, total, steps):
+    """BASELINE config C3 on one GPU: k = splitmix64 mod 2^30 (HLL), x ~ N(0, 1), y = 0.6 x + 0.8 e, 1 % nulls."""
+    from deequ_amd.table import Table, Column
+    cols = []
+    for name, kind, seed, vseed, st in (("k", N.SYNTH_KEY30, 0xC3000001, 0xC3000101, N.TYPE_LONG),
+                                        ("x", N.SYNTH_GAUSS01, 0xC3000002, 0xC3000102, N.TYPE_DOUBLE),
+                                        ("y", N.SYNTH_GAUSS_CORR, 0xC3000002, 0xC3000103, N.TYPE_DOUBLE)):
+        v = torch.empty(total, dtype=torch.int64 if st == N.TYPE_LONG else torch.float64, device=dev)
+        m = torch.zeros((total + 63) // 64 * 8, dtype=torch.uint8, device=dev)
+        ctx.synth_column(kind, seed, 0, total, v.data_ptr())
+        ctx.synth_validity(vseed, 0, total, 10, m.data_ptr())
+        c = Column(name, st, None, None, length=total)
+        c.device = {"values": v, "validity": m}
+        cols.append(c)
+    ctx.synchronize()
+    t = Table(cols)
+    w = ScanWorkload(torch, N, D, ctx, t, [D.ApproxCountDistinct("k"), D.Correlation("x", "y"), D.Completeness("k")],
+                     stream, dev, 1, "nccl")
+    el, kms, _ = timed(torch, None, 1, steps, 1, stream, w.step)
+    bpr = 3 * (8 + 1 / 8)
+    ach = bpr * total / (kms * 1e-3) / 1e9
+    return {"workload": "C3: ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 3 cols x 1e9 rows, 1% nulls",
+            "value": total / (el / steps), "unit": "rows/s", "ms_per_step": el / steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "kernel": "dq_scan avg %.3f ms (HIP events), %.3f B/row" % (kms, bpr)}}
+
+
+def bench_c4(torch, N, D, ctx, stream, dev, total, steps):
+    """BASELINE config C4 on one GPU: the frequency table of 1e9 int64 keys with exactly 1e8 distinct
+    (5e7 x 19 + 5e7 x 1) and the grouping analyzers' table aggregation, closed forms checked."""
+    import math
+    from deequ_amd import engine
+    from deequ_amd.table import Table, Column
+    distinct = total // 10
+    keys = torch.empty(total, dtype=torch.int64, device=dev)
+    ctx.synth_freq_keys(total, distinct, 0, total, keys.data_ptr())
+    ctx.synchronize()
+    c = Column("k", N.TYPE_LONG, None, None, length=total)
+    c.device = {"values": keys}
+    t = Table([c])
+    out = {}
+
+    def step(ev):
+        if ev is not None:
+            ev[0].record(stream)
+        ft = engine.frequencies(t, ["k"])
+        s = ft.summary(None)
+        if ev is not None:
+            ev[1].record(stream)
+        out["s"] = s
+        del ft
+        return s
+
+    el, kms, _ = timed(torch, None, 1, steps, 1, stream, step)
+    s = out["s"]
+    half = distinct // 2
+    big = (total - half) / half
+    ent = math.fsum([-half * (big / total) * math.log(big / total), -half * (1 / total) * math.log(1 / total)])
+    ok = (s["num_rows"], s["num_groups"], s["num_unique"]) == (total, distinct, half) and \
+        abs(s["entropy"] - ent) <= 1e-12 * ent
+    assert ok, (s, ent)
+    bpr = 8.0
+    table_bytes = 2 * 16 * distinct  # write + read of the 16-B slots of each group (SURVEY.md §8d)
+    ach = (bpr * total + table_bytes) / (el / steps) / 1e9
+    return {"workload": "C4: computeFrequencies + Uniqueness/Distinctness/UniqueValueRatio/CountDistinct/Entropy "
+                        "aggregation, 1e9 int64 keys, 1e8 distinct; closed forms exact",
+            "value": total / (el / steps), "unit": "rows/s", "ms_per_step": el / steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "kernel": "end-to-end build + summary, wall clock per step (partitioned LDS build, "
+                                   "DESIGN.md §3); algorithmic %.1f GB" % ((bpr * total + table_bytes) / 1e9)}}
 
 
 def cpu_baseline(seconds, sample_rows, threads=None):
@@ -127,6 +281,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-sample-rows", type=int, default=8_000_000)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="only the headline C2 line")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
     ap.add_argument("--device-override", type=int, default=None, help="run every rank on this GPU (rehearsal)")
     args = ap.parse_args()
@@ -164,58 +319,14 @@ def main():
     nrows = max(0, min(total, row0 + per) - row0)
     table = build_shard(torch, N, ctx, row0, nrows, dev)
     names = list(table.columns)
-    analyzers = c2_analyzers(D, names)
-    batch = D.ScanBatch(table)
-    offsets = [a.addOps(batch) for a in analyzers]
-    nops = len(batch.ops)
-    out = torch.empty(nops * N.STATE_SIZE, dtype=torch.uint8, device=dev)
-    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    gathered = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, device=coll_dev)
-    host = torch.empty(world * nops * N.STATE_SIZE, dtype=torch.uint8, pin_memory=True)
-    host_np = host.numpy()
-    cols = batch.native_columns()
-    preds = [p.to_native() for p in batch.preds]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    bytes_per_row = sum(8 + 1.0 / 8 for _ in names)  # values + validity bit, per column
 
-    def step(i=None):
-        if i is not None:
-            ev[i][0].record(stream)
-        ctx.scan(cols, nrows, batch.ops, preds, out_device_ptr=out.data_ptr())
-        if i is not None:
-            ev[i][1].record(stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out if args.dist_backend == "nccl" else out.cpu())  # RCCL over xGMI
-            src = gathered
-        else:
-            src = out
-        host[:src.numel()].copy_(src, non_blocking=True)
-        stream.synchronize()
-        # rank-ordered fold with the reference semigroup merges (State.sum), one C-ABI call
-        return N.fold_states(host_np, world, nops)
-
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        states = step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    scan_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-
+    c2 = ScanWorkload(torch, N, D, ctx, table, c2_analyzers(D, names), stream, dev, world, args.dist_backend)
+    elapsed, scan_ms, states = timed(torch, dist, world, args.steps, args.warmup, stream, c2.step)
     # sanity: the folded Size equals the table size
-    size_state = state_from_native(states[offsets[0][0]])
+    size_state = state_from_native(states[c2.offsets[0][0]])
     assert size_state.numMatches == total, (size_state, total)
 
-    bytes_per_row = sum(8 + 1.0 / 8 for _ in names)  # values + validity bit, per column
     alg_bytes = bytes_per_row * nrows
     achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
     ms_per_step = elapsed / args.steps * 1e3
@@ -236,7 +347,7 @@ def main():
         "data": "synthetic (counter-based splitmix64 columns generated in HBM, SURVEY.md §8d)",
         "config": {"workload": "C2 fused scan suite: Size + {Completeness, Mean, Sum, Minimum, Maximum, "
                                "StandardDeviation} x 8 cols (4 fp64 + 4 int64, 1% nulls) = 49 ops",
-                   "rows": total, "rows_per_gpu": nrows, "columns": len(names), "ops": nops,
+                   "rows": total, "rows_per_gpu": nrows, "columns": len(names), "ops": c2.nops,
                    "parallelism": "rows sharded dp%d + RCCL all-gather of states" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic[0] if traffic else None,
@@ -246,6 +357,29 @@ def main():
                                "on the scan stream, avg %.3f ms over %d steps; algorithmic bytes %.1f B/row x %d rows"
                                % (scan_ms, args.steps, bytes_per_row, nrows)},
     }
+    del c2
+    if not args.no_secondary:
+        sec = {}
+        s10 = ScanWorkload(torch, N, D, ctx, table, suite10_analyzers(D, names), stream, dev, world, args.dist_backend)
+        el, kms, st = timed(torch, dist, world, max(3, args.steps // 4), 1, stream, s10.step)
+        ach = alg_bytes / (kms * 1e-3) / 1e9
+        sec["suite10"] = {
+            "workload": "north-star 10-analyzer suite: C2 ops + Compliance(c > 0) + ApproxCountDistinct x 8 cols + "
+                        "Correlation(c_2k, c_2k+1) x 4 = %d ops, one fused pass" % s10.nops,
+            "value": total / (el / max(3, args.steps // 4)), "unit": "rows/s", "ms_per_step": el / max(3, args.steps // 4) * 1e3,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "kernel": "dq_scan avg %.3f ms (HIP events); VALU-bound: XXH64 + moments per value "
+                                   "(DESIGN.md §3)" % kms}}
+        del s10
+        if world == 1:
+            del table
+            torch.cuda.empty_cache()
+            sec["c3"] = bench_c3(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4))
+            torch.cuda.empty_cache()
+            sec["c4"] = bench_c4(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4))
+            torch.cuda.empty_cache()
+        result["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_sample_rows)
     if rank == 0:

@@ -26,21 +26,6 @@
 
 using namespace dq;
 
-struct dq_ctx {
-    int device = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    std::string err;
-    // Device arena, re-used by every call (grown outside of any timed/captured region).
-    uint8_t* arena = nullptr;
-    size_t arena_cap = 0;
-    // Pinned host staging for plan uploads and state downloads.
-    uint8_t* pinned = nullptr;
-    size_t pinned_cap = 0;
-    int cus = 256;
-    std::map<int, int> occupancy;  // launch shape -> workgroups per CU
-    int64_t scan_launches = 0;
-};
 
 namespace {
 
@@ -203,6 +188,7 @@ dq_ctx* dq_open(int device, int* status) {
 
 void dq_close(dq_ctx* ctx) {
     if (!ctx) return;
+    if (!ctx->subs.empty()) close_subs(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->arena) (void)hipFree(ctx->arena);
@@ -221,6 +207,10 @@ int dq_set_stream(dq_ctx* ctx, void* stream) {
 
 int dq_synchronize(dq_ctx* ctx) {
     if (!ctx) return DQ_ERR_INVALID_ARGUMENT;
+    for (dq_ctx* sub : ctx->subs) {
+        const int rc = dq_synchronize(sub);
+        if (rc) return fail(ctx, rc, "device %d: %s", sub->device, sub->err.c_str());
+    }
     DQ_HIP(ctx, hipSetDevice(ctx->device));
     DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return DQ_OK;
@@ -235,6 +225,30 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     if (nops < 0 || ncols < 0 || npreds < 0 || nrows < 0 || (nops > 0 && (!ops || !out)))
         return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "invalid arguments");
     if (nops == 0) return DQ_OK;
+    if (!ctx->subs.empty()) {
+        // multi-device context: host columns are row-sharded over the devices (multi.cpp)
+        if (flags & DQ_SCAN_OUT_DEVICE)
+            return fail(ctx, DQ_ERR_UNSUPPORTED, "a multi-device context returns host states (no DQ_SCAN_OUT_DEVICE)");
+        for (int c = 0; c < ncols; ++c) {
+            if (columns[c].flags & DQ_COL_DEVICE)
+                return fail(ctx, DQ_ERR_UNSUPPORTED, "device columns of a multi-device context go through dq_scan_sharded");
+            if (columns[c].length != nrows)
+                return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "column %d has %lld rows, batch has %lld", c,
+                            (long long)columns[c].length, (long long)nrows);
+        }
+        const int n = (int)ctx->subs.size();
+        std::vector<std::vector<dq_column>> cols(n, std::vector<dq_column>(std::max(ncols, 1)));
+        std::vector<std::vector<std::vector<int32_t>>> scratch(n);
+        std::vector<const dq_column*> ptrs(n);
+        std::vector<int64_t> rows(n);
+        for (int i = 0; i < n; ++i) {
+            int64_t r0 = 0;
+            shard_bounds(nrows, n, i, &r0, &rows[i]);
+            shard_columns(columns, ncols, r0, rows[i], cols[i].data(), scratch[i]);
+            ptrs[i] = cols[i].data();
+        }
+        return multi_scan(ctx, ptrs.data(), rows.data(), ncols, ops, nops, preds, npreds, out);
+    }
     DQ_HIP(ctx, hipSetDevice(ctx->device));
 
     // ---- validation ---------------------------------------------------------------------------

@@ -192,6 +192,57 @@ inline int rows_per_load_of(int e) {
     return s == 8 ? 2 : (s == 4 ? 4 : 8);
 }
 
+}  // namespace dq
+
+#ifdef __cplusplus
+#include <map>
+#include <string>
+#include <vector>
+// The context behind the C-ABI. A single-device context owns one stream, a device arena and pinned staging;
+// a multi-device context (dq_open_devices) owns one single-device sub-context per GPU and, when the devices
+// are distinct, one RCCL communicator per GPU for the frequency-table exchange.
+struct dq_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // Device arena, re-used by every call (grown outside of any timed/captured region).
+    uint8_t* arena = nullptr;
+    size_t arena_cap = 0;
+    // Pinned host staging for plan uploads and state downloads.
+    uint8_t* pinned = nullptr;
+    size_t pinned_cap = 0;
+    int cus = 256;
+    std::map<int, int> occupancy;  // launch shape -> workgroups per CU
+    int64_t scan_launches = 0;
+    // multi-device
+    std::vector<dq_ctx*> subs;   // one per device (empty: single-device context)
+    std::vector<int> devices;
+    void* comms = nullptr;       // ncclComm_t[ndev] when the devices are distinct, else nullptr (copy transport)
+};
+#endif
+
+namespace dq {
+
+// Multi-device orchestration (multi.cpp).
+int multi_scan(dq_ctx* ctx, const dq_column* const* shard_columns, const int64_t* shard_rows, int ncols,
+               const dq_op* ops, int nops, const dq_predicate* preds, int npreds, dq_state* out);
+// Row bounds of shard i of n rows over ndev devices (contiguous, 2048-row aligned).
+void shard_bounds(int64_t nrows, int ndev, int i, int64_t* row0, int64_t* count);
+// Host columns -> per-shard column views (string offsets rebased into `scratch`).
+void shard_columns(const dq_column* columns, int ncols, int64_t row0, int64_t count, dq_column* out,
+                   std::vector<std::vector<int32_t>>& scratch);
+void close_subs(dq_ctx* ctx);
+// Run fn(i, sub) on every device of a multi-device context concurrently; returns the first error.
+int for_each_device(dq_ctx* ctx, int (*fn)(int, dq_ctx*, void*), void* arg);
+// All-to-all of int64 records between the devices of a multi-device context: send[i] holds, for every
+// destination j, counts[i * ndev + j] records starting at send_off[i * ndev + j]; recv[j] receives them
+// ordered by source device at recv_off[j * ndev + i]. RCCL (ncclSend / ncclRecv in one group) when the
+// devices are distinct, device-to-device copies when a device repeats.
+int exchange_i64(dq_ctx* ctx, const std::vector<int64_t*>& send, const std::vector<int64_t*>& recv,
+                 const std::vector<int64_t>& counts, const std::vector<int64_t>& send_off,
+                 const std::vector<int64_t>& recv_off);
+
 // Kernel launchers (defined in the .hip files).
 // One launch per slot shape (kind, P, column count, float/integral storage); each launch walks its
 // slots with tiles interleaved over `grid` workgroups and writes partials[slot * gstride + block].

@@ -957,6 +957,11 @@ struct dq_freq_table {
     uint64_t cap = 0;
     int bits = 0;           // 2^bits bucket regions of kRegion slots
     int fast = 1;
+    // multi-device context: the table is the union of per-device parts with disjoint key sets (owner device =
+    // hash of the key); part j lives on part_ctx[j]'s GPU
+    std::vector<dq_freq_table*> parts;
+    std::vector<dq_ctx*> part_ctx;
+    int64_t total_rows = 0;
     int32_t key_type = 0;   // Spark type of the (single) key column, or of the canonical keys of a pair-built table
     int64_t num_rows_override = -1;  // tables built from (key, count) pairs carry the caller's numRows
     int64_t cached_n = -1;  // dq_freq_summarize memo (the table is immutable once built)
@@ -1308,6 +1313,212 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
     return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
 }
 
+
+// ---- multi-device grouping: owner-device bucketing of (canonical key, count) pairs -------------------------
+__device__ __forceinline__ int pair_owner(uint64_t canon, int nparts) {
+    return (int)((mix64(canon) >> 32) % (uint64_t)nparts);
+}
+
+__global__ void __launch_bounds__(kFreqBlock)
+pair_owner_count_kernel(const long long* __restrict__ keys, int64_t n, int nparts, unsigned long long* __restrict__ counts) {
+    __shared__ unsigned int lds[64];
+    for (int i = threadIdx.x; i < 64; i += kFreqBlock) lds[i] = 0;
+    __syncthreads();
+    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < n; r += (int64_t)gridDim.x * kFreqBlock)
+        atomicAdd(&lds[pair_owner((uint64_t)keys[r], nparts)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nparts; i += kFreqBlock)
+        if (lds[i]) atomicAdd(&counts[i], (unsigned long long)lds[i]);
+}
+
+__global__ void __launch_bounds__(kFreqBlock)
+pair_owner_scatter_kernel(const long long* __restrict__ keys, const long long* __restrict__ cnts, int64_t n, int nparts,
+                          unsigned long long* __restrict__ cursors, long long* __restrict__ out_keys,
+                          long long* __restrict__ out_cnts) {
+    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < n; r += (int64_t)gridDim.x * kFreqBlock) {
+        const int p = pair_owner((uint64_t)keys[r], nparts);
+        const unsigned long long at = atomicAdd(&cursors[p], 1ull);
+        out_keys[at] = keys[r];
+        out_cnts[at] = cnts[r];
+    }
+}
+
+struct MultiFreqJob {
+    std::vector<const dq_column*> cols;
+    std::vector<int64_t> rows;
+    int ncols;
+    const int32_t* key_columns;
+    const dq_freq_options* opt;
+    int ndev;
+    // per device
+    std::vector<dq_freq_table*> local;
+    std::vector<int64_t> local_rows, local_nulls;
+    std::vector<int64_t*> send_keys, send_cnts, recv_keys, recv_cnts;
+    std::vector<int64_t> counts;  // ndev x ndev
+};
+
+int multi_local_build(int i, dq_ctx* sub, void* arg) {
+    MultiFreqJob* j = static_cast<MultiFreqJob*>(arg);
+    dq_freq_table* t = nullptr;
+    int rc = dq_frequencies_ex(sub, j->cols[i], j->ncols, j->rows[i], j->key_columns, 1, j->opt, &t);
+    if (rc) return rc;
+    j->local[i] = t;
+    dq_freq_summary su;
+    rc = dq_freq_summarize(sub, t, 0, &su);
+    if (rc) return rc;
+    j->local_rows[i] = su.num_rows;
+    j->local_nulls[i] = su.null_count;
+    const int64_t g = su.num_groups - (su.null_count ? 1 : 0);
+    hipStream_t s = dq::ctx_stream(sub);
+    int64_t *ek = nullptr, *ec = nullptr;
+    if (hipMalloc(&ek, (size_t)std::max<int64_t>(g, 1) * 8) != hipSuccess ||
+        hipMalloc(&ec, (size_t)std::max<int64_t>(g, 1) * 8) != hipSuccess ||
+        hipMalloc(&j->send_keys[i], (size_t)std::max<int64_t>(g, 1) * 8) != hipSuccess ||
+        hipMalloc(&j->send_cnts[i], (size_t)std::max<int64_t>(g, 1) * 8) != hipSuccess)
+        return dq::ctx_fail(sub, DQ_ERR_OUT_OF_MEMORY, "exchange buffers");
+    const int64_t got = dq_freq_export_device(sub, t, g, ek, ec);
+    if (got < 0) return (int)got;
+    unsigned long long* dc = nullptr;
+    FQ_HIP(sub, hipMalloc(&dc, sizeof(unsigned long long) * 128));
+    FQ_HIP(sub, hipMemsetAsync(dc, 0, sizeof(unsigned long long) * 128, s));
+    const int grid = scan_grid((uint64_t)std::max<int64_t>(got, 1));
+    if (got) hipLaunchKernelGGL(pair_owner_count_kernel, dim3(grid), dim3(kFreqBlock), 0, s, (const long long*)ek, got,
+                                j->ndev, dc);
+    std::vector<unsigned long long> h(64);
+    FQ_HIP(sub, hipMemcpyAsync(h.data(), dc, 64 * 8, hipMemcpyDeviceToHost, s));
+    FQ_HIP(sub, hipStreamSynchronize(s));
+    std::vector<unsigned long long> cur(64, 0);
+    unsigned long long off = 0;
+    for (int p = 0; p < j->ndev; ++p) {
+        cur[p] = off;
+        j->counts[(size_t)i * j->ndev + p] = (int64_t)h[p];
+        off += h[p];
+    }
+    FQ_HIP(sub, hipMemcpyAsync(dc + 64, cur.data(), 64 * 8, hipMemcpyHostToDevice, s));
+    if (got) hipLaunchKernelGGL(pair_owner_scatter_kernel, dim3(grid), dim3(kFreqBlock), 0, s, (const long long*)ek,
+                                (const long long*)ec, got, j->ndev, dc + 64, (long long*)j->send_keys[i],
+                                (long long*)j->send_cnts[i]);
+    FQ_HIP(sub, hipGetLastError());
+    FQ_HIP(sub, hipStreamSynchronize(s));
+    (void)hipFree(ek);
+    (void)hipFree(ec);
+    (void)hipFree(dc);
+    dq_freq_free(sub, t);
+    j->local[i] = nullptr;
+    return DQ_OK;
+}
+
+struct OwnerBuildJob {
+    MultiFreqJob* j;
+    int32_t key_type;
+    int64_t nulls;
+    std::vector<dq_freq_table*> parts;
+};
+
+int multi_owner_build(int i, dq_ctx* sub, void* arg) {
+    OwnerBuildJob* o = static_cast<OwnerBuildJob*>(arg);
+    MultiFreqJob* j = o->j;
+    int64_t total = 0;
+    for (int src = 0; src < j->ndev; ++src) total += j->counts[(size_t)src * j->ndev + i];
+    return dq_freq_from_pairs(sub, o->key_type, j->recv_keys[i], j->recv_cnts[i], total, DQ_FREQ_PAIRS_DEVICE, total,
+                              i == 0 ? o->nulls : 0, &o->parts[i]);
+}
+
+int multi_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
+                      int nkeys, const dq_freq_options* opt, dq_freq_table** out) {
+    if (nkeys != 1 || key_columns[0] < 0 || key_columns[0] >= ncols || elem_of(columns[key_columns[0]].spark_type) == ET_NONE ||
+        opt->weights)
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED,
+                            "multi-device grouping: one fixed-width key column (strings / several keys: one device per context)");
+    for (int c = 0; c < ncols; ++c)
+        if (columns[c].flags & DQ_COL_DEVICE)
+            return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "multi-device grouping takes host columns");
+    const int n = (int)ctx->subs.size();
+    MultiFreqJob j;
+    j.ncols = ncols;
+    j.key_columns = key_columns;
+    j.opt = opt;
+    j.ndev = n;
+    j.local.assign(n, nullptr);
+    j.local_rows.assign(n, 0);
+    j.local_nulls.assign(n, 0);
+    j.send_keys.assign(n, nullptr);
+    j.send_cnts.assign(n, nullptr);
+    j.recv_keys.assign(n, nullptr);
+    j.recv_cnts.assign(n, nullptr);
+    j.counts.assign((size_t)n * n, 0);
+    std::vector<std::vector<dq_column>> cols(n, std::vector<dq_column>(std::max(ncols, 1)));
+    std::vector<std::vector<std::vector<int32_t>>> scratch(n);
+    j.rows.resize(n);
+    j.cols.resize(n);
+    for (int i = 0; i < n; ++i) {
+        int64_t r0 = 0;
+        dq::shard_bounds(nrows, n, i, &r0, &j.rows[i]);
+        dq::shard_columns(columns, ncols, r0, j.rows[i], cols[i].data(), scratch[i]);
+        j.cols[i] = cols[i].data();
+    }
+    auto release = [&]() {
+        for (int i = 0; i < n; ++i) {
+            (void)hipSetDevice(ctx->subs[i]->device);
+            for (int64_t* p : {j.send_keys[i], j.send_cnts[i], j.recv_keys[i], j.recv_cnts[i]})
+                if (p) (void)hipFree(p);
+            if (j.local[i]) dq_freq_free(ctx->subs[i], j.local[i]);
+        }
+    };
+    int rc = dq::for_each_device(ctx, multi_local_build, &j);  // local pre-aggregation + owner bucketing
+    if (rc) { release(); return rc; }
+    std::vector<int64_t> send_off((size_t)n * n), recv_off((size_t)n * n);
+    for (int i = 0; i < n; ++i) {
+        int64_t so = 0, ro = 0;
+        for (int p = 0; p < n; ++p) {
+            send_off[(size_t)i * n + p] = so;
+            so += j.counts[(size_t)i * n + p];
+            recv_off[(size_t)i * n + p] = ro;  // receiver i, records from source p
+            ro += j.counts[(size_t)p * n + i];
+        }
+        (void)hipSetDevice(ctx->subs[i]->device);
+        if (hipMalloc(&j.recv_keys[i], (size_t)std::max<int64_t>(ro, 1) * 8) != hipSuccess ||
+            hipMalloc(&j.recv_cnts[i], (size_t)std::max<int64_t>(ro, 1) * 8) != hipSuccess) {
+            release();
+            return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "exchange receive buffers");
+        }
+    }
+    rc = dq::exchange_i64(ctx, j.send_keys, j.recv_keys, j.counts, send_off, recv_off);
+    if (!rc) rc = dq::exchange_i64(ctx, j.send_cnts, j.recv_cnts, j.counts, send_off, recv_off);
+    if (rc) { release(); return rc; }
+    OwnerBuildJob o;
+    o.j = &j;
+    o.key_type = columns[key_columns[0]].spark_type;
+    o.nulls = 0;
+    int64_t total_rows = 0;
+    for (int i = 0; i < n; ++i) {
+        o.nulls += j.local_nulls[i];
+        total_rows += j.local_rows[i];
+    }
+    o.parts.assign(n, nullptr);
+    rc = dq::for_each_device(ctx, multi_owner_build, &o);
+    release();
+    if (rc) {
+        for (int i = 0; i < n; ++i)
+            if (o.parts[i]) dq_freq_free(ctx->subs[i], o.parts[i]);
+        return rc;
+    }
+    dq_freq_table* t = new dq_freq_table();
+    t->device = ctx->device;
+    memset(&t->ks, 0, sizeof(t->ks));
+    t->fast = 1;
+    t->key_type = o.key_type;
+    t->parts = o.parts;
+    t->part_ctx = ctx->subs;
+    t->total_rows = total_rows;
+    for (int i = 0; i < n; ++i) {  // the pair arrays die with this call: parts keep only their slots
+        o.parts[i]->ks.weights = nullptr;
+        o.parts[i]->ks.cols[0].values = nullptr;
+    }
+    *out = t;
+    return DQ_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1324,6 +1535,7 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
                       int nkeys, const dq_freq_options* opt, dq_freq_table** out) {
     if (!ctx || !out || !opt || nkeys <= 0 || nkeys > kMaxKeys || nrows < 0)
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_frequencies: invalid arguments");
+    if (!ctx->subs.empty()) return multi_frequencies(ctx, columns, ncols, nrows, key_columns, nkeys, opt, out);
     const uint32_t flags = opt->flags;
     *out = nullptr;
     const int dev = dq::ctx_device(ctx);
@@ -1419,6 +1631,30 @@ int dq_freq_key_kind(const dq_freq_table* t) { return !t ? -1 : (t->fast ? DQ_FR
 
 int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows, dq_freq_summary* out) {
     if (!ctx || !t || !out) return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_summarize: invalid arguments");
+    if (!t->parts.empty()) {
+        // union of disjoint per-device tables: counts add, entropy terms (global N) folded in device order
+        const int64_t n = entropy_rows > 0 ? entropy_rows : t->total_rows;
+        dq_freq_summary acc;
+        memset(&acc, 0, sizeof(acc));
+        double comp = 0.0;
+        for (size_t i = 0; i < t->parts.size(); ++i) {
+            dq_freq_summary p;
+            const int rc = dq_freq_summarize(t->part_ctx[i], t->parts[i], n, &p);
+            if (rc) return dq::ctx_fail(ctx, rc, t->part_ctx[i]->err.c_str());
+            acc.num_groups += p.num_groups;
+            acc.num_unique += p.num_unique;
+            acc.max_count = std::max(acc.max_count, p.max_count);
+            acc.null_count += p.null_count;
+            const double yk = p.entropy - comp;
+            const double tt = acc.entropy + yk;
+            comp = (tt - acc.entropy) - yk;
+            acc.entropy = tt;
+        }
+        acc.num_rows = t->total_rows;
+        acc.entropy_rows = n;
+        *out = acc;
+        return DQ_OK;
+    }
     FQ_HIP(ctx, hipSetDevice(t->device));
     hipStream_t s = dq::ctx_stream(ctx);
     const int64_t table_rows = t->num_rows_override >= 0 ? t->num_rows_override : (int64_t)t->host_ctr.num_rows;
@@ -1512,6 +1748,15 @@ static void decode_keys(const dq_freq_table* t, std::vector<unsigned long long>&
 
 int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* t, int64_t capacity, int64_t* keys, int64_t* counts) {
     if (!ctx || !t || capacity < 0 || (capacity > 0 && (!keys || !counts))) return DQ_ERR_INVALID_ARGUMENT;
+    if (!t->parts.empty()) {
+        int64_t n = 0;
+        for (size_t i = 0; i < t->parts.size() && n < capacity; ++i) {
+            const int64_t got = dq_freq_export(t->part_ctx[i], t->parts[i], capacity - n, keys + n, counts + n);
+            if (got < 0) return dq::ctx_fail(ctx, (int)got, t->part_ctx[i]->err.c_str());
+            n += got;
+        }
+        return n;
+    }
     if (hipSetDevice(t->device) != hipSuccess) return DQ_ERR_DEVICE;
     std::vector<unsigned long long> k, c;
     if (compact(ctx, t, 2, 0, (uint64_t)capacity, k, c) < 0) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "export failed");
@@ -1532,6 +1777,23 @@ int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* t, int64_t capacity, in
 int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* t, int64_t k, int64_t* keys, int64_t* counts) {
     if (!ctx || !t || k < 0 || (k > 0 && (!keys || !counts))) return DQ_ERR_INVALID_ARGUMENT;
     if (k == 0) return 0;
+    if (!t->parts.empty()) {
+        // every device's top-k, then the k largest of the candidates (ties: device order, then slot order)
+        std::vector<std::pair<int64_t, int64_t>> all;  // (count, key)
+        std::vector<int64_t> pk((size_t)k), pc((size_t)k);
+        for (size_t i = 0; i < t->parts.size(); ++i) {
+            const int64_t got = dq_freq_top(t->part_ctx[i], t->parts[i], k, pk.data(), pc.data());
+            if (got < 0) return dq::ctx_fail(ctx, (int)got, t->part_ctx[i]->err.c_str());
+            for (int64_t x = 0; x < got; ++x) all.push_back({pc[x], pk[x]});
+        }
+        std::stable_sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+        const int64_t n = std::min<int64_t>(k, (int64_t)all.size());
+        for (int64_t x = 0; x < n; ++x) {
+            keys[x] = all[x].second;
+            counts[x] = all[x].first;
+        }
+        return n;
+    }
     if (hipSetDevice(t->device) != hipSuccess) return DQ_ERR_DEVICE;
     hipStream_t s = dq::ctx_stream(ctx);
     // Radix select of the k-th largest count over three 11-bit digits.
@@ -1590,7 +1852,8 @@ int64_t dq_freq_export_device(dq_ctx* ctx, const dq_freq_table* t, int64_t capac
                               int64_t* counts_dev) {
     if (!ctx || !t || capacity < 0 || (capacity > 0 && (!keys_dev || !counts_dev)))
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_export_device: invalid arguments");
-    if (!t->fast) return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_freq_export_device: table keys are row references");
+    if (!t->fast || !t->parts.empty())
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_freq_export_device: needs a single-device table of values");
     FQ_HIP(ctx, hipSetDevice(t->device));
     hipStream_t s = dq::ctx_stream(ctx);
     unsigned long long* per_block = (unsigned long long*)((char*)t->scratch + kScanBlocks * sizeof(SummaryPartial));
@@ -1651,8 +1914,9 @@ int dq_freq_from_pairs(dq_ctx* ctx, int32_t key_spark_type, const int64_t* keys,
 
 int dq_freq_merge(dq_ctx* ctx, const dq_freq_table* a, const dq_freq_table* b, dq_freq_table** out) {
     if (!ctx || !a || !b || !out) return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_merge: invalid arguments");
-    if (!a->fast || !b->fast)
-        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_freq_merge: both tables must have one fixed-width key column");
+    if (!a->fast || !b->fast || !a->parts.empty() || !b->parts.empty())
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED,
+                            "dq_freq_merge: both tables must be single-device tables of one fixed-width key column");
     if (elem_of(a->key_type) != elem_of(b->key_type) || (a->key_type == DQ_TYPE_DOUBLE) != (b->key_type == DQ_TYPE_DOUBLE))
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_merge: key types differ");
     FQ_HIP(ctx, hipSetDevice(a->device));
@@ -1725,6 +1989,11 @@ int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq
 void dq_freq_free(dq_ctx* ctx, dq_freq_table* t) {
     (void)ctx;
     if (!t) return;
+    if (!t->parts.empty()) {
+        for (size_t i = 0; i < t->parts.size(); ++i) dq_freq_free(t->part_ctx[i], t->parts[i]);
+        delete t;
+        return;
+    }
     (void)hipSetDevice(t->device);
     (void)hipDeviceSynchronize();
     free_table_buffers(t);

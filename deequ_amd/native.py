@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
     "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge",
-    "dq_freq_mutual_information",
+    "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
 )
 
 
@@ -189,6 +189,11 @@ def load_library(path=None):
                                            c_int64, c_void_p]),
             "dq_freq_merge": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
             "dq_freq_mutual_information": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+            "dq_open_devices": (c_void_p, [c_void_p, c_int, ctypes.POINTER(c_int)]),
+            "dq_ctx_num_devices": (c_int, [c_void_p]),
+            "dq_ctx_uses_rccl": (c_int, [c_void_p]),
+            "dq_scan_sharded": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
+                                        c_void_p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
@@ -243,15 +248,28 @@ def fold_states(buf, nparts, nops):
 
 
 class Context:
-    """One dq_ctx bound to one GPU (one per process / rank)."""
+    """One dq_ctx bound to one GPU (one per process / rank), or — `devices` given — one context over several
+    GPUs of this node (dq_open_devices: row-sharded scans, RCCL exchange of grouping keys)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None):
         self.lib = load_library()
         status = ctypes.c_int(0)
-        self.handle = self.lib.dq_open(int(device), ctypes.byref(status))
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+            self.handle = self.lib.dq_open_devices(arr, len(devices), ctypes.byref(status))
+            device = int(devices[0])
+        else:
+            self.handle = self.lib.dq_open(int(device), ctypes.byref(status))
         if not self.handle:
-            raise NativeError(status.value, "dq_open(%d) failed: a MI355X GPU is required" % device)
+            raise NativeError(status.value, "dq_open(%r) failed: a MI355X GPU is required" % (devices or device))
         self.device = device
+        self.devices = list(devices) if devices is not None else [device]
+
+    def num_devices(self):
+        return self.lib.dq_ctx_num_devices(self.handle)
+
+    def uses_rccl(self):
+        return bool(self.lib.dq_ctx_uses_rccl(self.handle))
 
     def close(self):
         if self.handle:
@@ -348,9 +366,12 @@ _contexts = {}
 
 
 def context(device=0):
-    """Process-wide cached context for a device."""
-    ctx = _contexts.get(device)
+    """Process-wide cached context for a device. DQ_DEVICES="0,1,..." makes it one multi-device context over
+    those GPUs (every host-column scan / grouping of the runner is then row-sharded across them)."""
+    spec = os.environ.get("DQ_DEVICES")
+    key = ("multi", spec) if spec else device
+    ctx = _contexts.get(key)
     if ctx is None:
-        ctx = Context(device)
-        _contexts[device] = ctx
+        ctx = Context(device, devices=[int(d) for d in spec.split(",")] if spec else None)
+        _contexts[key] = ctx
     return ctx

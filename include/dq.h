@@ -200,6 +200,24 @@ dq_ctx* dq_open(int device, int* status);
 void dq_close(dq_ctx* ctx);
 const char* dq_last_error(const dq_ctx* ctx);
 
+/* One context over `ndev` GPUs of this node (multi-GPU row): dq_scan over host columns splits the
+ * rows into contiguous 2048-row-aligned shards, one per device, scans them concurrently and returns the states
+ * folded in device order with the reference merges (the partition merge inside R/AnalysisRunner.scala:313);
+ * dq_frequencies pre-aggregates each shard on its device and exchanges the (key, count) groups by owner device
+ * over RCCL (ncclSend / ncclRecv all-to-all over xGMI), so each group lives on exactly one device. The context
+ * owns one RCCL communicator per device (ncclCommInitAll) when the devices are distinct; a repeated device
+ * (several shards on one GPU, e.g. to test the sharded path on one card) moves the groups with device copies
+ * instead. ndev == 1 runs the same sharded path with one shard. ApproxQuantile / KLL / casts run on the first device. */
+dq_ctx* dq_open_devices(const int* devices, int ndev, int* status);
+int dq_ctx_num_devices(const dq_ctx* ctx);
+int dq_ctx_uses_rccl(const dq_ctx* ctx);   /* 1 when the context's exchange runs over RCCL */
+
+/* dq_scan over columns already resident in HBM across the devices of a multi-device context: shard i's columns
+ * (shard_columns[i][0..ncols), DQ_COL_DEVICE on device i, or host) hold shard_rows[i] rows. States come back
+ * folded in device order (host memory). */
+int dq_scan_sharded(dq_ctx* ctx, const dq_column* const* shard_columns, const int64_t* shard_rows, int ncols,
+                    const dq_op* ops, int nops, const dq_predicate* preds, int npreds, dq_state* out);
+
 /* Run kernels on this HIP stream (hipStream_t as void*); NULL = the context's own stream. */
 int dq_set_stream(dq_ctx* ctx, void* stream);
 int dq_synchronize(dq_ctx* ctx);
