@@ -637,6 +637,22 @@ scatter2_kernel(const Pass2Item* __restrict__ items, const unsigned long long* _
     }
 }
 
+struct SummaryPartial {
+    unsigned long long groups, unique, maxc, pad;
+    double ent, comp;
+};
+
+// Kahan-compensated fold of two summary partials (fixed order: a then b).
+__device__ __forceinline__ void summary_merge(SummaryPartial& a, const SummaryPartial& b) {
+    a.groups += b.groups;
+    a.unique += b.unique;
+    a.maxc = b.maxc > a.maxc ? b.maxc : a.maxc;
+    const double y = b.ent - (a.comp + b.comp);
+    const double t = a.ent + y;
+    a.comp = (t - a.ent) - y;
+    a.ent = t;
+}
+
 struct BuildItem {
     unsigned long long begin, end;  // range of the sorted keys
     unsigned int bucket;
@@ -679,11 +695,16 @@ __device__ __forceinline__ bool lds_insert(unsigned long long* lkey, C* lcnt, un
     return false;
 }
 
+// The grouping analyzers' table aggregation (runAnalyzersForParticularGrouping, R/AnalysisRunner.scala:480-548:
+// #groups, #(count == 1), max count, sum -(c/N) ln(c/N)) is folded into the build: a whole-bucket item knows its
+// region's final counts in LDS, so it writes its summary partial (parts[item]) and the table is never re-read for
+// the default N; a slice of a split bucket flags its partial (pad = 1) and the host scans the table instead.
 template <bool GENERAL, bool WEIGHTED>
 __global__ void __launch_bounds__(kBuildBlock)
 build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
              const unsigned long long* __restrict__ rows, const long long* __restrict__ weights,
-             Slot* __restrict__ slots, unsigned long long* __restrict__ reps, Counters* __restrict__ ctr) {
+             Slot* __restrict__ slots, unsigned long long* __restrict__ reps, Counters* __restrict__ ctr,
+             SummaryPartial* __restrict__ parts, double n) {
     using C = typename std::conditional<WEIGHTED, unsigned long long, unsigned int>::type;
     __shared__ unsigned long long lkey[kRegion];
     __shared__ C lcnt[kRegion];
@@ -717,14 +738,52 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
     Slot* region = slots + (uint64_t)it.bucket * kRegion;
     unsigned long long* rrep = GENERAL ? reps + (uint64_t)it.bucket * kRegion : nullptr;
     if (!it.split) {
+        SummaryPartial p = {0, 0, 0, 0, 0.0, 0.0};
         for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
             Slot sl;
             sl.key = lkey[i];
             sl.count = (unsigned long long)lcnt[i];
             region[i] = sl;
             if (GENERAL) rrep[i] = lrep[i];
+            const unsigned long long c = sl.count;
+            if (c == 0) continue;
+            p.groups++;
+            p.unique += c == 1;
+            p.maxc = c > p.maxc ? c : p.maxc;
+            if (n > 0) {
+                const double q = (double)c / n;
+                const double term = -q * log(q);
+                const double y = term - p.comp;
+                const double t = p.ent + y;
+                p.comp = (t - p.ent) - y;
+                p.ent = t;
+            }
+        }
+        if (parts) {
+            __shared__ SummaryPartial wred[kBuildBlock / 64];
+            const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+            for (int off = 32; off > 0; off >>= 1) {
+                SummaryPartial o;
+                o.groups = __shfl_down(p.groups, off, 64);
+                o.unique = __shfl_down(p.unique, off, 64);
+                o.maxc = __shfl_down(p.maxc, off, 64);
+                o.ent = __shfl_down(p.ent, off, 64);
+                o.comp = __shfl_down(p.comp, off, 64);
+                if (lane < off) summary_merge(p, o);
+            }
+            if (lane == 0) wred[wave] = p;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                for (int w = 1; w < kBuildBlock / 64; ++w) summary_merge(p, wred[w]);
+                p.pad = 0;
+                parts[blockIdx.x] = p;
+            }
         }
     } else {
+        if (parts && threadIdx.x == 0) {
+            SummaryPartial z = {0, 0, 0, 1, 0.0, 0.0};  // pad = 1: this region needs the table scan
+            parts[blockIdx.x] = z;
+        }
         bool mok = true;
         for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
             const unsigned long long h = lkey[i];
@@ -751,10 +810,6 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
 }
 
 // ---- table scans ---------------------------------------------------------------------------------
-struct SummaryPartial {
-    unsigned long long groups, unique, maxc, pad;
-    double ent, comp;
-};
 
 __global__ void __launch_bounds__(kFreqBlock)
 summary_kernel(const Slot* __restrict__ slots, uint64_t cap, double n, SummaryPartial* __restrict__ out) {
@@ -962,6 +1017,11 @@ struct dq_freq_table {
     std::vector<dq_freq_table*> parts;
     std::vector<dq_ctx*> part_ctx;
     int64_t total_rows = 0;
+    // summary folded into the build (default N = the build's numRows), see build_kernel
+    int pre_valid = 0;
+    int64_t pre_n = -1;
+    unsigned long long pre_groups = 0, pre_unique = 0, pre_maxc = 0;
+    double pre_ent = 0.0, pre_comp = 0.0;
     int32_t key_type = 0;   // Spark type of the (single) key column, or of the canonical keys of a pair-built table
     int64_t num_rows_override = -1;  // tables built from (key, count) pairs carry the caller's numRows
     int64_t cached_n = -1;  // dq_freq_summarize memo (the table is immutable once built)
@@ -1065,18 +1125,21 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     const int nitems = (int)items.size();
     hipLaunchKernelGGL(region_init_kernel, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, nitems, t->slots, t->reps);
     const long long* w = t->ks.weights;
+    SummaryPartial* bparts = nullptr;
+    FQ_HIP(ctx, buf.alloc((void**)&bparts, items.size() * sizeof(SummaryPartial)));
+    const double build_n = (double)t->host_ctr.num_rows;  // the count pass's numRows (copied before the build)
     if (general && weighted)
         hipLaunchKernelGGL((build_kernel<true, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr);
+                           t->slots, t->reps, t->ctr, bparts, build_n);
     else if (general)
         hipLaunchKernelGGL((build_kernel<true, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr);
+                           t->slots, t->reps, t->ctr, bparts, build_n);
     else if (weighted)
         hipLaunchKernelGGL((build_kernel<false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr);
+                           t->slots, t->reps, t->ctr, bparts, build_n);
     else
         hipLaunchKernelGGL((build_kernel<false, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr);
+                           t->slots, t->reps, t->ctr, bparts, build_n);
     FQ_HIP(ctx, hipGetLastError());
     if (general && nrows > 0) {
         const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
@@ -1084,7 +1147,35 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
                            t->ctr);
     }
     FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    std::vector<SummaryPartial> hparts(items.size());
+    FQ_HIP(ctx, hipMemcpyAsync(hparts.data(), bparts, items.size() * sizeof(SummaryPartial), hipMemcpyDeviceToHost, s));
     FQ_HIP(ctx, hipStreamSynchronize(s));
+    // the fused summary, folded in item order (deterministic) unless a split bucket needs the table scan
+    t->pre_valid = 0;
+    if (t->host_ctr.overflow == 0 && t->host_ctr.mismatch == 0) {
+        bool all = true;
+        unsigned long long groups = 0, unique = 0, maxc = 0;
+        double ent = 0.0, comp = 0.0;
+        for (const SummaryPartial& p : hparts) {
+            if (p.pad) { all = false; break; }
+            groups += p.groups;
+            unique += p.unique;
+            maxc = std::max(maxc, p.maxc);
+            const double y = (p.ent - p.comp) - comp;
+            const double tt = ent + y;
+            comp = (tt - ent) - y;
+            ent = tt;
+        }
+        if (all) {
+            t->pre_valid = 1;
+            t->pre_n = (int64_t)build_n;
+            t->pre_groups = groups;
+            t->pre_unique = unique;
+            t->pre_maxc = maxc;
+            t->pre_ent = ent;
+            t->pre_comp = comp;
+        }
+    }
     if (getenv("DQ_DEBUG_FREQ"))
         fprintf(stderr, "[freq] rows=%lld bits=%d items=%zu rows_taken=%llu ovf=%llu mis=%llu\n", (long long)nrows, bits,
                 items.size(), t->host_ctr.num_rows, t->host_ctr.overflow, t->host_ctr.mismatch);
@@ -1239,6 +1330,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         std::vector<unsigned long long> hkeep(xgrid), hoff(xgrid);
         FQ_HIP(ctx, hipMemcpyAsync(hregs.data(), regs, kSizingRegs * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
         FQ_HIP(ctx, hipMemcpyAsync(hkeep.data(), bk, sizeof(unsigned long long) * xgrid, hipMemcpyDeviceToHost, s));
+        FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
         FQ_HIP(ctx, hipStreamSynchronize(s));
         unsigned long long n = 0;
         for (int g = 0; g < xgrid; ++g) {
@@ -1663,12 +1755,6 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
         *out = t->cached;
         return DQ_OK;
     }
-    SummaryPartial* parts = (SummaryPartial*)t->scratch;
-    hipLaunchKernelGGL(summary_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->cap, (double)n, parts);
-    FQ_HIP(ctx, hipGetLastError());
-    std::vector<SummaryPartial> hp(kScanBlocks);
-    FQ_HIP(ctx, hipMemcpyAsync(hp.data(), parts, sizeof(SummaryPartial) * kScanBlocks, hipMemcpyDeviceToHost, s));
-    FQ_HIP(ctx, hipStreamSynchronize(s));
     unsigned long long groups = 0, unique = 0, maxc = 0;
     double ent = 0.0, comp = 0.0;
     auto add_term = [&](double term) {
@@ -1677,11 +1763,25 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
         comp = (tt - ent) - y;
         ent = tt;
     };
-    for (const SummaryPartial& p : hp) {
-        groups += p.groups;
-        unique += p.unique;
-        maxc = std::max(maxc, p.maxc);
-        add_term(p.ent - p.comp);
+    if (t->pre_valid && t->pre_n == n) {  // folded into the build: no table scan
+        groups = t->pre_groups;
+        unique = t->pre_unique;
+        maxc = t->pre_maxc;
+        ent = t->pre_ent;
+        comp = t->pre_comp;
+    } else {
+        SummaryPartial* parts = (SummaryPartial*)t->scratch;
+        hipLaunchKernelGGL(summary_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->cap, (double)n, parts);
+        FQ_HIP(ctx, hipGetLastError());
+        std::vector<SummaryPartial> hp(kScanBlocks);
+        FQ_HIP(ctx, hipMemcpyAsync(hp.data(), parts, sizeof(SummaryPartial) * kScanBlocks, hipMemcpyDeviceToHost, s));
+        FQ_HIP(ctx, hipStreamSynchronize(s));
+        for (const SummaryPartial& p : hp) {
+            groups += p.groups;
+            unique += p.unique;
+            maxc = std::max(maxc, p.maxc);
+            add_term(p.ent - p.comp);
+        }
     }
     // side groups: the fast path's EMPTY-colliding value and (Histogram) the NULL group
     for (unsigned long long extra : {t->host_ctr.sentinel, t->host_ctr.nulls}) {

@@ -25,7 +25,7 @@ from . import engine
 from .analyzers import (ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer, Histogram,
                         FrequenciesAndNumRows, Preconditions, metricFromFailure)
 from .metrics import (HistogramMetric, Distribution, DistributionValue, Success, Failure, wrap_if_necessary,
-                      MetricCalculationRuntimeException)
+                      MetricCalculationRuntimeException, UnsupportedOnDevice)
 from .runners import AnalyzerContext, ScanBatch, ScanResult
 
 
@@ -216,11 +216,28 @@ def _canonical_key(v, column):
 
 
 class DistributedAnalysisRunner:
-    """AnalysisRunner over a row shard per rank; every rank returns the same AnalyzerContext."""
+    """AnalysisRunner over a row shard per rank; every rank returns the same AnalyzerContext.
+
+    Failure protocol: every stage runs its local (per-rank) compute first, then every rank takes part in
+    one agreement collective (`_agree`) before any data collective, so a rank that fails locally (a regex
+    budget, an out-of-memory, a bad shard) never leaves its peers blocked in a collective it skips: all
+    ranks learn the first failing rank's error and turn it into the same failure metrics."""
 
     def __init__(self, exchange=None, local=None):
         self.ex = exchange or Exchange()
         self.local = local or GpuLocal()
+
+    def _agree(self, error):
+        """Collective on every rank: None if every rank succeeded, else the first failing rank's error (as a
+        MetricCalculationRuntimeException carrying its message) on every rank."""
+        flags = self.ex.all_reduce_i64([0 if error is None else 1])
+        if flags[0] == 0:
+            return None
+        msgs = self.ex.all_gather_blobs(b"" if error is None else ("%s: %s" % (type(error).__name__, error)).encode())
+        for r, m in enumerate(msgs):
+            if m:
+                return MetricCalculationRuntimeException("rank %d failed: %s" % (r, m.decode(errors="replace")))
+        return MetricCalculationRuntimeException("a rank failed")
 
     def run(self, shard, analyzers):
         uniq = []
@@ -241,10 +258,20 @@ class DistributedAnalysisRunner:
         if kll:
             self._kll_metrics(shard, kll, results)
         if shareable:
+            local_err = None
             try:
                 batch = ScanBatch(shard)
                 offsets = [a.addOps(batch) for a in shareable]
                 local_states, local_q = self.local.scan_states(batch)
+            except Exception as e:
+                local_err = e
+            agreed = self._agree(local_err)
+            if agreed is not None:
+                for a in shareable:
+                    results[a] = a.toFailureMetric(agreed)
+                shareable = []
+        if shareable:
+            try:
                 gathered = self.ex.all_gather_bytes(local_states)
                 states = ScanResult(fold_states(gathered.cpu().numpy(), self.ex.world, len(batch.ops)))
                 if batch.quantile_reqs:
@@ -269,6 +296,11 @@ class DistributedAnalysisRunner:
                     results[a] = a.toFailureMetric(e)
         by_cols = {}
         for a in passed:
+            if isinstance(a, Histogram) and a.binningUdf is not None:
+                # the binning UDF is a host function of this process; the sharded path groups raw keys
+                results[a] = a.toFailureMetric(UnsupportedOnDevice(
+                    "Histogram with a binningUdf is not supported by the multi-GPU runner"))
+                continue
             if isinstance(a, (GroupingAnalyzer, Histogram)):
                 cols = tuple(a.groupingColumns()) if isinstance(a, GroupingAnalyzer) else (a.column,)
                 by_cols.setdefault(cols, []).append(a)
@@ -277,7 +309,7 @@ class DistributedAnalysisRunner:
                 freq = self._frequencies(shard, list(cols))
             except Exception as e:
                 for a in group:
-                    results[a] = a.toFailureMetric(e)
+                    results[a] = a.toFailureMetric(wrap_if_necessary(e))
                 continue
             for a in group:
                 results[a] = self._grouping_metric(a, freq)
@@ -295,8 +327,16 @@ class DistributedAnalysisRunner:
         for column, p in params.items():
             size, f = (p.sketchSize, p.shrinkingFactor) if p is not None else \
                 (DEFAULT_SKETCH_SIZE, DEFAULT_SHRINKING_FACTOR)
+            blob, local_err = None, None
             try:
                 blob = self.local.kll_state(shard, column, size, f)
+            except Exception as e:
+                local_err = e
+            agreed = self._agree(local_err)
+            if agreed is not None:
+                merged[column] = agreed
+                continue
+            try:
                 acc = None
                 for b in self.ex.all_gather_blobs(blob):
                     st = KLLState.fromBytes(b)
@@ -310,12 +350,26 @@ class DistributedAnalysisRunner:
 
     def _frequencies(self, shard, cols):
         if len(cols) != 1 or shard[cols[0]].spark_type == N.TYPE_STRING:
-            raise MetricCalculationRuntimeException(
+            raise UnsupportedOnDevice(
                 "multi-GPU grouping supports one fixed-width key column (strings / multi-column: single GPU)")
         column = shard[cols[0]]
-        keys, send, nulls = self.local.partition(column, self.ex.world)
+        local_err = None
+        try:
+            keys, send, nulls = self.local.partition(column, self.ex.world)
+        except Exception as e:
+            local_err = e
+        agreed = self._agree(local_err)
+        if agreed is not None:
+            raise agreed
         owned = self.ex.all_to_all_keys(keys, send)
-        local_table = self.local.frequencies_of_keys(owned)
+        local_err, local_table = None, None
+        try:
+            local_table = self.local.frequencies_of_keys(owned)
+        except Exception as e:
+            local_err = e
+        agreed = self._agree(local_err)
+        if agreed is not None:
+            raise agreed
         taking, nulls_g = self.ex.all_reduce_i64([int(local_table.num_rows), nulls])
         return DistributedFrequencies(self.ex, local_table, column, taking, nulls_g)
 

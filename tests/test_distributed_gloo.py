@@ -241,3 +241,70 @@ def test_distributed_runner_matches_single_table_oracle(world):
             assert g == exp, (a, g, exp)
         else:
             assert abs(g - exp) <= 1e-12 * max(1.0, abs(exp)), (a, g, exp)
+
+
+class FailingOnRankOne(OracleLocal):
+    """Rank 1 fails locally in the scan, the KLL sketch and the key partitioning (a local failure
+    must not leave the other ranks blocked in a collective)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+
+    def scan_states(self, batch):
+        if self.rank == 1:
+            raise RuntimeError("regex backtracking limit exceeded")
+        return super().scan_states(batch)
+
+    def kll_state(self, shard, column, sketch_size, shrinking_factor):
+        if self.rank == 1:
+            raise MemoryError("out of device memory")
+        return super().kll_state(shard, column, sketch_size, shrinking_factor)
+
+    def partition(self, column, world):
+        if self.rank == 1:
+            raise RuntimeError("partition failed")
+        return super().partition(column, world)
+
+
+def _failing_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = full_table(600)
+        per = (t.nrows + world - 1) // world
+        mask = np.zeros(t.nrows, dtype=bool)
+        mask[rank * per:min(t.nrows, (rank + 1) * per)] = True
+        runner = D.distributed.DistributedAnalysisRunner(local=FailingOnRankOne(rank))
+        analyzers = [D.Size(), D.Mean("x"), D.KLLSketch("x"), D.Uniqueness(["k"]),
+                     D.Histogram("d", lambda s: s[:1])]
+        ctx = runner.run(t.select_rows(mask), analyzers)
+        out = {(repr(a) if a.__class__.__name__ != "Histogram" else "Histogram"):
+               (ctx.metric(a).value.isFailure, str(ctx.metric(a).value.failed) if ctx.metric(a).value.isFailure else None)
+               for a in analyzers}
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_one_failing_rank_fails_every_rank_without_hanging(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert results[r] == results[0]  # identical failure metrics on every rank
+    got = results[0]
+    assert got["Size(None)"][0] and "rank 1 failed" in got["Size(None)"][1]
+    assert got["Mean(x,None)"][0]
+    assert any(k.startswith("KLLSketch") and v[0] and "rank 1 failed" in v[1] for k, v in got.items())
+    assert got["Uniqueness(List(k))"][0] and "rank 1 failed" in got["Uniqueness(List(k))"][1]
+    hist = got["Histogram"]
+    assert hist[0] and "binningUdf" in hist[1]
