@@ -429,8 +429,7 @@ class PatternMatch(StandardScanShareableAnalyzer):
 
     def addOps(self, batch):
         col = batch.data[self.column] if self.column in batch.col_index else None
-        if col is not None and col.spark_type in (N.TYPE_FLOAT, N.TYPE_DOUBLE, N.TYPE_DECIMAL, N.TYPE_DATE,
-                                                  N.TYPE_TIMESTAMP):
+        if col is not None and col.spark_type in (N.TYPE_DECIMAL, N.TYPE_DATE, N.TYPE_TIMESTAMP):
             raise UnsupportedOnDevice(
                 "PatternMatch over %s: the GPU engine does not format this type as a string" % col.type_name)
         p = batch.regex_predicate(self.column, self.pattern_)

@@ -330,7 +330,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: malformed REGEX program", p);
             const int t = columns[c].spark_type;
             if (!(t == DQ_TYPE_STRING || t == DQ_TYPE_BOOLEAN || t == DQ_TYPE_BYTE || t == DQ_TYPE_SHORT ||
-                  t == DQ_TYPE_INT || t == DQ_TYPE_LONG))
+                  t == DQ_TYPE_INT || t == DQ_TYPE_LONG || t == DQ_TYPE_FLOAT || t == DQ_TYPE_DOUBLE))
                 return fail(ctx, DQ_ERR_UNSUPPORTED, "predicate %d: PatternMatch over this column type is not supported", p);
             col_used[c] = 1;
             continue;

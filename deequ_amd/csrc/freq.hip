@@ -55,7 +55,8 @@ constexpr uint64_t kEmpty = ~0ull;
 constexpr int kSizingRegs = 4096;  // HLL registers used only to size the table
 constexpr int kFreqBlock = 256;
 constexpr int kDigitBins = 256;    // radix partition: first pass on the low 8 bits of the key
-constexpr int kPartTile = 4096;    // keys per workgroup tile of the partition scatters (16 per lane)
+constexpr int kPartTile = 4096;    // keys per workgroup tile of the partition scatters (16 per lane), general path
+constexpr int kPartTileFast = 8192;// fast path: 32 per lane, so a tile's 256 per-digit runs average 256 B
 constexpr int kPass2Item = 65536;  // keys per work item of the second partition pass
 constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (fixed: deterministic partials)
 constexpr int kRegion = 4096;      // slots per bucket region (the LDS table of one workgroup)
@@ -274,7 +275,8 @@ __device__ __forceinline__ void chunk_of(int64_t nrows, int64_t& r0, int64_t& r1
 
 __global__ void __launch_bounds__(kFreqBlock)
 extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__ block_keep,
-                     uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, unsigned int* __restrict__ hist1) {
+                     uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, unsigned int* __restrict__ hist1,
+                     int tile_rows) {
     __shared__ unsigned int lds[kSizingRegs];
     __shared__ unsigned int dh[kDigitBins];
     __shared__ unsigned long long red[kFreqBlock / 64];
@@ -285,9 +287,9 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
     constexpr int U = 4;  // rows in flight per lane
     // tiles of kPartTile rows interleaved over the workgroups (tile g, g + G, ...): all workgroups stream
     // through one narrow address window, as the partition scatter that replays the same tiles does
-    const int64_t ntiles = (nrows + kPartTile - 1) / kPartTile;
+    const int64_t ntiles = (nrows + tile_rows - 1) / tile_rows;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
-    for (int64_t rb = tile * kPartTile + threadIdx.x, r1 = min((tile + 1) * (int64_t)kPartTile, nrows); rb < r1;
+    for (int64_t rb = tile * tile_rows + threadIdx.x, r1 = min((tile + 1) * (int64_t)tile_rows, nrows); rb < r1;
          rb += (int64_t)kFreqBlock * U) {
         uint64_t hv[U];
         bool ok[U], ngv[U];
@@ -350,13 +352,13 @@ sizing_reduce_kernel(const uint8_t* __restrict__ regs_part, int ngroups, unsigne
 // workgroup's offset — no shared counter, deterministic layout.
 __global__ void __launch_bounds__(kFreqBlock)
 extract_write_kernel(KeySpec ks, int64_t nrows, const unsigned long long* __restrict__ block_off,
-                     unsigned long long* __restrict__ hs, unsigned long long* __restrict__ rows) {
+                     unsigned long long* __restrict__ hs, unsigned long long* __restrict__ rows, int tile_rows) {
     __shared__ unsigned int wave_cnt[kFreqBlock / 64];
     unsigned long long base = block_off[blockIdx.x];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t ntiles = (nrows + kPartTile - 1) / kPartTile;  // the count pass's tiles
+    const int64_t ntiles = (nrows + tile_rows - 1) / tile_rows;  // the count pass's tiles
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
-    for (int64_t t0 = tile * kPartTile, r1 = min(t0 + (int64_t)kPartTile, nrows); t0 < r1; t0 += kFreqBlock) {
+    for (int64_t t0 = tile * tile_rows, r1 = min(t0 + (int64_t)tile_rows, nrows); t0 < r1; t0 += kFreqBlock) {
         const int64_t r = t0 + threadIdx.x;
         uint64_t h = 0;
         bool ng = false;
@@ -432,13 +434,13 @@ digit_scan_kernel(const unsigned int* __restrict__ hist, int ngroups, int nbins,
 
 // One tile (<= kPartTile keys in registers, digit per key) -> LDS staging ordered by digit -> global
 // runs at cursor[digit]. `bins` <= BINS. Returns after the cursors advanced.
-template <int BINS, bool GENERAL>
-__device__ __forceinline__ void scatter_tile(const uint64_t (&h)[kPartTile / kFreqBlock],
-                                             const uint64_t (&rw)[kPartTile / kFreqBlock], const bool (&keep)[kPartTile / kFreqBlock],
+template <int BINS, bool GENERAL, int TILE>
+__device__ __forceinline__ void scatter_tile(const uint64_t (&h)[TILE / kFreqBlock],
+                                             const uint64_t (&rw)[TILE / kFreqBlock], const bool (&keep)[TILE / kFreqBlock],
                                              int shift, unsigned int mask, unsigned int* hist, unsigned int* start,
                                              unsigned long long* cursor, unsigned long long* sh, unsigned long long* sr,
                                              unsigned long long* __restrict__ out_h, unsigned long long* __restrict__ out_r) {
-    constexpr int PER = kPartTile / kFreqBlock;
+    constexpr int PER = TILE / kFreqBlock;
     unsigned int rank[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j)
@@ -501,16 +503,16 @@ __device__ __forceinline__ void scatter_tile(const uint64_t (&h)[kPartTile / kFr
 }
 
 // Pass 1: rows -> 256 partitions (same workgroup chunks as extract_count_kernel).
-template <bool GENERAL>
+template <bool GENERAL, int TILE>
 __global__ void __launch_bounds__(kFreqBlock)
 partition1_kernel(KeySpec ks, int64_t nrows, const unsigned long long* __restrict__ off1,
                   const unsigned long long* __restrict__ totals, unsigned long long* __restrict__ out_h,
                   unsigned long long* __restrict__ out_r) {
-    constexpr int PER = kPartTile / kFreqBlock;
+    constexpr int PER = TILE / kFreqBlock;
     __shared__ unsigned int hist[kDigitBins], start[kDigitBins];
     __shared__ unsigned long long cursor[kDigitBins];
-    __shared__ unsigned long long sh[kPartTile];
-    __shared__ unsigned long long sr[GENERAL ? kPartTile : 1];
+    __shared__ unsigned long long sh[TILE];
+    __shared__ unsigned long long sr[GENERAL ? TILE : 1];
     {
         // cursor[d] = (exclusive scan of the digit totals)[d] + this workgroup's offset inside digit d
         __shared__ unsigned long long tot[kDigitBins];
@@ -526,20 +528,28 @@ partition1_kernel(KeySpec ks, int64_t nrows, const unsigned long long* __restric
         cursor[threadIdx.x] = (threadIdx.x ? tot[threadIdx.x - 1] : 0ull) + off1[(uint64_t)blockIdx.x * kDigitBins + threadIdx.x];
         __syncthreads();
     }
-    const int64_t ntiles = (nrows + kPartTile - 1) / kPartTile;
+    const int64_t ntiles = (nrows + TILE - 1) / TILE;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t t0 = tile * kPartTile, r1 = min(t0 + (int64_t)kPartTile, nrows);
+        const int64_t t0 = tile * TILE, r1 = min(t0 + (int64_t)TILE, nrows);
         uint64_t h[PER], rw[PER];
         bool keep[PER];
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const int64_t r = t0 + (int64_t)j * kFreqBlock + threadIdx.x;
+            if (!GENERAL) {  // one fixed-width key column: its mixed canonical value (row_key's fast path)
+                const KeyCol& c = ks.cols[0];
+                const bool in = r < r1 && is_valid(c, r);
+                h[j] = in ? mix64(canonical(c, r)) : kEmpty;
+                keep[j] = in && h[j] != kEmpty;
+                rw[j] = 0;
+                continue;
+            }
             bool ng = false;
             h[j] = 0;
             keep[j] = r < r1 && row_key(ks, r, h[j], ng) && !ng && h[j] != kEmpty;
             rw[j] = (unsigned long long)r;
         }
-        scatter_tile<kDigitBins, GENERAL>(h, rw, keep, 0, kDigitBins - 1, hist, start, cursor, sh, sr, out_h, out_r);
+        scatter_tile<kDigitBins, GENERAL, TILE>(h, rw, keep, 0, kDigitBins - 1, hist, start, cursor, sh, sr, out_h, out_r);
     }
 }
 
@@ -607,23 +617,23 @@ scan2_kernel(const unsigned int* __restrict__ cnt, const int* __restrict__ part_
 }
 
 // Pass 2 scatter: per work item, keys (and rows) -> their bucket's range.
-template <int BINS, bool GENERAL>
+template <int BINS, bool GENERAL, int TILE>
 __global__ void __launch_bounds__(kFreqBlock)
 scatter2_kernel(const Pass2Item* __restrict__ items, const unsigned long long* __restrict__ off, const unsigned long long* __restrict__ in_h,
                 const unsigned long long* __restrict__ in_r, int shift, unsigned int mask, unsigned long long* __restrict__ out_h,
                 unsigned long long* __restrict__ out_r) {
-    constexpr int PER = kPartTile / kFreqBlock;
+    constexpr int PER = TILE / kFreqBlock;
     __shared__ unsigned int hist[BINS], start[BINS];
     __shared__ unsigned long long cursor[BINS];
-    __shared__ unsigned long long sh[kPartTile];
-    __shared__ unsigned long long sr[GENERAL ? kPartTile : 1];
+    __shared__ unsigned long long sh[TILE];
+    __shared__ unsigned long long sr[GENERAL ? TILE : 1];
     const Pass2Item it = items[blockIdx.x];
     for (int b = threadIdx.x; b < BINS; b += kFreqBlock) {
         hist[b] = 0;
         cursor[b] = off[(uint64_t)blockIdx.x * BINS + b];
     }
     __syncthreads();
-    for (unsigned long long t0 = it.begin; t0 < it.end; t0 += kPartTile) {
+    for (unsigned long long t0 = it.begin; t0 < it.end; t0 += TILE) {
         uint64_t h[PER], rw[PER];
         bool keep[PER];
 #pragma unroll
@@ -633,7 +643,7 @@ scatter2_kernel(const Pass2Item* __restrict__ items, const unsigned long long* _
             h[j] = keep[j] ? __builtin_nontemporal_load(&in_h[i]) : 0ull;
             rw[j] = (GENERAL && keep[j]) ? in_r[i] : 0ull;
         }
-        scatter_tile<BINS, GENERAL>(h, rw, keep, shift, mask, hist, start, cursor, sh, sr, out_h, out_r);
+        scatter_tile<BINS, GENERAL, TILE>(h, rw, keep, shift, mask, hist, start, cursor, sh, sr, out_h, out_r);
     }
 }
 
@@ -1207,10 +1217,10 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
     if (general) FQ_HIP(ctx, buf.alloc((void**)&r1, n_alloc * 8));
     hipLaunchKernelGGL(digit_scan_kernel, dim3(kDigitBins), dim3(256), 0, s, hist1, xgrid, kDigitBins, off1, totals);
     if (general)
-        hipLaunchKernelGGL(partition1_kernel<true>, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
+        hipLaunchKernelGGL((partition1_kernel<true, kPartTile>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
                            (const unsigned long long*)off1, (const unsigned long long*)totals, h1, r1);
     else
-        hipLaunchKernelGGL(partition1_kernel<false>, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
+        hipLaunchKernelGGL((partition1_kernel<false, kPartTileFast>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
                            (const unsigned long long*)off1, (const unsigned long long*)totals, h1, r1);
     FQ_HIP(ctx, hipGetLastError());
     std::vector<unsigned long long> tot(kDigitBins), pbegin(kDigitBins + 1, 0);
@@ -1264,20 +1274,20 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
                 hipLaunchKernelGGL(scan2_kernel<4096>, dim3(kDigitBins), dim3(kFreqBlock), 0, s, cnt2, dpitems, dpbegin, bins, off2,
                                    dbstart, dbcount);
                 if (nitems && general)
-                    hipLaunchKernelGGL((scatter2_kernel<4096, true>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1, 8,
+                    hipLaunchKernelGGL((scatter2_kernel<4096, true, kPartTile>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1, 8,
                                        mask, h2, r2);
                 else if (nitems)
-                    hipLaunchKernelGGL((scatter2_kernel<4096, false>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1, 8,
+                    hipLaunchKernelGGL((scatter2_kernel<4096, false, kPartTileFast>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1, 8,
                                        mask, h2, r2);
             } else {
                 if (nitems) hipLaunchKernelGGL(count2_kernel<kDigitBins>, dim3(nitems), dim3(kFreqBlock), 0, s, ditems, h1, 8, mask, cnt2);
                 hipLaunchKernelGGL(scan2_kernel<kDigitBins>, dim3(kDigitBins), dim3(kFreqBlock), 0, s, cnt2, dpitems, dpbegin, bins,
                                    off2, dbstart, dbcount);
                 if (nitems && general)
-                    hipLaunchKernelGGL((scatter2_kernel<kDigitBins, true>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1,
+                    hipLaunchKernelGGL((scatter2_kernel<kDigitBins, true, kPartTile>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1,
                                        8, mask, h2, r2);
                 else if (nitems)
-                    hipLaunchKernelGGL((scatter2_kernel<kDigitBins, false>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1,
+                    hipLaunchKernelGGL((scatter2_kernel<kDigitBins, false, kPartTileFast>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, off2, h1, r1,
                                        8, mask, h2, r2);
             }
             FQ_HIP(ctx, hipGetLastError());
@@ -1321,7 +1331,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
         if (nrows > 0) {
             hipLaunchKernelGGL(extract_count_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows, bk, regs_part,
-                               t->ctr, hist1);
+                               t->ctr, hist1, general ? kPartTile : kPartTileFast);
             hipLaunchKernelGGL(sizing_reduce_kernel, dim3(kSizingRegs / 256, std::min(xgrid, 64)), dim3(256), 0, s,
                                (const uint8_t*)regs_part, xgrid, regs);
         }
@@ -1355,7 +1365,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         if (nrows > 0) {
             FQ_HIP(ctx, hipMemcpyAsync(bk + xgrid, hoff.data(), sizeof(unsigned long long) * xgrid, hipMemcpyHostToDevice, s));
             hipLaunchKernelGGL(extract_write_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
-                               (const unsigned long long*)(bk + xgrid), hs, rows);
+                               (const unsigned long long*)(bk + xgrid), hs, rows, general ? kPartTile : kPartTileFast);
             FQ_HIP(ctx, hipGetLastError());
         }
         unsigned long long *hs2 = nullptr, *rows2 = nullptr;

@@ -15,6 +15,7 @@
 
 #include "dq_common.h"
 #include "dq_internal.h"
+#include "java_dtoa.h"
 
 namespace dq {
 
@@ -265,7 +266,7 @@ regex_match_kernel(PredColumn col, const int32_t* __restrict__ image, int64_t nr
         bool valid = true;
         if (col.validity) valid = (col.validity[row >> 6] >> (row & 63)) & 1ull;
         if (valid) {
-            uint8_t buf[24];
+            uint8_t buf[32];
             const uint8_t* s;
             int n;
             switch (col.spark_type) {
@@ -275,6 +276,14 @@ regex_match_kernel(PredColumn col, const int32_t* __restrict__ image, int64_t nr
                     n = o1 - o0;
                     break;
                 }
+                case DQ_TYPE_DOUBLE:  // Cast(x AS STRING) = Double.toString / Float.toString (java_dtoa.h)
+                    n = java_double_to_chars(static_cast<const double*>(col.values)[row], buf);
+                    s = buf;
+                    break;
+                case DQ_TYPE_FLOAT:
+                    n = java_float_to_chars(static_cast<const float*>(col.values)[row], buf);
+                    s = buf;
+                    break;
                 case DQ_TYPE_BOOLEAN: {
                     const bool b = static_cast<const uint8_t*>(col.values)[row] != 0;
                     const char* txt = b ? "true" : "false";

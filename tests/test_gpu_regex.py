@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import deequ_amd as D
-from deequ_amd.table import Table, Column, _column_from_pylist
+from deequ_amd.table import Table, Column, _column_from_pylist, pack_validity
 import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -84,3 +84,26 @@ def test_catastrophic_backtracking_fails_loudly():
     t = Table([_column_from_pylist("s", "string", ["x" * 40])])
     m = D.PatternMatch("s", r"(x+x+)+y").calculate(t)
     assert m.value.isFailure  # budget exhausted: the batch fails instead of miscounting
+
+
+def test_pattern_match_over_double_and_float_columns():
+    """PatternMatch matches regexp_extract over Cast(x AS STRING) = Double.toString / Float.toString
+    (A/PatternMatch.scala:46-48), formatted on the GPU (deequ_amd/csrc/java_dtoa.h): plain and scientific
+    notation, signed zeros, NaN / Infinity, subnormals, the shortest round-trip digits."""
+    rng = np.random.default_rng(8)
+    n = 20000
+    d = np.concatenate([rng.normal(0, 1e3, n // 4), rng.uniform(-1, 1, n // 4) * 10.0 ** rng.integers(-12, 12, n // 4),
+                        rng.integers(-1000, 1000, n // 4) / 8.0,
+                        np.array([0.0, -0.0, np.nan, np.inf, -np.inf, 1e7, 9999999.0, 1e-3, 9.999e-4, 5e-324,
+                                  1.7976931348623157e308, 0.1, 1e23])])
+    d = np.concatenate([d, rng.standard_normal(n - len(d))])
+    valid = rng.random(len(d)) > 0.05
+    t = Table([Column("d", "double", d, pack_validity(valid)),
+               Column("f", "float", d.astype(np.float32), pack_validity(valid))])
+    analyzers = [D.PatternMatch(c, p) for c in ("d", "f") for p in
+                 (r"\d\.\d", r"E-?\d+$", r"^-?0\.0+[1-9]", r"^-?\d{1,3}\.\d{1,2}$", r"NaN|Infinity", r"^-0\.0$",
+                  r"\.0$", r"[1-9]\.[0-9]{5,}")]
+    got = states(t, analyzers)
+    for a, g in zip(analyzers, got):
+        exp = O.expected_state(t, a)
+        assert g == exp, (a.column, a.pattern, g, exp)

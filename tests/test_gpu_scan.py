@@ -31,10 +31,7 @@ def test_scan_kats_one_by_one(kats):
         t = table_from_fixture(kats["fixtures"][k["fixture"]])
         a = analyzer_from_spec(k["analyzer"])
         m = a.calculate(t)
-        if isinstance(a, D.PatternMatch) and t[a.column].spark_type == N.TYPE_DOUBLE:
-            # Java Double.toString is not restated on the GPU: this configuration fails loudly
-            assert m.value.isFailure and type(m.value.failed).__name__ == "UnsupportedOnDevice", m
-            continue
+        # PatternMatch over a double column included (AnalyzerTests.scala:664-668: 0.75 through Double.toString)
         check_metric(m, k["expected"], rel=1e-15 if k["analyzer"][0] == "StandardDeviation" else 0.0)
 
 
@@ -50,8 +47,6 @@ def test_scan_kats_fused_in_one_run(kats):
             a = analyzer_from_spec(k["analyzer"])
             if isinstance(k["expected"], dict) and k["expected"].get("failure") == "*":
                 continue  # an unresolvable predicate fails the whole batch (R/AnalysisRunner.scala:320-323)
-            if isinstance(a, D.PatternMatch) and t[a.column].spark_type == N.TYPE_DOUBLE:
-                continue
             analyzers.append(a)
             exps.append(k["expected"])
         before = engine.ctx().scan_launch_count()
