@@ -895,6 +895,148 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     return DQ_OK;
 }
 
+// Host columns streamed through HBM in row chunks (tables larger than HBM, or host-resident batches): the copy
+// of chunk i + 1 (its own stream, double-buffered device chunks) overlaps the fused scan of chunk i; every chunk's
+// states land in device memory and the chunks are folded in row order with the reference merges (the partition
+// merge of R/AnalysisRunner.scala:313) — the same result as any other row partitioning.
+int dq_scan_streamed(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const dq_op* ops, int nops,
+                     const dq_predicate* preds, int npreds, dq_state* out, int64_t chunk_rows) {
+    if (!ctx || (nops > 0 && (!ops || !out)) || ncols < 0 || nrows < 0 || chunk_rows <= 0)
+        return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_scan_streamed: invalid arguments");
+    ctx->err.clear();
+    if (!ctx->subs.empty()) return fail(ctx, DQ_ERR_UNSUPPORTED, "dq_scan_streamed takes a single-device context");
+    for (int c = 0; c < ncols; ++c)
+        if ((columns[c].flags & DQ_COL_DEVICE) || columns[c].length != nrows)
+            return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_scan_streamed: column %d must be a host column of %lld rows", c,
+                        (long long)nrows);
+    if (nops == 0) return DQ_OK;
+    chunk_rows = std::max<int64_t>(kTileRows, chunk_rows / kTileRows * kTileRows);
+    if (nrows <= chunk_rows) return dq_scan(ctx, columns, ncols, nrows, ops, nops, preds, npreds, out, 0);
+    DQ_HIP(ctx, hipSetDevice(ctx->device));
+    const int64_t nchunks = (nrows + chunk_rows - 1) / chunk_rows;
+    // device chunk buffers: 2 sets, each sized for the largest chunk of every column
+    std::vector<size_t> vcap(ncols, 0), bcap(ncols, 0), ocap(ncols, 0);
+    for (int c = 0; c < ncols; ++c) {
+        const dq_column& col = columns[c];
+        if (col.spark_type == DQ_TYPE_STRING) {
+            size_t mx = 0;
+            for (int64_t k = 0; k < nchunks; ++k) {
+                const int64_t r0 = k * chunk_rows, r1 = std::min(nrows, r0 + chunk_rows);
+                mx = std::max<size_t>(mx, (size_t)(col.offsets[r1] - col.offsets[r0]));
+            }
+            vcap[c] = mx + 16;
+            ocap[c] = ((size_t)chunk_rows + 1) * 4;
+        } else {
+            vcap[c] = (size_t)chunk_rows * elem_size(elem_of(col.spark_type)) + 16;
+        }
+        if (col.validity) bcap[c] = (size_t)chunk_rows / 8 + 8;
+    }
+    struct Set { std::vector<void*> v, b, o; hipEvent_t copied, scanned; };
+    Set sets[2];
+    hipStream_t cstream = nullptr;
+    std::vector<void*> allocs;
+    dq_state* dstates = nullptr;
+    std::vector<std::vector<int32_t>> rebased(2 * std::max(ncols, 1));
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(ctx->stream);
+        if (cstream) { (void)hipStreamSynchronize(cstream); (void)hipStreamDestroy(cstream); }
+        for (Set& st : sets) {
+            if (st.copied) (void)hipEventDestroy(st.copied);
+            if (st.scanned) (void)hipEventDestroy(st.scanned);
+        }
+        for (void* p : allocs) (void)hipFree(p);
+    };
+    for (Set& st : sets) {
+        st.copied = st.scanned = nullptr;
+        st.v.assign(ncols, nullptr);
+        st.b.assign(ncols, nullptr);
+        st.o.assign(ncols, nullptr);
+    }
+    int rc = DQ_OK;
+    auto dalloc = [&](size_t bytes) -> void* {
+        void* p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
+        allocs.push_back(p);
+        return p;
+    };
+    for (Set& st : sets) {
+        for (int c = 0; c < ncols && rc == DQ_OK; ++c) {
+            if (!(st.v[c] = dalloc(vcap[c]))) rc = DQ_ERR_OUT_OF_MEMORY;
+            if (bcap[c] && !(st.b[c] = dalloc(bcap[c]))) rc = DQ_ERR_OUT_OF_MEMORY;
+            if (ocap[c] && !(st.o[c] = dalloc(ocap[c]))) rc = DQ_ERR_OUT_OF_MEMORY;
+        }
+        if (rc == DQ_OK && (hipEventCreateWithFlags(&st.copied, hipEventDisableTiming) != hipSuccess ||
+                            hipEventCreateWithFlags(&st.scanned, hipEventDisableTiming) != hipSuccess))
+            rc = DQ_ERR_DEVICE;
+    }
+    if (rc == DQ_OK && !(dstates = (dq_state*)dalloc(sizeof(dq_state) * (size_t)nops * nchunks))) rc = DQ_ERR_OUT_OF_MEMORY;
+    if (rc == DQ_OK && hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking) != hipSuccess) rc = DQ_ERR_DEVICE;
+    if (rc != DQ_OK) {
+        cleanup();
+        return fail(ctx, rc, "dq_scan_streamed: chunk buffers of %lld rows do not fit", (long long)chunk_rows);
+    }
+    auto issue_copy = [&](int64_t k) -> int {
+        Set& st = sets[k & 1];
+        const int64_t r0 = k * chunk_rows, n = std::min(nrows, r0 + chunk_rows) - r0;
+        for (int c = 0; c < ncols; ++c) {
+            const dq_column& col = columns[c];
+            if (col.spark_type == DQ_TYPE_STRING) {
+                std::vector<int32_t>& ro = rebased[(k & 1) * ncols + c];
+                ro.resize((size_t)n + 1);
+                const int32_t base = col.offsets[r0];
+                for (int64_t i = 0; i <= n; ++i) ro[i] = col.offsets[r0 + i] - base;
+                if (ro[n]) DQ_HIP(ctx, hipMemcpyAsync(st.v[c], (const uint8_t*)col.values + base, ro[n], hipMemcpyHostToDevice, cstream));
+                DQ_HIP(ctx, hipMemcpyAsync(st.o[c], ro.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, cstream));
+            } else {
+                const size_t es = elem_size(elem_of(col.spark_type));
+                DQ_HIP(ctx, hipMemcpyAsync(st.v[c], (const uint8_t*)col.values + r0 * es, (size_t)n * es,
+                                           hipMemcpyHostToDevice, cstream));
+            }
+            if (col.validity)
+                DQ_HIP(ctx, hipMemcpyAsync(st.b[c], col.validity + r0 / 8, (size_t)(n + 7) / 8, hipMemcpyHostToDevice, cstream));
+        }
+        DQ_HIP(ctx, hipEventRecord(st.copied, cstream));
+        return DQ_OK;
+    };
+    rc = issue_copy(0);
+    std::vector<dq_column> dcols(std::max(ncols, 1));
+    for (int64_t k = 0; k < nchunks && rc == DQ_OK; ++k) {
+        Set& st = sets[k & 1];
+        if (k + 1 < nchunks) {
+            // buffer set (k + 1) & 1 was read by chunk k - 1's scan: wait for it, then start the next copy
+            if (k >= 1 && hipEventSynchronize(sets[(k + 1) & 1].scanned) != hipSuccess) { rc = DQ_ERR_DEVICE; break; }
+            rc = issue_copy(k + 1);
+            if (rc) break;
+        }
+        if (hipStreamWaitEvent(ctx->stream, st.copied, 0) != hipSuccess) { rc = DQ_ERR_DEVICE; break; }
+        const int64_t r0 = k * chunk_rows, n = std::min(nrows, r0 + chunk_rows) - r0;
+        for (int c = 0; c < ncols; ++c) {
+            dcols[c] = columns[c];
+            dcols[c].flags |= DQ_COL_DEVICE;
+            dcols[c].length = n;
+            dcols[c].values = st.v[c];
+            dcols[c].validity = columns[c].validity ? (const uint8_t*)st.b[c] : nullptr;
+            dcols[c].offsets = columns[c].spark_type == DQ_TYPE_STRING ? (const int32_t*)st.o[c] : nullptr;
+        }
+        rc = dq_scan(ctx, dcols.data(), ncols, n, ops, nops, preds, npreds, dstates + (size_t)k * nops, DQ_SCAN_OUT_DEVICE);
+        if (rc) break;
+        if (hipEventRecord(st.scanned, ctx->stream) != hipSuccess) { rc = DQ_ERR_DEVICE; break; }
+    }
+    std::vector<dq_state> hst;
+    if (rc == DQ_OK) {
+        hst.resize((size_t)nops * nchunks);
+        if (hipMemcpyAsync(hst.data(), dstates, sizeof(dq_state) * hst.size(), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            rc = DQ_ERR_DEVICE;
+    }
+    const std::string err = ctx->err;
+    cleanup();
+    if (rc) return fail(ctx, rc, "%s", err.empty() ? "dq_scan_streamed failed" : err.c_str());
+    rc = dq_state_fold(hst.data(), (int)nchunks, nops, out);  // chunks in row order
+    if (rc) return fail(ctx, rc, "dq_scan_streamed: state fold failed");
+    return DQ_OK;
+}
+
 int dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out) {
     if (!a || !b || !out || a->kind != b->kind) return DQ_ERR_INVALID_ARGUMENT;
     // Analyzers.merge (A/Analyzer.scala:367-386): None is the identity.
@@ -911,11 +1053,23 @@ int dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out) {
             r.u.num_matches_and_count.count += b->u.num_matches_and_count.count;
             break;
         case DQ_OP_MEAN:
-            r.u.mean.sum = a->u.mean.sum + b->u.mean.sum;
             r.u.mean.count = a->u.mean.count + b->u.mean.count;
+            if (a->u.mean.exact && b->u.mean.exact) {  // Long partials: wrap-around add, one final cast
+                r.u.mean.isum = (int64_t)((uint64_t)a->u.mean.isum + (uint64_t)b->u.mean.isum);
+                r.u.mean.sum = (double)r.u.mean.isum;
+            } else {
+                r.u.mean.sum = a->u.mean.sum + b->u.mean.sum;
+                r.u.mean.exact = 0;
+            }
             break;
         case DQ_OP_SUM:
-            r.u.dbl.value = a->u.dbl.value + b->u.dbl.value;
+            if (a->u.dbl.exact && b->u.dbl.exact) {
+                r.u.dbl.isum = (int64_t)((uint64_t)a->u.dbl.isum + (uint64_t)b->u.dbl.isum);
+                r.u.dbl.value = (double)r.u.dbl.isum;
+            } else {
+                r.u.dbl.value = a->u.dbl.value + b->u.dbl.value;
+                r.u.dbl.exact = 0;
+            }
             break;
         case DQ_OP_MINIMUM:
         case DQ_OP_MIN_LENGTH:

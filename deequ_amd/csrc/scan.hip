@@ -1090,10 +1090,14 @@ __global__ void finalize_kernel(const OpMap* __restrict__ ops, int nops, const S
         case DQ_OP_MEAN:
             st->u.mean.sum = om.is_float ? c.dsum : (double)c.isum / scale;
             st->u.mean.count = c.n;
+            st->u.mean.isum = c.isum;
+            st->u.mean.exact = (!om.is_float && om.decimal_scale == 0) ? 1 : 0;
             present = c.n > 0;
             break;
         case DQ_OP_SUM:
             st->u.dbl.value = om.is_float ? c.dsum : (double)c.isum / scale;
+            st->u.dbl.isum = c.isum;
+            st->u.dbl.exact = (!om.is_float && om.decimal_scale == 0) ? 1 : 0;
             present = c.n > 0;
             break;
         case DQ_OP_MINIMUM:

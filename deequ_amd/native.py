@@ -50,6 +50,7 @@ EXPORTED_SYMBOLS = (
     "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
+    "dq_scan_streamed",
 )
 
 
@@ -83,11 +84,12 @@ class _NumMatchesAndCount(ctypes.Structure):
 
 
 class _Mean(ctypes.Structure):
-    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64)]
+    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64), ("isum", ctypes.c_int64), ("exact", ctypes.c_int32),
+                ("pad", ctypes.c_int32)]
 
 
 class _Dbl(ctypes.Structure):
-    _fields_ = [("value", ctypes.c_double)]
+    _fields_ = [("value", ctypes.c_double), ("isum", ctypes.c_int64), ("exact", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
 class _StdDev(ctypes.Structure):
@@ -190,6 +192,8 @@ def load_library(path=None):
             "dq_freq_merge": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
             "dq_freq_mutual_information": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
             "dq_open_devices": (c_void_p, [c_void_p, c_int, ctypes.POINTER(c_int)]),
+            "dq_scan_streamed": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                         c_int64]),
             "dq_ctx_num_devices": (c_int, [c_void_p]),
             "dq_ctx_uses_rccl": (c_int, [c_void_p]),
             "dq_scan_sharded": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
@@ -314,6 +318,17 @@ class Context:
         out = (DqState * max(len(ops), 1))()
         rc = self.lib.dq_scan(self.handle, col_arr, ncol, int(nrows), op_arr, len(ops), pred_arr, len(preds), out, 0)
         self.check(rc, "dq_scan")
+        return [out[i] for i in range(len(ops))]
+
+    def scan_streamed(self, columns, nrows, ops, preds, chunk_rows):
+        """dq_scan_streamed: host columns streamed through HBM in row chunks (copy / scan overlapped)."""
+        col_arr = (DqColumn * max(len(columns), 1))(*columns)
+        op_arr = (DqOp * max(len(ops), 1))(*ops)
+        pred_arr = (DqPredicate * max(len(preds), 1))(*preds)
+        out = (DqState * max(len(ops), 1))()
+        rc = self.lib.dq_scan_streamed(self.handle, col_arr, len(columns), int(nrows), op_arr, len(ops), pred_arr,
+                                       len(preds), out, int(chunk_rows))
+        self.check(rc, "dq_scan_streamed")
         return [out[i] for i in range(len(ops))]
 
     def quantile_summary(self, column, nrows, relative_error):

@@ -3,6 +3,7 @@
 driving the MI355X engine. The scan-shareable analyzers of a run become ONE dq_scan call (one fused
 pass over HBM), exactly where the reference issues one `data.agg(...)` Spark job."""
 import json
+import os
 
 from . import native as N
 from . import engine
@@ -10,6 +11,13 @@ from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanS
                         FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies)
 from .expr import compile_predicate
 from .metrics import DoubleMetric, Success, UnsupportedOnDevice
+
+
+def stream_chunk_rows():
+    """DQ_STREAM_CHUNK_ROWS: host-resident tables larger than this many rows are scanned in streamed chunks
+    (copy of the next chunk overlapped with the scan of the current one) instead of being staged whole."""
+    v = os.environ.get("DQ_STREAM_CHUNK_ROWS")
+    return int(float(v)) if v else 0
 
 
 class ScanResult(list):
@@ -95,8 +103,15 @@ class ScanBatch:
     def run(self, out_device_ptr=None):
         res = ScanResult()
         if self.ops:
-            got = engine.ctx().scan(self.native_columns(), self.data.nrows, self.ops,
-                                    [p.to_native() for p in self.preds], out_device_ptr=out_device_ptr)
+            chunk = stream_chunk_rows()
+            host = all(self.data[n].device is None for n in self.names)
+            if chunk and host and out_device_ptr is None and self.data.nrows > chunk:
+                # host-resident table streamed through HBM in row chunks (dq_scan_streamed)
+                got = engine.ctx().scan_streamed(self.native_columns(), self.data.nrows, self.ops,
+                                                 [p.to_native() for p in self.preds], chunk)
+            else:
+                got = engine.ctx().scan(self.native_columns(), self.data.nrows, self.ops,
+                                        [p.to_native() for p in self.preds], out_device_ptr=out_device_ptr)
             if got is not None:
                 res.extend(got)
         if self.quantile_reqs:

@@ -62,13 +62,28 @@ class NumMatchesAndCount(DoubleValuedState):
         return "NumMatchesAndCount(%d,%d)" % (self.numMatches, self.count)
 
 
+def _long_add(a, b):
+    """Spark sums an integral column in a Long (wrapping on overflow) and casts the final total to Double
+    (A/Sum.scala:34-37, A/Mean.scala:37-42): partial states of one table split into chunks or shards carry that
+    exact Long, so their merge is the Long sum re-cast, not a sum of rounded doubles. States without it (other
+    column types, loaded from a state provider) merge as the reference's doubles."""
+    ea, eb = getattr(a, "exact", None), getattr(b, "exact", None)
+    if ea is None or eb is None:
+        return None
+    return (ea + eb + (1 << 63)) % (1 << 64) - (1 << 63)
+
+
 class MeanState(DoubleValuedState):
     """A/Mean.scala:25-34."""
 
-    def __init__(self, sum_, count):
+    def __init__(self, sum_, count, exact=None):
         self.sum_, self.count = float(sum_), int(count)
+        self.exact = exact  # the exact Long partial of an integral column (see _long_add), else None
 
     def sum(self, other):
+        e = _long_add(self, other)
+        if e is not None:
+            return MeanState(float(e), self.count + other.count, e)
         return MeanState(self.sum_ + other.sum_, self.count + other.count)
 
     def metricValue(self):
@@ -86,10 +101,14 @@ class MeanState(DoubleValuedState):
 class SumState(DoubleValuedState):
     """A/Sum.scala:25-33."""
 
-    def __init__(self, sum_):
+    def __init__(self, sum_, exact=None):
         self.sum_ = float(sum_)
+        self.exact = exact
 
     def sum(self, other):
+        e = _long_add(self, other)
+        if e is not None:
+            return SumState(float(e), e)
         return SumState(self.sum_ + other.sum_)
 
     def metricValue(self):
@@ -365,8 +384,12 @@ def state_to_native(kind, state):
         u.num_matches_and_count.count = state.count
     elif isinstance(state, MeanState):
         u.mean.sum, u.mean.count = state.sum_, state.count
+        if getattr(state, "exact", None) is not None:
+            u.mean.isum, u.mean.exact = state.exact, 1
     elif isinstance(state, SumState):
         u.dbl.value = state.sum_
+        if getattr(state, "exact", None) is not None:
+            u.dbl.isum, u.dbl.exact = state.exact, 1
     elif isinstance(state, MinState):
         u.dbl.value = state.minValue
     elif isinstance(state, MaxState):
@@ -398,9 +421,9 @@ def state_from_native(st):
     if k in (N.OP_COMPLETENESS, N.OP_COMPLIANCE):
         return NumMatchesAndCount(u.num_matches_and_count.num_matches, u.num_matches_and_count.count)
     if k == N.OP_MEAN:
-        return MeanState(u.mean.sum, u.mean.count)
+        return MeanState(u.mean.sum, u.mean.count, u.mean.isum if u.mean.exact else None)
     if k == N.OP_SUM:
-        return SumState(u.dbl.value)
+        return SumState(u.dbl.value, u.dbl.isum if u.dbl.exact else None)
     if k in (N.OP_MINIMUM, N.OP_MIN_LENGTH):
         return MinState(u.dbl.value)
     if k in (N.OP_MAXIMUM, N.OP_MAX_LENGTH):

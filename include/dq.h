@@ -158,8 +158,12 @@ typedef struct dq_state {
     union {
         struct { int64_t num_matches; } num_matches;                        /* NumMatches          */
         struct { int64_t num_matches; int64_t count; } num_matches_and_count;/* NumMatchesAndCount  */
-        struct { double sum; int64_t count; } mean;                         /* MeanState           */
-        struct { double value; } dbl;                                       /* Sum/Min/Max State   */
+        /* MeanState / SumState. For integral (non-decimal) columns Spark sums in a Long that wraps around and
+         * casts the FINAL sum to Double (A/Sum.scala:34-37): `isum` keeps that exact Long partial and
+         * `exact` = 1 so merges of shards / chunks (dq_state_merge, dq_state_fold) add the Longs and re-cast,
+         * rather than adding rounded doubles. `sum` / `value` is always (double)isum then. */
+        struct { double sum; int64_t count; int64_t isum; int32_t exact; int32_t pad; } mean;
+        struct { double value; int64_t isum; int32_t exact; int32_t pad; } dbl;  /* Sum/Min/Max State */
         struct { double n, avg, m2; } stddev;                               /* StandardDeviationState */
         struct { double n, x_avg, y_avg, ck, x_mk, y_mk; } corr;            /* CorrelationState    */
         struct { int64_t words[DQ_HLL_NUM_WORDS]; } hll;                    /* ApproxCountDistinctState */
@@ -229,6 +233,13 @@ int dq_synchronize(dq_ctx* ctx);
 int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows,
             const dq_op* ops, int nops, const dq_predicate* preds, int npreds,
             dq_state* out, uint32_t flags);
+
+/* dq_scan over host columns streamed through HBM in chunks of chunk_rows rows (rounded to 2048): the copy of the
+ * next chunk (its own stream, double-buffered device chunks) overlaps the scan of the current one, and the chunks'
+ * states are folded in row order with the reference merges — for tables larger than HBM and host-resident batches
+ * (end-to-end rate bound by the host link). Host columns only; `out` is host memory. */
+int dq_scan_streamed(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const dq_op* ops, int nops,
+                     const dq_predicate* preds, int npreds, dq_state* out, int64_t chunk_rows);
 
 /* Number of fused-scan kernel launches issued so far (the analogue of the SparkMonitor job count
  * asserted in T/analyzers/runners/AnalysisRunnerTests.scala:50-74). */

@@ -247,3 +247,19 @@ def test_synthetic_generators_match_oracle_bitwise():
     ctx.synchronize()
     from deequ_amd.table import unpack_validity
     assert np.array_equal(unpack_validity(vb.cpu().numpy(), n), O.synth_validity(0x5EED0100, 0, n, 10))
+
+
+@pytest.mark.parametrize("chunk", [2048, 65536])
+def test_streamed_host_scan_equals_staged_scan(chunk):
+    """dq_scan_streamed: host columns copied through HBM in row chunks (copy of chunk i + 1 overlapping the scan of
+    chunk i), chunk states folded in row order: the same states as one staged scan (exact for counts, Long sums,
+    min / max, HLL registers; fp sums / moments within 1e-12 of the exact oracle)."""
+    rng = np.random.default_rng(chunk)
+    t = random_table(rng, 250_001, with_nan=True)
+    analyzers = all_analyzers(t, "k < 30")
+    batch = D.ScanBatch(t)
+    offsets = [a.addOps(batch) for a in analyzers]
+    got = D.runners.ScanResult(engine.ctx().scan_streamed(batch.native_columns(), t.nrows, batch.ops,
+                                                          [p.to_native() for p in batch.preds], chunk))
+    for a, ops in zip(analyzers, offsets):
+        assert_state_parity(t, a, a.fromAggregationResult(got, ops))

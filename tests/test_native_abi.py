@@ -113,3 +113,26 @@ def test_state_merge_follows_reference_semigroups():
     assert N.merge_states(empty, mn).u.dbl.value == 3.0
     nan = _st(N.OP_MAXIMUM, dbl__value=float("nan"))
     assert np.isnan(N.merge_states(nan, _st(N.OP_MAXIMUM, dbl__value=1.0)).u.dbl.value)
+
+
+def test_integral_sum_partials_merge_as_wrapped_long():
+    """Chunks / shards of one integral column merge their exact Long partials (Spark: Long sum that wraps,
+    cast once to Double, A/Sum.scala:34-37), natively and in the host states; a rounded-double merge differs."""
+    from deequ_amd.states import MeanState, SumState, state_from_native, state_to_native
+    big, small = (1 << 63) - 7, 1 << 60
+    wrapped = (big + small + (1 << 63)) % (1 << 64) - (1 << 63)
+    a = _st(N.OP_MEAN, mean__sum=float(big), mean__count=2, mean__isum=big, mean__exact=1)
+    b = _st(N.OP_MEAN, mean__sum=float(small), mean__count=3, mean__isum=small, mean__exact=1)
+    m = N.merge_states(a, b)
+    assert (m.u.mean.isum, m.u.mean.exact, m.u.mean.sum, m.u.mean.count) == (wrapped, 1, float(wrapped), 5)
+    s = N.merge_states(_st(N.OP_SUM, dbl__value=float(big), dbl__isum=big, dbl__exact=1),
+                       _st(N.OP_SUM, dbl__value=float(small), dbl__isum=small, dbl__exact=1))
+    assert s.u.dbl.value == float(wrapped)
+    # one side without the exact partial (e.g. a persisted state): the reference's double merge
+    s = N.merge_states(_st(N.OP_SUM, dbl__value=1.5), _st(N.OP_SUM, dbl__value=2.0, dbl__isum=2, dbl__exact=1))
+    assert (s.u.dbl.value, s.u.dbl.exact) == (3.5, 0)
+    hm = MeanState(float(big), 2, big).sum(MeanState(float(small), 3, small))
+    assert (hm.sum_, hm.count, hm.exact) == (float(wrapped), 5, wrapped)
+    assert SumState(1.0, 1).sum(SumState(2.5)) == SumState(3.5)
+    back = state_from_native(state_to_native(N.OP_MEAN, hm))
+    assert back.exact == wrapped and back == hm
