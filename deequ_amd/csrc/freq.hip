@@ -1002,6 +1002,14 @@ mi_kernel(const Slot* __restrict__ slots, const unsigned long long* __restrict__
     if (threadIdx.x == 0) out[blockIdx.x] = red[0];
 }
 
+// Per source row: the count of its group in T (0 when it takes no part) — the join of the rows with their
+// frequencies. The rows are the table's own source rows, so the build's verification covers the fingerprints.
+__global__ void __launch_bounds__(kFreqBlock)
+row_counts_kernel(LookupTable T, int64_t nrows, long long* __restrict__ out) {
+    const int64_t stride = (int64_t)gridDim.x * kFreqBlock;
+    for (int64_t r = (int64_t)blockIdx.x * kFreqBlock + threadIdx.x; r < nrows; r += stride)
+        out[r] = (long long)lookup_count(T, r);
+}
 
 }  // namespace
 
@@ -1035,6 +1043,7 @@ struct dq_freq_table {
     double pre_ent = 0.0, pre_comp = 0.0;
     int32_t key_type = 0;   // Spark type of the (single) key column, or of the canonical keys of a pair-built table
     int64_t num_rows_override = -1;  // tables built from (key, count) pairs carry the caller's numRows
+    int64_t src_rows = -1;  // rows of the source columns (dq_frequencies_ex), -1 for pair-built / merged tables
     int64_t cached_n = -1;  // dq_freq_summarize memo (the table is immutable once built)
     dq_freq_summary cached;
     void* scratch = nullptr;  // device scratch for scans
@@ -1646,6 +1655,7 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
     hipStream_t s = dq::ctx_stream(ctx);
     dq_freq_table* t = new dq_freq_table();
     t->device = dev;
+    t->src_rows = nrows;
     memset(&t->ks, 0, sizeof(t->ks));
     std::vector<void*> staged;
     auto cleanup = [&]() {
@@ -2094,6 +2104,32 @@ int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq
     }
     *mi = sum;
     *present = groups > 0 ? 1 : 0;  // sum over zero joined rows is NULL (A/MutualInformation.scala:82-86)
+    return DQ_OK;
+}
+
+int dq_freq_row_counts(dq_ctx* ctx, const dq_freq_table* t, int64_t* counts, int64_t nrows, uint32_t flags) {
+    if (!ctx || !t || (!counts && nrows > 0))
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_row_counts: invalid arguments");
+    if (!t->parts.empty() || t->src_rows < 0 || !t->slots)
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_freq_row_counts: needs a single-device table built over rows");
+    if (nrows != t->src_rows)
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_row_counts: nrows differs from the table's source rows");
+    if (nrows == 0) return DQ_OK;
+    FQ_HIP(ctx, hipSetDevice(t->device));
+    hipStream_t s = dq::ctx_stream(ctx);
+    LookupTable T;
+    T.slots = t->slots;
+    T.ks = t->ks;
+    T.sentinel = t->host_ctr.sentinel;
+    T.bits = t->bits;
+    DevBuf buf;
+    long long* d = reinterpret_cast<long long*>(counts);
+    const bool dev_out = (flags & DQ_FREQ_PAIRS_DEVICE) != 0;
+    if (!dev_out) FQ_HIP(ctx, buf.alloc((void**)&d, (size_t)nrows * 8));
+    hipLaunchKernelGGL(row_counts_kernel, dim3(scan_grid((uint64_t)nrows)), dim3(kFreqBlock), 0, s, T, nrows, d);
+    FQ_HIP(ctx, hipGetLastError());
+    if (!dev_out) FQ_HIP(ctx, hipMemcpyAsync(counts, d, (size_t)nrows * 8, hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
     return DQ_OK;
 }
 

@@ -6,11 +6,15 @@ records of all ranks are all-gathered in ONE collective, and every rank folds th
 with the reference semigroup merges (dq_state_merge = State.sum, e.g. A/StandardDeviation.scala:37-44)
 — deterministic and identical on every rank; a plain all-reduce cannot express the Chan merge.
 
-Grouping analyzers (one fixed-width key column): every rank buckets the canonical keys of its
-non-NULL rows by owner rank (dq_partition_keys), the buckets travel in one all-to-all, and each
-owner builds the frequency table of the keys it owns, so group sets are disjoint across ranks. The
-global numRows is an all-reduce; #groups / #unique are sums; entropy terms use the global numRows and
-their per-rank sums are folded in rank order (A/GroupingAnalyzers.scala:53-79, R/AnalysisRunner.scala:480-548).
+Grouping analyzers (any key columns: fixed-width, strings, several columns): every rank builds the frequency
+table of its shard (the partition-local pre-aggregation of Spark's groupBy), exports its groups as a GroupBlock
+(key columns at the groups' representative rows + counts, deequ_amd/groups.py) and sends each group to the owner
+rank picked by a hash of its key, in one all-to-all. Each owner rebuilds one table over what it received, weighted
+by the counts, so duplicates across ranks merge and group sets are disjoint across ranks. The global numRows is an
+all-reduce; #groups / #unique are sums; entropy terms use the global numRows and their per-rank sums are folded in
+rank order (A/GroupingAnalyzers.scala:53-79, R/AnalysisRunner.scala:480-548). MutualInformation runs the joint
+groups through two owners: by hash(x), where every x's marginal px is complete, then by hash(y), where py is, and
+sums the terms (A/MutualInformation.scala:35-97).
 
 The per-rank compute is behind `GpuLocal` (libdq.so); the collective choreography is shared with the
 CPU test double in tests/test_distributed_gloo.py.
@@ -22,8 +26,12 @@ import numpy as np
 
 from . import native as N
 from . import engine
+from . import groups as G
 from .analyzers import (ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer, Histogram,
-                        FrequenciesAndNumRows, Preconditions, metricFromFailure)
+                        MutualInformation, FrequenciesAndNumRows, Preconditions, metricFromFailure, metricFromValue,
+                        metricFromEmpty)
+from .metrics import Entity
+from .table import Column
 from .metrics import (HistogramMetric, Distribution, DistributionValue, Success, Failure, wrap_if_necessary,
                       MetricCalculationRuntimeException, UnsupportedOnDevice)
 from .runners import AnalyzerContext, ScanBatch, ScanResult
@@ -90,36 +98,23 @@ class Exchange:
         self.dist.all_gather_into_tensor(out, t, group=self.group)
         return out.cpu().tolist()
 
-    def all_to_all_keys(self, keys, send_counts):
-        """keys: int64 tensor bucketed by destination rank; returns the keys this rank owns."""
+    def all_to_all_blobs(self, blobs):
+        """blobs[r] goes to rank r; returns the blobs every rank sent to this one, in rank order."""
         torch = self.torch
-        sc = torch.tensor(send_counts, dtype=torch.int64, device=self.device)
+        sizes = [len(b) for b in blobs]
+        sc = torch.tensor(sizes, dtype=torch.int64, device=self.device)
         rc = torch.empty_like(sc)
         self.dist.all_to_all_single(rc, sc, group=self.group)
-        recv_counts = [int(v) for v in rc.cpu().tolist()]
-        out = torch.empty(sum(recv_counts), dtype=torch.int64, device=self.device)
-        self.dist.all_to_all_single(out, keys.to(self.device), output_split_sizes=recv_counts,
-                                    input_split_sizes=list(send_counts), group=self.group)
-        return out
-
-    def all_gather_pairs(self, keys, counts, k):
-        """Top-k candidates of every rank -> list of (key, count)."""
-        torch = self.torch
-        pad = torch.full((k,), -1, dtype=torch.int64)
-        kk, cc = pad.clone(), pad.clone()
-        n = len(keys)
-        kk[:n] = torch.tensor(list(keys), dtype=torch.int64) if n else kk[:0]
-        cc[:n] = torch.tensor(list(counts), dtype=torch.int64) if n else cc[:0]
-        both = torch.cat([kk, cc]).to(self.device)
-        out = torch.empty(self.world * 2 * k, dtype=torch.int64, device=self.device)
-        self.dist.all_gather_into_tensor(out, both, group=self.group)
-        arr = out.cpu().numpy().reshape(self.world, 2, k)
-        pairs = []
-        for r in range(self.world):
-            for i in range(k):
-                if arr[r, 1, i] >= 0:
-                    pairs.append((int(arr[r, 0, i]), int(arr[r, 1, i])))
-        return pairs
+        recv = [int(v) for v in rc.cpu().tolist()]
+        send = torch.frombuffer(bytearray(b"".join(blobs) or b"\0"), dtype=torch.uint8)[:sum(sizes)].to(self.device)
+        out = torch.empty(sum(recv), dtype=torch.uint8, device=self.device)
+        self.dist.all_to_all_single(out, send, output_split_sizes=recv, input_split_sizes=sizes, group=self.group)
+        raw = out.cpu().numpy().tobytes()
+        res, at = [], 0
+        for n in recv:
+            res.append(raw[at:at + n])
+            at += n
+        return res
 
 
 class GpuLocal:
@@ -141,54 +136,81 @@ class GpuLocal:
         from .runners import KLLRunner
         return KLLRunner.sketch_column(shard, column, sketch_size, shrinking_factor).toBytes()
 
-    def partition(self, column, world):
-        import torch
-        ctx = engine.ctx()
-        keys = torch.empty(max(column.length, 1), dtype=torch.int64, device="cuda")
-        counts = (ctypes.c_int64 * world)()
-        nulls = ctypes.c_int64(0)
-        rc = ctx.lib.dq_partition_keys(ctx.handle, ctypes.byref(column.native()), column.length, world,
-                                       ctypes.c_void_p(keys.data_ptr()), counts, ctypes.byref(nulls))
-        ctx.check(rc, "dq_partition_keys")
-        send = [int(counts[i]) for i in range(world)]
-        return keys[:sum(send)], send, int(nulls.value)
+    def group_block(self, shard, cols, include_nulls):
+        """This shard's groups over `cols` (dq_frequencies on the GPU), as a host GroupBlock."""
+        ft = engine.frequencies(shard, cols, include_nulls)
+        keys, counts = ft.export_raw()
+        s = ft.summary(None)
+        if ft.key_kind() == N.FREQ_KEYS_VALUES:
+            c = shard[cols[0]]
+            columns = [G.column_from_canonical(c.name, c.spark_type, keys, c.decimal_precision, c.decimal_scale)]
+        else:
+            columns = [G.take(_host_column(shard[c]), keys) for c in cols]
+        return G.GroupBlock(columns, counts, s["num_rows"], s["null_count"])
 
-    def frequencies_of_keys(self, keys):
-        """Local table over owned canonical keys (grouping on their 64-bit patterns)."""
-        from .table import Table, Column
-        col = Column("k", N.TYPE_LONG, None, None, length=int(keys.numel()))
-        col.device = {"values": keys.to("cuda").contiguous()}
-        return engine.frequencies(Table([col]), ["k"])
+    def owned_table(self, block, include_nulls):
+        """The owner's table over the groups it received, weighted by their counts (dq_frequencies_ex)."""
+        return engine.frequencies(block.table(), block.names, include_nulls, weights=block.counts)
+
+    def table_summary(self, table, n):
+        return table.summary(n)
+
+    def top_block(self, table, block, k):
+        keys, counts = table.top_raw(k)
+        return self._block_of(table, block, keys, counts)
+
+    def merged_block(self, table, block):
+        keys, counts = table.export_raw()
+        return self._block_of(table, block, keys, counts)
+
+    def row_counts(self, block, cols):
+        """Per group of `block`: the total count of the groups sharing its `cols` key (0 when that key is NULL)."""
+        return engine.frequencies(block.table(), cols, False, weights=block.counts).row_counts()
+
+    def cast_column(self, shard, name, to_type):
+        from .profiles import _cast_column
+        return _cast_column(shard, name, to_type)
+
+    @staticmethod
+    def _block_of(table, block, keys, counts):
+        if table.key_kind() == N.FREQ_KEYS_VALUES:
+            c = block.columns[0]
+            return G.GroupBlock([G.column_from_canonical(c.name, c.spark_type, keys, c.decimal_precision,
+                                                         c.decimal_scale)], counts)
+        sub = block.subset(keys)
+        return G.GroupBlock(sub.columns, counts)
 
 
-def _decode_canonical(spark_type, decimal_scale, k):
-    u = np.uint64(k & 0xFFFFFFFFFFFFFFFF)
-    if spark_type == N.TYPE_DOUBLE:
-        return engine.GroupFloat(u.view(np.float64))
-    if spark_type == N.TYPE_FLOAT:
-        return engine.GroupFloat(np.uint32(int(u) & 0xFFFFFFFF).view(np.float32))
-    i = int(u.view(np.int64))
-    if spark_type == N.TYPE_BOOLEAN:
-        return bool(i)
-    if spark_type == N.TYPE_DECIMAL:
-        from decimal import Decimal
-        return Decimal(i).scaleb(-decimal_scale)
-    return i
+def _host_column(col):
+    """A column's host buffers (device-only columns are copied back)."""
+    if col.values is not None or col.device is None:
+        return col
+    from .table import Column
+    d = col.device
+    vals = d["values"].cpu().numpy()
+    if col.spark_type != N.TYPE_STRING:
+        from .table import NUMPY_OF
+        vals = vals.view(NUMPY_OF[col.spark_type])[:col.length]
+    validity = d["validity"].cpu().numpy() if d.get("validity") is not None else None
+    offsets = d["offsets"].cpu().numpy() if d.get("offsets") is not None else None
+    return Column(col.name, col.spark_type, vals, validity, offsets, col.decimal_precision, col.decimal_scale,
+                  length=col.length)
 
 
 class DistributedFrequencies:
-    """Global view of a hash-partitioned frequency table (the grouping state across ranks)."""
+    """Global view of a grouping whose groups are spread over the ranks by owner (disjoint key sets)."""
 
-    def __init__(self, exchange, local_table, column, num_rows, null_rows):
-        self.ex, self.local, self.column = exchange, local_table, column
-        self.num_rows = num_rows  # global
-        self.null_rows = null_rows  # global NULL rows (Histogram)
+    def __init__(self, runner, table, owned, column, num_rows, null_rows):
+        self.runner, self.ex, self.local = runner, runner.ex, runner.local
+        self.table, self.owned, self.schema, self.column = table, owned, owned.schema(), column
+        self.num_rows = num_rows  # global rows taking part (excluding Histogram's all-NULL rows)
+        self.null_rows = null_rows  # global all-NULL rows (Histogram's NULL group)
         self._summary = {}
 
     def summary(self, n=None):
         n = self.num_rows if n is None else n
         if n not in self._summary:
-            s = self.local.summary(n)
+            s = self.runner._local_step(lambda: self.local.table_summary(self.table, n))
             groups, unique = self.ex.all_reduce_i64([s["num_groups"], s["num_unique"]])
             ent = kahan_fold(self.ex.all_gather_f64(s["entropy"]))
             self._summary[n] = {"num_rows": self.num_rows, "num_groups": groups, "num_unique": unique,
@@ -200,19 +222,16 @@ class DistributedFrequencies:
         return self.summary()["num_groups"] + (1 if self.null_rows else 0)
 
     def top(self, k):
-        loc = self.local.top(k)
-        keys = [int(np.int64(np.uint64(_canonical_key(key[0], self.column)))) for key, c in loc]
-        pairs = self.ex.all_gather_pairs(keys, [c for _, c in loc], k)
-        out = [((_decode_canonical(self.column.spark_type, self.column.decimal_scale, kk),), c) for kk, c in pairs]
+        """The k largest groups over all ranks: each owner's top k, all-gathered and merged."""
+        blob = self.runner._local_step(lambda: G.pack(self.local.top_block(self.table, self.owned, k)))
+        cands = []
+        for b in self.ex.all_gather_blobs(blob):
+            blk = G.unpack(b, self.schema)
+            cands += list(zip(blk.keys(), blk.counts.tolist()))
         if self.null_rows:
-            out.append(((None,), self.null_rows))
-        out.sort(key=lambda kv: -kv[1])
-        return out[:k]
-
-
-def _canonical_key(v, column):
-    """Inverse of the local table's decode (it grouped canonical bits as LONG)."""
-    return int(v) & 0xFFFFFFFFFFFFFFFF
+            cands.append(((None,) * len(self.schema), self.null_rows))
+        cands.sort(key=lambda kv: -kv[1])
+        return cands[:k]
 
 
 class DistributedAnalysisRunner:
@@ -301,12 +320,19 @@ class DistributedAnalysisRunner:
                 results[a] = a.toFailureMetric(UnsupportedOnDevice(
                     "Histogram with a binningUdf is not supported by the multi-GPU runner"))
                 continue
-            if isinstance(a, (GroupingAnalyzer, Histogram)):
-                cols = tuple(a.groupingColumns()) if isinstance(a, GroupingAnalyzer) else (a.column,)
-                by_cols.setdefault(cols, []).append(a)
-        for cols, group in by_cols.items():
+            if isinstance(a, MutualInformation):
+                try:
+                    results[a] = self._mutual_information(shard, a)
+                except Exception as e:
+                    results[a] = a.toFailureMetric(wrap_if_necessary(e))
+                continue
+            if isinstance(a, Histogram):
+                by_cols.setdefault(((a.column,), True), []).append(a)
+            elif isinstance(a, GroupingAnalyzer):
+                by_cols.setdefault((tuple(a.groupingColumns()), False), []).append(a)
+        for (cols, include_nulls), group in by_cols.items():
             try:
-                freq = self._frequencies(shard, list(cols))
+                freq = self._frequencies(shard, list(cols), include_nulls)
             except Exception as e:
                 for a in group:
                     results[a] = a.toFailureMetric(wrap_if_necessary(e))
@@ -314,6 +340,72 @@ class DistributedAnalysisRunner:
             for a in group:
                 results[a] = self._grouping_metric(a, freq)
         return AnalyzerContext(results)
+
+    def _local_step(self, fn):
+        """Run one piece of per-rank compute, then agree on it: every rank returns its result, or every rank
+        raises the first failing rank's error."""
+        out, err = None, None
+        try:
+            out = fn()
+        except Exception as e:
+            err = e
+        agreed = self._agree(err)
+        if agreed is not None:
+            raise agreed
+        return out
+
+    def _shuffle(self, block, key_columns=None, null_is_value=False):
+        """Every group of this rank's `block` to its owner rank (hash of its key, or of `key_columns`): the groups
+        this rank owns, from every rank, as one block."""
+        world = self.ex.world
+
+        def split():
+            dest = G.owners(block, world, null_is_value, key_columns)
+            return [G.pack(block, np.nonzero(dest == r)[0]) for r in range(world)]
+        blobs = self._local_step(split)
+        received = self.ex.all_to_all_blobs(blobs)
+        schema = block.schema()
+        return self._local_step(lambda: G.concat([G.unpack(b, schema) for b in received], schema))
+
+    def _frequencies(self, shard, cols, include_nulls=False):
+        block = self._local_step(lambda: self.local.group_block(shard, cols, include_nulls))
+        owned = self._shuffle(block, null_is_value=include_nulls)
+        table = self._local_step(lambda: self.local.owned_table(owned, include_nulls))
+        num_rows, null_rows = self.ex.all_reduce_i64([int(owned.counts.sum()), block.null_rows])
+        return DistributedFrequencies(self, table, owned, shard[cols[0]], num_rows, null_rows)
+
+    def _mutual_information(self, shard, a):
+        """MutualInformation over row shards (A/MutualInformation.scala:35-97): the joint (x, y) groups go to their
+        owner by hash(x), which merges them (pxy) and sees every group of each of its x values (px); then to their
+        owner by hash(y) (py); every rank sums its terms and the per-rank sums are folded in rank order."""
+        x, y = a.columns
+        joint = self._local_step(lambda: self.local.group_block(shard, [x, y], False))
+        by_x = self._shuffle(joint, key_columns=[x])
+
+        def merge_x():
+            table = self.local.owned_table(by_x, False)
+            merged = self.local.merged_block(table, by_x)
+            px = self.local.row_counts(merged, [x])
+            return merged.with_column(Column("__deequ_px", N.TYPE_LONG, np.ascontiguousarray(px, dtype=np.int64)))
+        merged = self._local_step(merge_x)
+        by_y = self._shuffle(merged, key_columns=[y])
+
+        def terms():
+            py = self.local.row_counts(by_y, [y]).astype(np.float64)
+            both = ~by_y.column(x).null_mask() & ~by_y.column(y).null_mask()
+            pxy = by_y.counts[both].astype(np.float64)
+            px = np.asarray(by_y.column("__deequ_px").values)[both].astype(np.float64)
+            return pxy, px, py[both]
+        pxy, px, py = self._local_step(terms)
+        total, nterms = self.ex.all_reduce_i64([int(merged.counts.sum()), len(pxy)])
+        inst = ",".join(a.columns)
+        if nterms == 0:
+            return metricFromEmpty(a, "MutualInformation", inst, Entity.Mutlicolumn)
+        n = float(total)
+        # the reference's miUdf, term by term: (pxy / total) * log((pxy / total) / ((px / total) * (py / total)))
+        t = (pxy / n) * np.log((pxy / n) / ((px / n) * (py / n)))
+        value = math.fsum(self.ex.all_gather_f64(math.fsum(t.tolist())))
+        return metricFromValue(value, "MutualInformation", inst, Entity.Mutlicolumn)
 
     def _kll_metrics(self, shard, analyzers, results):
         """KLLRunner.computeKLLSketchesInExtraPass (R/KLLRunner.scala:91-116) over row shards: each rank
@@ -348,30 +440,29 @@ class DistributedAnalysisRunner:
             st = merged[a.column]
             results[a] = a.toFailureMetric(st) if isinstance(st, Exception) else a.calculateMetric(st)
 
-    def _frequencies(self, shard, cols):
-        if len(cols) != 1 or shard[cols[0]].spark_type == N.TYPE_STRING:
-            raise UnsupportedOnDevice(
-                "multi-GPU grouping supports one fixed-width key column (strings / multi-column: single GPU)")
-        column = shard[cols[0]]
-        local_err = None
-        try:
-            keys, send, nulls = self.local.partition(column, self.ex.world)
-        except Exception as e:
-            local_err = e
-        agreed = self._agree(local_err)
-        if agreed is not None:
-            raise agreed
-        owned = self.ex.all_to_all_keys(keys, send)
-        local_err, local_table = None, None
-        try:
-            local_table = self.local.frequencies_of_keys(owned)
-        except Exception as e:
-            local_err = e
-        agreed = self._agree(local_err)
-        if agreed is not None:
-            raise agreed
-        taking, nulls_g = self.ex.all_reduce_i64([int(local_table.num_rows), nulls])
-        return DistributedFrequencies(self.ex, local_table, column, taking, nulls_g)
+    def profile(self, shard, restrictToColumns=None, lowCardinalityHistogramThreshold=None, kllParameters=None,
+                predefinedTypes=None):
+        """ColumnProfiler.profile (M/profiles/ColumnProfiler.scala:91-208) over row shards: the same three passes,
+        each through this runner — the generic and numeric statistics as sharded scans (+ KLL), the low-cardinality
+        histograms as owner-sharded groupings (computeHistograms, :564-606). Every rank returns the same profiles."""
+        from .profiles import ColumnProfiler
+        thr = ColumnProfiler.DEFAULT_CARDINALITY_THRESHOLD if lowCardinalityHistogramThreshold is None \
+            else lowCardinalityHistogramThreshold
+        return ColumnProfiler.profile(shard, restrictToColumns, False, thr, kllParameters, predefinedTypes,
+                                      passes=ShardedProfilerPasses(self))
+
+    def _profile_histograms(self, shard, targets):
+        from .analyzers import _hist_key
+        out = {}
+        for name in targets:
+            freq = self._frequencies(shard, [name], include_nulls=True)
+            total = freq.num_rows + freq.null_rows
+            values = {}
+            for key, c in freq.top(freq.num_groups):
+                k = Histogram.NullFieldReplacement if key[0] is None else _hist_key(key[0], shard[name])
+                values[k] = DistributionValue(int(c), c / total)
+            out[name] = Distribution(values, len(values))
+        return out
 
     def _grouping_metric(self, a, freq):
         if isinstance(a, Histogram):
@@ -390,3 +481,20 @@ class DistributedAnalysisRunner:
             return a.computeMetricFrom(state)
         return a.toFailureMetric(MetricCalculationRuntimeException(
             "%s is not supported by the multi-GPU runner" % type(a).__name__))
+
+
+class ShardedProfilerPasses:
+    """The ColumnProfiler's passes over this rank's row shard (see DistributedAnalysisRunner.profile)."""
+
+    def __init__(self, runner):
+        self.runner = runner
+
+    def run(self, data, analyzers):
+        return self.runner.run(data, analyzers)
+
+    def cast(self, data, name, to_type):
+        # per-row casts need no exchange; a failure still has to be agreed on before the next collective
+        return self.runner._local_step(lambda: self.runner.local.cast_column(data, name, to_type))
+
+    def histograms(self, data, targets):
+        return self.runner._profile_histograms(data, targets)

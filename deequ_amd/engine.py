@@ -168,6 +168,35 @@ class FrequencyTable:
         self.ctx.check(rc, "dq_freq_mutual_information")
         return mi.value, bool(present.value)
 
+    def export_raw(self):
+        """Every group as (key, count) int64 arrays: the canonical value (DQ_FREQ_KEYS_VALUES) or the smallest row
+        index of the group in the source (DQ_FREQ_KEYS_ROWS); the NULL group of an include_nulls table excluded."""
+        n = self.num_groups
+        keys = np.zeros(max(n, 1), dtype=np.int64)
+        counts = np.zeros(max(n, 1), dtype=np.int64)
+        got = self.ctx.lib.dq_freq_export(self.ctx.handle, self.handle, n, keys.ctypes.data, counts.ctypes.data)
+        if got < 0:
+            raise N.NativeError(int(got), "dq_freq_export: %s" % self.ctx.last_error())
+        return keys[:got], counts[:got]
+
+    def top_raw(self, k):
+        """The k largest groups as (key, count) int64 arrays (keys as in export_raw)."""
+        k = int(min(k, self.num_groups))
+        keys = np.zeros(max(k, 1), dtype=np.int64)
+        counts = np.zeros(max(k, 1), dtype=np.int64)
+        n = self.ctx.lib.dq_freq_top(self.ctx.handle, self.handle, k, keys.ctypes.data, counts.ctypes.data)
+        if n < 0:
+            raise N.NativeError(int(n), "dq_freq_top: %s" % self.ctx.last_error())
+        return keys[:n], counts[:n]
+
+    def row_counts(self):
+        """dq_freq_row_counts: per source row, the count of its group (0 for rows taking no part)."""
+        n = self.source.nrows
+        out = np.zeros(max(n, 1), dtype=np.int64)
+        rc = self.ctx.lib.dq_freq_row_counts(self.ctx.handle, self.handle, out.ctypes.data, n, 0)
+        self.ctx.check(rc, "dq_freq_row_counts")
+        return out[:n]
+
     def __del__(self):
         try:
             if self.handle:
@@ -234,14 +263,28 @@ class FrequencyTable:
         return out
 
 
-def frequencies(table, key_columns, include_nulls=False):
+def frequencies(table, key_columns, include_nulls=False, weights=None):
+    """dq_frequencies over `key_columns` of `table`; with `weights` (int64 numpy array, one count per row) each row
+    stands for that many rows (dq_frequencies_ex: the pre-aggregated groups of other shards)."""
     context = ctx()
     names = list(table.columns)
     cols = [table[c].native() for c in names]
     keys = np.array([names.index(c) for c in key_columns], dtype=np.int32)
     arr = (N.DqColumn * max(len(cols), 1))(*cols)
     handle = ctypes.c_void_p()
-    rc = context.lib.dq_frequencies(context.handle, arr, len(cols), table.nrows, keys.ctypes.data, len(keys),
-                                    N.FREQ_INCLUDE_NULLS if include_nulls else 0, ctypes.byref(handle))
+    flags = N.FREQ_INCLUDE_NULLS if include_nulls else 0
+    if weights is None:
+        rc = context.lib.dq_frequencies(context.handle, arr, len(cols), table.nrows, keys.ctypes.data, len(keys),
+                                        flags, ctypes.byref(handle))
+    else:
+        w = np.ascontiguousarray(weights, dtype=np.int64)
+        if len(w) != table.nrows:
+            raise ValueError("weights: %d entries for %d rows" % (len(w), table.nrows))
+        opt = N.DqFreqOptions()
+        opt.flags = flags
+        opt.weights_device = 0
+        opt.weights = w.ctypes.data if len(w) else None
+        rc = context.lib.dq_frequencies_ex(context.handle, arr, len(cols), table.nrows, keys.ctypes.data, len(keys),
+                                           ctypes.byref(opt), ctypes.byref(handle))
     context.check(rc, "dq_frequencies")
     return FrequencyTable(context, handle, table, key_columns, include_nulls)

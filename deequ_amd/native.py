@@ -48,7 +48,7 @@ EXPORTED_SYMBOLS = (
     "dq_scan_launch_count", "dq_state_merge", "dq_state_fold", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
     "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
     "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
-    "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge",
+    "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
     "dq_scan_streamed",
 )
@@ -186,6 +186,7 @@ def load_library(path=None):
             "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
             "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),
             "dq_frequencies_ex": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
+            "dq_freq_row_counts": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_uint32]),
             "dq_freq_export_device": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
             "dq_freq_from_pairs": (c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_int64, c_uint32, c_int64,
                                            c_int64, c_void_p]),

@@ -164,7 +164,10 @@ class ColumnProfiler:
     @staticmethod
     def profile(data, restrictToColumns=None, printStatusUpdates=False,
                 lowCardinalityHistogramThreshold=DEFAULT_CARDINALITY_THRESHOLD, kllParameters=None,
-                predefinedTypes=None):
+                predefinedTypes=None, passes=None):
+        """`passes` runs the three passes' work: None = AnalysisRunner on this process's GPU (LocalPasses); the
+        sharded runner passes its own (distributed.ShardedProfilerPasses), so the same code profiles row shards."""
+        passes = passes or LocalPasses()
         predefinedTypes = dict(predefinedTypes or {})
         if restrictToColumns is not None:
             for c in restrictToColumns:
@@ -182,7 +185,7 @@ class ColumnProfiler:
                 first += [Completeness(name), ApproxCountDistinct(name), DataType(name)]
             else:
                 first += [Completeness(name), ApproxCountDistinct(name)]
-        res1 = AnalysisRunner.onData(data).addAnalyzers(first).addAnalyzer(Size()).run()
+        res1 = passes.run(data, first + [Size()])
         generic = ColumnProfiler._extract_generic(relevant, schema, res1, predefinedTypes)
 
         # ---- pass 2 ------------------------------------------------------------------------------
@@ -194,7 +197,7 @@ class ColumnProfiler:
         for name in data.fieldNames:
             if name in numeric:
                 to = N.TYPE_LONG if generic.typeOf(name) == DataTypeInstances.Integral else N.TYPE_DOUBLE
-                cast_cols.append(_cast_column(data, name, to))
+                cast_cols.append(passes.cast(data, name, to))
             else:
                 cast_cols.append(data[name])
         casted = Table(cast_cols)
@@ -202,7 +205,7 @@ class ColumnProfiler:
         for name in numeric:
             second += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name),
                        KLLSketch(name, kllParameters)]
-        res2 = AnalysisRunner.onData(casted).addAnalyzers(second).run() if second else None
+        res2 = passes.run(casted, second) if second else None
         stats = ColumnProfiler._extract_numeric(res2, numeric, kllParameters)
 
         # ---- pass 3 ------------------------------------------------------------------------------
@@ -213,7 +216,7 @@ class ColumnProfiler:
                    generic.typeOf(c) in (DataTypeInstances.String, DataTypeInstances.Boolean,
                                          DataTypeInstances.Integral, DataTypeInstances.Fractional) and
                    cnt <= lowCardinalityHistogramThreshold]
-        histograms = ColumnProfiler._compute_histograms(data, targets) if targets else {}
+        histograms = passes.histograms(data, targets) if targets else {}
 
         profiles = {}
         for name in relevant:
@@ -285,6 +288,19 @@ class ColumnProfiler:
                 values[k] = DistributionValue(int(c), c / total)
             out[name] = Distribution(values, len(values))
         return out
+
+
+class LocalPasses:
+    """The profiler's passes on this process's GPU: AnalysisRunner runs, GPU casts, dq_frequencies histograms."""
+
+    def run(self, data, analyzers):
+        return AnalysisRunner.onData(data).addAnalyzers(analyzers).run()
+
+    def cast(self, data, name, to_type):
+        return _cast_column(data, name, to_type)
+
+    def histograms(self, data, targets):
+        return ColumnProfiler._compute_histograms(data, targets)
 
 
 class ColumnProfilerRunBuilder:

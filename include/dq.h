@@ -314,6 +314,13 @@ int dq_freq_merge(dq_ctx* ctx, const dq_freq_table* a, const dq_freq_table* b, d
 int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq_freq_table* x,
                                const dq_freq_table* y, double* mi, int32_t* present);
 
+/* Per row of the table's own source (the nrows rows it was built over by dq_frequencies / dq_frequencies_ex): the
+ * count of the row's group, 0 for a row that takes no part (all key columns NULL without DQ_FREQ_INCLUDE_NULLS) —
+ * the join of the rows with their frequency table, as MutualInformation joins the joint groups with the marginal
+ * tables (A/MutualInformation.scala:50-74); the sharded MutualInformation attaches px / py to exchanged groups
+ * with it. `counts` holds nrows entries (a device pointer with DQ_FREQ_PAIRS_DEVICE). */
+int dq_freq_row_counts(dq_ctx* ctx, const dq_freq_table* table, int64_t* counts, int64_t nrows, uint32_t flags);
+
 /* ApproxQuantile / ApproxQuantiles (A/ApproxQuantile.scala:28-103, A/ApproxQuantiles.scala:39-101): replaces the
  * per-row PercentileDigest.add of StatefulApproxQuantile.update (C/StatefulApproxQuantile.scala:65-72). Computes
  * EXACT order statistics of the column's non-NULL values cast to double, in java.lang.Double.compare order

@@ -1,7 +1,8 @@
 """Multi-rank runner on CPU: world_size 2 (and 3) over gloo. The per-rank compute is a CPU test double
-(oracle states, numpy key partitioning) so this covers the collective choreography — state
-all-gather + rank-ordered fold, hash-partitioned all-to-all of keys, global numRows / entropy — while
-the GPU compute of each piece is covered by the -m gpu tests."""
+(oracle states, dict-based group tables) so this covers the collective choreography — state all-gather +
+rank-ordered fold, the owner shuffle of pre-aggregated groups (fixed-width, string and multi-column keys),
+global numRows / entropy, the two-owner MutualInformation, the sharded ColumnProfiler — while the GPU compute
+of each piece is covered by the -m gpu tests."""
 import math
 import os
 import socket
@@ -18,41 +19,6 @@ from deequ_amd.states import state_to_native
 from deequ_amd.table import Table, unpack_validity
 
 
-def mix64(z):
-    z = np.uint64(z)
-    with np.errstate(over="ignore"):
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        return z ^ (z >> np.uint64(31))
-
-
-def canonical_keys(col):
-    v = np.asarray(col.values)
-    if col.spark_type == N.TYPE_DOUBLE:
-        b = v.view(np.uint64).copy()
-        b[np.isnan(v)] = np.uint64(0x7FF8000000000000)
-        return b
-    return v.astype(np.int64).view(np.uint64)
-
-
-class OracleTable:
-    """Stand-in for the local frequency table over owned canonical keys."""
-
-    def __init__(self, keys):
-        self.u, self.c = np.unique(np.asarray(keys, dtype=np.uint64), return_counts=True)
-        self.num_rows = int(self.c.sum())
-
-    def summary(self, n=None):
-        n = n or self.num_rows
-        ent = math.fsum(float(-(c / n) * math.log(c / n)) for c in self.c)
-        return {"num_groups": len(self.c), "num_unique": int((self.c == 1).sum()), "entropy": ent,
-                "num_rows": self.num_rows}
-
-    def top(self, k):
-        order = np.argsort(-self.c, kind="stable")[:k]
-        return [((int(self.u[i].astype(np.int64)),), int(self.c[i])) for i in order]
-
-
 class OracleLocal:
     def scan_states(self, batch):
         import oracle as O
@@ -62,6 +28,13 @@ class OracleLocal:
             st = O.expected_state(batch.data, a, exact=False)
             if st is not None:  # the oracle's own state -> the product's State of the same reference class
                 st = getattr(D, type(st).__name__)(*st.key())
+                col = batch.data[a.column] if op.kind in (N.OP_MEAN, N.OP_SUM) else None
+                if col is not None and col.spark_type in (N.TYPE_BYTE, N.TYPE_SHORT, N.TYPE_INT, N.TYPE_LONG):
+                    # the shard's exact Long partial, as the GPU scan reports it (merged with wrap-around)
+                    wt, _ = O._where(batch.data, a.where)
+                    vals = np.asarray(col.values).astype(np.int64)[O._valid(col) & wt]
+                    with np.errstate(over="ignore"):
+                        st.exact = int(vals.sum(dtype=np.int64))
             raw += bytes(state_to_native(op.kind, st))
         digests = []
         for column, rel in batch.quantile_reqs:  # the runner's digest policy over oracle order statistics
@@ -80,16 +53,65 @@ class OracleLocal:
         vals = np.asarray(c.values, dtype=np.float64)[unpack_validity(c.validity, c.length)]
         return O.kll_state_bytes(vals, sketch_size, shrinking_factor)
 
-    def partition(self, column, world):
-        valid = unpack_validity(column.validity, column.length)
-        keys = canonical_keys(column)[valid]
-        owner = np.array([int(mix64(k) >> np.uint64(32)) % world for k in keys], dtype=np.int64)
-        order = np.argsort(owner, kind="stable")
-        counts = [int((owner == r).sum()) for r in range(world)]
-        return torch.from_numpy(keys[order].view(np.int64).copy()), counts, int((~valid).sum())
+    def cast_column(self, shard, name, to_type):
+        """ColumnProfiler.castColumn with the oracle's Spark string -> long / double casts."""
+        import oracle as O
+        from deequ_amd.table import _column_from_pylist
+        c = shard[name]
+        if c.spark_type == N.TYPE_STRING:
+            conv = O.spark_string_to_long if to_type == N.TYPE_LONG else O.java_parse_double
+            vals = [None if v is None else conv(v) for v in c.to_pylist()]
+        else:
+            vals = c.to_pylist()
+        return _column_from_pylist(name, to_type, vals)
 
-    def frequencies_of_keys(self, keys):
-        return OracleTable(keys.numpy().view(np.uint64))
+    # ---- grouping: dict-based stand-ins for the per-rank frequency tables ----------------------------------
+    def group_block(self, shard, cols, include_nulls):
+        import oracle as O
+        freq, nrows = O.frequencies(shard, cols, include_nulls=include_nulls)
+        nulls = freq.pop((None,) * len(cols), 0) if include_nulls else 0
+        return _block(list(freq.items()), [(c, shard[c].spark_type) for c in cols], nrows - nulls, nulls)
+
+    def owned_table(self, block, include_nulls):
+        d = {}
+        for key, c in zip(block.keys(), block.counts.tolist()):
+            d[key] = d.get(key, 0) + c
+        return d
+
+    def table_summary(self, table, n):
+        counts = list(table.values())
+        ent = math.fsum(-(c / n) * math.log(c / n) for c in counts) if counts and n else 0.0
+        return {"num_groups": len(counts), "num_unique": sum(1 for c in counts if c == 1), "entropy": ent,
+                "num_rows": sum(counts)}
+
+    def top_block(self, table, block, k):
+        items = sorted(table.items(), key=lambda kv: -kv[1])[:k]
+        return _block(items, [(c.name, c.spark_type) for c in block.columns])
+
+    def merged_block(self, table, block):
+        return _block(list(table.items()), [(c.name, c.spark_type) for c in block.columns])
+
+    def row_counts(self, block, cols):
+        idx = [block.names.index(c) for c in cols]
+        sub = [tuple(k[i] for i in idx) for k in block.keys()]
+        tot = {}
+        for key, c in zip(sub, block.counts.tolist()):
+            tot[key] = tot.get(key, 0) + c
+        return np.array([0 if all(v is None for v in key) else tot[key] for key in sub], dtype=np.int64)
+
+
+def _plain(v):
+    """oracle group key component -> a plain value for a column (NaN / -0.0 markers undone)."""
+    if isinstance(v, tuple):
+        return float("nan") if v == ("nan",) else -0.0
+    return float(v) if isinstance(v, float) else v
+
+
+def _block(items, schema, num_rows=0, null_rows=0):
+    from deequ_amd.groups import GroupBlock
+    from deequ_amd.table import _column_from_pylist
+    cols = [_column_from_pylist(name, t, [_plain(k[i]) for k, _ in items]) for i, (name, t) in enumerate(schema)]
+    return GroupBlock(cols, np.array([c for _, c in items], dtype=np.int64), num_rows, null_rows)
 
 
 def op_to_analyzer(batch, op):
@@ -108,6 +130,8 @@ def op_to_analyzer(batch, op):
         return D.Compliance("c", pred, where)
     if k == N.OP_CORRELATION:
         return D.Correlation(c0, c1, where)
+    if k == N.OP_DATATYPE:
+        return D.DataType(c0, where)
     cls = {N.OP_COMPLETENESS: D.Completeness, N.OP_MEAN: D.Mean, N.OP_SUM: D.Sum, N.OP_MINIMUM: D.Minimum,
            N.OP_MAXIMUM: D.Maximum, N.OP_STANDARD_DEVIATION: D.StandardDeviation,
            N.OP_APPROX_COUNT_DISTINCT: D.ApproxCountDistinct}[k]
@@ -260,10 +284,10 @@ class FailingOnRankOne(OracleLocal):
             raise MemoryError("out of device memory")
         return super().kll_state(shard, column, sketch_size, shrinking_factor)
 
-    def partition(self, column, world):
+    def group_block(self, shard, cols, include_nulls):
         if self.rank == 1:
             raise RuntimeError("partition failed")
-        return super().partition(column, world)
+        return super().group_block(shard, cols, include_nulls)
 
 
 def _failing_worker(rank, world, port, q):
@@ -308,3 +332,185 @@ def test_one_failing_rank_fails_every_rank_without_hanging(world):
     assert got["Uniqueness(List(k))"][0] and "rank 1 failed" in got["Uniqueness(List(k))"][1]
     hist = got["Histogram"]
     assert hist[0] and "binningUdf" in hist[1]
+
+
+def mixed_table(n=2400, seed=3):
+    from deequ_amd.table import _column_from_pylist
+    rng = np.random.default_rng(seed)
+    words = ["a", "b", "", "ccc", "dd", "héllo", "12", "x y"]
+    s = [None if rng.random() < 0.1 else words[i] for i in rng.integers(0, len(words), n)]
+    k = [None if rng.random() < 0.07 else int(v) for v in rng.integers(0, 30, n)]
+    special = [float("nan"), -0.0, 0.0, 1.5]
+    d = [None if rng.random() < 0.05 else (special[int(v) % 4] if v < 8 else float(v) / 4.0)
+         for v in rng.integers(0, 60, n)]
+    return Table([_column_from_pylist("s", "string", s), _column_from_pylist("k", N.TYPE_LONG, k),
+                  _column_from_pylist("d", N.TYPE_DOUBLE, d)])
+
+
+def grouping_analyzers():
+    return [D.Uniqueness(["s"]), D.Uniqueness(["s", "k"]), D.Distinctness(["k", "d"]), D.CountDistinct(["s", "d"]),
+            D.Entropy("s"), D.UniqueValueRatio(["s", "k", "d"]), D.Histogram("s"), D.Histogram("d", None, 5),
+            D.MutualInformation(["s", "k"]), D.MutualInformation(["k", "d"])]
+
+
+def _grouping_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = mixed_table()
+        per = (t.nrows + world - 1) // world
+        mask = np.zeros(t.nrows, dtype=bool)
+        mask[rank * per:min(t.nrows, (rank + 1) * per)] = True
+        ctx = D.distributed.DistributedAnalysisRunner(local=OracleLocal()).run(t.select_rows(mask),
+                                                                               grouping_analyzers())
+        out = {}
+        for a in grouping_analyzers():
+            v = ctx.metric(a).value
+            assert v.isSuccess, (a, v)
+            if isinstance(a, D.Histogram):
+                d = v.get()
+                out[repr(a)] = (d.numberOfBins, sorted((k, x.absolute, x.ratio) for k, x in d.values.items()))
+            else:
+                out[repr(a)] = v.get()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_workers(target, world, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=timeout) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(1, world):
+        assert results[r] == results[0]
+    return results[0]
+
+
+def _oracle_mi(t, cols):
+    import oracle as O
+    freq, nrows = O.frequencies(t, cols)
+    px, py = {}, {}
+    for (u, w), c in freq.items():
+        px[u] = px.get(u, 0) + c
+        py[w] = py.get(w, 0) + c
+    return math.fsum((c / nrows) * math.log((c / nrows) / ((px[u] / nrows) * (py[w] / nrows)))
+                     for (u, w), c in freq.items() if u is not None and w is not None)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_string_and_multicolumn_grouping_and_mutual_information(world):
+    """string / multi-column keys and MutualInformation over row shards equal the single-table
+    oracle (A/GroupingAnalyzers.scala:53-79, A/MutualInformation.scala:35-97, A/Histogram.scala:66-96)."""
+    import oracle as O
+    from deequ_amd.analyzers import _hist_key
+    got = _run_workers(_grouping_worker, world)
+    t = mixed_table()
+    for a in grouping_analyzers():
+        name = type(a).__name__
+        g = got[repr(a)]
+        if name == "Histogram":
+            freq, n = O.frequencies(t, [a.column], include_nulls=True)
+            assert g[0] == len(freq)
+            exp = sorted(freq.values(), reverse=True)[:a.maxDetailBins]
+            assert sorted((c for _, c, _ in g[1]), reverse=True) == exp
+            for key, c, ratio in g[1]:
+                assert ratio == c / n
+            if a.column == "s":  # every group shown: the keys themselves
+                want = {(_hist_key(k[0]) if k[0] is not None else "NullValue"): c for k, c in freq.items()}
+                assert {k: c for k, c, _ in g[1]} == want
+            continue
+        if name == "MutualInformation":
+            exp = _oracle_mi(t, a.columns)
+            assert abs(g - exp) <= 1e-12 * max(1.0, abs(exp)), (a, g, exp)
+            continue
+        freq, nrows = O.frequencies(t, a.columns)
+        s = O.grouping_summary(freq, nrows)
+        exp = {"Uniqueness": s["num_unique"] / nrows, "Distinctness": s["num_groups"] / nrows,
+               "Entropy": s["entropy"], "CountDistinct": float(s["num_groups"]),
+               "UniqueValueRatio": s["num_unique"] / s["num_groups"]}[name]
+        assert abs(g - exp) <= 1e-12 * max(1.0, abs(exp)), (a, g, exp)
+
+
+def test_group_block_pack_roundtrip_and_owner_hash():
+    """The exchange format: pack / unpack is lossless (strings, NULLs, NaN / -0.0 bit patterns) and the owner of a
+    key does not depend on which rank's block (or which position) it comes from."""
+    from deequ_amd import groups as G
+    t = mixed_table(500, seed=9)
+    items = [((s, k, d), 1) for s, k, d in zip(t["s"].to_pylist(), t["k"].to_pylist(), t["d"].to_pylist())]
+    blk = _block(items, [("s", N.TYPE_STRING), ("k", N.TYPE_LONG), ("d", N.TYPE_DOUBLE)])
+    back = G.unpack(G.pack(blk), blk.schema())
+    assert back.keys() == blk.keys() and back.counts.tolist() == blk.counts.tolist()
+    rev = blk.subset(np.arange(blk.size)[::-1])
+    o1, o2 = G.owners(blk, 5), G.owners(rev, 5)
+    assert (o1 == o2[::-1]).all() and set(o1.tolist()) == set(range(5))
+    assert (G.owners(blk, 3, key_columns=["k"]) == G.owners(_block([((k,), 1) for k in t["k"].to_pylist()],
+                                                                    [("k", N.TYPE_LONG)]), 3)).all()
+    sub = G.concat([blk.subset(np.arange(0, 200)), blk.subset(np.arange(200, blk.size))], blk.schema())
+    assert sub.keys() == blk.keys()
+
+
+def _profile_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from test_gpu_profile_c5 import c5_table
+        t = c5_table(3000)
+        per = (t.nrows + world - 1) // world
+        mask = np.zeros(t.nrows, dtype=bool)
+        mask[rank * per:min(t.nrows, (rank + 1) * per)] = True
+        prof = D.distributed.DistributedAnalysisRunner(local=OracleLocal()).profile(t.select_rows(mask))
+        out = {"numRecords": prof.numRecords}
+        for name, p in prof.profiles.items():
+            d = {"completeness": p.completeness, "approx": p.approximateNumDistinctValues, "type": p.dataType,
+                 "inferred": p.isDataTypeInferred, "typeCounts": p.typeCounts,
+                 "hist": None if p.histogram is None else
+                 ({k: (v.absolute, v.ratio) for k, v in p.histogram.values.items()}, p.histogram.numberOfBins)}
+            if isinstance(p, D.NumericColumnProfile):
+                d.update(minimum=p.minimum, maximum=p.maximum, sum=p.sum, mean=p.mean, stdDev=p.stdDev,
+                         kll_n=sum(b.count for b in p.kll.buckets))
+            out[name] = d
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_column_profiler_matches_single_table_oracle(world):
+    """the 3-pass ColumnProfiler over row shards (reduced C5 table: 20 mixed columns) equals the
+    oracle's restatement of the profiler on the whole table (M/profiles/ColumnProfiler.scala:91-208, 357-606)."""
+    import oracle as O
+    from test_gpu_profile_c5 import c5_table
+    got = _run_workers(_profile_worker, world, timeout=300)
+    t = c5_table(3000)
+    exp = O.expected_profile(t)
+    assert got["numRecords"] == t.nrows
+    hist = 0
+    for name, e in exp.items():
+        p = got[name]
+        assert (p["completeness"], p["approx"], p["type"], p["inferred"], p["typeCounts"]) == \
+            (e["completeness"], e["approx_distinct"], e["dataType"], e["inferred"], e["typeCounts"]), name
+        if e["dataType"] in ("Integral", "Fractional"):
+            st = e["numeric"]
+            assert (p["minimum"], p["maximum"]) == (st["min"], st["max"]), name
+            for key in ("sum", "mean", "stdDev"):
+                ok = p[key] == st[key] if (key == "sum" and e["dataType"] == "Integral") else \
+                    abs(p[key] - st[key]) <= 1e-12 * max(abs(st[key]), 1e-300)
+                assert ok, (name, key, p[key], st[key])
+            assert p["kll_n"] == st["n"], name
+        if e["histogram"] is None:
+            assert p["hist"] is None, name
+        else:
+            hist += 1
+            values, nbins = p["hist"]
+            assert {k: v[0] for k, v in values.items()} == e["histogram"] and nbins == len(e["histogram"]), name
+            assert all(v[1] == v[0] / t.nrows for v in values.values()), name
+    assert hist >= 5
