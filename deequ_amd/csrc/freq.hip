@@ -340,12 +340,12 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
 // Max over workgroups of the per-workgroup sizing registers: grid (kSizingRegs / 256, G), each thread
 // folds a run of workgroups for one register.
 __global__ void __launch_bounds__(256)
-sizing_reduce_kernel(const uint8_t* __restrict__ regs_part, int ngroups, unsigned int* __restrict__ regs) {
+sizing_reduce_kernel(const uint8_t* __restrict__ regs_part, int ngroups, int nregs, unsigned int* __restrict__ regs) {
     const int reg = blockIdx.x * 256 + threadIdx.x;
     const int per = (ngroups + gridDim.y - 1) / gridDim.y;
     const int g0 = blockIdx.y * per, g1 = min(ngroups, g0 + per);
     unsigned int m = 0;
-    for (int g = g0; g < g1; ++g) m = max(m, (unsigned int)regs_part[(uint64_t)g * kSizingRegs + reg]);
+    for (int g = g0; g < g1; ++g) m = max(m, (unsigned int)regs_part[(uint64_t)g * nregs + reg]);
     if (m) atomicMax(&regs[reg], m);
 }
 
@@ -646,6 +646,262 @@ scatter2_kernel(const Pass2Item* __restrict__ items, const unsigned long long* _
         }
         scatter_tile<BINS, GENERAL, TILE>(h, rw, keep, shift, mask, hist, start, cursor, sh, sr, out_h, out_r);
     }
+}
+
+// ---- fast path (one fixed-width key column, unweighted): partitions of fixed capacity, runs reserved with atomics --
+// Pass 1 and pass 2 of the fast path need no count pass over the keys: every bucket gets a fixed capacity (its
+// expected share of the keys plus slack), and each tile reserves its per-bucket runs with one global atomicAdd
+// per non-empty bucket (256 per 8 K keys at most). The order inside a bucket is then arrival order. That does not
+// matter to the aggregation that follows, and the table build already takes LDS insertion order anyway.
+// A bucket that would overflow its capacity raises a flag. That happens with heavy hitters: one value repeated on
+// a large share of the rows. The host then redoes the build on the exactly-counted path
+// (extract_count -> partition1 -> count2 / scan2 / scatter2).
+
+constexpr int kFastRegs = 1024;  // sizing HLL registers of the fast pass 1 (1 KB per workgroup; sizing only)
+
+// Raw bits of a W-byte cell, loaded without any branch on the element type (a runtime switch around the load
+// would put a wait after every load: one row in flight per lane); canonical_of() converts after the loads.
+template <int W>
+__device__ __forceinline__ uint64_t load_bits(const void* values, int64_t r) {
+    if (W == 8) return static_cast<const uint64_t*>(values)[r];
+    if (W == 4) return static_cast<const uint32_t*>(values)[r];
+    if (W == 2) return static_cast<const uint16_t*>(values)[r];
+    return static_cast<const uint8_t*>(values)[r];
+}
+
+template <int W>
+__device__ __forceinline__ uint64_t canonical_of(int elem, uint64_t raw) {
+    if (W == 8) {
+        if (elem == ET_F64) {
+            const bool nan = (raw & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
+            return nan ? 0x7ff8000000000000ull : raw;
+        }
+        return raw;
+    }
+    if (W == 4) {
+        if (elem == ET_F32) {
+            const bool nan = (raw & 0x7FFFFFFFu) > 0x7F800000u;
+            return nan ? 0x7fc00000ull : raw;
+        }
+        return (uint64_t)(int64_t)(int32_t)(uint32_t)raw;
+    }
+    if (W == 2) return (uint64_t)(int64_t)(int16_t)(uint16_t)raw;
+    return elem == ET_U8 ? (raw ? 1ull : 0ull) : (uint64_t)(int64_t)(int8_t)(uint8_t)raw;
+}
+
+// One tile already in registers (h, keep) -> LDS staging ordered by digit -> global runs reserved with atomics:
+// digit b's run goes to bucket k = bucket_of(b), at k * cap + atomicAdd(&gcursor[k], hist[b]), when it fits the
+// bucket's capacity; otherwise *lovf is raised and nothing more is written.
+template <int BINS, int TILE, typename BucketOf, typename Prefetch>
+__device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / kFreqBlock], unsigned int keepm,
+                                                     int shift, unsigned int mask, unsigned int* hist, unsigned int* start,
+                                                     unsigned long long* cursor, unsigned long long* sh,
+                                                     unsigned long long* __restrict__ gcursor, unsigned long long cap,
+                                                     BucketOf bucket_of, unsigned int* lovf, unsigned int* lbad,
+                                                     unsigned long long limit, unsigned long long* __restrict__ out_h,
+                                                     Prefetch prefetch) {
+    constexpr int PER = TILE / kFreqBlock;
+    static_assert(PER <= 32, "keep flags are one bit per key");
+    unsigned int rank[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+        rank[j] = ((keepm >> j) & 1u) ? atomicAdd(&hist[(unsigned int)(h[j] >> shift) & mask], 1u) : 0u;
+    __syncthreads();
+    constexpr int RUN = BINS / kFreqBlock > 0 ? BINS / kFreqBlock : 1;
+    __shared__ unsigned int wsum[kFreqBlock / 64];
+    unsigned int total;
+    {
+        const int b0 = threadIdx.x * RUN;
+        unsigned int acc = 0;
+#pragma unroll
+        for (int b = 0; b < RUN; ++b) acc += hist[b0 + b];
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        unsigned int inc = acc;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned int v = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        unsigned int run = inc - acc;
+        total = 0;
+#pragma unroll
+        for (int w = 0; w < kFreqBlock / 64; ++w) {
+            if (w < wave) run += wsum[w];
+            total += wsum[w];
+        }
+#pragma unroll
+        for (int b = 0; b < RUN; ++b) {
+            const unsigned int hb = hist[b0 + b];
+            start[b0 + b] = run;
+            run += hb;
+            if (hb) {
+                const unsigned long long k = bucket_of(b0 + b);
+                const unsigned long long at = atomicAdd(&gcursor[k], (unsigned long long)hb);
+                if (at + hb > cap) *lovf = 1u;
+                cursor[b0 + b] = k * cap + at;
+            }
+        }
+    }
+    __syncthreads();  // start[] / cursor[] of every digit written before any thread places its keys
+    // the next tile's loads go out only now: a wait for the reservation atomics above (vmcnt counts loads, stores
+    // and atomics in order) would otherwise wait for them too
+    prefetch();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (!((keepm >> j) & 1u)) continue;
+        sh[start[(unsigned int)(h[j] >> shift) & mask] + rank[j]] = h[j];
+    }
+    __syncthreads();
+    if (!*lovf) {  // (uniform: read after the barrier that follows every write of the flag)
+        for (unsigned int i = threadIdx.x; i < total; i += kFreqBlock) {
+            const unsigned long long hv = sh[i];
+            const unsigned int d = (unsigned int)(hv >> shift) & mask;
+            const unsigned long long pos = cursor[d] + (i - start[d]);
+            if (pos < limit) out_h[pos] = hv;  // always true; a violated invariant is reported, never written
+            else *lbad = 1u;
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < BINS; b += kFreqBlock) hist[b] = 0;
+    __syncthreads();
+}
+
+// Fast pass 1: rows -> 256 partitions of `cap` keys each (partition d at d * cap), plus the side counters and the
+// sizing registers (per workgroup, reduced by sizing_reduce_kernel). W = the key column's cell width. The next
+// tile's cells are loaded while the current tile is scattered (after its reservation atomics returned).
+template <int TILE, int W>
+__global__ void __launch_bounds__(kFreqBlock)
+partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long long cap,
+                       unsigned long long* __restrict__ gcursor, unsigned long long* __restrict__ out_h,
+                       uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr) {
+    constexpr int PER = TILE / kFreqBlock;
+    __shared__ unsigned int hist[kDigitBins], start[kDigitBins];
+    __shared__ unsigned long long cursor[kDigitBins];
+    __shared__ unsigned long long sh[TILE];
+    __shared__ unsigned int regs[kFastRegs];
+    __shared__ unsigned long long red[kFreqBlock / 64];
+    __shared__ unsigned int lovf, lbad;
+    for (int i = threadIdx.x; i < kFastRegs; i += kFreqBlock) regs[i] = 0;
+    hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) lovf = lbad = 0;
+    __syncthreads();
+    unsigned long long taken = 0, sent = 0, nulls = 0;
+    const int64_t ntiles = (nrows + TILE - 1) / TILE;
+    const bool has_validity = c.validity != nullptr;
+    uint64_t raw[PER];
+    unsigned int vbyte[PER];  // the validity byte holding the row's bit (0xFF without a bitmap)
+    auto load = [&](int64_t tl) {
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int64_t r = tl * TILE + (int64_t)j * kFreqBlock + threadIdx.x;
+            const bool in = r < nrows;
+            raw[j] = in ? load_bits<W>(c.values, r) : 0ull;
+            vbyte[j] = !in ? 0u : (has_validity ? (unsigned int)c.validity[r >> 3] : 0xFFu);
+        }
+    };
+    int64_t tile = blockIdx.x;
+    if (tile < ntiles) load(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const int64_t t0 = tile * TILE;
+        uint64_t h[PER];
+        unsigned int keepm = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int64_t r = t0 + (int64_t)j * kFreqBlock + threadIdx.x;
+            const bool in = r < nrows;
+            const bool valid = (vbyte[j] >> (r & 7)) & 1u;
+            h[j] = mix64(canonical_of<W>(c.elem, raw[j]));
+            const bool keep = valid && h[j] != kEmpty;
+            keepm |= (keep ? 1u : 0u) << j;
+            taken += (valid || (in && include_nulls)) ? 1 : 0;
+            nulls += (in && !valid && include_nulls) ? 1 : 0;
+            sent += (valid && h[j] == kEmpty) ? 1 : 0;
+        }
+        const int64_t next = tile + gridDim.x;
+        // the sizing sketch sees the keys whose bits 40..42 are zero: a 1/8 sample of the distinct keys (each key is
+        // in or out on every row), scaled back by 8 on the host
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (!((keepm >> j) & 1u) || ((h[j] >> 40) & 7u)) continue;
+            const unsigned int idx = (unsigned int)(h[j] >> 54);
+            const unsigned int rank = (unsigned int)__clzll((long long)((h[j] << 10) | (1ull << 9))) + 1u;
+            if (rank > regs[idx]) atomicMax(&regs[idx], rank);
+        }
+        scatter_tile_reserve<kDigitBins, TILE>(h, keepm, 0, kDigitBins - 1, hist, start, cursor, sh, gcursor, cap,
+                                               [](int b) { return (unsigned long long)b; }, &lovf, &lbad,
+                                               cap * kDigitBins, out_h, [&]() {
+            if (next < ntiles) load(next);
+        });
+    }
+    taken = block_sum_u64(taken, red);
+    sent = block_sum_u64(sent, red);
+    nulls = block_sum_u64(nulls, red);
+    if (threadIdx.x == 0) {
+        if (taken) atomicAdd(&ctr->num_rows, taken);
+        if (sent) atomicAdd(&ctr->sentinel, sent);
+        if (nulls) atomicAdd(&ctr->nulls, nulls);
+        if (lovf) atomicAdd(&ctr->pad[0], 1ull);
+        if (lbad) atomicAdd(&ctr->pad[2], 1ull);
+    }
+    for (int i = threadIdx.x; i < kFastRegs / 4; i += kFreqBlock) {
+        const unsigned int w = regs[4 * i] | (regs[4 * i + 1] << 8) | (regs[4 * i + 2] << 16) | (regs[4 * i + 3] << 24);
+        reinterpret_cast<unsigned int*>(regs_part + (uint64_t)blockIdx.x * kFastRegs)[i] = w;
+    }
+}
+
+struct FastItem {
+    unsigned long long begin, end;  // range of one partition's pass-1 output
+    unsigned int part, pad;
+};
+
+// Fast pass 2: per work item (a chunk of one partition), keys -> bucket part + 256 * (next bits), bucket k at
+// k * cap. The next tile is loaded before the current one is scattered.
+template <int BINS, int TILE>
+__global__ void __launch_bounds__(kFreqBlock)
+scatter2_fast_kernel(const FastItem* __restrict__ items, const unsigned long long* __restrict__ in_h, unsigned int mask,
+                     unsigned long long cap, unsigned long long* __restrict__ gcursor, unsigned long long* __restrict__ out_h,
+                     Counters* __restrict__ ctr) {
+    constexpr int PER = TILE / kFreqBlock;
+    __shared__ unsigned int hist[BINS], start[BINS];
+    __shared__ unsigned long long cursor[BINS];
+    __shared__ unsigned long long sh[TILE];
+    __shared__ unsigned int lovf, lbad;
+    const FastItem it = items[blockIdx.x];
+    for (int b = threadIdx.x; b < BINS; b += kFreqBlock) hist[b] = 0;
+    if (threadIdx.x == 0) lovf = lbad = 0;
+    __syncthreads();
+    const unsigned long long part = it.part;
+    uint64_t nxt[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const unsigned long long i = it.begin + (unsigned long long)j * kFreqBlock + threadIdx.x;
+        nxt[j] = i < it.end ? __builtin_nontemporal_load(&in_h[i]) : kEmpty;
+    }
+    for (unsigned long long t0 = it.begin; t0 < it.end; t0 += TILE) {
+        uint64_t h[PER];
+        unsigned int keepm = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            h[j] = nxt[j];
+            keepm |= (t0 + (unsigned long long)j * kFreqBlock + threadIdx.x < it.end ? 1u : 0u) << j;
+        }
+        const unsigned long long n0 = t0 + TILE;
+        scatter_tile_reserve<BINS, TILE>(h, keepm, 8, mask, hist, start, cursor, sh, gcursor, cap,
+                                         [part](int b) { return part + (unsigned long long)kDigitBins * b; }, &lovf, &lbad,
+                                         cap * kDigitBins * (mask + 1ull), out_h, [&]() {
+            if (n0 < it.end) {
+#pragma unroll
+                for (int j = 0; j < PER; ++j) {
+                    const unsigned long long i = n0 + (unsigned long long)j * kFreqBlock + threadIdx.x;
+                    nxt[j] = i < it.end ? __builtin_nontemporal_load(&in_h[i]) : kEmpty;
+                }
+            }
+        });
+    }
+    if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->pad[1], 1ull);
+    if (threadIdx.x == 0 && lbad) atomicAdd(&ctr->pad[2], 1ull);
 }
 
 struct SummaryPartial {
@@ -1317,6 +1573,130 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
     return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency table build did not converge");
 }
 
+// Fast path (one fixed-width key column, unweighted, large inputs): fixed-capacity buckets with atomically
+// reserved runs (partition1_fast -> scatter2_fast -> regions), no count pass. Sets *done = false, having built
+// nothing that the exact path cannot redo, when a bucket overflows its capacity (heavy hitters) or the table is
+// too small or too large for the two-pass bucketing.
+constexpr int64_t kFastMinRows = 1 << 24;
+
+int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* done) {
+    *done = false;
+    hipStream_t s = dq::ctx_stream(ctx);
+    const int xgrid = scan_grid((uint64_t)nrows);
+    // pass 1: 256 partitions of cap1 keys (the expected share plus slack for hashing variance and repeats)
+    const unsigned long long cap1 = (unsigned long long)(nrows / kDigitBins) + (unsigned long long)(nrows / kDigitBins) / 32 + 65536;
+    unsigned long long *gc1 = nullptr, *h1 = nullptr;
+    unsigned int* regs = nullptr;
+    uint8_t* regs_part = nullptr;
+    FQ_HIP(ctx, buf.alloc((void**)&gc1, sizeof(unsigned long long) * kDigitBins));
+    FQ_HIP(ctx, buf.alloc((void**)&h1, cap1 * kDigitBins * 8));
+    FQ_HIP(ctx, buf.alloc((void**)&regs, kFastRegs * sizeof(unsigned int)));
+    FQ_HIP(ctx, buf.alloc((void**)&regs_part, (size_t)kFastRegs * xgrid));
+    FQ_HIP(ctx, hipMemsetAsync(gc1, 0, sizeof(unsigned long long) * kDigitBins, s));
+    FQ_HIP(ctx, hipMemsetAsync(regs, 0, kFastRegs * sizeof(unsigned int), s));
+    FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
+    const int inul = t->ks.include_nulls ? 1 : 0;
+    const bool t8k = getenv("DQ_FREQ_P1_8K") != nullptr;  // tuning knob (A/B of the pass-1 tile)
+    if (t8k && elem_size((ElemType)t->ks.cols[0].elem) == 8)
+        hipLaunchKernelGGL((partition1_fast_kernel<kPartTileFast, 8>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+                           nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+    else switch (elem_size((ElemType)t->ks.cols[0].elem)) {
+        case 8:
+            hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 8>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+                               nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+            break;
+        case 4:
+            hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 4>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+                               nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+            break;
+        case 2:
+            hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 2>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+                               nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+            break;
+        default:
+            hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 1>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+                               nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+            break;
+    }
+    hipLaunchKernelGGL(sizing_reduce_kernel, dim3(kFastRegs / 256, std::min(xgrid, 64)), dim3(256), 0, s,
+                       (const uint8_t*)regs_part, xgrid, kFastRegs, regs);
+    FQ_HIP(ctx, hipGetLastError());
+    std::vector<unsigned int> hregs(kFastRegs);
+    std::vector<unsigned long long> pcount(kDigitBins);
+    FQ_HIP(ctx, hipMemcpyAsync(hregs.data(), regs, kFastRegs * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipMemcpyAsync(pcount.data(), gc1, sizeof(unsigned long long) * kDigitBins, hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    if (t->host_ctr.pad[2]) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency fast build: run position out of range");
+    if (t->host_ctr.pad[0]) return DQ_OK;  // a partition overflowed: the exact path
+    unsigned long long n = 0;
+    for (unsigned long long c : pcount) n += c;
+    const double est = n ? 8.0 * hll_raw_estimate(hregs) : 0.0;  // the sketch holds a 1/8 sample of the keys
+    int bits = 0;
+    while (bits < 40 && est / (double)(1ull << bits) > (double)kRegionTarget) ++bits;
+    if (getenv("DQ_DEBUG_FREQ"))
+        fprintf(stderr, "[freq fast] rows=%lld n=%llu est=%.1f bits=%d\n", (long long)nrows, n, est, bits);
+    if (bits < 8 || bits > kMaxPartBits) return DQ_OK;
+    unsigned long long* h2 = nullptr;
+    size_t h2_bytes = 0;
+    for (int grow = 0; grow < 8 && bits <= kMaxPartBits; ++grow, ++bits) {
+        std::vector<unsigned long long> bstart, bcount;
+        const unsigned long long* sorted = h1;
+        if (bits == 8) {
+            bstart.resize(kDigitBins);
+            for (int d = 0; d < kDigitBins; ++d) bstart[d] = (unsigned long long)d * cap1;
+            bcount = pcount;
+        } else {
+            const int bins = 1 << (bits - 8);
+            const uint64_t nb = 1ull << bits;
+            const unsigned long long per = n / nb;
+            const unsigned long long cap2 = per + per / 4 + 2048;
+            std::vector<FastItem> items;
+            for (int p = 0; p < kDigitBins; ++p)
+                for (unsigned long long x = 0; x < pcount[p]; x += kPass2Item)
+                    items.push_back(FastItem{(unsigned long long)p * cap1 + x,
+                                             (unsigned long long)p * cap1 + std::min<unsigned long long>(pcount[p], x + kPass2Item),
+                                             (unsigned int)p, 0u});
+            const int nitems = (int)items.size();
+            FastItem* ditems = nullptr;
+            unsigned long long* gc2 = nullptr;
+            FQ_HIP(ctx, buf.alloc((void**)&ditems, sizeof(FastItem) * std::max(nitems, 1)));
+            FQ_HIP(ctx, buf.alloc((void**)&gc2, sizeof(unsigned long long) * nb));
+            if (cap2 * nb * 8 > h2_bytes) {
+                h2_bytes = cap2 * nb * 8;
+                FQ_HIP(ctx, buf.alloc((void**)&h2, h2_bytes));
+            }
+            FQ_HIP(ctx, hipMemsetAsync(gc2, 0, sizeof(unsigned long long) * nb, s));
+            if (nitems) FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), sizeof(FastItem) * nitems, hipMemcpyHostToDevice, s));
+            const unsigned int mask = (unsigned int)bins - 1;
+            if (nitems && bins > kDigitBins)
+                hipLaunchKernelGGL((scatter2_fast_kernel<4096, kPartTile>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, h1,
+                                   mask, cap2, gc2, h2, t->ctr);
+            else if (nitems)
+                hipLaunchKernelGGL((scatter2_fast_kernel<kDigitBins, kPartTileFast>), dim3(nitems), dim3(kFreqBlock), 0, s,
+                                   ditems, h1, mask, cap2, gc2, h2, t->ctr);
+            FQ_HIP(ctx, hipGetLastError());
+            bcount.resize(nb);
+            FQ_HIP(ctx, hipMemcpyAsync(bcount.data(), gc2, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, s));
+            FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+            FQ_HIP(ctx, hipStreamSynchronize(s));
+            if (t->host_ctr.pad[2]) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency fast build: run position out of range");
+            if (t->host_ctr.pad[1]) return DQ_OK;  // a bucket overflowed: the exact path
+            bstart.resize(nb);
+            for (uint64_t k = 0; k < nb; ++k) bstart[k] = k * cap2;
+            sorted = h2;
+        }
+        bool overflow = false, collision = false;
+        const int rc = build_regions(ctx, t, nrows, buf, sorted, nullptr, bstart, bcount, bits, &overflow, &collision);
+        if (rc != DQ_OK) return rc;
+        if (!overflow) {
+            *done = true;
+            return DQ_OK;
+        }
+    }
+    return DQ_OK;
+}
+
 // extract (+ sizing) -> bucketing on the low `bits` bits of the keys -> per-bucket LDS aggregation. Tables of
 // 8..20 bucket bits take the radix-partition path; the others compact the keys and sort them on the bucket
 // bits with rocPRIM. A bucket whose distinct keys overflow its region (or a fingerprint collision on the
@@ -1326,6 +1706,11 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
     DevBuf buf;
     const bool general = !t->fast || t->ks.weights != nullptr;  // carry row indices (representatives / weights)
     const bool no_partition = getenv("DQ_FREQ_NO_PARTITION") != nullptr;
+    if (t->fast && !t->ks.weights && !no_partition && nrows >= kFastMinRows && !getenv("DQ_FREQ_EXACT")) {
+        bool done = false;
+        const int rc = build_fast(ctx, t, nrows, buf, &done);
+        if (rc != DQ_OK || done) return rc;
+    }
     for (int seed_attempt = 0; seed_attempt < 4; ++seed_attempt) {
         unsigned long long *hs = nullptr, *rows = nullptr, *bk = nullptr;
         unsigned int *regs = nullptr, *hist1 = nullptr;
@@ -1343,7 +1728,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
             hipLaunchKernelGGL(extract_count_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows, bk, regs_part,
                                t->ctr, hist1, kPartTile);
             hipLaunchKernelGGL(sizing_reduce_kernel, dim3(kSizingRegs / 256, std::min(xgrid, 64)), dim3(256), 0, s,
-                               (const uint8_t*)regs_part, xgrid, regs);
+                               (const uint8_t*)regs_part, xgrid, kSizingRegs, regs);
         }
         FQ_HIP(ctx, hipGetLastError());
         std::vector<unsigned int> hregs(kSizingRegs);

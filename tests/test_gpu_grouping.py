@@ -168,3 +168,74 @@ def test_c4_closed_form_at_reduced_scale():
     # device generator == oracle generator on a slice
     sl = keys[123456:123456 + 4096].cpu().numpy()
     assert np.array_equal(sl, O.synth_freq_keys(total, distinct, 123456, 4096))
+
+
+def _value_mixing_to_all_ones():
+    """The int64 whose splitmix64 finalizer is 2^64 - 1 (the inverse finalizer of all ones)."""
+    m = (1 << 64) - 1
+
+    def inv(a):
+        x = a
+        for _ in range(6):
+            x = (x * (2 - a * x)) & m
+        return x
+
+    def unxorshift(z, k):
+        r = z
+        for _ in range(64 // k + 1):
+            r = z ^ (r >> k)
+        return r & m
+    z = m
+    z = unxorshift(z, 31)
+    z = (z * inv(0x94D049BB133111EB)) & m
+    z = unxorshift(z, 27)
+    z = (z * inv(0xBF58476D1CE4E5B9)) & m
+    z = unxorshift(z, 30)
+    return z - (1 << 64) if z >= 1 << 63 else z
+
+
+def _sorted_pairs(ft):
+    k, c = ft.export_pairs()
+    o = np.lexsort((c, k))
+    return k[o], c[o]
+
+
+@pytest.mark.parametrize("case", ["uniform", "repeats", "heavy_hitter", "nulls_nan_sentinel"])
+def test_fast_build_equals_exact_build(case, monkeypatch):
+    """The fast build (fixed-capacity buckets, atomically reserved runs, no count pass; >= 2^24 rows) against the
+    exactly-counted build on the same keys: identical groups, counts and summary. A heavy hitter overflows a
+    bucket and must take the exact path by itself."""
+    import torch
+    n = 40_000_000
+    rng = np.random.default_rng(7)
+    if case == "uniform":
+        v = rng.integers(0, 2 ** 62, n, dtype=np.int64)
+        v[::1_000_003] = _value_mixing_to_all_ones()  # its mixed key is the EMPTY slot marker
+    elif case == "repeats":
+        v = rng.integers(0, n // 19, n, dtype=np.int64)
+    elif case == "heavy_hitter":
+        v = np.where(rng.random(n) < 0.3, 12345, rng.integers(0, 10 ** 6, n)).astype(np.int64)
+    else:
+        v = rng.integers(-500_000, 500_000, n).astype(np.float64) / 8.0
+        v[rng.random(n) < 0.01] = np.nan
+        v[rng.random(n) < 0.01] = -0.0
+    valid = rng.random(n) > 0.02 if case == "nulls_nan_sentinel" else None
+    col = Column("k", N.TYPE_DOUBLE if v.dtype == np.float64 else N.TYPE_LONG, None, None, length=n)
+    col.device = {"values": torch.from_numpy(v).cuda()}
+    if valid is not None:
+        col.device["validity"] = torch.from_numpy(pack_validity(valid)).cuda()
+    t = Table([col])
+    for include_nulls in ((False, True) if valid is not None else (False,)):
+        fast = engine.frequencies(t, ["k"], include_nulls)
+        monkeypatch.setenv("DQ_FREQ_EXACT", "1")
+        exact = engine.frequencies(t, ["k"], include_nulls)
+        monkeypatch.delenv("DQ_FREQ_EXACT")
+        sf, se = fast.summary(None), exact.summary(None)
+        for key in ("num_rows", "num_groups", "num_unique", "max_count", "null_count"):
+            assert sf[key] == se[key], (case, key, sf, se)
+        assert abs(sf["entropy"] - se["entropy"]) <= 1e-12 * se["entropy"]
+        kf, cf = _sorted_pairs(fast)
+        ke, ce = _sorted_pairs(exact)
+        assert np.array_equal(kf, ke) and np.array_equal(cf, ce), case
+        assert [c for _, c in fast.top(5)] == [c for _, c in exact.top(5)]
+        del fast, exact
