@@ -148,6 +148,61 @@ void* ctx_pinned_buf(dq_ctx* ctx, size_t bytes) {
     if (hipStreamSynchronize(ctx->stream) != hipSuccess) return nullptr;  // earlier copies from it are done
     return ctx->pinned;
 }
+
+constexpr size_t kScratchCacheCap = size_t(48) << 30;  // idle bytes kept for re-use
+
+void scratch_trim(dq_ctx* ctx) {
+    if (ctx->scratch_free.empty()) return;
+    (void)hipSetDevice(ctx->device);
+    for (const dq_ctx::CachedBlock& b : ctx->scratch_free) {
+        (void)hipStreamSynchronize(b.stream);
+        (void)hipFree(b.ptr);
+    }
+    ctx->scratch_free.clear();
+    ctx->scratch_cached = 0;
+}
+
+void* scratch_alloc(dq_ctx* ctx, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 256);
+    int best = -1;
+    for (int i = 0; i < (int)ctx->scratch_free.size(); ++i) {
+        const size_t b = ctx->scratch_free[i].bytes;
+        if (b >= bytes && b <= 2 * bytes && (best < 0 || b < ctx->scratch_free[best].bytes)) best = i;
+    }
+    if (best >= 0) {
+        dq_ctx::CachedBlock blk = ctx->scratch_free[best];
+        ctx->scratch_free.erase(ctx->scratch_free.begin() + best);
+        ctx->scratch_cached -= blk.bytes;
+        // last used on another stream (dq_set_stream since): that work must be done before this stream reuses it
+        if (blk.stream != ctx->stream && hipStreamSynchronize(blk.stream) != hipSuccess) {
+            (void)hipFree(blk.ptr);
+            return nullptr;
+        }
+        return blk.ptr;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) == hipSuccess) return p;
+    (void)hipGetLastError();
+    scratch_trim(ctx);  // the cache may hold what this allocation needs
+    if (hipMalloc(&p, bytes) == hipSuccess) return p;
+    (void)hipGetLastError();
+    return nullptr;
+}
+
+void scratch_release(dq_ctx* ctx, void* ptr, size_t bytes) {
+    if (!ptr) return;
+    bytes = std::max<size_t>(bytes, 256);
+    ctx->scratch_free.push_back(dq_ctx::CachedBlock{ptr, bytes, ctx->stream});
+    ctx->scratch_cached += bytes;
+    while (ctx->scratch_cached > kScratchCacheCap && !ctx->scratch_free.empty()) {
+        // release the oldest block (its stream's queued work first)
+        dq_ctx::CachedBlock b = ctx->scratch_free.front();
+        ctx->scratch_free.erase(ctx->scratch_free.begin());
+        ctx->scratch_cached -= b.bytes;
+        (void)hipStreamSynchronize(b.stream);
+        (void)hipFree(b.ptr);
+    }
+}
 }  // namespace dq
 
 // =================================================================================================
@@ -191,6 +246,7 @@ void dq_close(dq_ctx* ctx) {
     if (!ctx->subs.empty()) close_subs(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    scratch_trim(ctx);
     if (ctx->arena) (void)hipFree(ctx->arena);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);

@@ -215,6 +215,15 @@ struct dq_ctx {
     int cus = 256;
     std::map<int, int> occupancy;  // launch shape -> workgroups per CU
     int64_t scan_launches = 0;
+    // Released device scratch of the grouping builds (multi-GB partition buffers and tables), re-used in stream
+    // order instead of a hipMalloc / hipFree pair per call; bounded, freed at dq_close and on allocation failure.
+    struct CachedBlock {
+        void* ptr;
+        size_t bytes;
+        hipStream_t stream;  // the stream of its last use
+    };
+    std::vector<CachedBlock> scratch_free;
+    size_t scratch_cached = 0;
     // multi-device
     std::vector<dq_ctx*> subs;   // one per device (empty: single-device context)
     std::vector<int> devices;
@@ -223,6 +232,13 @@ struct dq_ctx {
 #endif
 
 namespace dq {
+
+// Cached device scratch (see dq_ctx::scratch_free): a block of >= bytes (best fit, at most twice the request)
+// or a new hipMalloc; nullptr when the device is out of memory even after the cache was released.
+void* scratch_alloc(dq_ctx* ctx, size_t bytes);
+// Hand a block back to the cache (its last use was queued on the ctx stream).
+void scratch_release(dq_ctx* ctx, void* ptr, size_t bytes);
+void scratch_trim(dq_ctx* ctx);
 
 // Multi-device orchestration (multi.cpp).
 int multi_scan(dq_ctx* ctx, const dq_column* const* shard_columns, const int64_t* shard_rows, int ncols,

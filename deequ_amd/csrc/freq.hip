@@ -658,6 +658,10 @@ scatter2_kernel(const Pass2Item* __restrict__ items, const unsigned long long* _
 // (extract_count -> partition1 -> count2 / scan2 / scatter2).
 
 constexpr int kFastRegs = 1024;  // sizing HLL registers of the fast pass 1 (1 KB per workgroup; sizing only)
+// Pass-1 run cursors, one per 128-byte line: every workgroup of the chip reserves on the same 256 counters, and
+// atomics on one line serialise (16 counters to a line would be 16-way contention on top of the reservation's).
+constexpr int kCursorStride = 16;
+constexpr int kXcds = 8;  // MI355X: 8 XCDs, workgroup i runs on XCD i % 8
 
 // Raw bits of a W-byte cell, loaded without any branch on the element type (a runtime switch around the load
 // would put a wait after every load: one row in flight per lane); canonical_of() converts after the loads.
@@ -692,12 +696,13 @@ __device__ __forceinline__ uint64_t canonical_of(int elem, uint64_t raw) {
 // One tile already in registers (h, keep) -> LDS staging ordered by digit -> global runs reserved with atomics:
 // digit b's run goes to bucket k = bucket_of(b), at k * cap + atomicAdd(&gcursor[k], hist[b]), when it fits the
 // bucket's capacity; otherwise *lovf is raised and nothing more is written.
-template <int BINS, int TILE, typename BucketOf, typename Prefetch>
+template <int BINS, int TILE, typename BucketOf, typename CounterOf, typename Prefetch>
 __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / kFreqBlock], unsigned int keepm,
                                                      int shift, unsigned int mask, unsigned int* hist, unsigned int* start,
                                                      unsigned long long* cursor, unsigned long long* sh,
                                                      unsigned long long* __restrict__ gcursor, unsigned long long cap,
-                                                     BucketOf bucket_of, unsigned int* lovf, unsigned int* lbad,
+                                                     BucketOf bucket_of, CounterOf counter_of, unsigned int* lovf,
+                                                     unsigned int* lbad,
                                                      unsigned long long limit, unsigned long long* __restrict__ out_h,
                                                      Prefetch prefetch) {
     constexpr int PER = TILE / kFreqBlock;
@@ -738,7 +743,7 @@ __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / 
             run += hb;
             if (hb) {
                 const unsigned long long k = bucket_of(b0 + b);
-                const unsigned long long at = atomicAdd(&gcursor[k], (unsigned long long)hb);
+                const unsigned long long at = atomicAdd(&gcursor[counter_of(b0 + b)], (unsigned long long)hb);
                 if (at + hb > cap) *lovf = 1u;
                 cursor[b0 + b] = k * cap + at;
             }
@@ -768,7 +773,8 @@ __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / 
     __syncthreads();
 }
 
-// Fast pass 1: rows -> 256 partitions of `cap` keys each (partition d at d * cap), plus the side counters and the
+// Fast pass 1: rows -> 256 partitions x 8 XCD sub-regions of `cap` keys each (sub-region (d, x) at (8 d + x) * cap),
+// plus the side counters and the
 // sizing registers (per workgroup, reduced by sizing_reduce_kernel). W = the key column's cell width. The next
 // tile's cells are loaded while the current tile is scattered (after its reservation atomics returned).
 template <int TILE, int W>
@@ -790,6 +796,9 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
     unsigned long long taken = 0, sent = 0, nulls = 0;
     const int64_t ntiles = (nrows + TILE - 1) / TILE;
     const bool has_validity = c.validity != nullptr;
+    // workgroups are dealt round-robin to the XCDs: each XCD's workgroups fill their own sub-region of every
+    // partition, so a reservation counter is shared by 1/8 of the chip (and stays with one XCD's traffic)
+    const unsigned int xcd = blockIdx.x % kXcds;
     uint64_t raw[PER];
     unsigned int vbyte[PER];  // the validity byte holding the row's bit (0xFF without a bitmap)
     auto load = [&](int64_t tl) {
@@ -820,18 +829,20 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
             sent += (valid && h[j] == kEmpty) ? 1 : 0;
         }
         const int64_t next = tile + gridDim.x;
-        // the sizing sketch sees the keys whose bits 40..42 are zero: a 1/8 sample of the distinct keys (each key is
-        // in or out on every row), scaled back by 8 on the host
+        // the sizing sketch sees the keys whose low 3 bits are zero: a 1/8 sample of the distinct keys (each key is
+        // in or out on every row), scaled back by 8 on the host. The sample bits must lie below every bit a rank can
+        // reach (a forced-zero run inside the rank field would inflate the maxima, and the estimate with them).
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            if (!((keepm >> j) & 1u) || ((h[j] >> 40) & 7u)) continue;
+            if (!((keepm >> j) & 1u) || (h[j] & 7u)) continue;
             const unsigned int idx = (unsigned int)(h[j] >> 54);
             const unsigned int rank = (unsigned int)__clzll((long long)((h[j] << 10) | (1ull << 9))) + 1u;
             if (rank > regs[idx]) atomicMax(&regs[idx], rank);
         }
         scatter_tile_reserve<kDigitBins, TILE>(h, keepm, 0, kDigitBins - 1, hist, start, cursor, sh, gcursor, cap,
-                                               [](int b) { return (unsigned long long)b; }, &lovf, &lbad,
-                                               cap * kDigitBins, out_h, [&]() {
+                                               [xcd](int b) { return (unsigned long long)b * kXcds + xcd; },
+                                               [xcd](int b) { return ((unsigned long long)b * kXcds + xcd) * kCursorStride; },
+                                               &lovf, &lbad, cap * kDigitBins * kXcds, out_h, [&]() {
             if (next < ntiles) load(next);
         });
     }
@@ -857,7 +868,8 @@ struct FastItem {
 };
 
 // Fast pass 2: per work item (a chunk of one partition), keys -> bucket part + 256 * (next bits), bucket k at
-// k * cap. The next tile is loaded before the current one is scattered.
+// k * cap; its reservation counter is part * bins + b, so a partition's counters share lines only with each other.
+// The next tile is loaded before the current one is scattered.
 template <int BINS, int TILE>
 __global__ void __launch_bounds__(kFreqBlock)
 scatter2_fast_kernel(const FastItem* __restrict__ items, const unsigned long long* __restrict__ in_h, unsigned int mask,
@@ -889,7 +901,8 @@ scatter2_fast_kernel(const FastItem* __restrict__ items, const unsigned long lon
         }
         const unsigned long long n0 = t0 + TILE;
         scatter_tile_reserve<BINS, TILE>(h, keepm, 8, mask, hist, start, cursor, sh, gcursor, cap,
-                                         [part](int b) { return part + (unsigned long long)kDigitBins * b; }, &lovf, &lbad,
+                                         [part](int b) { return part + (unsigned long long)kDigitBins * b; },
+                                         [part, mask](int b) { return part * (mask + 1ull) + b; }, &lovf, &lbad,
                                          cap * kDigitBins * (mask + 1ull), out_h, [&]() {
             if (n0 < it.end) {
 #pragma unroll
@@ -1305,13 +1318,28 @@ struct dq_freq_table {
     void* scratch = nullptr;  // device scratch for scans
     size_t scratch_bytes = 0;
     std::vector<void*> staged;  // host key columns copied to HBM (rows are re-read by verify/export)
+    // slots / reps come from the building context's scratch cache and go back to it when the table is freed
+    // through that context (any other way: hipFree)
+    dq_ctx* home = nullptr;
+    size_t slots_bytes = 0, reps_bytes = 0;
 };
 
 namespace {
 
-void free_table_buffers(dq_freq_table* t) {
-    if (t->slots) (void)hipFree(t->slots);
-    if (t->reps) (void)hipFree(t->reps);
+void release_slots(dq_freq_table* t, dq_ctx* ctx) {
+    const bool cache = ctx && ctx == t->home;
+    if (t->slots) {
+        if (cache) dq::scratch_release(ctx, t->slots, t->slots_bytes); else (void)hipFree(t->slots);
+    }
+    if (t->reps) {
+        if (cache) dq::scratch_release(ctx, t->reps, t->reps_bytes); else (void)hipFree(t->reps);
+    }
+    t->slots = nullptr;
+    t->reps = nullptr;
+}
+
+void free_table_buffers(dq_freq_table* t, dq_ctx* ctx) {
+    release_slots(t, ctx);
     if (t->ctr) (void)hipFree(t->ctr);
     if (t->scratch) (void)hipFree(t->scratch);
     t->slots = nullptr;
@@ -1350,15 +1378,19 @@ int scan_grid(uint64_t n) {
 
 namespace {
 
-struct DevBuf {  // scratch device buffers of one build, released on every path
-    std::vector<void*> ptrs;
+struct DevBuf {  // scratch device buffers of one build (the context's scratch cache), released on every path
+    dq_ctx* ctx;
+    std::vector<std::pair<void*, size_t>> ptrs;
+    explicit DevBuf(dq_ctx* c) : ctx(c) {}
     ~DevBuf() {
-        for (void* p : ptrs) (void)hipFree(p);
+        for (const auto& p : ptrs) dq::scratch_release(ctx, p.first, p.second);
     }
     hipError_t alloc(void** p, size_t bytes) {
-        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
-        if (e == hipSuccess) ptrs.push_back(*p);
-        return e;
+        bytes = std::max<size_t>(bytes, 16);
+        *p = dq::scratch_alloc(ctx, bytes);
+        if (!*p) return hipErrorOutOfMemory;
+        ptrs.push_back({*p, bytes});
+        return hipSuccess;
     }
 };
 
@@ -1386,12 +1418,13 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
             items.push_back(BuildItem{x, std::min<unsigned long long>(b1, x + kSliceRows), (unsigned int)bk, 1u});
     }
     const uint64_t cap = nb * kRegion;
-    if (t->slots) (void)hipFree(t->slots);
-    if (t->reps) (void)hipFree(t->reps);
-    t->slots = nullptr;
-    t->reps = nullptr;
-    if (hipMalloc(&t->slots, cap * sizeof(Slot)) != hipSuccess ||
-        (general && hipMalloc(&t->reps, cap * sizeof(unsigned long long)) != hipSuccess))
+    release_slots(t, ctx);
+    t->home = ctx;
+    t->slots_bytes = cap * sizeof(Slot);
+    t->reps_bytes = general ? cap * sizeof(unsigned long long) : 0;
+    t->slots = (Slot*)dq::scratch_alloc(ctx, t->slots_bytes);
+    if (general && t->slots) t->reps = (unsigned long long*)dq::scratch_alloc(ctx, t->reps_bytes);
+    if (!t->slots || (general && !t->reps))
         return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
     t->cap = cap;
     t->bits = bits;
@@ -1583,24 +1616,24 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     *done = false;
     hipStream_t s = dq::ctx_stream(ctx);
     const int xgrid = scan_grid((uint64_t)nrows);
-    // pass 1: 256 partitions of cap1 keys (the expected share plus slack for hashing variance and repeats)
-    const unsigned long long cap1 = (unsigned long long)(nrows / kDigitBins) + (unsigned long long)(nrows / kDigitBins) / 32 + 65536;
+    // pass 1: 256 partitions x 8 XCD sub-regions of cap1 keys (the expected share plus slack for hashing variance
+    // and repeated keys)
+    constexpr int kSub = kDigitBins * kXcds;
+    const unsigned long long share = (unsigned long long)(nrows / kSub);
+    const unsigned long long cap1 = share + share / 8 + 16384;
     unsigned long long *gc1 = nullptr, *h1 = nullptr;
     unsigned int* regs = nullptr;
     uint8_t* regs_part = nullptr;
-    FQ_HIP(ctx, buf.alloc((void**)&gc1, sizeof(unsigned long long) * kDigitBins));
-    FQ_HIP(ctx, buf.alloc((void**)&h1, cap1 * kDigitBins * 8));
+    FQ_HIP(ctx, buf.alloc((void**)&gc1, sizeof(unsigned long long) * kSub * kCursorStride));
+    FQ_HIP(ctx, buf.alloc((void**)&h1, cap1 * kSub * 8));
     FQ_HIP(ctx, buf.alloc((void**)&regs, kFastRegs * sizeof(unsigned int)));
     FQ_HIP(ctx, buf.alloc((void**)&regs_part, (size_t)kFastRegs * xgrid));
-    FQ_HIP(ctx, hipMemsetAsync(gc1, 0, sizeof(unsigned long long) * kDigitBins, s));
+    FQ_HIP(ctx, hipMemsetAsync(gc1, 0, sizeof(unsigned long long) * kSub * kCursorStride, s));
     FQ_HIP(ctx, hipMemsetAsync(regs, 0, kFastRegs * sizeof(unsigned int), s));
     FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
     const int inul = t->ks.include_nulls ? 1 : 0;
-    const bool t8k = getenv("DQ_FREQ_P1_8K") != nullptr;  // tuning knob (A/B of the pass-1 tile)
-    if (t8k && elem_size((ElemType)t->ks.cols[0].elem) == 8)
-        hipLaunchKernelGGL((partition1_fast_kernel<kPartTileFast, 8>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
-                           nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
-    else switch (elem_size((ElemType)t->ks.cols[0].elem)) {
+    // (measured: an 8 K-key pass-1 tile runs 8.1 ms against 6.1 ms for 4 K on C4 -- twice the registers)
+    switch (elem_size((ElemType)t->ks.cols[0].elem)) {
         case 8:
             hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 8>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
                                nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
@@ -1622,13 +1655,15 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
                        (const uint8_t*)regs_part, xgrid, kFastRegs, regs);
     FQ_HIP(ctx, hipGetLastError());
     std::vector<unsigned int> hregs(kFastRegs);
-    std::vector<unsigned long long> pcount(kDigitBins);
+    std::vector<unsigned long long> pcount(kSub), pstrided((size_t)kSub * kCursorStride);
     FQ_HIP(ctx, hipMemcpyAsync(hregs.data(), regs, kFastRegs * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
-    FQ_HIP(ctx, hipMemcpyAsync(pcount.data(), gc1, sizeof(unsigned long long) * kDigitBins, hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipMemcpyAsync(pstrided.data(), gc1, sizeof(unsigned long long) * kSub * kCursorStride,
+                               hipMemcpyDeviceToHost, s));
     FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
     FQ_HIP(ctx, hipStreamSynchronize(s));
     if (t->host_ctr.pad[2]) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency fast build: run position out of range");
     if (t->host_ctr.pad[0]) return DQ_OK;  // a partition overflowed: the exact path
+    for (int q = 0; q < kSub; ++q) pcount[q] = pstrided[(size_t)q * kCursorStride];
     unsigned long long n = 0;
     for (unsigned long long c : pcount) n += c;
     const double est = n ? 8.0 * hll_raw_estimate(hregs) : 0.0;  // the sketch holds a 1/8 sample of the keys
@@ -1637,26 +1672,36 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     if (getenv("DQ_DEBUG_FREQ"))
         fprintf(stderr, "[freq fast] rows=%lld n=%llu est=%.1f bits=%d\n", (long long)nrows, n, est, bits);
     if (bits < 8 || bits > kMaxPartBits) return DQ_OK;
+    bits = std::max(bits, 9);  // a partition is 8 sub-regions: the second pass gathers them into buckets
     unsigned long long* h2 = nullptr;
     size_t h2_bytes = 0;
     for (int grow = 0; grow < 8 && bits <= kMaxPartBits; ++grow, ++bits) {
         std::vector<unsigned long long> bstart, bcount;
         const unsigned long long* sorted = h1;
-        if (bits == 8) {
-            bstart.resize(kDigitBins);
-            for (int d = 0; d < kDigitBins; ++d) bstart[d] = (unsigned long long)d * cap1;
-            bcount = pcount;
-        } else {
+        {
             const int bins = 1 << (bits - 8);
             const uint64_t nb = 1ull << bits;
             const unsigned long long per = n / nb;
             const unsigned long long cap2 = per + per / 4 + 2048;
+            // work items: chunks of each sub-region, dealt round-robin over the partitions so the workgroups in flight
+            // reserve on different buckets' counters
+            std::vector<std::vector<FastItem>> by_part(kDigitBins);
+            for (int q = 0; q < kSub; ++q) {
+                const unsigned long long base = (unsigned long long)q * cap1;
+                for (unsigned long long x = 0; x < pcount[q]; x += kPass2Item)
+                    by_part[q / kXcds].push_back(FastItem{base + x, base + std::min<unsigned long long>(pcount[q], x + kPass2Item),
+                                                          (unsigned int)(q / kXcds), 0u});
+            }
             std::vector<FastItem> items;
-            for (int p = 0; p < kDigitBins; ++p)
-                for (unsigned long long x = 0; x < pcount[p]; x += kPass2Item)
-                    items.push_back(FastItem{(unsigned long long)p * cap1 + x,
-                                             (unsigned long long)p * cap1 + std::min<unsigned long long>(pcount[p], x + kPass2Item),
-                                             (unsigned int)p, 0u});
+            for (size_t round = 0;; ++round) {
+                bool any = false;
+                for (int p = 0; p < kDigitBins; ++p)
+                    if (round < by_part[p].size()) {
+                        items.push_back(by_part[p][round]);
+                        any = true;
+                    }
+                if (!any) break;
+            }
             const int nitems = (int)items.size();
             FastItem* ditems = nullptr;
             unsigned long long* gc2 = nullptr;
@@ -1676,14 +1721,18 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
                 hipLaunchKernelGGL((scatter2_fast_kernel<kDigitBins, kPartTileFast>), dim3(nitems), dim3(kFreqBlock), 0, s,
                                    ditems, h1, mask, cap2, gc2, h2, t->ctr);
             FQ_HIP(ctx, hipGetLastError());
-            bcount.resize(nb);
-            FQ_HIP(ctx, hipMemcpyAsync(bcount.data(), gc2, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, s));
+            std::vector<unsigned long long> pb(nb);
+            FQ_HIP(ctx, hipMemcpyAsync(pb.data(), gc2, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, s));
             FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
             FQ_HIP(ctx, hipStreamSynchronize(s));
             if (t->host_ctr.pad[2]) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency fast build: run position out of range");
             if (t->host_ctr.pad[1]) return DQ_OK;  // a bucket overflowed: the exact path
             bstart.resize(nb);
-            for (uint64_t k = 0; k < nb; ++k) bstart[k] = k * cap2;
+            bcount.resize(nb);
+            for (uint64_t k = 0; k < nb; ++k) {
+                bstart[k] = k * cap2;
+                bcount[k] = pb[(k & (kDigitBins - 1)) * (uint64_t)bins + (k >> 8)];
+            }
             sorted = h2;
         }
         bool overflow = false, collision = false;
@@ -1703,7 +1752,7 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
 // general path) restarts with more bucket bits (or a new seed).
 int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
     hipStream_t s = dq::ctx_stream(ctx);
-    DevBuf buf;
+    DevBuf buf(ctx);
     const bool general = !t->fast || t->ks.weights != nullptr;  // carry row indices (representatives / weights)
     const bool no_partition = getenv("DQ_FREQ_NO_PARTITION") != nullptr;
     if (t->fast && !t->ks.weights && !no_partition && nrows >= kFastMinRows && !getenv("DQ_FREQ_EXACT")) {
@@ -2114,7 +2163,7 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
     int rc = build_table(ctx, t, nrows);
     if (rc) {
         cleanup();
-        free_table_buffers(t);
+        free_table_buffers(t, ctx);
         delete t;
         return rc;
     }
@@ -2432,7 +2481,7 @@ int dq_freq_merge(dq_ctx* ctx, const dq_freq_table* a, const dq_freq_table* b, d
     rc = dq_freq_summarize(ctx, b, 0, &sb);
     if (rc) return rc;
     const int64_t ca = sa.num_groups - (sa.null_count ? 1 : 0), cb = sb.num_groups - (sb.null_count ? 1 : 0);
-    DevBuf buf;
+    DevBuf buf(ctx);
     int64_t *k = nullptr, *c = nullptr;
     FQ_HIP(ctx, buf.alloc((void**)&k, (size_t)std::max<int64_t>(ca + cb, 1) * 8));
     FQ_HIP(ctx, buf.alloc((void**)&c, (size_t)std::max<int64_t>(ca + cb, 1) * 8));
@@ -2507,7 +2556,7 @@ int dq_freq_row_counts(dq_ctx* ctx, const dq_freq_table* t, int64_t* counts, int
     T.ks = t->ks;
     T.sentinel = t->host_ctr.sentinel;
     T.bits = t->bits;
-    DevBuf buf;
+    DevBuf buf(ctx);
     long long* d = reinterpret_cast<long long*>(counts);
     const bool dev_out = (flags & DQ_FREQ_PAIRS_DEVICE) != 0;
     if (!dev_out) FQ_HIP(ctx, buf.alloc((void**)&d, (size_t)nrows * 8));
@@ -2528,7 +2577,7 @@ void dq_freq_free(dq_ctx* ctx, dq_freq_table* t) {
     }
     (void)hipSetDevice(t->device);
     (void)hipDeviceSynchronize();
-    free_table_buffers(t);
+    free_table_buffers(t, ctx);
     delete t;
 }
 

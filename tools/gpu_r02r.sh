@@ -3,7 +3,7 @@ R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_grouping.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r02r_tests.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/r02r_tests.log
 [ $rc -ne 0 ] && exit $rc
-cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/r02r_prof" -o run --output-format csv -- python3 "$R/tools/c4_phases.py" 1e9 4 > "$R/gpurun_out/r02r_prof.log" 2>&1; echo "prof rc=$?"
+cd /tmp && DQ_DEBUG_FREQ=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/r02r_prof" -o run --output-format csv -- python3 "$R/tools/c4_phases.py" 1e9 4 > "$R/gpurun_out/r02r_prof.log" 2>&1; echo "prof rc=$?"
 export DQ_FREQ_P1_8K=1
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/r02r_prof8k" -o run --output-format csv -- python3 "$R/tools/c4_phases.py" 1e9 4 > "$R/gpurun_out/r02r_prof8k.log" 2>&1; echo "prof8k rc=$?"
 grep "step 3" "$R/gpurun_out/r02r_prof.log" "$R/gpurun_out/r02r_prof8k.log"
