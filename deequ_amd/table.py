@@ -186,7 +186,11 @@ def _column_from_arrow(name, arr, pa):
         if t.precision > 18:
             raise ValueError("column %s: DecimalType(%d,%d) exceeds the 64-bit unscaled range"
                              % (name, t.precision, t.scale))
-        unscaled = np.array([0 if v is None else int(v.scaleb(t.scale)) for v in arr.to_pylist()], dtype=np.int64)
+        # decimal128 cells are 16-byte little-endian two's complement; precision <= 18 fits the low 8 bytes
+        cells = np.frombuffer(arr.buffers()[1], dtype=np.int64)[2 * arr.offset:2 * (arr.offset + n)]
+        unscaled = np.ascontiguousarray(cells[0::2])
+        if validity is not None:
+            unscaled = np.where(unpack_validity(validity, n), unscaled, 0)
         return Column(name, N.TYPE_DECIMAL, unscaled, validity, decimal_precision=t.precision,
                       decimal_scale=t.scale)
     if pa.types.is_timestamp(t):
