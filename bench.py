@@ -201,8 +201,9 @@ def bench_c4(torch, N, D, ctx, stream, dev, total, steps):
             "value": total / (el / steps), "unit": "rows/s", "ms_per_step": el / steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": ach / PEAK_HBM_GBPS, "traffic": None,
-                         "kernel": "end-to-end build + summary, wall clock per step (partitioned LDS build, "
-                                   "DESIGN.md §3); algorithmic %.1f GB" % ((bpr * total + table_bytes) / 1e9)}}
+                         "kernel": "end-to-end build + summary, wall clock per step (fast grouping: partition1_fast "
+                                   "-> scatter2_fast -> build, DESIGN.md §3); algorithmic %.1f GB (keys read once + "
+                                   "the groups' slots written and read once)" % ((bpr * total + table_bytes) / 1e9)}}
 
 
 def bench_host_streamed(torch, N, D, ctx, dev, rows, steps, chunk_rows=1 << 25):

@@ -62,8 +62,9 @@ constexpr int kPass2Item = 65536;  // keys per work item of the second partition
 constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (fixed: deterministic partials)
 constexpr int kRegion = 4096;      // slots per bucket region (the LDS table of one workgroup)
 // Distinct keys per bucket the bucket count aims at (load <= ~0.63). rocPRIM sorts 8 bits per pass
-// on gfx950, so 1e8 distinct keys take b = 16 (2 passes) rather than 17 (3 passes).
-constexpr int kRegionTarget = 3200;
+// on gfx950, so 1e8 distinct keys take b = 16 (2 passes) rather than 17 (3 passes). (Measured on C4: a
+// target of 3200 -- b = 15, load 0.75 -- halves the table but the LDS probing makes the build 3.2 -> 4.5 ms.)
+constexpr int kRegionTarget = 2600;
 constexpr int64_t kSliceRows = 1 << 18;  // rows per build work item (larger buckets are split)
 
 struct KeyCol {
