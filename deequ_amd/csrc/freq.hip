@@ -1291,6 +1291,15 @@ int ctx_device(dq_ctx* ctx);
 int ctx_fail(dq_ctx* ctx, int code, const char* msg);
 }
 
+// Key cells of a set of groups as host columns (values / offsets / validity) plus their counts: the groups a
+// device owns in a multi-device table over general keys.
+struct GatheredKeys {
+    std::vector<std::vector<uint8_t>> values, validity;
+    std::vector<std::vector<int32_t>> offsets;
+    std::vector<dq_column> cols;
+    std::vector<int64_t> counts;
+};
+
 struct dq_freq_table {
     int device = 0;
     KeySpec ks;
@@ -1306,6 +1315,10 @@ struct dq_freq_table {
     std::vector<dq_freq_table*> parts;
     std::vector<dq_ctx*> part_ctx;
     int64_t total_rows = 0;
+    // general keys on several devices: part j's rows are groups gathered from the shards; part_rows[j][r] is the
+    // row of the caller's table that group r stands for (its smallest row), so exported keys stay row indices
+    std::vector<std::vector<int64_t>> part_rows;
+    std::vector<GatheredKeys> part_keys;  // and the key cells + counts of those groups (MutualInformation)
     // summary folded into the build (default N = the build's numRows), see build_kernel
     int pre_valid = 0;
     int64_t pre_n = -1;
@@ -1971,15 +1984,231 @@ int multi_owner_build(int i, dq_ctx* sub, void* arg) {
                               i == 0 ? o->nulls : 0, &o->parts[i]);
 }
 
+// ---- general keys (strings, several columns) on a multi-device context -------------------------------------
+// Each device pre-aggregates its shard (dq_frequencies_ex on the general path) and exports its groups as
+// (smallest row, count). Every group goes to the owner device picked by a hash of its key; the owner gathers
+// the key cells of its groups (in row order) and builds the weighted table over them, so the groups of one key
+// from every shard merge and the parts are disjoint. Groups are few next to rows, so their key bytes travel
+// through host memory; the fixed-width path above moves (key, count) pairs device to device over RCCL.
+
+// Grouping equality on the host: canonical fixed-width bits (NaN canonical, -0.0 != 0.0), string bytes, NULL a
+// fixed component (or "NullValue" for a Histogram string column) -- equal keys hash equally.
+uint64_t host_key_hash(const dq_column* columns, const int32_t* key_columns, int nkeys, int64_t r, bool null_is_value) {
+    uint64_t acc = 0x243F6A8885A308D3ULL;
+    for (int i = 0; i < nkeys; ++i) {
+        const dq_column& c = columns[key_columns[i]];
+        const bool valid = !c.validity || ((c.validity[r >> 3] >> (r & 7)) & 1);
+        uint64_t ch;
+        if (c.spark_type == DQ_TYPE_STRING) {
+            if (valid) {
+                const int32_t o0 = c.offsets[r], o1 = c.offsets[r + 1];
+                ch = xxh_bytes(static_cast<const uint8_t*>(c.values) + o0, o1 - o0, 42);
+            } else {
+                ch = null_is_value ? xxh_bytes((const uint8_t*)"NullValue", 9, 42) : 0x6A09E667F3BCC909ULL;
+            }
+        } else if (valid) {
+            uint64_t v;
+            switch (elem_of(c.spark_type)) {
+                case ET_U8: v = static_cast<const uint8_t*>(c.values)[r] ? 1ull : 0ull; break;
+                case ET_I8: v = (uint64_t)(int64_t) static_cast<const int8_t*>(c.values)[r]; break;
+                case ET_I16: v = (uint64_t)(int64_t) static_cast<const int16_t*>(c.values)[r]; break;
+                case ET_I32: v = (uint64_t)(int64_t) static_cast<const int32_t*>(c.values)[r]; break;
+                case ET_F32: v = (uint64_t)float_to_int_bits(static_cast<const float*>(c.values)[r]); break;
+                case ET_F64: v = double_to_long_bits(static_cast<const double*>(c.values)[r]); break;
+                default: v = static_cast<const uint64_t*>(c.values)[r]; break;
+            }
+            ch = mix64(v);
+        } else {
+            ch = 0x6A09E667F3BCC909ULL;
+        }
+        acc = mix64(acc + 0xC2B2AE3D27D4EB4FULL * (uint64_t)(i + 1) + ch);
+    }
+    return acc;
+}
+
+
+void gather_keys(const dq_column* columns, const int32_t* key_columns, int nkeys, const std::vector<int64_t>& rows,
+                 GatheredKeys& g) {
+    const size_t n = rows.size();
+    g.values.assign(nkeys, {});
+    g.validity.assign(nkeys, {});
+    g.offsets.assign(nkeys, {});
+    g.cols.assign(nkeys, dq_column());
+    for (int i = 0; i < nkeys; ++i) {
+        const dq_column& c = columns[key_columns[i]];
+        dq_column& o = g.cols[i];
+        o = c;
+        o.flags = 0;
+        o.length = (int64_t)n;
+        std::vector<uint8_t>& vb = g.validity[i];
+        vb.assign((n + 7) / 8 + 8, 0);
+        bool all = true;
+        for (size_t k = 0; k < n; ++k) {
+            const int64_t r = rows[k];
+            const bool valid = !c.validity || ((c.validity[r >> 3] >> (r & 7)) & 1);
+            if (valid) vb[k >> 3] |= (uint8_t)(1u << (k & 7)); else all = false;
+        }
+        o.validity = all ? nullptr : vb.data();
+        if (c.spark_type == DQ_TYPE_STRING) {
+            std::vector<int32_t>& off = g.offsets[i];
+            off.assign(n + 1, 0);
+            size_t total = 0;
+            for (size_t k = 0; k < n; ++k) {
+                total += (size_t)(c.offsets[rows[k] + 1] - c.offsets[rows[k]]);
+                off[k + 1] = (int32_t)total;
+            }
+            g.values[i].assign(total + 16, 0);
+            for (size_t k = 0; k < n; ++k) {
+                const int32_t o0 = c.offsets[rows[k]], len = c.offsets[rows[k] + 1] - o0;
+                if (len) memcpy(g.values[i].data() + off[k], static_cast<const uint8_t*>(c.values) + o0, (size_t)len);
+            }
+            o.offsets = off.data();
+        } else {
+            const int w = std::max(1, elem_size(elem_of(c.spark_type)));
+            g.values[i].assign(n * w + 16, 0);
+            for (size_t k = 0; k < n; ++k)
+                memcpy(g.values[i].data() + k * w, static_cast<const uint8_t*>(c.values) + rows[k] * w, (size_t)w);
+            o.offsets = nullptr;
+        }
+        o.values = g.values[i].data();
+    }
+}
+
+struct GeneralJob {
+    const dq_column* columns;       // the caller's (host) columns
+    std::vector<std::vector<dq_column>> shard_cols;
+    std::vector<int64_t> row0, rows;
+    int ncols, nkeys;
+    const int32_t* key_columns;
+    const dq_freq_options* opt;
+    int ndev;
+    bool null_is_value;
+    std::vector<std::vector<int64_t>> grp_rows, grp_counts;  // per device: exported groups (global rows)
+    std::vector<int64_t> local_rows, local_nulls;
+    // per owner
+    std::vector<std::vector<int64_t>> own_rows, own_counts;
+    std::vector<GatheredKeys> own_keys;
+    std::vector<dq_freq_table*> parts;
+};
+
+int general_local(int i, dq_ctx* sub, void* arg) {
+    GeneralJob* j = static_cast<GeneralJob*>(arg);
+    dq_freq_table* t = nullptr;
+    int rc = dq_frequencies_ex(sub, j->shard_cols[i].data(), j->ncols, j->rows[i], j->key_columns, j->nkeys, j->opt, &t);
+    if (rc) return rc;
+    dq_freq_summary su;
+    rc = dq_freq_summarize(sub, t, 0, &su);
+    if (!rc) {
+        j->local_rows[i] = su.num_rows;
+        j->local_nulls[i] = su.null_count;
+        const int64_t g = su.num_groups - (su.null_count ? 1 : 0);
+        j->grp_rows[i].assign((size_t)std::max<int64_t>(g, 1), 0);
+        j->grp_counts[i].assign((size_t)std::max<int64_t>(g, 1), 0);
+        const int64_t got = dq_freq_export(sub, t, g, j->grp_rows[i].data(), j->grp_counts[i].data());
+        if (got < 0) {
+            rc = (int)got;
+        } else {
+            j->grp_rows[i].resize((size_t)got);
+            j->grp_counts[i].resize((size_t)got);
+            for (int64_t& r : j->grp_rows[i]) r += j->row0[i];
+        }
+    }
+    dq_freq_free(sub, t);
+    return rc;
+}
+
+int general_owner(int i, dq_ctx* sub, void* arg) {
+    GeneralJob* j = static_cast<GeneralJob*>(arg);
+    GatheredKeys& g = j->own_keys[i];
+    gather_keys(j->columns, j->key_columns, j->nkeys, j->own_rows[i], g);
+    g.counts = j->own_counts[i];
+    std::vector<int32_t> keys(j->nkeys);
+    for (int k = 0; k < j->nkeys; ++k) keys[k] = k;
+    dq_freq_options o = *j->opt;
+    o.weights = j->own_counts[i].empty() ? nullptr : j->own_counts[i].data();
+    o.weights_device = 0;
+    return dq_frequencies_ex(sub, g.cols.data(), j->nkeys, (int64_t)j->own_rows[i].size(), keys.data(), j->nkeys, &o,
+                             &j->parts[i]);
+}
+
+int multi_frequencies_general(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows,
+                              const int32_t* key_columns, int nkeys, const dq_freq_options* opt, dq_freq_table** out) {
+    const int n = (int)ctx->subs.size();
+    GeneralJob j;
+    j.columns = columns;
+    j.ncols = ncols;
+    j.nkeys = nkeys;
+    j.key_columns = key_columns;
+    j.opt = opt;
+    j.ndev = n;
+    j.null_is_value = (opt->flags & DQ_FREQ_INCLUDE_NULLS) && nkeys == 1 && columns[key_columns[0]].spark_type == DQ_TYPE_STRING;
+    j.shard_cols.assign(n, std::vector<dq_column>(std::max(ncols, 1)));
+    j.row0.assign(n, 0);
+    j.rows.assign(n, 0);
+    j.grp_rows.assign(n, {});
+    j.grp_counts.assign(n, {});
+    j.local_rows.assign(n, 0);
+    j.local_nulls.assign(n, 0);
+    std::vector<std::vector<std::vector<int32_t>>> scratch(n);
+    for (int i = 0; i < n; ++i) {
+        dq::shard_bounds(nrows, n, i, &j.row0[i], &j.rows[i]);
+        dq::shard_columns(columns, ncols, j.row0[i], j.rows[i], j.shard_cols[i].data(), scratch[i]);
+    }
+    int rc = dq::for_each_device(ctx, general_local, &j);
+    if (rc) return rc;
+    // owner of every group; each owner's groups in row order (its smallest row stays the group's smallest row)
+    j.own_rows.assign(n, {});
+    j.own_counts.assign(n, {});
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> own(n);
+    for (int i = 0; i < n; ++i)
+        for (size_t k = 0; k < j.grp_rows[i].size(); ++k) {
+            const int64_t r = j.grp_rows[i][k];
+            const int dst = (int)((mix64(host_key_hash(columns, key_columns, nkeys, r, j.null_is_value)) >> 32) % (uint64_t)n);
+            own[dst].push_back({r, j.grp_counts[i][k]});
+        }
+    for (int i = 0; i < n; ++i) {
+        std::sort(own[i].begin(), own[i].end());
+        for (const auto& rc_ : own[i]) {
+            j.own_rows[i].push_back(rc_.first);
+            j.own_counts[i].push_back(rc_.second);
+        }
+    }
+    j.parts.assign(n, nullptr);
+    j.own_keys.assign(n, GatheredKeys());
+    rc = dq::for_each_device(ctx, general_owner, &j);
+    if (rc) {
+        for (int i = 0; i < n; ++i)
+            if (j.parts[i]) dq_freq_free(ctx->subs[i], j.parts[i]);
+        return rc;
+    }
+    dq_freq_table* t = new dq_freq_table();
+    t->device = ctx->device;
+    memset(&t->ks, 0, sizeof(t->ks));
+    t->fast = 0;
+    t->key_type = nkeys == 1 ? columns[key_columns[0]].spark_type : 0;
+    t->parts = j.parts;
+    t->part_ctx = ctx->subs;
+    t->part_rows = std::move(j.own_rows);
+    t->part_keys = std::move(j.own_keys);  // (moving the inner vectors keeps the column pointers valid)
+    int64_t total_rows = 0;
+    for (int i = 0; i < n; ++i) total_rows += j.local_rows[i];
+    t->total_rows = total_rows;
+    *out = t;
+    return DQ_OK;
+}
+
 int multi_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
                       int nkeys, const dq_freq_options* opt, dq_freq_table** out) {
-    if (nkeys != 1 || key_columns[0] < 0 || key_columns[0] >= ncols || elem_of(columns[key_columns[0]].spark_type) == ET_NONE ||
-        opt->weights)
-        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED,
-                            "multi-device grouping: one fixed-width key column (strings / several keys: one device per context)");
     for (int c = 0; c < ncols; ++c)
         if (columns[c].flags & DQ_COL_DEVICE)
             return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "multi-device grouping takes host columns");
+    if (opt->weights)
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "multi-device grouping: weighted input takes a one-device context");
+    for (int k = 0; k < nkeys; ++k)
+        if (key_columns[k] < 0 || key_columns[k] >= ncols)
+            return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_frequencies: bad key column");
+    if (nkeys != 1 || elem_of(columns[key_columns[0]].spark_type) == ET_NONE)
+        return multi_frequencies_general(ctx, columns, ncols, nrows, key_columns, nkeys, opt, out);
     const int n = (int)ctx->subs.size();
     MultiFreqJob j;
     j.ncols = ncols;
@@ -2309,6 +2538,8 @@ int64_t dq_freq_export(dq_ctx* ctx, const dq_freq_table* t, int64_t capacity, in
         for (size_t i = 0; i < t->parts.size() && n < capacity; ++i) {
             const int64_t got = dq_freq_export(t->part_ctx[i], t->parts[i], capacity - n, keys + n, counts + n);
             if (got < 0) return dq::ctx_fail(ctx, (int)got, t->part_ctx[i]->err.c_str());
+            if (!t->part_rows.empty())
+                for (int64_t x = n; x < n + got; ++x) keys[x] = t->part_rows[i][(size_t)keys[x]];
             n += got;
         }
         return n;
@@ -2340,7 +2571,8 @@ int64_t dq_freq_top(dq_ctx* ctx, const dq_freq_table* t, int64_t k, int64_t* key
         for (size_t i = 0; i < t->parts.size(); ++i) {
             const int64_t got = dq_freq_top(t->part_ctx[i], t->parts[i], k, pk.data(), pc.data());
             if (got < 0) return dq::ctx_fail(ctx, (int)got, t->part_ctx[i]->err.c_str());
-            for (int64_t x = 0; x < got; ++x) all.push_back({pc[x], pk[x]});
+            for (int64_t x = 0; x < got; ++x)
+                all.push_back({pc[x], t->part_rows.empty() ? pk[x] : t->part_rows[i][(size_t)pk[x]]});
         }
         std::stable_sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
         const int64_t n = std::min<int64_t>(k, (int64_t)all.size());
@@ -2501,14 +2733,93 @@ int dq_freq_merge(dq_ctx* ctx, const dq_freq_table* a, const dq_freq_table* b, d
     return rc;
 }
 
+namespace {
+int mi_tables(dq_ctx* ctx, const dq_freq_table* joint, const dq_freq_table* x, const dq_freq_table* y, double* mi,
+              int32_t* present);
+
+// A multi-device (x, y) table: its parts hold disjoint groups. The joint groups are gathered into one weighted
+// table on the context's first device and the marginals are grouped from them -- the reference's own marginal
+// tables (jointStats.groupBy(col).agg(sum(count)), A/MutualInformation.scala:50-58).
+int mi_composite(dq_ctx* ctx, const dq_freq_table* joint, double* mi, int32_t* present) {
+    if (joint->part_keys.size() != joint->parts.size() || joint->part_keys.empty() || joint->part_keys[0].cols.size() != 2)
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_mutual_information: needs a two-column joint table");
+    // concatenate the parts' groups
+    GatheredKeys all;
+    all.values.assign(2, {});
+    all.validity.assign(2, {});
+    all.offsets.assign(2, {});
+    all.cols.assign(2, dq_column());
+    size_t g = 0;
+    for (const GatheredKeys& p : joint->part_keys) g += p.counts.size();
+    for (const GatheredKeys& p : joint->part_keys) all.counts.insert(all.counts.end(), p.counts.begin(), p.counts.end());
+    for (int c = 0; c < 2; ++c) {
+        const dq_column& c0 = joint->part_keys[0].cols[c];
+        dq_column& o = all.cols[c];
+        o = c0;
+        o.length = (int64_t)g;
+        all.validity[c].assign((g + 7) / 8 + 8, 0);
+        bool any_null = false;
+        size_t at = 0;
+        if (c0.spark_type == DQ_TYPE_STRING) all.offsets[c].assign(g + 1, 0);
+        const int w = std::max(1, elem_size(elem_of(c0.spark_type)));
+        for (const GatheredKeys& p : joint->part_keys) {
+            const dq_column& pc = p.cols[c];
+            const size_t pn = p.counts.size();
+            for (size_t k = 0; k < pn; ++k) {
+                const bool valid = !pc.validity || ((pc.validity[k >> 3] >> (k & 7)) & 1);
+                if (valid) all.validity[c][(at + k) >> 3] |= (uint8_t)(1u << ((at + k) & 7)); else any_null = true;
+            }
+            if (c0.spark_type == DQ_TYPE_STRING) {
+                const size_t base = all.values[c].size();
+                const size_t bytes = pn ? (size_t)pc.offsets[pn] : 0;
+                all.values[c].insert(all.values[c].end(), static_cast<const uint8_t*>(pc.values),
+                                     static_cast<const uint8_t*>(pc.values) + bytes);
+                for (size_t k = 0; k < pn; ++k) all.offsets[c][at + k + 1] = (int32_t)(base + pc.offsets[k + 1]);
+            } else {
+                all.values[c].insert(all.values[c].end(), static_cast<const uint8_t*>(pc.values),
+                                     static_cast<const uint8_t*>(pc.values) + pn * w);
+            }
+            at += pn;
+        }
+        all.values[c].resize(all.values[c].size() + 16, 0);
+        o.values = all.values[c].data();
+        o.validity = any_null ? all.validity[c].data() : nullptr;
+        o.offsets = c0.spark_type == DQ_TYPE_STRING ? all.offsets[c].data() : nullptr;
+        o.flags = 0;
+    }
+    dq_freq_options opt;
+    memset(&opt, 0, sizeof(opt));
+    opt.weights = all.counts.empty() ? nullptr : all.counts.data();
+    const int32_t kj[2] = {0, 1}, kx[1] = {0}, ky[1] = {1};
+    dq_freq_table *J = nullptr, *X = nullptr, *Y = nullptr;
+    dq_ctx* c0 = ctx->subs.empty() ? ctx : ctx->subs[0];  // one device: the first of the context
+    int rc = dq_frequencies_ex(c0, all.cols.data(), 2, (int64_t)g, kj, 2, &opt, &J);
+    if (!rc) rc = dq_frequencies_ex(c0, all.cols.data(), 2, (int64_t)g, kx, 1, &opt, &X);
+    if (!rc) rc = dq_frequencies_ex(c0, all.cols.data(), 2, (int64_t)g, ky, 1, &opt, &Y);
+    if (!rc) rc = mi_tables(c0, J, X, Y, mi, present);
+    if (rc && c0 != ctx) ctx->err = c0->err;
+    if (J) dq_freq_free(c0, J);
+    if (X) dq_freq_free(c0, X);
+    if (Y) dq_freq_free(c0, Y);
+    return rc;
+}
+}  // namespace
+
 int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq_freq_table* x,
                                const dq_freq_table* y, double* mi, int32_t* present) {
     if (!ctx || !joint || !x || !y || !mi || !present)
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_mutual_information: invalid arguments");
+    if (!joint->parts.empty()) return mi_composite(ctx, joint, mi, present);
     if (joint->fast || joint->ks.ncols != 2 || !joint->reps || x->ks.ncols != 1 || y->ks.ncols != 1 ||
         x->ks.weights || y->ks.weights || joint->ks.weights)
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT,
                             "dq_freq_mutual_information: needs the (x, y) table and the x / y tables of the same rows");
+    return mi_tables(ctx, joint, x, y, mi, present);
+}
+
+namespace {
+int mi_tables(dq_ctx* ctx, const dq_freq_table* joint, const dq_freq_table* x, const dq_freq_table* y, double* mi,
+              int32_t* present) {
     FQ_HIP(ctx, hipSetDevice(joint->device));
     hipStream_t s = dq::ctx_stream(ctx);
     LookupTable X, Y;
@@ -2541,6 +2852,7 @@ int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq
     *present = groups > 0 ? 1 : 0;  // sum over zero joined rows is NULL (A/MutualInformation.scala:82-86)
     return DQ_OK;
 }
+}  // namespace
 
 int dq_freq_row_counts(dq_ctx* ctx, const dq_freq_table* t, int64_t* counts, int64_t nrows, uint32_t flags) {
     if (!ctx || !t || (!counts && nrows > 0))

@@ -86,13 +86,40 @@ def test_sharded_frequencies_match_oracle(multi, kind):
         assert m.value.isSuccess, (a, m)
 
 
-def test_sharded_strings_grouping_is_refused_loudly(multi):
-    from deequ_amd.table import _column_from_pylist
-    t = Table([_column_from_pylist("s", "string", ["a", "b", "a"])])
-    m = D.Uniqueness(["s"]).calculate(t)
-    if multi.num_devices() == 1:
-        return
-    assert m.value.isFailure and "multi-device grouping" in str(m.value.failed)
+@pytest.mark.parametrize("cols", [["s"], ["s", "k"], ["k", "d"]])
+def test_sharded_general_grouping_matches_oracle(multi, cols):
+    """String / multi-column keys on a multi-device context: per-device pre-aggregation, groups to their hash owner,
+    weighted owner tables; exported keys are rows of the caller's table (the group's smallest row)."""
+    from test_distributed_gloo import mixed_table
+    t = mixed_table(30_000, seed=8)
+    for include_nulls in ((False, True) if len(cols) == 1 else (False,)):
+        ft = engine.frequencies(t, cols, include_nulls=include_nulls)
+        freq, nrows = O.frequencies(t, cols, include_nulls=include_nulls)
+        exp = O.grouping_summary(freq, nrows)
+        s = ft.summary(None)
+        assert (s["num_rows"], s["num_groups"], s["num_unique"]) == (nrows, exp["num_groups"], exp["num_unique"])
+        assert abs(s["entropy"] - exp["entropy"]) <= 1e-12 * exp["entropy"]
+        got = {tuple(O._group_key(x) for x in key): c for key, c in ft.to_dict().items()}
+        assert got == freq
+        keys, counts = ft.export_raw()
+        py = list(zip(*[t[n].to_pylist() for n in cols]))
+        first = {}
+        for r, row in enumerate(py):
+            first.setdefault(tuple(O._group_key(x) for x in row), r)
+        for r, c in zip(keys.tolist(), counts.tolist()):  # a group's key is its smallest row
+            key = tuple(O._group_key(x) for x in py[r])
+            assert freq[key] == c and first[key] == r
+        assert [c for _, c in ft.top(7)] == sorted(freq.values(), reverse=True)[:7]
+
+
+def test_sharded_mutual_information_matches_oracle(multi):
+    from test_distributed_gloo import mixed_table, _oracle_mi
+    t = mixed_table(30_000, seed=12)
+    for cols in (["s", "k"], ["k", "d"]):
+        m = D.MutualInformation(cols).calculate(t)
+        assert m.value.isSuccess, m
+        exp = _oracle_mi(t, cols)
+        assert abs(m.value.get() - exp) <= 1e-12 * max(1.0, abs(exp)), (cols, m.value.get(), exp)
 
 
 def test_scan_sharded_over_device_resident_shards():
