@@ -141,6 +141,28 @@ __device__ __forceinline__ void corr_merge(CorrPartial& a, const CorrPartial& b)
     a.n = newN;
 }
 
+// corr_merge for the per-lane batch fold (b.n >= 1): one refined reciprocal of the new count replaces the two
+// divisions (the batch folds run once per 8 rows per lane; the cross-lane folds keep corr_merge).
+__device__ __forceinline__ void corr_merge_batch(CorrPartial& a, const CorrPartial& b) {
+    if (a.n == 0.0) {
+        a = b;
+        return;
+    }
+    const double n1 = a.n, n2 = b.n;
+    const double newN = n1 + n2;
+    const double rn = rcp_refined(newN);
+    const double dx = b.xa - a.xa;
+    const double dxN = dx * rn;
+    const double dy = b.ya - a.ya;
+    const double dyN = dy * rn;
+    a.xa = a.xa + dxN * n2;
+    a.ya = a.ya + dyN * n2;
+    a.ck = a.ck + b.ck + dx * dyN * n1 * n2;
+    a.xm = a.xm + b.xm + dx * dxN * n1 * n2;
+    a.ym = a.ym + b.ym + dy * dyN * n1 * n2;
+    a.n = newN;
+}
+
 __device__ __forceinline__ void slot_init(SlotPartial& p) {
     col_init(p.c[0]);
     col_init(p.c[1]);
@@ -521,6 +543,11 @@ __device__ __forceinline__ void to_partial(ColPartial& p, const IAcc& a) {
 // counted only in that (rare, divergent) case: Spark orders NaN above every double, which the finaliser
 // applies through nnan (max = NaN if nnan > 0, min = NaN if nnan == n). An inf - inf batch sum also lands
 // in that branch and counts zero NaNs.
+// 1.0 for a kept row of the batch mask, 0.0 otherwise (the low word of both is 0: one 32-bit select).
+__device__ __forceinline__ double on_factor(uint32_t m, int k) {
+    return as_f64((uint64_t)(((m >> k) & 1u) ? 0x3FF00000u : 0u) << 32);
+}
+
 __device__ __forceinline__ void accumulate(FAcc& a, const uint64_t (&v)[8], uint32_t m, uint32_t flags) {
     const int cnt = __popc(m);
     if (cnt == 0) return;
@@ -553,7 +580,8 @@ __device__ __forceinline__ void accumulate(FAcc& a, const uint64_t (&v)[8], uint
             double m2b = 0.0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const double d = ((m >> k) & 1u) ? xz[k] - mb : 0.0;
+                // (x - mean) * {1.0, 0.0}: one 32-bit select builds the factor, exact for the kept rows
+                const double d = (xz[k] - mb) * on_factor(m, k);
                 m2b = __builtin_fma(d, d, m2b);
             }
             moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
@@ -585,14 +613,14 @@ __device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint
         double s = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            xd[k] = (double)(int64_t)v[k];
-            s += ((m >> k) & 1u) ? xd[k] : 0.0;
+            xd[k] = (double)(int64_t)v[k];       // finite for every row, kept or not
+            s = __builtin_fma(xd[k], on_factor(m, k), s);  // x * 1.0 + s rounds like x + s; x * 0.0 adds +-0
         }
         const double mb = s * rcp_refined((double)cnt);
         double m2b = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const double d = ((m >> k) & 1u) ? xd[k] - mb : 0.0;
+            const double d = (xd[k] - mb) * on_factor(m, k);
             m2b = __builtin_fma(d, d, m2b);
         }
         moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
@@ -644,28 +672,34 @@ __device__ __forceinline__ void accumulate_corr(CorrPartial& c, const uint64_t (
                                                 uint32_t m) {
     const int cnt = __popc(m);
     if (cnt == 0) return;
+    // masked rows become 0.0 once (their bits may be anything, NaN included); the deviations are then masked by
+    // a {1.0, 0.0} factor and accumulated with fma
+    double xv[8], yv[8];
     double sx = 0.0, sy = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const bool on = (m >> k) & 1u;
-        sx += on ? to_double(x[k], FX) : 0.0;
-        sy += on ? to_double(y[k], FY) : 0.0;
+        xv[k] = on ? to_double(x[k], FX) : 0.0;
+        yv[k] = on ? to_double(y[k], FY) : 0.0;
+        sx += xv[k];
+        sy += yv[k];
     }
     CorrPartial b;
     b.n = (double)cnt;
-    b.xa = sx / b.n;
-    b.ya = sy / b.n;
+    const double inv = rcp_refined(b.n);  // one reciprocal for both means (instead of two IEEE divisions)
+    b.xa = sx * inv;
+    b.ya = sy * inv;
     b.ck = b.xm = b.ym = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const bool on = (m >> k) & 1u;
-        const double dx = to_double(x[k], FX) - b.xa;
-        const double dy = to_double(y[k], FY) - b.ya;
-        b.ck += on ? dx * dy : 0.0;
-        b.xm += on ? dx * dx : 0.0;
-        b.ym += on ? dy * dy : 0.0;
+        const double f = on_factor(m, k);
+        const double dx = xv[k] - b.xa, dy = yv[k] - b.ya;
+        const double dxf = dx * f, dyf = dy * f;
+        b.ck = __builtin_fma(dxf, dy, b.ck);
+        b.xm = __builtin_fma(dxf, dx, b.xm);
+        b.ym = __builtin_fma(dyf, dy, b.ym);
     }
-    corr_merge(c, b);
+    corr_merge_batch(c, b);
 }
 
 // Hash class of a Spark type for XxHash64Function: 0 = hashInt of the int value, 1 = hashInt of the
