@@ -182,3 +182,55 @@ def test_c3_hll_and_correlation_at_scale_sharded():
     assert sh[analyzers[0]].words == cols[0]["words"]
     _check_corr(sh[analyzers[1]], corrs[0], "C3 sharded")
     assert (sh[analyzers[2]].numMatches, sh[analyzers[2]].count) == (cols[0]["n"], ROWS)
+
+
+def test_c4_full_scale_closed_forms_histogram_and_null_variant(monkeypatch):
+    """BASELINE C4 at full size: 1e9 int64 keys, exactly 1e8 distinct (5e7 x 19 + 5e7 x 1).
+    Closed forms exact (entropy within 1e-12 of the fsum value), Histogram with 1e8 bins whose top-1000 counts are
+    all 19 (a multiset: ties), ratio = 19 / 1e9. The 1 %-null variant has no closed form: its fast build (fixed
+    buckets, atomically reserved runs) must equal the exactly-counted build -- the path pinned against the oracle at
+    smaller sizes -- in the summary, the top-1000 and order-free checksums of the whole export."""
+    import torch
+    R = ROWS
+    Dn = R // 10
+    ctx = engine.ctx()
+    keys = torch.empty(R, dtype=torch.int64, device="cuda")
+    ctx.synth_freq_keys(R, Dn, 0, R, keys.data_ptr())
+    ctx.synchronize()
+    col = Column("k", N.TYPE_LONG, None, None, length=R)
+    col.device = {"values": keys}
+    t = Table([col])
+    ft = engine.frequencies(t, ["k"])
+    s = ft.summary(None)
+    half = Dn // 2
+    big = (R - half) / half
+    ent = math.fsum([-half * (big / R) * math.log(big / R), -half * (1 / R) * math.log(1 / R)])
+    assert (s["num_rows"], s["num_groups"], s["num_unique"], s["max_count"]) == (R, Dn, half, int(big))
+    assert abs(s["entropy"] - ent) <= 1e-12 * ent
+    del ft
+    h = D.Histogram("k", None, 1000).calculate(t).value.get()
+    assert h.numberOfBins == Dn and len(h.values) == 1000
+    assert all(v.absolute == int(big) and v.ratio == big / R for v in h.values.values())
+    valid = torch.zeros((R + 63) // 64 * 8, dtype=torch.uint8, device="cuda")
+    ctx.synth_validity(0x5EED0C4, 0, R, 10, valid.data_ptr())
+    ctx.synchronize()
+    col.device["validity"] = valid
+    got = []
+    for exact in (False, True):
+        if exact:
+            monkeypatch.setenv("DQ_FREQ_EXACT", "1")
+        ft = engine.frequencies(t, ["k"])
+        sm = ft.summary(None)
+        k, c = ft.export_raw()
+        ku = k.view(np.uint64)
+        cu = c.astype(np.uint64)
+        with np.errstate(over="ignore"):
+            chk = (int(ku.sum(dtype=np.uint64)), int((ku * cu).sum(dtype=np.uint64)), int((ku ^ (cu << np.uint64(40))).sum(dtype=np.uint64)))
+        got.append(((sm["num_rows"], sm["num_groups"], sm["num_unique"], sm["max_count"]), sm["entropy"],
+                    sorted(x for _, x in ft.top(1000)), chk, int(c.sum()), len(k)))
+        del ft, k, c
+    monkeypatch.delenv("DQ_FREQ_EXACT")
+    (a, ea, ta, ca, na, ga), (b, eb, tb, cb, nb, gb) = got
+    assert a == b and ta == tb and ca == cb and na == nb == a[0] and ga == gb == a[1]
+    assert abs(ea - eb) <= 1e-12 * eb
+    assert 0.985 * R < a[0] < 0.995 * R  # ~1 % nulls dropped
