@@ -957,7 +957,7 @@ __global__ void region_init_kernel(const BuildItem* __restrict__ items, int nite
 // time per lane (independent global loads in flight), and each probe is a single LDS compare-and-
 // swap EMPTY -> h whose returned value says inserted / found / occupied.
 constexpr int kBuildBlock = 512;
-constexpr int kBuildUnroll = 4;
+constexpr int kBuildUnroll = 8;
 
 // LDS counts: 32-bit for row counting (a work item holds <= kSliceRows rows), 64-bit for weighted input.
 template <typename C>
