@@ -196,11 +196,22 @@ def bench_c4(torch, N, D, ctx, stream, dev, total, steps):
     bpr = 8.0
     table_bytes = 2 * 16 * distinct  # write + read of the 16-B slots of each group
     ach = (bpr * total + table_bytes) / (el / steps) / 1e9
+    traffic = None
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "c4_traffic_*.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if int(d.get("rows", -1)) == total:
+            traffic = (d["total_GB_per_call"], os.path.relpath(path, ROOT))
     return {"workload": "C4: computeFrequencies + Uniqueness/Distinctness/UniqueValueRatio/CountDistinct/Entropy "
                         "aggregation, 1e9 int64 keys, 1e8 distinct; closed forms exact",
             "value": total / (el / steps), "unit": "rows/s", "ms_per_step": el / steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "frac": ach / PEAK_HBM_GBPS, "traffic": traffic[0] if traffic else None,
+                         "traffic_unit": "GB per build (HBM FETCH+WRITE from rocprofv3 PMC, %s)"
+                                         % (traffic[1] if traffic else "not measured at this size"),
                          "kernel": "end-to-end build + summary, wall clock per step (fast grouping: partition1_fast "
                                    "-> scatter2_fast -> build, DESIGN.md §3); algorithmic %.1f GB (keys read once + "
                                    "the groups' slots written and read once)" % ((bpr * total + table_bytes) / 1e9)}}
