@@ -10,10 +10,12 @@ generators before timing.
 The same JSON line carries `secondary` measurements of the other BASELINE workloads, each timed the
 same way (its own steps, HIP events on the scan stream, its own roofline):
   suite10  the north-star 10-analyzer suite over the same 8 columns (C2 ops + Compliance(c > 0) +
-           ApproxCountDistinct + Correlation(c_2k, c_2k+1): 73 ops), every rank count;
+           ApproxCountDistinct + Correlation(c_2k, c_2k+1): 69 ops), every rank count;
   c3       ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 1e9 rows (N = 1);
   c4       the grouping analyzers' frequency table (computeFrequencies + the fused table aggregation) on
-           1e9 int64 keys with exactly 1e8 distinct, closed forms checked (N = 1).
+           1e9 int64 keys with exactly 1e8 distinct, closed forms checked (N = 1);
+  c2_host_streamed  the C2 suite over pinned host columns streamed through HBM (dq_scan_streamed): the
+           end-to-end rate including the host link, never the headline value (N = 1).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--no-secondary]
 """
