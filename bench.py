@@ -219,6 +219,76 @@ def bench_c4(torch, N, D, ctx, stream, dev, total, steps):
                                    "the groups' slots written and read once)" % ((bpr * total + table_bytes) / 1e9)}}
 
 
+C5_NUMERIC = [("d_dyad", 1), ("d_unif", 2), ("d_n100", 3), ("d_gauss", 6), ("d_corr", 7),
+              ("l_i32a", 4), ("l_key30a", 5), ("l_i32b", 4), ("l_key30b", 5), ("l_i32c", 4)]
+C5_STRINGS = [("s_cat50", 101), ("s_bool", 102), ("s_cat100", 103), ("s_int", 104), ("s_dec", 105), ("s_mixnum", 106),
+              ("s_text0", 107), ("s_text1", 107), ("s_text2", 107), ("s_text3", 107)]
+
+
+def c5_shard(torch, N, ctx, dev, rows):
+    """One GPU's shard of BASELINE config C5 generated in HBM: 5 fp64 + 5 int64 columns (the C2 generators) and 10
+    UTF-8 string columns (3 low-cardinality, 3 numeric-looking, 4 free text 1-20 characters), 5 % nulls each."""
+    from deequ_amd.table import Table, Column
+    cols, nbytes = [], 0
+    for j, (name, kind) in enumerate(C5_NUMERIC):
+        dt = torch.float64 if kind in (1, 2, 3, 6, 7) else torch.int64
+        v = torch.empty(rows, dtype=dt, device=dev)
+        ctx.synth_column(kind, 0xC5000000 + j, 0, rows, v.data_ptr())
+        c = Column(name, N.TYPE_DOUBLE if dt == torch.float64 else N.TYPE_LONG, None, None, length=rows)
+        c.device = {"values": v}
+        cols.append(c)
+        nbytes += 8 * rows
+    for j, (name, kind) in enumerate(C5_STRINGS):
+        off = torch.empty(rows + 1, dtype=torch.int32, device=dev)
+        total = ctx.synth_strings(kind, 0xC5100000 + j, 0, rows, off.data_ptr())
+        data = torch.zeros(total + 16, dtype=torch.uint8, device=dev)
+        ctx.synth_strings(kind, 0xC5100000 + j, 0, rows, off.data_ptr(), data.data_ptr())
+        c = Column(name, N.TYPE_STRING, None, None, length=rows)
+        c.device = {"values": data, "offsets": off}
+        cols.append(c)
+        nbytes += total + 4 * rows
+    for j, c in enumerate(cols):
+        m = torch.zeros((rows + 63) // 64 * 8, dtype=torch.uint8, device=dev)
+        ctx.synth_validity(0xC5200000 + j, 0, rows, 50, m.data_ptr())
+        c.device["validity"] = m
+        nbytes += rows / 8
+    ctx.synchronize()
+    return Table(cols), nbytes
+
+
+def bench_c5(torch, N, D, ctx, dev, rows, steps):
+    """BASELINE config C5 at one GPU's shard size: the full 3-pass ColumnProfiler (generic statistics, numeric
+    statistics + KLL over the numeric and numeric-looking string columns after Spark's casts, exact histograms of
+    the low-cardinality columns) over a 20-column mixed table in HBM. Wall time per profile, sanity-checked."""
+    t, nbytes = c5_shard(torch, N, ctx, dev, rows)
+    prof = None
+    D.ColumnProfiler.profile(t)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        prof = D.ColumnProfiler.profile(t)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    assert prof.numRecords == rows
+    for name, p in prof.profiles.items():
+        assert 0.94 < p.completeness < 0.96, (name, p.completeness)
+    hist = {n: p.histogram for n, p in prof.profiles.items() if p.histogram is not None}
+    assert hist["s_bool"].numberOfBins == 3 and hist["s_cat50"].numberOfBins == 51, hist.keys()
+    assert sum(v.absolute for v in hist["s_cat100"].values.values()) == rows
+    types = {n: p.dataType for n, p in prof.profiles.items()}
+    assert types["s_int"] == "Integral" and types["s_dec"] == "Fractional" and types["s_text0"] == "String", types
+    ach = nbytes / el / 1e9
+    return {"workload": "C5 shard: ColumnProfiler passes 1-3 (Completeness, ApproxCountDistinct, DataType; Min / Max / "
+                        "Mean / StdDev / Sum / KLL on 13 numeric and cast numeric-string columns; exact histograms of "
+                        "%d low-cardinality columns) over %d rows x 20 columns (5 fp64, 5 int64, 10 UTF-8), 5%% nulls"
+                        % (len(hist), rows),
+            "value": rows / el, "unit": "rows/s", "ms_per_step": el * 1e3,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "kernel": "end-to-end profile wall time; achieved = the table's bytes (%.1f GB: values, "
+                                   "offsets, UTF-8 data, validity) once per profile" % (nbytes / 1e9)}}
+
+
 def bench_host_streamed(torch, N, D, ctx, dev, rows, steps, chunk_rows=1 << 25):
     """The C2 suite over HOST-resident columns (pinned memory) streamed through HBM in row chunks
     (dq_scan_streamed: the copy of chunk i + 1 overlaps the scan of chunk i): the end-to-end rate, bound by the
@@ -437,6 +507,8 @@ def main():
             sec["c4"] = bench_c4(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4))
             torch.cuda.empty_cache()
             sec["c2_host_streamed"] = bench_host_streamed(torch, N, D, ctx, dev, min(total, 200_000_000), 2)
+            torch.cuda.empty_cache()
+            sec["c5_shard"] = bench_c5(torch, N, D, ctx, dev, min(total, 100_000_000), 2)
             torch.cuda.empty_cache()
         result["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -19,6 +19,7 @@
 #include <string>
 #include <tuple>
 #include <vector>
+#include <vector>
 
 #include "dq_common.h"
 #include "dq_internal.h"
@@ -1282,6 +1283,35 @@ int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int6
     if (nrows == 0) return DQ_OK;
     DQ_HIP(ctx, hipSetDevice(ctx->device));
     launch_synth_column(kind, seed, row0, nrows, values_dev, ctx->stream);
+    DQ_HIP(ctx, hipGetLastError());
+    return DQ_OK;
+}
+
+int dq_synth_strings(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int64_t nrows, int32_t* offsets_dev,
+                     void* bytes_dev, int64_t* total_bytes) {
+    if (!ctx || nrows < 0 || !offsets_dev || !total_bytes || kind < DQ_SYNTH_STR_CAT50 || kind > DQ_SYNTH_STR_TEXT)
+        return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_synth_strings: invalid arguments");
+    DQ_HIP(ctx, hipSetDevice(ctx->device));
+    if (!bytes_dev) {
+        // lengths into offsets[1..n], then an exclusive scan on the host (offsets are int32: < 2 GiB of text)
+        DQ_HIP(ctx, hipMemsetAsync(offsets_dev, 0, 4, ctx->stream));
+        if (nrows) launch_synth_string_lengths(kind, seed, row0, nrows, offsets_dev + 1, ctx->stream);
+        DQ_HIP(ctx, hipGetLastError());
+        std::vector<int32_t> h((size_t)nrows + 1);
+        DQ_HIP(ctx, hipMemcpyAsync(h.data(), offsets_dev, ((size_t)nrows + 1) * 4, hipMemcpyDeviceToHost, ctx->stream));
+        DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        int64_t acc = 0;
+        for (int64_t i = 1; i <= nrows; ++i) {
+            acc += h[(size_t)i];
+            if (acc > INT32_MAX) return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_synth_strings: more than 2 GiB of text");
+            h[(size_t)i] = (int32_t)acc;
+        }
+        DQ_HIP(ctx, hipMemcpyAsync(offsets_dev, h.data(), ((size_t)nrows + 1) * 4, hipMemcpyHostToDevice, ctx->stream));
+        DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        *total_bytes = acc;
+        return DQ_OK;
+    }
+    if (nrows) launch_synth_string_bytes(kind, seed, row0, nrows, offsets_dev, bytes_dev, ctx->stream);
     DQ_HIP(ctx, hipGetLastError());
     return DQ_OK;
 }

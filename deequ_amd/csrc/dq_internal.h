@@ -283,6 +283,9 @@ void launch_regex(const PredColumn& col, const int32_t* image_dev, int64_t nrows
                   uint64_t* out_t, uint64_t* out_nn, int32_t* status, hipStream_t s);
 void launch_synth_column(int kind, uint64_t seed, int64_t row0, int64_t nrows, void* out, hipStream_t s);
 void launch_synth_freq_keys(int64_t total, int64_t distinct, int64_t row0, int64_t nrows, int64_t* out, hipStream_t s);
+void launch_synth_string_lengths(int kind, uint64_t seed, int64_t row0, int64_t nrows, int32_t* lens, hipStream_t s);
+void launch_synth_string_bytes(int kind, uint64_t seed, int64_t row0, int64_t nrows, const int32_t* offsets, void* bytes,
+                               hipStream_t s);
 void launch_synth_validity(uint64_t seed, int64_t row0, int64_t nrows, int permille, uint8_t* out,
                            hipStream_t s);
 

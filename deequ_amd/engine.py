@@ -219,8 +219,7 @@ class FrequencyTable:
     def _key_of_row(self, r):
         key = []
         for c in self.key_columns:
-            valid = c.validity is None or bool((c.validity[r >> 3] >> (r & 7)) & 1)
-            v = c.value_at(int(r)) if valid else None
+            v = c.value_at(int(r)) if c.valid_at(int(r)) else None
             key.append(GroupFloat(v) if isinstance(v, float) else v)
         return tuple(key)
 

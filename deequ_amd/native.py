@@ -4,6 +4,7 @@ The library is loaded from the package directory (built in-tree by __graft_entry
 There is no CPU fallback: if the library or a GPU is missing, operations raise.
 """
 import ctypes
+import sys
 import os
 import threading
 
@@ -39,6 +40,8 @@ P_LIKE, P_LENGTH, P_CAST_DOUBLE, P_CAST_LONG, P_CAST_STRING_NUM, P_REGEX = 40, 4
 V_BOOL, V_LONG, V_DOUBLE, V_STRING = 1, 2, 3, 4
 
 SYNTH_DYADIC, SYNTH_UNIFORM, SYNTH_NORMAL, SYNTH_INT32R, SYNTH_KEY30, SYNTH_GAUSS01, SYNTH_GAUSS_CORR = range(1, 8)
+SYNTH_STR_CAT50, SYNTH_STR_BOOL, SYNTH_STR_CAT100, SYNTH_STR_INT, SYNTH_STR_DEC, SYNTH_STR_MIXNUM, SYNTH_STR_TEXT = \
+    101, 102, 103, 104, 105, 106, 107
 
 HLL_NUM_WORDS = 52
 
@@ -48,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "dq_scan_launch_count", "dq_state_merge", "dq_state_fold", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
     "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
     "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
-    "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts",
+    "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts", "dq_synth_strings",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
     "dq_scan_streamed",
 )
@@ -187,6 +190,8 @@ def load_library(path=None):
             "dq_synth_validity": (c_int, [c_void_p, ctypes.c_uint64, c_int64, c_int64, ctypes.c_int32, c_void_p]),
             "dq_frequencies_ex": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
             "dq_freq_row_counts": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_uint32]),
+            "dq_synth_strings": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p, c_void_p,
+                                         c_void_p]),
             "dq_freq_export_device": (c_int64, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
             "dq_freq_from_pairs": (c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_int64, c_uint32, c_int64,
                                            c_int64, c_void_p]),
@@ -365,15 +370,36 @@ class Context:
                                             ctypes.c_void_p(values_dev_ptr), ctypes.c_void_p(validity_dev_ptr)),
                    "dq_cast_column")
 
+    @staticmethod
+    def _after_torch_stream():
+        """The generators run on the context's stream; a buffer torch just allocated and filled (torch.zeros) on its
+        own stream must be complete before they write into it."""
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            torch.cuda.current_stream().synchronize()
+
     def synth_column(self, kind, seed, row0, nrows, dev_ptr):
+        self._after_torch_stream()
         self.check(self.lib.dq_synth_column(self.handle, kind, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows,
                                             ctypes.c_void_p(dev_ptr)), "dq_synth_column")
 
     def synth_freq_keys(self, total_rows, distinct, row0, nrows, dev_ptr):
+        self._after_torch_stream()
         self.check(self.lib.dq_synth_freq_keys(self.handle, int(total_rows), int(distinct), int(row0), int(nrows),
                                                ctypes.c_void_p(dev_ptr)), "dq_synth_freq_keys")
 
+    def synth_strings(self, kind, seed, row0, nrows, offsets_ptr, bytes_ptr=None):
+        """dq_synth_strings: offsets first (returns the text bytes), then the bytes."""
+        self._after_torch_stream()
+        total = ctypes.c_int64(0)
+        self.check(self.lib.dq_synth_strings(self.handle, int(kind), seed & 0xFFFFFFFFFFFFFFFF, int(row0), int(nrows),
+                                             ctypes.c_void_p(offsets_ptr),
+                                             ctypes.c_void_p(bytes_ptr) if bytes_ptr else None, ctypes.byref(total)),
+                   "dq_synth_strings")
+        return int(total.value)
+
     def synth_validity(self, seed, row0, nrows, null_permille, dev_ptr):
+        self._after_torch_stream()
         self.check(self.lib.dq_synth_validity(self.handle, seed & 0xFFFFFFFFFFFFFFFF, row0, nrows, null_permille,
                                               ctypes.c_void_p(dev_ptr)), "dq_synth_validity")
 

@@ -97,11 +97,37 @@ class Column:
             out.append(self.value_at(i) if valid[i] else None)
         return out
 
+    def valid_at(self, i):
+        """Row i is non-NULL (reads one validity byte from HBM for a device-only column)."""
+        if self.validity is not None:
+            return bool((self.validity[i >> 3] >> (i & 7)) & 1)
+        if self.values is None and self.device is not None and self.device.get("validity") is not None:
+            return bool((int(self.device["validity"][i >> 3].item()) >> (i & 7)) & 1)
+        return True
+
     def value_at(self, i):
+        if self.values is None and self.device is not None:
+            return self._device_value_at(i)
         if self.spark_type == N.TYPE_STRING:
             o = self.offsets
             return bytes(self.values[o[i]:o[i + 1]]).decode("utf-8")
-        v = self.values[i]
+        return self._decode_cell(self.values[i])
+
+    def _device_value_at(self, i):
+        """One cell of a device-only column (top-N keys, representatives of a few groups: tiny copies)."""
+        d = self.device
+        if self.spark_type == N.TYPE_STRING:
+            o = d["offsets"][i:i + 2].cpu().numpy()
+            return bytes(d["values"][int(o[0]):int(o[1])].cpu().numpy()).decode("utf-8")
+        t = d["values"]
+        dt = np.dtype(NUMPY_OF[self.spark_type])
+        if str(t.dtype) == "torch.uint8" and dt.itemsize > 1:
+            v = t[i * dt.itemsize:(i + 1) * dt.itemsize].cpu().numpy().view(dt)[0]
+        else:
+            v = t[i:i + 1].cpu().numpy().astype(dt)[0]
+        return self._decode_cell(v)
+
+    def _decode_cell(self, v):
         if self.spark_type == N.TYPE_BOOLEAN:
             return bool(v)
         if self.spark_type in (N.TYPE_FLOAT, N.TYPE_DOUBLE):

@@ -383,6 +383,18 @@ int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int6
  * so exactly `distinct` keys exist when (total_rows - distinct) is a multiple of distinct / 2. */
 int dq_synth_freq_keys(dq_ctx* ctx, int64_t total_rows, int64_t distinct, int64_t row0, int64_t nrows,
                        int64_t* keys_dev);
+/* UTF-8 string columns of config C5. Two calls: with bytes_dev == NULL, writes the int32 Arrow
+ * offsets (nrows + 1 entries, device) and *total_bytes; then with bytes_dev (>= total_bytes + 16 bytes) writes the
+ * strings. Kinds: */
+#define DQ_SYNTH_STR_CAT50 101  /* "cat_<0..49>"                                           */
+#define DQ_SYNTH_STR_BOOL 102   /* "true" / "false"                                        */
+#define DQ_SYNTH_STR_CAT100 103 /* "v<00..99>"                                             */
+#define DQ_SYNTH_STR_INT 104    /* an integer in [-1e6, 1e6)                               */
+#define DQ_SYNTH_STR_DEC 105    /* "<0..999>.<00..99>"                                     */
+#define DQ_SYNTH_STR_MIXNUM 106 /* 70 %: an integer in [-5000, 5000); 30 %: "<+-int>.<ddd>" */
+#define DQ_SYNTH_STR_TEXT 107   /* 1-20 characters of [a-z0-9 ]                           */
+int dq_synth_strings(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int64_t nrows, int32_t* offsets_dev,
+                     void* bytes_dev, int64_t* total_bytes);
 /* Validity bitmap (ceil(nrows/64) words) with P(null) = null_permille / 1000. */
 int dq_synth_validity(dq_ctx* ctx, uint64_t seed, int64_t row0, int64_t nrows, int32_t null_permille,
                       uint8_t* validity_dev);
