@@ -670,10 +670,19 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     // ---- device memory layout -----------------------------------------------------------------
     // Launch groups: one kernel launch per slot shape; each gets a grid sized to fill the chip once.
     const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
-    struct Group { int kind, P, nc; bool f0, f1, heavy; int grid; std::vector<int32_t> slots; };
+    struct Group { int kind, P, nc; bool f0, f1; int heavy; int grid; std::vector<int32_t> slots; };
     std::vector<Group> groups;
-    auto shape_key = [](int kind, int P, int nc, bool f0, bool f1, bool heavy) {
-        return (((((kind * 16 + P) * 4 + nc) * 2 + f0) * 2 + f1) * 2 + heavy);
+    auto shape_key = [](int kind, int P, int nc, bool f0, bool f1, int heavy) {
+        return (((((kind * 16 + P) * 4 + nc) * 2 + f0) * 2 + f1) * 3 + heavy);
+    };
+    // heavy 2 (8-byte columns only): every column carries stats, moments, HLL and a fused compare the heavy kernel
+    // evaluates on its fast path, pairs carry the correlation, and there is no `where` -> the branch-free variant
+    auto full_col = [](const ColDesc& c) {
+        const bool fl = c.elem == ET_F64;
+        const uint32_t all = CF_STATS | CF_MOMENTS | CF_HLL;
+        const bool fast_pred = fl ? (c.pred_kind != FP_NONE && (c.pred_kind == FP_LONG || c.pred_d == c.pred_d))
+                                  : c.pred_kind == FP_LONG;
+        return (c.flags & all) == all && fast_pred;
     };
     std::map<int, int> group_of;
     for (int s = 0; s < (int)slots.size(); ++s) {
@@ -683,9 +692,14 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         const int P = sd.kind == SK_VALUES ? sd.rows_per_load : 8;
         const int nc = sd.kind == SK_VALUES ? sd.ncols : 1;
         // HLL registers or a fused predicate need the larger (HEAVY) kernel instantiation.
-        bool heavy = false;
+        int heavy = 0;
         for (int k = 0; sd.kind == SK_VALUES && k < sd.ncols; ++k)
-            heavy |= (sd.col[k].flags & CF_HLL) || sd.col[k].pred_kind != FP_NONE;
+            if ((sd.col[k].flags & CF_HLL) || sd.col[k].pred_kind != FP_NONE) heavy = 1;
+        if (heavy && P == 2 && sd.where_t == nullptr && (sd.ncols == 1 || sd.corr)) {
+            bool full = true;
+            for (int k = 0; k < sd.ncols; ++k) full &= full_col(sd.col[k]);
+            if (full) heavy = 2;
+        }
         const int kind = sd.kind;
         const int key = shape_key(kind, P, nc, f0, f1, heavy);
         auto it = group_of.find(key);

@@ -262,10 +262,10 @@ int exchange_i64(dq_ctx* ctx, const std::vector<int64_t*>& send, const std::vect
 // Kernel launchers (defined in the .hip files).
 // One launch per slot shape (kind, P, column count, float/integral storage); each launch walks its
 // slots with tiles interleaved over `grid` workgroups and writes partials[slot * gstride + block].
-int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, bool heavy, const SlotDesc* slots,
+int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, int heavy, const SlotDesc* slots,
                       const int32_t* group, int ngroup, int64_t nrows, int64_t ntiles, int gstride, int grid,
                       SlotPartial* partials, uint8_t* hll_partials, hipStream_t s);
-int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1, bool heavy);
+int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1, int heavy);
 void launch_reduce_partials(const SlotPartial* partials, const int32_t* nblocks_of, int nslots, int gstride,
                             SlotPartial* finals, hipStream_t s);
 void launch_reduce_hll(const uint8_t* hll_partials, const int32_t* nblocks_of, int nhll, int gstride,

@@ -1001,6 +1001,609 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
 }
 
 
+// ------------------------------------------------------------------------------------------------
+// HEAVY slots over 8-byte columns (LONG / TIMESTAMP / DECIMAL storage, DOUBLE): HLL registers, fused
+// Compliance `col <op> const`, the moments and Correlation in one pass — the north-star suite, VALU-bound on
+// XXH64. Written for the instruction count:
+//  * each lane owns 8 consecutive rows of the tile (4 x 16-B loads at a 64-B lane stride), so its validity /
+//    where bits are one bitmap byte (no bit gathering);
+//  * per-row masks are one v_bfe_i32 (0 / ~0); masked values are cleared with two v_and, min / max use a NaN
+//    stand-in built with one v_bfi (raw v_min_f64 / v_max_f64 drop a NaN operand; no canonicalising moves);
+//  * integral columns are converted to double once (3 instructions) and that double serves the moments, the
+//    correlation and the min / max (exact while |x| < 2^53 — checked per batch, exact int64 fallback);
+//  * the fused compare counts hits on the cleared values and corrects the masked rows with the wave-uniform
+//    result of `0 <op> const`; HLL updates are unconditional LDS max of (rank & mask) (rank 0 is a no-op); the
+//    2^-23 case of a zero rank field takes a per-tile exact re-hash.
+// Bit-exact HLL registers, counts, integral sums and min / max; fp64 moments within rounding of the batch order.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t row_mask(uint32_t m, int k) { return (uint32_t)(((int)(m << (31 - k))) >> 31); }
+__device__ __forceinline__ double pack_f64(uint32_t hi, uint32_t lo) { return as_f64(((uint64_t)hi << 32) | lo); }
+__device__ __forceinline__ uint32_t hi32(double d) { return (uint32_t)(f64_bits(d) >> 32); }
+__device__ __forceinline__ uint32_t lo32(double d) { return (uint32_t)f64_bits(d); }
+__device__ __forceinline__ double and_f64(double d, uint32_t mk) { return pack_f64(hi32(d) & mk, lo32(d) & mk); }
+// v_min_f64 / v_max_f64 without the compiler's canonicalising v_max_f64 x, x of each operand: a NaN operand is
+// dropped (a signalling NaN can make the result NaN; batches with NaN rows take the exact path).
+__device__ __forceinline__ double raw_min(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double raw_max(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {  // leading zeros, 0xFFFFFFFF for 0
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// (double)(int64_t)v correctly rounded in 3 instructions (hi * 2^32 is exact; one rounding in the fma)
+__device__ __forceinline__ double i64_to_f64(uint64_t v) {
+    return __builtin_fma((double)(int32_t)(uint32_t)(v >> 32), 4294967296.0, (double)(uint32_t)v);
+}
+__device__ __forceinline__ double one_if(uint32_t mk) { return pack_f64(mk & 0x3FF00000u, 0u); }
+
+// Fused compare of the cleared value (masked rows hold 0 / 0.0) — Spark semantics (NaN above every number,
+// NaN = NaN, -0.0 = 0.0) for a non-NaN double constant; integral columns against a LONG constant compare as long.
+template <bool F>
+__device__ __forceinline__ uint32_t cmp_hits8(const double (&xd)[8], const uint64_t (&xi)[8], int op, double y,
+                                              int64_t yi) {
+    uint32_t h = 0;
+#define DQ_CMP8(expr) _Pragma("unroll") for (int k = 0; k < 8; ++k) h += (expr) ? 1u : 0u; break;
+    if (F) {
+        switch (op) {
+            case DQ_P_EQ: DQ_CMP8(xd[k] == y)
+            case DQ_P_NE: DQ_CMP8(!(xd[k] == y))
+            case DQ_P_LT: DQ_CMP8(xd[k] < y)
+            case DQ_P_LE: DQ_CMP8(xd[k] <= y)
+            case DQ_P_GT: DQ_CMP8(!(xd[k] <= y))
+            default: DQ_CMP8(!(xd[k] < y))
+        }
+    } else {
+        switch (op) {
+            case DQ_P_EQ: DQ_CMP8((int64_t)xi[k] == yi)
+            case DQ_P_NE: DQ_CMP8((int64_t)xi[k] != yi)
+            case DQ_P_LT: DQ_CMP8((int64_t)xi[k] < yi)
+            case DQ_P_LE: DQ_CMP8((int64_t)xi[k] <= yi)
+            case DQ_P_GT: DQ_CMP8((int64_t)xi[k] > yi)
+            default: DQ_CMP8((int64_t)xi[k] >= yi)
+        }
+    }
+#undef DQ_CMP8
+    return h;
+}
+
+// XXH64 hashLong (seed 42) of a long (or of doubleToLongBits) up to the final multiply's high word (see hll_idx_rank);
+// returns that word: idx = g >> 23, rank field t = g << 9.
+__device__ __forceinline__ uint32_t xxh_long_ghi(uint64_t lv) {
+    uint64_t h = SPARK_HLL_SEED + P64_5 + 8ULL;
+    h ^= rotl64(lv * P64_2, 31) * P64_1;
+    h = rotl64(h, 27) * P64_1 + P64_4;
+    h ^= h >> 33;
+    h *= P64_2;
+    h ^= h >> 29;
+    const uint32_t hl = (uint32_t)h, hh = (uint32_t)(h >> 32);
+    constexpr uint32_t p3l = (uint32_t)P64_3, p3h = (uint32_t)(P64_3 >> 32);
+    return __umulhi(hl, p3l) + hl * p3h + hh * p3l;
+}
+
+struct HAccF {  // DOUBLE column
+    uint32_t n, nnan, pt;
+    double sum, mn, mx, mean, m2;
+};
+struct HAccI {  // 8-byte integral column
+    uint32_t n, pt;
+    int64_t isum, imn, imx;  // imn / imx: exact fallback of batches with |value| >= 2^53
+    double mn, mx, mean, m2;
+};
+template <bool F> struct HAccOf { using type = HAccI; };
+template <> struct HAccOf<true> { using type = HAccF; };
+
+__device__ __forceinline__ void hacc_init(HAccF& a) {
+    a.n = a.nnan = a.pt = 0;
+    a.sum = 0.0;
+    a.mn = a.mx = __builtin_nan("");
+    a.mean = a.m2 = 0.0;
+}
+__device__ __forceinline__ void hacc_init(HAccI& a) {
+    a.n = a.pt = 0;
+    a.isum = 0;
+    a.imn = INT64_MAX;
+    a.imx = INT64_MIN;
+    a.mn = a.mx = __builtin_nan("");
+    a.mean = a.m2 = 0.0;
+}
+__device__ __forceinline__ void hacc_to(FAcc& o, const HAccF& a) {
+    o.n = a.n;
+    o.nnan = a.nnan;
+    o.pt = a.pt;
+    o.sum = a.sum;
+    o.mn = a.mn != a.mn ? INFINITY : a.mn;
+    o.mx = a.mx != a.mx ? -INFINITY : a.mx;
+    o.mean = a.mean;
+    o.m2 = a.m2;
+}
+__device__ __forceinline__ void hacc_to(IAcc& o, const HAccI& a) {
+    o.n = a.n;
+    o.pt = a.pt;
+    o.sum = a.isum;
+    o.mn = a.imn;
+    o.mx = a.imx;
+    if (a.mn == a.mn && (int64_t)a.mn < o.mn) o.mn = (int64_t)a.mn;  // |mn| < 2^53: exact
+    if (a.mx == a.mx && (int64_t)a.mx > o.mx) o.mx = (int64_t)a.mx;
+    o.mean = a.mean;
+    o.m2 = a.m2;
+}
+
+// Chan merge of one batch (cnt >= 1 rows, mean mb, m2b) into the lane moments.
+__device__ __forceinline__ void hmoments_merge(uint32_t na, double& mean, double& m2, uint32_t cnt, double mb,
+                                               double m2b) {
+    if (na == 0) {
+        mean = mb;
+        m2 = m2b;
+        return;
+    }
+    const double n1 = (double)na, n2 = (double)cnt;
+    const double delta = mb - mean;
+    const double deltaN = delta * rcp_refined(n1 + n2);
+    mean = __builtin_fma(deltaN, n2, mean);
+    m2 = m2 + m2b + delta * deltaN * (n1 * n2);
+}
+
+struct HeavyCol {  // wave-uniform description of one column's work in the heavy kernel
+    bool stats, moments, hll, pred;
+    int op;
+    uint32_t zhit;  // 1 if `0 <op> const` holds (masked rows hold 0 / 0.0)
+    double y;
+    int64_t yi;
+};
+
+__device__ __forceinline__ HeavyCol heavy_col_of(const ColDesc& c, bool F) {
+    HeavyCol h;
+    h.stats = (c.flags & CF_STATS) != 0;
+    h.moments = (c.flags & CF_MOMENTS) != 0;
+    h.hll = (c.flags & CF_HLL) != 0;
+    h.op = c.pred_op;
+    h.yi = c.pred_i;
+    h.y = c.pred_kind == FP_LONG ? (double)c.pred_i : c.pred_d;
+    // fast fused compare: DOUBLE column vs a non-NaN constant, integral column vs a LONG constant
+    h.pred = c.pred_kind != FP_NONE && (F ? (h.y == h.y) : c.pred_kind == FP_LONG);
+    const double zero = 0.0;
+    bool z;
+    if (F || c.pred_kind != FP_LONG) {
+        switch (h.op) {
+            case DQ_P_EQ: z = zero == h.y; break;
+            case DQ_P_NE: z = !(zero == h.y); break;
+            case DQ_P_LT: z = zero < h.y; break;
+            case DQ_P_LE: z = zero <= h.y; break;
+            case DQ_P_GT: z = !(zero <= h.y); break;
+            default: z = !(zero < h.y); break;
+        }
+    } else {
+        switch (h.op) {
+            case DQ_P_EQ: z = 0 == h.yi; break;
+            case DQ_P_NE: z = 0 != h.yi; break;
+            case DQ_P_LT: z = 0 < h.yi; break;
+            case DQ_P_LE: z = 0 <= h.yi; break;
+            case DQ_P_GT: z = 0 > h.yi; break;
+            default: z = 0 >= h.yi; break;
+        }
+    }
+    h.zhit = z ? 1u : 0u;
+    return h;
+}
+
+// One column's 8 rows of the tile. xd receives the value as double for the correlation phase (DOUBLE: cleared
+// bits; integral: the converted raw value, finite); `fin` is false when a valid DOUBLE row is inf / NaN.
+// `need_xd`: stats, moments, the fused compare or the correlation read the values; otherwise (ApproxCountDistinct
+// alone) only the hash loop runs.
+template <bool F, bool FULL>
+__device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, const uint64_t (&v)[8], uint32_t m,
+                                               const HeavyCol& hc, const ColDesc& c, uint32_t* regs, uint32_t& tmin,
+                                               bool need_xd, double (&xd)[8], bool& fin) {
+    const uint32_t cnt = __popc(m);
+    uint64_t xi[8];  // cleared integral values
+    double s = 0.0;
+    fin = true;
+    uint32_t hm = m;  // rows hashed from their raw bits below
+    if (FULL || need_xd) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t mk = row_mask(m, k);
+            if constexpr (F) {
+                xd[k] = and_f64(as_f64(v[k]), mk);
+                s += xd[k];
+            } else {
+                xi[k] = ((uint64_t)((uint32_t)(v[k] >> 32) & mk) << 32) | ((uint32_t)v[k] & mk);
+                xd[k] = i64_to_f64(v[k]);
+                if (FULL || hc.moments) s = __builtin_fma(xd[k], one_if(mk), s);
+            }
+        }
+    } else if (F) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += as_f64(v[k]);  // NaN detector only (masked rows may raise it spuriously)
+    }
+    double mn = __builtin_nan(""), mx = __builtin_nan("");
+    if (FULL || hc.stats) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t mk = row_mask(m, k);
+            // NaN stand-in for masked rows: v_min / v_max drop it
+            const double xn = pack_f64((hi32(xd[k]) & mk) | (~mk & 0x7FF80000u), lo32(xd[k]));
+            mn = raw_min(mn, xn);
+            mx = raw_max(mx, xn);
+        }
+    }
+    if constexpr (F) {
+        if (__builtin_expect(!(s - s == 0.0), 0)) {
+            fin = false;
+            if (s != s) {
+                // NaN among the valid rows (or inf - inf): exact NaN count and NaN-free extremes of the batch; the
+                // NaN rows leave the raw-bits hash loop and add the canonical NaN's register once (doubleToLongBits)
+                uint32_t nanm = 0;
+                mn = INFINITY;
+                mx = -INFINITY;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const double x = as_f64(v[k]);
+                    const bool on = (m >> k) & 1u;
+                    nanm |= (on && x != x) ? (1u << k) : 0u;
+                    if (on && x == x) {
+                        mn = x < mn ? x : mn;
+                        mx = x > mx ? x : mx;
+                    }
+                }
+                const uint32_t nn = __popc(nanm);
+                a.nnan += nn;
+                if (mn == INFINITY && mx == -INFINITY && nn == cnt) mn = mx = __builtin_nan("");
+                hm = m & ~nanm;
+                if ((FULL || hc.hll) && nanm) {
+                    const uint32_t p = hll_idx_rank<2>(f64_bits(__builtin_nan("")));
+                    atomicMax(&regs[p & 0xffffu], p >> 16);
+                }
+            }
+        }
+        if (FULL || hc.stats) {
+            a.sum += s;
+            a.mn = raw_min(a.mn, mn);
+            a.mx = raw_max(a.mx, mx);
+        }
+    } else {
+        if (FULL || hc.stats) {
+            int64_t bs = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) bs = (int64_t)((uint64_t)bs + xi[k]);
+            a.isum = (int64_t)((uint64_t)a.isum + (uint64_t)bs);
+            const bool big = fabs(mn) >= 9007199254740992.0 || fabs(mx) >= 9007199254740992.0;
+            if (__builtin_expect(big, 0)) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int64_t x = (int64_t)v[k];
+                    const bool on = (m >> k) & 1u;
+                    a.imn = (on && x < a.imn) ? x : a.imn;
+                    a.imx = (on && x > a.imx) ? x : a.imx;
+                }
+            } else {
+                a.mn = raw_min(a.mn, mn);
+                a.mx = raw_max(a.mx, mx);
+            }
+        }
+    }
+    if ((FULL || hc.moments) && cnt) {
+        const double mb = s * rcp_refined((double)cnt);
+        double m2b = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t mk = row_mask(m, k);
+            const double d = F ? and_f64(xd[k] - mb, mk) : (xd[k] - mb) * one_if(mk);
+            m2b = __builtin_fma(d, d, m2b);
+        }
+        hmoments_merge(a.n, a.mean, a.m2, cnt, mb, m2b);
+    }
+    if (FULL || hc.pred) a.pt += cmp_hits8<F>(xd, xi, hc.op, hc.y, hc.yi) - hc.zhit * (8u - cnt);
+    else if (c.pred_kind != FP_NONE) a.pt += fused_pred_count<F>(c, v, m);  // NaN constant / mixed kinds
+    a.n += cnt;
+    if (FULL || hc.hll) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t g = xxh_long_ghi(v[k]);  // DOUBLE: raw bits (NaN rows were taken out of hm above)
+            const uint32_t t = g << 9;
+            tmin = min(tmin, t);
+            const uint32_t rank = ffbh_raw(t & row_mask(hm, k)) + 1u;  // 0 for a masked row (and for t == 0)
+            atomicMax(&regs[g >> 23], rank);
+        }
+    }
+}
+
+// Correlation of the rows valid in both columns (CorrelationState per 8-row batch + Chan merge). xd / yd hold
+// finite values on the fast path (cleared DOUBLE rows, converted integral rows), so a {1.0, 0.0} factor selects
+// the rows of the pair; a lane whose DOUBLE batch holds a valid inf / NaN clears the bits instead.
+template <bool FX, bool FY>
+__device__ __forceinline__ void heavy_corr_rows(CorrPartial& cp, const double (&xd)[8], const double (&yd)[8],
+                                                uint32_t m, bool fin) {
+    const uint32_t cnt = __popc(m);
+    if (cnt == 0) return;
+    CorrPartial b;
+    b.n = (double)cnt;
+    b.ck = b.xm = b.ym = 0.0;
+    const double inv = rcp_refined(b.n);
+    if (__builtin_expect(fin, 1)) {
+        double sx = 0.0, sy = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double f = one_if(row_mask(m, k));
+            sx = __builtin_fma(xd[k], f, sx);
+            sy = __builtin_fma(yd[k], f, sy);
+        }
+        b.xa = sx * inv;
+        b.ya = sy * inv;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double f = one_if(row_mask(m, k));
+            const double dx = xd[k] - b.xa, dy = yd[k] - b.ya;
+            const double dxf = dx * f, dyf = dy * f;
+            b.ck = __builtin_fma(dxf, dy, b.ck);
+            b.xm = __builtin_fma(dxf, dx, b.xm);
+            b.ym = __builtin_fma(dyf, dy, b.ym);
+        }
+    } else {
+        double xv[8], yv[8];
+        double sx = 0.0, sy = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t mk = row_mask(m, k);
+            xv[k] = and_f64(xd[k], mk);
+            yv[k] = and_f64(yd[k], mk);
+            sx += xv[k];
+            sy += yv[k];
+        }
+        b.xa = sx * inv;
+        b.ya = sy * inv;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t mk = row_mask(m, k);
+            const double dx = and_f64(xv[k] - b.xa, mk), dy = and_f64(yv[k] - b.ya, mk);
+            b.ck = __builtin_fma(dx, dy, b.ck);
+            b.xm = __builtin_fma(dx, dx, b.xm);
+            b.ym = __builtin_fma(dy, dy, b.ym);
+        }
+    }
+    corr_merge_batch(cp, b);
+}
+
+// The rare path of the HLL update: exact index / rank of every valid row of the lane (max is idempotent).
+template <bool F>
+__device__ __forceinline__ void heavy_hll_exact(uint32_t* regs, const uint64_t (&v)[8], uint32_t m) {
+    for (int k = 0; k < 8; ++k)
+        if ((m >> k) & 1u) {
+            const uint32_t p = hll_idx_rank<F ? 2 : 3>(v[k]);
+            atomicMax(&regs[p & 0xffffu], p >> 16);
+        }
+}
+
+// Lane's 8 consecutive rows of a full tile and their validity byte.
+__device__ __forceinline__ void heavy_load(const ColDesc& c, int64_t t, int tid, uint64_t (&v)[8]) {
+    const __amdgpu_buffer_rsrc_t r = tile_rsrc(c.values, t * kTileRows * 8, kTileRows * 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 64 + i * 16, 0, 0);
+        v[2 * i] = pack64(x.x, x.y);
+        v[2 * i + 1] = pack64(x.z, x.w);
+    }
+}
+__device__ __forceinline__ uint32_t heavy_bits(const uint64_t* bm, int64_t t, int tid) {
+    return bm ? (uint32_t)reinterpret_cast<const uint8_t*>(bm)[t * (kTileRows / 8) + tid] : 0xFFu;
+}
+// The partial last tile: bounded loads, rows past the end masked off.
+__device__ __forceinline__ uint32_t heavy_tail(const ColDesc& c, int64_t t, int tid, int64_t nrows, uint64_t (&v)[8]) {
+    const int64_t r0 = t * kTileRows + (int64_t)tid * 8;
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int64_t r = r0 + k;
+        const bool in = r < nrows;
+        v[k] = in ? static_cast<const uint64_t*>(c.values)[r] : 0ull;
+        const bool ok = in && (c.validity == nullptr ||
+                               ((reinterpret_cast<const uint8_t*>(c.validity)[r >> 3] >> (r & 7)) & 1));
+        m |= (ok ? 1u : 0u) << k;
+    }
+    return m;
+}
+
+// FULL: every column has stats, moments, HLL and a fast fused compare, pairs have the correlation, no `where`
+// (the north-star suite) — the per-flag branches compile away.
+template <int NC, bool F0, bool F1, bool FULL>
+__global__ void __launch_bounds__(kBlock, 1)
+scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__ group, int ngroup, int64_t nrows,
+                   int64_t ntiles, int gstride, SlotPartial* __restrict__ partials, uint8_t* __restrict__ hll_partials) {
+    using A0 = typename HAccOf<F0>::type;
+    using A1 = typename HAccOf<F1>::type;
+    __shared__ uint32_t hll_lds[NC][kHllRegs];
+    __shared__ BlockRed<NC, F0, F1> red;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int64_t G = gridDim.x;
+    for (int gi = 0; gi < ngroup; ++gi) {
+        const int s = group[gi];
+        const SlotDesc sd = slots[s];
+        const ColDesc c0 = sd.col[0];
+        const ColDesc c1 = sd.col[1];
+        const HeavyCol h0 = heavy_col_of(c0, F0);
+        const HeavyCol h1 = heavy_col_of(c1, F1);
+        const bool corr = NC > 1 && (FULL || sd.corr);
+        const bool has_where = !FULL && sd.where_t != nullptr;
+        const bool need0 = corr || h0.stats || h0.moments || c0.pred_kind != FP_NONE;
+        const bool need1 = corr || h1.stats || h1.moments || c1.pred_kind != FP_NONE;
+        A0 a0;
+        A1 a1;
+        hacc_init(a0);
+        hacc_init(a1);
+        CorrPartial cp;
+        cp.n = cp.xa = cp.ya = cp.ck = cp.xm = cp.ym = 0.0;
+        uint32_t wt = 0, wnn = 0;
+        for (int i = tid; i < NC * kHllRegs; i += kBlock) (&hll_lds[0][0])[i] = 0;
+        __syncthreads();
+        auto fold = [&](const uint64_t (&x)[8], const uint64_t (&y)[8], uint32_t mx, uint32_t my, uint32_t w,
+                        uint32_t wn) {
+            if (has_where) {
+                wt += __popc(w);
+                wnn += __popc(wn);
+                mx &= w;
+                my &= w;
+            }
+            uint32_t tmin = 0xFFFFFFFFu;
+            double xd[8], yd[8];
+            bool fx = true, fy = true;
+            heavy_col_rows<F0, FULL>(a0, x, mx, h0, c0, hll_lds[0], tmin, need0, xd, fx);
+            if (NC > 1) {
+                heavy_col_rows<F1, FULL>(a1, y, my, h1, c1, hll_lds[NC - 1], tmin, need1, yd, fy);
+                if (corr) heavy_corr_rows<F0, F1>(cp, xd, yd, mx & my, fx && fy);
+            }
+            if (__builtin_expect(tmin == 0u, 0)) {
+                if (FULL || h0.hll) heavy_hll_exact<F0>(hll_lds[0], x, mx);
+                if (NC > 1 && (FULL || h1.hll)) heavy_hll_exact<F1>(hll_lds[NC - 1], y, my);
+            }
+        };
+        const int64_t nfull = nrows / kTileRows;
+        int64_t t = blockIdx.x;
+        uint64_t x[8], y[8];
+        uint32_t bx = 0xFF, by = 0xFF, bw = 0xFF, bn = 0xFF;
+        if (t < nfull) {
+            heavy_load(c0, t, tid, x);
+            bx = heavy_bits(c0.validity, t, tid);
+            if (NC > 1) {
+                heavy_load(c1, t, tid, y);
+                by = heavy_bits(c1.validity, t, tid);
+            }
+            if (has_where) {
+                bw = heavy_bits(sd.where_t, t, tid);
+                bn = heavy_bits(sd.where_nn, t, tid);
+            }
+        }
+        for (; t < nfull; t += G) {
+            const int64_t tn = t + G;
+            uint64_t xn[8], yn[8];
+            uint32_t nbx = 0xFF, nby = 0xFF, nbw = 0xFF, nbn = 0xFF;
+            if (tn < nfull) {
+                heavy_load(c0, tn, tid, xn);
+                nbx = heavy_bits(c0.validity, tn, tid);
+                if (NC > 1) {
+                    heavy_load(c1, tn, tid, yn);
+                    nby = heavy_bits(c1.validity, tn, tid);
+                }
+                if (has_where) {
+                    nbw = heavy_bits(sd.where_t, tn, tid);
+                    nbn = heavy_bits(sd.where_nn, tn, tid);
+                }
+            }
+            fold(x, y, bx, by, bw, bn);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                x[k] = xn[k];
+                if (NC > 1) y[k] = yn[k];
+            }
+            bx = nbx;
+            by = nby;
+            bw = nbw;
+            bn = nbn;
+        }
+        if (nfull < ntiles && blockIdx.x == nfull % G) {
+            const uint32_t mx = heavy_tail(c0, nfull, tid, nrows, x);
+            const uint32_t my = NC > 1 ? heavy_tail(c1, nfull, tid, nrows, y) : 0u;
+            uint32_t w = 0, wn = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int64_t r = nfull * kTileRows + (int64_t)tid * 8 + k;
+                const bool in = r < nrows;
+                w |= (in ? 1u : 0u) << k;
+            }
+            if (has_where) {
+                wn = w & heavy_bits(sd.where_nn, nfull, tid);
+                w &= heavy_bits(sd.where_t, nfull, tid);
+            } else {
+                wn = w;
+            }
+            if (NC == 1) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) y[k] = 0;
+            }
+            fold(x, y, mx, my, w, wn);
+        }
+        // lane states -> the scan's partial structs, then the shared wave / workgroup reduction
+        typename AccOf<F0>::type r0;
+        typename AccOf<F1>::type r1;
+        hacc_to(r0, a0);
+        if (NC > 1) hacc_to(r1, a1);
+        else acc_init(r1);
+        int64_t lwt = wt, lwnn = wnn;
+#pragma unroll 1
+        for (int off = 32; off > 0; off >>= 1) {
+            typename AccOf<F0>::type o0;
+            acc_shfl(o0, r0, off);
+            const int64_t owt = shfl_down_i64(lwt, off), ownn = shfl_down_i64(lwnn, off);
+            typename AccOf<F1>::type o1;
+            CorrPartial oc;
+            if (NC > 1) {
+                acc_shfl(o1, r1, off);
+                corr_shfl(oc, cp, off);
+            }
+            if (lane < off) {
+                acc_merge(r0, o0);
+                lwt += owt;
+                lwnn += ownn;
+                if (NC > 1) {
+                    acc_merge(r1, o1);
+                    corr_merge(cp, oc);
+                }
+            }
+        }
+        if (lane == 0) {
+            red.a0[wave] = r0;
+            red.wt[wave] = lwt;
+            red.wnn[wave] = lwnn;
+            if (NC > 1) {
+                red.a1[wave] = r1;
+                red.cp[wave] = cp;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < kBlock / 64; ++w) {
+                acc_merge(r0, red.a0[w]);
+                lwt += red.wt[w];
+                lwnn += red.wnn[w];
+                if (NC > 1) {
+                    acc_merge(r1, red.a1[w]);
+                    corr_merge(cp, red.cp[w]);
+                }
+            }
+            SlotPartial* dst = partials + (int64_t)s * gstride + blockIdx.x;
+            store_partial(dst->c[0], r0);
+            if (NC > 1) {
+                store_partial(dst->c[1], r1);
+                dst->corr = cp;
+            } else {
+                store_empty(dst->c[1]);
+                dst->corr.n = dst->corr.xa = dst->corr.ya = dst->corr.ck = dst->corr.xm = dst->corr.ym = 0.0;
+            }
+            dst->wt = lwt;
+            dst->wnn = lwnn;
+            dst->pt = dst->pnn = dst->vt = dst->pad = 0;
+        }
+        for (int c = 0; c < NC; ++c) {
+            const bool hl = c == 0 ? h0.hll : h1.hll;
+            const int hs = c == 0 ? c0.hll_slot : c1.hll_slot;
+            if (hl && hs >= 0) {
+                uint8_t* dst = hll_partials + ((int64_t)hs * gstride + blockIdx.x) * kHllRegs;
+                for (int i = tid; i < kHllRegs; i += kBlock) dst[i] = (uint8_t)hll_lds[c][i];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+
 // Bits-only slots (Size(where), Completeness of an unread column, Compliance): one 64-row bitmap
 // word per lane per step, tiles interleaved over workgroups like the value kernels.
 __global__ void __launch_bounds__(kBlock)
@@ -1183,24 +1786,38 @@ __global__ void finalize_kernel(const OpMap* __restrict__ ops, int nops, const S
 // Launchers
 // ------------------------------------------------------------------------------------------------
 template <int P, int NC, bool F0, bool F1>
-static const void* values_kernel_ptr(bool heavy) {
+static const void* values_kernel_ptr(int heavy) {
     return heavy ? reinterpret_cast<const void*>(&scan_values_kernel<P, NC, F0, F1, true>)
                  : reinterpret_cast<const void*>(&scan_values_kernel<P, NC, F0, F1, false>);
 }
 
-static const void* values_kernel_for(int P, int nc, bool f0, bool f1, bool heavy) {
+static const void* values_kernel_for(int P, int nc, bool f0, bool f1, int heavy) {
+    if (heavy && P == 2) {  // 8-byte columns: the lean heavy kernel (heavy == 2: every flag on, no `where`)
+#define DQ_HK(n, a, b) \
+    if (nc == n && f0 == a && f1 == b) \
+        return heavy == 2 ? reinterpret_cast<const void*>(&scan_heavy8_kernel<n, a, b, true>) \
+                          : reinterpret_cast<const void*>(&scan_heavy8_kernel<n, a, b, false>);
+        DQ_HK(1, false, false) DQ_HK(1, true, false)
+        DQ_HK(2, false, false) DQ_HK(2, false, true) DQ_HK(2, true, false) DQ_HK(2, true, true)
+#undef DQ_HK
+    }
 #define DQ_VK(p, n, a, b) \
     if (P == p && nc == n && f0 == a && f1 == b) return values_kernel_ptr<p, n, a, b>(heavy);
-    DQ_VK(2, 1, false, false) DQ_VK(2, 1, true, false) DQ_VK(4, 1, false, false) DQ_VK(4, 1, true, false)
+    // P = 2 (8-byte elements): HEAVY slots went to scan_heavy8_kernel above
+#define DQ_VK2(n, a, b) \
+    if (P == 2 && nc == n && f0 == a && f1 == b) return reinterpret_cast<const void*>(&scan_values_kernel<2, n, a, b, false>);
+    DQ_VK2(1, false, false) DQ_VK2(1, true, false)
+    DQ_VK2(2, false, false) DQ_VK2(2, false, true) DQ_VK2(2, true, false) DQ_VK2(2, true, true)
+#undef DQ_VK2
+    DQ_VK(4, 1, false, false) DQ_VK(4, 1, true, false)
     DQ_VK(8, 1, false, false) DQ_VK(8, 1, true, false)
-    DQ_VK(2, 2, false, false) DQ_VK(2, 2, false, true) DQ_VK(2, 2, true, false) DQ_VK(2, 2, true, true)
     DQ_VK(4, 2, false, false) DQ_VK(4, 2, false, true) DQ_VK(4, 2, true, false) DQ_VK(4, 2, true, true)
     DQ_VK(8, 2, false, false) DQ_VK(8, 2, false, true) DQ_VK(8, 2, true, false) DQ_VK(8, 2, true, true)
 #undef DQ_VK
     return nullptr;
 }
 
-int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1, bool heavy) {
+int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1, int heavy) {
     const void* k = kind == SK_BITS ? reinterpret_cast<const void*>(&scan_bits_kernel) : values_kernel_for(P, nc, f0, f1, heavy);
     if (!k) return 0;
     int n = 0;
@@ -1208,7 +1825,7 @@ int scan_group_blocks_per_cu(int kind, int P, int nc, bool f0, bool f1, bool hea
     return n;
 }
 
-int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, bool heavy, const SlotDesc* slots, const int32_t* group,
+int launch_scan_group(int kind, int P, int nc, bool f0, bool f1, int heavy, const SlotDesc* slots, const int32_t* group,
                       int ngroup, int64_t nrows, int64_t ntiles, int gstride, int grid, SlotPartial* partials,
                       uint8_t* hll_partials, hipStream_t s) {
     if (kind == SK_BITS) {
