@@ -29,6 +29,13 @@
 
 namespace dq {
 
+// Cache policy of the striped column loads (buffer aux: bit 1 = nt on gfx950): once-read streams, measured
+// 2-3 % faster on C2 (profiles/r02/c2_policy_r02ap.log). The lane-owned 64-B runs of scan_heavy8_kernel keep the
+// default policy: their four 16-B loads per line rely on the line staying cached (nt made them 1.5x slower).
+#ifndef DQ_SCAN_AUX
+#define DQ_SCAN_AUX 2
+#endif
+
 __device__ __forceinline__ double as_f64(uint64_t u) { return __longlong_as_double((long long)u); }
 __device__ __forceinline__ uint64_t f64_bits(double d) { return (uint64_t)__double_as_longlong(d); }
 
@@ -265,7 +272,7 @@ __device__ __forceinline__ uint32_t bits_padded(const uint64_t* __restrict__ bm,
     for (int j = 0; j < L; ++j) {
         // row0 = tile + j * 256 * P + tid * P; its 64-bit word inside the tile and bit offset:
         const int rel = j * (kBlock * P) + tid * P;
-        const v2i_t w = __builtin_amdgcn_raw_buffer_load_b64(r, (rel >> 6) * 8, 0, 0);
+        const v2i_t w = __builtin_amdgcn_raw_buffer_load_b64(r, (rel >> 6) * 8, 0, DQ_SCAN_AUX);
         const uint64_t word = ((uint64_t)(uint32_t)w.y << 32) | (uint32_t)w.x;
         m |= (uint32_t)((word >> (rel & 63)) & pm) << (j * P);
     }
@@ -327,7 +334,7 @@ __device__ __forceinline__ void load_values(const ColDesc& c, int64_t tile, int 
                 // P == 2: load i covers rows i*512 + 2*tid (+0, +1); P == 8: rows 8*tid + 2i (+0, +1)
                 const int voff = P == 8 ? tid * 64 + i * 16 : tid * 16;
                 const int soff = P == 8 ? 0 : i * 4096;
-                const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+                const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, DQ_SCAN_AUX);
                 v[2 * i] = pack64(x.x, x.y);
                 v[2 * i + 1] = pack64(x.z, x.w);
             }
@@ -338,7 +345,7 @@ __device__ __forceinline__ void load_values(const ColDesc& c, int64_t tile, int 
             for (int i = 0; i < 2; ++i) {
                 const int voff = P == 8 ? tid * 32 + i * 16 : tid * 16;
                 const int soff = P == 8 ? 0 : i * 4096;
-                const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+                const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, DQ_SCAN_AUX);
                 const int xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -349,7 +356,7 @@ __device__ __forceinline__ void load_values(const ColDesc& c, int64_t tile, int 
             return;
         }
         if (esz == 2) {
-            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16, 0, 0);
+            const v4i_t x = __builtin_amdgcn_raw_buffer_load_b128(r, tid * 16, 0, DQ_SCAN_AUX);
             const uint32_t w[4] = {(uint32_t)x.x, (uint32_t)x.y, (uint32_t)x.z, (uint32_t)x.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -358,7 +365,7 @@ __device__ __forceinline__ void load_values(const ColDesc& c, int64_t tile, int 
             }
             return;
         }
-        const v2i_t x = __builtin_amdgcn_raw_buffer_load_b64(r, tid * 8, 0, 0);
+        const v2i_t x = __builtin_amdgcn_raw_buffer_load_b64(r, tid * 8, 0, DQ_SCAN_AUX);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t b = ((uint32_t)(i < 4 ? x.x : x.y) >> (8 * (i & 3))) & 0xFFu;

@@ -187,11 +187,31 @@ __device__ __forceinline__ int64_t shfl_down_i64s(int64_t x, int off) {
 
 }  // namespace
 
+// One row's string ops over data[o0, o1) — `data` is the column's bytes in HBM, or the wave's staged copy in LDS.
+__device__ __forceinline__ void string_row(const StrSlot& s, const uint8_t* data, int64_t o0, int64_t o1, bool want_hll,
+                                           int64_t& mn, int64_t& mx, int64_t (&dt)[5], uint32_t* regs) {
+    if (s.flags & SF_LEN) {
+        const int64_t len = utf8_length(data, o0, o1);
+        mn = len < mn ? len : mn;
+        mx = len > mx ? len : mx;
+    }
+    if (s.flags & SF_DTYPE) dt[classify_string(data, o0, o1)] += 1;
+    if (want_hll) {
+        const uint64_t x = xxh64_utf8(data, o0, o1, SPARK_HLL_SEED);
+        atomicMax(&regs[hll_index(x)], hll_rank(x));
+    }
+}
+
+// Bytes of one wave's 64 consecutive strings staged in LDS (coalesced dword loads of the whole byte range instead of
+// each lane's scattered byte / dword loads); ranges longer than this are read from HBM directly.
+constexpr int kStrStageWords = 512;
+
 __global__ void __launch_bounds__(kBlock)
 scan_strings_kernel(const StrSlot* __restrict__ slots, int nslots, int64_t nrows, int gstride,
                     StrPartial* __restrict__ partials, uint8_t* __restrict__ hll_partials) {
     __shared__ uint32_t regs[kHllRegs];
     __shared__ StrPartial red[kBlock / 64];
+    __shared__ uint32_t stage[kBlock / 64][kStrStageWords];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int si = 0; si < nslots; ++si) {
         const StrSlot s = slots[si];
@@ -204,24 +224,39 @@ scan_strings_kernel(const StrSlot* __restrict__ slots, int nslots, int64_t nrows
         int64_t n = 0, mn = INT64_MAX, mx = INT64_MIN;
         int64_t dt[5] = {0, 0, 0, 0, 0};
         const int64_t stride = (int64_t)gridDim.x * kBlock;
-        for (int64_t row = (int64_t)blockIdx.x * kBlock + tid; row < nrows; row += stride) {
-            bool on = s.validity == nullptr || ((s.validity[row >> 6] >> (row & 63)) & 1ull);
-            if (s.where_t) on = on && ((s.where_t[row >> 6] >> (row & 63)) & 1ull);
-            if (!on) continue;
-            ++n;
+        // wave-uniform loop over groups of 64 consecutive rows (lane = row within the group)
+        for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < nrows; base += stride) {
+            const int64_t row = base + lane;
+            bool on = row < nrows;
+            if (on) {
+                on = s.validity == nullptr || ((s.validity[row >> 6] >> (row & 63)) & 1ull);
+                if (s.where_t) on = on && ((s.where_t[row >> 6] >> (row & 63)) & 1ull);
+            }
+            n += on ? 1 : 0;
             if (str) {
-                const int64_t o0 = s.offsets[row], o1 = s.offsets[row + 1];
-                if (s.flags & SF_LEN) {
-                    const int64_t len = utf8_length(s.data, o0, o1);
-                    mn = len < mn ? len : mn;
-                    mx = len > mx ? len : mx;
+                const int64_t last = base + 64 < nrows ? base + 64 : nrows;
+                const int64_t b0 = s.offsets[base], b1 = s.offsets[last];
+                const int64_t a0 = b0 & ~(int64_t)3;
+                // staged bytes: [a0, b1 + 12) — le64_at reads up to 12 bytes past a string's end (the buffer has
+                // >= 16 readable bytes past the column's last string)
+                const int64_t nwords = (b1 + 12 - a0 + 3) >> 2;
+                if (nwords <= kStrStageWords) {
+                    for (int64_t i = lane; i < nwords; i += 64) stage[wave][i] = load_word(s.data, a0 + 4 * i);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    if (on) {
+                        const int64_t o0 = s.offsets[row] - a0, o1 = s.offsets[row + 1] - a0;
+                        string_row(s, reinterpret_cast<const uint8_t*>(&stage[wave][0]), o0, o1, want_hll, mn, mx, dt,
+                                   regs);
+                    }
+                    // the next group's staging writes after every lane's reads of this one (LDS keeps a wave's
+                    // accesses in order)
+                    __builtin_amdgcn_wave_barrier();
+                } else if (on) {
+                    string_row(s, s.data, s.offsets[row], s.offsets[row + 1], want_hll, mn, mx, dt, regs);
                 }
-                if (s.flags & SF_DTYPE) dt[classify_string(s.data, o0, o1)] += 1;
-                if (want_hll) {
-                    const uint64_t x = xxh64_utf8(s.data, o0, o1, SPARK_HLL_SEED);
-                    atomicMax(&regs[hll_index(x)], hll_rank(x));
-                }
-            } else if (s.flags & SF_DTYPE) {
+            } else if (on && (s.flags & SF_DTYPE)) {
                 dt[numeric_class(s, row)] += 1;
             }
         }
