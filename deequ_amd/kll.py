@@ -23,10 +23,8 @@ def _order_key(v):
     """Ordering.Double.compare (java.lang.Double.compare): -0.0 < 0.0, NaN largest — what `.sorted`
     and `sortBy` use."""
     if v != v:
-        return (2, 0.0)
-    if v == 0.0:
-        return (0, -0.5 if math.copysign(1.0, v) < 0 else 0.0)
-    return (0, v)
+        return (2, 0.0, 0)
+    return (0, v, 0 if math.copysign(1.0, v) < 0 else 1)  # -0.0 just below 0.0, above every negative
 
 
 def _capacity(sketch_size, shrinking_factor, height):
@@ -152,32 +150,56 @@ class QuantileNonSample:
     def getRankExclusive(self, item):
         return int(self.getRanks([item], exclusive=True)[0])
 
-    def getRanks(self, items, exclusive):
-        """getRank / getRankExclusive for many query items at once (same IEEE comparisons)."""
+    def _rank_index(self):
+        """(IEEE-sorted non-NaN items, cumulative weights with a leading 0, total weight of NaN items)."""
         import numpy as np
         t, w = self._output_arrays()
-        q = np.asarray(items, dtype=np.float64)[:, None]
-        with np.errstate(invalid="ignore"):
-            hit = (t[None, :] < q) if exclusive else ~(t[None, :] > q)
-        return (hit * w[None, :]).sum(axis=1)
+        nan = np.isnan(t)
+        keep = ~nan
+        order = np.argsort(t[keep], kind="stable")
+        ts = t[keep][order]
+        cw = np.concatenate([np.zeros(1, dtype=np.int64), np.cumsum(w[keep][order])])
+        return ts, cw, int(w[nan].sum())
+
+    def getRanks(self, items, exclusive, index=None):
+        """getRank / getRankExclusive for many query items at once, with the reference's IEEE comparisons:
+        exclusive = weight of items `< q` (none for a NaN query); inclusive = weight of items with `!(item > q)`,
+        i.e. items <= q plus every NaN item (all items for a NaN query). Binary searches over the sorted items."""
+        import numpy as np
+        ts, cw, nanw = index if index is not None else self._rank_index()
+        q = np.asarray(items, dtype=np.float64)
+        qnan = np.isnan(q)
+        qq = np.where(qnan, 0.0, q)
+        if exclusive:
+            r = cw[np.searchsorted(ts, qq, side="left")]
+            return np.where(qnan, 0, r)
+        r = cw[np.searchsorted(ts, qq, side="right")] + nanw
+        return np.where(qnan, cw[-1] + nanw, r)
 
     def quantiles(self, q):
-        """QuantileNonSample.quantiles (A/QuantileNonSample.scala:249-281)."""
-        output = self._output()
-        if not output:
+        """QuantileNonSample.quantiles (A/QuantileNonSample.scala:249-281): items sorted in Double.compare order,
+        the walk over cumulative weights done with binary searches (same picks as the reference's loop, including
+        the entries left at the first item once the walk has consumed the last one)."""
+        import numpy as np
+        t, w = self._output_arrays()
+        n = len(t)
+        if n == 0:
             return []
-        items = sorted(output, key=lambda p: _order_key(p[0]))
-        total = sum(w for _, w in items)
-        next_thresh = total // q
-        curq, i, so_far = 1, 0, 0
-        res = [items[0][0]] * (q - 1)
-        while i < len(items) and curq < q:
-            while so_far < next_thresh:
-                so_far += items[i][1]
-                i += 1
-            res[curq - 1] = items[min(i, len(items) - 1)][0]
-            curq += 1
-            next_thresh = curq * total // q
+        u = t.view(np.uint64).copy()
+        u[np.isnan(t)] = np.uint64(0x7ff8000000000000)
+        key = np.where((u >> np.uint64(63)) != 0, ~u, u | np.uint64(1 << 63))
+        order = np.argsort(key, kind="stable")
+        ts, c = t[order], np.cumsum(w[order])
+        total = int(c[-1])
+        res = [float(ts[0])] * (q - 1)
+        i = 0
+        for curq in range(1, q):
+            if i >= n:
+                break
+            thresh = curq * total // q
+            if thresh > 0:
+                i = max(i, int(np.searchsorted(c, thresh, side="left")) + 1)
+            res[curq - 1] = float(ts[min(i, n - 1)])
         return res
 
     def getCompactorItemsCount(self):
@@ -352,12 +374,13 @@ def bucket_distribution(state, numberOfBuckets):
     start, end = state.globalMin, state.globalMax
     lows = [start + (end - start) * i / float(numberOfBuckets) for i in range(numberOfBuckets)]
     highs = [start + (end - start) * (i + 1) / float(numberOfBuckets) for i in range(numberOfBuckets)]
-    ex_low = sk.getRanks(lows, exclusive=True) if numberOfBuckets else []
-    ex_high = sk.getRanks(highs, exclusive=True) if numberOfBuckets else []
+    index = sk._rank_index()
+    ex_low = sk.getRanks(lows, exclusive=True, index=index) if numberOfBuckets else []
+    ex_high = sk.getRanks(highs, exclusive=True, index=index) if numberOfBuckets else []
     buckets = []
     for i in range(numberOfBuckets):
         if i == numberOfBuckets - 1:
-            cnt = sk.getRank(highs[i]) - int(ex_low[i])
+            cnt = int(sk.getRanks([highs[i]], exclusive=False, index=index)[0]) - int(ex_low[i])
         else:
             cnt = int(ex_high[i]) - int(ex_low[i])
         buckets.append(BucketValue(lows[i], highs[i], cnt))

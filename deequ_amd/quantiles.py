@@ -41,10 +41,8 @@ class Stats:
 def _java_double_key(v):
     """Ordering.Double (java.lang.Double.compare): -0.0 < 0.0, NaN largest."""
     if v != v:
-        return (2, 0.0)
-    if v == 0.0:
-        return (0, -0.5 if math.copysign(1.0, v) < 0 else 0.0)
-    return (0, v)
+        return (2, 0.0, 0)
+    return (0, v, 0 if math.copysign(1.0, v) < 0 else 1)  # -0.0 just below 0.0, above every negative
 
 
 def _compress_immut(current, merge_threshold):

@@ -100,3 +100,58 @@ def test_kll_preconditions_and_metric_shape():
     flat = metric.flatten()
     assert [d.name for d in flat] == ["KLL.buckets"] + ["KLL.low", "KLL.high", "KLL.count"] * 2
     assert flat[0].value.get() == 2.0 and flat[3].value.get() == 4.0
+
+
+def _slow_quantiles(sk, q):
+    """The reference's quantiles loop (A/QuantileNonSample.scala:249-281) over (item, weight) pairs."""
+    import math
+    out = []
+    for i, c in enumerate(sk.compactors[:sk.curNumOfCompactors]):
+        out.extend((v, 1 << i) for v in c.buffer)
+    if not out:
+        return []
+
+    def key(v):
+        if v != v:
+            return (2, 0.0, 0)
+        return (0, v, 0 if math.copysign(1.0, v) < 0 else 1)  # Double.compare: -0.0 < 0.0
+    items = sorted(out, key=lambda p: key(p[0]))
+    total = sum(w for _, w in items)
+    nt, curq, i, so_far = total // q, 1, 0, 0
+    res = [items[0][0]] * (q - 1)
+    while i < len(items) and curq < q:
+        while so_far < nt:
+            so_far += items[i][1]
+            i += 1
+        res[curq - 1] = items[min(i, len(items) - 1)][0]
+        curq += 1
+        nt = curq * total // q
+    return res
+
+
+def _slow_rank(sk, x, exclusive):
+    r = 0
+    for i, c in enumerate(sk.compactors[:sk.curNumOfCompactors]):
+        for v in c.buffer:
+            if (v < x) if exclusive else not (v > x):
+                r += 1 << i
+    return r
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_vectorised_quantiles_and_ranks_match_the_reference_loops(seed):
+    rng = np.random.default_rng(seed)
+    sk = QuantileNonSample(64 if seed % 2 else 2048, 0.64)
+    n = [0, 1, 3, 50, 5000, 40000][seed]
+    pool = np.concatenate([rng.normal(0, 10, 50), [0.0, -0.0, np.nan, np.inf, -np.inf, 1.5, 1.5]])
+    for v in rng.choice(pool, n) if n else []:
+        sk.update(float(v))
+    for q in (2, 7, 100, 1000):
+        got, exp = sk.quantiles(q), _slow_quantiles(sk, q)
+        assert len(got) == len(exp)
+        assert all((a == b and math.copysign(1, a) == math.copysign(1, b)) or (a != a and b != b)
+                   for a, b in zip(got, exp)), (q, got[:5], exp[:5])
+    probes = [float(x) for x in pool[:20]] + [0.0, -0.0, float("nan"), float("inf"), -1e300]
+    for ex in (True, False):
+        got = sk.getRanks(probes, exclusive=ex)
+        assert [int(g) for g in got] == [_slow_rank(sk, x, ex) for x in probes]

@@ -142,3 +142,14 @@ def test_java_order_of_oracle():
     t = Table.from_arrays({"x": np.array([np.nan, 0.0, -0.0, -np.inf, 1.0])})
     s = O.java_sorted_doubles(t, "x")
     assert math.isinf(s[0]) and math.copysign(1, s[1]) < 0 and math.copysign(1, s[2]) > 0 and math.isnan(s[4])
+
+
+def test_java_double_order_puts_negative_zero_between_negatives_and_zero():
+    """Double.compare order: every negative < -0.0 < 0.0 < positives < NaN (a -0.0 mapped to -0.5 misordered
+    (-0.5, 0) values before)."""
+    from deequ_amd.quantiles import _java_double_key
+    from deequ_amd.kll import _order_key
+    vals = [float("nan"), 0.25, 0.0, -0.0, -0.05, -0.7, float("-inf"), float("inf")]
+    for key in (_java_double_key, _order_key):
+        got = sorted(vals, key=key)
+        assert [repr(v) for v in got] == ["-inf", "-0.7", "-0.05", "-0.0", "0.0", "0.25", "inf", "nan"]
