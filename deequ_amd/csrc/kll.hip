@@ -119,6 +119,46 @@ kll_write_kernel(KllColumn c, int64_t nrows, const unsigned long long* __restric
     }
 }
 
+// NULL compaction, between the passes: exclusive prefix of the tile counts (one workgroup) and the total, so only
+// the total travels to the host (the compaction schedule is a function of it).
+__global__ void __launch_bounds__(1024)
+kll_scan_kernel(const unsigned int* __restrict__ counts, int64_t ntiles, unsigned long long* __restrict__ offs,
+                unsigned long long* __restrict__ total) {
+    __shared__ unsigned long long part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (ntiles + 1023) / 1024;
+    const int64_t b0 = t * per, b1 = b0 + per < ntiles ? b0 + per : ntiles;
+    unsigned long long acc = 0;
+    for (int64_t i = b0; i < b1; ++i) acc += counts[i];
+    part[t] = acc;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the 1024 thread sums
+        const unsigned long long v = t >= o ? part[t - o] : 0ull;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    unsigned long long run = part[t] - acc;
+    for (int64_t i = b0; i < b1; ++i) {
+        offs[i] = run;
+        run += counts[i];
+    }
+    if (t == 1023) *total = part[1023];
+}
+
+// Final buffers: each level's unconsumed tail gathered into one contiguous array (one read-back per sketch).
+struct KllTail {
+    unsigned long long src;   // device address of the level's first unconsumed item
+    unsigned long long len;
+    unsigned long long dst;   // index in the gathered array
+};
+__global__ void __launch_bounds__(256)
+kll_gather_kernel(const KllTail* __restrict__ tails, double* __restrict__ out) {
+    const KllTail tl = tails[blockIdx.x];
+    const double* src = reinterpret_cast<const double*>(tl.src);
+    for (unsigned long long i = threadIdx.x; i < tl.len; i += 256) out[tl.dst + i] = src[i];
+}
+
 // One compaction, packed in 8 bytes: start of the compacted range in its level's stream (bits 0-39),
 // L (bits 40-54, <= 16384) and the compactor offset (bit 63). Compactions consume a level's stream
 // contiguously from 0 and every L is even, so the picks go to next-level slot start / 2.
@@ -231,6 +271,121 @@ kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ 
     }
 }
 
+// Compactions of L = P + rx items with P = T*E a power of two and 0 <= rx <= 64 (the schedule's L sit just above
+// powers of two: 2060, 1030, 516, 258, ...): the first P items take the exact-size merge sort above, the rx newest
+// ones are sorted by wave 0 (bitonic over lanes) and merged by rank — a main item moves up by the extras strictly
+// below it, an extra lands after the main items <= it — instead of padding the range to 1.5x in a larger class.
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
+    const int lo = __shfl_xor((int)(uint32_t)x, m, 64), hi = __shfl_xor((int)(uint32_t)(x >> 32), m, 64);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+template <int T, int E>
+__global__ void __launch_bounds__(T)
+kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
+                     unsigned long long* __restrict__ minmax) {
+    constexpr int P = T * E;
+    constexpr int XM = 64;
+    static_assert(T >= XM, "wave 0 sorts the extras");
+    __shared__ uint64_t k[P + T];
+    __shared__ uint64_t ex[XM];
+    auto at = [](int i) { return i + i / E; };
+    const uint64_t sg = segs[blockIdx.x];
+    const uint64_t start = sg & ((1ull << 40) - 1);
+    const int len = (int)((sg >> 40) & 0x7FFF);
+    const int rx = len - P;  // 0..XM (host-checked)
+    const int t = threadIdx.x;
+    const double* in = src + start;
+    uint64_t v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) v[r] = kll_key(in[t * E + r]);
+    uint64_t xk = ~0ull;
+    if (t < XM && t < rx) xk = kll_key(in[P + t]);
+    kll_reg_sort<E>(v);
+    for (int w = E; w < P; w <<= 1) {
+#pragma unroll
+        for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
+        __syncthreads();
+        const int diag = E * (t & (2 * (w / E) - 1));
+        const int A = (t * E) - diag, B = A + w;
+        int lo = diag > w ? diag - w : 0, hi = diag < w ? diag : w;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (k[at(A + mid)] <= k[at(B + diag - 1 - mid)]) lo = mid + 1;
+            else hi = mid;
+        }
+        int ai = A + lo, bi = B + diag - lo;
+        const int aend = A + w, bend = B + w;
+        uint64_t ah = ai < aend ? k[at(ai)] : ~0ull, bh = bi < bend ? k[at(bi)] : ~0ull;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const bool takeA = bi >= bend || (ai < aend && ah <= bh);
+            if (takeA) {
+                v[r] = ah;
+                ++ai;
+                ah = ai < aend ? k[at(ai)] : ~0ull;
+            } else {
+                v[r] = bh;
+                ++bi;
+                bh = bi < bend ? k[at(bi)] : ~0ull;
+            }
+        }
+        __syncthreads();
+    }
+    // the sorted main array in LDS (the extras' ranks) and the extras sorted by wave 0
+#pragma unroll
+    for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
+    if (t < XM) {
+#pragma unroll
+        for (int size = 2; size <= XM; size <<= 1)
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const uint64_t y = shfl_xor_u64(xk, stride);
+                const bool keep_min = ((t & stride) == 0) == ((t & size) == 0);
+                xk = keep_min ? (y < xk ? y : xk) : (y > xk ? y : xk);
+            }
+        ex[t] = xk;
+    }
+    __syncthreads();
+    const int half = len >> 1;
+    const int off = (int)(sg >> 63);
+    double* out = dst + (start >> 1);
+    // main items: sorted index t*E + r plus the extras strictly below
+    int c = 0, hb = rx;
+    while (c < hb) {
+        const int mid = (c + hb) >> 1;
+        if (ex[mid] < v[0]) c = mid + 1;
+        else hb = mid;
+    }
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        while (c < rx && ex[c] < v[r]) ++c;
+        const int d = t * E + r + c - off;
+        if (d >= 0 && (d & 1) == 0 && (d >> 1) < half) out[d >> 1] = kll_value(v[r]);
+    }
+    // extras: their index among the extras plus the main items <= them
+    if (t < rx) {
+        const uint64_t x = ex[t];
+        int lo = 0, hi = P;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (k[at(mid)] <= x) lo = mid + 1;
+            else hi = mid;
+        }
+        const int d = lo + t - off;
+        if (d >= 0 && (d & 1) == 0 && (d >> 1) < half) out[d >> 1] = kll_value(x);
+    }
+    if (minmax && t == 0 && len > 0) {
+        uint64_t mn = k[at(0)], mx = k[at(P - 1)];
+        if (rx > 0) {
+            mn = ex[0] < mn ? ex[0] : mn;
+            mx = ex[rx - 1] > mx ? ex[rx - 1] : mx;
+        }
+        if (mn < *(volatile unsigned long long*)&minmax[0]) atomicMin(&minmax[0], (unsigned long long)mn);
+        if (mx > *(volatile unsigned long long*)&minmax[1]) atomicMax(&minmax[1], (unsigned long long)mx);
+    }
+}
+
 // Compaction classes: (threads, keys per thread), capacity T*E.
 struct KllClass {
     int t, e;
@@ -239,7 +394,16 @@ constexpr KllClass kKllClasses[] = {{64, 4},   {64, 8},   {64, 12},   {64, 16}, 
                                     {256, 12}, {256, 16}, {512, 12},  {512, 16},  {1024, 12}, {1024, 16}};
 constexpr int kKllNumClasses = sizeof(kKllClasses) / sizeof(kKllClasses[0]);
 
+// Exact-size classes of kll_compact_x_kernel: P = 256 << j (T, E), for L in [P, P + 64].
+constexpr KllClass kKllXClasses[] = {{64, 4}, {64, 8}, {128, 8}, {256, 8}, {512, 8}, {1024, 8}, {1024, 16}};
+constexpr int kKllNumXClasses = sizeof(kKllXClasses) / sizeof(kKllXClasses[0]);
+constexpr int kKllAllClasses = kKllNumClasses + kKllNumXClasses;
+
 int kll_class_of(int len) {
+    for (int j = kKllNumXClasses - 1; j >= 0; --j) {
+        const int P = kKllXClasses[j].t * kKllXClasses[j].e;
+        if (len >= P && len - P <= 64) return kKllNumClasses + j;
+    }
     for (int c = 0; c < kKllNumClasses; ++c)
         if (kKllClasses[c].t * kKllClasses[c].e >= len) return c;
     return -1;
@@ -264,6 +428,16 @@ int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nse
         KLL_CASE(10, 1024, 12)
         KLL_CASE(11, 1024, 16)
 #undef KLL_CASE
+#define KLL_XCASE(C, T, E) \
+    case C: hipLaunchKernelGGL((kll_compact_x_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax); break;
+        KLL_XCASE(12, 64, 4)
+        KLL_XCASE(13, 64, 8)
+        KLL_XCASE(14, 128, 8)
+        KLL_XCASE(15, 256, 8)
+        KLL_XCASE(16, 512, 8)
+        KLL_XCASE(17, 1024, 8)
+        KLL_XCASE(18, 1024, 16)
+#undef KLL_XCASE
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -281,15 +455,19 @@ namespace {
 
 using namespace dq;
 
-struct KBuffers {
-    std::vector<void*> ptrs;
+struct KBuffers {  // per-call device buffers from the context's scratch cache (no hipMalloc / hipFree per sketch)
+    dq_ctx* ctx;
+    std::vector<std::pair<void*, size_t>> ptrs;
+    explicit KBuffers(dq_ctx* c) : ctx(c) {}
     ~KBuffers() {
-        for (void* p : ptrs) (void)hipFree(p);
+        for (const auto& p : ptrs) dq::scratch_release(ctx, p.first, p.second);
     }
     hipError_t alloc(void** p, size_t bytes) {
-        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
-        if (e == hipSuccess) ptrs.push_back(*p);
-        return e;
+        bytes = std::max<size_t>(bytes, 16);
+        *p = dq::scratch_alloc(ctx, bytes);
+        if (!*p) return hipErrorOutOfMemory;
+        ptrs.push_back({*p, bytes});
+        return hipSuccess;
     }
 };
 
@@ -322,7 +500,7 @@ struct KllLevel {
     int64_t pos = 0;       // first unconsumed item of this level's stream
     int64_t arrived = 0;   // items appended to this level's stream
     std::vector<uint64_t> segs;                   // compactions, in order
-    int64_t per_class[16] = {0};                  // compactions per kernel class
+    int64_t per_class[32] = {0};                  // compactions per kernel class
 };
 
 struct KllSchedule {
@@ -412,7 +590,7 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     const int dev = dq::ctx_device(ctx);
     KL_HIP(ctx, hipSetDevice(dev));
     hipStream_t s = dq::ctx_stream(ctx);
-    KBuffers buf;
+    KBuffers buf(ctx);
 
     KllColumn kc;
     kc.elem = elem_of(t);
@@ -442,25 +620,22 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     const bool zero_copy = kc.elem == ET_F64 && kc.validity == nullptr;
     const int64_t ntiles = (nrows + kKllStageRows - 1) / kKllStageRows;
     unsigned long long* doffs = nullptr;
-    std::vector<unsigned long long> offs;
     if (zero_copy) {
         stream0 = static_cast<const double*>(kc.values);
     } else if (nrows > 0) {
         unsigned int* dcounts = nullptr;
+        unsigned long long* dtotal = nullptr;
         KL_HIP(ctx, buf.alloc((void**)&dcounts, sizeof(unsigned int) * ntiles));
         KL_HIP(ctx, buf.alloc((void**)&doffs, sizeof(unsigned long long) * ntiles));
+        KL_HIP(ctx, buf.alloc((void**)&dtotal, sizeof(unsigned long long)));
+        unsigned long long* htotal = static_cast<unsigned long long*>(dq::ctx_pinned_buf(ctx, 8));
+        if (!htotal) return DQ_ERR_OUT_OF_MEMORY;
         hipLaunchKernelGGL(kll_count_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows, dcounts);
+        hipLaunchKernelGGL(kll_scan_kernel, dim3(1), dim3(1024), 0, s, (const unsigned int*)dcounts, ntiles, doffs, dtotal);
         KL_HIP(ctx, hipGetLastError());
-        std::vector<unsigned int> counts(ntiles);
-        KL_HIP(ctx, hipMemcpyAsync(counts.data(), dcounts, sizeof(unsigned int) * ntiles, hipMemcpyDeviceToHost, s));
+        KL_HIP(ctx, hipMemcpyAsync(htotal, dtotal, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
         KL_HIP(ctx, hipStreamSynchronize(s));
-        offs.resize(ntiles);
-        unsigned long long acc = 0;
-        for (int64_t i = 0; i < ntiles; ++i) {
-            offs[i] = acc;
-            acc += counts[i];
-        }
-        n = (int64_t)acc;
+        n = (int64_t)*htotal;
     } else {
         n = 0;
     }
@@ -485,14 +660,17 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     const size_t up_off = (dense_bytes + 255) / 256 * 256;
     const size_t seg_off = up_off + ((size_t)upper * 8 + 255) / 256 * 256;
     const size_t mm_off = seg_off + (nseg_all * 8 + 255) / 256 * 256;
-    uint8_t* scratch = static_cast<uint8_t*>(dq::ctx_scratch(ctx, mm_off + 256));
+    int64_t ntail = 0;  // items left in the final buffers
+    for (const KllLevel& l : sc.levels) ntail += l.len;
+    const size_t tail_off = mm_off + 256;
+    const size_t gat_off = tail_off + (nlev * sizeof(KllTail) + 255) / 256 * 256;
+    uint8_t* scratch = static_cast<uint8_t*>(dq::ctx_scratch(ctx, gat_off + (size_t)ntail * 8 + 256));
     if (!scratch) return DQ_ERR_OUT_OF_MEMORY;
     double* dup = reinterpret_cast<double*>(scratch + up_off);
     uint64_t* dsegs = reinterpret_cast<uint64_t*>(scratch + seg_off);
     unsigned long long* dminmax = reinterpret_cast<unsigned long long*>(scratch + mm_off);
     if (!zero_copy && n > 0) {
         double* dense = reinterpret_cast<double*>(scratch);
-        KL_HIP(ctx, hipMemcpyAsync(doffs, offs.data(), sizeof(unsigned long long) * ntiles, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows,
                            (const unsigned long long*)doffs, dense);
         KL_HIP(ctx, hipGetLastError());
@@ -506,13 +684,18 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
         int cls;
     };
     std::vector<Launch> launches;
-    uint64_t* hsegs = nseg_all ? static_cast<uint64_t*>(dq::ctx_pinned_buf(ctx, nseg_all * 8)) : nullptr;
-    if (nseg_all && !hsegs) return DQ_ERR_OUT_OF_MEMORY;
+    // pinned staging: [segment descriptors][level tails][gathered final buffers + min / max keys]
+    const size_t pin_tails = nseg_all * 8, pin_out = pin_tails + nlev * sizeof(KllTail);
+    uint8_t* pin = static_cast<uint8_t*>(dq::ctx_pinned_buf(ctx, pin_out + (size_t)ntail * 8 + 16));
+    if (!pin) return DQ_ERR_OUT_OF_MEMORY;
+    uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin);
+    KllTail* htails = reinterpret_cast<KllTail*>(pin + pin_tails);
+    double* hgat = reinterpret_cast<double*>(pin + pin_out);
     size_t pos = 0;
     for (size_t h = 0; h < nlev; ++h) {
         const KllLevel& l = sc.levels[h];
-        size_t cursor[kKllNumClasses];
-        for (int c = 0; c < kKllNumClasses; ++c) {
+        size_t cursor[kKllAllClasses];
+        for (int c = 0; c < kKllAllClasses; ++c) {
             cursor[c] = pos;
             if (l.per_class[c]) launches.push_back({h, pos, (size_t)l.per_class[c], c});
             pos += (size_t)l.per_class[c];
@@ -539,18 +722,34 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
                 (long long)n, nlev, nseg_all, ms(t0, t1), ms(t1, t2));
     }
 
-    // ---- final buffers --------------------------------------------------------------------------
+    // ---- final buffers: one gather + one read-back -------------------------------------------------
+    KllTail* dtails = reinterpret_cast<KllTail*>(scratch + tail_off);
+    double* dgat = reinterpret_cast<double*>(scratch + gat_off);
+    {
+        unsigned long long at = 0;
+        for (size_t h = 0; h < nlev; ++h) {
+            const KllLevel& l = sc.levels[h];
+            const double* src = (h == 0 ? stream0 : dup + lbase[h]) + l.pos;
+            htails[h] = KllTail{(unsigned long long)(uintptr_t)src, (unsigned long long)l.len, at};
+            at += (unsigned long long)l.len;
+        }
+        KL_HIP(ctx, hipMemcpyAsync(dtails, htails, nlev * sizeof(KllTail), hipMemcpyHostToDevice, s));
+        if (ntail) hipLaunchKernelGGL(kll_gather_kernel, dim3((unsigned)nlev), dim3(256), 0, s, (const KllTail*)dtails, dgat);
+        KL_HIP(ctx, hipGetLastError());
+        if (ntail) KL_HIP(ctx, hipMemcpyAsync(hgat, dgat, sizeof(double) * (size_t)ntail, hipMemcpyDeviceToHost, s));
+        KL_HIP(ctx, hipMemcpyAsync(hgat + ntail, dminmax, 16, hipMemcpyDeviceToHost, s));
+        KL_HIP(ctx, hipStreamSynchronize(s));
+    }
     std::vector<std::vector<double>> fin(nlev);
-    for (size_t h = 0; h < nlev; ++h) {
-        const KllLevel& l = sc.levels[h];
-        fin[h].resize((size_t)l.len);
-        if (l.len == 0) continue;
-        const double* src = (h == 0 ? stream0 : dup + lbase[h]) + l.pos;
-        KL_HIP(ctx, hipMemcpyAsync(fin[h].data(), src, sizeof(double) * (size_t)l.len, hipMemcpyDeviceToHost, s));
+    {
+        int64_t at = 0;
+        for (size_t h = 0; h < nlev; ++h) {
+            fin[h].assign(hgat + at, hgat + at + sc.levels[h].len);
+            at += sc.levels[h].len;
+        }
     }
     unsigned long long mm[2];
-    KL_HIP(ctx, hipMemcpyAsync(mm, dminmax, sizeof(mm), hipMemcpyDeviceToHost, s));
-    KL_HIP(ctx, hipStreamSynchronize(s));
+    memcpy(mm, hgat + ntail, sizeof(mm));
 
     // UntypedQuantileNonSample.updateUntyped: math.min / math.max folds from Int.MaxValue.toDouble /
     // Int.MinValue.toDouble (java.lang.Math: NaN-propagating, -0.0 < 0.0) = the order-key extremes
