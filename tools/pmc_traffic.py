@@ -11,7 +11,7 @@ import argparse
 import csv
 import json
 
-SCAN_KERNELS = ("scan_values_kernel", "scan_bits_kernel", "predicate_kernel", "reduce_partials_kernel",
+SCAN_KERNELS = ("scan_values_kernel", "scan_heavy8_kernel", "scan_bits_kernel", "predicate_kernel", "reduce_partials_kernel",
                 "reduce_hll_kernel", "finalize_kernel")
 
 
