@@ -383,6 +383,21 @@ def cpu_baseline(seconds, sample_rows, threads=None):
                       "Welford; not deequ/Spark itself)" % (sample_rows, threads, rows / sample_rows, el)}
 
 
+def committed_json(pattern, rows, need=None):
+    """(content, path) of the last profiles/<round>/<pattern> whose "rows" equals `rows` (any when None) and that holds
+    the key `need` (when given), or None."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", pattern))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if (rows is None or int(d.get("rows", -1)) == rows) and (need is None or need in d):
+            best = (d, os.path.relpath(path, ROOT))
+    return best
+
+
 def measured_traffic(rows_per_gpu):
     """HBM bytes per dq_scan call of this workload from the committed rocprofv3 PMC passes
     (tools/gpu_pmc.sh -> tools/pmc_traffic.py -> profiles/<round>/c2_traffic_*.json), in GB, or None
@@ -490,14 +505,33 @@ def main():
         s10 = ScanWorkload(torch, N, D, ctx, table, suite10_analyzers(D, names), stream, dev, world, args.dist_backend)
         el, kms, st = timed(torch, dist, world, max(3, args.steps // 4), 1, stream, s10.step)
         ach = alg_bytes / (kms * 1e-3) / 1e9
+        s10_traffic = committed_json("suite10_traffic_*.json", nrows)
+        s10_valu = committed_json("suite10_sq_counters_*.json", None, need="runs")
+        valu = None
+        if s10_valu is not None and world == 1 and nrows == 1_000_000_000:
+            # VALU roofline of the (VALU-bound) heavy kernels: wave64 VALU instructions per call (rocprofv3 SQ_INSTS_VALU,
+            # the last committed run) x 64 lanes / the measured scan time, against 256 CUs x 64 lanes x 2.4 GHz
+            runs = s10_valu[0]["runs"]
+            last = runs[sorted(runs)[-1]]
+            insts = sum(k["SQ_INSTS_VALU"] for k in last.values())
+            peak = 256 * 64 * 2.4e9 / 1e12
+            a = insts * 64 / (kms * 1e-3) / 1e12
+            valu = {"bound": "valu", "achieved": a, "peak": peak, "unit": "Tlane-op/s", "frac": a / peak,
+                    "insts_per_call": insts, "source": s10_valu[1],
+                    "note": "SQ_INSTS_VALU of the committed profile; the chip ran at ~2.0 GHz under this load "
+                            "(SQ_BUSY_CYCLES), so frac against 2.4 GHz understates issue utilisation (~0.82)"}
         sec["suite10"] = {
             "workload": "north-star 10-analyzer suite: C2 ops + Compliance(c > 0) + ApproxCountDistinct x 8 cols + "
                         "Correlation(c_2k, c_2k+1) x 4 = %d ops, one fused pass" % s10.nops,
             "value": total / (el / max(3, args.steps // 4)), "unit": "rows/s", "ms_per_step": el / max(3, args.steps // 4) * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "frac": ach / PEAK_HBM_GBPS,
+                         "traffic": s10_traffic[0]["traffic_bytes_per_call"] / 1e9 if s10_traffic else None,
+                         "traffic_unit": "GB per dq_scan call (rocprofv3 PMC, %s)" % (s10_traffic[1] if s10_traffic
+                                                                                      else "not measured"),
                          "kernel": "dq_scan avg %.3f ms (HIP events); VALU-bound: XXH64 + moments per value "
-                                   "(DESIGN.md §3)" % kms}}
+                                   "(DESIGN.md §3)" % kms},
+            "valu_roofline": valu}
         del s10
         if world == 1:
             del table
