@@ -1799,7 +1799,9 @@ static const void* values_kernel_ptr(int heavy) {
 }
 
 static const void* values_kernel_for(int P, int nc, bool f0, bool f1, int heavy) {
-    if (heavy && P == 2) {  // 8-byte columns: the lean heavy kernel (heavy == 2: every flag on, no `where`)
+    // 8-byte columns: HEAVY slots and Correlation pairs take the lean kernel (heavy == 2: every flag on, no `where`);
+    // the striped kernel's pair instantiation runs at 1 wave / SIMD (255 VGPRs), this one at 2
+    if ((heavy || nc == 2) && P == 2) {
 #define DQ_HK(n, a, b) \
     if (nc == n && f0 == a && f1 == b) \
         return heavy == 2 ? reinterpret_cast<const void*>(&scan_heavy8_kernel<n, a, b, true>) \
