@@ -6,8 +6,8 @@
 // R/AnalysisRunner.scala:480-548): #groups, #(count == 1), sum -(c/N) ln(c/N), plus Histogram's
 // variant (A/Histogram.scala:54-70: every row counts, NULL is the "NullValue" group) and top-N.
 //
-// Table: open addressing with linear probing over 16-byte slots {u64 key, u32 count, u32 pad} so a
-// probe touches one cache line. Keys:
+// Table: 2^b regions x kRegion slots of 16 bytes {u64 key, u64 count} (Spark counts with Long); a key lives in
+// region key & (2^b - 1) and probes linearly from its top bits. Keys:
 //   * fast path (one fixed-width key column): key = mix(canonical 64-bit value), mix = the bijective
 //     splitmix64 finalizer, so distinct values never collide; the one value that maps to the EMPTY
 //     marker is counted in a side counter. Spark groups on binary row equality: NaN is
@@ -16,20 +16,22 @@
 //     of every key column, plus the group's smallest row index; a verification pass compares every
 //     row with its group's representative row and the build is redone with a new seed if two
 //     distinct keys ever shared a fingerprint, so results are exact.
-// Build = partitioned aggregation, no global atomics on the hot path:
-//   1. extract: a count pass (side counters + a 4096-register HLL estimate of the distinct keys +
-//      per-workgroup counts), then every taking-part row's 64-bit key h (and, general path, its row
-//      index) compacted in row order into an array;
-//   2. the estimate picks b bucket bits so a bucket holds ~1024 distinct keys on average; a
-//      rocPRIM radix sort on b bits of h makes every bucket a contiguous run;
-//   3. one workgroup per bucket (heavy buckets are split into slices) aggregates its run in an LDS
-//      open-addressing table of kRegion slots and stores it as region `bucket` of the global table
-//      (a slice of a split bucket merges its LDS table into the region with global atomics).
-// The table is 2^b regions x kRegion slots; a key lives in region h & (2^b - 1) (its LOW bits: the
-// rocPRIM 4.2 radix sort of ROCm 7.2 returned unsorted output for 64-bit keys with begin_bit > 0 in
-// tools/micro/rp_bits.hip, while [0, b) sorts correctly), probing from its top 12 bits inside it.
-// Summaries, radix-select top-N and exports are table scans with per-workgroup partials folded in a
-// fixed order (deterministic).
+// Build = partitioned aggregation, no global atomics on the hot path; b is chosen from an HLL estimate of the
+// distinct keys so a region holds <= kRegionTarget of them:
+//   * fast build (one fixed-width key column, >= 2^24 rows, unweighted): partition1_fast reads the rows and
+//     scatters the keys into 256 partitions x 8 XCD sub-regions of fixed capacity, each 4096-key tile ordered by
+//     digit in LDS and its per-digit runs reserved with one atomicAdd per digit; scatter2_fast splits every
+//     partition on the next digit bits into the 2^b buckets the same way. No count pass; a bucket that would
+//     overflow (heavy hitters) sends the build to the exact path;
+//   * exact build (weighted, multi-column, string keys, small inputs, the fallback): extract_count (per-workgroup
+//     digit histograms + sizing) -> partition1 -> count2 / scan2 / scatter2 with deterministic offsets, or compact
+//     + rocPRIM radix sort on the low b bits for tables outside the two-pass range;
+//   * build_kernel: one workgroup per bucket (heavy buckets split into slices) aggregates its keys in an LDS
+//     table and stores region `bucket` (a slice merges into it with global atomics); a whole-bucket item also
+//     writes its part of the grouping summary (#groups, #count == 1, max count, entropy terms).
+// Summaries, radix-select top-N, exports, the K8 merge (weighted rebuild of both tables' pairs), MutualInformation
+// (joint table + marginal lookups) and the multi-device exchange are table scans with per-workgroup partials folded
+// in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
