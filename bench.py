@@ -133,32 +133,40 @@ def build_shard(torch, N, ctx, row0, nrows, dev):
     return Table(cols)
 
 
-def bench_c3(torch, N, D, ctx, stream, dev, total, steps):
-    """BASELINE config C3 on one GPU: k = splitmix64 mod 2^30 (HLL), x ~ N(0, 1), y = 0.6 x + 0.8 e, 1 % nulls."""
+def bench_c3(torch, N, D, ctx, stream, dev, total, steps, dist=None, world=1, rank=0, backend="nccl"):
+    """BASELINE config C3: k = splitmix64 mod 2^30 (HLL), x ~ N(0, 1), y = 0.6 x + 0.8 e, 1 % nulls, rows sharded
+    contiguously over the ranks (2048-row aligned); per step the fused scan of the shard, the RCCL all-gather of the
+    states and their rank-ordered fold (HLL registers max-merged, CorrelationState Chan-merged)."""
     from deequ_amd.table import Table, Column
+    per = (total + world - 1) // world
+    per = (per + 2047) // 2048 * 2048
+    row0 = min(rank * per, total)
+    nrows = max(0, min(total, row0 + per) - row0)
     cols = []
     for name, kind, seed, vseed, st in (("k", N.SYNTH_KEY30, 0xC3000001, 0xC3000101, N.TYPE_LONG),
                                         ("x", N.SYNTH_GAUSS01, 0xC3000002, 0xC3000102, N.TYPE_DOUBLE),
                                         ("y", N.SYNTH_GAUSS_CORR, 0xC3000002, 0xC3000103, N.TYPE_DOUBLE)):
-        v = torch.empty(total, dtype=torch.int64 if st == N.TYPE_LONG else torch.float64, device=dev)
-        m = torch.zeros((total + 63) // 64 * 8, dtype=torch.uint8, device=dev)
-        ctx.synth_column(kind, seed, 0, total, v.data_ptr())
-        ctx.synth_validity(vseed, 0, total, 10, m.data_ptr())
-        c = Column(name, st, None, None, length=total)
+        v = torch.empty(max(nrows, 1), dtype=torch.int64 if st == N.TYPE_LONG else torch.float64, device=dev)
+        m = torch.zeros(max((nrows + 63) // 64 * 8, 8), dtype=torch.uint8, device=dev)
+        ctx.synth_column(kind, seed, row0, nrows, v.data_ptr())
+        ctx.synth_validity(vseed, row0, nrows, 10, m.data_ptr())
+        c = Column(name, st, None, None, length=nrows)
         c.device = {"values": v, "validity": m}
         cols.append(c)
     ctx.synchronize()
     t = Table(cols)
     w = ScanWorkload(torch, N, D, ctx, t, [D.ApproxCountDistinct("k"), D.Correlation("x", "y"), D.Completeness("k")],
-                     stream, dev, 1, "nccl")
-    el, kms, _ = timed(torch, None, 1, steps, 1, stream, w.step)
+                     stream, dev, world, backend)
+    el, kms, _ = timed(torch, dist, world, steps, 1, stream, w.step)
     bpr = 3 * (8 + 1 / 8)
-    ach = bpr * total / (kms * 1e-3) / 1e9
-    return {"workload": "C3: ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 3 cols x 1e9 rows, 1% nulls",
+    ach = bpr * nrows / (kms * 1e-3) / 1e9
+    return {"workload": "C3: ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 3 cols x 1e9 rows, 1%% nulls, "
+                        "rows sharded over %d GPU(s), states all-gathered (RCCL) and folded in rank order" % world,
             "value": total / (el / steps), "unit": "rows/s", "ms_per_step": el / steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": ach / PEAK_HBM_GBPS, "traffic": None,
-                         "kernel": "dq_scan avg %.3f ms (HIP events), %.3f B/row" % (kms, bpr)}}
+                         "kernel": "dq_scan avg %.3f ms (HIP events, this rank), %.3f B/row x %d rows per GPU"
+                                   % (kms, bpr, nrows)}}
 
 
 def bench_c4(torch, N, D, ctx, stream, dev, total, steps):
@@ -533,11 +541,12 @@ def main():
                                    "(DESIGN.md §3)" % kms},
             "valu_roofline": valu}
         del s10
+        del table
+        torch.cuda.empty_cache()
+        sec["c3"] = bench_c3(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4), dist, world, rank,
+                             args.dist_backend)
+        torch.cuda.empty_cache()
         if world == 1:
-            del table
-            torch.cuda.empty_cache()
-            sec["c3"] = bench_c3(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4))
-            torch.cuda.empty_cache()
             sec["c4"] = bench_c4(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4))
             torch.cuda.empty_cache()
             sec["c2_host_streamed"] = bench_host_streamed(torch, N, D, ctx, dev, min(total, 200_000_000), 2)
