@@ -399,7 +399,7 @@ constexpr KllClass kKllXClasses[] = {{64, 4}, {64, 8}, {128, 8}, {256, 8}, {512,
 constexpr int kKllNumXClasses = sizeof(kKllXClasses) / sizeof(kKllXClasses[0]);
 constexpr int kKllAllClasses = kKllNumClasses + kKllNumXClasses;
 
-int kll_class_of(int len) {
+int kll_class_of_slow(int len) {
     for (int j = kKllNumXClasses - 1; j >= 0; --j) {
         const int P = kKllXClasses[j].t * kKllXClasses[j].e;
         if (len >= P && len - P <= 64) return kKllNumClasses + j;
@@ -407,6 +407,16 @@ int kll_class_of(int len) {
     for (int c = 0; c < kKllNumClasses; ++c)
         if (kKllClasses[c].t * kKllClasses[c].e >= len) return c;
     return -1;
+}
+
+// kll_class_of_slow tabulated over every compaction length the schedule admits (called per compaction, twice).
+int kll_class_of(int len) {
+    static const std::vector<int8_t> lut = [] {
+        std::vector<int8_t> t(kKllMaxPad + 1);
+        for (int l = 0; l <= kKllMaxPad; ++l) t[l] = (int8_t)kll_class_of_slow(l);
+        return t;
+    }();
+    return len >= 0 && len <= kKllMaxPad ? lut[len] : kll_class_of_slow(len);
 }
 
 int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nseg, double* dst,
@@ -640,6 +650,16 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
         n = 0;
     }
 
+    // the dense level-0 stream (a buffer of its own, so its write runs while the host computes the schedule)
+    if (!zero_copy && n > 0) {
+        double* dense = nullptr;
+        KL_HIP(ctx, buf.alloc((void**)&dense, (size_t)n * 8));
+        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows,
+                           (const unsigned long long*)doffs, dense);
+        KL_HIP(ctx, hipGetLastError());
+        stream0 = dense;
+    }
+
     // ---- the compaction schedule (count-only) ------------------------------------------------------
     KllSchedule sc;
     if (!kll_schedule(n, sketch_size, shrinking_factor, sc))
@@ -647,7 +667,7 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     const size_t nlev = sc.levels.size();
     const auto t1 = std::chrono::steady_clock::now();
 
-    // ---- device scratch (the context arena): [dense level-0 stream][levels >= 1][descriptors][min/max]
+    // ---- device scratch (the context arena): [levels >= 1][descriptors][min/max][tails][gathered final buffers]
     std::vector<int64_t> lbase(nlev, 0);
     int64_t upper = 0;
     for (size_t h = 1; h < nlev; ++h) {
@@ -656,8 +676,7 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     }
     size_t nseg_all = 0;
     for (const KllLevel& l : sc.levels) nseg_all += l.segs.size();
-    const size_t dense_bytes = zero_copy ? 0 : (size_t)n * 8;
-    const size_t up_off = (dense_bytes + 255) / 256 * 256;
+    const size_t up_off = 0;
     const size_t seg_off = up_off + ((size_t)upper * 8 + 255) / 256 * 256;
     const size_t mm_off = seg_off + (nseg_all * 8 + 255) / 256 * 256;
     int64_t ntail = 0;  // items left in the final buffers
@@ -669,13 +688,6 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     double* dup = reinterpret_cast<double*>(scratch + up_off);
     uint64_t* dsegs = reinterpret_cast<uint64_t*>(scratch + seg_off);
     unsigned long long* dminmax = reinterpret_cast<unsigned long long*>(scratch + mm_off);
-    if (!zero_copy && n > 0) {
-        double* dense = reinterpret_cast<double*>(scratch);
-        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows,
-                           (const unsigned long long*)doffs, dense);
-        KL_HIP(ctx, hipGetLastError());
-        stream0 = dense;
-    }
 
     // compactions grouped per (level, kernel class), staged in pinned memory: one launch per group; the
     // order inside a level is free because every compaction's input range and output slot are explicit
