@@ -11,9 +11,10 @@ The same JSON line carries `secondary` measurements of the other BASELINE worklo
 same way (its own steps, HIP events on the scan stream, its own roofline):
   suite10  the north-star 10-analyzer suite over the same 8 columns (C2 ops + Compliance(c > 0) +
            ApproxCountDistinct + Correlation(c_2k, c_2k+1): 69 ops), every rank count;
-  c3       ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 1e9 rows (N = 1);
+  c3       ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 1e9 rows sharded over the ranks;
   c4       the grouping analyzers' frequency table (computeFrequencies + the fused table aggregation) on
-           1e9 int64 keys with exactly 1e8 distinct, closed forms checked (N = 1);
+           1e9 int64 keys with exactly 1e8 distinct, closed forms checked (N = 1; N > 1: row shards, device
+           (key, count) pairs exchanged by RCCL all-to-all, owner tables);
   c2_host_streamed  the C2 suite over pinned host columns streamed through HBM (dq_scan_streamed): the
            end-to-end rate including the host link, never the headline value (N = 1).
 
@@ -225,6 +226,60 @@ def bench_c4(torch, N, D, ctx, stream, dev, total, steps):
                          "kernel": "end-to-end build + summary, wall clock per step (fast grouping: partition1_fast "
                                    "-> scatter2_fast -> build, DESIGN.md §3); algorithmic %.1f GB (keys read once + "
                                    "the groups' slots written and read once)" % ((bpr * total + table_bytes) / 1e9)}}
+
+
+def bench_c4_dist(torch, N, D, dev, total, steps, dist, world, rank):
+    """BASELINE config C4 over `world` GPUs: each rank holds a contiguous shard of the 1e9 keys (1e8 distinct) and the
+    DistributedAnalysisRunner computes Uniqueness / Distinctness / UniqueValueRatio / CountDistinct / Entropy: local
+    tables -> device (key, count) pairs -> RCCL all-to-all to the key's owner -> owner tables -> all-reduced summary.
+    Closed forms checked on every rank."""
+    import math
+    from deequ_amd import engine
+    from deequ_amd.distributed import DistributedAnalysisRunner
+    from deequ_amd.table import Table, Column
+    distinct = total // 10
+    per = (total + world - 1) // world
+    per = (per + 2047) // 2048 * 2048
+    row0 = min(rank * per, total)
+    nrows = max(0, min(total, row0 + per) - row0)
+    ctx = engine.ctx()
+    keys = torch.empty(max(nrows, 1), dtype=torch.int64, device=dev)
+    ctx.synth_freq_keys(total, distinct, row0, nrows, keys.data_ptr())
+    ctx.synchronize()
+    c = Column("k", N.TYPE_LONG, None, None, length=nrows)
+    c.device = {"values": keys}
+    t = Table([c])
+    analyzers = [D.Uniqueness(["k"]), D.Distinctness(["k"]), D.UniqueValueRatio(["k"]), D.CountDistinct(["k"]),
+                 D.Entropy("k")]
+    runner = DistributedAnalysisRunner()
+    out = {}
+
+    stream = torch.cuda.current_stream()
+
+    def step(ev):
+        if ev is not None:
+            ev[0].record(stream)
+        out["r"] = runner.run(t, analyzers)
+        if ev is not None:
+            ev[1].record(stream)
+
+    el, _, _ = timed(torch, dist, world, steps, 1, stream, step)
+    r = out["r"]
+    half = distinct // 2
+    big = (total - half) / half
+    ent = math.fsum([-half * (big / total) * math.log(big / total), -half * (1 / total) * math.log(1 / total)])
+    got = [r.metric(a).value.get() for a in analyzers]
+    exp = [half / total, distinct / total, half / distinct, float(distinct), ent]
+    assert all(abs(g - e) <= 1e-12 * abs(e) for g, e in zip(got, exp)), (got, exp)
+    bpr = 8.0
+    ach = (bpr * nrows + 2 * 16 * distinct / world) / (el / steps) / 1e9
+    return {"workload": "C4 over %d GPUs: DistributedAnalysisRunner grouping analyzers on 1e9 int64 keys (1e8 distinct), "
+                        "device (key, count) pairs exchanged by RCCL all-to-all to their owner rank; closed forms exact"
+                        % world,
+            "value": total / (el / steps), "unit": "rows/s", "ms_per_step": el / steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "kernel": "end-to-end step per rank (local build + exchange + owner build + summary)"}}
 
 
 C5_NUMERIC = [("d_dyad", 1), ("d_unif", 2), ("d_n100", 3), ("d_gauss", 6), ("d_corr", 7),
@@ -546,6 +601,9 @@ def main():
         sec["c3"] = bench_c3(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4), dist, world, rank,
                              args.dist_backend)
         torch.cuda.empty_cache()
+        if world > 1:
+            sec["c4"] = bench_c4_dist(torch, N, D, dev, total, max(3, args.steps // 4), dist, world, rank)
+            torch.cuda.empty_cache()
         if world == 1:
             sec["c4"] = bench_c4(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4))
             torch.cuda.empty_cache()

@@ -98,6 +98,24 @@ class Exchange:
         self.dist.all_gather_into_tensor(out, t, group=self.group)
         return out.cpu().tolist()
 
+    def all_to_all_tensors(self, tensors, send_counts):
+        """Rows of each tensor (same leading length, grouped by destination rank, send_counts[r] rows to rank r) to
+        their destination ranks, on the exchange device (RCCL over xGMI for nccl): the received tensors, in source
+        rank order, and the received counts."""
+        torch = self.torch
+        sc = send_counts.to(device=self.device, dtype=torch.int64)
+        rc = torch.empty_like(sc)
+        self.dist.all_to_all_single(rc, sc, group=self.group)
+        send = [int(v) for v in sc.cpu().tolist()]
+        recv = [int(v) for v in rc.cpu().tolist()]
+        out = []
+        for t in tensors:
+            src = t.to(self.device).contiguous()
+            dst = torch.empty(sum(recv), dtype=t.dtype, device=self.device)
+            self.dist.all_to_all_single(dst, src, output_split_sizes=recv, input_split_sizes=send, group=self.group)
+            out.append(dst)
+        return out, recv
+
     def all_to_all_blobs(self, blobs):
         """blobs[r] goes to rank r; returns the blobs every rank sent to this one, in rank order."""
         torch = self.torch
@@ -147,6 +165,37 @@ class GpuLocal:
         else:
             columns = [G.take(_host_column(shard[c]), keys) for c in cols]
         return G.GroupBlock(columns, counts, s["num_rows"], s["null_count"])
+
+    def pair_export(self, shard, col, include_nulls):
+        """This shard's table over one fixed-width key column as device (canonical key, count) int64 tensors, plus
+        its rows taking part and its NULL-key rows; None when the table is not keyed by values."""
+        import torch
+        ft = engine.frequencies(shard, [col], include_nulls)
+        if ft.key_kind() != N.FREQ_KEYS_VALUES:
+            return None
+        n = ft.num_groups
+        keys = torch.empty(max(n, 1), dtype=torch.int64, device="cuda")
+        counts = torch.empty(max(n, 1), dtype=torch.int64, device="cuda")
+        torch.cuda.current_stream().synchronize()  # allocated on torch's stream; written on the context's
+        ctx = engine.ctx()
+        got = ctx.lib.dq_freq_export_device(ctx.handle, ft.handle, n, keys.data_ptr(), counts.data_ptr())
+        if got < 0:
+            raise N.NativeError(int(got), "dq_freq_export_device: %s" % ctx.last_error())
+        ctx.synchronize()
+        s = ft.summary(None)
+        keys, counts = keys[:got], counts[:got]
+        return keys, counts, int(counts.sum().item()) if got else 0, int(s["null_count"])
+
+    def pairs_table(self, key_type, keys, counts, decimal_scale=0):
+        """The owner's table of the (canonical key, count) pairs it received (device tensors; duplicates add)."""
+        import torch
+        keys = keys.to("cuda").contiguous()
+        counts = counts.to("cuda").contiguous()
+        torch.cuda.current_stream().synchronize()
+        n = int(keys.numel())
+        return engine.FrequencyTable.from_pairs(key_type, (keys.data_ptr(), n), (counts.data_ptr(), n),
+                                                int(counts.sum().item()) if n else 0, 0, decimal_scale,
+                                                device_ptrs=True)
 
     def owned_table(self, block, include_nulls):
         """The owner's table over the groups it received, weighted by their counts (dq_frequencies_ex)."""
@@ -368,11 +417,41 @@ class DistributedAnalysisRunner:
         return self._local_step(lambda: G.concat([G.unpack(b, schema) for b in received], schema))
 
     def _frequencies(self, shard, cols, include_nulls=False):
+        if len(cols) == 1 and shard[cols[0]].spark_type != N.TYPE_STRING and hasattr(self.local, "pair_export"):
+            freq = self._frequencies_pairs(shard, cols[0], include_nulls)
+            if freq is not None:
+                return freq
         block = self._local_step(lambda: self.local.group_block(shard, cols, include_nulls))
         owned = self._shuffle(block, null_is_value=include_nulls)
         table = self._local_step(lambda: self.local.owned_table(owned, include_nulls))
         num_rows, null_rows = self.ex.all_reduce_i64([int(owned.counts.sum()), block.null_rows])
         return DistributedFrequencies(self, table, owned, shard[cols[0]], num_rows, null_rows)
+
+    def _frequencies_pairs(self, shard, col, include_nulls):
+        """One fixed-width key column: the shard's groups stay on the device as (canonical key, count) pairs, go to
+        their owner rank (a hash of the key) in one all-to-all on the exchange device (RCCL for nccl), and each owner
+        builds the weighted table of the pairs it received (dq_freq_from_pairs) — groups, not rows, cross ranks and
+        nothing passes through host memory. None (on every rank) when the table is not keyed by values."""
+        torch = self.ex.torch
+        world = self.ex.world
+        local = self._local_step(lambda: self.local.pair_export(shard, col, include_nulls))
+        if self.ex.all_reduce_i64([0 if local is None else 1])[0] != world:
+            return None
+        keys, counts, rows, nulls = local
+
+        def route():
+            mixed = keys ^ (keys >> 33)  # canonical keys of any fixed-width type spread over the owners
+            owner = torch.remainder(mixed & 0x7FFFFFFFFFFF, world)
+            order = torch.sort(owner, stable=True).indices
+            return keys[order], counts[order], torch.bincount(owner, minlength=world)
+        k_sorted, c_sorted, send = self._local_step(route)
+        (rk, rc), _ = self.ex.all_to_all_tensors([k_sorted, c_sorted], send)
+        c = shard[col]
+        table = self._local_step(lambda: self.local.pairs_table(c.spark_type, rk, rc, c.decimal_scale))
+        num_rows, null_rows = self.ex.all_reduce_i64([rows, nulls])
+        stub = G.GroupBlock([G.column_from_canonical(c.name, c.spark_type, np.zeros(0, dtype=np.int64),
+                                                     c.decimal_precision, c.decimal_scale)], np.zeros(0, dtype=np.int64))
+        return DistributedFrequencies(self, table, stub, c, num_rows, null_rows)
 
     def _mutual_information(self, shard, a):
         """MutualInformation over row shards (A/MutualInformation.scala:35-97): the joint (x, y) groups go to their
