@@ -509,57 +509,66 @@ struct KllLevel {
     int32_t offset = 0;    // NonSampleCompactor.offset
     int64_t pos = 0;       // first unconsumed item of this level's stream
     int64_t arrived = 0;   // items appended to this level's stream
-    std::vector<uint64_t> segs;                   // compactions, in order
     int64_t per_class[32] = {0};                  // compactions per kernel class
 };
 
 struct KllSchedule {
     std::vector<KllLevel> levels;
+    std::vector<uint64_t>* segs = nullptr;  // every compaction in schedule order, its level in bits 55-62
     int64_t actual = 0;
     int64_t total = 0;
 };
 
+constexpr int kKllMaxLevels = 64;
+
+// A bitmask of the levels whose buffer reached capacity makes condense's "lowest full level" one ctz, and an
+// update that finds no full level jumps straight to the next level-0 fill (nothing changes in between); the
+// compactions go to a per-thread buffer that keeps its pages across calls (~145k entries for 1e8 items).
 bool kll_schedule(int64_t n, int sketch_size, double f, KllSchedule& sc) {
-    std::vector<int> caps;
-    auto cap = [&](int h) {
-        while ((int)caps.size() <= h) caps.push_back(kll_capacity(sketch_size, f, (int)caps.size()));
-        return (int64_t)caps[h];
-    };
+    static thread_local std::vector<uint64_t> events;
+    events.clear();
+    sc.segs = &events;
+    int64_t cap[kKllMaxLevels + 1];
+    for (int h = 0; h <= kKllMaxLevels; ++h) cap[h] = kll_capacity(sketch_size, f, h);
     sc.levels.assign(1, KllLevel());
-    sc.total = cap(0);
+    sc.levels.reserve(kKllMaxLevels + 1);
+    sc.total = cap[0];
     sc.actual = 0;
+    uint64_t full = 0;  // bit h: levels[h].len >= cap[h]
     int64_t rem = n;
     while (rem > 0) {
-        const int64_t k = std::min<int64_t>(rem, std::max<int64_t>(1, sc.total - sc.actual + 1));
-        sc.levels[0].len += k;
-        sc.levels[0].arrived += k;
+        KllLevel& l0 = sc.levels[0];
+        int64_t k = std::max<int64_t>(1, sc.total - sc.actual + 1);
+        if (sc.actual > sc.total && full == 0) k = std::max<int64_t>(k, cap[0] - l0.len);
+        k = std::min<int64_t>(rem, k);
+        l0.len += k;
+        l0.arrived += k;
         sc.actual += k;
         rem -= k;
-        if (sc.actual <= sc.total) continue;
-        for (size_t h = 0; h < sc.levels.size(); ++h) {
-            if (sc.levels[h].len < cap((int)h)) continue;
-            if (h + 1 >= sc.levels.size()) {
-                if (sc.levels.size() >= 120) return false;
-                sc.levels.push_back(KllLevel());
-                sc.total = 0;
-                for (size_t i = 0; i < sc.levels.size(); ++i) sc.total += cap((int)i);
-            }
-            KllLevel& lv = sc.levels[h];
-            const int64_t items = lv.len;
-            const int64_t L = items - items % 2;
-            if (L > kKllMaxPad) return false;
-            if (lv.ncomp % 2 == 1) lv.offset = 1 - lv.offset;
-            KllLevel& up = sc.levels[h + 1];
-            lv.segs.push_back(kll_desc((uint64_t)lv.pos, (uint32_t)L, (uint32_t)lv.offset));
-            ++lv.per_class[kll_class_of((int)L)];
-            lv.pos += L;
-            lv.len = items % 2;
-            up.len += L / 2;
-            up.arrived += L / 2;
-            lv.ncomp += 1;
-            sc.actual -= L / 2;  // = the sum of buffer lengths, as getCompactorItemsCount recomputes it
-            break;
+        if (l0.len >= cap[0]) full |= 1ull;
+        if (sc.actual <= sc.total || full == 0) continue;
+        const int h = __builtin_ctzll(full);
+        if (h + 1 >= (int)sc.levels.size()) {
+            if ((int)sc.levels.size() >= kKllMaxLevels) return false;
+            sc.levels.push_back(KllLevel());
+            sc.total += cap[sc.levels.size() - 1];
         }
+        KllLevel& lv = sc.levels[h];
+        const int64_t items = lv.len;
+        const int64_t L = items - items % 2;
+        if (L > kKllMaxPad) return false;
+        if (lv.ncomp % 2 == 1) lv.offset = 1 - lv.offset;
+        KllLevel& up = sc.levels[h + 1];
+        events.push_back(kll_desc((uint64_t)lv.pos, (uint32_t)L, (uint32_t)lv.offset) | ((uint64_t)h << 55));
+        ++lv.per_class[kll_class_of((int)L)];
+        lv.pos += L;
+        lv.len = items % 2;
+        full &= ~(1ull << h);
+        up.len += L / 2;
+        up.arrived += L / 2;
+        if (up.len >= cap[h + 1]) full |= 1ull << (h + 1);
+        lv.ncomp += 1;
+        sc.actual -= L / 2;  // = the sum of buffer lengths, as getCompactorItemsCount recomputes it
     }
     return true;
 }
@@ -675,7 +684,7 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
         upper += sc.levels[h].arrived;
     }
     size_t nseg_all = 0;
-    for (const KllLevel& l : sc.levels) nseg_all += l.segs.size();
+    nseg_all = sc.segs->size();
     const size_t up_off = 0;
     const size_t seg_off = up_off + ((size_t)upper * 8 + 255) / 256 * 256;
     const size_t mm_off = seg_off + (nseg_all * 8 + 255) / 256 * 256;
@@ -704,16 +713,17 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     KllTail* htails = reinterpret_cast<KllTail*>(pin + pin_tails);
     double* hgat = reinterpret_cast<double*>(pin + pin_out);
     size_t pos = 0;
+    std::vector<size_t> cursor(nlev * kKllAllClasses);
     for (size_t h = 0; h < nlev; ++h) {
         const KllLevel& l = sc.levels[h];
-        size_t cursor[kKllAllClasses];
         for (int c = 0; c < kKllAllClasses; ++c) {
-            cursor[c] = pos;
+            cursor[h * kKllAllClasses + c] = pos;
             if (l.per_class[c]) launches.push_back({h, pos, (size_t)l.per_class[c], c});
             pos += (size_t)l.per_class[c];
         }
-        for (const uint64_t d : l.segs) hsegs[cursor[kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
     }
+    for (const uint64_t d : *sc.segs)  // grouped by (level, class), schedule order inside a group
+        hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
     if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, s));
     const unsigned long long mm_init[2] = {~0ull, 0ull};
     KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, s));
