@@ -58,6 +58,9 @@ constexpr int kSizingRegs = 4096;  // HLL registers used only to size the table
 constexpr int kFreqBlock = 256;
 constexpr int kDigitBins = 256;    // radix partition: first pass on the low 8 bits of the key
 constexpr int kPartTile = 4096;    // keys per workgroup tile of the partition scatters (16 per lane), general path
+// fast pass 1 tile (keys per workgroup tile); measured on C4 end to end (profiles/r02/c4_p1_tile_r02bh.log):
+// 2048 -> 15.2-15.5 ms, 4096 -> 13.8-13.9 ms, 8192 -> 17.5 ms
+constexpr int kP1TileFast = 4096;
 constexpr int kPartTileFast = 8192;// second pass, fast path: 32 per lane, so a tile's 256 per-digit runs average 256 B
                                    // (measured: scatter2 5.85 -> 4.88 ms on C4; partition1 slows down at 8192)
 constexpr int kPass2Item = 65536;  // keys per work item of the second partition pass
@@ -1651,19 +1654,19 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     // (measured: an 8 K-key pass-1 tile runs 8.1 ms against 6.1 ms for 4 K on C4 -- twice the registers)
     switch (elem_size((ElemType)t->ks.cols[0].elem)) {
         case 8:
-            hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 8>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+            hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, 8>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
                                nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
             break;
         case 4:
-            hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 4>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+            hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, 4>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
                                nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
             break;
         case 2:
-            hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 2>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+            hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, 2>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
                                nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
             break;
         default:
-            hipLaunchKernelGGL((partition1_fast_kernel<kPartTile, 1>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
+            hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, 1>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
                                nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
             break;
     }
