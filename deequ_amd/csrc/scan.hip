@@ -418,6 +418,35 @@ __device__ __forceinline__ uint64_t spark_hash(uint64_t v, int spark_type) {
     }
 }
 
+// Lane-level helpers shared by the striped and the lean kernels (see scan_heavy8_kernel).
+__device__ __forceinline__ uint32_t row_mask(uint32_t m, int k) { return (uint32_t)(((int)(m << (31 - k))) >> 31); }
+__device__ __forceinline__ double pack_f64(uint32_t hi, uint32_t lo) { return as_f64(((uint64_t)hi << 32) | lo); }
+__device__ __forceinline__ uint32_t hi32(double d) { return (uint32_t)(f64_bits(d) >> 32); }
+__device__ __forceinline__ uint32_t lo32(double d) { return (uint32_t)f64_bits(d); }
+__device__ __forceinline__ double and_f64(double d, uint32_t mk) { return pack_f64(hi32(d) & mk, lo32(d) & mk); }
+// v_min_f64 / v_max_f64 without the compiler's canonicalising v_max_f64 x, x of each operand: a NaN operand is
+// dropped (a signalling NaN can make the result NaN; batches with NaN rows take the exact path).
+__device__ __forceinline__ double raw_min(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double raw_max(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {  // leading zeros, 0xFFFFFFFF for 0
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// (double)(int64_t)v correctly rounded in 3 instructions (hi * 2^32 is exact; one rounding in the fma)
+__device__ __forceinline__ double i64_to_f64(uint64_t v) {
+    return __builtin_fma((double)(int32_t)(uint32_t)(v >> 32), 4294967296.0, (double)(uint32_t)v);
+}
+__device__ __forceinline__ double one_if(uint32_t mk) { return pack_f64(mk & 0x3FF00000u, 0u); }
+
 // ------------------------------------------------------------------------------------------------
 // Per-lane accumulators, specialised by storage class so only live state occupies VGPRs.
 // ------------------------------------------------------------------------------------------------
@@ -428,6 +457,7 @@ struct FAcc {  // FLOAT / DOUBLE column
 struct IAcc {  // integral column (Long sum with wrap-around, integer min/max)
     int64_t n, sum, mn, mx, pt;
     double mean, m2;
+    double dmn, dmx;  // striped kernel: extremes of batches whose values are all exact doubles (|x| < 2^53)
 };
 template <bool F> struct AccOf { using type = IAcc; };
 template <> struct AccOf<true> { using type = FAcc; };
@@ -444,6 +474,14 @@ __device__ __forceinline__ void acc_init(IAcc& a) {
     a.mn = INT64_MAX;
     a.mx = INT64_MIN;
     a.mean = a.m2 = 0.0;
+    a.dmn = a.dmx = __builtin_nan("");
+}
+// Folds the double-tracked extremes into the int64 ones before the cross-lane reduction (exact: |x| < 2^53).
+__device__ __forceinline__ void acc_finish(FAcc&) {}
+__device__ __forceinline__ void acc_finish(IAcc& a) {
+    if (a.dmn == a.dmn && (int64_t)a.dmn < a.mn) a.mn = (int64_t)a.dmn;
+    if (a.dmx == a.dmx && (int64_t)a.dmx > a.mx) a.mx = (int64_t)a.dmx;
+    a.dmn = a.dmx = __builtin_nan("");
 }
 
 __device__ __forceinline__ void acc_merge(FAcc& a, const FAcc& b) {
@@ -597,40 +635,54 @@ __device__ __forceinline__ void accumulate(FAcc& a, const uint64_t (&v)[8], uint
     a.n += cnt;
 }
 
+// Integral batch: each value converted to double once (3 instructions, exact while |x| < 2^53) for the moments and
+// the min / max (raw v_min / v_max over NaN stand-ins; a batch holding a larger magnitude takes the exact int64
+// compares instead), the Long sum over bit-cleared values.
 __device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint32_t m, uint32_t flags) {
     const int cnt = __popc(m);
     if (cnt == 0) return;
-    if (flags & CF_STATS) {
-        int64_t s = 0, mn = INT64_MAX, mx = INT64_MIN;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int64_t x = (int64_t)v[k];
-            const bool on = (m >> k) & 1u;
-            s = (int64_t)((uint64_t)s + (on ? (uint64_t)x : 0ull));
-            mn = (on && x < mn) ? x : mn;
-            mx = (on && x > mx) ? x : mx;
-        }
-        a.sum = (int64_t)((uint64_t)a.sum + (uint64_t)s);
-        a.mn = mn < a.mn ? mn : a.mn;
-        a.mx = mx > a.mx ? mx : a.mx;
-    }
-    if (flags & CF_MOMENTS) {
-        // Spark casts each value to Double before the moment update (C/StatefulStdDevPop.scala:24).
+    const bool stats = (flags & CF_STATS) != 0, moments = (flags & CF_MOMENTS) != 0;
+    if (stats || moments) {
         double xd[8];
-        double s = 0.0;
+        uint64_t bs = 0;
+        double s = 0.0, mn = __builtin_nan(""), mx = __builtin_nan("");
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            xd[k] = (double)(int64_t)v[k];       // finite for every row, kept or not
-            s = __builtin_fma(xd[k], on_factor(m, k), s);  // x * 1.0 + s rounds like x + s; x * 0.0 adds +-0
+            const uint32_t mk = row_mask(m, k);
+            xd[k] = i64_to_f64(v[k]);
+            if (stats) {
+                bs += ((uint64_t)((uint32_t)(v[k] >> 32) & mk) << 32) | ((uint32_t)v[k] & mk);
+                const double xn = pack_f64((hi32(xd[k]) & mk) | (~mk & 0x7FF80000u), lo32(xd[k]));
+                mn = raw_min(mn, xn);
+                mx = raw_max(mx, xn);
+            }
+            if (moments) s = __builtin_fma(xd[k], one_if(mk), s);
         }
-        const double mb = s * rcp_refined((double)cnt);
-        double m2b = 0.0;
+        if (stats) {
+            a.sum = (int64_t)((uint64_t)a.sum + bs);
+            if (__builtin_expect(fabs(mn) >= 9007199254740992.0 || fabs(mx) >= 9007199254740992.0, 0)) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const double d = (xd[k] - mb) * on_factor(m, k);
-            m2b = __builtin_fma(d, d, m2b);
+                for (int k = 0; k < 8; ++k) {
+                    const int64_t x = (int64_t)v[k];
+                    const bool on = (m >> k) & 1u;
+                    a.mn = (on && x < a.mn) ? x : a.mn;
+                    a.mx = (on && x > a.mx) ? x : a.mx;
+                }
+            } else {
+                a.dmn = raw_min(a.dmn, mn);
+                a.dmx = raw_max(a.dmx, mx);
+            }
         }
-        moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
+        if (moments) {
+            const double mb = s * rcp_refined((double)cnt);
+            double m2b = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double d = (xd[k] - mb) * one_if(row_mask(m, k));
+                m2b = __builtin_fma(d, d, m2b);
+            }
+            moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
+        }
     }
     a.n += cnt;
 }
@@ -938,6 +990,8 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
             if (NC > 1) load_values<P, F1>(c1, nfull * kTileRows, tid, false, nrows, y);
             fold(nfull * kTileRows, false, x, y);
         }
+        acc_finish(a0);
+        acc_finish(a1);
         // wave64 tree, then the 4 wave results in a fixed order.
 #pragma unroll 1
         for (int off = 32; off > 0; off >>= 1) {
@@ -1023,33 +1077,6 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
 //    2^-23 case of a zero rank field takes a per-tile exact re-hash.
 // Bit-exact HLL registers, counts, integral sums and min / max; fp64 moments within rounding of the batch order.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t row_mask(uint32_t m, int k) { return (uint32_t)(((int)(m << (31 - k))) >> 31); }
-__device__ __forceinline__ double pack_f64(uint32_t hi, uint32_t lo) { return as_f64(((uint64_t)hi << 32) | lo); }
-__device__ __forceinline__ uint32_t hi32(double d) { return (uint32_t)(f64_bits(d) >> 32); }
-__device__ __forceinline__ uint32_t lo32(double d) { return (uint32_t)f64_bits(d); }
-__device__ __forceinline__ double and_f64(double d, uint32_t mk) { return pack_f64(hi32(d) & mk, lo32(d) & mk); }
-// v_min_f64 / v_max_f64 without the compiler's canonicalising v_max_f64 x, x of each operand: a NaN operand is
-// dropped (a signalling NaN can make the result NaN; batches with NaN rows take the exact path).
-__device__ __forceinline__ double raw_min(double a, double b) {
-    double r;
-    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ double raw_max(double a, double b) {
-    double r;
-    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {  // leading zeros, 0xFFFFFFFF for 0
-    uint32_t r;
-    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
-    return r;
-}
-// (double)(int64_t)v correctly rounded in 3 instructions (hi * 2^32 is exact; one rounding in the fma)
-__device__ __forceinline__ double i64_to_f64(uint64_t v) {
-    return __builtin_fma((double)(int32_t)(uint32_t)(v >> 32), 4294967296.0, (double)(uint32_t)v);
-}
-__device__ __forceinline__ double one_if(uint32_t mk) { return pack_f64(mk & 0x3FF00000u, 0u); }
 
 // Fused compare of the cleared value (masked rows hold 0 / 0.0) — Spark semantics (NaN above every number,
 // NaN = NaN, -0.0 = 0.0) for a non-NaN double constant; integral columns against a LONG constant compare as long.
@@ -1141,6 +1168,7 @@ __device__ __forceinline__ void hacc_to(IAcc& o, const HAccI& a) {
     if (a.mx == a.mx && (int64_t)a.mx > o.mx) o.mx = (int64_t)a.mx;
     o.mean = a.mean;
     o.m2 = a.m2;
+    o.dmn = o.dmx = __builtin_nan("");
 }
 
 // Chan merge of one batch (cnt >= 1 rows, mean mb, m2b) into the lane moments.

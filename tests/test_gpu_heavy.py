@@ -97,3 +97,14 @@ def test_full_variant_run_to_run_reproducible():
         assert (m1.isSuccess == m2.isSuccess) and (not m1.isSuccess or
                                                    (math.isnan(m1.get()) and math.isnan(m2.get())) or
                                                    m1.get() == m2.get()), x
+
+
+@pytest.mark.parametrize("n", [2049, 300007])
+def test_striped_kernel_edge_data(n):
+    """The striped kernel (no HLL / compare / correlation): integral min / max tracked as doubles with the exact
+    int64 fallback for batches beyond 2^53, Long sums, NaN / inf / -0.0 rows and garbage in NULL slots."""
+    t = edge_table(n, n + 5)
+    analyzers = [D.Size()]
+    for c in ("a", "b", "l", "k"):
+        analyzers += [D.Completeness(c), D.Mean(c), D.Sum(c), D.Minimum(c), D.Maximum(c), D.StandardDeviation(c)]
+    run_parity(t, analyzers)
