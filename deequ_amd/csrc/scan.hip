@@ -638,52 +638,57 @@ __device__ __forceinline__ void accumulate(FAcc& a, const uint64_t (&v)[8], uint
 // Integral batch: each value converted to double once (3 instructions, exact while |x| < 2^53) for the moments and
 // the min / max (raw v_min / v_max over NaN stand-ins; a batch holding a larger magnitude takes the exact int64
 // compares instead), the Long sum over bit-cleared values.
+template <bool S, bool M>
+__device__ __forceinline__ void accumulate_int(IAcc& a, const uint64_t (&v)[8], uint32_t m, int cnt) {
+    double xd[8];
+    uint64_t bs = 0;
+    double s = 0.0, mn = __builtin_nan(""), mx = __builtin_nan("");
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t mk = row_mask(m, k);
+        xd[k] = i64_to_f64(v[k]);
+        if constexpr (S) {
+            bs += ((uint64_t)((uint32_t)(v[k] >> 32) & mk) << 32) | ((uint32_t)v[k] & mk);
+            const double xn = pack_f64((hi32(xd[k]) & mk) | (~mk & 0x7FF80000u), lo32(xd[k]));
+            mn = raw_min(mn, xn);
+            mx = raw_max(mx, xn);
+        }
+        if constexpr (M) s = __builtin_fma(xd[k], one_if(mk), s);
+    }
+    if constexpr (S) {
+        a.sum = (int64_t)((uint64_t)a.sum + bs);
+        if (__builtin_expect(fabs(mn) >= 9007199254740992.0 || fabs(mx) >= 9007199254740992.0, 0)) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int64_t x = (int64_t)v[k];
+                const bool on = (m >> k) & 1u;
+                a.mn = (on && x < a.mn) ? x : a.mn;
+                a.mx = (on && x > a.mx) ? x : a.mx;
+            }
+        } else {
+            a.dmn = raw_min(a.dmn, mn);
+            a.dmx = raw_max(a.dmx, mx);
+        }
+    }
+    if constexpr (M) {
+        const double mb = s * rcp_refined((double)cnt);
+        double m2b = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double d = (xd[k] - mb) * one_if(row_mask(m, k));
+            m2b = __builtin_fma(d, d, m2b);
+        }
+        moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
+    }
+}
 __device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint32_t m, uint32_t flags) {
     const int cnt = __popc(m);
     if (cnt == 0) return;
+    // the flags are wave-uniform: one branch per batch picks a straight-line body
     const bool stats = (flags & CF_STATS) != 0, moments = (flags & CF_MOMENTS) != 0;
-    if (stats || moments) {
-        double xd[8];
-        uint64_t bs = 0;
-        double s = 0.0, mn = __builtin_nan(""), mx = __builtin_nan("");
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t mk = row_mask(m, k);
-            xd[k] = i64_to_f64(v[k]);
-            if (stats) {
-                bs += ((uint64_t)((uint32_t)(v[k] >> 32) & mk) << 32) | ((uint32_t)v[k] & mk);
-                const double xn = pack_f64((hi32(xd[k]) & mk) | (~mk & 0x7FF80000u), lo32(xd[k]));
-                mn = raw_min(mn, xn);
-                mx = raw_max(mx, xn);
-            }
-            if (moments) s = __builtin_fma(xd[k], one_if(mk), s);
-        }
-        if (stats) {
-            a.sum = (int64_t)((uint64_t)a.sum + bs);
-            if (__builtin_expect(fabs(mn) >= 9007199254740992.0 || fabs(mx) >= 9007199254740992.0, 0)) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int64_t x = (int64_t)v[k];
-                    const bool on = (m >> k) & 1u;
-                    a.mn = (on && x < a.mn) ? x : a.mn;
-                    a.mx = (on && x > a.mx) ? x : a.mx;
-                }
-            } else {
-                a.dmn = raw_min(a.dmn, mn);
-                a.dmx = raw_max(a.dmx, mx);
-            }
-        }
-        if (moments) {
-            const double mb = s * rcp_refined((double)cnt);
-            double m2b = 0.0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const double d = (xd[k] - mb) * one_if(row_mask(m, k));
-                m2b = __builtin_fma(d, d, m2b);
-            }
-            moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
-        }
-    }
+    if (stats && moments) accumulate_int<true, true>(a, v, m, cnt);
+    else if (stats) accumulate_int<true, false>(a, v, m, cnt);
+    else if (moments) accumulate_int<false, true>(a, v, m, cnt);
     a.n += cnt;
 }
 
