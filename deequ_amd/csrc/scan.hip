@@ -642,7 +642,7 @@ template <bool S, bool M>
 __device__ __forceinline__ void accumulate_int(IAcc& a, const uint64_t (&v)[8], uint32_t m, int cnt) {
     double xd[8];
     uint64_t bs = 0;
-    double s = 0.0, mn = __builtin_nan(""), mx = __builtin_nan("");
+    double mn = __builtin_nan(""), mx = __builtin_nan("");
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const uint32_t mk = row_mask(m, k);
@@ -653,7 +653,6 @@ __device__ __forceinline__ void accumulate_int(IAcc& a, const uint64_t (&v)[8], 
             mn = raw_min(mn, xn);
             mx = raw_max(mx, xn);
         }
-        if constexpr (M) s = __builtin_fma(xd[k], one_if(mk), s);
     }
     if constexpr (S) {
         a.sum = (int64_t)((uint64_t)a.sum + bs);
@@ -671,14 +670,25 @@ __device__ __forceinline__ void accumulate_int(IAcc& a, const uint64_t (&v)[8], 
         }
     }
     if constexpr (M) {
-        const double mb = s * rcp_refined((double)cnt);
-        double m2b = 0.0;
+        // Deviations from a shift c, then one reciprocal: with c = the running mean (or, on the lane's first
+        // batch, any value of the batch) the Chan merge of (cnt, mean_b, m2_b) into (n, mean, m2) collapses to
+        // mean' = c + S1 / n', m2' = m2 + S2 - S1^2 / n' (S1, S2: sums of the shifted deviations; n' = n + cnt).
+        double c = a.mean;
+        if (a.n == 0) {
+            c = 0.0;
+#pragma unroll
+            for (int k = 7; k >= 0; --k) c = ((m >> k) & 1u) ? xd[k] : c;
+        }
+        double s1 = 0.0, s2 = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const double d = (xd[k] - mb) * one_if(row_mask(m, k));
-            m2b = __builtin_fma(d, d, m2b);
+            const double d = (xd[k] - c) * one_if(row_mask(m, k));
+            s1 += d;
+            s2 = __builtin_fma(d, d, s2);
         }
-        moments_merge_batch(a.n, a.mean, a.m2, cnt, mb, m2b);
+        const double r = rcp_refined((double)(a.n + cnt));
+        a.mean = __builtin_fma(s1, r, c);
+        a.m2 += __builtin_fma(-s1 * s1, r, s2);
     }
 }
 __device__ __forceinline__ void accumulate(IAcc& a, const uint64_t (&v)[8], uint32_t m, uint32_t flags) {
@@ -1257,7 +1267,6 @@ __device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, cons
             } else {
                 xi[k] = ((uint64_t)((uint32_t)(v[k] >> 32) & mk) << 32) | ((uint32_t)v[k] & mk);
                 xd[k] = i64_to_f64(v[k]);
-                if (FULL || hc.moments) s = __builtin_fma(xd[k], one_if(mk), s);
             }
         }
     } else if (F) {
@@ -1330,13 +1339,33 @@ __device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, cons
             }
         }
     }
-    if ((FULL || hc.moments) && cnt) {
+    if constexpr (!F) {
+        if ((FULL || hc.moments) && cnt) {
+            // finite values: shifted deviations and one reciprocal (see accumulate_int)
+            double c0 = a.mean;
+            if (a.n == 0) {
+                c0 = 0.0;
+#pragma unroll
+                for (int k = 7; k >= 0; --k) c0 = ((m >> k) & 1u) ? xd[k] : c0;
+            }
+            double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const double d = (xd[k] - c0) * one_if(row_mask(m, k));
+                s1 += d;
+                s2 = __builtin_fma(d, d, s2);
+            }
+            const double r = rcp_refined((double)(a.n + cnt));
+            a.mean = __builtin_fma(s1, r, c0);
+            a.m2 += __builtin_fma(-s1 * s1, r, s2);
+        }
+    } else if ((FULL || hc.moments) && cnt) {
         const double mb = s * rcp_refined((double)cnt);
         double m2b = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint32_t mk = row_mask(m, k);
-            const double d = F ? and_f64(xd[k] - mb, mk) : (xd[k] - mb) * one_if(mk);
+            const double d = and_f64(xd[k] - mb, mk);
             m2b = __builtin_fma(d, d, m2b);
         }
         hmoments_merge(a.n, a.mean, a.m2, cnt, mb, m2b);
