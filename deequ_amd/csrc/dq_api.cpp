@@ -49,6 +49,22 @@ int fail(dq_ctx* ctx, int code, const char* fmt, ...) {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// DQ_SCAN_CONCURRENT=1: the scan's launch shapes run concurrently on side streams (read per call).
+bool scan_concurrency() {
+    const char* e = getenv("DQ_SCAN_CONCURRENT");
+    return e && e[0] == '1';
+}
+
+int ensure_side_streams(dq_ctx* ctx) {
+    if (ctx->fork_ev) return DQ_OK;
+    for (int i = 0; i < dq_ctx::kSide; ++i) {
+        DQ_HIP(ctx, hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking));
+        DQ_HIP(ctx, hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming));
+    }
+    DQ_HIP(ctx, hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
+    return DQ_OK;
+}
+
 // Bump allocator over the context arena. Two passes: measure, then (after growth) assign.
 struct Bump {
     size_t off = 0;
@@ -250,6 +266,11 @@ void dq_close(dq_ctx* ctx) {
     scratch_trim(ctx);
     if (ctx->arena) (void)hipFree(ctx->arena);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    for (int i = 0; i < dq_ctx::kSide; ++i) {
+        if (ctx->side[i]) (void)hipStreamDestroy(ctx->side[i]);
+        if (ctx->join_ev[i]) (void)hipEventDestroy(ctx->join_ev[i]);
+    }
+    if (ctx->fork_ev) (void)hipEventDestroy(ctx->fork_ev);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
     delete ctx;
 }
@@ -714,9 +735,15 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         }
         groups[it->second].slots.push_back(s);
     }
+    // concurrent launches: each shape gets its share of the chip so the launches are co-resident
+    const int nlaunch = (int)groups.size() + (nsslots ? 1 : 0);
+    const bool concurrent = scan_concurrency() && nlaunch > 1 && ensure_side_streams(ctx) == DQ_OK;
+    if (concurrent)
+        for (Group& g : groups) g.grid = std::max(1, (g.grid + nlaunch - 1) / nlaunch);
     int gstride = 1;
     for (const Group& g : groups) gstride = std::max(gstride, g.grid);
-    const int sgrid = nsslots ? string_scan_grid(ctx->cus, nrows) : 0;
+    int sgrid = nsslots ? string_scan_grid(ctx->cus, nrows) : 0;
+    if (concurrent && sgrid) sgrid = std::max(1, (sgrid + nlaunch - 1) / nlaunch);
     gstride = std::max(gstride, sgrid);
     std::vector<int32_t> slot_nblocks(std::max<size_t>(slots.size(), 1), 1);
     for (const Group& g : groups)
@@ -901,16 +928,6 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             if (rc) return rc;
             rc = upload(dslot_nb, slot_nblocks.data(), sizeof(int32_t) * slot_nblocks.size());
             if (rc) return rc;
-            size_t off = 0;
-            for (const Group& g : groups) {
-                if (launch_scan_group(g.kind, g.P, g.nc, g.f0, g.f1, g.heavy, dslots, dgroups + off, (int)g.slots.size(), nrows,
-                                      ntiles, gstride, g.grid, partials, hllp, ctx->stream) != 0)
-                    return fail(ctx, DQ_ERR_DEVICE, "scan launch failed for shape (%d,%d,%d)", g.kind, g.P, g.nc);
-                DQ_HIP(ctx, hipGetLastError());
-                off += g.slots.size();
-            }
-            launch_reduce_partials(partials, dslot_nb, nslots, gstride, finals, ctx->stream);
-            DQ_HIP(ctx, hipGetLastError());
         }
         if (nsslots) {
             for (StrSlot& ss : sslots) {
@@ -924,7 +941,41 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             }
             rc = upload(dsslots, sslots.data(), sizeof(StrSlot) * nsslots);
             if (rc) return rc;
-            launch_string_scan(dsslots, nsslots, nrows, sgrid, gstride, spartials, hllp, ctx->stream);
+        }
+        // the scan launches: in order on the ctx stream, or one stream each (fork / join) when concurrent
+        int used_side = 0;
+        auto launch_stream = [&](int i) -> hipStream_t {
+            if (!concurrent || i == 0) return ctx->stream;
+            const int j = (i - 1) % dq_ctx::kSide;
+            used_side = std::max(used_side, j + 1);
+            return ctx->side[j];
+        };
+        if (concurrent) {
+            DQ_HIP(ctx, hipEventRecord(ctx->fork_ev, ctx->stream));
+            for (int j = 0; j < std::min(nlaunch - 1, dq_ctx::kSide); ++j)
+                DQ_HIP(ctx, hipStreamWaitEvent(ctx->side[j], ctx->fork_ev, 0));
+        }
+        int li = 0;
+        if (nslots) {
+            size_t off = 0;
+            for (const Group& g : groups) {
+                if (launch_scan_group(g.kind, g.P, g.nc, g.f0, g.f1, g.heavy, dslots, dgroups + off, (int)g.slots.size(), nrows,
+                                      ntiles, gstride, g.grid, partials, hllp, launch_stream(li++)) != 0)
+                    return fail(ctx, DQ_ERR_DEVICE, "scan launch failed for shape (%d,%d,%d)", g.kind, g.P, g.nc);
+                DQ_HIP(ctx, hipGetLastError());
+                off += g.slots.size();
+            }
+        }
+        if (nsslots) {
+            launch_string_scan(dsslots, nsslots, nrows, sgrid, gstride, spartials, hllp, launch_stream(li++));
+            DQ_HIP(ctx, hipGetLastError());
+        }
+        for (int j = 0; j < used_side; ++j) {
+            DQ_HIP(ctx, hipEventRecord(ctx->join_ev[j], ctx->side[j]));
+            DQ_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->join_ev[j], 0));
+        }
+        if (nslots) {
+            launch_reduce_partials(partials, dslot_nb, nslots, gstride, finals, ctx->stream);
             DQ_HIP(ctx, hipGetLastError());
         }
         if (nslots || nsslots) ctx->scan_launches++;

@@ -213,6 +213,12 @@ struct dq_ctx {
     uint8_t* pinned = nullptr;
     size_t pinned_cap = 0;
     int cus = 256;
+    // Side streams: scan launches of different shapes (and the string scan) run concurrently, forked from and
+    // joined back to `stream` by events, so a VALU-heavy shape shares the CUs with a memory-bound one.
+    static constexpr int kSide = 3;
+    hipStream_t side[kSide] = {};
+    hipEvent_t fork_ev = nullptr;
+    hipEvent_t join_ev[kSide] = {};
     std::map<int, int> occupancy;  // launch shape -> workgroups per CU
     int64_t scan_launches = 0;
     // Released device scratch of the grouping builds (multi-GB partition buffers and tables), re-used in stream
