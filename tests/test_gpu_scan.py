@@ -36,7 +36,9 @@ def test_scan_kats_one_by_one(kats):
 
 
 def test_scan_kats_fused_in_one_run(kats):
-    # All shareable analyzers of a fixture in ONE AnalysisRunner run -> ONE fused scan launch.
+    # All shareable analyzers of a fixture in ONE AnalysisRunner run -> ONE fused scan call (dq_scan_launch_count
+    # counts calls). HBM passes are not counted here: columns that a `where` / non-fused Compliance predicate reads
+    # are read once more by the predicate pass (predicate_kernel), the scan reads every column once.
     by_fixture = {}
     for k in scan_kats(kats):
         by_fixture.setdefault(k["fixture"], []).append(k)
