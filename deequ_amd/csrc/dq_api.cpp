@@ -49,10 +49,126 @@ int fail(dq_ctx* ctx, int code, const char* fmt, ...) {
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// DQ_PRED_VM=1: every predicate on the general VM (A/B and cross-checks of the simple-predicate kernel).
+bool pred_vm_forced() {
+    const char* e = getenv("DQ_PRED_VM");
+    return e && e[0] == '1';
+}
+
 // DQ_SCAN_CONCURRENT=1: the scan's launch shapes run concurrently on side streams (read per call).
 bool scan_concurrency() {
     const char* e = getenv("DQ_SCAN_CONCURRENT");
     return e && e[0] == '1';
+}
+
+// Recognises the predicates pred_simple_kernel evaluates (see PredSimple): a symbolic run of the postfix program.
+bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, int ncols, PredSimple& out) {
+    memset(&out, 0, sizeof(out));
+    enum { E_COL, E_CONST, E_BOOL };
+    struct Ent { int kind, idx; };
+    std::vector<Ent> st;
+    auto fixed_numeric = [&](int c) {
+        if (c < 0 || c >= ncols) return false;
+        switch (columns[c].spark_type) {
+            case DQ_TYPE_BOOLEAN: case DQ_TYPE_BYTE: case DQ_TYPE_SHORT: case DQ_TYPE_INT: case DQ_TYPE_DATE:
+            case DQ_TYPE_LONG: case DQ_TYPE_TIMESTAMP: case DQ_TYPE_FLOAT: case DQ_TYPE_DOUBLE: return true;
+            default: return false;
+        }
+    };
+    auto emit = [&](int b) {
+        if (out.nb >= kPredBCode) return false;
+        out.b[out.nb++] = (int8_t)b;
+        return true;
+    };
+    auto term = [&](int col, int op, int k) -> int {  // k: constant index, or -1 for IS [NOT] NULL
+        if (out.nterms >= kPredTerms) return -1;
+        PredTerm& q = out.t[out.nterms];
+        q.col = col;
+        q.op = op;
+        if (k >= 0) {
+            const dq_const& c = pr.consts[k];
+            const int ty = columns[col].spark_type;
+            q.dbl = (ty == DQ_TYPE_FLOAT || ty == DQ_TYPE_DOUBLE || c.tag == DQ_V_DOUBLE) ? 1 : 0;
+            q.ci = c.i64;
+            q.cd = c.tag == DQ_V_DOUBLE ? c.f64 : (double)c.i64;
+        }
+        return out.nterms++;
+    };
+    auto flip = [](int op) {
+        switch (op) {
+            case DQ_P_LT: return (int)DQ_P_GT;
+            case DQ_P_LE: return (int)DQ_P_GE;
+            case DQ_P_GT: return (int)DQ_P_LT;
+            case DQ_P_GE: return (int)DQ_P_LE;
+            default: return op;
+        }
+    };
+    auto const_ok = [&](int k) {
+        if (k < 0 || k >= pr.n_consts) return false;
+        const int tag = pr.consts[k].tag;
+        return tag == DQ_V_BOOL || tag == DQ_V_LONG || tag == DQ_V_DOUBLE;
+    };
+    for (int pc = 0; pc + 1 < pr.code_len; pc += 2) {
+        const int op = pr.code[pc], arg = pr.code[pc + 1];
+        switch (op) {
+            case DQ_P_COL:
+                if (!fixed_numeric(arg)) return false;
+                st.push_back({E_COL, arg});
+                break;
+            case DQ_P_CONST:
+                if (!const_ok(arg)) return false;
+                st.push_back({E_CONST, arg});
+                break;
+            case DQ_P_EQ: case DQ_P_NE: case DQ_P_LT: case DQ_P_LE: case DQ_P_GT: case DQ_P_GE: {
+                if (st.size() < 2) return false;
+                const Ent b = st.back(); st.pop_back();
+                const Ent a = st.back(); st.pop_back();
+                int k;
+                if (a.kind == E_COL && b.kind == E_CONST) k = term(a.idx, op, b.idx);
+                else if (a.kind == E_CONST && b.kind == E_COL) k = term(b.idx, flip(op), a.idx);
+                else return false;
+                if (k < 0 || !emit(k)) return false;
+                st.push_back({E_BOOL, 0});
+                break;
+            }
+            case DQ_P_IS_NULL: case DQ_P_IS_NOT_NULL: {
+                if (st.empty() || st.back().kind != E_COL) return false;
+                const int k = term(st.back().idx, op, -1);
+                st.pop_back();
+                if (k < 0 || !emit(k)) return false;
+                st.push_back({E_BOOL, 0});
+                break;
+            }
+            case DQ_P_AND: case DQ_P_OR: {
+                if (st.size() < 2 || st[st.size() - 1].kind != E_BOOL || st[st.size() - 2].kind != E_BOOL) return false;
+                st.pop_back();
+                if (!emit(op == DQ_P_AND ? kPB_AND : kPB_OR)) return false;
+                break;
+            }
+            case DQ_P_NOT:
+                if (st.empty() || st.back().kind != E_BOOL || !emit(kPB_NOT)) return false;
+                break;
+            case DQ_P_IN: {  // x IN (c1..cn) with non-NULL constants == (x = c1) OR ... OR (x = cn)
+                const int n = arg;
+                if (n < 1 || (int)st.size() < n + 1) return false;
+                const size_t base = st.size() - n - 1;
+                if (st[base].kind != E_COL) return false;
+                for (int i = 0; i < n; ++i) {
+                    if (st[base + 1 + i].kind != E_CONST) return false;
+                    const int k = term(st[base].idx, DQ_P_EQ, st[base + 1 + i].idx);
+                    if (k < 0 || !emit(k)) return false;
+                    if (i > 0 && !emit(kPB_OR)) return false;
+                }
+                st.resize(base);
+                st.push_back({E_BOOL, 0});
+                break;
+            }
+            default:
+                return false;
+        }
+        if (st.size() > 24) return false;
+    }
+    return st.size() == 1 && st[0].kind == E_BOOL && out.nterms > 0;
 }
 
 int ensure_side_streams(dq_ctx* ctx) {
@@ -886,6 +1002,8 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                     launch_regex(pc[pr.code[1]], (const int32_t*)((const uint8_t*)pstr[p] + k.str_offset), nrows, pwords,
                                  pt[p], pn[p], rx_status + p, ctx->stream);
                     any_regex = true;
+                } else if (PredSimple ps; !pred_vm_forced() && compile_simple_predicate(pr, columns, ncols, ps)) {
+                    launch_pred_simple(ps, (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p], ctx->stream);
                 } else {
                     launch_predicate((const PredProgram*)pprog[p], (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p],
                                      ctx->stream);

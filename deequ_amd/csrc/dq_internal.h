@@ -163,6 +163,28 @@ struct PredProgram {
     int32_t n_consts;
 };
 
+// A predicate that is a boolean combination (AND / OR / NOT) of leaves `column <op> constant` and `column IS [NOT]
+// NULL` over fixed-width numeric columns (IN lists of constants become OR chains of `=`): each leaf is evaluated into
+// a (TRUE, NOT-NULL) bit pair per row and the combination runs on a per-lane bit stack, all in registers
+// (pred_simple_kernel). Everything else runs on the general VM (predicate_kernel).
+constexpr int kPredTerms = 16;
+constexpr int kPredBCode = 64;
+constexpr int8_t kPB_AND = -1, kPB_OR = -2, kPB_NOT = -3;
+struct PredTerm {
+    int32_t col;
+    int32_t op;   // DQ_P_EQ..DQ_P_GE, DQ_P_IS_NULL, DQ_P_IS_NOT_NULL
+    int32_t dbl;  // compare as double (Spark NaN ordering) instead of as long
+    int32_t pad;
+    int64_t ci;
+    double cd;
+};
+struct PredSimple {
+    int32_t nterms;
+    int32_t nb;
+    PredTerm t[kPredTerms];
+    int8_t b[kPredBCode];  // postfix: >= 0 pushes term b[i]; kPB_AND / kPB_OR / kPB_NOT
+};
+
 inline int elem_of(int32_t spark_type) {
     switch (spark_type) {
         case DQ_TYPE_BOOLEAN: return ET_U8;
@@ -278,6 +300,8 @@ void launch_reduce_hll(const uint8_t* hll_partials, const int32_t* nblocks_of, i
                        uint8_t* hll_final, hipStream_t s);
 void launch_finalize(const OpMap* ops, int nops, const SlotPartial* finals, const uint8_t* hll_final,
                      dq_state* out, hipStream_t s);
+void launch_pred_simple(const PredSimple& prog, const PredColumn* cols_dev, int64_t nrows, int64_t padded_words,
+                        uint64_t* out_t, uint64_t* out_nn, hipStream_t s);
 void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
                       int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s);
 int string_scan_grid(int cus, int64_t nrows);

@@ -468,6 +468,199 @@ predicate_kernel(const PredProgram* __restrict__ progp, const PredColumn* __rest
     }
 }
 
+// ---- simple predicates (PredSimple): leaves into bit pairs, the boolean postfix on a per-lane bit stack --------------
+namespace {
+
+__device__ __forceinline__ double load_as_double(const PredColumn& c, int64_t row) {
+    switch (c.spark_type) {
+        case DQ_TYPE_BOOLEAN: return static_cast<const uint8_t*>(c.values)[row] != 0 ? 1.0 : 0.0;
+        case DQ_TYPE_BYTE: return (double)static_cast<const int8_t*>(c.values)[row];
+        case DQ_TYPE_SHORT: return (double)static_cast<const int16_t*>(c.values)[row];
+        case DQ_TYPE_INT: case DQ_TYPE_DATE: return (double)static_cast<const int32_t*>(c.values)[row];
+        case DQ_TYPE_FLOAT: return (double)static_cast<const float*>(c.values)[row];
+        case DQ_TYPE_DOUBLE: return static_cast<const double*>(c.values)[row];
+        default: return (double)static_cast<const int64_t*>(c.values)[row];  // LONG / TIMESTAMP
+    }
+}
+__device__ __forceinline__ int64_t load_as_long(const PredColumn& c, int64_t row) {
+    switch (c.spark_type) {
+        case DQ_TYPE_BOOLEAN: return static_cast<const uint8_t*>(c.values)[row] != 0 ? 1 : 0;
+        case DQ_TYPE_BYTE: return static_cast<const int8_t*>(c.values)[row];
+        case DQ_TYPE_SHORT: return static_cast<const int16_t*>(c.values)[row];
+        case DQ_TYPE_INT: case DQ_TYPE_DATE: return static_cast<const int32_t*>(c.values)[row];
+        default: return static_cast<const int64_t*>(c.values)[row];  // LONG / TIMESTAMP
+    }
+}
+
+}  // namespace
+
+// One wave evaluates kPredRows x 64 rows: lane L takes rows base + 64 j + L (j < kPredRows), so ballot j is bitmap
+// word j of the wave and each term issues kPredRows coalesced loads before it compares (latency hidden by the batch).
+constexpr int kPredRows = 8;
+
+template <typename T>
+__device__ __forceinline__ void load_rows(const void* values, int64_t row0, int64_t nrows, T (&x)[kPredRows]) {
+    const T* v = static_cast<const T*>(values);
+#pragma unroll
+    for (int j = 0; j < kPredRows; ++j) {
+        const int64_t r = row0 + 64 * j;
+        x[j] = r < nrows ? v[r] : T(0);
+    }
+}
+
+__device__ __forceinline__ void term_rows(const PredTerm& q, const PredColumn& c, int64_t row0, int64_t nrows,
+                                          uint32_t k, uint32_t (&tb)[kPredRows], uint32_t (&nb)[kPredRows]) {
+    bool valid[kPredRows];
+#pragma unroll
+    for (int j = 0; j < kPredRows; ++j) {
+        const int64_t r = row0 + 64 * j;
+        valid[j] = r < nrows &&
+                   (!c.validity || ((reinterpret_cast<const uint8_t*>(c.validity)[r >> 3] >> (r & 7)) & 1));
+    }
+    if (q.op == DQ_P_IS_NULL || q.op == DQ_P_IS_NOT_NULL) {
+#pragma unroll
+        for (int j = 0; j < kPredRows; ++j) {
+            const bool in = row0 + 64 * j < nrows;
+            tb[j] |= (uint32_t)(in && ((q.op == DQ_P_IS_NULL) != valid[j])) << k;
+            nb[j] |= (uint32_t)in << k;
+        }
+        return;
+    }
+    int c3[kPredRows];
+    if (q.dbl) {
+        double x[kPredRows];
+        switch (c.spark_type) {  // wave-uniform
+            case DQ_TYPE_DOUBLE: load_rows(c.values, row0, nrows, x); break;
+            case DQ_TYPE_LONG: case DQ_TYPE_TIMESTAMP: {
+                int64_t y[kPredRows];
+                load_rows(c.values, row0, nrows, y);
+#pragma unroll
+                for (int j = 0; j < kPredRows; ++j) x[j] = (double)y[j];
+                break;
+            }
+            case DQ_TYPE_FLOAT: {
+                float f[kPredRows];
+                load_rows(c.values, row0, nrows, f);
+#pragma unroll
+                for (int j = 0; j < kPredRows; ++j) x[j] = (double)f[j];
+                break;
+            }
+            default: {
+#pragma unroll
+                for (int j = 0; j < kPredRows; ++j) x[j] = 0.0;
+                for (int j = 0; j < kPredRows; ++j)
+                    if (row0 + 64 * j < nrows) x[j] = load_as_double(c, row0 + 64 * j);
+                break;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kPredRows; ++j) c3[j] = cmp_double(x[j], q.cd);
+    } else {
+        int64_t x[kPredRows];
+        switch (c.spark_type) {  // wave-uniform
+            case DQ_TYPE_LONG: case DQ_TYPE_TIMESTAMP: load_rows(c.values, row0, nrows, x); break;
+            case DQ_TYPE_INT: case DQ_TYPE_DATE: {
+                int32_t y[kPredRows];
+                load_rows(c.values, row0, nrows, y);
+#pragma unroll
+                for (int j = 0; j < kPredRows; ++j) x[j] = y[j];
+                break;
+            }
+            default: {
+#pragma unroll
+                for (int j = 0; j < kPredRows; ++j) x[j] = 0;
+                for (int j = 0; j < kPredRows; ++j)
+                    if (row0 + 64 * j < nrows) x[j] = load_as_long(c, row0 + 64 * j);
+                break;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kPredRows; ++j) c3[j] = x[j] < q.ci ? -1 : (x[j] > q.ci ? 1 : 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kPredRows; ++j) {
+        bool r;
+        switch (q.op) {
+            case DQ_P_EQ: r = c3[j] == 0; break;
+            case DQ_P_NE: r = c3[j] != 0; break;
+            case DQ_P_LT: r = c3[j] < 0; break;
+            case DQ_P_LE: r = c3[j] <= 0; break;
+            case DQ_P_GT: r = c3[j] > 0; break;
+            default: r = c3[j] >= 0; break;
+        }
+        tb[j] |= (uint32_t)(valid[j] && r) << k;
+        nb[j] |= (uint32_t)valid[j] << k;
+    }
+}
+
+__global__ void __launch_bounds__(256)
+pred_simple_kernel(const PredSimple P, const PredColumn* __restrict__ cols, int64_t nrows, int64_t padded_words,
+                   uint64_t* __restrict__ out_t, uint64_t* __restrict__ out_nn) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kPredRows;  // first word
+    const int64_t row0 = w0 * 64 + lane;
+    uint32_t tb[kPredRows], nb[kPredRows];
+#pragma unroll
+    for (int j = 0; j < kPredRows; ++j) tb[j] = nb[j] = 0;
+    for (int k = 0; k < P.nterms; ++k) term_rows(P.t[k], cols[P.t[k].col], row0, nrows, (uint32_t)k, tb, nb);
+    // SQL three-valued AND / OR / NOT on a per-row bit stack; a TRUE bit always has its NOT-NULL bit
+    uint32_t st[kPredRows], sn[kPredRows];
+#pragma unroll
+    for (int j = 0; j < kPredRows; ++j) st[j] = sn[j] = 0;
+    int sp = 0;
+    for (int i = 0; i < P.nb; ++i) {  // wave-uniform
+        const int o = P.b[i];
+        if (o >= 0) {
+#pragma unroll
+            for (int j = 0; j < kPredRows; ++j) {
+                st[j] |= ((tb[j] >> o) & 1u) << sp;
+                sn[j] |= ((nb[j] >> o) & 1u) << sp;
+            }
+            ++sp;
+        } else if (o == kPB_NOT) {
+            const uint32_t m = 1u << (sp - 1);
+#pragma unroll
+            for (int j = 0; j < kPredRows; ++j) st[j] ^= sn[j] & m;
+        } else {
+            const uint32_t keep = (1u << (sp - 2)) - 1u;
+#pragma unroll
+            for (int j = 0; j < kPredRows; ++j) {
+                const uint32_t ta = (st[j] >> (sp - 2)) & 1u, na = (sn[j] >> (sp - 2)) & 1u;
+                const uint32_t tc = (st[j] >> (sp - 1)) & 1u, nc = (sn[j] >> (sp - 1)) & 1u;
+                uint32_t rt, rn;
+                if (o == kPB_AND) {
+                    const uint32_t af = na & (ta ^ 1u), cf = nc & (tc ^ 1u);
+                    rn = af | cf | (na & nc);
+                    rt = (af | cf) ? 0u : (na & nc);
+                } else {
+                    rt = ta | tc;
+                    rn = rt | (na & nc);
+                }
+                st[j] = (st[j] & keep) | (rt << (sp - 2));
+                sn[j] = (sn[j] & keep) | (rn << (sp - 2));
+            }
+            --sp;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kPredRows; ++j) {
+        const uint64_t bt = __ballot(st[j] & 1u);
+        const uint64_t bn = __ballot(sn[j] & 1u);
+        if (lane == 0 && w0 + j < padded_words) {
+            out_t[w0 + j] = bt;
+            out_nn[w0 + j] = bn;
+        }
+    }
+}
+
+void launch_pred_simple(const PredSimple& prog, const PredColumn* cols_dev, int64_t nrows, int64_t padded_words,
+                        uint64_t* out_t, uint64_t* out_nn, hipStream_t s) {
+    const int64_t words_per_block = 4 * kPredRows;  // 4 waves
+    const int64_t blocks = (padded_words + words_per_block - 1) / words_per_block;
+    hipLaunchKernelGGL(pred_simple_kernel, dim3((unsigned)blocks), dim3(256), 0, s, prog, cols_dev, nrows,
+                       padded_words, out_t, out_nn);
+}
+
 void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
                       int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s) {
     const int64_t rows = padded_words * 64;
