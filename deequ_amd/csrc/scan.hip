@@ -262,10 +262,39 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, in
 }
 
 // Bits of a padded bitmap (predicate outputs: always readable up to the tile end).
-template <int P>
+// SCALAR: a wave's rows of load j span P consecutive bitmap words at a wave-uniform address, read by scalar loads
+// (read-only, constant address space) instead of 64-lane vector loads of mostly the same word; each lane then picks
+// its word and bits. Used for the `where` bitmaps: with where + validity both on vector loads the where scan ran at
+// 8.0 vs 5.25 ms per int64 launch, with both scalar C2 (validity only) lost 0.6 ms (profiles/r02/where_bits_r02bt.log).
+template <int P, bool SCALAR = false>
 __device__ __forceinline__ uint32_t bits_padded(const uint64_t* __restrict__ bm, int64_t tile, int tid) {
     constexpr int L = 8 / P;
     constexpr uint32_t pm = (1u << P) - 1u;
+    if constexpr (SCALAR) {
+    typedef const __attribute__((address_space(4))) uint64_t* cptr;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const cptr base = (cptr)(bm + (tile >> 6)) + wv * P;
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        const cptr q = base + j * (kBlock * P / 64);
+        // readfirstlane keeps the words uniform: without it the select below folds into one divergent-address load
+        auto uword = [&](int i) {
+            const uint64_t v = q[i];
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+        };
+        uint64_t word = uword(0);
+#pragma unroll
+        for (int i = 1; i < P; ++i) {
+            const uint64_t wi = uword(i);
+            word = ((lane * P) >> 6) == i ? wi : word;
+        }
+        m |= (uint32_t)((word >> ((lane * P) & 63)) & pm) << (j * P);
+    }
+    return m;
+    }
     const __amdgpu_buffer_rsrc_t r = tile_rsrc(bm, tile >> 3, kTileRows / 8);
     uint32_t m = 0;
 #pragma unroll
@@ -919,9 +948,9 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
             uint32_t mx = bits_valid<P>(c0.validity, tb, tid, full, nrows);
             uint32_t my = NC > 1 ? bits_valid<P>(c1.validity, tb, tid, full, nrows) : 0u;
             if (has_where) {
-                const uint32_t w = bits_padded<P>(sd.where_t, tb, tid);
+                const uint32_t w = bits_padded<P, true>(sd.where_t, tb, tid);
                 wt += __popc(w);
-                wnn += __popc(bits_padded<P>(sd.where_nn, tb, tid));
+                wnn += __popc(bits_padded<P, true>(sd.where_nn, tb, tid));
                 mx &= w;
                 my &= w;
             }
@@ -966,9 +995,9 @@ scan_values_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                 uint32_t mx = bits_valid<P>(c0.validity, tb, tid, true, nrows);
                 uint32_t my = bits_valid<P>(c1.validity, tb, tid, true, nrows);
                 if (has_where) {
-                    const uint32_t w = bits_padded<P>(sd.where_t, tb, tid);
+                    const uint32_t w = bits_padded<P, true>(sd.where_t, tb, tid);
                     wt += __popc(w);
-                    wnn += __popc(bits_padded<P>(sd.where_nn, tb, tid));
+                    wnn += __popc(bits_padded<P, true>(sd.where_nn, tb, tid));
                     mx &= w;
                     my &= w;
                 }
