@@ -413,7 +413,11 @@ class DataType(ScanShareableAnalyzer):
 class PatternMatch(StandardScanShareableAnalyzer):
     """A/PatternMatch.scala:37-55: sum(when(regexp_extract(col, pattern, 0) != "", 1).otherwise(0))
     under `where`, plus conditionalCount. The pattern runs on the GPU's backtracking regex engine
-    (deequ_amd/regex.py, csrc/regex.hip); a NULL value counts 0."""
+    (deequ_amd/regex.py, csrc/regex.hip); a NULL value counts 0.
+
+    FLOAT / DOUBLE values are matched against the shortest round-trip digits laid out as Java's toString
+    (csrc/java_dtoa.h). JDK 8's FloatingDecimal is not always shortest (JDK-4511638: some values print with
+    more digits than needed): for such values the match count is parity unpinned against a Java 8 Spark."""
     _fields = ("column", "pattern_", "where")
     name = "PatternMatch"
 
@@ -625,8 +629,8 @@ class FrequenciesAndNumRows:
             rows = self.numRows + other.numRows
             if isinstance(a, engine.PairFrequencies) and isinstance(b, engine.PairFrequencies):
                 keys, inv = np.unique(np.concatenate([a.keys, b.keys]), return_inverse=True)
-                counts = np.bincount(inv, weights=np.concatenate([a.counts, b.counts]).astype(np.float64),
-                                     minlength=len(keys)).astype(np.int64)
+                counts = np.zeros(len(keys), dtype=np.int64)  # Long counts: exact beyond 2^53
+                np.add.at(counts, inv, np.concatenate([a.counts, b.counts]))
                 return FrequenciesAndNumRows(engine.PairFrequencies(a.key_type, keys, counts, rows,
                                                                     a.null_count + b.null_count, a.decimal_scale,
                                                                     a.names), rows, self.columns)

@@ -44,6 +44,26 @@ def fold_states(raw, world, nops):
     return N.fold_states(raw, world, nops)
 
 
+def _signed64(c):
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+_MIX_C1, _MIX_C2 = _signed64(0xBF58476D1CE4E5B9), _signed64(0x94D049BB133111EB)
+
+
+def owner_ranks(torch, keys, world):
+    """Owner rank of each canonical 64-bit key (int64 tensor): (mix64(key) >> 32) % world, the splitmix64 finalizer
+    of freq.hip / groups.py on wrapping int64 arithmetic (logical shifts masked out of torch's arithmetic ones).
+    Raw canonical bits would not do: integer-valued DOUBLE keys have all-zero low bits and FLOAT keys zero high
+    bits, which would send every such group to one rank."""
+    z = keys ^ ((keys >> 30) & 0x3FFFFFFFF)
+    z = z * _MIX_C1
+    z = z ^ ((z >> 27) & 0x1FFFFFFFFF)
+    z = z * _MIX_C2
+    z = z ^ ((z >> 31) & 0x1FFFFFFFF)
+    return torch.remainder((z >> 32) & 0xFFFFFFFF, world)
+
+
 def kahan_fold(values):
     s, c = 0.0, 0.0
     for v in values:
@@ -440,8 +460,7 @@ class DistributedAnalysisRunner:
         keys, counts, rows, nulls = local
 
         def route():
-            mixed = keys ^ (keys >> 33)  # canonical keys of any fixed-width type spread over the owners
-            owner = torch.remainder(mixed & 0x7FFFFFFFFFFF, world)
+            owner = owner_ranks(torch, keys, world)
             order = torch.sort(owner, stable=True).indices
             return keys[order], counts[order], torch.bincount(owner, minlength=world)
         k_sorted, c_sorted, send = self._local_step(route)

@@ -55,21 +55,42 @@ def _powers(base, n):
     return p
 
 
-def string_hashes(values, offsets):
-    """Per string of a (UTF-8 bytes, int32 offsets) column: a 64-bit hash of its bytes and length."""
-    values = np.asarray(values, dtype=np.uint8)
-    offsets = np.asarray(offsets, dtype=np.int64)
-    total = int(offsets[-1]) if len(offsets) else 0
-    start, end = offsets[:-1], offsets[1:]
+def _string_hashes_span(values, start, end):
+    """string_hashes over strings [start_i, end_i) that all lie in `values` (one bounded slice)."""
+    total = len(values)
     with np.errstate(over="ignore"):
         pw = _powers(_P, total)
         pref = np.zeros(total + 1, dtype=np.uint64)
         if total:
-            pref[1:] = np.cumsum(values[:total].astype(np.uint64) * pw[:total], dtype=np.uint64)
+            pref[1:] = np.cumsum(values.astype(np.uint64) * pw[:total], dtype=np.uint64)
         inv = _powers(_P_INV, total)
         h = (pref[end] - pref[start]) * inv[start]
         h = h + (end - start).astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F)
     return mix64(h)
+
+
+_HASH_SLICE_BYTES = 1 << 24
+
+
+def string_hashes(values, offsets, slice_bytes=None):
+    """Per string of a (UTF-8 bytes, int32 offsets) column: a 64-bit hash of its bytes and length. The polynomial
+    prefix sums run over row slices of about `slice_bytes` bytes (the hash of a string does not depend on where it
+    sits), so host memory stays ~24 B per byte of one slice rather than of the whole column."""
+    values = np.asarray(values, dtype=np.uint8)
+    offsets = np.asarray(offsets, dtype=np.int64)
+    n = max(len(offsets) - 1, 0)
+    out = np.empty(n, dtype=np.uint64)
+    budget = max(1, int(slice_bytes or _HASH_SLICE_BYTES))
+    r = 0
+    while r < n:
+        base = int(offsets[r])
+        # last row whose end stays within the budget (at least one row per slice)
+        e = int(np.searchsorted(offsets, base + budget, side="right")) - 1
+        e = min(max(e, r + 1), n)
+        lo, hi = offsets[r:e] - base, offsets[r + 1:e + 1] - base
+        out[r:e] = _string_hashes_span(values[base:int(offsets[e])], lo, hi)
+        r = e
+    return out
 
 
 def column_hashes(col, null_is_value=False):

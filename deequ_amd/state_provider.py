@@ -269,6 +269,9 @@ def _pairs_table(state):
         vals = pa.array((keys.view(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.float32))
     elif t == N.TYPE_BOOLEAN:
         vals = pa.array(keys != 0)
+    elif t == N.TYPE_DATE:
+        # Arrow casts int32 -> date32, not int64 -> date32 (canonical keys are sign-extended int32 days)
+        vals = pa.array(keys.astype(np.int32), type=pa.int32()).cast(pa.date32())
     else:
         vals = pa.array(keys).cast(_arrow_of(t))
     counts = np.asarray(counts, dtype=np.int64)

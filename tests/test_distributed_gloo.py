@@ -457,6 +457,40 @@ def test_group_block_pack_roundtrip_and_owner_hash():
     assert sub.keys() == blk.keys()
 
 
+def test_string_hashes_do_not_depend_on_the_slice_size():
+    """groups.string_hashes runs its prefix sums over bounded byte slices (host memory ~24 B per key
+    byte of the whole block otherwise); every slice size gives the same hashes, empty strings included."""
+    from deequ_amd import groups as G
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 50, 3000)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    vals = rng.integers(0, 256, int(offs[-1])).astype(np.uint8)
+    ref = G.string_hashes(vals, offs, slice_bytes=1 << 30)
+    for sb in (1, 7, 64, 4096):
+        assert np.array_equal(G.string_hashes(vals, offs, slice_bytes=sb), ref)
+    same = G.string_hashes(np.frombuffer(b"abcabc", np.uint8), np.array([0, 3, 6], np.int32), slice_bytes=2)
+    assert same[0] == same[1]
+
+
+def test_pair_exchange_owner_balance_for_integer_valued_float_keys():
+    """The device pair path routes canonical keys by (mix64(key) >> 32) % world: integer-valued DOUBLE
+    keys (all-zero low bits) and FLOAT keys (zero high bits) spread over every rank like any other keys, and the
+    owner equals the host group exchange's mix64 routing."""
+    from deequ_amd import engine, groups as G
+    from deequ_amd.distributed import owner_ranks
+    for spark_type, vals in ((N.TYPE_DOUBLE, np.arange(-20000, 20000, dtype=np.float64)),
+                             (N.TYPE_FLOAT, np.arange(0, 40000, dtype=np.float32)),
+                             (N.TYPE_DOUBLE, np.arange(1, 40001) * 0.5),
+                             (N.TYPE_LONG, np.arange(40000, dtype=np.int64) << 40)):
+        keys = engine.canonical_keys(spark_type, vals)
+        for world in (2, 4, 8):
+            own = owner_ranks(torch, torch.from_numpy(keys.copy()), world).numpy()
+            ref = (G.mix64(keys.view(np.uint64)) >> np.uint64(32)) % np.uint64(world)
+            assert np.array_equal(own, ref.astype(np.int64))
+            share = np.bincount(own, minlength=world) / len(keys)
+            assert share.min() > 0.8 / world and share.max() < 1.2 / world, (spark_type, world, share)
+
+
 def _profile_worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

@@ -164,6 +164,24 @@ def test_float_grouping_keys_merge_bitwise_across_persisted_states(tmp_path):
     assert d[(GroupFloat(nan),)] == 3 and d[(GroupFloat(-0.0),)] == 1 and d[(GroupFloat(0.0),)] == 1
 
 
+def test_date_keyed_frequency_state_round_trip(tmp_path):
+    """A single DATE key persisted from its canonical (key, count) arrays (Arrow has no int64 -> date32
+    cast) and read back as pairs, NULL group included."""
+    import numpy as np
+    import deequ_amd.native as N
+    from deequ_amd import engine
+    days = np.array([-3, 0, 18000, 2 ** 31 - 1], dtype=np.int64)
+    pf = engine.PairFrequencies(N.TYPE_DATE, engine.canonical_keys(N.TYPE_DATE, days), [1, 2, 3, 4], 12, 2, 0, ["d"])
+    state = FrequenciesAndNumRows(pf, 12, ["d"])
+    provider = D.HdfsStateProvider(None, str(tmp_path / "dt"))
+    u = D.CountDistinct(["d"])
+    provider.persist(u, state)
+    back = provider.load(u).frequencies
+    assert isinstance(back, engine.PairFrequencies) and back.key_type == N.TYPE_DATE
+    got = sorted(zip(back.keys.tolist(), back.counts.tolist()))
+    assert got == sorted(zip(days.tolist(), [1, 2, 3, 4])) and back.null_count == 2 and back.num_rows == 12
+
+
 def test_histogram_identity_and_tostring():
     """case class Histogram(column, binningUdf, maxDetailBins): the UDF takes part in equality and toString
     (the HdfsStateProvider file id hashes that string); Scala renders Double fields with Double.toString."""
