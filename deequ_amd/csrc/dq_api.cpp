@@ -171,6 +171,13 @@ bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, 
     return st.size() == 1 && st[0].kind == E_BOOL && out.nterms > 0;
 }
 
+// Which kernel a launch group runs (mirrors values_kernel_for in scan.hip).
+int scan_kernel_family(int kind, int P, int nc, int heavy) {
+    if (kind == SK_BITS) return DQ_KERNEL_BITS;
+    if ((heavy || nc == 2) && P == 2) return heavy == 2 ? DQ_KERNEL_HEAVY8_FULL : DQ_KERNEL_HEAVY8;
+    return heavy ? DQ_KERNEL_STRIPED_HEAVY : DQ_KERNEL_STRIPED;
+}
+
 int ensure_side_streams(dq_ctx* ctx) {
     if (ctx->fork_ev) return DQ_OK;
     for (int i = 0; i < dq_ctx::kSide; ++i) {
@@ -411,6 +418,13 @@ int dq_synchronize(dq_ctx* ctx) {
 }
 
 int64_t dq_scan_launch_count(const dq_ctx* ctx) { return ctx ? ctx->scan_launches : -1; }
+
+int64_t dq_scan_kernel_launches(const dq_ctx* ctx, int32_t kernel) {
+    if (!ctx || kernel < 0 || kernel >= DQ_KERNEL_COUNT) return -1;
+    int64_t n = ctx->kernel_launches[kernel];
+    for (const dq_ctx* sub : ctx->subs) n += sub->kernel_launches[kernel];
+    return n;
+}
 
 int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const dq_op* ops, int nops,
             const dq_predicate* preds, int npreds, dq_state* out, uint32_t flags) {
@@ -1001,12 +1015,15 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                     const dq_const& k = pr.consts[pr.code[3]];
                     launch_regex(pc[pr.code[1]], (const int32_t*)((const uint8_t*)pstr[p] + k.str_offset), nrows, pwords,
                                  pt[p], pn[p], rx_status + p, ctx->stream);
+                    ctx->kernel_launches[DQ_KERNEL_REGEX]++;
                     any_regex = true;
                 } else if (PredSimple ps; !pred_vm_forced() && compile_simple_predicate(pr, columns, ncols, ps)) {
                     launch_pred_simple(ps, (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p], ctx->stream);
+                    ctx->kernel_launches[DQ_KERNEL_PRED_SIMPLE]++;
                 } else {
                     launch_predicate((const PredProgram*)pprog[p], (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p],
                                      ctx->stream);
+                    ctx->kernel_launches[DQ_KERNEL_PRED_VM]++;
                 }
                 DQ_HIP(ctx, hipGetLastError());
             }
@@ -1081,12 +1098,14 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                                       ntiles, gstride, g.grid, partials, hllp, launch_stream(li++)) != 0)
                     return fail(ctx, DQ_ERR_DEVICE, "scan launch failed for shape (%d,%d,%d)", g.kind, g.P, g.nc);
                 DQ_HIP(ctx, hipGetLastError());
+                ctx->kernel_launches[scan_kernel_family(g.kind, g.P, g.nc, g.heavy)]++;
                 off += g.slots.size();
             }
         }
         if (nsslots) {
             launch_string_scan(dsslots, nsslots, nrows, sgrid, gstride, spartials, hllp, launch_stream(li++));
             DQ_HIP(ctx, hipGetLastError());
+            ctx->kernel_launches[DQ_KERNEL_STRINGS]++;
         }
         for (int j = 0; j < used_side; ++j) {
             DQ_HIP(ctx, hipEventRecord(ctx->join_ev[j], ctx->side[j]));

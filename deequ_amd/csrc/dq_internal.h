@@ -243,6 +243,7 @@ struct dq_ctx {
     hipEvent_t join_ev[kSide] = {};
     std::map<int, int> occupancy;  // launch shape -> workgroups per CU
     int64_t scan_launches = 0;
+    int64_t kernel_launches[DQ_KERNEL_COUNT] = {};  // by dq_scan_kernel
     // Released device scratch of the grouping builds (multi-GB partition buffers and tables), re-used in stream
     // order instead of a hipMalloc / hipFree pair per call; bounded, freed at dq_close and on allocation failure.
     struct CachedBlock {

@@ -11,7 +11,8 @@
  *   - Every call returns 0 (DQ_OK) on success or a negative dq_status; dq_last_error(ctx) then
  *     holds a message. A failed dq_scan fails EVERY op of the batch, mirroring the catch-all in
  *     runScanningAnalyzers (R/AnalysisRunner.scala:320-323).
- *   - A dq_ctx is bound to one GPU and is not re-entrant; use one ctx per process/rank.
+ *   - A dq_ctx from dq_open is bound to one GPU; one from dq_open_devices spans several GPUs of the node. A ctx
+ *     is not re-entrant: one driver thread per ctx, one ctx per process/rank.
  *   - States are returned in native byte order (little-endian on x86/MI355X hosts) with the
  *     field order of the reference's HdfsStateProvider layouts (A/StateProvider.scala:187-262).
  *
@@ -244,6 +245,24 @@ int dq_scan_streamed(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t n
 /* Number of fused-scan kernel launches issued so far (the analogue of the SparkMonitor job count
  * asserted in T/analyzers/runners/AnalysisRunnerTests.scala:50-74). */
 int64_t dq_scan_launch_count(const dq_ctx* ctx);
+
+/* Kernel launches of the scan path by kernel (all devices of a multi-device context), so a test can prove which
+ * kernel shape evaluated its ops (tests/test_gpu_configs.py). */
+typedef enum dq_scan_kernel {
+    DQ_KERNEL_STRIPED = 0,        /* scan_values_kernel: count / sum / min / max / moments, striped 16-B loads     */
+    DQ_KERNEL_STRIPED_HEAVY = 1,  /* scan_values_kernel HEAVY: HLL / fused compare over 1-, 2-, 4-byte columns    */
+    DQ_KERNEL_HEAVY8 = 2,         /* scan_heavy8_kernel: 8-byte HLL / fused compare / Correlation pairs           */
+    DQ_KERNEL_HEAVY8_FULL = 3,    /* scan_heavy8_kernel with every flag on and no `where` (the north-star suite)  */
+    DQ_KERNEL_BITS = 4,           /* scan_bits_kernel: Size(where), unread Completeness, non-fused Compliance     */
+    DQ_KERNEL_PRED_SIMPLE = 5,    /* pred_simple_kernel: a simple predicate into TRUE / NOT-NULL bitmaps          */
+    DQ_KERNEL_PRED_VM = 6,        /* predicate_kernel: the general predicate VM                                   */
+    DQ_KERNEL_REGEX = 7,          /* regex_match_kernel (PatternMatch)                                            */
+    DQ_KERNEL_STRINGS = 8,        /* scan_strings_kernel                                                          */
+    DQ_KERNEL_WHERE_FUSED = 9,    /* a value scan that also evaluates a `where` and writes its masks              */
+    DQ_KERNEL_WHERE_MASKS = 10,   /* where_masks_kernel: a `where` into per-column masks (no fused producer)       */
+    DQ_KERNEL_COUNT = 11
+} dq_scan_kernel;
+int64_t dq_scan_kernel_launches(const dq_ctx* ctx, int32_t kernel);
 
 /* Semigroup merge of two states of the same op kind (State.sum, per analyzer file);
  * also used for the rank-ordered fold after the RCCL all-gather. */

@@ -436,6 +436,10 @@ typedef struct {
     int64_t n, nnan, isum, imin, imax, pred_true;
     double dmin, dmax;
     double ex_sum, ex_mean, ex_m2;
+    /* Spark's own arithmetic order: per partition a sequential Double sum and CentralMomentAgg update, the
+     * partitions' states merged in partition order (Sum: +, StandardDeviationState.sum). The deviation of these
+     * from ex_* is the reference's own error at this size. */
+    double sp_sum, sp_mean, sp_m2;
     uint8_t regs[512];
 } oracle_gen_col;
 
@@ -481,9 +485,70 @@ typedef struct {
 
 typedef struct { int64_t n; kbn sx, sy, sxx, syy, sxy; } corr_acc;
 
-int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0, int64_t nrows, int npairs,
-                           const int32_t* pairs, int threads, oracle_gen_col* out, oracle_gen_corr* corr_out) {
-    if (ncols <= 0 || ncols > 64 || nrows <= 0) return -1;
+/* A `where` filter or Compliance predicate over the generated columns: leaves `column <op> constant` combined by
+ * one AND or OR, in SQL three-valued logic (A/Analyzer.scala:409-432, A/Compliance.scala:49-52): a leaf over a NULL
+ * value is NULL; AND is FALSE if any leaf is FALSE, else NULL if any is NULL; OR is TRUE if any leaf is TRUE, else
+ * NULL if any is NULL. A DOUBLE column compares as double with Spark's NaN ordering (NaN = NaN, NaN above every
+ * number); a LONG column compares as long against a long constant (is_dbl = 0) or as double (is_dbl = 1). */
+typedef struct {
+    int32_t col, op, is_dbl, pad;   /* op: 0 <, 1 <=, 2 =, 3 !=, 4 >, 5 >= */
+    int64_t ci;
+    double cd;
+} oracle_gen_leaf;
+
+typedef struct {
+    int32_t nleaves;                /* 1..4 */
+    int32_t comb;                   /* 0 AND, 1 OR */
+    oracle_gen_leaf leaf[4];
+} oracle_gen_pred;
+
+/* -1 NULL, 0 FALSE, 1 TRUE */
+static int gen_leaf(const oracle_gen_leaf* l, const oracle_gen_spec* specs, const int* valid, const uint64_t* raw) {
+    if (!valid[l->col]) return -1;
+    int c;
+    if (specs[l->col].spark_type == T_DOUBLE || l->is_dbl) {
+        double x;
+        if (specs[l->col].spark_type == T_DOUBLE) memcpy(&x, &raw[l->col], 8);
+        else x = (double)(int64_t)raw[l->col];
+        const double y = l->cd;
+        c = nan_gt(x, y) ? 1 : (nan_gt(y, x) ? -1 : 0);
+    } else {
+        const int64_t x = (int64_t)raw[l->col];
+        c = x < l->ci ? -1 : (x > l->ci ? 1 : 0);
+    }
+    switch (l->op) {
+        case 0: return c < 0;
+        case 1: return c <= 0;
+        case 2: return c == 0;
+        case 3: return c != 0;
+        case 4: return c > 0;
+        default: return c >= 0;
+    }
+}
+
+static int gen_pred(const oracle_gen_pred* p, const oracle_gen_spec* specs, const int* valid, const uint64_t* raw) {
+    int any_null = 0;
+    for (int i = 0; i < p->nleaves; ++i) {
+        const int v = gen_leaf(&p->leaf[i], specs, valid, raw);
+        if (v < 0) any_null = 1;
+        else if (p->comb == 0 && v == 0) return 0;
+        else if (p->comb == 1 && v == 1) return 1;
+    }
+    return any_null ? -1 : (p->comb == 0 ? 1 : 0);
+}
+
+/* where: NULL = no filter. where_counts[0..1] = rows with `where` TRUE / NOT NULL (Size(where) and the presence rule
+ * of conditionalCount). Every column / pair aggregate runs over rows with `where` TRUE (conditionalSelection).
+ * pred_counts[2 i + 0..1] = rows with `where` TRUE and predicate i TRUE / NOT NULL (Compliance numerator and its
+ * presence). */
+int oracle_generated_suite_ex(int ncols, const oracle_gen_spec* specs, int64_t row0, int64_t nrows, int npairs,
+                              const int32_t* pairs, int threads, const oracle_gen_pred* where, int npreds,
+                              const oracle_gen_pred* preds, oracle_gen_col* out, oracle_gen_corr* corr_out,
+                              int64_t* where_counts, int64_t* pred_counts) {
+    if (ncols <= 0 || ncols > 64 || nrows <= 0 || npreds < 0 || npreds > 16) return -1;
+    if (where && (where->nleaves < 1 || where->nleaves > 4)) return -1;
+    for (int i = 0; i < npreds; ++i)
+        if (preds[i].nleaves < 1 || preds[i].nleaves > 4) return -1;
     long double shift[64];
     for (int c = 0; c < ncols; ++c) shift[c] = raw_value(specs[c].spark_type, synth_raw(specs[c].kind, specs[c].seed, (uint64_t)row0));
     gen_acc* acc = (gen_acc*)calloc((size_t)ncols, sizeof(gen_acc));
@@ -494,8 +559,14 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
         acc[c].imax = INT64_MIN;
         acc[c].first = 1;
     }
-    const int64_t chunk = 1 << 16;
-    const int64_t nchunks = (nrows + chunk - 1) / chunk;
+    int64_t wt = 0, wnn = 0, pc[32];
+    memset(pc, 0, sizeof(pc));
+    /* kSparkParts contiguous row partitions (Spark's partitioning of a range scan); each is walked in row order */
+    enum { kSparkParts = 64 };
+    const int64_t psize = (nrows + kSparkParts - 1) / kSparkParts;
+    typedef struct { double n, avg, m2, sum; } spark_acc;
+    spark_acc* sacc = (spark_acc*)calloc((size_t)kSparkParts * (size_t)ncols, sizeof(spark_acc));
+    if (!sacc) return -2;
     if (threads <= 0) threads = 1;
 #pragma omp parallel num_threads(threads)
     {
@@ -508,19 +579,44 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
         }
         double* x = (double*)malloc(sizeof(double) * (size_t)ncols);
         int* ok = (int*)malloc(sizeof(int) * (size_t)ncols);
-#pragma omp for schedule(dynamic, 4)
-        for (int64_t k = 0; k < nchunks; ++k) {
-            const int64_t lo = row0 + k * chunk;
-            int64_t hi = lo + chunk;
+        int* valid = (int*)malloc(sizeof(int) * (size_t)ncols);
+        uint64_t* raw = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)ncols);
+        int64_t lwt = 0, lwnn = 0, lpc[32];
+        memset(lpc, 0, sizeof(lpc));
+#pragma omp for schedule(dynamic, 1)
+        for (int64_t k = 0; k < kSparkParts; ++k) {
+            const int64_t lo = row0 + k * psize;
+            int64_t hi = lo + psize;
             if (hi > row0 + nrows) hi = row0 + nrows;
+            spark_acc* sa = sacc + k * ncols;
             for (int64_t r = lo; r < hi; ++r) {
                 for (int c = 0; c < ncols; ++c) {
                     const oracle_gen_spec* sp = &specs[c];
-                    ok[c] = sp->permille < 0 || (int)(oracle_splitmix64(sp->vseed, (uint64_t)r) % 1000ULL) >= sp->permille;
+                    valid[c] = sp->permille < 0 || (int)(oracle_splitmix64(sp->vseed, (uint64_t)r) % 1000ULL) >= sp->permille;
+                    raw[c] = synth_raw(sp->kind, sp->seed, (uint64_t)r);
+                }
+                int sel = 1;
+                if (where) {
+                    const int w = gen_pred(where, specs, valid, raw);
+                    sel = w == 1;
+                    lwt += w == 1;
+                    lwnn += w >= 0;
+                } else {
+                    ++lwt;
+                    ++lwnn;
+                }
+                if (!sel) continue;
+                for (int i = 0; i < npreds; ++i) {
+                    const int v = gen_pred(&preds[i], specs, valid, raw);
+                    lpc[2 * i] += v == 1;
+                    lpc[2 * i + 1] += v >= 0;
+                }
+                for (int c = 0; c < ncols; ++c) {
+                    const oracle_gen_spec* sp = &specs[c];
+                    ok[c] = valid[c];
                     if (!ok[c]) continue;
-                    const uint64_t raw = synth_raw(sp->kind, sp->seed, (uint64_t)r);
                     double v;
-                    memcpy(&v, &raw, 8);
+                    memcpy(&v, &raw[c], 8);
                     gen_acc* a = &la[c];
                     a->n++;
                     if (sp->spark_type == T_DOUBLE) {
@@ -529,10 +625,10 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
                         if (a->first || nan_gt(v, a->dmax)) a->dmax = v;
                         kbn_add(&a->sum, (long double)v);
                         if (sp->pred_gt0 && (v > 0.0 || v != v)) a->pred_true++;
-                        if (sp->hll) hll_add(a->regs, hash_long(v == v ? raw : 0x7ff8000000000000ULL));
+                        if (sp->hll) hll_add(a->regs, hash_long(v == v ? raw[c] : 0x7ff8000000000000ULL));
                         x[c] = v;
                     } else {
-                        const int64_t iv = (int64_t)raw;
+                        const int64_t iv = (int64_t)raw[c];
                         a->isum = (int64_t)((uint64_t)a->isum + (uint64_t)iv);
                         if (iv < a->imin) a->imin = iv;
                         if (iv > a->imax) a->imax = iv;
@@ -541,6 +637,14 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
                         x[c] = (double)iv;
                     }
                     a->first = 0;
+                    {   /* Spark order inside the partition: Sum, CentralMomentAgg.update (C/StatefulStdDevPop.scala) */
+                        spark_acc* q = &sa[c];
+                        if (sp->spark_type == T_DOUBLE) q->sum += x[c];
+                        const double n1 = q->n + 1.0, delta = x[c] - q->avg, deltaN = delta / n1;
+                        q->avg += deltaN;
+                        q->m2 += delta * (delta - deltaN);
+                        q->n = n1;
+                    }
                     const long double d = (long double)x[c] - shift[c];
                     kbn_add(&a->s1, d);
                     kbn_add(&a->s2, d * d);
@@ -562,6 +666,9 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
         }
 #pragma omp critical
         {
+            wt += lwt;
+            wnn += lwnn;
+            for (int i = 0; i < 2 * npreds; ++i) pc[i] += lpc[i];
             for (int c = 0; c < ncols; ++c) {
                 gen_acc* a = &acc[c];
                 const gen_acc* b = &la[c];
@@ -594,7 +701,14 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
         free(lc);
         free(x);
         free(ok);
+        free(valid);
+        free(raw);
     }
+    if (where_counts) {
+        where_counts[0] = wt;
+        where_counts[1] = wnn;
+    }
+    for (int i = 0; i < 2 * npreds && pred_counts; ++i) pred_counts[i] = pc[i];
     for (int c = 0; c < ncols; ++c) {
         const gen_acc* a = &acc[c];
         oracle_gen_col* o = &out[c];
@@ -608,6 +722,21 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
         o->dmin = a->n ? a->dmin : NAN;
         o->dmax = a->n ? a->dmax : NAN;
         memcpy(o->regs, a->regs, 512);
+        {   /* partitions merged in order: Double +, StandardDeviationState.sum (A/StandardDeviation.scala:37-44) */
+            double n = 0.0, avg = 0.0, m2 = 0.0, sum = 0.0;
+            for (int k = 0; k < kSparkParts; ++k) {
+                const spark_acc* q = &sacc[k * ncols + c];
+                sum += q->sum;
+                if (q->n == 0.0) continue;
+                const double nn = n + q->n, delta = q->avg - avg, deltaN = nn == 0.0 ? 0.0 : delta / nn;
+                m2 = m2 + q->m2 + delta * deltaN * n * q->n;
+                avg = avg + deltaN * q->n;
+                n = nn;
+            }
+            o->sp_sum = specs[c].spark_type == T_DOUBLE ? sum : (double)a->isum;
+            o->sp_mean = avg;
+            o->sp_m2 = m2;
+        }
         if (a->n > 0) {
             const long double k = shift[c];
             const long double n = (long double)a->n, s1 = kbn_val(&a->s1), s2 = kbn_val(&a->s2);
@@ -634,5 +763,12 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
     }
     free(acc);
     free(cacc);
+    free(sacc);
     return 0;
+}
+
+int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0, int64_t nrows, int npairs,
+                           const int32_t* pairs, int threads, oracle_gen_col* out, oracle_gen_corr* corr_out) {
+    return oracle_generated_suite_ex(ncols, specs, row0, nrows, npairs, pairs, threads, NULL, 0, NULL, out, corr_out,
+                                     NULL, NULL);
 }

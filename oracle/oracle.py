@@ -45,12 +45,22 @@ class OracleGenCol(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int64), ("nnan", ctypes.c_int64), ("isum", ctypes.c_int64), ("imin", ctypes.c_int64),
                 ("imax", ctypes.c_int64), ("pred_true", ctypes.c_int64), ("dmin", ctypes.c_double),
                 ("dmax", ctypes.c_double), ("ex_sum", ctypes.c_double), ("ex_mean", ctypes.c_double),
-                ("ex_m2", ctypes.c_double), ("regs", ctypes.c_uint8 * 512)]
+                ("ex_m2", ctypes.c_double), ("sp_sum", ctypes.c_double), ("sp_mean", ctypes.c_double),
+                ("sp_m2", ctypes.c_double), ("regs", ctypes.c_uint8 * 512)]
 
 
 class OracleGenCorr(ctypes.Structure):
     _fields_ = [("n", ctypes.c_double), ("x_avg", ctypes.c_double), ("y_avg", ctypes.c_double),
                 ("ck", ctypes.c_double), ("x_mk", ctypes.c_double), ("y_mk", ctypes.c_double)]
+
+
+class OracleGenLeaf(ctypes.Structure):
+    _fields_ = [("col", ctypes.c_int32), ("op", ctypes.c_int32), ("is_dbl", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("ci", ctypes.c_int64), ("cd", ctypes.c_double)]
+
+
+class OracleGenPred(ctypes.Structure):
+    _fields_ = [("nleaves", ctypes.c_int32), ("comb", ctypes.c_int32), ("leaf", OracleGenLeaf * 4)]
 
 
 _lib = None
@@ -88,6 +98,12 @@ def lib():
         L.oracle_generated_suite.argtypes = [ctypes.c_int, ctypes.POINTER(OracleGenSpec), ctypes.c_int64,
                                              ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                              ctypes.POINTER(OracleGenCol), ctypes.POINTER(OracleGenCorr)]
+        L.oracle_generated_suite_ex.restype = ctypes.c_int
+        L.oracle_generated_suite_ex.argtypes = [ctypes.c_int, ctypes.POINTER(OracleGenSpec), ctypes.c_int64,
+                                                ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                                ctypes.POINTER(OracleGenPred), ctypes.c_int,
+                                                ctypes.POINTER(OracleGenPred), ctypes.POINTER(OracleGenCol),
+                                                ctypes.POINTER(OracleGenCorr), ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -131,11 +147,33 @@ def synth_validity(seed, row0, n, permille):
     return m.astype(bool)
 
 
-def generated_suite(specs, row0, nrows, pairs=(), threads=None):
-    """Streamed oracle over generated columns (dq_oracle.c oracle_generated_suite): `specs` are dicts
+_GEN_OPS = {"<": 0, "<=": 1, "=": 2, "!=": 3, ">": 4, ">=": 5}
+
+
+def _gen_pred(specs, pred):
+    """(comb, [(column index, op, constant)...]) -> OracleGenPred. comb is "and" / "or"; a Python float constant
+    compares as double, an int as long (as double against a DOUBLE column)."""
+    comb, leaves = pred
+    if not 1 <= len(leaves) <= 4:
+        raise ValueError("1..4 leaves")
+    p = OracleGenPred()
+    p.nleaves = len(leaves)
+    p.comb = {"and": 0, "or": 1}[comb]
+    for i, (c, op, k) in enumerate(leaves):
+        is_dbl = isinstance(k, float) or specs[c]["spark_type"] == T_DOUBLE
+        p.leaf[i] = OracleGenLeaf(c, _GEN_OPS[op], int(is_dbl), 0, 0 if isinstance(k, float) else int(k), float(k))
+    return p
+
+
+def generated_suite(specs, row0, nrows, pairs=(), threads=None, where=None, preds=()):
+    """Streamed oracle over generated columns (dq_oracle.c oracle_generated_suite_ex): `specs` are dicts
     with kind, spark_type, seed, vseed, permille (< 0 = no nulls), hll, pred_gt0. Returns (per-column
     dicts, per-pair correlation dicts). Exact counts / Long sums / min / max / Compliance counts / HLL
-    registers; exact (compensated long double) sums, moments and co-moments."""
+    registers; exact (compensated long double) sums, moments and co-moments.
+
+    `where` (comb, leaves) filters every aggregate (conditionalSelection, A/Analyzer.scala:409-432); `preds` are
+    Compliance predicates counted over the where-TRUE rows. Given either, a third value is returned:
+    {"where_true", "where_nn", "preds": [(true, not_null), ...]}."""
     if threads is None:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count() or 1
         threads = max(1, min(threads, 16))
@@ -147,9 +185,15 @@ def generated_suite(specs, row0, nrows, pairs=(), threads=None):
     npairs = len(pairs)
     pa = np.array([c for p in pairs for c in p] or [0], dtype=np.int32)
     outp = (OracleGenCorr * max(npairs, 1))()
-    rc = lib().oracle_generated_suite(len(specs), arr, row0, nrows, npairs, pa.ctypes.data, threads, outc, outp)
+    wp = _gen_pred(specs, where) if where is not None else None
+    parr = (OracleGenPred * max(len(preds), 1))(*[_gen_pred(specs, p) for p in preds])
+    wc = np.zeros(2, dtype=np.int64)
+    pc = np.zeros(2 * max(len(preds), 1), dtype=np.int64)
+    rc = lib().oracle_generated_suite_ex(len(specs), arr, row0, nrows, npairs, pa.ctypes.data, threads,
+                                         ctypes.byref(wp) if wp is not None else None, len(preds), parr, outc, outp,
+                                         wc.ctypes.data, pc.ctypes.data)
     if rc != 0:
-        raise RuntimeError("oracle_generated_suite failed: %d" % rc)
+        raise RuntimeError("oracle_generated_suite_ex failed: %d" % rc)
     cols = []
     for o in outc:
         d = {f: getattr(o, f) for f, _ in OracleGenCol._fields_ if f != "regs"}
@@ -159,8 +203,11 @@ def generated_suite(specs, row0, nrows, pairs=(), threads=None):
         d["words"] = [int(w) for w in words]
         cols.append(d)
     corrs = [{f: getattr(outp[i], f) for f, _ in OracleGenCorr._fields_} for i in range(npairs)]
-    return cols, corrs
-
+    if where is None and not preds:
+        return cols, corrs
+    counts = {"where_true": int(wc[0]), "where_nn": int(wc[1]),
+              "preds": [(int(pc[2 * i]), int(pc[2 * i + 1])) for i in range(len(preds))]}
+    return cols, corrs, counts
 
 
 # ---- the oracle's own State algebra and metric formulas -----------------------------------------------

@@ -142,6 +142,124 @@ def test_c2_suite10_parity_at_scale():
         _check_corr(st[D.Correlation(names[x], names[y])], o, (names[x], names[y]))
 
 
+def c2_ops(names, where=None):
+    """BASELINE C2's 49 ops (bench.py c2_analyzers), optionally all under one `where`."""
+    out = [D.Size(where)]
+    for c in names:
+        out += [D.Completeness(c, where), D.Mean(c, where), D.Sum(c, where), D.Minimum(c, where),
+                D.Maximum(c, where), D.StandardDeviation(c, where)]
+    return out
+
+
+def _check_c2_column(st, name, sp, o, count, where=None):
+    """Bars of BASELINE.json north_star: bit-exact counts, Long sums, min / max and dyadic double sums; 1e-12 for the
+    other double sums and the moments (mean against max(|mean|, sigma))."""
+    dbl = sp["spark_type"] == N.TYPE_DOUBLE
+    exact_sum = sp["kind"] == 1 or not dbl
+    exp_sum = o["ex_sum"] if dbl else float(o["isum"])
+    comp = st[D.Completeness(name, where)]
+    assert (comp.numMatches, comp.count) == (o["n"], count), name
+    mean = st[D.Mean(name, where)]
+    assert mean.count == o["n"], name
+    assert (mean.sum_ == exp_sum) if exact_sum else _rel(mean.sum_, exp_sum), (name, mean.sum_, exp_sum)
+    s = st[D.Sum(name, where)].sum_
+    assert (s == exp_sum) if exact_sum else _rel(s, exp_sum), (name, s, exp_sum)
+    assert st[D.Minimum(name, where)].minValue == (o["dmin"] if dbl else float(o["imin"])), name
+    assert st[D.Maximum(name, where)].maxValue == (o["dmax"] if dbl else float(o["imax"])), name
+    sd = st[D.StandardDeviation(name, where)]
+    sigma = math.sqrt(o["ex_m2"] / o["n"])
+    assert sd.n == o["n"], name
+    assert _rel(sd.avg, o["ex_mean"], max(abs(o["ex_mean"]), sigma)), (name, sd.avg, o["ex_mean"])
+    assert _rel(sd.m2, o["ex_m2"]), (name, sd.m2, o["ex_m2"], (sd.m2 - o["ex_m2"]) / o["ex_m2"])
+    # the reference's own arithmetic order (64 sequential partitions merged in order) against the same exact value
+    return {"col": name, "gpu_m2_rel": (sd.m2 - o["ex_m2"]) / o["ex_m2"],
+            "spark_m2_rel": (o["sp_m2"] - o["ex_m2"]) / o["ex_m2"],
+            "gpu_mean_err": (sd.avg - o["ex_mean"]) / max(abs(o["ex_mean"]), sigma),
+            "spark_mean_err": (o["sp_mean"] - o["ex_mean"]) / max(abs(o["ex_mean"]), sigma),
+            "gpu_sum_rel": (s - exp_sum) / abs(exp_sum) if exp_sum else 0.0,
+            "spark_sum_rel": (o["sp_sum"] - exp_sum) / abs(exp_sum) if exp_sum else 0.0}
+
+
+def _launch_delta(before):
+    after = engine.ctx().kernel_launches()
+    return {k: after[k] - before[k] for k in after if after[k] != before[k]}
+
+
+def _report(tag, rows):
+    print("\n%s: relative error vs the exact oracle (GPU | Spark-order restatement)" % tag)
+    for r in rows:
+        print("  %-3s m2 %+.2e | %+.2e   mean %+.2e | %+.2e   sum %+.2e | %+.2e" % (
+            r["col"], r["gpu_m2_rel"], r["spark_m2_rel"], r["gpu_mean_err"], r["spark_mean_err"], r["gpu_sum_rel"],
+            r["spark_sum_rel"]))
+
+
+def test_c2_headline_shape_parity_at_scale():
+    """the exact 49-op C2 list bench.py times (no HLL / compare, so every column runs on the striped
+    scan_values_kernel: one launch for the 4 fp64 slots, one for the 4 int64 slots) over the 1e9-row generator, against
+    the exact streamed oracle; the launch counters prove which kernel evaluated it."""
+    specs = c2_specs()
+    names = [s["name"] for s in specs]
+    table = _device_table(specs, ROWS)
+    before = engine.ctx().kernel_launches()
+    st = _states(table, c2_ops(names))
+    assert _launch_delta(before) == {"striped": 2}
+    del table
+    cols, _ = O.generated_suite(specs, 0, ROWS)
+    assert st[D.Size()].numMatches == ROWS
+    _report("C2 %d rows" % ROWS, [_check_c2_column(st, sp["name"], sp, o, ROWS) for sp, o in zip(specs, cols)])
+
+
+WHERE_ROWS = int(float(os.environ.get("DQ_WHERE_ROWS", "2e8")))
+
+
+def test_c2_under_where_parity_at_scale():
+    """The C2 suite with every analyzer under `where c4 < 0` (conditionalSelection / conditionalCount,
+    A/Analyzer.scala:409-432; c4 is int64 with 1 % nulls, so the filter is NULL on those rows) against the oracle's
+    where-aware generated suite: Size(where) = rows with c4 < 0, every Completeness count the same, every aggregate over
+    the selected rows only."""
+    specs = c2_specs()
+    names = [s["name"] for s in specs]
+    w = "c4 < 0"
+    table = _device_table(specs, WHERE_ROWS)
+    before = engine.ctx().kernel_launches()
+    st = _states(table, c2_ops(names, w))
+    launches = _launch_delta(before)
+    del table
+    cols, _, cnt = O.generated_suite(specs, 0, WHERE_ROWS, where=("and", [(4, "<", 0)]))
+    print("\nlaunches:", launches)
+    assert st[D.Size(w)].numMatches == cnt["where_true"]
+    assert 0.45 * WHERE_ROWS < cnt["where_true"] < 0.55 * WHERE_ROWS
+    _report("C2 under %s, %d rows" % (w, WHERE_ROWS),
+            [_check_c2_column(st, sp["name"], sp, o, cnt["where_true"], w) for sp, o in zip(specs, cols)])
+
+
+def test_compound_compliance_parity_at_scale():
+    """Compliance("c4 < 0 OR c5 > 1") (A/Compliance.scala:37-53: sum(cast(pred AS int)), a NULL predicate counts 0;
+    SQL OR: TRUE if either side is TRUE, NULL if neither is TRUE and one is NULL) and the same under a compound
+    `where c0 > 0 AND c6 >= 0` with a Mean, at >= 1e8 rows against the oracle."""
+    specs = c2_specs()
+    table = _device_table(specs, WHERE_ROWS)
+    comp = D.Compliance("neg_or_big", "c4 < 0 OR c5 > 1")
+    w = "c0 > 0 AND c6 >= 0"
+    compw = D.Compliance("neg_or_big_w", "c4 < 0 OR c5 > 1", w)
+    mean_w = D.Mean("c3", w)
+    before = engine.ctx().kernel_launches()
+    st = _states(table, [comp, compw, mean_w, D.Size(w)])
+    print("\nlaunches:", _launch_delta(before))
+    del table
+    pred = ("or", [(4, "<", 0), (5, ">", 1)])
+    cols, _, cnt = O.generated_suite(specs, 0, WHERE_ROWS, preds=[pred])
+    t, nn = cnt["preds"][0]
+    assert (st[comp].numMatches, st[comp].count) == (t, WHERE_ROWS)
+    assert nn < WHERE_ROWS  # rows where both sides are NULL or FALSE/NULL exist: the NULL rule is exercised
+    cols, _, cntw = O.generated_suite(specs, 0, WHERE_ROWS, where=("and", [(0, ">", 0.0), (6, ">=", 0)]), preds=[pred])
+    tw, _ = cntw["preds"][0]
+    assert (st[compw].numMatches, st[compw].count) == (tw, cntw["where_true"])
+    assert st[D.Size(w)].numMatches == cntw["where_true"]
+    o = cols[3]
+    assert st[mean_w].count == o["n"] and _rel(st[mean_w].sum_, o["ex_sum"]), (st[mean_w].sum_, o["ex_sum"])
+
+
 def c3_specs():
     return [dict(name="k", kind=N.SYNTH_KEY30, spark_type=N.TYPE_LONG, seed=0xC3000001, vseed=0xC3000101, permille=10,
                  hll=1),
