@@ -585,6 +585,14 @@ class KLLSketch(ScanShareableAnalyzer):
 
 
 # ---- grouping analyzers (A/GroupingAnalyzers.scala) ----------------------------------------------
+def _host_key_column(col):
+    """A key column with host buffers (device-resident columns are copied back once)."""
+    if getattr(col, "values", None) is not None or not getattr(col, "device", None):
+        return col
+    from .distributed import _host_column
+    return _host_column(col)
+
+
 def _canonical_group_key(key):
     """A group key tuple with every float wrapped as engine.GroupFloat (bitwise equality, NaN canonical,
     -0.0 != 0.0), so keys from device tables, persisted states and host dicts join exactly."""
@@ -597,18 +605,31 @@ def _canonical_group_key(key):
 
 
 class FrequenciesAndNumRows:
-    """A/GroupingAnalyzers.scala:123-156. `frequencies` is a device (key -> count) table produced by
-    dq_frequencies, or a host dict after a state merge (outer join with counts added)."""
+    """A/GroupingAnalyzers.scala:123-156. `frequencies` is one of
+      * engine.FrequencyTable — the device (key -> count) table built by dq_frequencies;
+      * engine.PairFrequencies — (canonical key, count) arrays of one fixed-width key (a persisted state);
+      * groups.GroupBlock — the groups of any key shape as host key columns + counts (persisted / merged states;
+        a merge concatenates blocks, so a key may repeat: the weighted GPU build that evaluates it adds them);
+      * dict[tuple -> int] — a host state built in Python (small)."""
 
     def __init__(self, frequencies, numRows, columns=None, summary=None):
-        self.frequencies = frequencies  # engine.FrequencyTable or dict[tuple -> int]
+        self.frequencies = frequencies
         self.numRows = int(numRows)
         self.columns = columns
+        self._device = None
 
     def as_dict(self):
-        if isinstance(self.frequencies, dict):
-            return self.frequencies
-        return self.frequencies.to_dict()
+        from . import groups as G
+        f = self.frequencies
+        if isinstance(f, dict):
+            return f
+        if isinstance(f, G.GroupBlock):
+            out = {}
+            for k, c in zip(f.keys(), f.counts.tolist()):
+                k = _canonical_group_key(k)
+                out[k] = out.get(k, 0) + int(c)
+            return out
+        return f.to_dict()
 
     def _values_side(self):
         """This state as a single fixed-width-key table (device FrequencyTable or host PairFrequencies), or None."""
@@ -623,7 +644,8 @@ class FrequenciesAndNumRows:
         """Null-safe full outer join on the keys, counts added (A/GroupingAnalyzers.scala:127-147). Keys are
         compared with Spark's grouping equality (floating values bitwise, NaN canonical). Single fixed-width
         keys merge on the GPU (dq_freq_merge) when either side is a device table, as canonical 64-bit
-        pairs otherwise; other key shapes join as host dicts."""
+        pairs otherwise; any other key shape concatenates the two sides' groups (GroupBlock), which the weighted
+        GPU build behind every metric of the state aggregates."""
         a, b = self._values_side(), other._values_side()
         if a is not None and b is not None and a.key_type == b.key_type:
             rows = self.numRows + other.numRows
@@ -637,12 +659,57 @@ class FrequenciesAndNumRows:
             ta = a.to_device() if isinstance(a, engine.PairFrequencies) else a
             tb = b.to_device() if isinstance(b, engine.PairFrequencies) else b
             return FrequenciesAndNumRows(ta.merge(tb), rows, self.columns)
+        ba, bb = self.group_block(), other.group_block()
+        if ba is None and bb is not None and isinstance(self.frequencies, dict):
+            ba = _block_from_dict(self.frequencies, bb)
+        if bb is None and ba is not None and isinstance(other.frequencies, dict):
+            bb = _block_from_dict(other.frequencies, ba)
+        if ba is not None and bb is not None and ba.schema() == bb.schema():
+            from . import groups as G
+            merged = G.concat([ba, bb], ba.schema())
+            return FrequenciesAndNumRows(merged, self.numRows + other.numRows, self.columns)
         merged = {}
         for src in (self.as_dict(), other.as_dict()):
             for k, v in src.items():
                 k = _canonical_group_key(k)
                 merged[k] = merged.get(k, 0) + v
         return FrequenciesAndNumRows(merged, self.numRows + other.numRows, self.columns)
+
+    def group_block(self):
+        """The groups as a host GroupBlock (key cells + counts, vectorised: no per-group Python), or None for a
+        host dict, a Histogram table (NULL group) or a pair table without key columns."""
+        from . import groups as G
+        f = self.frequencies
+        if isinstance(f, G.GroupBlock):
+            return f
+        if isinstance(f, engine.PairFrequencies):
+            if f.null_count:
+                return None
+            name = (f.names or self.columns or ["c0"])[0]
+            return G.GroupBlock([G.column_from_canonical(name, f.key_type, f.keys, 18 if f.decimal_scale else 0,
+                                                         f.decimal_scale)], f.counts)
+        if not isinstance(f, engine.FrequencyTable) or f.include_nulls or f.source is None:
+            return None
+        keys, counts = f.export_raw()
+        if f.key_kind() == N.FREQ_KEYS_VALUES:
+            c = f.key_columns[0]
+            cols = [G.column_from_canonical(c.name, c.spark_type, keys, c.decimal_precision, c.decimal_scale)]
+        else:
+            cols = [G.take(_host_key_column(c), keys) for c in f.key_columns]
+        return G.GroupBlock(cols, counts, f.num_rows, 0)
+
+    def device_table(self):
+        """The state as a device FrequencyTable: a GroupBlock is built once on the GPU, weighted by its counts
+        (dq_frequencies_ex), so repeated keys of a merged block add up."""
+        from . import groups as G
+        f = self.frequencies
+        if isinstance(f, engine.FrequencyTable):
+            return f
+        if self._device is None and isinstance(f, G.GroupBlock):
+            self._device = engine.frequencies(f.table(), f.names, False, weights=f.counts)
+        if self._device is None and isinstance(f, engine.PairFrequencies):
+            self._device = f.to_device()
+        return self._device
 
     def summary(self, entropy_rows=None):
         n = self.numRows if entropy_rows is None else entropy_rows
@@ -659,7 +726,24 @@ class FrequenciesAndNumRows:
                 p = counts / n
                 ent = float(-(p * np.log(p)).sum())
             return {"num_groups": len(counts), "num_unique": int((counts == 1).sum()), "entropy": ent}
-        return self.frequencies.summary(n)
+        return self.device_table().summary(n)
+
+
+def _block_from_dict(freq, like):
+    """A host dict state as a GroupBlock of `like`'s key schema (small Python-built states)."""
+    from . import groups as G
+    from .table import _column_from_pylist
+    if any(c.spark_type == N.TYPE_DECIMAL for c in like.columns):
+        return None  # the Python decimal decoding picks its own scale
+    keys = list(freq.keys())
+    cols = []
+    for i, c in enumerate(like.columns):
+        items = [k[i] for k in keys]
+        items = [float(v) if isinstance(v, engine.GroupFloat) else v for v in items]
+        col = _column_from_pylist(c.name, c.spark_type, items)
+        col.decimal_precision, col.decimal_scale = c.decimal_precision, c.decimal_scale
+        cols.append(col)
+    return G.GroupBlock(cols, np.array([freq[k] for k in keys], dtype=np.int64))
 
 
 def computeFrequencies(data, groupingColumns, include_nulls=False):
@@ -783,11 +867,14 @@ class MutualInformation(FrequencyBasedAnalyzer):
         if state is None:
             return metricFromEmpty(self, self.name, inst, Entity.Mutlicolumn)
         f = state.frequencies
+        if not isinstance(f, (dict, engine.FrequencyTable)):
+            f = state.device_table()  # a persisted / merged GroupBlock: its weighted build
         if isinstance(f, engine.FrequencyTable) and f.source is not None and len(f.names) == 2 and \
                 state.numRows == f.num_rows:
-            # on the GPU: the joint table plus the two marginal tables of the same rows (dq_freq_mutual_information)
-            x = engine.frequencies(f.source, [f.names[0]])
-            y = engine.frequencies(f.source, [f.names[1]])
+            # on the GPU: the joint table plus the two marginal tables of the same rows (dq_freq_mutual_information);
+            # a merged / loaded state is a weighted build over its groups, and so are its marginals
+            x = engine.frequencies(f.source, [f.names[0]], weights=f.weights)
+            y = engine.frequencies(f.source, [f.names[1]], weights=f.weights)
             value, present = f.mutual_information(x, y)
             if not present:
                 return metricFromEmpty(self, self.name, inst, Entity.Mutlicolumn)

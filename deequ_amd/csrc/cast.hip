@@ -11,6 +11,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "dq_common.h"
@@ -123,10 +125,55 @@ struct CBuffers {
 
 extern "C" {
 
-int dq_cast_column(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_dev,
-                   uint8_t* validity_dev) {
-    if (!ctx || !column || nrows < 0 || column->length != nrows || (nrows > 0 && (!values_dev || !validity_dev)))
+static int cast_single(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_dev,
+                       uint8_t* validity_dev);
+
+int dq_cast_column(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_out,
+                   uint8_t* validity_out) {
+    if (!ctx || !column || nrows < 0 || column->length != nrows || (nrows > 0 && (!values_out || !validity_out)))
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_cast_column: invalid arguments");
+    const int nsub = dq::ctx_num_subs(ctx);
+    if (nsub == 0) return cast_single(ctx, column, nrows, to_type, values_out, validity_out);
+    // multi-device context: host column in, host results out; each device casts its contiguous row shard (2048-row
+    // aligned, so its validity words start on a word boundary) and copies its slice of the results back
+    if (column->flags & DQ_COL_DEVICE) return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "a multi-device context takes host columns");
+    std::vector<int> rc(nsub, DQ_OK);
+    std::vector<std::string> err(nsub);
+    std::vector<dq_column> cols(nsub, *column);
+    std::vector<std::vector<std::vector<int32_t>>> scratch(nsub);
+    std::vector<std::thread> th;
+    for (int i = 0; i < nsub; ++i) {
+        int64_t r0 = 0, cnt = 0;
+        dq::shard_bounds(nrows, nsub, i, &r0, &cnt);
+        dq::shard_columns(column, 1, r0, cnt, &cols[i], scratch[i]);
+        th.emplace_back([&, i, r0, cnt]() {
+            if (cnt == 0) return;
+            dq_ctx* sub = dq::ctx_sub(ctx, i);
+            void* dv = nullptr;
+            void* dm = nullptr;
+            const size_t vb = (size_t)cnt * 8, mb = (size_t)(cnt + 63) / 64 * 8;
+            if (hipSetDevice(dq::ctx_device(sub)) != hipSuccess || hipMalloc(&dv, vb) != hipSuccess ||
+                hipMalloc(&dm, mb) != hipSuccess) {
+                rc[i] = DQ_ERR_OUT_OF_MEMORY;
+            } else {
+                rc[i] = cast_single(sub, &cols[i], cnt, to_type, dv, (uint8_t*)dm);
+                if (rc[i] == DQ_OK &&
+                    (hipMemcpy((uint8_t*)values_out + (size_t)r0 * 8, dv, vb, hipMemcpyDeviceToHost) != hipSuccess ||
+                     hipMemcpy(validity_out + (size_t)r0 / 8, dm, mb, hipMemcpyDeviceToHost) != hipSuccess))
+                    rc[i] = DQ_ERR_DEVICE;
+            }
+            if (dv) (void)hipFree(dv);
+            if (dm) (void)hipFree(dm);
+        });
+    }
+    for (auto& x : th) x.join();
+    for (int i = 0; i < nsub; ++i)
+        if (rc[i] != DQ_OK) return dq::ctx_fail(ctx, rc[i], "dq_cast_column: a device's shard failed");
+    return DQ_OK;
+}
+
+static int cast_single(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_dev,
+                       uint8_t* validity_dev) {
     const int t = column->spark_type;
     const bool is_string = t == DQ_TYPE_STRING;
     if (is_string && !column->offsets)

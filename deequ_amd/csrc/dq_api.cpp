@@ -23,7 +23,7 @@
 
 #include "dq_common.h"
 #include "dq_internal.h"
-#include "hll_bias_p9.h"
+
 
 using namespace dq;
 
@@ -65,7 +65,7 @@ bool scan_concurrency() {
 bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, int ncols, PredSimple& out) {
     memset(&out, 0, sizeof(out));
     enum { E_COL, E_CONST, E_BOOL };
-    struct Ent { int kind, idx; };
+    struct Ent { int kind, idx; bool neg = false; };  // neg: a constant under unary minus (`x < -1`)
     std::vector<Ent> st;
     auto fixed_numeric = [&](int c) {
         if (c < 0 || c >= ncols) return false;
@@ -80,7 +80,7 @@ bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, 
         out.b[out.nb++] = (int8_t)b;
         return true;
     };
-    auto term = [&](int col, int op, int k) -> int {  // k: constant index, or -1 for IS [NOT] NULL
+    auto term = [&](int col, int op, int k, bool neg = false) -> int {  // k: constant index, or -1 for IS [NOT] NULL
         if (out.nterms >= kPredTerms) return -1;
         PredTerm& q = out.t[out.nterms];
         q.col = col;
@@ -89,8 +89,9 @@ bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, 
             const dq_const& c = pr.consts[k];
             const int ty = columns[col].spark_type;
             q.dbl = (ty == DQ_TYPE_FLOAT || ty == DQ_TYPE_DOUBLE || c.tag == DQ_V_DOUBLE) ? 1 : 0;
-            q.ci = c.i64;
-            q.cd = c.tag == DQ_V_DOUBLE ? c.f64 : (double)c.i64;
+            // Spark's UnaryMinus on a literal: a Long negates with wrap-around, a Double flips its sign
+            q.ci = neg ? (int64_t)(0ull - (uint64_t)c.i64) : c.i64;
+            q.cd = c.tag == DQ_V_DOUBLE ? (neg ? -c.f64 : c.f64) : (double)q.ci;
         }
         return out.nterms++;
     };
@@ -124,8 +125,8 @@ bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, 
                 const Ent b = st.back(); st.pop_back();
                 const Ent a = st.back(); st.pop_back();
                 int k;
-                if (a.kind == E_COL && b.kind == E_CONST) k = term(a.idx, op, b.idx);
-                else if (a.kind == E_CONST && b.kind == E_COL) k = term(b.idx, flip(op), a.idx);
+                if (a.kind == E_COL && b.kind == E_CONST) k = term(a.idx, op, b.idx, b.neg);
+                else if (a.kind == E_CONST && b.kind == E_COL) k = term(b.idx, flip(op), a.idx, a.neg);
                 else return false;
                 if (k < 0 || !emit(k)) return false;
                 st.push_back({E_BOOL, 0});
@@ -148,6 +149,13 @@ bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, 
             case DQ_P_NOT:
                 if (st.empty() || st.back().kind != E_BOOL || !emit(kPB_NOT)) return false;
                 break;
+            case DQ_P_NEG: {  // -constant (a LONG / DOUBLE literal): folded into the leaf's constant
+                if (st.empty() || st.back().kind != E_CONST) return false;
+                const int tag = pr.consts[st.back().idx].tag;
+                if (tag != DQ_V_LONG && tag != DQ_V_DOUBLE) return false;
+                st.back().neg = !st.back().neg;
+                break;
+            }
             case DQ_P_IN: {  // x IN (c1..cn) with non-NULL constants == (x = c1) OR ... OR (x = cn)
                 const int n = arg;
                 if (n < 1 || (int)st.size() < n + 1) return false;
@@ -155,7 +163,7 @@ bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, 
                 if (st[base].kind != E_COL) return false;
                 for (int i = 0; i < n; ++i) {
                     if (st[base + 1 + i].kind != E_CONST) return false;
-                    const int k = term(st[base].idx, DQ_P_EQ, st[base + 1 + i].idx);
+                    const int k = term(st[base].idx, DQ_P_EQ, st[base + 1 + i].idx, st[base + 1 + i].neg);
                     if (k < 0 || !emit(k)) return false;
                     if (i > 0 && !emit(kPB_OR)) return false;
                 }
@@ -174,6 +182,7 @@ bool compile_simple_predicate(const dq_predicate& pr, const dq_column* columns, 
 // Which kernel a launch group runs (mirrors values_kernel_for in scan.hip).
 int scan_kernel_family(int kind, int P, int nc, int heavy) {
     if (kind == SK_BITS) return DQ_KERNEL_BITS;
+    if (heavy == 3) return DQ_KERNEL_WHERE_FUSED;
     if ((heavy || nc == 2) && P == 2) return heavy == 2 ? DQ_KERNEL_HEAVY8_FULL : DQ_KERNEL_HEAVY8;
     return heavy ? DQ_KERNEL_STRIPED_HEAVY : DQ_KERNEL_STRIPED;
 }
@@ -243,36 +252,6 @@ int64_t padded_words_for(int64_t nrows) {
     return tiles * (kTileRows / 64);
 }
 
-// ------------------------------------------------------------------------------------------------
-// Host state algebra (State.sum of each reference state)
-// ------------------------------------------------------------------------------------------------
-void hll_merge_words(const int64_t* a, const int64_t* b, int64_t* out) {
-    // DeequHyperLogLogPlusPlusUtils.merge (C/StatefulHyperloglogPlus.scala:188-208)
-    int idx = 0;
-    for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) {
-        uint64_t wa = (uint64_t)a[w], wb = (uint64_t)b[w], word = 0;
-        uint64_t mask = 63;
-        for (int i = 0; idx < DQ_HLL_REGISTERS && i < 10; ++i, ++idx) {
-            word |= std::max(wa & mask, wb & mask);
-            mask <<= 6;
-        }
-        out[w] = (int64_t)word;
-    }
-}
-
-double java_math_min(double a, double b) {
-    if (a != a) return a;
-    if (b != b) return b;
-    if (a == 0.0 && b == 0.0) return signbit(a) ? a : b;
-    return a <= b ? a : b;
-}
-double java_math_max(double a, double b) {
-    if (a != a) return a;
-    if (b != b) return b;
-    if (a == 0.0 && b == 0.0) return signbit(a) ? b : a;
-    return a >= b ? a : b;
-}
-
 }  // namespace
 
 namespace dq {
@@ -280,6 +259,8 @@ hipStream_t ctx_stream(dq_ctx* ctx) { return ctx->stream; }
 int ctx_device(dq_ctx* ctx) { return ctx->device; }
 int ctx_cus(dq_ctx* ctx) { return ctx->cus; }
 int ctx_fail(dq_ctx* ctx, int code, const char* msg) { return fail(ctx, code, "%s", msg); }
+int ctx_num_subs(dq_ctx* ctx) { return (int)ctx->subs.size(); }
+dq_ctx* ctx_sub(dq_ctx* ctx, int i) { return ctx->subs[i]; }
 // The context's device arena / pinned staging buffer, grown to `bytes` (NULL + error set on failure).
 // Used by one call at a time (a ctx is not re-entrant); work queued on the ctx stream stays ordered.
 void* ctx_scratch(dq_ctx* ctx, size_t bytes) { return ensure_arena(ctx, bytes) == DQ_OK ? ctx->arena : nullptr; }
@@ -732,6 +713,22 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         sopmap.push_back(m);
     }
 
+    // `where` filters evaluated inside the scan (WhereOut, dq_internal.h): every simple predicate used as a `where`
+    // (DQ_WHERE_MASKS=0 or DQ_PRED_VM=1: the bitmap pass for all of them, for A/B runs).
+    std::vector<char> wmasked(npreds, 0);
+    std::vector<PredSimple> wprog(npreds);
+    {
+        const char* e = getenv("DQ_WHERE_MASKS");
+        const bool masks_on = !pred_vm_forced() && !(e && e[0] == '0');
+        for (int i = 0; i < nops && masks_on; ++i) {
+            const int p = ops[i].where;
+            if (p < 0 || wmasked[p]) continue;
+            const dq_predicate& pr = preds[p];
+            if (pr.code_len == 4 && pr.code[2] == DQ_P_REGEX) continue;
+            if (compile_simple_predicate(pr, columns, ncols, wprog[p])) wmasked[p] = 1;
+        }
+    }
+
     // Ops -> OpMap; bits-only slots for Size(where), Completeness of unread columns, Compliance.
     std::vector<OpMap> opmap(nops);
     std::map<std::tuple<int, int, int>, int> bits_slots;  // (kind, col/pred, where) -> slot
@@ -761,9 +758,11 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             m.is_float = (t == DQ_TYPE_FLOAT || t == DQ_TYPE_DOUBLE);
             m.decimal_scale = t == DQ_TYPE_DECIMAL ? columns[c].decimal_scale : 0;
         }
+        m.wslot = -1;
+        const bool masked_where = op.where >= 0 && wmasked[op.where];
         switch (op.kind) {
             case DQ_OP_SIZE:
-                if (op.where >= 0) m.slot = bits_slot(0, -1, op.where);
+                if (op.where >= 0 && !masked_where) m.slot = bits_slot(0, -1, op.where);
                 break;
             case DQ_OP_COMPLIANCE:
                 if (fused_col[i] >= 0) {
@@ -782,7 +781,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                     m.colpos = it->second.pos;
                 } else if (columns[c].validity == nullptr) {
                     m.from_bits = 2;  // all rows valid: matches = conditionalCount
-                    if (op.where >= 0) m.slot = bits_slot(0, -1, op.where);
+                    if (op.where >= 0 && !masked_where) m.slot = bits_slot(0, -1, op.where);
                 } else {
                     m.slot = bits_slot(1, c, op.where);
                     m.from_bits = 1;
@@ -808,6 +807,90 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             }
         }
     }
+    // Masked `where` plan: the producer (a one-column 8-byte value slot under the filter whose terms read only that
+    // column, else an SK_WHERE slot filled by where_masks_kernel), the consumer masks, and whether bits / string
+    // slots still read the filter's bitmaps.
+    struct WherePlan {
+        int producer = -1;           // value slot evaluating the filter inside its scan
+        int wslot = -1;              // slot holding the TRUE / NOT-NULL counts
+        bool bitmaps = false;
+        std::vector<int> mask_col;   // consumer columns, one mask each
+    };
+    std::vector<WherePlan> wplan(npreds);
+    std::vector<std::pair<int, int>> slot_masks(slots.size() * 2, {-1, -1});  // (slot, k) -> (pred, mask index)
+    std::vector<int> slot_producer_of(slots.size(), -1);
+    auto slot_where = [&](const SlotDesc& sd) { return (int)(intptr_t)sd.where_t - 1; };
+    for (int p = 0; p < npreds; ++p) {
+        if (!wmasked[p]) continue;
+        WherePlan& wp = wplan[p];
+        int depth = 0, maxd = 0;
+        for (int i = 0; i < wprog[p].nb; ++i) {
+            depth += wprog[p].b[i] >= 0 ? 1 : (wprog[p].b[i] == kPB_NOT ? 0 : -1);
+            maxd = std::max(maxd, depth);
+        }
+        for (int s = 0; s < (int)slots.size() && wp.producer < 0 && maxd <= kWhereStack; ++s) {
+            const SlotDesc& sd = slots[s];
+            if (sd.kind != SK_VALUES || sd.ncols != 1 || slot_where(sd) != p) continue;
+            const int x = (int)(intptr_t)sd.col[0].values;
+            const int t = columns[x].spark_type;
+            if (!(t == DQ_TYPE_LONG || t == DQ_TYPE_TIMESTAMP || t == DQ_TYPE_DOUBLE)) continue;
+            bool own = true;
+            for (int k = 0; k < wprog[p].nterms; ++k) own &= wprog[p].t[k].col == x;
+            if (own) wp.producer = s;
+        }
+        for (int s = 0; s < (int)slots.size(); ++s) {
+            SlotDesc& sd = slots[s];
+            if (sd.kind == SK_BITS && (slot_where(sd) == p || ((int)sd.col[0].flags == 2 && (int)(intptr_t)sd.col[0].values == p)))
+                wp.bitmaps = true;
+            if (sd.kind != SK_VALUES || slot_where(sd) != p) continue;
+            if (s == wp.producer) continue;
+            for (int k = 0; k < sd.ncols; ++k) {
+                const int c = (int)(intptr_t)sd.col[k].values;
+                auto it = std::find(wp.mask_col.begin(), wp.mask_col.end(), c);
+                int mi = (int)(it - wp.mask_col.begin());
+                if (it == wp.mask_col.end()) wp.mask_col.push_back(c);
+                slot_masks[2 * s + k] = {p, mi};
+            }
+        }
+        for (const StrSlot& ss : sslots)
+            if ((int)(intptr_t)ss.where_t - 1 == p) wp.bitmaps = true;
+        if ((int)wp.mask_col.size() > kWhereMasks) {  // too many consumers for one producer: the bitmap pass
+            wmasked[p] = 0;
+            wp = WherePlan();
+            for (auto& sm : slot_masks)
+                if (sm.first == p) sm = {-1, -1};
+            continue;
+        }
+    }
+    // Size(where) / from_bits == 2 Completeness were planned without a bits slot for masked filters: give back the
+    // bits slots to filters that fell back above.
+    for (int i = 0; i < nops; ++i) {
+        const dq_op& op = ops[i];
+        if (op.where < 0 || wmasked[op.where] || opmap[i].slot >= 0) continue;
+        if (op.kind == DQ_OP_SIZE || (op.kind == DQ_OP_COMPLETENESS && opmap[i].from_bits == 2))
+            opmap[i].slot = bits_slot(0, -1, op.where);
+    }
+    slot_masks.resize(slots.size() * 2, {-1, -1});
+    slot_producer_of.resize(slots.size(), -1);
+    for (int p = 0; p < npreds; ++p) {
+        if (!wmasked[p]) continue;
+        WherePlan& wp = wplan[p];
+        if (wp.producer >= 0) {
+            wp.wslot = wp.producer;
+            slot_producer_of[wp.producer] = p;
+            slots[wp.producer].where_t = nullptr;
+        } else {
+            wp.wslot = new_slot(SK_WHERE);
+            slot_masks.resize(slots.size() * 2, {-1, -1});
+            slot_producer_of.resize(slots.size(), -1);
+        }
+        for (int s = 0; s < (int)slots.size(); ++s)
+            if (slots[s].kind == SK_VALUES && slot_where(slots[s]) == p) slots[s].where_t = nullptr;
+    }
+    for (int i = 0; i < nops; ++i) {
+        const int p = ops[i].where;
+        if (p >= 0) opmap[i].wslot = wmasked[p] ? wplan[p].wslot : opmap[i].slot;
+    }
     const int nslots = (int)slots.size();
     if (nslots > kMaxSlots) return fail(ctx, DQ_ERR_UNSUPPORTED, "too many slots (%d)", nslots);
     // Predicates evaluated by the VM pass: `where` filters and Compliance predicates not fused into
@@ -817,6 +900,16 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
         if (ops[i].where >= 0) pred_used[ops[i].where] = 1;
         if (ops[i].kind == DQ_OP_COMPLIANCE && fused_col[i] < 0) pred_used[ops[i].predicate] = 1;
     }
+    // pred_used: the predicate gets TRUE / NOT-NULL bitmaps (allocated); pred_pass: a predicate pass writes them (a
+    // masked `where` writes them from its producer, only when something reads them)
+    std::vector<char> pred_pass(pred_used);
+    int nstandalone = 0;
+    for (int p = 0; p < npreds; ++p) {
+        if (!wmasked[p]) continue;
+        pred_pass[p] = 0;
+        if (!wplan[p].bitmaps) pred_used[p] = 0;
+        if (wplan[p].producer < 0) ++nstandalone;
+    }
 
     // ---- device memory layout -----------------------------------------------------------------
     // Launch groups: one kernel launch per slot shape; each gets a grid sized to fill the chip once.
@@ -824,7 +917,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     struct Group { int kind, P, nc; bool f0, f1; int heavy; int grid; std::vector<int32_t> slots; };
     std::vector<Group> groups;
     auto shape_key = [](int kind, int P, int nc, bool f0, bool f1, int heavy) {
-        return (((((kind * 16 + P) * 4 + nc) * 2 + f0) * 2 + f1) * 3 + heavy);
+        return (((((kind * 16 + P) * 4 + nc) * 2 + f0) * 2 + f1) * 4 + heavy);
     };
     // heavy 2 (8-byte columns only): every column carries stats, moments, HLL and a fused compare the heavy kernel
     // evaluates on its fast path, pairs carry the correlation, and there is no `where` -> the branch-free variant
@@ -838,6 +931,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     std::map<int, int> group_of;
     for (int s = 0; s < (int)slots.size(); ++s) {
         const SlotDesc& sd = slots[s];
+        if (sd.kind == SK_WHERE) continue;
         const bool f0 = sd.kind == SK_VALUES && (sd.col[0].elem == ET_F32 || sd.col[0].elem == ET_F64);
         const bool f1 = sd.kind == SK_VALUES && sd.ncols > 1 && (sd.col[1].elem == ET_F32 || sd.col[1].elem == ET_F64);
         const int P = sd.kind == SK_VALUES ? sd.rows_per_load : 8;
@@ -851,6 +945,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             for (int k = 0; k < sd.ncols; ++k) full &= full_col(sd.col[k]);
             if (full) heavy = 2;
         }
+        if (slot_producer_of[s] >= 0) heavy = 3;
         const int kind = sd.kind;
         const int key = shape_key(kind, P, nc, f0, f1, heavy);
         auto it = group_of.find(key);
@@ -875,9 +970,15 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     int sgrid = nsslots ? string_scan_grid(ctx->cus, nrows) : 0;
     if (concurrent && sgrid) sgrid = std::max(1, (sgrid + nlaunch - 1) / nlaunch);
     gstride = std::max(gstride, sgrid);
+    // producers first: their masks are read by the other launches
+    std::stable_sort(groups.begin(), groups.end(), [](const Group& a, const Group& b) { return (a.heavy == 3) > (b.heavy == 3); });
     std::vector<int32_t> slot_nblocks(std::max<size_t>(slots.size(), 1), 1);
     for (const Group& g : groups)
         for (int32_t s : g.slots) slot_nblocks[s] = g.grid;
+    const int64_t wchunks = (padded_words_for(nrows) + 7) / 8;  // where_masks_kernel: 8 words per wave, 4 waves
+    const int wgrid = (int)std::max<int64_t>(1, std::min<int64_t>((wchunks + 3) / 4, gstride));
+    for (int p = 0; p < npreds; ++p)
+        if (wmasked[p] && wplan[p].producer < 0) slot_nblocks[wplan[p].wslot] = wgrid;
     std::vector<int32_t> hll_nblocks(std::max(nhll, 1), 1);
     for (const auto& kv : uses)
         if (kv.second.hll >= 0) hll_nblocks[kv.second.hll] = slot_nblocks[kv.second.slot];
@@ -889,8 +990,8 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
     std::vector<const void*> dval(ncols, nullptr), dvalid(ncols, nullptr), doffs(ncols, nullptr);
     size_t arena_need = 0;
     std::vector<size_t> stage_off(ncols, 0);
-    int npred_used = 0;
-    for (int p = 0; p < npreds; ++p) npred_used += pred_used[p];
+    int npred_pass = 0;
+    for (int p = 0; p < npreds; ++p) npred_pass += pred_pass[p];
     for (int pass = 0; pass < 2; ++pass) {
         Bump b;
         b.base = pass ? ctx->arena : nullptr;
@@ -925,11 +1026,19 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             pt[p] = (uint64_t*)b.take((size_t)pwords * 8);
             pn[p] = (uint64_t*)b.take((size_t)pwords * 8);
         }
+        // masked `where`: the producer's descriptor and one mask per consumer column
+        std::vector<WhereOut*> wodev(npreds, nullptr);
+        std::vector<std::vector<uint64_t*>> wmask(npreds);
+        for (int p = 0; p < npreds; ++p) {
+            if (!wmasked[p]) continue;
+            wodev[p] = (WhereOut*)b.take(sizeof(WhereOut));
+            for (size_t m = 0; m < wplan[p].mask_col.size(); ++m) wmask[p].push_back((uint64_t*)b.take((size_t)pwords * 8));
+        }
         void* pcols = b.take(sizeof(PredColumn) * std::max(ncols, 1));
         int32_t* rx_status = (int32_t*)b.take(sizeof(int32_t) * std::max(npreds, 1));
         std::vector<void*> pprog(npreds, nullptr), pcode(npreds, nullptr), pconst(npreds, nullptr), pstr(npreds, nullptr);
         for (int p = 0; p < npreds; ++p) {
-            if (!pred_used[p]) continue;
+            if (!pred_pass[p]) continue;
             pprog[p] = b.take(sizeof(PredProgram));
             pcode[p] = b.take(sizeof(int32_t) * preds[p].code_len);
             pconst[p] = b.take(sizeof(dq_const) * std::max(preds[p].n_consts, 1));
@@ -957,7 +1066,9 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                          sizeof(PredColumn) * std::max(ncols, 1) + sizeof(SlotDesc) * std::max(nslots, 1) +
                          sizeof(OpMap) * nops + sizeof(dq_state) * nops + 4 * (slot_nblocks.size() + hll_nblocks.size() + nslots) + 8192;
             for (int p = 0; p < npreds; ++p)
-                if (pred_used[p])
+                if (wmasked[p]) pin += sizeof(WhereOut) + 256;
+            for (int p = 0; p < npreds; ++p)
+                if (pred_pass[p])
                     pin += sizeof(PredProgram) + sizeof(int32_t) * preds[p].code_len +
                            sizeof(dq_const) * std::max(preds[p].n_consts, 1) + std::max<int64_t>(preds[p].strings_len, 1) + 256;
             rc = ensure_pinned(ctx, pin);
@@ -976,7 +1087,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             return DQ_OK;
         };
         bool any_regex = false;
-        if (npred_used) {
+        if (npred_pass || nstandalone) {
             DQ_HIP(ctx, hipMemsetAsync(rx_status, 0, sizeof(int32_t) * std::max(npreds, 1), ctx->stream));
             std::vector<PredColumn> pc(std::max(ncols, 1));
             for (int c = 0; c < ncols; ++c) {
@@ -991,7 +1102,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             int rc = upload(pcols, pc.data(), sizeof(PredColumn) * pc.size());
             if (rc) return rc;
             for (int p = 0; p < npreds; ++p) {
-                if (!pred_used[p]) continue;
+                if (!pred_pass[p]) continue;
                 const dq_predicate& pr = preds[p];
                 rc = upload(pcode[p], pr.code, sizeof(int32_t) * pr.code_len);
                 if (rc) return rc;
@@ -1028,6 +1139,30 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 DQ_HIP(ctx, hipGetLastError());
             }
         }
+        // masked `where` descriptors; the standalone producers run here, before every scan launch
+        for (int p = 0; p < npreds; ++p) {
+            if (!wmasked[p]) continue;
+            const WherePlan& wp = wplan[p];
+            WhereOut wo;
+            memset(&wo, 0, sizeof(wo));
+            wo.prog = wprog[p];
+            wo.nmasks = (int)wp.mask_col.size();
+            wo.bitmaps = wp.bitmaps ? 1 : 0;
+            wo.where_t = pt[p];
+            wo.where_nn = pn[p];
+            for (int m = 0; m < wo.nmasks; ++m) {
+                wo.valid[m] = (const uint64_t*)dvalid[wp.mask_col[m]];
+                wo.mask[m] = wmask[p][m];
+            }
+            int rc = upload(wodev[p], &wo, sizeof(wo));
+            if (rc) return rc;
+            if (wp.producer < 0) {
+                launch_where_masks(wodev[p], wprog[p], (const PredColumn*)pcols, nrows, pwords, partials, wp.wslot, gstride,
+                                   slot_nblocks[wp.wslot], ctx->stream);
+                DQ_HIP(ctx, hipGetLastError());
+                ctx->kernel_launches[DQ_KERNEL_WHERE_MASKS]++;
+            }
+        }
         // resolve slot descriptors
         for (int s = 0; s < nslots; ++s) {
             SlotDesc& sd = slots[s];
@@ -1041,7 +1176,10 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                     sd.col[k].validity = (const uint64_t*)dvalid[c];
                     sd.col[k].spark_type = columns[c].spark_type;
                     sd.col[k].elem = elem_of(columns[c].spark_type);
+                    const auto& sm = slot_masks[2 * s + k];
+                    if (sm.first >= 0) sd.col[k].validity = wmask[sm.first][sm.second];  // valid & where TRUE
                 }
+                sd.wout = slot_producer_of[s] >= 0 ? wodev[slot_producer_of[s]] : nullptr;
             } else {
                 const int tag = (int)sd.col[0].flags;
                 const int ref = (int)(intptr_t)sd.col[0].values;
@@ -1085,22 +1223,31 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             used_side = std::max(used_side, j + 1);
             return ctx->side[j];
         };
+        int li = 0;
+        size_t goff = 0;
+        size_t gi = 0;
+        auto launch_group = [&](const Group& g, hipStream_t st) -> int {
+            if (launch_scan_group(g.kind, g.P, g.nc, g.f0, g.f1, g.heavy, dslots, dgroups + goff, (int)g.slots.size(), nrows,
+                                  ntiles, gstride, g.grid, partials, hllp, st) != 0)
+                return fail(ctx, DQ_ERR_DEVICE, "scan launch failed for shape (%d,%d,%d)", g.kind, g.P, g.nc);
+            DQ_HIP(ctx, hipGetLastError());
+            ctx->kernel_launches[scan_kernel_family(g.kind, g.P, g.nc, g.heavy)]++;
+            goff += g.slots.size();
+            return DQ_OK;
+        };
+        // `where` producers first, on the ctx stream: every other launch reads their masks
+        for (; gi < groups.size() && groups[gi].heavy == 3; ++gi) {
+            rc = launch_group(groups[gi], ctx->stream);
+            if (rc) return rc;
+        }
         if (concurrent) {
             DQ_HIP(ctx, hipEventRecord(ctx->fork_ev, ctx->stream));
             for (int j = 0; j < std::min(nlaunch - 1, dq_ctx::kSide); ++j)
                 DQ_HIP(ctx, hipStreamWaitEvent(ctx->side[j], ctx->fork_ev, 0));
         }
-        int li = 0;
-        if (nslots) {
-            size_t off = 0;
-            for (const Group& g : groups) {
-                if (launch_scan_group(g.kind, g.P, g.nc, g.f0, g.f1, g.heavy, dslots, dgroups + off, (int)g.slots.size(), nrows,
-                                      ntiles, gstride, g.grid, partials, hllp, launch_stream(li++)) != 0)
-                    return fail(ctx, DQ_ERR_DEVICE, "scan launch failed for shape (%d,%d,%d)", g.kind, g.P, g.nc);
-                DQ_HIP(ctx, hipGetLastError());
-                ctx->kernel_launches[scan_kernel_family(g.kind, g.P, g.nc, g.heavy)]++;
-                off += g.slots.size();
-            }
+        for (; gi < groups.size(); ++gi) {
+            rc = launch_group(groups[gi], launch_stream(li++));
+            if (rc) return rc;
         }
         if (nsslots) {
             launch_string_scan(dsslots, nsslots, nrows, sgrid, gstride, spartials, hllp, launch_stream(li++));
@@ -1136,7 +1283,7 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             DQ_HIP(ctx, hipMemcpyAsync(hs, rx_status, sizeof(int32_t) * std::max(npreds, 1), hipMemcpyDeviceToHost, ctx->stream));
             DQ_HIP(ctx, hipStreamSynchronize(ctx->stream));
             for (int p = 0; p < npreds; ++p)
-                if (pred_used[p] && hs[p])
+                if (pred_pass[p] && hs[p])
                     return fail(ctx, DQ_ERR_UNSUPPORTED, "predicate %d: regex backtracking limit exceeded", p);
         }
         if (!(flags & DQ_SCAN_OUT_DEVICE)) {
@@ -1294,189 +1441,6 @@ int dq_scan_streamed(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t n
     rc = dq_state_fold(hst.data(), (int)nchunks, nops, out);  // chunks in row order
     if (rc) return fail(ctx, rc, "dq_scan_streamed: state fold failed");
     return DQ_OK;
-}
-
-int dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out) {
-    if (!a || !b || !out || a->kind != b->kind) return DQ_ERR_INVALID_ARGUMENT;
-    // Analyzers.merge (A/Analyzer.scala:367-386): None is the identity.
-    if (!a->present) { *out = *b; return DQ_OK; }
-    if (!b->present) { *out = *a; return DQ_OK; }
-    dq_state r = *a;
-    switch (a->kind) {
-        case DQ_OP_SIZE:
-            r.u.num_matches.num_matches = a->u.num_matches.num_matches + b->u.num_matches.num_matches;
-            break;
-        case DQ_OP_COMPLETENESS:
-        case DQ_OP_COMPLIANCE:
-            r.u.num_matches_and_count.num_matches += b->u.num_matches_and_count.num_matches;
-            r.u.num_matches_and_count.count += b->u.num_matches_and_count.count;
-            break;
-        case DQ_OP_MEAN:
-            r.u.mean.count = a->u.mean.count + b->u.mean.count;
-            if (a->u.mean.exact && b->u.mean.exact) {  // Long partials: wrap-around add, one final cast
-                r.u.mean.isum = (int64_t)((uint64_t)a->u.mean.isum + (uint64_t)b->u.mean.isum);
-                r.u.mean.sum = (double)r.u.mean.isum;
-            } else {
-                r.u.mean.sum = a->u.mean.sum + b->u.mean.sum;
-                r.u.mean.exact = 0;
-            }
-            break;
-        case DQ_OP_SUM:
-            if (a->u.dbl.exact && b->u.dbl.exact) {
-                r.u.dbl.isum = (int64_t)((uint64_t)a->u.dbl.isum + (uint64_t)b->u.dbl.isum);
-                r.u.dbl.value = (double)r.u.dbl.isum;
-            } else {
-                r.u.dbl.value = a->u.dbl.value + b->u.dbl.value;
-                r.u.dbl.exact = 0;
-            }
-            break;
-        case DQ_OP_MINIMUM:
-        case DQ_OP_MIN_LENGTH:
-            r.u.dbl.value = java_math_min(a->u.dbl.value, b->u.dbl.value);
-            break;
-        case DQ_OP_MAXIMUM:
-        case DQ_OP_MAX_LENGTH:
-            r.u.dbl.value = java_math_max(a->u.dbl.value, b->u.dbl.value);
-            break;
-        case DQ_OP_STANDARD_DEVIATION: {  // A/StandardDeviation.scala:37-44
-            const double n = a->u.stddev.n, on = b->u.stddev.n;
-            const double newN = n + on;
-            const double delta = b->u.stddev.avg - a->u.stddev.avg;
-            const double deltaN = newN == 0.0 ? 0.0 : delta / newN;
-            r.u.stddev.n = newN;
-            r.u.stddev.avg = a->u.stddev.avg + deltaN * on;
-            r.u.stddev.m2 = a->u.stddev.m2 + b->u.stddev.m2 + delta * deltaN * n * on;
-            break;
-        }
-        case DQ_OP_CORRELATION: {  // A/Correlation.scala:37-52
-            const double n1 = a->u.corr.n, n2 = b->u.corr.n, newN = n1 + n2;
-            const double dx = b->u.corr.x_avg - a->u.corr.x_avg;
-            const double dxN = newN == 0.0 ? 0.0 : dx / newN;
-            const double dy = b->u.corr.y_avg - a->u.corr.y_avg;
-            const double dyN = newN == 0.0 ? 0.0 : dy / newN;
-            r.u.corr.n = newN;
-            r.u.corr.x_avg = a->u.corr.x_avg + dxN * n2;
-            r.u.corr.y_avg = a->u.corr.y_avg + dyN * n2;
-            r.u.corr.ck = a->u.corr.ck + b->u.corr.ck + dx * dyN * n1 * n2;
-            r.u.corr.x_mk = a->u.corr.x_mk + b->u.corr.x_mk + dx * dxN * n1 * n2;
-            r.u.corr.y_mk = a->u.corr.y_mk + b->u.corr.y_mk + dy * dyN * n1 * n2;
-            break;
-        }
-        case DQ_OP_APPROX_COUNT_DISTINCT:
-            hll_merge_words(a->u.hll.words, b->u.hll.words, r.u.hll.words);
-            break;
-        case DQ_OP_DATATYPE:
-            r.u.datatype.num_null += b->u.datatype.num_null;
-            r.u.datatype.num_fractional += b->u.datatype.num_fractional;
-            r.u.datatype.num_integral += b->u.datatype.num_integral;
-            r.u.datatype.num_boolean += b->u.datatype.num_boolean;
-            r.u.datatype.num_string += b->u.datatype.num_string;
-            break;
-        default:
-            return DQ_ERR_UNSUPPORTED;
-    }
-    *out = r;
-    return DQ_OK;
-}
-
-int dq_state_fold(const dq_state* states, int nparts, int nops, dq_state* out) {
-    // Rank-ordered semigroup fold (Analyzers.merge per op, A/Analyzer.scala:367-386) of nparts x nops
-    // records laid out part-major, as an all-gather of per-rank dq_scan outputs delivers them.
-    if ((nparts > 0 && nops > 0 && (!states || !out)) || nparts < 0 || nops < 0) return DQ_ERR_INVALID_ARGUMENT;
-    for (int i = 0; i < nops; ++i) {
-        dq_state acc = states[i];
-        for (int r = 1; r < nparts; ++r) {
-            dq_state next;
-            const int rc = dq_state_merge(&acc, &states[(size_t)r * nops + i], &next);
-            if (rc) return rc;
-            acc = next;
-        }
-        out[i] = acc;
-    }
-    return DQ_OK;
-}
-
-// DeequHyperLogLogPlusPlusUtils.estimateBias (C/StatefulHyperloglogPlus.scala:259-297), P = 9, K = 6.
-static double hll_estimate_bias(double e) {
-    const double* est = DQ_HLL_P9_RAW;
-    const int num = DQ_HLL_P9_N;
-    // java.util.Arrays.binarySearch: index if found, else -(insertion point) - 1 -> insertion point
-    int lo = 0, hi = num - 1, nearest = -1;
-    while (lo <= hi) {
-        const int mid = (int)(((unsigned)lo + (unsigned)hi) >> 1);
-        const double mv = est[mid];
-        if (mv < e) lo = mid + 1;
-        else if (mv > e) hi = mid - 1;
-        else {
-            // Double.compare semantics; the table holds no NaN / signed zeros.
-            nearest = mid;
-            break;
-        }
-    }
-    if (nearest < 0) nearest = lo;
-    auto distance = [&](int i) {
-        const double d = e - est[i];
-        return d * d;
-    };
-    const int K = 6;
-    int low = std::max(nearest - K + 1, 0);
-    int high = std::min(low + K, num);
-    while (high < num && distance(high) < distance(low)) {
-        ++low;
-        ++high;
-    }
-    double bias = 0.0;
-    for (int i = low; i < high; ++i) bias += DQ_HLL_P9_BIAS[i];
-    return bias / (high - low);
-}
-
-double dq_hll_count(const int64_t words[DQ_HLL_NUM_WORDS]) {
-    const int P = 9, M = 512;
-    const double alphaM2 = (0.7213 / (1.0 + 1.079 / M)) * M * M;
-    double zInverse = 0.0, V = 0.0;
-    int idx = 0;
-    for (int w = 0; w < DQ_HLL_NUM_WORDS; ++w) {
-        const uint64_t word = (uint64_t)words[w];
-        int shift = 0;
-        for (int i = 0; idx < M && i < 10; ++i, ++idx, shift += 6) {
-            const int64_t Midx = (int64_t)((word >> shift) & 63u);
-            // Scala `1 << Midx` on an Int: JVM shift distance is Midx & 31, result is a 32-bit int.
-            const int32_t pow2 = (int32_t)((uint32_t)1u << (Midx & 31));
-            zInverse += 1.0 / (double)pow2;
-            if (Midx == 0) V += 1.0;
-        }
-    }
-    auto corrected = [&]() {
-        const double e = alphaM2 / zInverse;
-        return (P < 19 && e < 5.0 * M) ? e - hll_estimate_bias(e) : e;
-    };
-    double estimate;
-    if (V > 0) {
-        const double H = M * log(M / V);
-        estimate = H <= DQ_HLL_P9_THRESHOLD ? H : corrected();
-    } else {
-        estimate = corrected();
-    }
-    // Math.round(double): floor(x + 0.5) as a long
-    return (double)(int64_t)floor(estimate + 0.5);
-}
-
-int64_t dq_spark_hash64(int32_t spark_type, const void* value, int64_t len) {
-    if (!value) return 0;
-    switch (spark_type) {
-        case DQ_TYPE_BOOLEAN: return (int64_t)xxh_int(*(const uint8_t*)value ? 1u : 0u, SPARK_HLL_SEED);
-        case DQ_TYPE_BYTE: return (int64_t)xxh_int((uint32_t)(int32_t)*(const int8_t*)value, SPARK_HLL_SEED);
-        case DQ_TYPE_SHORT: return (int64_t)xxh_int((uint32_t)(int32_t)*(const int16_t*)value, SPARK_HLL_SEED);
-        case DQ_TYPE_INT:
-        case DQ_TYPE_DATE: return (int64_t)xxh_int((uint32_t)*(const int32_t*)value, SPARK_HLL_SEED);
-        case DQ_TYPE_LONG:
-        case DQ_TYPE_TIMESTAMP:
-        case DQ_TYPE_DECIMAL: return (int64_t)xxh_long((uint64_t)*(const int64_t*)value, SPARK_HLL_SEED);
-        case DQ_TYPE_FLOAT: return (int64_t)xxh_int(float_to_int_bits(*(const float*)value), SPARK_HLL_SEED);
-        case DQ_TYPE_DOUBLE: return (int64_t)xxh_long(double_to_long_bits(*(const double*)value), SPARK_HLL_SEED);
-        case DQ_TYPE_STRING: return (int64_t)xxh_bytes((const uint8_t*)value, len, SPARK_HLL_SEED);
-        default: return 0;
-    }
 }
 
 int dq_synth_column(dq_ctx* ctx, int32_t kind, uint64_t seed, int64_t row0, int64_t nrows, void* values_dev) {

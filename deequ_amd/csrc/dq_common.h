@@ -6,10 +6,14 @@
 // The counter-based splitmix64 generator defines the synthetic BASELINE inputs.
 #pragma once
 
-#include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#if defined(DQ_HOST_ONLY)  // host-only builds of the pure host code (the sanitizer build, tests/sanitize/)
+#define DQ_HD inline
+#else
+#include <hip/hip_runtime.h>
 #define DQ_HD __host__ __device__ __forceinline__
+#endif
 
 namespace dq {
 

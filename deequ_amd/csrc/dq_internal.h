@@ -55,7 +55,13 @@ struct ColDesc {
     double pred_d;             // constant (FP_DOUBLE)
 };
 
-enum SlotKind : int32_t { SK_VALUES = 0, SK_BITS = 1 };
+enum SlotKind : int32_t {
+    SK_VALUES = 0,
+    SK_BITS = 1,
+    SK_WHERE = 2,  // holds the TRUE / NOT-NULL row counts of a `where` evaluated by where_masks_kernel (not a scan launch)
+};
+
+struct WhereOut;
 
 struct SlotDesc {
     ColDesc col[2];
@@ -68,6 +74,7 @@ struct SlotDesc {
     int32_t ncols;             // SK_VALUES: 1 or 2
     int32_t corr;              // compute CorrelationState of (col0, col1)
     int32_t rows_per_load;     // P: 2, 4 or 8
+    const WhereOut* wout;      // where producer: this slot's scan evaluates a `where` from col[0] (scan_heavy8_kernel)
 };
 
 struct ColPartial {
@@ -107,6 +114,8 @@ struct OpMap {
     int32_t hll_slot;    // ApproxCountDistinct register set
     int32_t decimal_scale;
     int32_t from_bits;   // Completeness answered from a bits-only slot (vt) instead of c[colpos].n
+    int32_t wslot;       // slot whose wt / wnn are the op's conditionalCount (its `where`); -1 = no where
+    int32_t pad;
     int64_t nrows;       // count(*) of the batch
 };
 
@@ -183,6 +192,24 @@ struct PredSimple {
     int32_t nb;
     PredTerm t[kPredTerms];
     int8_t b[kPredBCode];  // postfix: >= 0 pushes term b[i]; kPB_AND / kPB_OR / kPB_NOT
+};
+
+// A `where` evaluated inside the scan (simple predicates): instead of TRUE / NOT-NULL bitmaps that every
+// slot under the filter re-reads and pop-counts, the producer writes one mask per consumer column, valid & where TRUE,
+// which that column's scan then reads in place of its validity (running the no-`where` kernels). The producer is the
+// scan of the filter's own column when the filter reads only that 8-byte column (scan_heavy8_kernel, WP) or else a
+// pass of its own (where_masks_kernel); either also counts the TRUE / NOT-NULL rows (conditionalCount) into a slot
+// partial, and writes the bitmaps only when bits / string slots read them.
+constexpr int kWhereMasks = 32;
+constexpr int kWhereStack = 8;  // fused producer: 8-row bytes on a 64-bit stack
+struct WhereOut {
+    PredSimple prog;                      // fused producer: every term's column is the slot's col[0]
+    int32_t nmasks;
+    int32_t bitmaps;                      // 1: write where_t / where_nn
+    uint64_t* where_t;                    // padded bitmaps (pwords words)
+    uint64_t* where_nn;
+    const uint64_t* valid[kWhereMasks];   // consumer column validity (nullptr = all valid; exactly ceil(nrows/8) bytes)
+    uint64_t* mask[kWhereMasks];          // out: valid & where TRUE, padded bitmap
 };
 
 inline int elem_of(int32_t spark_type) {
@@ -269,6 +296,14 @@ void* scratch_alloc(dq_ctx* ctx, size_t bytes);
 void scratch_release(dq_ctx* ctx, void* ptr, size_t bytes);
 void scratch_trim(dq_ctx* ctx);
 
+// Context accessors for the .hip translation units (dq_api.cpp).
+hipStream_t ctx_stream(dq_ctx* ctx);
+int ctx_device(dq_ctx* ctx);
+int ctx_fail(dq_ctx* ctx, int code, const char* msg);
+int ctx_cus(dq_ctx* ctx);
+int ctx_num_subs(dq_ctx* ctx);       // devices of a multi-device context (dq_open_devices), 0 for a single-device one
+dq_ctx* ctx_sub(dq_ctx* ctx, int i);  // the single-device context of device i of a multi-device one
+
 // Multi-device orchestration (multi.cpp).
 int multi_scan(dq_ctx* ctx, const dq_column* const* shard_columns, const int64_t* shard_rows, int ncols,
                const dq_op* ops, int nops, const dq_predicate* preds, int npreds, dq_state* out);
@@ -303,6 +338,10 @@ void launch_finalize(const OpMap* ops, int nops, const SlotPartial* finals, cons
                      dq_state* out, hipStream_t s);
 void launch_pred_simple(const PredSimple& prog, const PredColumn* cols_dev, int64_t nrows, int64_t padded_words,
                         uint64_t* out_t, uint64_t* out_nn, hipStream_t s);
+// Standalone `where` producer: masks / bitmaps of WhereOut (its terms' columns index cols_dev) and per-block row
+// counts into partials[wslot * gstride + block] for `grid` blocks.
+void launch_where_masks(const WhereOut* wo_dev, const PredSimple& prog, const PredColumn* cols_dev, int64_t nrows,
+                        int64_t padded_words, SlotPartial* partials, int wslot, int gstride, int grid, hipStream_t s);
 void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
                       int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s);
 int string_scan_grid(int cus, int64_t nrows);

@@ -11,14 +11,41 @@
 //     otherwise `slow` is set (and hexadecimal literals set it too) so the caller can fail loudly.
 #pragma once
 
-#include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#if defined(DQ_HOST_ONLY)  // host-only build (tests/sanitize/): the same parsers, checked by ASan / UBSan
+#define DQ_PARSE_FN inline
+#define __constant__
+#else
+#include <hip/hip_runtime.h>
+#define DQ_PARSE_FN __host__ __device__ inline
+#endif
 
 #include "pow5_table.h"
 
 namespace dq {
 
-__device__ inline bool spark_string_to_long(const uint8_t* s, int n, int64_t& out) {
+DQ_PARSE_FN int parse_clz64(uint64_t w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __clzll((long long)w);
+#else
+    return __builtin_clzll(w);
+#endif
+}
+DQ_PARSE_FN double parse_bits_double(uint64_t u) {
+    union { uint64_t u; double d; } c;
+    c.u = u;
+    return c.d;
+}
+DQ_PARSE_FN uint64_t parse_umulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+DQ_PARSE_FN bool spark_string_to_long(const uint8_t* s, int n, int64_t& out) {
     if (n == 0) return false;
     uint8_t b = s[0];
     const bool negative = b == '-';
@@ -55,7 +82,7 @@ struct AdjustedMantissa {
 };
 
 // Eisel-Lemire compute_float for binary64 (w != 0 path; see tools/gen_pow5_table.py for references).
-__device__ inline AdjustedMantissa el_compute_float(int64_t q, uint64_t w) {
+DQ_PARSE_FN AdjustedMantissa el_compute_float(int64_t q, uint64_t w) {
     AdjustedMantissa a;
     if (w == 0 || q < DQ_POW5_MIN_Q) {
         a.power2 = 0;
@@ -67,14 +94,14 @@ __device__ inline AdjustedMantissa el_compute_float(int64_t q, uint64_t w) {
         a.mantissa = 0;
         return a;
     }
-    const int lz = __clzll((long long)w);
+    const int lz = parse_clz64(w);
     w <<= lz;
     const int index = 2 * (int)(q - DQ_POW5_MIN_Q);
     const uint64_t precision_mask = 0xFFFFFFFFFFFFFFFFull >> 55;
-    uint64_t p_hi = __umul64hi(w, dq_pow5_128[index]);
+    uint64_t p_hi = parse_umulhi64(w, dq_pow5_128[index]);
     uint64_t p_lo = w * dq_pow5_128[index];
     if ((p_hi & precision_mask) == precision_mask) {
-        const uint64_t s_hi = __umul64hi(w, dq_pow5_128[index + 1]);
+        const uint64_t s_hi = parse_umulhi64(w, dq_pow5_128[index + 1]);
         p_lo += s_hi;
         if (s_hi > p_lo) ++p_hi;
     }
@@ -111,14 +138,14 @@ __device__ inline AdjustedMantissa el_compute_float(int64_t q, uint64_t w) {
     return a;
 }
 
-__device__ inline bool match_word(const uint8_t* s, int i, int n, const char* w, int wl) {
+DQ_PARSE_FN bool match_word(const uint8_t* s, int i, int n, const char* w, int wl) {
     if (n - i != wl) return false;
     for (int k = 0; k < wl; ++k)
         if (s[i + k] != (uint8_t)w[k]) return false;
     return true;
 }
 
-__device__ inline bool java_parse_double(const uint8_t* s, int n, double& out, bool& slow) {
+DQ_PARSE_FN bool java_parse_double(const uint8_t* s, int n, double& out, bool& slow) {
     int i = 0;
     while (i < n && s[i] <= ' ') ++i;  // String.trim
     while (n > i && s[n - 1] <= ' ') --n;
@@ -130,12 +157,12 @@ __device__ inline bool java_parse_double(const uint8_t* s, int n, double& out, b
     }
     if (i < n && s[i] == 'N') {
         if (!match_word(s, i, n, "NaN", 3)) return false;
-        out = __longlong_as_double(0x7ff8000000000000LL);
+        out = parse_bits_double(0x7ff8000000000000ULL);
         return true;
     }
     if (i < n && s[i] == 'I') {
         if (!match_word(s, i, n, "Infinity", 8)) return false;
-        out = neg ? -__longlong_as_double(0x7ff0000000000000LL) : __longlong_as_double(0x7ff0000000000000LL);
+        out = neg ? -parse_bits_double(0x7ff0000000000000ULL) : parse_bits_double(0x7ff0000000000000ULL);
         return true;
     }
     if (i + 1 < n && s[i] == '0' && (s[i + 1] == 'x' || s[i + 1] == 'X')) {
@@ -217,7 +244,7 @@ __device__ inline bool java_parse_double(const uint8_t* s, int n, double& out, b
         bits = a.mantissa | ((uint64_t)a.power2 << 52);
     }
     if (neg) bits |= 0x8000000000000000ull;
-    out = __longlong_as_double((long long)bits);
+    out = parse_bits_double((uint64_t)bits);
     return true;
 }
 

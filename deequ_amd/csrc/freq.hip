@@ -2815,8 +2815,11 @@ int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq
     if (!ctx || !joint || !x || !y || !mi || !present)
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_mutual_information: invalid arguments");
     if (!joint->parts.empty()) return mi_composite(ctx, joint, mi, present);
+    // weighted builds (pre-aggregated groups: a merged or persisted state) are fine when all three share the rows and
+    // their weights, as a state's marginals are grouped from its joint groups (A/MutualInformation.scala:50-58)
+    const bool wj = joint->ks.weights != nullptr;
     if (joint->fast || joint->ks.ncols != 2 || !joint->reps || x->ks.ncols != 1 || y->ks.ncols != 1 ||
-        x->ks.weights || y->ks.weights || joint->ks.weights)
+        (x->ks.weights != nullptr) != wj || (y->ks.weights != nullptr) != wj)
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT,
                             "dq_freq_mutual_information: needs the (x, y) table and the x / y tables of the same rows");
     return mi_tables(ctx, joint, x, y, mi, present);

@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <vector>
 
 #include "dq_common.h"
@@ -456,6 +457,8 @@ int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nse
 hipStream_t ctx_stream(dq_ctx* ctx);
 int ctx_device(dq_ctx* ctx);
 int ctx_fail(dq_ctx* ctx, int code, const char* msg);
+int ctx_num_subs(dq_ctx* ctx);
+dq_ctx* ctx_sub(dq_ctx* ctx, int i);
 void* ctx_scratch(dq_ctx* ctx, size_t bytes);
 void* ctx_pinned_buf(dq_ctx* ctx, size_t bytes);
 
@@ -593,10 +596,199 @@ void put_f64(std::vector<uint8_t>& o, double d) {
         if (e_ != hipSuccess) return dq::ctx_fail((ctx), DQ_ERR_DEVICE, hipGetErrorString(e_));   \
     } while (0)
 
+namespace {
+
+// ---- host-side QuantileNonSample.merge over KLLState bytes (A/QuantileNonSample.scala:218-234, condense :94-111,
+// NonSampleCompactor.compact A/NonSampleCompactor.scala:42-66; KLLState.sum / mergeUntyped, A/KLLSketch.scala:49-54,
+// R/KLLRunner.scala:40-44): the partition sketches of a multi-device context folded in device order.
+struct KComp {
+    int32_t ncomp = 0, offset = 0;
+    std::vector<double> buf;
+};
+struct KState {
+    double gmin = 0, gmax = 0;
+    int32_t sketch = 0, cur = 0, actual = 0, total = 0;
+    double f = 0;
+    std::vector<KComp> c;
+};
+
+uint32_t get_be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+double get_f64(const uint8_t* p) {
+    uint64_t u = 0;
+    for (int i = 0; i < 8; ++i) u = (u << 8) | p[i];
+    double d;
+    memcpy(&d, &u, 8);
+    return d;
+}
+
+bool kll_parse(const std::vector<uint8_t>& b, KState& s) {
+    size_t at = 0;
+    auto need = [&](size_t n) { return at + n <= b.size(); };
+    if (!need(16 + 28)) return false;
+    s.gmin = get_f64(&b[0]);
+    s.gmax = get_f64(&b[8]);
+    at = 16;
+    s.sketch = (int32_t)get_be32(&b[at]);
+    s.f = get_f64(&b[at + 4]);
+    s.cur = (int32_t)get_be32(&b[at + 12]);
+    s.actual = (int32_t)get_be32(&b[at + 16]);
+    s.total = (int32_t)get_be32(&b[at + 20]);
+    const int32_t ncomp = (int32_t)get_be32(&b[at + 24]);
+    at += 28;
+    if (ncomp < 0 || ncomp > kKllMaxLevels) return false;
+    s.c.assign(ncomp, KComp());
+    for (int h = 0; h < ncomp; ++h) {
+        if (!need(12)) return false;
+        s.c[h].ncomp = (int32_t)get_be32(&b[at]);
+        s.c[h].offset = (int32_t)get_be32(&b[at + 4]);
+        const int32_t len = (int32_t)get_be32(&b[at + 8]);
+        at += 12;
+        if (len < 0 || !need((size_t)len * 8)) return false;
+        s.c[h].buf.resize(len);
+        for (int i = 0; i < len; ++i) s.c[h].buf[i] = get_f64(&b[at + 8 * (size_t)i]);
+        at += (size_t)len * 8;
+    }
+    return true;
+}
+
+void kll_serialize(const KState& s, std::vector<uint8_t>& o) {
+    o.clear();
+    put_f64(o, s.gmin);
+    put_f64(o, s.gmax);
+    put_be32(o, s.sketch);
+    put_f64(o, s.f);
+    put_be32(o, s.cur);
+    put_be32(o, s.actual);
+    put_be32(o, s.total);
+    put_be32(o, (int32_t)s.c.size());
+    for (const KComp& c : s.c) {
+        put_be32(o, c.ncomp);
+        put_be32(o, c.offset);
+        put_be32(o, (int32_t)c.buf.size());
+        for (double d : c.buf) put_f64(o, d);
+    }
+}
+
+int32_t kll_items(const KState& s) {
+    int64_t n = 0;
+    for (int h = 0; h < s.cur && h < (int)s.c.size(); ++h) n += (int64_t)s.c[h].buf.size();
+    return (int32_t)n;
+}
+
+void kll_expand(KState& s) {
+    s.c.push_back(KComp());
+    s.cur = (int32_t)s.c.size();
+    int64_t t = 0;
+    for (int h = 0; h < s.cur; ++h) t += kll_capacity(s.sketch, s.f, h);
+    s.total = (int32_t)t;
+}
+
+// NonSampleCompactor.compact: the first len = items - items % 2 items sorted (Ordering.Double: -0.0 < 0.0, NaN
+// largest), every second from offset (flipped on odd compaction counts) goes up, the odd last item stays.
+void kll_compact(KComp& c, std::vector<double>& out) {
+    const size_t items = c.buf.size(), len = items - items % 2;
+    if (c.ncomp % 2 == 1) c.offset = 1 - c.offset;
+    std::vector<double> srt(c.buf.begin(), c.buf.begin() + len);
+    std::stable_sort(srt.begin(), srt.end(), [](double a, double b) { return host_key(a) < host_key(b); });
+    out.clear();
+    for (size_t i = (size_t)c.offset; i < len; i += 2) out.push_back(srt[i]);
+    std::vector<double> keep;
+    if (items % 2 == 1) keep.push_back(c.buf[items - 1]);
+    c.buf.swap(keep);
+    c.ncomp += 1;
+}
+
+void kll_condense(KState& s) {
+    for (size_t h = 0; h < s.c.size(); ++h) {
+        if ((int64_t)s.c[h].buf.size() >= kll_capacity(s.sketch, s.f, (int)h)) {
+            if ((int)h + 1 >= s.cur) kll_expand(s);
+            std::vector<double> out;
+            kll_compact(s.c[h], out);
+            s.c[h + 1].buf.insert(s.c[h + 1].buf.end(), out.begin(), out.end());
+            s.actual = kll_items(s);
+            break;
+        }
+    }
+}
+
+// java.lang.Math.max / min on doubles: NaN if either is NaN, -0.0 < 0.0
+double java_max(double a, double b) {
+    if (a != a || b != b) return NAN;
+    return host_key(a) >= host_key(b) ? a : b;
+}
+double java_min(double a, double b) {
+    if (a != a || b != b) return NAN;
+    return host_key(a) <= host_key(b) ? a : b;
+}
+
+bool kll_merge(KState& a, const KState& b) {
+    while (a.cur < b.cur) kll_expand(a);
+    for (int i = 0; i < b.cur; ++i) a.c[i].buf.insert(a.c[i].buf.end(), b.c[i].buf.begin(), b.c[i].buf.end());
+    a.actual = kll_items(a);
+    for (int guard = 0; a.actual >= a.total; ++guard) {
+        if (guard > (1 << 20)) return false;
+        kll_condense(a);
+    }
+    a.gmax = java_max(a.gmax, b.gmax);
+    a.gmin = java_min(a.gmin, b.gmin);
+    return true;
+}
+
+}  // namespace
+
 extern "C" {
+
+static int64_t kll_sketch_single(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t sketch_size,
+                                 double shrinking_factor, uint8_t* state_out, int64_t capacity,
+                                 std::vector<uint8_t>* keep);
 
 int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t sketch_size,
                       double shrinking_factor, uint8_t* state_out, int64_t capacity) {
+    if (!ctx || !column || nrows < 0 || column->length != nrows || capacity < 0 || (capacity > 0 && !state_out))
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_kll_sketch: invalid arguments");
+    const int nsub = dq::ctx_num_subs(ctx);
+    if (nsub == 0) return kll_sketch_single(ctx, column, nrows, sketch_size, shrinking_factor, state_out, capacity, nullptr);
+    // multi-device context: one partition per device (contiguous row shards, KLLRunner.sketchPartitions per
+    // partition), sketched concurrently, merged in device order on the host (KLLRunner's reduce of the partition
+    // sketches, R/KLLRunner.scala:104-112)
+    if (column->flags & DQ_COL_DEVICE) return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "a multi-device context takes host columns");
+    std::vector<std::vector<uint8_t>> parts(nsub);
+    std::vector<int64_t> rc(nsub, 0);
+    std::vector<dq_column> cols(nsub, *column);
+    std::vector<std::vector<std::vector<int32_t>>> scratch(nsub);
+    std::vector<std::thread> th;
+    for (int i = 0; i < nsub; ++i) {
+        int64_t r0 = 0, cnt = 0;
+        dq::shard_bounds(nrows, nsub, i, &r0, &cnt);
+        dq::shard_columns(column, 1, r0, cnt, &cols[i], scratch[i]);
+        th.emplace_back([&, i, cnt]() {
+            dq_ctx* sub = dq::ctx_sub(ctx, i);
+            if (hipSetDevice(dq::ctx_device(sub)) != hipSuccess) {
+                rc[i] = DQ_ERR_DEVICE;
+                return;
+            }
+            rc[i] = kll_sketch_single(sub, &cols[i], cnt, sketch_size, shrinking_factor, nullptr, 0, &parts[i]);
+        });
+    }
+    for (auto& x : th) x.join();
+    for (int i = 0; i < nsub; ++i)
+        if (rc[i] < 0) return dq::ctx_fail(ctx, (int)rc[i], "dq_kll_sketch: a device's partition failed");
+    KState acc;
+    if (!kll_parse(parts[0], acc)) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: malformed partition state");
+    for (int i = 1; i < nsub; ++i) {
+        KState b;
+        if (!kll_parse(parts[i], b) || !kll_merge(acc, b))
+            return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: partition merge failed");
+    }
+    std::vector<uint8_t> o;
+    kll_serialize(acc, o);
+    if ((int64_t)o.size() <= capacity) memcpy(state_out, o.data(), o.size());
+    return (int64_t)o.size();
+}
+
+static int64_t kll_sketch_single(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t sketch_size,
+                                 double shrinking_factor, uint8_t* state_out, int64_t capacity,
+                                 std::vector<uint8_t>* keep) {
     if (!ctx || !column || nrows < 0 || column->length != nrows || capacity < 0 || (capacity > 0 && !state_out))
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_kll_sketch: invalid arguments");
     if (!(shrinking_factor == shrinking_factor))
@@ -808,7 +1000,8 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
         put_be32(o, (int32_t)fin[h].size());
         for (double d : fin[h]) put_f64(o, d);
     }
-    if ((int64_t)o.size() <= capacity) memcpy(state_out, o.data(), o.size());
+    if (keep) *keep = o;
+    else if ((int64_t)o.size() <= capacity) memcpy(state_out, o.data(), o.size());
     return (int64_t)o.size();
 }
 

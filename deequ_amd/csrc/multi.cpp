@@ -57,34 +57,6 @@ static const Rccl& rccl() {
     return r;
 }
 
-void shard_bounds(int64_t nrows, int ndev, int i, int64_t* row0, int64_t* count) {
-    int64_t per = (nrows + ndev - 1) / std::max(ndev, 1);
-    per = (per + kTileRows - 1) / kTileRows * kTileRows;
-    const int64_t r0 = std::min<int64_t>((int64_t)i * per, nrows);
-    *row0 = r0;
-    *count = std::max<int64_t>(0, std::min<int64_t>(nrows, r0 + per) - r0);
-}
-
-void shard_columns(const dq_column* columns, int ncols, int64_t row0, int64_t count, dq_column* out,
-                   std::vector<std::vector<int32_t>>& scratch) {
-    scratch.resize(ncols);
-    for (int c = 0; c < ncols; ++c) {
-        dq_column col = columns[c];
-        col.length = count;
-        if (col.validity) col.validity += row0 / 8;  // row0 is a multiple of 2048
-        if (col.spark_type == DQ_TYPE_STRING) {
-            const int32_t base = col.offsets ? col.offsets[row0] : 0;
-            scratch[c].resize((size_t)count + 1);
-            for (int64_t k = 0; k <= count; ++k) scratch[c][k] = col.offsets[row0 + k] - base;
-            col.offsets = scratch[c].data();
-            col.values = static_cast<const uint8_t*>(col.values) + base;
-        } else {
-            col.values = static_cast<const uint8_t*>(col.values) + row0 * elem_size(elem_of(col.spark_type));
-        }
-        out[c] = col;
-    }
-}
-
 int for_each_device(dq_ctx* ctx, int (*fn)(int, dq_ctx*, void*), void* arg) {
     const int n = (int)ctx->subs.size();
     std::vector<int> rc(n, DQ_OK);
@@ -268,3 +240,4 @@ void close_subs(dq_ctx* ctx) {
     ctx->subs.clear();
 }
 }  // namespace dq
+static_assert(dq::kTileRows == 2048, "host_algebra.cpp shards on 2048-row tiles");

@@ -653,6 +653,117 @@ pred_simple_kernel(const PredSimple P, const PredColumn* __restrict__ cols, int6
     }
 }
 
+// Standalone `where` producer (WhereOut): the simple predicate over kPredRows words per wave as in pred_simple_kernel,
+// grid-strided over `gridDim.x` blocks; lane j < kPredRows then writes word j of every consumer mask (valid & TRUE) and,
+// if asked, of the bitmaps; the TRUE / NOT-NULL counts go to this block's partial of the filter's SK_WHERE slot.
+__device__ __forceinline__ uint64_t valid_word(const uint64_t* v, int64_t w, int64_t nrows) {
+    if (v == nullptr) return ~0ull;
+    if ((w + 1) * 64 <= nrows) return v[w];
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(v);
+    const int64_t nb = (nrows + 7) >> 3;
+    uint64_t x = 0;
+    for (int i = 0; i < 8; ++i)
+        if (w * 8 + i < nb) x |= (uint64_t)b[w * 8 + i] << (8 * i);
+    return x;
+}
+
+__global__ void __launch_bounds__(256)
+where_masks_kernel(const PredSimple P, const WhereOut* __restrict__ wo, const PredColumn* __restrict__ cols,
+                   int64_t nrows, int64_t padded_words, SlotPartial* __restrict__ partials, int wslot, int gstride) {
+    __shared__ int64_t red[2][4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t wt = 0, wnn = 0;
+    const int64_t nchunks = (padded_words + kPredRows - 1) / kPredRows;  // kPredRows words per wave
+    for (int64_t ch = (int64_t)blockIdx.x * 4 + wave; ch < nchunks; ch += (int64_t)gridDim.x * 4) {
+        const int64_t w0 = ch * kPredRows;
+        const int64_t row0 = w0 * 64 + lane;
+        uint32_t tb[kPredRows], nb[kPredRows];
+#pragma unroll
+        for (int j = 0; j < kPredRows; ++j) tb[j] = nb[j] = 0;
+        for (int k = 0; k < P.nterms; ++k) term_rows(P.t[k], cols[P.t[k].col], row0, nrows, (uint32_t)k, tb, nb);
+        uint32_t st[kPredRows], sn[kPredRows];
+#pragma unroll
+        for (int j = 0; j < kPredRows; ++j) st[j] = sn[j] = 0;
+        int sp = 0;
+        for (int i = 0; i < P.nb; ++i) {
+            const int o = P.b[i];
+            if (o >= 0) {
+#pragma unroll
+                for (int j = 0; j < kPredRows; ++j) {
+                    st[j] |= ((tb[j] >> o) & 1u) << sp;
+                    sn[j] |= ((nb[j] >> o) & 1u) << sp;
+                }
+                ++sp;
+            } else if (o == kPB_NOT) {
+                const uint32_t m = 1u << (sp - 1);
+#pragma unroll
+                for (int j = 0; j < kPredRows; ++j) st[j] ^= sn[j] & m;
+            } else {
+                const uint32_t keep = (1u << (sp - 2)) - 1u;
+#pragma unroll
+                for (int j = 0; j < kPredRows; ++j) {
+                    const uint32_t ta = (st[j] >> (sp - 2)) & 1u, na = (sn[j] >> (sp - 2)) & 1u;
+                    const uint32_t tc = (st[j] >> (sp - 1)) & 1u, nc = (sn[j] >> (sp - 1)) & 1u;
+                    uint32_t rt, rn;
+                    if (o == kPB_AND) {
+                        const uint32_t af = na & (ta ^ 1u), cf = nc & (tc ^ 1u);
+                        rn = af | cf | (na & nc);
+                        rt = (af | cf) ? 0u : (na & nc);
+                    } else {
+                        rt = ta | tc;
+                        rn = rt | (na & nc);
+                    }
+                    st[j] = (st[j] & keep) | (rt << (sp - 2));
+                    sn[j] = (sn[j] & keep) | (rn << (sp - 2));
+                }
+                --sp;
+            }
+        }
+        uint64_t mine_t = 0, mine_n = 0;
+#pragma unroll
+        for (int j = 0; j < kPredRows; ++j) {
+            const uint64_t bt = __ballot(st[j] & 1u);
+            const uint64_t bn = __ballot(sn[j] & 1u);
+            wt += __popcll(bt);
+            wnn += __popcll(bn);
+            mine_t = lane == j ? bt : mine_t;
+            mine_n = lane == j ? bn : mine_n;
+        }
+        const int64_t w = w0 + lane;
+        if (lane < kPredRows && w < padded_words) {
+            const int nm = wo->nmasks;
+            for (int m = 0; m < nm; ++m) wo->mask[m][w] = valid_word(wo->valid[m], w, nrows) & mine_t;
+            if (wo->bitmaps) {
+                wo->where_t[w] = mine_t;
+                wo->where_nn[w] = mine_n;
+            }
+        }
+    }
+    if (lane == 0) {
+        red[0][wave] = wt;
+        red[1][wave] = wnn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SlotPartial& o = partials[(int64_t)wslot * gstride + blockIdx.x];
+        SlotPartial z;
+        memset(&z, 0, sizeof(z));
+        z.c[0].imin = z.c[1].imin = INT64_MAX;
+        z.c[0].imax = z.c[1].imax = INT64_MIN;
+        z.c[0].dmin = z.c[1].dmin = INFINITY;
+        z.c[0].dmax = z.c[1].dmax = -INFINITY;
+        z.wt = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+        z.wnn = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+        o = z;
+    }
+}
+
+void launch_where_masks(const WhereOut* wo_dev, const PredSimple& prog, const PredColumn* cols_dev, int64_t nrows,
+                        int64_t padded_words, SlotPartial* partials, int wslot, int gstride, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(where_masks_kernel, dim3((unsigned)grid), dim3(256), 0, s, prog, wo_dev, cols_dev, nrows,
+                       padded_words, partials, wslot, gstride);
+}
+
 void launch_pred_simple(const PredSimple& prog, const PredColumn* cols_dev, int64_t nrows, int64_t padded_words,
                         uint64_t* out_t, uint64_t* out_nn, hipStream_t s) {
     const int64_t words_per_block = 4 * kPredRows;  // 4 waves

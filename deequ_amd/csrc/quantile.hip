@@ -28,6 +28,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "dq_common.h"
@@ -186,6 +188,8 @@ hipStream_t ctx_stream(dq_ctx* ctx);
 int ctx_device(dq_ctx* ctx);
 int ctx_fail(dq_ctx* ctx, int code, const char* msg);
 int ctx_cus(dq_ctx* ctx);
+int ctx_num_subs(dq_ctx* ctx);      // devices of a multi-device context, 0 for a single-device one
+dq_ctx* ctx_sub(dq_ctx* ctx, int i);
 
 }  // namespace dq
 
@@ -222,6 +226,80 @@ struct QBuffers {
         if (e_ != hipSuccess) return dq::ctx_fail((ctx), DQ_ERR_DEVICE, hipGetErrorString(e_));   \
     } while (0)
 
+namespace {
+
+// One shard of the column on one device: the whole column on a single-device context, one contiguous row range per
+// device on a multi-device one (dq_open_devices). Every pass runs per shard on its own device and stream; the host
+// adds the shards' histograms, so the order statistics are those of the whole column for any device count.
+struct QShard {
+    dq_ctx* ctx = nullptr;
+    QColumn qc;
+    int64_t nrows = 0;
+    QBuffers buf;
+    uint64_t* dkeys = nullptr;
+    uint8_t* dok = nullptr;
+    uint64_t* dspl = nullptr;
+    unsigned long long* dhist = nullptr;
+    uint32_t* dtarget = nullptr;
+    unsigned long long* dcursor = nullptr;
+    uint64_t* dcand = nullptr;
+    int64_t ncand = 0;
+    int grid = 1;
+    std::vector<uint64_t> sk;
+    std::vector<uint8_t> sok;
+    std::vector<unsigned long long> hist;
+    std::string err;
+};
+
+hipError_t q_stage_and_sample(QShard& sh, const dq_column& col) {
+    hipError_t e = hipSetDevice(ctx_device(sh.ctx));
+    if (e != hipSuccess) return e;
+    hipStream_t s = ctx_stream(sh.ctx);
+    const int t = col.spark_type;
+    memset(&sh.qc, 0, sizeof(sh.qc));
+    sh.qc.elem = elem_of(t);
+    sh.qc.decimal_scale = t == DQ_TYPE_DECIMAL ? col.decimal_scale : 0;
+    sh.qc.pow10 = pow(10.0, (double)sh.qc.decimal_scale);
+    const int64_t nrows = sh.nrows;
+    const size_t vbytes = (size_t)nrows * elem_size(sh.qc.elem);
+    const size_t bbytes = (size_t)(nrows + 63) / 64 * 8;
+    if (col.flags & DQ_COL_DEVICE) {
+        sh.qc.values = col.values;
+        sh.qc.validity = (const uint64_t*)col.validity;
+    } else {
+        void *v = nullptr, *m = nullptr;
+        if ((e = sh.buf.alloc(&v, vbytes)) != hipSuccess) return e;
+        if (nrows && (e = hipMemcpyAsync(v, col.values, vbytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+        if (col.validity) {
+            if ((e = sh.buf.alloc(&m, bbytes)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(m, 0, bbytes, s)) != hipSuccess) return e;
+            if (nrows && (e = hipMemcpyAsync(m, col.validity, (size_t)(nrows + 7) / 8, hipMemcpyHostToDevice, s)) != hipSuccess)
+                return e;
+        }
+        sh.qc.values = v;
+        sh.qc.validity = (const uint64_t*)m;
+    }
+    sh.sk.assign(kQSample, 0);
+    sh.sok.assign(kQSample, 0);
+    if (nrows == 0) return hipSuccess;
+    if ((e = sh.buf.alloc((void**)&sh.dkeys, sizeof(uint64_t) * kQSample)) != hipSuccess) return e;
+    if ((e = sh.buf.alloc((void**)&sh.dok, kQSample)) != hipSuccess) return e;
+    hipLaunchKernelGGL(q_sample_kernel, dim3(kQSample / 256), dim3(256), 0, s, sh.qc, nrows, sh.dkeys, sh.dok);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(sh.sk.data(), sh.dkeys, sizeof(uint64_t) * kQSample, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return e;
+    if ((e = hipMemcpyAsync(sh.sok.data(), sh.dok, kQSample, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+}  // namespace
+
+#define QS_HIP(ctx, expr)                                                                                  \
+    do {                                                                                                   \
+        hipError_t e_ = (expr);                                                                            \
+        if (e_ != hipSuccess) return dq::ctx_fail((ctx), DQ_ERR_DEVICE, hipGetErrorString(e_));            \
+    } while (0)
+
 extern "C" {
 
 int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows, double relative_error,
@@ -241,73 +319,70 @@ int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows,
     *count_out = 0;
     if (nrows == 0) return 0;
     if (nrows >= (1LL << 46)) return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_quantile_summary: too many rows");
-    const int dev = dq::ctx_device(ctx);
-    QT_HIP(ctx, hipSetDevice(dev));
-    hipStream_t s = dq::ctx_stream(ctx);
-    QBuffers buf;
+    const int nsub = dq::ctx_num_subs(ctx);
+    if (nsub > 0 && (column->flags & DQ_COL_DEVICE))
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "a multi-device context takes host columns");
 
-    // ---- column (device-resident, or staged) ---------------------------------------------------
-    QColumn qc;
-    memset(&qc, 0, sizeof(qc));
-    qc.elem = elem_of(t);
-    qc.decimal_scale = t == DQ_TYPE_DECIMAL ? column->decimal_scale : 0;
-    qc.pow10 = pow(10.0, (double)qc.decimal_scale);
-    const size_t vbytes = (size_t)nrows * elem_size(qc.elem);
-    const size_t bbytes = (size_t)(nrows + 63) / 64 * 8;
-    if (column->flags & DQ_COL_DEVICE) {
-        qc.values = column->values;
-        qc.validity = (const uint64_t*)column->validity;
-    } else {
-        void *v = nullptr, *m = nullptr;
-        QT_HIP(ctx, buf.alloc(&v, vbytes));
-        QT_HIP(ctx, hipMemcpyAsync(v, column->values, vbytes, hipMemcpyHostToDevice, s));
-        if (column->validity) {
-            QT_HIP(ctx, buf.alloc(&m, bbytes));
-            QT_HIP(ctx, hipMemsetAsync(m, 0, bbytes, s));
-            QT_HIP(ctx, hipMemcpyAsync(m, column->validity, (size_t)(nrows + 7) / 8, hipMemcpyHostToDevice, s));
+    // ---- shards: one per device, staged and sampled concurrently -----------------------------------
+    const int ns_dev = nsub > 0 ? nsub : 1;
+    std::vector<QShard> sh(ns_dev);
+    std::vector<dq_column> cols(ns_dev, *column);
+    std::vector<std::vector<std::vector<int32_t>>> scratch(ns_dev);
+    for (int i = 0; i < ns_dev; ++i) {
+        sh[i].ctx = nsub > 0 ? dq::ctx_sub(ctx, i) : ctx;
+        int64_t r0 = 0, cnt = nrows;
+        if (nsub > 0) {
+            dq::shard_bounds(nrows, nsub, i, &r0, &cnt);
+            dq::shard_columns(column, 1, r0, cnt, &cols[i], scratch[i]);
         }
-        qc.values = v;
-        qc.validity = (const uint64_t*)m;
+        sh[i].nrows = cnt;
     }
-
-    // ---- 1. stratified sample -> splitters -------------------------------------------------------
-    uint64_t* dkeys = nullptr;
-    uint8_t* dok = nullptr;
-    QT_HIP(ctx, buf.alloc((void**)&dkeys, sizeof(uint64_t) * kQSample));
-    QT_HIP(ctx, buf.alloc((void**)&dok, kQSample));
-    hipLaunchKernelGGL(q_sample_kernel, dim3(kQSample / 256), dim3(256), 0, s, qc, nrows, dkeys, dok);
-    QT_HIP(ctx, hipGetLastError());
-    std::vector<uint64_t> sk(kQSample);
-    std::vector<uint8_t> sok(kQSample);
-    QT_HIP(ctx, hipMemcpyAsync(sk.data(), dkeys, sizeof(uint64_t) * kQSample, hipMemcpyDeviceToHost, s));
-    QT_HIP(ctx, hipMemcpyAsync(sok.data(), dok, kQSample, hipMemcpyDeviceToHost, s));
-    QT_HIP(ctx, hipStreamSynchronize(s));
+    {
+        std::vector<hipError_t> rc(ns_dev, hipSuccess);
+        std::vector<std::thread> th;
+        for (int i = 0; i < ns_dev; ++i) th.emplace_back([&, i]() { rc[i] = q_stage_and_sample(sh[i], cols[i]); });
+        for (auto& x : th) x.join();
+        for (int i = 0; i < ns_dev; ++i)
+            if (rc[i] != hipSuccess) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, hipGetErrorString(rc[i]));
+    }
+    // splitters from every shard's stratified sample (equi-depth over the union; exactness does not depend on them)
     std::vector<uint64_t> valid;
-    valid.reserve(kQSample);
-    for (int i = 0; i < kQSample; ++i)
-        if (sok[i]) valid.push_back(sk[i]);
+    valid.reserve((size_t)kQSample * ns_dev);
+    for (int i = 0; i < ns_dev; ++i)
+        for (int j = 0; j < kQSample && sh[i].nrows; ++j)
+            if (sh[i].sok[j]) valid.push_back(sh[i].sk[j]);
     std::sort(valid.begin(), valid.end());
     std::vector<uint64_t> spl(kQBuckets, ~0ULL);  // entry kQBuckets-1 stays +inf (no key reaches it)
     const size_t m = valid.size();
     if (m > 0)
         for (int j = 0; j < kQBuckets - 1; ++j) spl[j] = valid[(size_t)(j + 1) * m / kQBuckets < m ? (size_t)(j + 1) * m / kQBuckets : m - 1];
-    uint64_t* dspl = nullptr;
-    QT_HIP(ctx, buf.alloc((void**)&dspl, sizeof(uint64_t) * kQBuckets));
-    QT_HIP(ctx, hipMemcpyAsync(dspl, spl.data(), sizeof(uint64_t) * kQBuckets, hipMemcpyHostToDevice, s));
 
-    // ---- 2. histogram ----------------------------------------------------------------------------
-    unsigned long long *dhist = nullptr, *deq = nullptr;
-    QT_HIP(ctx, buf.alloc((void**)&dhist, sizeof(unsigned long long) * kQBuckets * 2));
-    deq = dhist + kQBuckets;
-    QT_HIP(ctx, hipMemsetAsync(dhist, 0, sizeof(unsigned long long) * kQBuckets * 2, s));
-    const int64_t lanes_needed = (nrows + kQRowsPerLane - 1) / kQRowsPerLane;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((lanes_needed + kQBlock - 1) / kQBlock,
-                                                                 (int64_t)dq::ctx_cus(ctx) * 2));
-    hipLaunchKernelGGL(q_hist_kernel, dim3(grid), dim3(kQBlock), 0, s, qc, nrows, (const uint64_t*)dspl, dhist, deq);
-    QT_HIP(ctx, hipGetLastError());
-    std::vector<unsigned long long> hist(kQBuckets * 2);
-    QT_HIP(ctx, hipMemcpyAsync(hist.data(), dhist, sizeof(unsigned long long) * kQBuckets * 2, hipMemcpyDeviceToHost, s));
-    QT_HIP(ctx, hipStreamSynchronize(s));
+    // ---- 2. histogram per shard, added on the host ------------------------------------------------
+    for (QShard& q : sh) {
+        if (!q.nrows) continue;
+        QS_HIP(ctx, hipSetDevice(dq::ctx_device(q.ctx)));
+        hipStream_t s = dq::ctx_stream(q.ctx);
+        QS_HIP(ctx, q.buf.alloc((void**)&q.dspl, sizeof(uint64_t) * kQBuckets));
+        QS_HIP(ctx, hipMemcpyAsync(q.dspl, spl.data(), sizeof(uint64_t) * kQBuckets, hipMemcpyHostToDevice, s));
+        QS_HIP(ctx, q.buf.alloc((void**)&q.dhist, sizeof(unsigned long long) * kQBuckets * 2));
+        QS_HIP(ctx, hipMemsetAsync(q.dhist, 0, sizeof(unsigned long long) * kQBuckets * 2, s));
+        const int64_t lanes_needed = (q.nrows + kQRowsPerLane - 1) / kQRowsPerLane;
+        q.grid = (int)std::max<int64_t>(1, std::min<int64_t>((lanes_needed + kQBlock - 1) / kQBlock,
+                                                             (int64_t)dq::ctx_cus(q.ctx) * 2));
+        hipLaunchKernelGGL(q_hist_kernel, dim3(q.grid), dim3(kQBlock), 0, s, q.qc, q.nrows, (const uint64_t*)q.dspl,
+                           q.dhist, q.dhist + kQBuckets);
+        QS_HIP(ctx, hipGetLastError());
+        q.hist.assign(kQBuckets * 2, 0);
+        QS_HIP(ctx, hipMemcpyAsync(q.hist.data(), q.dhist, sizeof(unsigned long long) * kQBuckets * 2,
+                                   hipMemcpyDeviceToHost, s));
+    }
+    std::vector<unsigned long long> hist(kQBuckets * 2, 0);
+    for (QShard& q : sh) {
+        if (!q.nrows) continue;
+        QS_HIP(ctx, hipSetDevice(dq::ctx_device(q.ctx)));
+        QS_HIP(ctx, hipStreamSynchronize(dq::ctx_stream(q.ctx)));
+        for (int b = 0; b < kQBuckets * 2; ++b) hist[b] += q.hist[b];
+    }
     const unsigned long long* eq = hist.data() + kQBuckets;
     int64_t n = 0;
     for (int b = 0; b < kQBuckets; ++b) n += (int64_t)hist[b];
@@ -348,6 +423,7 @@ int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows,
         rank_resid[i] = resid;
         ranks_out[i] = r;
     }
+    // global bucket segments of the sorted candidates; per shard, its own bucket-contiguous layout
     std::vector<unsigned long long> cursor(kQBuckets, 0);
     int64_t ncand = 0;
     for (int b = 0; b < kQBuckets; ++b) {
@@ -358,26 +434,53 @@ int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows,
     }
     if (ncand == 0) return ns;
 
-    // ---- 4. compaction ---------------------------------------------------------------------------
-    uint32_t* dtarget = nullptr;
-    unsigned long long* dcursor = nullptr;
-    uint64_t *dcand = nullptr, *dsorted = nullptr;
-    QT_HIP(ctx, buf.alloc((void**)&dtarget, sizeof(uint32_t) * kQBuckets));
-    QT_HIP(ctx, buf.alloc((void**)&dcursor, sizeof(unsigned long long) * kQBuckets));
-    QT_HIP(ctx, buf.alloc((void**)&dcand, sizeof(uint64_t) * ncand));
-    QT_HIP(ctx, buf.alloc((void**)&dsorted, sizeof(uint64_t) * ncand));
-    QT_HIP(ctx, hipMemcpyAsync(dtarget, target.data(), sizeof(uint32_t) * kQBuckets, hipMemcpyHostToDevice, s));
-    QT_HIP(ctx, hipMemcpyAsync(dcursor, cursor.data(), sizeof(unsigned long long) * kQBuckets, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(q_compact_kernel, dim3(grid), dim3(kQBlock), 0, s, qc, nrows, (const uint64_t*)dspl,
-                       (const uint32_t*)dtarget, dcursor, dcand);
-    QT_HIP(ctx, hipGetLastError());
+    // ---- 4. compaction per shard, candidates gathered on the first shard's device ------------------
+    QShard& s0 = sh[0];
+    uint64_t *dall = nullptr, *dsorted = nullptr;
+    QS_HIP(ctx, hipSetDevice(dq::ctx_device(s0.ctx)));
+    QS_HIP(ctx, s0.buf.alloc((void**)&dall, sizeof(uint64_t) * ncand));
+    QS_HIP(ctx, s0.buf.alloc((void**)&dsorted, sizeof(uint64_t) * ncand));
+    int64_t at = 0;
+    for (QShard& q : sh) {
+        if (!q.nrows) continue;
+        std::vector<unsigned long long> lcur(kQBuckets, 0);
+        int64_t nloc = 0;
+        for (int b = 0; b < kQBuckets; ++b) {
+            if (target[b] == kQNoTarget) continue;
+            lcur[b] = (unsigned long long)nloc;
+            nloc += (int64_t)q.hist[b] - (b > 0 ? (int64_t)q.hist[kQBuckets + b] : 0);
+        }
+        q.ncand = nloc;
+        if (nloc == 0) continue;
+        QS_HIP(ctx, hipSetDevice(dq::ctx_device(q.ctx)));
+        hipStream_t s = dq::ctx_stream(q.ctx);
+        QS_HIP(ctx, q.buf.alloc((void**)&q.dtarget, sizeof(uint32_t) * kQBuckets));
+        QS_HIP(ctx, q.buf.alloc((void**)&q.dcursor, sizeof(unsigned long long) * kQBuckets));
+        QS_HIP(ctx, q.buf.alloc((void**)&q.dcand, sizeof(uint64_t) * nloc));
+        QS_HIP(ctx, hipMemcpyAsync(q.dtarget, target.data(), sizeof(uint32_t) * kQBuckets, hipMemcpyHostToDevice, s));
+        QS_HIP(ctx, hipMemcpyAsync(q.dcursor, lcur.data(), sizeof(unsigned long long) * kQBuckets, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(q_compact_kernel, dim3(q.grid), dim3(kQBlock), 0, s, q.qc, q.nrows, (const uint64_t*)q.dspl,
+                           (const uint32_t*)q.dtarget, q.dcursor, q.dcand);
+        QS_HIP(ctx, hipGetLastError());
+        QS_HIP(ctx, hipMemcpyPeerAsync(dall + at, dq::ctx_device(s0.ctx), q.dcand, dq::ctx_device(q.ctx),
+                                       sizeof(uint64_t) * nloc, s));
+        at += nloc;
+    }
+    for (QShard& q : sh) {
+        if (!q.ncand) continue;
+        QS_HIP(ctx, hipSetDevice(dq::ctx_device(q.ctx)));
+        QS_HIP(ctx, hipStreamSynchronize(dq::ctx_stream(q.ctx)));
+    }
+    if (at != ncand) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_quantile_summary: candidate count mismatch");
 
-    // ---- 5. sort the candidates (bucket segments are already in key order) ----------------------
+    // ---- 5. sort all candidates (bucket segments follow key order) --------------------------------
+    QS_HIP(ctx, hipSetDevice(dq::ctx_device(s0.ctx)));
+    hipStream_t s = dq::ctx_stream(s0.ctx);
     size_t tmp_bytes = 0;
-    QT_HIP(ctx, rocprim::radix_sort_keys(nullptr, tmp_bytes, dcand, dsorted, (size_t)ncand, 0, 64, s));
+    QS_HIP(ctx, rocprim::radix_sort_keys(nullptr, tmp_bytes, dall, dsorted, (size_t)ncand, 0, 64, s));
     void* dtmp = nullptr;
-    QT_HIP(ctx, buf.alloc(&dtmp, tmp_bytes));
-    QT_HIP(ctx, rocprim::radix_sort_keys(dtmp, tmp_bytes, dcand, dsorted, (size_t)ncand, 0, 64, s));
+    QS_HIP(ctx, s0.buf.alloc(&dtmp, tmp_bytes));
+    QS_HIP(ctx, rocprim::radix_sort_keys(dtmp, tmp_bytes, dall, dsorted, (size_t)ncand, 0, 64, s));
 
     // ---- 6. gather -------------------------------------------------------------------------------
     std::vector<int64_t> idx;
@@ -390,15 +493,15 @@ int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows,
     const int ng = (int)idx.size();
     int64_t* didx = nullptr;
     double* dvals = nullptr;
-    QT_HIP(ctx, buf.alloc((void**)&didx, sizeof(int64_t) * ng));
-    QT_HIP(ctx, buf.alloc((void**)&dvals, sizeof(double) * ng));
-    QT_HIP(ctx, hipMemcpyAsync(didx, idx.data(), sizeof(int64_t) * ng, hipMemcpyHostToDevice, s));
+    QS_HIP(ctx, s0.buf.alloc((void**)&didx, sizeof(int64_t) * ng));
+    QS_HIP(ctx, s0.buf.alloc((void**)&dvals, sizeof(double) * ng));
+    QS_HIP(ctx, hipMemcpyAsync(didx, idx.data(), sizeof(int64_t) * ng, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(q_gather_kernel, dim3((ng + 255) / 256), dim3(256), 0, s, (const uint64_t*)dsorted,
                        (const int64_t*)didx, ng, dvals);
-    QT_HIP(ctx, hipGetLastError());
+    QS_HIP(ctx, hipGetLastError());
     std::vector<double> got(ng);
-    QT_HIP(ctx, hipMemcpyAsync(got.data(), dvals, sizeof(double) * ng, hipMemcpyDeviceToHost, s));
-    QT_HIP(ctx, hipStreamSynchronize(s));
+    QS_HIP(ctx, hipMemcpyAsync(got.data(), dvals, sizeof(double) * ng, hipMemcpyDeviceToHost, s));
+    QS_HIP(ctx, hipStreamSynchronize(s));
     for (int j = 0; j < ng; ++j) values_out[which[j]] = got[j];
     return ns;
 }

@@ -1509,9 +1509,128 @@ __device__ __forceinline__ uint32_t heavy_tail(const ColDesc& c, int64_t t, int 
     return m;
 }
 
+// ---- `where` producer (WhereOut, dq_internal.h) ----------------------------------------------------------------------
+// The lane's 8 consecutive rows of one 8-byte column against one PredSimple term: TRUE / NOT-NULL row bytes (Spark
+// comparison: NaN = NaN and above every number for double compares, long compares for integral vs long constant).
+template <bool F>
+__device__ __forceinline__ void where_term8(const PredTerm& q, const uint64_t (&v)[8], uint32_t valid, uint32_t inr,
+                                            uint32_t& t, uint32_t& n) {
+    if (q.op == DQ_P_IS_NULL || q.op == DQ_P_IS_NOT_NULL) {
+        t = (q.op == DQ_P_IS_NULL ? ~valid : valid) & inr;
+        n = inr;
+        return;
+    }
+    const uint32_t truth = cmp_truth_mask(q.op);  // bit 0: <, bit 1: =, bit 2: >
+    uint32_t hit = 0;
+    if (!F && !q.dbl) {
+        const int64_t y = q.ci;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t x = (int64_t)v[k];
+            const uint32_t sel = x < y ? 0u : (x > y ? 2u : 1u);
+            hit |= ((truth >> sel) & 1u) << k;
+        }
+    } else {
+        const double y = q.cd;
+        const bool yn = y != y;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double x = F ? as_f64(v[k]) : (double)(int64_t)v[k];
+            const bool xn = x != x;
+            const uint32_t sel = (xn || yn) ? ((xn && yn) ? 1u : (xn ? 2u : 0u)) : (x < y ? 0u : (x > y ? 2u : 1u));
+            hit |= ((truth >> sel) & 1u) << k;
+        }
+    }
+    n = valid & inr;
+    t = hit & n;
+}
+
+// The PredSimple postfix over 8-row bytes, SQL three-valued logic on a byte stack in two 64-bit registers (depth <=
+// kWhereStack, checked on the host). Returns TRUE bits in the low byte, NOT-NULL bits in the next.
+template <bool F>
+__device__ __forceinline__ uint32_t where_eval8(const PredSimple& P, const uint64_t (&v)[8], uint32_t valid,
+                                                uint32_t inr) {
+    uint64_t st = 0, sn = 0;
+    const int nb = P.nb;
+    for (int i = 0; i < nb; ++i) {  // wave-uniform
+        const int o = P.b[i];
+        if (o >= 0) {
+            uint32_t t, n;
+            where_term8<F>(P.t[o], v, valid, inr, t, n);
+            st = (st << 8) | t;
+            sn = (sn << 8) | n;
+        } else if (o == kPB_NOT) {
+            const uint64_t t = st & 0xFFu, n = sn & 0xFFu;
+            st = (st & ~0xFFull) | (n & ~t);
+        } else {
+            const uint64_t tc = st & 0xFFu, nc = sn & 0xFFu;
+            st >>= 8;
+            sn >>= 8;
+            const uint64_t ta = st & 0xFFu, na = sn & 0xFFu;
+            uint64_t rt, rn;
+            if (o == kPB_AND) {
+                const uint64_t f = (na & ~ta) | (nc & ~tc);  // a FALSE side decides
+                rt = ta & tc;
+                rn = f | (na & nc);
+            } else {
+                rt = ta | tc;
+                rn = rt | (na & nc);
+            }
+            st = (st & ~0xFFull) | rt;
+            sn = (sn & ~0xFFull) | rn;
+        }
+    }
+    return (uint32_t)(st & 0xFFu) | ((uint32_t)(sn & 0xFFu) << 8);
+}
+
+// Four lanes' row bytes -> one dword (rows 32 q .. 32 q + 31 of the tile) in every lane of the quad.
+__device__ __forceinline__ uint32_t quad_pack(uint32_t byte, int lane) {
+    uint32_t p = byte << (8 * (lane & 3));
+    p |= (uint32_t)__builtin_amdgcn_mov_dpp((int)p, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    p |= (uint32_t)__builtin_amdgcn_mov_dpp((int)p, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    return p;
+}
+
+// Bitmap bytes [b0, b0 + 4) of a user validity bitmap of exactly vbytes bytes (bounded in the tail tile).
+__device__ __forceinline__ uint32_t valid_dword(const uint64_t* vb, int64_t b0, int64_t vbytes, bool full) {
+    if (vb == nullptr) return 0xFFFFFFFFu;
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(vb);
+    if (full) return *reinterpret_cast<const uint32_t*>(b + b0);
+    uint32_t d = 0;
+    for (int i = 0; i < 4; ++i)
+        if (b0 + i < vbytes) d |= (uint32_t)b[b0 + i] << (8 * i);
+    return d;
+}
+
+// Writes the producer's outputs for tile t: per consumer valid & where TRUE, and the where bitmaps if asked for.
+__device__ __forceinline__ void where_emit(const WhereOut* __restrict__ wo, int64_t t, int tid, uint32_t w, uint32_t wn,
+                                           bool full, int64_t vbytes) {
+    const int lane = tid & 63;
+    const uint32_t pw = quad_pack(w, lane);
+    const uint32_t pn = quad_pack(wn, lane);
+    if ((lane & 3) != 0) return;
+    const int64_t b0 = t * (kTileRows / 8) + tid;  // this quad's first bitmap byte
+    const int nm = wo->nmasks;
+    // 8 consumers at a time: their validity loads are all in flight before the first store waits on one
+    for (int m0 = 0; m0 < nm; m0 += 8) {  // wave-uniform
+        uint32_t vd[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) vd[k] = m0 + k < nm ? valid_dword(wo->valid[m0 + k], b0, vbytes, full) : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (m0 + k < nm) *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->mask[m0 + k]) + b0) = vd[k] & pw;
+    }
+    if (wo->bitmaps) {
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->where_t) + b0) = pw;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->where_nn) + b0) = pn;
+    }
+}
+
 // FULL: every column has stats, moments, HLL and a fast fused compare, pairs have the correlation, no `where`
 // (the north-star suite) — the per-flag branches compile away.
-template <int NC, bool F0, bool F1, bool FULL>
+// WP (NC == 1): the slot is a `where` producer (sd.wout): its column's values and validity evaluate the filter, the
+// filter masks the slot's own rows and goes out as consumer masks (where_emit).
+template <int NC, bool F0, bool F1, bool FULL, bool WP = false>
 __global__ void __launch_bounds__(kBlock, 1)
 scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__ group, int ngroup, int64_t nrows,
                    int64_t ntiles, int gstride, SlotPartial* __restrict__ partials, uint8_t* __restrict__ hll_partials) {
@@ -1530,7 +1649,9 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
         const HeavyCol h0 = heavy_col_of(c0, F0);
         const HeavyCol h1 = heavy_col_of(c1, F1);
         const bool corr = NC > 1 && (FULL || sd.corr);
-        const bool has_where = !FULL && sd.where_t != nullptr;
+        const bool has_where = WP || (!FULL && sd.where_t != nullptr);
+        const WhereOut* __restrict__ wo = sd.wout;
+        const int64_t vbytes = (nrows + 7) >> 3;
         const bool need0 = corr || h0.stats || h0.moments || c0.pred_kind != FP_NONE;
         const bool need1 = corr || h1.stats || h1.moments || c1.pred_kind != FP_NONE;
         A0 a0;
@@ -1574,7 +1695,7 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                 heavy_load(c1, t, tid, y);
                 by = heavy_bits(c1.validity, t, tid);
             }
-            if (has_where) {
+            if (has_where && !WP) {
                 bw = heavy_bits(sd.where_t, t, tid);
                 bn = heavy_bits(sd.where_nn, t, tid);
             }
@@ -1590,10 +1711,16 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                     heavy_load(c1, tn, tid, yn);
                     nby = heavy_bits(c1.validity, tn, tid);
                 }
-                if (has_where) {
+                if (has_where && !WP) {
                     nbw = heavy_bits(sd.where_t, tn, tid);
                     nbn = heavy_bits(sd.where_nn, tn, tid);
                 }
+            }
+            if constexpr (WP) {
+                const uint32_t e = where_eval8<F0>(wo->prog, x, bx, 0xFFu);
+                bw = e & 0xFFu;
+                bn = e >> 8;
+                where_emit(wo, t, tid, bw, bn, true, vbytes);
             }
             fold(x, y, bx, by, bw, bn);
 #pragma unroll
@@ -1616,7 +1743,12 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                 const bool in = r < nrows;
                 w |= (in ? 1u : 0u) << k;
             }
-            if (has_where) {
+            if (WP) {
+                const uint32_t e = where_eval8<F0>(wo->prog, x, mx, w);
+                wn = e >> 8;
+                w = e & 0xFFu;
+                where_emit(wo, nfull, tid, w, wn, false, vbytes);
+            } else if (has_where) {
                 wn = w & heavy_bits(sd.where_nn, nfull, tid);
                 w &= heavy_bits(sd.where_t, nfull, tid);
             } else {
@@ -1799,8 +1931,14 @@ __global__ void finalize_kernel(const OpMap* __restrict__ ops, int nops, const S
     const ColPartial& c = sp.c[om.colpos > 0 ? 1 : 0];
     // conditionalCount(where) (A/Analyzer.scala:426-432): count(*), or sum(cast(where AS long)),
     // which is NULL when no row has a non-null `where` value.
-    const int64_t cond_count = om.has_where ? sp.wt : om.nrows;
-    const bool cond_count_present = om.has_where ? (sp.wnn > 0) : true;
+    // The where counts live in the op's own slot, or in the slot of the filter's producer (masked `where`).
+    int64_t wt = sp.wt, wnn = sp.wnn;
+    if (om.has_where && om.wslot >= 0 && om.wslot != om.slot) {
+        wt = finals[om.wslot].wt;
+        wnn = finals[om.wslot].wnn;
+    }
+    const int64_t cond_count = om.has_where ? wt : om.nrows;
+    const bool cond_count_present = om.has_where ? (wnn > 0) : true;
     const double scale = om.decimal_scale > 0 ? pow10i(om.decimal_scale) : 1.0;
     switch (om.kind) {
         case DQ_OP_SIZE:
@@ -1892,6 +2030,11 @@ static const void* values_kernel_ptr(int heavy) {
 static const void* values_kernel_for(int P, int nc, bool f0, bool f1, int heavy) {
     // 8-byte columns: HEAVY slots and Correlation pairs take the lean kernel (heavy == 2: every flag on, no `where`);
     // the striped kernel's pair instantiation runs at 1 wave / SIMD (255 VGPRs), this one at 2
+    if (heavy == 3) {  // `where` producer over one 8-byte column
+        if (P != 2 || nc != 1 || f1) return nullptr;
+        return f0 ? reinterpret_cast<const void*>(&scan_heavy8_kernel<1, true, false, false, true>)
+                  : reinterpret_cast<const void*>(&scan_heavy8_kernel<1, false, false, false, true>);
+    }
     if ((heavy || nc == 2) && P == 2) {
 #define DQ_HK(n, a, b) \
     if (nc == n && f0 == a && f1 == b) \

@@ -119,6 +119,7 @@ class FrequencyTable:
         if key_type is None and self.key_columns:
             key_type, decimal_scale = self.key_columns[0].spark_type, self.key_columns[0].decimal_scale
         self.key_type, self.decimal_scale = key_type, decimal_scale
+        self.weights = None  # per source row counts of a weighted build (dq_frequencies_ex)
         s = self.summary(None)
         self.num_rows = s["num_rows"]
         self.num_groups = s["num_groups"]
@@ -286,4 +287,6 @@ def frequencies(table, key_columns, include_nulls=False, weights=None):
         rc = context.lib.dq_frequencies_ex(context.handle, arr, len(cols), table.nrows, keys.ctypes.data, len(keys),
                                            ctypes.byref(opt), ctypes.byref(handle))
     context.check(rc, "dq_frequencies")
-    return FrequencyTable(context, handle, table, key_columns, include_nulls)
+    ft = FrequencyTable(context, handle, table, key_columns, include_nulls)
+    ft.weights = None if weights is None else w
+    return ft

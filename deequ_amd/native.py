@@ -279,6 +279,7 @@ class Context:
             raise NativeError(status.value, "dq_open(%r) failed: a MI355X GPU is required" % (devices or device))
         self.device = device
         self.devices = list(devices) if devices is not None else [device]
+        self.multi = devices is not None  # dq_open_devices: host columns in, host results out
 
     def num_devices(self):
         return self.lib.dq_ctx_num_devices(self.handle)

@@ -148,10 +148,17 @@ def _cast_column(data, name, to_type):
             (to_type == N.TYPE_DOUBLE and t in (N.TYPE_FLOAT, N.TYPE_DOUBLE)):
         return col
     n = data.nrows
+    ctx = engine.ctx()
+    if ctx.multi:  # a multi-device context casts each device's row shard into host buffers (include/dq.h)
+        import numpy as np
+        vals = np.empty(max(n, 1), dtype=np.float64 if to_type == N.TYPE_DOUBLE else np.int64)
+        mask = np.zeros(max((n + 63) // 64, 1) * 8, dtype=np.uint8)
+        ctx.cast_column(col.native(), n, to_type, vals.ctypes.data, mask.ctypes.data)
+        return Column(name, to_type, vals[:n], mask[:(n + 7) // 8], length=n)
     dev = torch.device("cuda", engine.device())
     vals = torch.empty(max(n, 1), dtype=torch.float64 if to_type == N.TYPE_DOUBLE else torch.int64, device=dev)
     mask = torch.zeros(max((n + 63) // 64, 1) * 8, dtype=torch.uint8, device=dev)
-    engine.ctx().cast_column(col.native(), n, to_type, vals.data_ptr(), mask.data_ptr())
+    ctx.cast_column(col.native(), n, to_type, vals.data_ptr(), mask.data_ptr())
     out = Column(name, to_type, None, None, length=n)
     out.device = {"values": vals, "validity": mask}
     return out

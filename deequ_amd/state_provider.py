@@ -200,6 +200,8 @@ class HdfsStateProvider:
             shutil.rmtree(path) if os.path.isdir(path) else os.remove(path)
         tbl = _pairs_table(state)
         if tbl is None:
+            tbl = _block_table(state)
+        if tbl is None:
             freq = state.as_dict()
             columns = list(state.columns) if state.columns else \
                 ["c%d" % i for i in range(len(next(iter(freq))) if freq else 1)]
@@ -225,6 +227,9 @@ class HdfsStateProvider:
         pairs = _load_pairs(path, files, num_rows)
         if pairs is not None:
             return pairs
+        block = _load_block(path, files, num_rows)
+        if block is not None:
+            return block
         freq = {}
         columns = None
         for f in files:
@@ -280,6 +285,52 @@ def _pairs_table(state):
         counts = np.append(counts, np.int64(nulls))
     name = (list(state.columns) or ["c0"])[0]
     return pa.Table.from_arrays([vals, pa.array(counts, type=pa.int64())], names=[name, COUNT_COL])
+
+
+def _block_table(state):
+    """The parquet table of a state whose groups are a GroupBlock (string / multi-column keys: key columns + the
+    count column, built from the column buffers, no per-group Python); a merged block (keys may repeat) is first
+    aggregated by its weighted GPU build. None for other states."""
+    import pyarrow as pa
+    from . import groups as G
+    from .table import column_to_arrow
+    f = state.frequencies
+    if isinstance(f, G.GroupBlock) and not getattr(f, "distinct", False):
+        ft = state.device_table()
+        keys, counts = ft.export_raw()
+        f = G.GroupBlock([G.take(c, keys) for c in f.columns], counts)
+    elif not isinstance(f, G.GroupBlock):
+        if not isinstance(f, engine.FrequencyTable) or f.key_kind() == N.FREQ_KEYS_VALUES:
+            return None
+        f = state.group_block()
+        if f is None:
+            return None
+    arrays = [column_to_arrow(c, pa) for c in f.columns]
+    return pa.Table.from_arrays(arrays + [pa.array(f.counts, type=pa.int64())], names=f.names + [COUNT_COL])
+
+
+def _load_block(path, files, num_rows):
+    """A persisted state of any key shape as a GroupBlock (Arrow buffers -> columns, vectorised); its groups are
+    distinct, and the weighted GPU build behind its metrics reads them with their counts."""
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from . import groups as G
+    from .table import Table
+    if not files:
+        return None
+    t = pa.concat_tables([pq.read_table(os.path.join(path, f)) for f in files])
+    keys = [n for n in t.column_names if n != COUNT_COL]
+    if COUNT_COL not in t.column_names or not keys:
+        return None
+    try:
+        kt = Table.from_arrow(t.select(keys))
+    except ValueError:
+        return None
+    counts = np.asarray(t.column(COUNT_COL).combine_chunks().to_numpy(zero_copy_only=False), dtype=np.int64)
+    block = G.GroupBlock([kt[k] for k in keys], counts, int(counts.sum()), 0)
+    block.distinct = True
+    return A.FrequenciesAndNumRows(block, num_rows, keys)
 
 
 def _load_pairs(path, files, num_rows):

@@ -231,6 +231,34 @@ def _column_from_arrow(name, arr, pa):
     return Column(name, spark, vals, validity)
 
 
+def column_to_arrow(col, pa):
+    """A host column -> pyarrow array of its Spark type (inverse of _column_from_arrow), from the buffers."""
+    n = col.length
+    valid = unpack_validity(col.validity, n)
+    mask = None if valid.all() else ~valid
+    vbuf = None if mask is None else pa.py_buffer(np.packbits(valid, bitorder="little").tobytes())
+    t = col.spark_type
+    if t == N.TYPE_STRING:
+        off = np.ascontiguousarray(np.asarray(col.offsets, dtype=np.int32)[:n + 1])
+        data = np.ascontiguousarray(np.asarray(col.values, dtype=np.uint8)[:int(off[-1]) if n else 0])
+        return pa.Array.from_buffers(pa.string(), n, [vbuf, pa.py_buffer(off.tobytes()), pa.py_buffer(data.tobytes())],
+                                     null_count=-1)
+    if t == N.TYPE_BOOLEAN:
+        return pa.array(np.asarray(col.values)[:n] != 0, mask=mask)
+    if t == N.TYPE_DATE:
+        return pa.array(np.asarray(col.values, dtype=np.int32)[:n], type=pa.int32(), mask=mask).cast(pa.date32())
+    if t == N.TYPE_TIMESTAMP:
+        return pa.array(np.asarray(col.values, dtype=np.int64)[:n], type=pa.int64(), mask=mask).cast(pa.timestamp("us"))
+    if t == N.TYPE_DECIMAL:
+        u = np.asarray(col.values, dtype=np.int64)[:n]
+        cells = np.empty(2 * n, dtype=np.int64)
+        cells[0::2] = u
+        cells[1::2] = np.where(u < 0, -1, 0)
+        return pa.Array.from_buffers(pa.decimal128(max(col.decimal_precision, 1), col.decimal_scale), n,
+                                     [vbuf, pa.py_buffer(cells.tobytes())], null_count=-1)
+    return pa.array(np.asarray(col.values, dtype=NUMPY_OF[t])[:n], mask=mask)
+
+
 class Table:
     """Named columns of equal length (the DataFrame stand-in of the drop-in API)."""
 

@@ -212,7 +212,10 @@ const char* dq_last_error(const dq_ctx* ctx);
  * over RCCL (ncclSend / ncclRecv all-to-all over xGMI), so each group lives on exactly one device. The context
  * owns one RCCL communicator per device (ncclCommInitAll) when the devices are distinct; a repeated device
  * (several shards on one GPU, e.g. to test the sharded path on one card) moves the groups with device copies
- * instead. ndev == 1 runs the same sharded path with one shard. ApproxQuantile / KLL / casts run on the first device. */
+ * instead. ndev == 1 runs the same sharded path with one shard. dq_quantile_summary runs its selection passes on every
+ * device's shard and returns the order statistics of the whole column (the same samples as one device); dq_kll_sketch
+ * sketches one partition per device and merges them in device order (QuantileNonSample.merge, as KLLRunner's reduce
+ * over partitions, R/KLLRunner.scala:104-112); dq_cast_column casts every device's shard into HOST result buffers. */
 dq_ctx* dq_open_devices(const int* devices, int ndev, int* status);
 int dq_ctx_num_devices(const dq_ctx* ctx);
 int dq_ctx_uses_rccl(const dq_ctx* ctx);   /* 1 when the context's exchange runs over RCCL */
@@ -329,7 +332,8 @@ int dq_freq_merge(dq_ctx* ctx, const dq_freq_table* a, const dq_freq_table* b, d
 /* MutualInformation.computeMetricFrom (A/MutualInformation.scala:35-97): joint = the (x, y) table, x / y = the
  * single-column tables of the same rows (their counts are the marginals of the joint table's non-NULL keys).
  * *mi = sum over joint groups with both keys non-NULL of (pxy/N) ln((pxy/N) / ((px/N)(py/N))), N = joint numRows;
- * *present = 0 when no group joins (the reference's NULL sum -> empty state). */
+ * *present = 0 when no group joins (the reference's NULL sum -> empty state). The three tables are built over the
+ * same rows: all unweighted, or all weighted by the same per-row counts (dq_frequencies_ex over a state's groups). */
 int dq_freq_mutual_information(dq_ctx* ctx, const dq_freq_table* joint, const dq_freq_table* x,
                                const dq_freq_table* y, double* mi, int32_t* present);
 
@@ -370,7 +374,8 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
  * DECIMAL(p <= 18) -> Decimal.toLong (truncating) / Decimal.toDouble, BOOLEAN -> 0/1. values_dev receives nrows x 8 B,
  * validity_dev ceil(nrows / 64) x 8 B (LSB-first bitmap); both device memory, 8-B aligned. Returns DQ_OK, or
  * DQ_ERR_UNSUPPORTED when a string needs Double.parseDouble's arbitrary-precision path (hexadecimal literal, or
- * more than 19 significant digits on a rounding boundary) — never a silent guess. */
+ * more than 19 significant digits on a rounding boundary) — never a silent guess. On a multi-device context
+ * (dq_open_devices) the column is a host column and values_dev / validity_dev are HOST buffers of the same sizes. */
 int dq_cast_column(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t to_type, void* values_dev,
                    uint8_t* validity_dev);
 
