@@ -835,7 +835,7 @@ def _eval(node, row):
 def predicate_masks(table, text):
     """(TRUE mask, NOT-NULL mask) of a SQL predicate over every row."""
     tree = OracleParser(text).parse()
-    cols = {n: table[n].to_pylist() for n in table.columns}
+    cols = {n: _pylist(table[n]) for n in table.columns}
     t = np.zeros(table.nrows, dtype=bool)
     nn = np.zeros(table.nrows, dtype=bool)
     for i in range(table.nrows):
@@ -845,10 +845,54 @@ def predicate_masks(table, text):
     return t, nn
 
 
-# ---- expected states per analyzer ---------------------------------------------------------------
+# ---- the oracle's own reading of a column's Arrow-style buffers (never the product's decoders) ----------
+def _host_buffer(col, key):
+    """A column buffer as numpy: host arrays as they are; a device-resident column's buffer copied back."""
+    v = getattr(col, {"values": "values", "validity": "validity", "offsets": "offsets"}[key])
+    if v is None and getattr(col, "device", None):
+        d = col.device.get(key)
+        v = None if d is None else d.cpu().numpy()
+    return v
+
+
 def _valid(col):
-    from deequ_amd.table import unpack_validity
-    return unpack_validity(col.validity, col.length)
+    """Validity: bit (i mod 8) of byte (i div 8), LSB first; no bitmap = every row valid."""
+    n = col.length
+    vb = _host_buffer(col, "validity")
+    if vb is None:
+        return np.ones(n, dtype=bool)
+    b = np.frombuffer(bytes(np.asarray(vb, dtype=np.uint8)[:(n + 7) // 8]), dtype=np.uint8)
+    i = np.arange(n, dtype=np.int64)
+    return ((b[i >> 3] >> (i & 7).astype(np.uint8)) & 1).astype(bool)
+
+
+def _cell(col, i):
+    """Row i's value as a Python object: UTF-8 text between offsets[i] and offsets[i + 1], or the fixed-width cell
+    read as its Spark type (BOOLEAN a byte, DECIMAL the unscaled long / 10^scale)."""
+    t = col.spark_type
+    vals = _host_buffer(col, "values")
+    if t == T_STRING:
+        off = _host_buffer(col, "offsets")
+        a, b = int(off[i]), int(off[i + 1])
+        return bytes(np.asarray(vals, dtype=np.uint8)[a:b]).decode("utf-8")
+    width = {T_BOOLEAN: 1, T_BYTE: 1, T_SHORT: 2, T_INT: 4, T_DATE: 4, T_FLOAT: 4}.get(t, 8)
+    raw = np.asarray(vals).view(np.uint8)[i * width:(i + 1) * width].tobytes()
+    if t == T_BOOLEAN:
+        return raw != b"\x00"
+    if t == T_FLOAT:
+        return float(np.frombuffer(raw, dtype="<f4")[0])
+    if t == T_DOUBLE:
+        return float(np.frombuffer(raw, dtype="<f8")[0])
+    x = int.from_bytes(raw, "little", signed=True)
+    return x / (10 ** col.decimal_scale) if t == T_DECIMAL else x
+
+
+def _pylist(col):
+    valid = _valid(col)
+    return [_cell(col, i) if valid[i] else None for i in range(col.length)]
+
+
+# ---- expected states per analyzer ---------------------------------------------------------------
 
 
 def _where(table, where):
@@ -967,7 +1011,7 @@ def expected_state(table, analyzer, exact=True):
         c = table[analyzer.column]
         wt, _ = _where(table, analyzer.where)
         m = _valid(c) & wt
-        lens = [len(c.value_at(i)) for i in range(c.length) if m[i]]
+        lens = [len(_cell(c, i)) for i in range(c.length) if m[i]]
         if not lens:
             return None
         return S.MinState(float(min(lens))) if name == "MinLength" else S.MaxState(float(max(lens)))
@@ -1054,7 +1098,7 @@ def spark_cast_to_string(col, i):
     from decimal import Decimal
     t = col.spark_type
     if t == T_STRING:
-        return col.value_at(i)
+        return _cell(col, i)
     v = col.values[i]
     if t == T_BOOLEAN:
         return "true" if v else "false"
@@ -1092,7 +1136,7 @@ def java_bigdecimal_to_string(unscaled, scale):
 def frequencies(table, columns, include_nulls=False):
     """computeFrequencies: {key tuple: count} over rows with >= 1 non-null key (all rows if
     include_nulls, Histogram semantics), plus numRows."""
-    cols = [table[c].to_pylist() for c in columns]
+    cols = [_pylist(table[c]) for c in columns]
     freq = {}
     nrows = 0
     for i in range(table.nrows):
@@ -1382,7 +1426,7 @@ def expected_profile(table, threshold=120):
         p = {"completeness": int(valid.sum()) / n}
         p["approx_distinct"] = int(hll_count([int(w) for w in _hll_words_of(table, name)]))
         if c.spark_type == T_STRING:
-            py = c.to_pylist()
+            py = _pylist(c)
             cache, counts = {}, {"Unknown": 0, "Fractional": 0, "Integral": 0, "Boolean": 0, "String": 0}
             names = {1: "Fractional", 2: "Integral", 3: "Boolean", 4: "String"}
             for v in py:
@@ -1404,7 +1448,7 @@ def expected_profile(table, threshold=120):
             if c.spark_type == T_STRING:
                 conv = spark_string_to_long if p["dataType"] == "Integral" else java_parse_double
                 cache, vals = {}, []
-                for v in c.to_pylist():
+                for v in _pylist(c):
                     if v is None:
                         continue
                     if v not in cache:
