@@ -161,11 +161,16 @@ def bench_c3(torch, N, D, ctx, stream, dev, total, steps, dist=None, world=1, ra
     el, kms, _ = timed(torch, dist, world, steps, 1, stream, w.step)
     bpr = 3 * (8 + 1 / 8)
     ach = bpr * nrows / (kms * 1e-3) / 1e9
-    return {"workload": "C3: ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 3 cols x 1e9 rows, 1%% nulls, "
-                        "rows sharded over %d GPU(s), states all-gathered (RCCL) and folded in rank order" % world,
+    c3_traffic = committed_json("c3_traffic_*.json", nrows) if world == 1 else None
+    return {"workload": "C3: ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 3 cols x %d rows, 1%% nulls, "
+                        "rows sharded over %d GPU(s), states all-gathered (RCCL) and folded in rank order"
+                        % (total, world),
             "value": total / (el / steps), "unit": "rows/s", "ms_per_step": el / steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "frac": ach / PEAK_HBM_GBPS,
+                         "traffic": c3_traffic[0]["traffic_bytes_per_call"] / 1e9 if c3_traffic else None,
+                         "traffic_unit": "GB per dq_scan call (rocprofv3 PMC, %s)" % (c3_traffic[1] if c3_traffic
+                                                                                      else "not measured"),
                          "kernel": "dq_scan avg %.3f ms (HIP events, this rank), %.3f B/row x %d rows per GPU"
                                    % (kms, bpr, nrows)}}
 
@@ -341,13 +346,17 @@ def bench_c5(torch, N, D, ctx, dev, rows, steps):
     types = {n: p.dataType for n, p in prof.profiles.items()}
     assert types["s_int"] == "Integral" and types["s_dec"] == "Fractional" and types["s_text0"] == "String", types
     ach = nbytes / el / 1e9
+    c5_traffic = committed_json("c5_traffic_*.json", rows)
     return {"workload": "C5 shard: ColumnProfiler passes 1-3 (Completeness, ApproxCountDistinct, DataType; Min / Max / "
                         "Mean / StdDev / Sum / KLL on 13 numeric and cast numeric-string columns; exact histograms of "
                         "%d low-cardinality columns) over %d rows x 20 columns (5 fp64, 5 int64, 10 UTF-8), 5%% nulls"
                         % (len(hist), rows),
             "value": rows / el, "unit": "rows/s", "ms_per_step": el * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": ach / PEAK_HBM_GBPS, "traffic": None,
+                         "frac": ach / PEAK_HBM_GBPS,
+                         "traffic": c5_traffic[0]["traffic_bytes_per_call"] / 1e9 if c5_traffic else None,
+                         "traffic_unit": "GB per profile (rocprofv3 PMC, %s)" % (c5_traffic[1] if c5_traffic
+                                                                                 else "not measured"),
                          "kernel": "end-to-end profile wall time; achieved = the table's bytes (%.1f GB: values, "
                                    "offsets, UTF-8 data, validity) once per profile" % (nbytes / 1e9)}}
 
@@ -444,6 +453,107 @@ def cpu_baseline(seconds, sample_rows, threads=None):
             "sample": "oracle_scan_spark over a %d-row x 8-col sample of the C2 columns in %d row partitions "
                       "(one host thread each), %.1f sample passes in %.1f s (Spark-order count/sum/min/max/"
                       "Welford; not deequ/Spark itself)" % (sample_rows, threads, rows / sample_rows, el)}
+
+
+def _timed_threads(seconds, threads, work):
+    """Run work(i) -> rows in `threads` host threads (ctypes releases the GIL) until `seconds` have passed;
+    (rows done, elapsed s)."""
+    import threading
+    done = [0] * threads
+    start = threading.Barrier(threads + 1)
+    deadline = [0.0]
+
+    def worker(i):
+        start.wait()
+        while True:
+            done[i] += work(i)
+            if time.perf_counter() >= deadline[0]:
+                break
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    t0 = time.perf_counter()
+    deadline[0] = t0 + seconds
+    start.wait()
+    for t in ts:
+        t.join()
+    return sum(done), time.perf_counter() - t0
+
+
+def _cpu_threads(threads=None):
+    if threads is None:
+        threads = min(16, int(os.environ.get("OMP_NUM_THREADS", 0)) or os.cpu_count() or 1)
+    return max(1, int(threads))
+
+
+def cpu_baseline_suite10(seconds, sample_rows, threads=None):
+    """CPU leg of the suite10 line: the oracle's Spark-order row loops (oracle_scan_suite10_col: count / Sum /
+    Min / Max / CentralMomentAgg / Compliance(c > 0) / HLL++ update per column; oracle_corr_spark per pair) over a
+    bounded sample of the C2 columns, one contiguous row partition per host thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    L = O.lib()
+    L.oracle_scan_suite10_col.restype = ctypes.c_int64
+    L.oracle_scan_suite10_col.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_void_p]
+    L.oracle_corr_spark.restype = ctypes.c_int64
+    L.oracle_corr_spark.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    threads = min(_cpu_threads(threads), sample_rows)
+    cols = []
+    for c, kind in enumerate(C2_KINDS):
+        v = O.synth_column(kind, SEED + c, 0, sample_rows)
+        m = O.synth_validity(SEED + 0x100 + c, 0, sample_rows, 10).astype(np.uint8)
+        cols.append((7 if kind in (1, 2, 3) else 5, v, m))
+    bounds = [sample_rows * i // threads for i in range(threads + 1)]
+    regs = [np.zeros(512, dtype=np.uint8) for _ in range(threads)]
+    outs = [np.zeros(6) for _ in range(threads)]
+
+    def work(i):
+        lo, hi = bounds[i], bounds[i + 1]
+        for st, v, m in cols:
+            L.oracle_scan_suite10_col(st, v[lo:].ctypes.data, m[lo:].ctypes.data, hi - lo, regs[i].ctypes.data,
+                                      outs[i].ctypes.data)
+        for k in range(4):
+            (tx, x, mx), (ty, y, my) = cols[2 * k], cols[2 * k + 1]
+            L.oracle_corr_spark(tx, x[lo:].ctypes.data, mx[lo:].ctypes.data, ty, y[lo:].ctypes.data, my[lo:].ctypes.data,
+                                hi - lo, outs[i].ctypes.data)
+        return hi - lo
+
+    rows, el = _timed_threads(seconds, threads, work)
+    return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": "oracle_scan_suite10_col x 8 + oracle_corr_spark x 4 over a %d-row sample of the C2 columns in %d "
+                      "row partitions (one host thread each), %.1f sample passes in %.1f s (Spark-order row updates "
+                      "incl. XXH64 + HLL++; not deequ/Spark itself)" % (sample_rows, threads, rows / sample_rows, el)}
+
+
+def cpu_baseline_c4(seconds, sample_rows, threads=None):
+    """CPU leg of the C4 line: count(*) GROUP BY key as a per-partition open-addressing hash aggregate
+    (oracle_count_keys) over a bounded sample of the C4 keys, one partition per host thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    L = O.lib()
+    L.oracle_count_keys.restype = ctypes.c_int64
+    L.oracle_count_keys.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    threads = min(_cpu_threads(threads), sample_rows)
+    keys = O.synth_freq_keys(1_000_000_000, 100_000_000, 0, sample_rows)
+    bounds = [sample_rows * i // threads for i in range(threads + 1)]
+    per = max(bounds[i + 1] - bounds[i] for i in range(threads))
+    cap = 1 << max(4, int(per * 2 - 1).bit_length())
+    tables = [np.zeros(2 * cap, dtype=np.int64) for _ in range(threads)]
+    used = [np.zeros(cap, dtype=np.uint8) for _ in range(threads)]
+
+    def work(i):
+        lo, hi = bounds[i], bounds[i + 1]
+        L.oracle_count_keys(keys[lo:].ctypes.data, hi - lo, tables[i].ctypes.data, used[i].ctypes.data, cap)
+        return hi - lo
+
+    rows, el = _timed_threads(seconds, threads, work)
+    return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": "oracle_count_keys (open-addressing count(*) GROUP BY key per partition) over the first %d C4 keys "
+                      "in %d partitions (one host thread each), %.1f sample passes in %.1f s (partial tables only; "
+                      "not deequ/Spark itself)" % (sample_rows, threads, rows / sample_rows, el)}
 
 
 def committed_json(pattern, rows, need=None):
@@ -596,6 +706,33 @@ def main():
                                    "(DESIGN.md §3)" % kms},
             "valu_roofline": valu}
         del s10
+        # C2 with every analyzer under `where c4 < 0` (conditionalSelection): the filter is evaluated by c4's own scan
+        w = "c4 < 0"
+        c2w_an = [D.Size(w)]
+        for cn in names:
+            c2w_an += [D.Completeness(cn, w), D.Mean(cn, w), D.Sum(cn, w), D.Minimum(cn, w), D.Maximum(cn, w),
+                       D.StandardDeviation(cn, w)]
+        c2w = ScanWorkload(torch, N, D, ctx, table, c2w_an, stream, dev, world, args.dist_backend)
+        before = ctx.kernel_launches()
+        el, kms, _ = timed(torch, dist, world, max(3, args.steps // 4), 1, stream, c2w.step)
+        after = ctx.kernel_launches()
+        ach = alg_bytes / (kms * 1e-3) / 1e9
+        c2w_traffic = committed_json("c2where_traffic_*.json", nrows)
+        sec["c2_where"] = {
+            "workload": "C2's 49 ops, every one under `where %s` (int64 column, 1%% nulls: ~50%% of the rows selected)" % w,
+            "value": total / (el / max(3, args.steps // 4)), "unit": "rows/s",
+            "ms_per_step": el / max(3, args.steps // 4) * 1e3,
+            "launches_per_step": {k: (after[k] - before[k]) / (max(3, args.steps // 4) + 1)
+                                  for k in after if after[k] != before[k]},
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": ach / PEAK_HBM_GBPS,
+                         "traffic": c2w_traffic[0]["traffic_bytes_per_call"] / 1e9 if c2w_traffic else None,
+                         "traffic_unit": "GB per dq_scan call (rocprofv3 PMC, %s)" % (c2w_traffic[1] if c2w_traffic
+                                                                                      else "not measured"),
+                         "kernel": "dq_scan avg %.3f ms (HIP events): the filter column's scan produces the valid & "
+                                   "where masks the other columns' scans read; algorithmic %.1f B/row as C2"
+                                   % (kms, bytes_per_row)}}
+        del c2w
         del table
         torch.cuda.empty_cache()
         sec["c3"] = bench_c3(torch, N, D, ctx, stream, dev, total, max(3, args.steps // 4), dist, world, rank,
@@ -614,6 +751,11 @@ def main():
         result["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.cpu_sample_rows)
+        if "secondary" in result:
+            sec = result["secondary"]
+            sec["suite10"]["cpu_baseline"] = cpu_baseline_suite10(args.cpu_seconds / 2, args.cpu_sample_rows // 2)
+            if "c4" in sec:
+                sec["c4"]["cpu_baseline"] = cpu_baseline_c4(args.cpu_seconds / 2, 1 << 24)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -666,7 +666,7 @@ class FrequenciesAndNumRows:
             bb = _block_from_dict(other.frequencies, ba)
         if ba is not None and bb is not None and ba.schema() == bb.schema():
             from . import groups as G
-            merged = G.concat([ba, bb], ba.schema())
+            merged = G.BlockParts([ba, bb], ba.schema())  # joined in HBM by the metric's build, not on the host
             return FrequenciesAndNumRows(merged, self.numRows + other.numRows, self.columns)
         merged = {}
         for src in (self.as_dict(), other.as_dict()):
@@ -705,7 +705,10 @@ class FrequenciesAndNumRows:
         f = self.frequencies
         if isinstance(f, engine.FrequencyTable):
             return f
-        if self._device is None and isinstance(f, G.GroupBlock):
+        if self._device is None and isinstance(f, G.BlockParts):
+            table, counts = f.device_table()
+            self._device = engine.frequencies(table, f.names, False, weights=counts)
+        elif self._device is None and isinstance(f, G.GroupBlock):
             self._device = engine.frequencies(f.table(), f.names, False, weights=f.counts)
         if self._device is None and isinstance(f, engine.PairFrequencies):
             self._device = f.to_device()

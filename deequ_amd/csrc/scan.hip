@@ -1602,6 +1602,39 @@ __device__ __forceinline__ uint32_t valid_dword(const uint64_t* vb, int64_t b0, 
     return d;
 }
 
+// Full tiles: the first kWherePf consumers' validity dwords of tile t are loaded together with the tile's values
+// (prefetch), so the mask stores never wait on a load issued after the next tile's prefetch (vmcnt is in order).
+constexpr int kWherePf = 8;
+__device__ __forceinline__ void where_prefetch(const WhereOut* __restrict__ wo, int64_t t, int tid,
+                                               uint32_t (&vd)[kWherePf]) {
+    const int nm = wo->nmasks;
+    const int64_t b0 = t * (kTileRows / 8) + tid;
+#pragma unroll
+    for (int k = 0; k < kWherePf; ++k) vd[k] = (k < nm && (tid & 3) == 0) ? valid_dword(wo->valid[k], b0, 0, true) : 0u;
+}
+
+// Writes a full tile's producer outputs from the prefetched validity (stores only; consumers past kWherePf load).
+__device__ __forceinline__ void where_emit_full(const WhereOut* __restrict__ wo, int64_t t, int tid, uint32_t w,
+                                                uint32_t wn, const uint32_t (&vd)[kWherePf]) {
+    const int lane = tid & 63;
+    const uint32_t pw = quad_pack(w, lane);
+    const uint32_t pn = quad_pack(wn, lane);
+    if ((lane & 3) != 0) return;
+    const int64_t b0 = t * (kTileRows / 8) + tid;
+    const int nm = wo->nmasks;
+#pragma unroll
+    for (int k = 0; k < kWherePf; ++k)
+        if (k < nm) *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->mask[k]) + b0) = vd[k] & pw;
+    for (int m = kWherePf; m < nm; ++m) {  // wave-uniform, rare
+        const uint32_t v = valid_dword(wo->valid[m], b0, 0, true);
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->mask[m]) + b0) = v & pw;
+    }
+    if (wo->bitmaps) {
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->where_t) + b0) = pw;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->where_nn) + b0) = pn;
+    }
+}
+
 // Writes the producer's outputs for tile t: per consumer valid & where TRUE, and the where bitmaps if asked for.
 __device__ __forceinline__ void where_emit(const WhereOut* __restrict__ wo, int64_t t, int tid, uint32_t w, uint32_t wn,
                                            bool full, int64_t vbytes) {
@@ -1688,6 +1721,10 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
         int64_t t = blockIdx.x;
         uint64_t x[8], y[8];
         uint32_t bx = 0xFF, by = 0xFF, bw = 0xFF, bn = 0xFF;
+        uint32_t vdc[WP ? kWherePf : 1], vdn[WP ? kWherePf : 1];
+        if constexpr (WP) {
+            if (t < nfull) where_prefetch(wo, t, tid, vdc);
+        }
         if (t < nfull) {
             heavy_load(c0, t, tid, x);
             bx = heavy_bits(c0.validity, t, tid);
@@ -1704,6 +1741,12 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
             const int64_t tn = t + G;
             uint64_t xn[8], yn[8];
             uint32_t nbx = 0xFF, nby = 0xFF, nbw = 0xFF, nbn = 0xFF;
+            if constexpr (WP) {  // the filter of this tile and its mask stores go out before the next tile's loads
+                const uint32_t e = where_eval8<F0>(wo->prog, x, bx, 0xFFu);
+                bw = e & 0xFFu;
+                bn = e >> 8;
+                where_emit_full(wo, t, tid, bw, bn, vdc);
+            }
             if (tn < nfull) {
                 heavy_load(c0, tn, tid, xn);
                 nbx = heavy_bits(c0.validity, tn, tid);
@@ -1715,14 +1758,13 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                     nbw = heavy_bits(sd.where_t, tn, tid);
                     nbn = heavy_bits(sd.where_nn, tn, tid);
                 }
-            }
-            if constexpr (WP) {
-                const uint32_t e = where_eval8<F0>(wo->prog, x, bx, 0xFFu);
-                bw = e & 0xFFu;
-                bn = e >> 8;
-                where_emit(wo, t, tid, bw, bn, true, vbytes);
+                if constexpr (WP) where_prefetch(wo, tn, tid, vdn);
             }
             fold(x, y, bx, by, bw, bn);
+            if constexpr (WP) {
+#pragma unroll
+                for (int k = 0; k < kWherePf; ++k) vdc[k] = vdn[k];
+            }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 x[k] = xn[k];

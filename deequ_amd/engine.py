@@ -277,13 +277,14 @@ def frequencies(table, key_columns, include_nulls=False, weights=None):
         rc = context.lib.dq_frequencies(context.handle, arr, len(cols), table.nrows, keys.ctypes.data, len(keys),
                                         flags, ctypes.byref(handle))
     else:
-        w = np.ascontiguousarray(weights, dtype=np.int64)
+        on_device = hasattr(weights, "data_ptr")  # a torch tensor in HBM (int64, one count per row)
+        w = weights if on_device else np.ascontiguousarray(weights, dtype=np.int64)
         if len(w) != table.nrows:
             raise ValueError("weights: %d entries for %d rows" % (len(w), table.nrows))
         opt = N.DqFreqOptions()
         opt.flags = flags
-        opt.weights_device = 0
-        opt.weights = w.ctypes.data if len(w) else None
+        opt.weights_device = 1 if on_device else 0
+        opt.weights = (w.data_ptr() if on_device else w.ctypes.data) if len(w) else None
         rc = context.lib.dq_frequencies_ex(context.handle, arr, len(cols), table.nrows, keys.ctypes.data, len(keys),
                                            ctypes.byref(opt), ctypes.byref(handle))
     context.check(rc, "dq_frequencies")

@@ -264,8 +264,90 @@ def unpack(blob, schema):
     return GroupBlock(cols, counts)
 
 
+class BlockParts(GroupBlock):
+    """The groups of several blocks of one schema, concatenated lazily: the host columns are joined only when read;
+    device_table() copies each part straight into device buffers (no host-side concatenation of the key bytes)."""
+
+    def __init__(self, parts, schema):
+        self.parts = [p for b in parts for p in (b.parts if isinstance(b, BlockParts) else [b]) if p.size]
+        self._schema = list(schema)
+        self._joined = None
+        self.num_rows = sum(p.num_rows for p in self.parts)
+        self.null_rows = sum(p.null_rows for p in self.parts)
+
+    def _join(self):
+        if self._joined is None:
+            self._joined = concat(self.parts, self._schema)
+        return self._joined
+
+    columns = property(lambda self: self._join().columns)
+    counts = property(lambda self: self._join().counts)
+
+    @property
+    def size(self):
+        return sum(p.size for p in self.parts)
+
+    @property
+    def names(self):
+        return [n for n, _, _, _ in self._schema]
+
+    def schema(self):
+        return list(self._schema)
+
+    def device_table(self):
+        """(deequ_amd.table.Table of device columns, device int64 counts): each part's buffers copied into its
+        slice of the device buffers, string offsets rebased on the device."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        n = self.size
+        cols = []
+        for i, (name, t, prec, scale) in enumerate(self._schema):
+            parts = [b.columns[i] for b in self.parts]
+            c = Column(name, t, None, None, length=n, decimal_precision=prec, decimal_scale=scale)
+            d = {}
+            if t == N.TYPE_STRING:
+                nbytes = sum(int(p.offsets[p.length]) - int(p.offsets[0]) for p in parts)
+                data = torch.zeros(nbytes + 16, dtype=torch.uint8, device=dev)
+                off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+                off[0] = 0
+                at, base = 0, 0
+                for p in parts:
+                    o = np.asarray(p.offsets, dtype=np.int32)[:p.length + 1]
+                    a, b = int(o[0]), int(o[-1])
+                    data[base:base + b - a].copy_(torch.from_numpy(np.asarray(p.values, dtype=np.uint8)[a:b]))
+                    po = torch.from_numpy(np.ascontiguousarray(o[1:])).to(dev)
+                    off[at + 1:at + 1 + p.length] = po - a + base
+                    at += p.length
+                    base += b - a
+                d["values"], d["offsets"] = data, off
+            else:
+                dt = NUMPY_OF[t]
+                vals = torch.empty(max(n, 1), dtype=torch.from_numpy(np.zeros(1, dtype=dt)).dtype, device=dev)
+                at = 0
+                for p in parts:
+                    vals[at:at + p.length].copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(p.values)[:p.length])))
+                    at += p.length
+                d["values"] = vals
+            if any(p.validity is not None for p in parts):
+                valid = np.concatenate([unpack_validity(p.validity, p.length) for p in parts])
+                if not valid.all():
+                    bits = pack_validity(valid)
+                    m = np.zeros((n + 63) // 64 * 8, dtype=np.uint8)
+                    m[:len(bits)] = bits
+                    d["validity"] = torch.from_numpy(m).to(dev)
+            c.device = d
+            cols.append(c)
+        counts = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        at = 0
+        for p in self.parts:
+            counts[at:at + p.size].copy_(torch.from_numpy(np.ascontiguousarray(p.counts)))
+            at += p.size
+        torch.cuda.synchronize()
+        return Table(cols), counts[:n]
+
+
 def concat(blocks, schema):
-    """One block of the groups of several (same schema)."""
+    """One block of the groups of several (same schema): buffers concatenated once, offsets rebased in place."""
     blocks = [b for b in blocks if b.size]
     if not blocks:
         return unpack(struct.pack("<q", 0), schema)
@@ -274,15 +356,26 @@ def concat(blocks, schema):
     cols = []
     for i, (name, t, prec, scale) in enumerate(schema):
         parts = [b.columns[i] for b in blocks]
-        valid = np.concatenate([unpack_validity(c.validity, c.length) for c in parts])
-        validity = None if valid.all() else pack_validity(valid)
+        validity = None
+        if any(c.validity is not None for c in parts):
+            valid = np.concatenate([unpack_validity(c.validity, c.length) for c in parts])
+            validity = None if valid.all() else pack_validity(valid)
+        n = sum(c.length for c in parts)
         if t == N.TYPE_STRING:
-            lens = np.concatenate([np.diff(np.asarray(c.offsets, dtype=np.int64)) for c in parts])
-            off = np.zeros(len(lens) + 1, dtype=np.int64)
-            np.cumsum(lens, out=off[1:])
-            data = np.concatenate([np.asarray(c.values, dtype=np.uint8)[:int(c.offsets[-1])] for c in parts])
-            cols.append(Column(name, t, data, validity, off.astype(np.int32), length=len(lens)))
+            off = np.empty(n + 1, dtype=np.int64)
+            off[0] = 0
+            at, base = 1, 0
+            for c in parts:
+                o = np.asarray(c.offsets, dtype=np.int64)[:c.length + 1]
+                off[at:at + c.length] = o[1:] - o[0] + base
+                base += int(o[-1] - o[0])
+                at += c.length
+            if base >= 2 ** 31:
+                raise ValueError("concatenated string keys exceed the int32 Arrow offsets")
+            data = np.concatenate([np.asarray(c.values, dtype=np.uint8)[int(c.offsets[0]):int(c.offsets[c.length])]
+                                   for c in parts])
+            cols.append(Column(name, t, data, validity, off.astype(np.int32), length=n))
         else:
-            cols.append(Column(name, t, np.concatenate([np.asarray(c.values) for c in parts]), validity,
+            cols.append(Column(name, t, np.concatenate([np.asarray(c.values)[:c.length] for c in parts]), validity,
                                decimal_precision=prec, decimal_scale=scale))
     return GroupBlock(cols, np.concatenate([b.counts for b in blocks]))

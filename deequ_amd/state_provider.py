@@ -224,10 +224,11 @@ class HdfsStateProvider:
         path = self._freq_dir(ident)
         files = sorted(f for f in os.listdir(path) if f.endswith(".parquet"))
         (num_rows,) = struct.unpack(">q", self._read(self._bin(ident, "-num_rows"))[:8])
-        pairs = _load_pairs(path, files, num_rows)
+        table = _read_parts(path, files)
+        pairs = _load_pairs(table, num_rows)
         if pairs is not None:
             return pairs
-        block = _load_block(path, files, num_rows)
+        block = _load_block(table, num_rows)
         if block is not None:
             return block
         freq = {}
@@ -309,17 +310,24 @@ def _block_table(state):
     return pa.Table.from_arrays(arrays + [pa.array(f.counts, type=pa.int64())], names=f.names + [COUNT_COL])
 
 
-def _load_block(path, files, num_rows):
+def _read_parts(path, files):
+    """The part files of a frequency state as one Arrow table (read once, Arrow's own threads), or None."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    if not files:
+        return None
+    return pa.concat_tables([pq.read_table(os.path.join(path, f)) for f in files]) if len(files) == 1 else \
+        pq.ParquetDataset([os.path.join(path, f) for f in files]).read(use_threads=True)
+
+
+def _load_block(t, num_rows):
     """A persisted state of any key shape as a GroupBlock (Arrow buffers -> columns, vectorised); its groups are
     distinct, and the weighted GPU build behind its metrics reads them with their counts."""
     import numpy as np
-    import pyarrow as pa
-    import pyarrow.parquet as pq
     from . import groups as G
     from .table import Table
-    if not files:
+    if t is None:
         return None
-    t = pa.concat_tables([pq.read_table(os.path.join(path, f)) for f in files])
     keys = [n for n in t.column_names if n != COUNT_COL]
     if COUNT_COL not in t.column_names or not keys:
         return None
@@ -333,15 +341,13 @@ def _load_block(path, files, num_rows):
     return A.FrequenciesAndNumRows(block, num_rows, keys)
 
 
-def _load_pairs(path, files, num_rows):
+def _load_pairs(t, num_rows):
     """A persisted single fixed-width-key frequency state as canonical (key, count) arrays
     (engine.PairFrequencies), or None when the key columns are of another shape."""
     import numpy as np
     import pyarrow as pa
-    import pyarrow.parquet as pq
-    if not files:
+    if t is None:
         return None
-    t = pa.concat_tables([pq.read_table(os.path.join(path, f)) for f in files])
     keys = [n for n in t.column_names if n != COUNT_COL]
     if len(keys) != 1:
         return None

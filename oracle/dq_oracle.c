@@ -772,3 +772,99 @@ int oracle_generated_suite(int ncols, const oracle_gen_spec* specs, int64_t row0
     return oracle_generated_suite_ex(ncols, specs, row0, nrows, npairs, pairs, threads, NULL, 0, NULL, out, corr_out,
                                      NULL, NULL);
 }
+
+/* ---- CPU baseline legs of bench.py (restated per-row work of the reference, timed on the host) ----------------
+ * suite10: one column's Spark-order row loop for every op of the north-star suite on it: count, Sum (Long wrap /
+ * Double), NaN-largest Min / Max, CentralMomentAgg update, Compliance(col > 0) and the HLL++ register update
+ * (XXH64 hashLong of the value, StatefulHyperloglogPlus.update); pairs add the Spark Corr update. Returns rows. */
+int64_t oracle_scan_suite10_col(int spark_type, const void* values, const uint8_t* valid, int64_t nrows,
+                                uint8_t* regs512, double* out6) {
+    const uint8_t* v = (const uint8_t*)values;
+    const int frac = spark_type == T_DOUBLE;
+    int64_t n = 0, isum = 0, imin = INT64_MAX, imax = INT64_MIN, pt = 0;
+    double dsum = 0.0, dmin = NAN, dmax = NAN, wn = 0.0, wavg = 0.0, wm2 = 0.0;
+    for (int64_t i = 0; i < nrows; ++i) {
+        if (!valid[i]) continue;
+        uint64_t raw;
+        memcpy(&raw, v + 8 * i, 8);
+        double x;
+        if (frac) {
+            memcpy(&x, &raw, 8);
+            dsum += x;
+            if (n == 0 || nan_gt(dmin, x)) dmin = x;
+            if (n == 0 || nan_gt(x, dmax)) dmax = x;
+            pt += (x > 0.0 || x != x);
+            hll_add(regs512, hash_long(x == x ? raw : 0x7ff8000000000000ULL));
+        } else {
+            const int64_t xi = (int64_t)raw;
+            x = (double)xi;
+            isum = (int64_t)((uint64_t)isum + (uint64_t)xi);
+            if (xi < imin) imin = xi;
+            if (xi > imax) imax = xi;
+            pt += xi > 0;
+            hll_add(regs512, hash_long(raw));
+        }
+        ++n;
+        const double n1 = wn + 1.0, delta = x - wavg, deltaN = delta / n1;
+        wavg += deltaN;
+        wm2 += delta * (delta - deltaN);
+        wn = n1;
+    }
+    out6[0] = (double)n;
+    out6[1] = frac ? dsum : (double)isum;
+    out6[2] = frac ? dmin : (double)imin;
+    out6[3] = frac ? dmax : (double)imax;
+    out6[4] = wn > 0 ? sqrt(wm2 / wn) : NAN;
+    out6[5] = (double)pt;
+    return nrows;
+}
+
+int64_t oracle_corr_spark(int tx, const void* xv, const uint8_t* vx, int ty, const void* yv, const uint8_t* vy,
+                          int64_t nrows, double* out6) {
+    const uint8_t* xp = (const uint8_t*)xv;
+    const uint8_t* yp = (const uint8_t*)yv;
+    double n = 0, xa = 0, ya = 0, ck = 0, xm = 0, ym = 0;
+    for (int64_t i = 0; i < nrows; ++i) {
+        if (!vx[i] || !vy[i]) continue;
+        const double x = as_f64(tx, xp + 8 * i, 0), y = as_f64(ty, yp + 8 * i, 0);
+        const double n1 = n + 1.0, dx = x - xa, dy = y - ya;
+        xa += dx / n1;
+        ya += dy / n1;
+        ck += dx * (y - ya);
+        xm += dx * (x - xa);
+        ym += dy * (y - ya);
+        n = n1;
+    }
+    out6[0] = n; out6[1] = xa; out6[2] = ya; out6[3] = ck; out6[4] = xm; out6[5] = ym;
+    return nrows;
+}
+
+/* C4: the grouping hash aggregate (count(*) GROUP BY key) as a single-threaded open-addressing table over the
+ * canonical 64-bit keys (Spark's HashAggregate per partition); returns the number of groups. table: cap slots of
+ * (key, count) pairs, cap a power of two larger than the distinct keys; used marks occupied slots. */
+int64_t oracle_count_keys(const int64_t* keys, int64_t n, int64_t* table, uint8_t* used, int64_t cap) {
+    memset(used, 0, (size_t)cap);
+    int64_t groups = 0;
+    const uint64_t mask = (uint64_t)cap - 1;
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t z = (uint64_t)keys[i];
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        uint64_t p = (z ^ (z >> 31)) & mask;
+        for (;;) {
+            if (!used[p]) {
+                used[p] = 1;
+                table[2 * p] = keys[i];
+                table[2 * p + 1] = 1;
+                ++groups;
+                break;
+            }
+            if (table[2 * p] == keys[i]) {
+                ++table[2 * p + 1];
+                break;
+            }
+            p = (p + 1) & mask;
+        }
+    }
+    return groups;
+}

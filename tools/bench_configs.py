@@ -27,7 +27,8 @@ PEAK = 8000.0
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", required=True, choices=["c3", "c4", "suite10", "s10_nocorr", "corr4", "hll8", "c2", "kll", "kll_nulls"])
+    ap.add_argument("--config", required=True, choices=["c3", "c4", "suite10", "s10_nocorr", "corr4", "hll8", "c2", "kll",
+                                                         "kll_nulls", "c2where", "c5"])
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--distinct", type=float, default=1e8)
     ap.add_argument("--steps", type=int, default=5)
@@ -60,11 +61,23 @@ def main():
             c.device["validity"] = m
         return c
 
-    if args.config == "c3":
+    if args.config == "c3":  # the columns of bench.bench_c3
         t = Table([col("k", 5, 0xC3000001, N.TYPE_LONG), col("x", 6, 0xC3000002, N.TYPE_DOUBLE),
-                   col("y", 6, 0xC3000003, N.TYPE_DOUBLE)])
+                   col("y", 7, 0xC3000002, N.TYPE_DOUBLE)])
         analyzers = [D.ApproxCountDistinct("k"), D.Correlation("x", "y"), D.Completeness("k")]
         bytes_per_row = 3 * (8 + 1 / 8)
+    elif args.config == "c2where":
+        t = bench.build_shard(torch, N, ctx, 0, R, dev)
+        w = "c4 < 0"
+        analyzers = [D.Size(w)]
+        for c in t.columns:
+            analyzers += [D.Completeness(c, w), D.Mean(c, w), D.Sum(c, w), D.Minimum(c, w), D.Maximum(c, w),
+                          D.StandardDeviation(c, w)]
+        bytes_per_row = 8 * (8 + 1 / 8)
+    elif args.config == "c5":
+        t, nbytes = bench.c5_shard(torch, N, ctx, dev, R)
+        analyzers = None
+        bytes_per_row = nbytes / R
     elif args.config in ("s10_nocorr", "corr4", "hll8", "c2"):
         # cost breakdown of suite10 (diagnostics)
         t = bench.build_shard(torch, N, ctx, 0, R, dev)
@@ -104,6 +117,8 @@ def main():
     ctx.synchronize()
 
     def run():
+        if analyzers is None:  # c5: the 3-pass ColumnProfiler
+            return D.ColumnProfiler.profile(t)
         return D.AnalysisRunner.onData(t).addAnalyzers(analyzers).run()
 
     for _ in range(args.warmup):
@@ -116,7 +131,7 @@ def main():
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
     sec = float(np.median(times))
-    out = {"config": args.config, "rows": R, "analyzers": len(analyzers), "ms": sec * 1e3, "rows_per_s": R / sec,
+    out = {"config": args.config, "rows": R, "analyzers": len(analyzers or []), "ms": sec * 1e3, "rows_per_s": R / sec,
            "algorithmic_GBps": bytes_per_row * R / sec / 1e9, "frac_of_peak": bytes_per_row * R / sec / 1e9 / PEAK,
            "note": "end-to-end AnalysisRunner.run() wall time (plan + kernels + host metrics), median of %d"
                    % args.steps}
@@ -129,7 +144,7 @@ def main():
         out["check"] = {"Uniqueness": got["Uniqueness"] == half / R, "Distinctness": got["Distinctness"] == Dn / R,
                         "UniqueValueRatio": got["UniqueValueRatio"] == 0.5, "CountDistinct": got["CountDistinct"] == Dn,
                         "Entropy_rel_err": abs(got["Entropy"] - exact_ent) / exact_ent}
-    else:
+    elif analyzers:
         out["sample_metrics"] = {repr(a): repr(res.metric(a).value.get())[:200] for a in analyzers[:3]}
     print(json.dumps(out), flush=True)
 

@@ -32,12 +32,12 @@ for step in "$@"; do
       timeout -k 10 600 python -u $arg > gpurun_out/${TAG}_py$i.log 2>&1
       rc=$?; tail -20 gpurun_out/${TAG}_py$i.log ;;
     prof)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$i -o p -- python -u $arg > gpurun_out/${TAG}_prof$i.log 2>&1
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof$i -o p -- python -u $arg > gpurun_out/${TAG}_prof$i.log 2>&1
       rc=$?; tail -5 gpurun_out/${TAG}_prof$i.log ;;
     pmc)
       ctrs=${arg%%:*}
       cmd=${arg#*:}
-      timeout -s KILL 180 rocprofv3 --pmc $ctrs -d gpurun_out/${TAG}_pmc$i -o p -- python -u $cmd > gpurun_out/${TAG}_pmc$i.log 2>&1
+      timeout -s KILL 180 rocprofv3 --pmc $ctrs --output-format csv -d gpurun_out/${TAG}_pmc$i -o p -- python -u $cmd > gpurun_out/${TAG}_pmc$i.log 2>&1
       rc=$?; tail -3 gpurun_out/${TAG}_pmc$i.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
