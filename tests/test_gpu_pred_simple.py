@@ -74,6 +74,19 @@ def _key(s):
     return None if s is None else repr(s)
 
 
+def _same(a, x, y):
+    """Fast path vs VM: bit-exact, except fp64 sums of a DOUBLE column (MeanState.sum_), whose summation order
+    follows the kernel shape that ran (a `where` produced by the filter column's own scan folds in another order
+    than the VM's bitmaps) -- those within the north star's 1e-12 relative bar."""
+    if isinstance(a, D.Mean) and x is not None and y is not None:
+        if x.count != y.count:
+            return False
+        if x.sum_ == y.sum_ or (x.sum_ != x.sum_ and y.sum_ != y.sum_):
+            return True
+        return abs(x.sum_ - y.sum_) <= 1e-12 * abs(y.sum_)
+    return _key(x) == _key(y)
+
+
 @pytest.mark.parametrize("n", [1, 130, 70001])
 def test_simple_predicates_match_vm_and_oracle(n):
     t = typed_table(n, n)
@@ -82,7 +95,7 @@ def test_simple_predicates_match_vm_and_oracle(n):
         fast = _run(t, an, vm=False)
         vm = _run(t, an, vm=True)
         for a, x, y in zip(an, fast, vm):
-            assert _key(x) == _key(y), (pred, a, x, y)
+            assert _same(a, x, y), (pred, a, x, y)
             assert_state_parity(t, a, x)
 
 
