@@ -293,35 +293,41 @@ C5_STRINGS = [("s_cat50", 101), ("s_bool", 102), ("s_cat100", 103), ("s_int", 10
               ("s_text0", 107), ("s_text1", 107), ("s_text2", 107), ("s_text3", 107)]
 
 
-def c5_shard(torch, N, ctx, dev, rows):
+def c5_shard(torch, N, ctx, dev, rows, chunk_rows=125_000_000):
     """One GPU's shard of BASELINE config C5 generated in HBM: 5 fp64 + 5 int64 columns (the C2 generators) and 10
-    UTF-8 string columns (3 low-cardinality, 3 numeric-looking, 4 free text 1-20 characters), 5 % nulls each."""
-    from deequ_amd.table import Table, Column
-    cols, nbytes = [], 0
-    for j, (name, kind) in enumerate(C5_NUMERIC):
-        dt = torch.float64 if kind in (1, 2, 3, 6, 7) else torch.int64
-        v = torch.empty(rows, dtype=dt, device=dev)
-        ctx.synth_column(kind, 0xC5000000 + j, 0, rows, v.data_ptr())
-        c = Column(name, N.TYPE_DOUBLE if dt == torch.float64 else N.TYPE_LONG, None, None, length=rows)
-        c.device = {"values": v}
-        cols.append(c)
-        nbytes += 8 * rows
-    for j, (name, kind) in enumerate(C5_STRINGS):
-        off = torch.empty(rows + 1, dtype=torch.int32, device=dev)
-        total = ctx.synth_strings(kind, 0xC5100000 + j, 0, rows, off.data_ptr())
-        data = torch.zeros(total + 16, dtype=torch.uint8, device=dev)
-        ctx.synth_strings(kind, 0xC5100000 + j, 0, rows, off.data_ptr(), data.data_ptr())
-        c = Column(name, N.TYPE_STRING, None, None, length=rows)
-        c.device = {"values": data, "offsets": off}
-        cols.append(c)
-        nbytes += total + 4 * rows
-    for j, c in enumerate(cols):
-        m = torch.zeros((rows + 63) // 64 * 8, dtype=torch.uint8, device=dev)
-        ctx.synth_validity(0xC5200000 + j, 0, rows, 50, m.data_ptr())
-        c.device["validity"] = m
-        nbytes += rows / 8
+    UTF-8 string columns (3 low-cardinality, 3 numeric-looking, 4 free text 1-20 characters), 5 % nulls each. A
+    shard above `chunk_rows` rows is held as row chunks (ChunkedTable): one string column's bytes of the 2.5e8-row
+    shard exceed its int32 Arrow offsets."""
+    from deequ_amd.table import ChunkedTable, Table, Column
+    chunks, nbytes = [], 0
+    for r0 in range(0, rows, chunk_rows):
+        n = min(chunk_rows, rows - r0)
+        cols = []
+        for j, (name, kind) in enumerate(C5_NUMERIC):
+            dt = torch.float64 if kind in (1, 2, 3, 6, 7) else torch.int64
+            v = torch.empty(n, dtype=dt, device=dev)
+            ctx.synth_column(kind, 0xC5000000 + j, r0, n, v.data_ptr())
+            c = Column(name, N.TYPE_DOUBLE if dt == torch.float64 else N.TYPE_LONG, None, None, length=n)
+            c.device = {"values": v}
+            cols.append(c)
+            nbytes += 8 * n
+        for j, (name, kind) in enumerate(C5_STRINGS):
+            off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            total = ctx.synth_strings(kind, 0xC5100000 + j, r0, n, off.data_ptr())
+            data = torch.zeros(total + 16, dtype=torch.uint8, device=dev)
+            ctx.synth_strings(kind, 0xC5100000 + j, r0, n, off.data_ptr(), data.data_ptr())
+            c = Column(name, N.TYPE_STRING, None, None, length=n)
+            c.device = {"values": data, "offsets": off}
+            cols.append(c)
+            nbytes += total + 4 * n
+        for j, c in enumerate(cols):
+            m = torch.zeros((n + 63) // 64 * 8, dtype=torch.uint8, device=dev)
+            ctx.synth_validity(0xC5200000 + j, r0, n, 50, m.data_ptr())
+            c.device["validity"] = m
+            nbytes += n / 8
+        chunks.append(Table(cols))
     ctx.synchronize()
-    return Table(cols), nbytes
+    return (chunks[0] if len(chunks) == 1 else ChunkedTable(chunks)), nbytes
 
 
 def bench_c5(torch, N, D, ctx, dev, rows, steps):
@@ -347,10 +353,12 @@ def bench_c5(torch, N, D, ctx, dev, rows, steps):
     assert types["s_int"] == "Integral" and types["s_dec"] == "Fractional" and types["s_text0"] == "String", types
     ach = nbytes / el / 1e9
     c5_traffic = committed_json("c5_traffic_*.json", rows)
+    passes = c5_pass_times(torch, D, t)
     return {"workload": "C5 shard: ColumnProfiler passes 1-3 (Completeness, ApproxCountDistinct, DataType; Min / Max / "
                         "Mean / StdDev / Sum / KLL on 13 numeric and cast numeric-string columns; exact histograms of "
-                        "%d low-cardinality columns) over %d rows x 20 columns (5 fp64, 5 int64, 10 UTF-8), 5%% nulls"
-                        % (len(hist), rows),
+                        "%d low-cardinality columns) over %d rows x 20 columns (5 fp64, 5 int64, 10 UTF-8), 5%% nulls, "
+                        "held as %d row chunk(s) (one GPU's share of the 8-GPU 2e9-row table)"
+                        % (len(hist), rows, len(getattr(t, "chunks", [t]))),
             "value": rows / el, "unit": "rows/s", "ms_per_step": el * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": ach / PEAK_HBM_GBPS,
@@ -358,7 +366,42 @@ def bench_c5(torch, N, D, ctx, dev, rows, steps):
                          "traffic_unit": "GB per profile (rocprofv3 PMC, %s)" % (c5_traffic[1] if c5_traffic
                                                                                  else "not measured"),
                          "kernel": "end-to-end profile wall time; achieved = the table's bytes (%.1f GB: values, "
-                                   "offsets, UTF-8 data, validity) once per profile" % (nbytes / 1e9)}}
+                                   "offsets, UTF-8 data, validity) once per profile" % (nbytes / 1e9)},
+            "passes_ms": passes}
+
+
+def c5_pass_times(torch, D, t):
+    """Wall time of each ColumnProfiler pass of one extra (untimed) profile, the device synchronised at every pass
+    boundary: pass 1 (Completeness, ApproxCountDistinct, DataType, Size), the pass-2 casts, pass 2 (numeric
+    statistics scan + the KLL extra pass), pass 3 (histograms)."""
+    from deequ_amd.profiles import LocalPasses
+
+    class Timed(LocalPasses):
+        def __init__(self):
+            self.ms, self.runs = {}, 0
+
+        def _t(self, key, fn):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = fn()
+            torch.cuda.synchronize()
+            self.ms[key] = self.ms.get(key, 0.0) + (time.perf_counter() - t0) * 1e3
+            return out
+
+        def run(self, data, analyzers):
+            self.runs += 1
+            return self._t("pass1_generic" if self.runs == 1 else "pass2_numeric_and_kll",
+                           lambda: LocalPasses.run(self, data, analyzers))
+
+        def cast(self, data, name, to_type):
+            return self._t("pass2_casts", lambda: LocalPasses.cast(self, data, name, to_type))
+
+        def histograms(self, data, targets):
+            return self._t("pass3_histograms", lambda: LocalPasses.histograms(self, data, targets))
+
+    p = Timed()
+    D.ColumnProfiler.profile(t, passes=p)
+    return {k: round(v, 2) for k, v in p.ms.items()}
 
 
 def bench_host_streamed(torch, N, D, ctx, dev, rows, steps, chunk_rows=1 << 25):
@@ -746,7 +789,7 @@ def main():
             torch.cuda.empty_cache()
             sec["c2_host_streamed"] = bench_host_streamed(torch, N, D, ctx, dev, min(total, 200_000_000), 2)
             torch.cuda.empty_cache()
-            sec["c5_shard"] = bench_c5(torch, N, D, ctx, dev, min(total, 100_000_000), 2)
+            sec["c5_shard"] = bench_c5(torch, N, D, ctx, dev, min(total, 250_000_000), 2)
             torch.cuda.empty_cache()
         result["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -20,7 +20,7 @@ from .runners import (AnalysisRunner, KLLRunner, AnalysisRunBuilder, AnalyzerCon
                       ScanBatch)
 from .checks import (Check, CheckLevel, CheckStatus, ConstraintStatus, ConstrainableDataTypes, VerificationSuite,
                      VerificationResult)
-from .table import Table, Column
+from .table import ChunkedTable, Table, Column
 from .profiles import (ColumnProfiler, ColumnProfilerRunner, ColumnProfilerRunBuilder, ColumnProfiles,
                        StandardColumnProfile, NumericColumnProfile, DataTypeInstances)
 from .state_provider import HdfsStateProvider, FileSystemStateProvider

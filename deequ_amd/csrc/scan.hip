@@ -448,7 +448,8 @@ __device__ __forceinline__ uint64_t spark_hash(uint64_t v, int spark_type) {
 }
 
 // Lane-level helpers shared by the striped and the lean kernels (see scan_heavy8_kernel).
-__device__ __forceinline__ uint32_t row_mask(uint32_t m, int k) { return (uint32_t)(((int)(m << (31 - k))) >> 31); }
+// bit k of m as 0 / 0xFFFFFFFF: one v_bfe_i32 (the shift pair it equals is sometimes left as two instructions)
+__device__ __forceinline__ uint32_t row_mask(uint32_t m, int k) { return (uint32_t)__builtin_amdgcn_sbfe((int)m, k, 1); }
 __device__ __forceinline__ double pack_f64(uint32_t hi, uint32_t lo) { return as_f64(((uint64_t)hi << 32) | lo); }
 __device__ __forceinline__ uint32_t hi32(double d) { return (uint32_t)(f64_bits(d) >> 32); }
 __device__ __forceinline__ uint32_t lo32(double d) { return (uint32_t)f64_bits(d); }
@@ -475,6 +476,13 @@ __device__ __forceinline__ double i64_to_f64(uint64_t v) {
     return __builtin_fma((double)(int32_t)(uint32_t)(v >> 32), 4294967296.0, (double)(uint32_t)v);
 }
 __device__ __forceinline__ double one_if(uint32_t mk) { return pack_f64(mk & 0x3FF00000u, 0u); }
+// x * {1.0, 0.0} as one v_mul_f64: left to itself the compiler turns the multiply by one_if() into two v_and_b32
+// of the halves (finite x only, which is all the callers pass)
+__device__ __forceinline__ double mul_raw(double a, double b) {
+    double r;
+    asm("v_mul_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // ------------------------------------------------------------------------------------------------
 // Per-lane accumulators, specialised by storage class so only live state occupies VGPRs.
@@ -1338,7 +1346,7 @@ __device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, cons
                 hm = m & ~nanm;
                 if ((FULL || hc.hll) && nanm) {
                     const uint32_t p = hll_idx_rank<2>(f64_bits(__builtin_nan("")));
-                    atomicMax(&regs[p & 0xffffu], p >> 16);
+                    atomicMax(reinterpret_cast<int*>(&regs[p & 0xffffu]), (int)(p >> 16) - 1);
                 }
             }
         }
@@ -1380,7 +1388,7 @@ __device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, cons
             double s1 = 0.0, s2 = 0.0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const double d = (xd[k] - c0) * one_if(row_mask(m, k));
+                const double d = mul_raw(xd[k] - c0, one_if(row_mask(m, k)));
                 s1 += d;
                 s2 = __builtin_fma(d, d, s2);
             }
@@ -1388,6 +1396,21 @@ __device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, cons
             a.mean = __builtin_fma(s1, r, c0);
             a.m2 += __builtin_fma(-s1 * s1, r, s2);
         }
+    } else if ((FULL || hc.moments) && cnt && __builtin_expect(fin && a.n != 0, 1)) {
+        // finite batch: deviations from the running mean as the integral path, one reciprocal of the new count; masked
+        // rows hold 0.0 and get a 0.0 factor. A lane's first batch (and a batch with a valid inf / NaN) takes the
+        // batch mean + Chan merge below.
+        const double c0 = a.mean;
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double d = mul_raw(xd[k] - c0, one_if(row_mask(m, k)));
+            s1 += d;
+            s2 = __builtin_fma(d, d, s2);
+        }
+        const double r = rcp_refined((double)(a.n + cnt));
+        a.mean = __builtin_fma(s1, r, c0);
+        a.m2 += __builtin_fma(-s1 * s1, r, s2);
     } else if ((FULL || hc.moments) && cnt) {
         const double mb = s * rcp_refined((double)cnt);
         double m2b = 0.0;
@@ -1408,8 +1431,9 @@ __device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, cons
             const uint32_t g = xxh_long_ghi(v[k]);  // DOUBLE: raw bits (NaN rows were taken out of hm above)
             const uint32_t t = g << 9;
             tmin = min(tmin, t);
-            const uint32_t rank = ffbh_raw(t & row_mask(hm, k)) + 1u;  // 0 for a masked row (and for t == 0)
-            atomicMax(&regs[g >> 23], rank);
+            // the registers hold rank - 1 as signed ints (-1 = empty): ffbh's -1 for a masked row (and for t == 0) is
+            // the no-op, and the + 1 is paid once per register at the end instead of once per value
+            atomicMax(reinterpret_cast<int*>(&regs[g >> 23]), (int)ffbh_raw(t & row_mask(hm, k)));
         }
     }
 }
@@ -1422,30 +1446,39 @@ __device__ __forceinline__ void heavy_corr_rows(CorrPartial& cp, const double (&
                                                 uint32_t m, bool fin) {
     const uint32_t cnt = __popc(m);
     if (cnt == 0) return;
+    if (__builtin_expect(fin && cp.n != 0.0, 1)) {
+        // deviations from the lane's running means (cx, cy): with d = x - cx, e = y - cy over the batch and
+        // n' = n + cnt, xAvg' = cx + sum d / n', ck' = ck + sum d e - (sum d)(sum e) / n' (xMk, yMk alike) -- the
+        // algebra of the CorrelationState merge (A/Correlation.scala:37-52), one reciprocal per batch. A lane's first
+        // batch (and a batch with a valid inf / NaN) takes the batch-mean form below.
+        const double cx = cp.xa, cy = cp.ya;
+        double sd = 0.0, se = 0.0, sdd = 0.0, see = 0.0, sde = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const double f = one_if(row_mask(m, k));
+            const double d = mul_raw(xd[k] - cx, f), e = mul_raw(yd[k] - cy, f);
+            sd += d;
+            se += e;
+            sdd = __builtin_fma(d, d, sdd);
+            see = __builtin_fma(e, e, see);
+            sde = __builtin_fma(d, e, sde);
+        }
+        const double n1 = cp.n + (double)cnt;
+        const double r = rcp_refined(n1);
+        const double sdr = sd * r, ser = se * r;
+        cp.xa = __builtin_fma(sd, r, cx);
+        cp.ya = __builtin_fma(se, r, cy);
+        cp.ck += __builtin_fma(-sd, ser, sde);
+        cp.xm += __builtin_fma(-sd, sdr, sdd);
+        cp.ym += __builtin_fma(-se, ser, see);
+        cp.n = n1;
+        return;
+    }
     CorrPartial b;
     b.n = (double)cnt;
     b.ck = b.xm = b.ym = 0.0;
     const double inv = rcp_refined(b.n);
-    if (__builtin_expect(fin, 1)) {
-        double sx = 0.0, sy = 0.0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const double f = one_if(row_mask(m, k));
-            sx = __builtin_fma(xd[k], f, sx);
-            sy = __builtin_fma(yd[k], f, sy);
-        }
-        b.xa = sx * inv;
-        b.ya = sy * inv;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const double f = one_if(row_mask(m, k));
-            const double dx = xd[k] - b.xa, dy = yd[k] - b.ya;
-            const double dxf = dx * f, dyf = dy * f;
-            b.ck = __builtin_fma(dxf, dy, b.ck);
-            b.xm = __builtin_fma(dxf, dx, b.xm);
-            b.ym = __builtin_fma(dyf, dy, b.ym);
-        }
-    } else {
+    {
         double xv[8], yv[8];
         double sx = 0.0, sy = 0.0;
 #pragma unroll
@@ -1476,7 +1509,7 @@ __device__ __forceinline__ void heavy_hll_exact(uint32_t* regs, const uint64_t (
     for (int k = 0; k < 8; ++k)
         if ((m >> k) & 1u) {
             const uint32_t p = hll_idx_rank<F ? 2 : 3>(v[k]);
-            atomicMax(&regs[p & 0xffffu], p >> 16);
+            atomicMax(reinterpret_cast<int*>(&regs[p & 0xffffu]), (int)(p >> 16) - 1);
         }
 }
 
@@ -1694,7 +1727,7 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
         CorrPartial cp;
         cp.n = cp.xa = cp.ya = cp.ck = cp.xm = cp.ym = 0.0;
         uint32_t wt = 0, wnn = 0;
-        for (int i = tid; i < NC * kHllRegs; i += kBlock) (&hll_lds[0][0])[i] = 0;
+        for (int i = tid; i < NC * kHllRegs; i += kBlock) (&hll_lds[0][0])[i] = 0xFFFFFFFFu;  // rank - 1 = -1
         __syncthreads();
         auto fold = [&](const uint64_t (&x)[8], const uint64_t (&y)[8], uint32_t mx, uint32_t my, uint32_t w,
                         uint32_t wn) {
@@ -1868,7 +1901,7 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
             const int hs = c == 0 ? c0.hll_slot : c1.hll_slot;
             if (hl && hs >= 0) {
                 uint8_t* dst = hll_partials + ((int64_t)hs * gstride + blockIdx.x) * kHllRegs;
-                for (int i = tid; i < kHllRegs; i += kBlock) dst[i] = (uint8_t)hll_lds[c][i];
+                for (int i = tid; i < kHllRegs; i += kBlock) dst[i] = (uint8_t)(hll_lds[c][i] + 1u);
             }
         }
         __syncthreads();

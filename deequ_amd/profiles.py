@@ -20,7 +20,7 @@ from .analyzers import (Size, Completeness, ApproxCountDistinct, DataType, Minim
                         StandardDeviation, Sum, KLLSketch, Histogram, _hist_key)
 from .metrics import Distribution, DistributionValue
 from .runners import AnalysisRunner
-from .table import Table, Column
+from .table import ChunkedTable, Table, Column
 
 
 class DataTypeInstances:
@@ -200,14 +200,9 @@ class ColumnProfiler:
             print("### PROFILING: Computing numeric column statistics in pass (2/3)...")
         numeric = [n for n in relevant
                    if generic.typeOf(n) in (DataTypeInstances.Integral, DataTypeInstances.Fractional)]
-        cast_cols = []
-        for name in data.fieldNames:
-            if name in numeric:
-                to = N.TYPE_LONG if generic.typeOf(name) == DataTypeInstances.Integral else N.TYPE_DOUBLE
-                cast_cols.append(passes.cast(data, name, to))
-            else:
-                cast_cols.append(data[name])
-        casted = Table(cast_cols)
+        casts = {name: N.TYPE_LONG if generic.typeOf(name) == DataTypeInstances.Integral else N.TYPE_DOUBLE
+                 for name in numeric}
+        casted = _cast_table(passes, data, casts)
         second = []
         for name in numeric:
             second += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name),
@@ -297,6 +292,33 @@ class ColumnProfiler:
         return out
 
 
+def _cast_table(passes, data, casts):
+    """castNumericStringColumns (:326-344): every column in `casts` cast to its type, the others as they are; a
+    ChunkedTable casts chunk by chunk."""
+    if isinstance(data, ChunkedTable):
+        return ChunkedTable([_cast_table(passes, chunk, casts) for chunk in data.chunks])
+    return Table([passes.cast(data, name, casts[name]) if name in casts else data[name] for name in data.fieldNames])
+
+
+def _chunked_histograms(data, targets):
+    """computeHistograms over a ChunkedTable: each chunk's exact per-value counts (dq_frequencies), summed per value
+    (the histogram columns are the low-cardinality ones: at most lowCardinalityHistogramThreshold groups each)."""
+    from . import engine
+    out = {}
+    for name in targets:
+        counts = {}
+        for chunk in data.chunks:
+            for key, c in engine.frequencies(chunk, [name], include_nulls=True).to_dict().items():
+                counts[key] = counts.get(key, 0) + int(c)
+        total = sum(counts.values())
+        values = {}
+        for key, c in counts.items():
+            k = Histogram.NullFieldReplacement if key[0] is None else _hist_key(key[0], data[name])
+            values[k] = DistributionValue(int(c), c / total)
+        out[name] = Distribution(values, len(values))
+    return out
+
+
 class LocalPasses:
     """The profiler's passes on this process's GPU: AnalysisRunner runs, GPU casts, dq_frequencies histograms."""
 
@@ -307,6 +329,8 @@ class LocalPasses:
         return _cast_column(data, name, to_type)
 
     def histograms(self, data, targets):
+        if isinstance(data, ChunkedTable):
+            return _chunked_histograms(data, targets)
         return ColumnProfiler._compute_histograms(data, targets)
 
 

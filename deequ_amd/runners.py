@@ -11,6 +11,7 @@ from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanS
                         FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies)
 from .expr import compile_predicate
 from .metrics import DoubleMetric, Success, UnsupportedOnDevice
+from .table import ChunkedTable
 
 
 def stream_chunk_rows():
@@ -274,6 +275,8 @@ class AnalysisRunner:
         """R/AnalysisRunner.scala:97-203 (repository reuse and file output are out of scope)."""
         if not analyzers:
             return AnalyzerContext.empty()
+        if isinstance(data, ChunkedTable):
+            return AnalysisRunner._run_chunked(data, analyzers, aggregateWith, saveStatesWith)
         allAnalyzers = []
         for a in analyzers:  # VerificationSuite does not dedupe; the result map does
             if a not in allAnalyzers:
@@ -298,6 +301,26 @@ class AnalysisRunner:
             _, metrics = AnalysisRunner._runGroupingAnalyzers(data, list(cols), group, aggregateWith, saveStatesWith)
             grouped = grouped + metrics
         return preconditionFailures + nonGrouped + grouped + kllMetrics
+
+    @staticmethod
+    def _run_chunked(data, analyzers, aggregateWith=None, saveStatesWith=None):
+        """A ChunkedTable: every chunk runs the analysis (its scan, grouping and KLL passes on the GPU) and persists
+        its states in memory; the chunk states (and the states of `aggregateWith`) then merge in chunk order through
+        runOnAggregatedStates — Spark's partial aggregates of one `agg` over the partitions, merged by the same
+        State.sum. An analyzer that failed on any chunk keeps that chunk's failure metric."""
+        providers, failures = [], {}
+        for chunk in data.chunks:
+            p = InMemoryStateProvider()
+            res = AnalysisRunner.doAnalysisRun(chunk, analyzers, saveStatesWith=p)
+            for a, m in res.metricMap.items():
+                if not m.value.isSuccess and a not in failures:
+                    failures[a] = m
+            providers.append(p)
+        if aggregateWith is not None:
+            providers.append(aggregateWith)
+        merged = AnalysisRunner.runOnAggregatedStates(data.schema, Analysis(list(analyzers)), providers,
+                                                      saveStatesWith)
+        return merged + AnalyzerContext(failures)
 
     @staticmethod
     def _runScanningAnalyzers(data, analyzers, aggregateWith=None, saveStatesTo=None):

@@ -404,6 +404,43 @@ class Table:
         return self
 
 
+class ChunkedTable:
+    """A table held as consecutive row chunks (Arrow record batches) of one schema: the shape of a DataFrame's
+    partitions, and how a shard whose string bytes exceed one column's int32 offsets (2^31 bytes) is held.
+    AnalysisRunner runs every chunk and merges the chunk states with the reference's semigroup merges
+    (runOnAggregatedStates, R/AnalysisRunner.scala:385-460) — the per-partition aggregation Spark performs inside
+    one `agg`; ColumnProfiler runs its three passes the same way."""
+
+    def __init__(self, chunks):
+        chunks = list(chunks)
+        if not chunks:
+            raise ValueError("a ChunkedTable needs at least one chunk")
+        schema = chunks[0].schema
+        for t in chunks[1:]:
+            if t.schema != schema:
+                raise ValueError("chunks of a ChunkedTable must share one schema")
+        self.chunks = chunks
+        self.nrows = sum(t.nrows for t in chunks)
+
+    @property
+    def schema(self):
+        return self.chunks[0].schema
+
+    @property
+    def fieldNames(self):
+        return self.chunks[0].fieldNames
+
+    def __getitem__(self, name):
+        """The first chunk's column: type and metadata only (values live in every chunk)."""
+        return self.chunks[0][name]
+
+    def __contains__(self, name):
+        return name in self.chunks[0]
+
+    def count(self):
+        return self.nrows
+
+
 def _infer_py_type(items):
     nn = [x for x in items if x is not None]
     if not nn:

@@ -14,6 +14,8 @@ import os
 import subprocess
 import sys
 
+import weakref
+
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -832,8 +834,15 @@ def _eval(node, row):
     raise ValueError(k)
 
 
+_MASKS = weakref.WeakKeyDictionary()  # table -> {predicate text: masks} (tables are not mutated by the tests)
+_CELLS = weakref.WeakKeyDictionary()  # column -> its cells as Python objects
+
+
 def predicate_masks(table, text):
     """(TRUE mask, NOT-NULL mask) of a SQL predicate over every row."""
+    memo = _MASKS.setdefault(table, {})
+    if text in memo:
+        return memo[text]
     tree = OracleParser(text).parse()
     cols = {n: _pylist(table[n]) for n in table.columns}
     t = np.zeros(table.nrows, dtype=bool)
@@ -842,6 +851,7 @@ def predicate_masks(table, text):
         v = _eval(tree, {n: cols[n][i] for n in cols})
         nn[i] = v is not None
         t[i] = v is True or (v is not None and not isinstance(v, bool) and v != 0)
+    memo[text] = (t, nn)
     return t, nn
 
 
@@ -887,9 +897,36 @@ def _cell(col, i):
     return x / (10 ** col.decimal_scale) if t == T_DECIMAL else x
 
 
+_LE = {T_BYTE: "<i1", T_SHORT: "<i2", T_INT: "<i4", T_DATE: "<i4", T_FLOAT: "<f4", T_DOUBLE: "<f8"}
+
+
 def _pylist(col):
+    """Every row's cell (None for NULL), the column decoded once: the same reading as _cell, vectorised."""
+    if col in _CELLS:
+        return _CELLS[col]
     valid = _valid(col)
-    return [_cell(col, i) if valid[i] else None for i in range(col.length)]
+    n = col.length
+    t = col.spark_type
+    vals = _host_buffer(col, "values")
+    if t == T_STRING:
+        off = [int(x) for x in np.asarray(_host_buffer(col, "offsets"))[:n + 1]]
+        data = bytes(np.asarray(vals, dtype=np.uint8)[:off[-1] if n else 0])
+        cells = [data[off[i]:off[i + 1]].decode("utf-8") if valid[i] else None for i in range(n)]
+    else:
+        width = {T_BOOLEAN: 1, T_BYTE: 1, T_SHORT: 2, T_INT: 4, T_DATE: 4, T_FLOAT: 4}.get(t, 8)
+        raw = np.asarray(vals).view(np.uint8)[:n * width].tobytes()
+        if t == T_BOOLEAN:
+            xs = [b != 0 for b in raw]
+        else:
+            xs = np.frombuffer(raw, dtype=_LE.get(t, "<i8")).tolist()
+            if t == T_DECIMAL:
+                xs = [x / (10 ** col.decimal_scale) for x in xs]
+        cells = [x if valid[i] else None for i, x in enumerate(xs)]
+    try:
+        _CELLS[col] = cells
+    except TypeError:  # a column type that cannot be weakly referenced: no memo
+        pass
+    return cells
 
 
 # ---- expected states per analyzer ---------------------------------------------------------------

@@ -70,3 +70,19 @@ def test_from_parquet_round_trip(tmp_path):
     assert rows_of(t) == ROWS
     assert rows_of(Table.from_parquet(p, columns=["price", "att1"])) == [(r[3], r[1]) for r in ROWS]
     assert t.schema["count"] == "IntegerType"
+
+
+def test_chunked_table_schema_and_rows():
+    """ChunkedTable (row chunks of one schema: Arrow record batches / DataFrame partitions): rows add up, the schema
+    is the chunks' common one, and chunks of different schemas are refused."""
+    import pytest
+    from deequ_amd.table import ChunkedTable, Table
+    a = Table.from_pydict({"x": [1, 2, None], "s": ["a", None, "c"]})
+    b = Table.from_pydict({"x": [4], "s": ["d"]})
+    ct = ChunkedTable([a, b])
+    assert ct.nrows == 4 and ct.count() == 4
+    assert list(ct.schema.items()) == list(a.schema.items()) and ct.fieldNames == ["x", "s"] and "s" in ct
+    with pytest.raises(ValueError):
+        ChunkedTable([a, Table.from_pydict({"x": [1.5], "s": ["e"]})])
+    with pytest.raises(ValueError):
+        ChunkedTable([])

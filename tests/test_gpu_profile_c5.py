@@ -25,6 +25,10 @@ ROWS = int(float(os.environ.get("DQ_C5_ROWS", "1e6")))
 
 
 def c5_table(n, seed=5):
+    return Table.from_arrow(c5_arrow(n, seed))
+
+
+def c5_arrow(n, seed=5):
     import pyarrow as pa
     rng = np.random.default_rng(seed)
 
@@ -69,7 +73,7 @@ def c5_table(n, seed=5):
         if k == 3:  # some multi-byte UTF-8 (characters, not bytes, count for lengths; HLL hashes the bytes)
             txt = [t + "é" if i % 17 == 0 else t for i, t in enumerate(txt)]
         add("s_text%d" % k, strings(txt, nulls()), None)
-    return Table.from_arrow(pa.Table.from_arrays(arrays, names=names))
+    return pa.Table.from_arrays(arrays, names=names)
 
 
 def _close(a, b, rel=1e-12):
@@ -81,7 +85,38 @@ def test_c5_reduced_column_profile_against_oracle():
     assert len(t.columns) == 20
     exp = O.expected_profile(t)
     t.to_device()
-    prof = D.ColumnProfiler.profile(t)
+    _check_profile(t, D.ColumnProfiler.profile(t), exp)
+
+
+def test_c5_chunked_column_profile_against_oracle():
+    """The same table as 3 row chunks (ChunkedTable: how a shard whose string bytes exceed int32 offsets is held):
+    each pass runs per chunk and the chunk states merge with the reference's State.sum (HLL registers max, moments
+    Chan-merged, KLL sketches merged, DataType / histogram counts added) -- equal to the oracle over the whole
+    table, HLL estimates bit-exact."""
+    pat = c5_arrow(ROWS)
+    full = Table.from_arrow(pat)
+    exp = O.expected_profile(full)
+    cut = [0, ROWS // 3, ROWS // 3 + ROWS // 4 + 7, ROWS]
+    chunks = [Table.from_arrow(pat.slice(a, b - a)).to_device() for a, b in zip(cut, cut[1:])]
+    ct = D.ChunkedTable(chunks)
+    assert ct.nrows == ROWS
+    _check_profile(full, D.ColumnProfiler.profile(ct), exp)
+    # AnalysisRunner over the chunks equals the single-table run (scan, grouping and KLL analyzers)
+    an = [D.Size(), D.Completeness("s_int"), D.Mean("d_n100"), D.Sum("l_wide"), D.Maximum("l_neg"),
+          D.StandardDeviation("d_norm"), D.ApproxCountDistinct("s_text0"), D.Uniqueness(["s_cat50", "l_lowc"]),
+          D.Entropy("s_cat100"), D.Correlation("d_norm", "d_unif"), D.KLLSketch("d_unif")]
+    full.to_device()
+    want = D.AnalysisRunner.onData(full).addAnalyzers(an).run()
+    got = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in an:
+        w, g = want.metric(a).value.get(), got.metric(a).value.get()
+        if isinstance(a, D.KLLSketch):
+            assert sum(b.count for b in g.buckets) == sum(b.count for b in w.buckets), a
+        else:
+            assert _close(g, w), (a, g, w)
+
+
+def _check_profile(t, prof, exp):
     assert prof.numRecords == ROWS
     seen_hist = seen_numeric_string = 0
     for name, e in exp.items():
