@@ -828,7 +828,9 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             depth += wprog[p].b[i] >= 0 ? 1 : (wprog[p].b[i] == kPB_NOT ? 0 : -1);
             maxd = std::max(maxd, depth);
         }
-        for (int s = 0; s < (int)slots.size() && wp.producer < 0 && maxd <= kWhereStack; ++s) {
+        // (DQ_WHERE_FUSED=0: every masked filter from where_masks_kernel, the filter column a consumer -- A/B runs)
+        const bool fuse_producer = !(getenv("DQ_WHERE_FUSED") && getenv("DQ_WHERE_FUSED")[0] == '0');
+        for (int s = 0; s < (int)slots.size() && wp.producer < 0 && maxd <= kWhereStack && fuse_producer; ++s) {
             const SlotDesc& sd = slots[s];
             if (sd.kind != SK_VALUES || sd.ncols != 1 || slot_where(sd) != p) continue;
             const int x = (int)(intptr_t)sd.col[0].values;

@@ -526,9 +526,9 @@ constexpr int kKllMaxLevels = 64;
 
 // A bitmask of the levels whose buffer reached capacity makes condense's "lowest full level" one ctz, and an
 // update that finds no full level jumps straight to the next level-0 fill (nothing changes in between); the
-// compactions go to a per-thread buffer that keeps its pages across calls (~145k entries for 1e8 items).
-bool kll_schedule(int64_t n, int sketch_size, double f, KllSchedule& sc) {
-    static thread_local std::vector<uint64_t> events;
+// compactions go to the caller's buffer (~145k entries for 1e8 items).
+bool kll_schedule(int64_t n, int sketch_size, double f, KllSchedule& sc, std::vector<uint64_t>* out) {
+    std::vector<uint64_t>& events = *out;
     events.clear();
     sc.segs = &events;
     int64_t cap[kKllMaxLevels + 1];
@@ -786,223 +786,313 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     return (int64_t)o.size();
 }
 
+static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, int32_t sketch_size,
+                            double shrinking_factor, std::vector<std::vector<uint8_t>>& states);
+
 static int64_t kll_sketch_single(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t sketch_size,
                                  double shrinking_factor, uint8_t* state_out, int64_t capacity,
                                  std::vector<uint8_t>* keep) {
-    if (!ctx || !column || nrows < 0 || column->length != nrows || capacity < 0 || (capacity > 0 && !state_out))
-        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_kll_sketch: invalid arguments");
+    std::vector<std::vector<uint8_t>> st;
+    const int rc = kll_sketch_batch(ctx, column, 1, nrows, sketch_size, shrinking_factor, st);
+    if (rc != DQ_OK) return rc;
+    const std::vector<uint8_t>& o = st[0];
+    if (keep) *keep = o;
+    else if ((int64_t)o.size() <= capacity) memcpy(state_out, o.data(), o.size());
+    return (int64_t)o.size();
+}
+
+int64_t dq_kll_sketch_columns(dq_ctx* ctx, const dq_column* columns, int32_t ncols, int64_t nrows, int32_t sketch_size,
+                              double shrinking_factor, uint8_t* state_out, int64_t capacity, int64_t* sizes) {
+    if (!ctx || ncols < 0 || (ncols > 0 && (!columns || !sizes)) || nrows < 0 || capacity < 0 ||
+        (capacity > 0 && !state_out))
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_kll_sketch_columns: invalid arguments");
+    for (int i = 0; i < ncols; ++i)
+        if (columns[i].length != nrows)
+            return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_kll_sketch_columns: column length differs from nrows");
+    std::vector<std::vector<uint8_t>> st(ncols);
+    if (dq::ctx_num_subs(ctx) == 0) {
+        const int rc = kll_sketch_batch(ctx, columns, ncols, nrows, sketch_size, shrinking_factor, st);
+        if (rc != DQ_OK) return rc;
+    } else {  // multi-device context: each column through dq_kll_sketch's per-device partitions
+        for (int i = 0; i < ncols; ++i) {
+            const int64_t need = dq_kll_sketch(ctx, &columns[i], nrows, sketch_size, shrinking_factor, nullptr, 0);
+            if (need < 0) return need;
+            st[i].resize((size_t)need);
+            const int64_t got = dq_kll_sketch(ctx, &columns[i], nrows, sketch_size, shrinking_factor, st[i].data(), need);
+            if (got < 0) return got;
+        }
+    }
+    int64_t total = 0;
+    for (int i = 0; i < ncols; ++i) {
+        sizes[i] = (int64_t)st[i].size();
+        total += sizes[i];
+    }
+    if (total <= capacity) {
+        int64_t at = 0;
+        for (int i = 0; i < ncols; ++i) {
+            if (!st[i].empty()) memcpy(state_out + at, st[i].data(), st[i].size());
+            at += (int64_t)st[i].size();
+        }
+    }
+    return total;
+}
+
+// One call's columns, each one partition in row order: the NULL-compaction counts of every column, ONE host round
+// trip, the compaction schedules on parallel host threads, every column's dense write + compaction launches + final
+// gather queued on the stream, ONE more round trip, then each column's KLLState bytes.
+struct KColumnRun {
+    KllColumn kc;
+    bool zero_copy = false;
+    int64_t ntiles = 0, n = 0;
+    unsigned long long* doffs = nullptr;
+    const double* stream0 = nullptr;
+    KllSchedule sc;
+    std::vector<uint64_t> events;
+    std::vector<int64_t> lbase;
+    int64_t ntail = 0;
+    size_t pin_at = 0;          // this column's region of the pinned staging area
+    double* hgat = nullptr;     // pinned: gathered final buffers, then the 2 min / max keys
+};
+
+static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, int32_t sketch_size,
+                            double shrinking_factor, std::vector<std::vector<uint8_t>>& states) {
+    states.assign(ncols, std::vector<uint8_t>());
     if (!(shrinking_factor == shrinking_factor))
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_kll_sketch: shrinking factor is NaN");
-    const int t = column->spark_type;
-    // KLLRunner.emptySketches (R/KLLRunner.scala:118-145): Byte/Short/Int/Long/Float/Double only.
-    if (!(t == DQ_TYPE_BYTE || t == DQ_TYPE_SHORT || t == DQ_TYPE_INT || t == DQ_TYPE_LONG || t == DQ_TYPE_FLOAT ||
-          t == DQ_TYPE_DOUBLE))
-        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_kll_sketch: Cannot handle column type");
+    for (int i = 0; i < ncols; ++i) {
+        const int t = columns[i].spark_type;
+        if (!(t == DQ_TYPE_BYTE || t == DQ_TYPE_SHORT || t == DQ_TYPE_INT || t == DQ_TYPE_LONG || t == DQ_TYPE_FLOAT ||
+              t == DQ_TYPE_DOUBLE))
+            return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_kll_sketch: Cannot handle column type");
+    }
     const int dev = dq::ctx_device(ctx);
     KL_HIP(ctx, hipSetDevice(dev));
     hipStream_t s = dq::ctx_stream(ctx);
     KBuffers buf(ctx);
-
-    KllColumn kc;
-    kc.elem = elem_of(t);
-    const size_t vbytes = (size_t)nrows * elem_size(kc.elem);
-    const size_t bbytes = (size_t)(nrows + 63) / 64 * 8;
-    if (column->flags & DQ_COL_DEVICE) {
-        kc.values = column->values;
-        kc.validity = (const uint64_t*)column->validity;
-    } else {
-        void *v = nullptr, *m = nullptr;
-        KL_HIP(ctx, buf.alloc(&v, vbytes));
-        if (nrows) KL_HIP(ctx, hipMemcpyAsync(v, column->values, vbytes, hipMemcpyHostToDevice, s));
-        if (column->validity) {
-            KL_HIP(ctx, buf.alloc(&m, bbytes));
-            KL_HIP(ctx, hipMemsetAsync(m, 0, bbytes, s));
-            if (nrows)
-                KL_HIP(ctx, hipMemcpyAsync(m, column->validity, (size_t)(nrows + 7) / 8, hipMemcpyHostToDevice, s));
-        }
-        kc.values = v;
-        kc.validity = (const uint64_t*)m;
-    }
-
-    // ---- level-0 stream: the non-NULL values as doubles in row order -----------------------------
     const auto t0 = std::chrono::steady_clock::now();
-    const double* stream0 = nullptr;
-    int64_t n = nrows;
-    const bool zero_copy = kc.elem == ET_F64 && kc.validity == nullptr;
+    std::vector<KColumnRun> run(ncols);
     const int64_t ntiles = (nrows + kKllStageRows - 1) / kKllStageRows;
-    unsigned long long* doffs = nullptr;
-    if (zero_copy) {
-        stream0 = static_cast<const double*>(kc.values);
-    } else if (nrows > 0) {
-        unsigned int* dcounts = nullptr;
-        unsigned long long* dtotal = nullptr;
-        KL_HIP(ctx, buf.alloc((void**)&dcounts, sizeof(unsigned int) * ntiles));
-        KL_HIP(ctx, buf.alloc((void**)&doffs, sizeof(unsigned long long) * ntiles));
-        KL_HIP(ctx, buf.alloc((void**)&dtotal, sizeof(unsigned long long)));
-        unsigned long long* htotal = static_cast<unsigned long long*>(dq::ctx_pinned_buf(ctx, 8));
-        if (!htotal) return DQ_ERR_OUT_OF_MEMORY;
-        hipLaunchKernelGGL(kll_count_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows, dcounts);
-        hipLaunchKernelGGL(kll_scan_kernel, dim3(1), dim3(1024), 0, s, (const unsigned int*)dcounts, ntiles, doffs, dtotal);
-        KL_HIP(ctx, hipGetLastError());
-        KL_HIP(ctx, hipMemcpyAsync(htotal, dtotal, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    unsigned long long* dtotals = nullptr;
+    KL_HIP(ctx, buf.alloc((void**)&dtotals, sizeof(unsigned long long) * std::max(ncols, 1)));
+    int ncount = 0;
+    for (int i = 0; i < ncols; ++i) {
+        const dq_column* column = &columns[i];
+        KColumnRun& r = run[i];
+        r.kc.elem = elem_of(column->spark_type);
+        const size_t vbytes = (size_t)nrows * elem_size(r.kc.elem);
+        const size_t bbytes = (size_t)(nrows + 63) / 64 * 8;
+        if (column->flags & DQ_COL_DEVICE) {
+            r.kc.values = column->values;
+            r.kc.validity = (const uint64_t*)column->validity;
+        } else {
+            void *v = nullptr, *m = nullptr;
+            KL_HIP(ctx, buf.alloc(&v, vbytes));
+            if (nrows) KL_HIP(ctx, hipMemcpyAsync(v, column->values, vbytes, hipMemcpyHostToDevice, s));
+            if (column->validity) {
+                KL_HIP(ctx, buf.alloc(&m, bbytes));
+                KL_HIP(ctx, hipMemsetAsync(m, 0, bbytes, s));
+                if (nrows)
+                    KL_HIP(ctx, hipMemcpyAsync(m, column->validity, (size_t)(nrows + 7) / 8, hipMemcpyHostToDevice, s));
+            }
+            r.kc.values = v;
+            r.kc.validity = (const uint64_t*)m;
+        }
+        r.ntiles = ntiles;
+        r.zero_copy = r.kc.elem == ET_F64 && r.kc.validity == nullptr;
+        if (r.zero_copy) {
+            r.stream0 = static_cast<const double*>(r.kc.values);
+            r.n = nrows;
+        } else if (nrows > 0) {
+            unsigned int* dcounts = nullptr;
+            KL_HIP(ctx, buf.alloc((void**)&dcounts, sizeof(unsigned int) * ntiles));
+            KL_HIP(ctx, buf.alloc((void**)&r.doffs, sizeof(unsigned long long) * ntiles));
+            hipLaunchKernelGGL(kll_count_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, r.kc, nrows, dcounts);
+            hipLaunchKernelGGL(kll_scan_kernel, dim3(1), dim3(1024), 0, s, (const unsigned int*)dcounts, ntiles, r.doffs,
+                               dtotals + i);
+            KL_HIP(ctx, hipGetLastError());
+            ++ncount;
+        }
+    }
+    if (ncount) {  // one round trip for every column's non-NULL count
+        unsigned long long* htotals = static_cast<unsigned long long*>(dq::ctx_pinned_buf(ctx, 8 * (size_t)ncols));
+        if (!htotals) return DQ_ERR_OUT_OF_MEMORY;
+        KL_HIP(ctx, hipMemcpyAsync(htotals, dtotals, 8 * (size_t)ncols, hipMemcpyDeviceToHost, s));
         KL_HIP(ctx, hipStreamSynchronize(s));
-        n = (int64_t)*htotal;
-    } else {
-        n = 0;
+        for (int i = 0; i < ncols; ++i)
+            if (!run[i].zero_copy) run[i].n = nrows > 0 ? (int64_t)htotals[i] : 0;
     }
-
-    // the dense level-0 stream (a buffer of its own, so its write runs while the host computes the schedule)
-    if (!zero_copy && n > 0) {
+    // dense level-0 streams go out while the host computes the (count-only) compaction schedules
+    for (int i = 0; i < ncols; ++i) {
+        KColumnRun& r = run[i];
+        if (r.zero_copy || r.n <= 0) continue;
         double* dense = nullptr;
-        KL_HIP(ctx, buf.alloc((void**)&dense, (size_t)n * 8));
-        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, kc, nrows,
-                           (const unsigned long long*)doffs, dense);
+        KL_HIP(ctx, buf.alloc((void**)&dense, (size_t)r.n * 8));
+        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)r.ntiles), dim3(kKllStageBlock), 0, s, r.kc, nrows,
+                           (const unsigned long long*)r.doffs, dense);
         KL_HIP(ctx, hipGetLastError());
-        stream0 = dense;
+        r.stream0 = dense;
     }
-
-    // ---- the compaction schedule (count-only) ------------------------------------------------------
-    KllSchedule sc;
-    if (!kll_schedule(n, sketch_size, shrinking_factor, sc))
-        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_kll_sketch: sketch parameters need a compaction larger than 16384 items");
-    const size_t nlev = sc.levels.size();
+    {
+        std::vector<int> ok(ncols, 1);
+        auto work = [&](int i) { ok[i] = kll_schedule(run[i].n, sketch_size, shrinking_factor, run[i].sc, &run[i].events); };
+        if (ncols == 1) {
+            work(0);
+        } else {
+            std::vector<std::thread> th;
+            const int nth = std::min(ncols, std::max(1, (int)std::thread::hardware_concurrency()));
+            for (int w = 0; w < nth; ++w)
+                th.emplace_back([&, w]() {
+                    for (int i = w; i < ncols; i += nth) work(i);
+                });
+            for (auto& x : th) x.join();
+        }
+        for (int i = 0; i < ncols; ++i)
+            if (!ok[i])
+                return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED,
+                                    "dq_kll_sketch: sketch parameters need a compaction larger than 16384 items");
+    }
     const auto t1 = std::chrono::steady_clock::now();
 
-    // ---- device scratch (the context arena): [levels >= 1][descriptors][min/max][tails][gathered final buffers]
-    std::vector<int64_t> lbase(nlev, 0);
-    int64_t upper = 0;
-    for (size_t h = 1; h < nlev; ++h) {
-        lbase[h] = upper;
-        upper += sc.levels[h].arrived;
+    // pinned staging for every column: [segment descriptors][level tails][gathered final buffers + min / max keys]
+    size_t pin_total = 0;
+    for (KColumnRun& r : run) {
+        const size_t nlev = r.sc.levels.size(), nseg = r.events.size();
+        r.ntail = 0;
+        for (const KllLevel& l : r.sc.levels) r.ntail += l.len;
+        r.pin_at = pin_total;
+        pin_total += (nseg * 8 + nlev * sizeof(KllTail) + (size_t)r.ntail * 8 + 16 + 255) / 256 * 256;
     }
-    size_t nseg_all = 0;
-    nseg_all = sc.segs->size();
-    const size_t up_off = 0;
-    const size_t seg_off = up_off + ((size_t)upper * 8 + 255) / 256 * 256;
-    const size_t mm_off = seg_off + (nseg_all * 8 + 255) / 256 * 256;
-    int64_t ntail = 0;  // items left in the final buffers
-    for (const KllLevel& l : sc.levels) ntail += l.len;
-    const size_t tail_off = mm_off + 256;
-    const size_t gat_off = tail_off + (nlev * sizeof(KllTail) + 255) / 256 * 256;
-    uint8_t* scratch = static_cast<uint8_t*>(dq::ctx_scratch(ctx, gat_off + (size_t)ntail * 8 + 256));
-    if (!scratch) return DQ_ERR_OUT_OF_MEMORY;
-    double* dup = reinterpret_cast<double*>(scratch + up_off);
-    uint64_t* dsegs = reinterpret_cast<uint64_t*>(scratch + seg_off);
-    unsigned long long* dminmax = reinterpret_cast<unsigned long long*>(scratch + mm_off);
-
-    // compactions grouped per (level, kernel class), staged in pinned memory: one launch per group; the
-    // order inside a level is free because every compaction's input range and output slot are explicit
-    struct Launch {
-        size_t level, first, count;
-        int cls;
-    };
-    std::vector<Launch> launches;
-    // pinned staging: [segment descriptors][level tails][gathered final buffers + min / max keys]
-    const size_t pin_tails = nseg_all * 8, pin_out = pin_tails + nlev * sizeof(KllTail);
-    uint8_t* pin = static_cast<uint8_t*>(dq::ctx_pinned_buf(ctx, pin_out + (size_t)ntail * 8 + 16));
+    uint8_t* pin = static_cast<uint8_t*>(dq::ctx_pinned_buf(ctx, std::max<size_t>(pin_total, 16)));
     if (!pin) return DQ_ERR_OUT_OF_MEMORY;
-    uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin);
-    KllTail* htails = reinterpret_cast<KllTail*>(pin + pin_tails);
-    double* hgat = reinterpret_cast<double*>(pin + pin_out);
-    size_t pos = 0;
-    std::vector<size_t> cursor(nlev * kKllAllClasses);
-    for (size_t h = 0; h < nlev; ++h) {
-        const KllLevel& l = sc.levels[h];
-        for (int c = 0; c < kKllAllClasses; ++c) {
-            cursor[h * kKllAllClasses + c] = pos;
-            if (l.per_class[c]) launches.push_back({h, pos, (size_t)l.per_class[c], c});
-            pos += (size_t)l.per_class[c];
-        }
-    }
-    for (const uint64_t d : *sc.segs)  // grouped by (level, class), schedule order inside a group
-        hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
-    if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, s));
     const unsigned long long mm_init[2] = {~0ull, 0ull};
-    KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, s));
-    const auto t2 = std::chrono::steady_clock::now();
+    for (KColumnRun& r : run) {
+        KllSchedule& sc = r.sc;
+        const size_t nlev = sc.levels.size(), nseg_all = r.events.size();
+        r.lbase.assign(nlev, 0);
+        int64_t upper = 0;
+        for (size_t h = 1; h < nlev; ++h) {
+            r.lbase[h] = upper;
+            upper += sc.levels[h].arrived;
+        }
+        // device: [upper levels' streams][segment descriptors][min / max][level tails][gathered final buffers]
+        const size_t seg_off = ((size_t)upper * 8 + 255) / 256 * 256;
+        const size_t mm_off = seg_off + (nseg_all * 8 + 255) / 256 * 256;
+        const size_t tail_off = mm_off + 256;
+        const size_t gat_off = tail_off + (nlev * sizeof(KllTail) + 255) / 256 * 256;
+        uint8_t* scratch = nullptr;
+        KL_HIP(ctx, buf.alloc((void**)&scratch, gat_off + (size_t)r.ntail * 8 + 256));
+        double* dup = reinterpret_cast<double*>(scratch);
+        uint64_t* dsegs = reinterpret_cast<uint64_t*>(scratch + seg_off);
+        unsigned long long* dminmax = reinterpret_cast<unsigned long long*>(scratch + mm_off);
+        KllTail* dtails = reinterpret_cast<KllTail*>(scratch + tail_off);
+        double* dgat = reinterpret_cast<double*>(scratch + gat_off);
+        uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin + r.pin_at);
+        KllTail* htails = reinterpret_cast<KllTail*>(pin + r.pin_at + nseg_all * 8);
+        r.hgat = reinterpret_cast<double*>(pin + r.pin_at + nseg_all * 8 + nlev * sizeof(KllTail));
 
-    for (const Launch& L : launches) {  // a level that compacted always has a level above it
-        const size_t h = L.level;
-        const double* src = h == 0 ? stream0 : dup + lbase[h];
-        double* dst = dup + lbase[h + 1];
-        if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, s) != 0)
-            return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
-    }
-    if (getenv("DQ_KLL_TIMING")) {
-        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-            return std::chrono::duration<double, std::milli>(b - a).count();
+        // compactions grouped per (level, kernel class): one launch per group; the order inside a level is free
+        // because every compaction's input range and output slot are explicit
+        struct Launch {
+            size_t level, first, count;
+            int cls;
         };
-        fprintf(stderr, "[dq_kll_sketch] n=%lld levels=%zu compactions=%zu count+schedule %.2f ms, staging %.2f ms\n",
-                (long long)n, nlev, nseg_all, ms(t0, t1), ms(t1, t2));
-    }
-
-    // ---- final buffers: one gather + one read-back -------------------------------------------------
-    KllTail* dtails = reinterpret_cast<KllTail*>(scratch + tail_off);
-    double* dgat = reinterpret_cast<double*>(scratch + gat_off);
-    {
+        std::vector<Launch> launches;
+        size_t pos = 0;
+        std::vector<size_t> cursor(nlev * kKllAllClasses);
+        for (size_t h = 0; h < nlev; ++h) {
+            const KllLevel& l = sc.levels[h];
+            for (int c = 0; c < kKllAllClasses; ++c) {
+                cursor[h * kKllAllClasses + c] = pos;
+                if (l.per_class[c]) launches.push_back({h, pos, (size_t)l.per_class[c], c});
+                pos += (size_t)l.per_class[c];
+            }
+        }
+        for (const uint64_t d : r.events)  // grouped by (level, class), schedule order inside a group
+            hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
+        if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, s));
+        KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, s));
+        for (const Launch& L : launches) {  // a level that compacted always has a level above it
+            const size_t h = L.level;
+            const double* src = h == 0 ? r.stream0 : dup + r.lbase[h];
+            double* dst = dup + r.lbase[h + 1];
+            if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, s) != 0)
+                return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
+        }
+        // final buffers: one gather, one read-back (completed by the single synchronisation below)
         unsigned long long at = 0;
         for (size_t h = 0; h < nlev; ++h) {
             const KllLevel& l = sc.levels[h];
-            const double* src = (h == 0 ? stream0 : dup + lbase[h]) + l.pos;
+            const double* src = (h == 0 ? r.stream0 : dup + r.lbase[h]) + l.pos;
             htails[h] = KllTail{(unsigned long long)(uintptr_t)src, (unsigned long long)l.len, at};
             at += (unsigned long long)l.len;
         }
         KL_HIP(ctx, hipMemcpyAsync(dtails, htails, nlev * sizeof(KllTail), hipMemcpyHostToDevice, s));
-        if (ntail) hipLaunchKernelGGL(kll_gather_kernel, dim3((unsigned)nlev), dim3(256), 0, s, (const KllTail*)dtails, dgat);
+        if (r.ntail) hipLaunchKernelGGL(kll_gather_kernel, dim3((unsigned)nlev), dim3(256), 0, s, (const KllTail*)dtails, dgat);
         KL_HIP(ctx, hipGetLastError());
-        if (ntail) KL_HIP(ctx, hipMemcpyAsync(hgat, dgat, sizeof(double) * (size_t)ntail, hipMemcpyDeviceToHost, s));
-        KL_HIP(ctx, hipMemcpyAsync(hgat + ntail, dminmax, 16, hipMemcpyDeviceToHost, s));
-        KL_HIP(ctx, hipStreamSynchronize(s));
+        if (r.ntail) KL_HIP(ctx, hipMemcpyAsync(r.hgat, dgat, sizeof(double) * (size_t)r.ntail, hipMemcpyDeviceToHost, s));
+        KL_HIP(ctx, hipMemcpyAsync(r.hgat + r.ntail, dminmax, 16, hipMemcpyDeviceToHost, s));
     }
-    std::vector<std::vector<double>> fin(nlev);
-    {
+    const auto t2 = std::chrono::steady_clock::now();
+    KL_HIP(ctx, hipStreamSynchronize(s));
+    if (getenv("DQ_KLL_TIMING")) {
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        size_t nseg = 0;
+        for (const KColumnRun& r : run) nseg += r.events.size();
+        fprintf(stderr, "[dq_kll_sketch] columns=%d rows=%lld compactions=%zu counts+schedules %.2f ms, staging+launch %.2f ms, "
+                "device %.2f ms\n", ncols, (long long)nrows, nseg, ms(t0, t1), ms(t1, t2),
+                ms(t2, std::chrono::steady_clock::now()));
+    }
+
+    for (int i = 0; i < ncols; ++i) {
+        const KColumnRun& r = run[i];
+        const KllSchedule& sc = r.sc;
+        const size_t nlev = sc.levels.size();
+        std::vector<std::vector<double>> fin(nlev);
         int64_t at = 0;
         for (size_t h = 0; h < nlev; ++h) {
-            fin[h].assign(hgat + at, hgat + at + sc.levels[h].len);
+            fin[h].assign(r.hgat + at, r.hgat + at + sc.levels[h].len);
             at += sc.levels[h].len;
         }
-    }
-    unsigned long long mm[2];
-    memcpy(mm, hgat + ntail, sizeof(mm));
-
-    // UntypedQuantileNonSample.updateUntyped: math.min / math.max folds from Int.MaxValue.toDouble /
-    // Int.MinValue.toDouble (java.lang.Math: NaN-propagating, -0.0 < 0.0) = the order-key extremes
-    // of every item, NaN if any item is NaN.
-    uint64_t kmin = mm[0], kmax = mm[1];
-    for (double d : fin[0]) {
-        kmin = std::min<uint64_t>(kmin, host_key(d));
-        kmax = std::max<uint64_t>(kmax, host_key(d));
-    }
-    double vmin = 2147483647.0, vmax = -2147483648.0;
-    if (n > 0) {
-        const double lo = host_value(kmin), hi = host_value(kmax);
-        if (hi != hi) {
-            vmin = vmax = NAN;
-        } else {
-            vmin = host_key(lo) < host_key(vmin) ? lo : vmin;
-            vmax = host_key(hi) > host_key(vmax) ? hi : vmax;
+        unsigned long long mm[2];
+        memcpy(mm, r.hgat + r.ntail, sizeof(mm));
+        // UntypedQuantileNonSample.updateUntyped: math.min / math.max folds from Int.MaxValue.toDouble /
+        // Int.MinValue.toDouble (java.lang.Math: NaN-propagating, -0.0 < 0.0) = the order-key extremes
+        // of every item, NaN if any item is NaN.
+        uint64_t kmin = mm[0], kmax = mm[1];
+        for (double d : fin[0]) {
+            kmin = std::min<uint64_t>(kmin, host_key(d));
+            kmax = std::max<uint64_t>(kmax, host_key(d));
+        }
+        double vmin = 2147483647.0, vmax = -2147483648.0;
+        if (r.n > 0) {
+            const double lo = host_value(kmin), hi = host_value(kmax);
+            if (hi != hi) {
+                vmin = vmax = NAN;
+            } else {
+                vmin = host_key(lo) < host_key(vmin) ? lo : vmin;
+                vmax = host_key(hi) > host_key(vmax) ? hi : vmax;
+            }
+        }
+        // ---- KLLState bytes (big-endian ByteBuffer) -----------------------------------------------
+        std::vector<uint8_t>& o = states[i];
+        put_f64(o, vmin);
+        put_f64(o, vmax);
+        put_be32(o, sketch_size);
+        put_f64(o, shrinking_factor);
+        put_be32(o, (int32_t)nlev);              // curNumOfCompactors
+        put_be32(o, (int32_t)sc.actual);         // compactorActualSize
+        put_be32(o, (int32_t)sc.total);          // compactorTotalSize
+        put_be32(o, (int32_t)nlev);              // compactors.length
+        for (size_t h = 0; h < nlev; ++h) {
+            put_be32(o, sc.levels[h].ncomp);
+            put_be32(o, sc.levels[h].offset);
+            put_be32(o, (int32_t)fin[h].size());
+            for (double d : fin[h]) put_f64(o, d);
         }
     }
-
-    // ---- KLLState bytes (big-endian ByteBuffer) ---------------------------------------------------
-    std::vector<uint8_t> o;
-    put_f64(o, vmin);
-    put_f64(o, vmax);
-    put_be32(o, sketch_size);
-    put_f64(o, shrinking_factor);
-    put_be32(o, (int32_t)nlev);              // curNumOfCompactors
-    put_be32(o, (int32_t)sc.actual);         // compactorActualSize
-    put_be32(o, (int32_t)sc.total);          // compactorTotalSize
-    put_be32(o, (int32_t)nlev);              // compactors.length
-    for (size_t h = 0; h < nlev; ++h) {
-        put_be32(o, sc.levels[h].ncomp);
-        put_be32(o, sc.levels[h].offset);
-        put_be32(o, (int32_t)fin[h].size());
-        for (double d : fin[h]) put_f64(o, d);
-    }
-    if (keep) *keep = o;
-    else if ((int64_t)o.size() <= capacity) memcpy(state_out, o.data(), o.size());
-    return (int64_t)o.size();
+    return DQ_OK;
 }
 
 }  // extern "C"

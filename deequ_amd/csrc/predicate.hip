@@ -671,7 +671,18 @@ __global__ void __launch_bounds__(256)
 where_masks_kernel(const PredSimple P, const WhereOut* __restrict__ wo, const PredColumn* __restrict__ cols,
                    int64_t nrows, int64_t padded_words, SlotPartial* __restrict__ partials, int wslot, int gstride) {
     __shared__ int64_t red[2][4];
+    __shared__ const uint64_t* valid[kWhereMasks];
+    __shared__ uint64_t* mask[kWhereMasks];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nm = wo->nmasks;
+    const bool bitmaps = wo->bitmaps != 0;
+    uint64_t* const where_t = wo->where_t;
+    uint64_t* const where_nn = wo->where_nn;
+    if (threadIdx.x < kWhereMasks) {
+        valid[threadIdx.x] = wo->valid[threadIdx.x];
+        mask[threadIdx.x] = wo->mask[threadIdx.x];
+    }
+    __syncthreads();
     int64_t wt = 0, wnn = 0;
     const int64_t nchunks = (padded_words + kPredRows - 1) / kPredRows;  // kPredRows words per wave
     for (int64_t ch = (int64_t)blockIdx.x * 4 + wave; ch < nchunks; ch += (int64_t)gridDim.x * 4) {
@@ -729,14 +740,21 @@ where_masks_kernel(const PredSimple P, const WhereOut* __restrict__ wo, const Pr
             mine_t = lane == j ? bt : mine_t;
             mine_n = lane == j ? bn : mine_n;
         }
-        const int64_t w = w0 + lane;
-        if (lane < kPredRows && w < padded_words) {
-            const int nm = wo->nmasks;
-            for (int m = 0; m < nm; ++m) wo->mask[m][w] = valid_word(wo->valid[m], w, nrows) & mine_t;
-            if (wo->bitmaps) {
-                wo->where_t[w] = mine_t;
-                wo->where_nn[w] = mine_n;
-            }
+        // the chunk's kPredRows words x the consumer masks spread over the 64 lanes (lane L: word L % kPredRows of
+        // mask m0 + L / kPredRows): one validity load and one store per lane, the loads of a group all in flight
+        // before its stores (pointers from the kernel-start copies, so no store can alias them)
+        const int jw = lane % kPredRows;
+        const uint64_t word_t = __shfl(mine_t, jw, 64);
+        const int64_t w = w0 + jw;
+        for (int m0 = 0; m0 < nm; m0 += 64 / kPredRows) {  // wave-uniform
+            const int m = m0 + lane / kPredRows;
+            const bool on = m < nm && w < padded_words;
+            const uint64_t v = on ? valid_word(valid[m], w, nrows) : 0ull;
+            if (on) mask[m][w] = v & word_t;
+        }
+        if (bitmaps && lane < kPredRows && w0 + lane < padded_words) {
+            where_t[w0 + lane] = mine_t;
+            where_nn[w0 + lane] = mine_n;
         }
     }
     if (lane == 0) {

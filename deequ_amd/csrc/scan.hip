@@ -1638,45 +1638,70 @@ __device__ __forceinline__ uint32_t valid_dword(const uint64_t* vb, int64_t b0, 
 // Full tiles: the first kWherePf consumers' validity dwords of tile t are loaded together with the tile's values
 // (prefetch), so the mask stores never wait on a load issued after the next tile's prefetch (vmcnt is in order).
 constexpr int kWherePf = 8;
-__device__ __forceinline__ void where_prefetch(const WhereOut* __restrict__ wo, int64_t t, int tid,
-                                               uint32_t (&vd)[kWherePf]) {
-    const int nm = wo->nmasks;
+
+// A producer slot's WhereOut fields read once at the slot's start into wave-uniform registers: read through `wo` inside
+// the tile loop, every pointer was reloaded after each mask store (a store may alias the WhereOut) and every store
+// waited on that reload.
+struct WhereRegs {
+    const WhereOut* wo;
+    int nm, bitmaps;
+    const uint64_t* valid[kWherePf];
+    uint64_t* mask[kWherePf];
+    uint64_t* where_t;
+    uint64_t* where_nn;
+};
+__device__ __forceinline__ WhereRegs where_regs(const WhereOut* __restrict__ wo) {
+    WhereRegs r;
+    r.wo = wo;
+    r.nm = wo ? wo->nmasks : 0;
+    r.bitmaps = wo ? wo->bitmaps : 0;
+#pragma unroll
+    for (int k = 0; k < kWherePf; ++k) {
+        r.valid[k] = wo && k < r.nm ? wo->valid[k] : nullptr;
+        r.mask[k] = wo && k < r.nm ? wo->mask[k] : nullptr;
+    }
+    r.where_t = wo ? wo->where_t : nullptr;
+    r.where_nn = wo ? wo->where_nn : nullptr;
+    return r;
+}
+
+__device__ __forceinline__ void where_prefetch(const WhereRegs& W, int64_t t, int tid, uint32_t (&vd)[kWherePf]) {
     const int64_t b0 = t * (kTileRows / 8) + tid;
 #pragma unroll
-    for (int k = 0; k < kWherePf; ++k) vd[k] = (k < nm && (tid & 3) == 0) ? valid_dword(wo->valid[k], b0, 0, true) : 0u;
+    for (int k = 0; k < kWherePf; ++k) vd[k] = (k < W.nm && (tid & 3) == 0) ? valid_dword(W.valid[k], b0, 0, true) : 0u;
 }
 
 // Writes a full tile's producer outputs from the prefetched validity (stores only; consumers past kWherePf load).
-__device__ __forceinline__ void where_emit_full(const WhereOut* __restrict__ wo, int64_t t, int tid, uint32_t w,
-                                                uint32_t wn, const uint32_t (&vd)[kWherePf]) {
+__device__ __forceinline__ void where_emit_full(const WhereRegs& W, int64_t t, int tid, uint32_t w, uint32_t wn,
+                                                const uint32_t (&vd)[kWherePf]) {
     const int lane = tid & 63;
     const uint32_t pw = quad_pack(w, lane);
     const uint32_t pn = quad_pack(wn, lane);
     if ((lane & 3) != 0) return;
     const int64_t b0 = t * (kTileRows / 8) + tid;
-    const int nm = wo->nmasks;
 #pragma unroll
     for (int k = 0; k < kWherePf; ++k)
-        if (k < nm) *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->mask[k]) + b0) = vd[k] & pw;
-    for (int m = kWherePf; m < nm; ++m) {  // wave-uniform, rare
-        const uint32_t v = valid_dword(wo->valid[m], b0, 0, true);
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->mask[m]) + b0) = v & pw;
+        if (k < W.nm) *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(W.mask[k]) + b0) = vd[k] & pw;
+    for (int m = kWherePf; m < W.nm; ++m) {  // wave-uniform, rare
+        const uint32_t v = valid_dword(W.wo->valid[m], b0, 0, true);
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(W.wo->mask[m]) + b0) = v & pw;
     }
-    if (wo->bitmaps) {
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->where_t) + b0) = pw;
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->where_nn) + b0) = pn;
+    if (W.bitmaps) {
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(W.where_t) + b0) = pw;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(W.where_nn) + b0) = pn;
     }
 }
 
 // Writes the producer's outputs for tile t: per consumer valid & where TRUE, and the where bitmaps if asked for.
-__device__ __forceinline__ void where_emit(const WhereOut* __restrict__ wo, int64_t t, int tid, uint32_t w, uint32_t wn,
-                                           bool full, int64_t vbytes) {
+__device__ __forceinline__ void where_emit(const WhereRegs& W, int64_t t, int tid, uint32_t w, uint32_t wn, bool full,
+                                           int64_t vbytes) {
     const int lane = tid & 63;
     const uint32_t pw = quad_pack(w, lane);
     const uint32_t pn = quad_pack(wn, lane);
     if ((lane & 3) != 0) return;
     const int64_t b0 = t * (kTileRows / 8) + tid;  // this quad's first bitmap byte
-    const int nm = wo->nmasks;
+    const int nm = W.nm;
+    const WhereOut* __restrict__ wo = W.wo;
     // 8 consumers at a time: their validity loads are all in flight before the first store waits on one
     for (int m0 = 0; m0 < nm; m0 += 8) {  // wave-uniform
         uint32_t vd[8];
@@ -1686,9 +1711,9 @@ __device__ __forceinline__ void where_emit(const WhereOut* __restrict__ wo, int6
         for (int k = 0; k < 8; ++k)
             if (m0 + k < nm) *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->mask[m0 + k]) + b0) = vd[k] & pw;
     }
-    if (wo->bitmaps) {
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->where_t) + b0) = pw;
-        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(wo->where_nn) + b0) = pn;
+    if (W.bitmaps) {
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(W.where_t) + b0) = pw;
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(W.where_nn) + b0) = pn;
     }
 }
 
@@ -1717,6 +1742,7 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
         const bool corr = NC > 1 && (FULL || sd.corr);
         const bool has_where = WP || (!FULL && sd.where_t != nullptr);
         const WhereOut* __restrict__ wo = sd.wout;
+        const WhereRegs wr = where_regs(WP ? wo : nullptr);
         const int64_t vbytes = (nrows + 7) >> 3;
         const bool need0 = corr || h0.stats || h0.moments || c0.pred_kind != FP_NONE;
         const bool need1 = corr || h1.stats || h1.moments || c1.pred_kind != FP_NONE;
@@ -1756,7 +1782,7 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
         uint32_t bx = 0xFF, by = 0xFF, bw = 0xFF, bn = 0xFF;
         uint32_t vdc[WP ? kWherePf : 1], vdn[WP ? kWherePf : 1];
         if constexpr (WP) {
-            if (t < nfull) where_prefetch(wo, t, tid, vdc);
+            if (t < nfull) where_prefetch(wr, t, tid, vdc);
         }
         if (t < nfull) {
             heavy_load(c0, t, tid, x);
@@ -1778,7 +1804,7 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                 const uint32_t e = where_eval8<F0>(wo->prog, x, bx, 0xFFu);
                 bw = e & 0xFFu;
                 bn = e >> 8;
-                where_emit_full(wo, t, tid, bw, bn, vdc);
+                where_emit_full(wr, t, tid, bw, bn, vdc);
             }
             if (tn < nfull) {
                 heavy_load(c0, tn, tid, xn);
@@ -1791,7 +1817,7 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                     nbw = heavy_bits(sd.where_t, tn, tid);
                     nbn = heavy_bits(sd.where_nn, tn, tid);
                 }
-                if constexpr (WP) where_prefetch(wo, tn, tid, vdn);
+                if constexpr (WP) where_prefetch(wr, tn, tid, vdn);
             }
             fold(x, y, bx, by, bw, bn);
             if constexpr (WP) {
@@ -1822,7 +1848,7 @@ scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict
                 const uint32_t e = where_eval8<F0>(wo->prog, x, mx, w);
                 wn = e >> 8;
                 w = e & 0xFFu;
-                where_emit(wo, nfull, tid, w, wn, false, vbytes);
+                where_emit(wr, nfull, tid, w, wn, false, vbytes);
             } else if (has_where) {
                 wn = w & heavy_bits(sd.where_nn, nfull, tid);
                 w &= heavy_bits(sd.where_t, nfull, tid);

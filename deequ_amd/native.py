@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = (
     "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts", "dq_synth_strings",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
-    "dq_scan_streamed", "dq_scan_kernel_launches",
+    "dq_scan_streamed", "dq_scan_kernel_launches", "dq_kll_sketch_columns",
 )
 
 
@@ -189,6 +189,8 @@ def load_library(path=None):
                                               c_void_p, c_void_p]),
             "dq_kll_sketch": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_int32, ctypes.c_double, c_void_p,
                                         c_int64]),
+            "dq_kll_sketch_columns": (c_int64, [c_void_p, c_void_p, ctypes.c_int32, c_int64, ctypes.c_int32,
+                                                ctypes.c_double, c_void_p, c_int64, c_void_p]),
             "dq_cast_column": (c_int, [c_void_p, c_void_p, c_int64, ctypes.c_int32, c_void_p, c_void_p]),
             "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
             "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
@@ -372,6 +374,26 @@ class Context:
                 self.check(int(n), "dq_kll_sketch")
             if n <= cap:
                 return buf[:n].tobytes()
+            cap = int(n)
+
+    def kll_sketch_columns(self, columns, nrows, sketch_size, shrinking_factor):
+        """dq_kll_sketch_columns: the KLLState bytes of each column (one partition each, rows in order), sketched in
+        one call (parallel host schedules, one round trip)."""
+        arr = (DqColumn * max(len(columns), 1))(*columns)
+        sizes = np.zeros(max(len(columns), 1), dtype=np.int64)
+        cap = 1 << 18
+        while True:
+            buf = np.empty(cap, dtype=np.uint8)
+            n = self.lib.dq_kll_sketch_columns(self.handle, arr, len(columns), int(nrows), int(sketch_size),
+                                               float(shrinking_factor), buf.ctypes.data, cap, sizes.ctypes.data)
+            if n < 0:
+                self.check(int(n), "dq_kll_sketch_columns")
+            if n <= cap:
+                out, at = [], 0
+                for k in range(len(columns)):
+                    out.append(buf[at:at + int(sizes[k])].tobytes())
+                    at += int(sizes[k])
+                return out
             cap = int(n)
 
     def cast_column(self, column, nrows, to_type, values_dev_ptr, validity_dev_ptr):

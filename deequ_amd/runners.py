@@ -248,11 +248,19 @@ class KLLRunner:
         params = {}
         for a in analyzers:  # columnsAndParameters: `.toMap`, the last analyzer of a column wins
             params[a.column] = a.kllParameters
-        sketches = {}
+        from .kll import KLLState
+        by_params = {}
         for column, p in params.items():
             size, f = (p.sketchSize, p.shrinkingFactor) if p is not None else \
                 (DEFAULT_SKETCH_SIZE, DEFAULT_SHRINKING_FACTOR)
-            sketches[column] = KLLRunner.sketch_column(data, column, size, f)
+            if data.schema[column] not in KLLRunner._SUPPORTED:  # KLLRunner.emptySketches (:118-145)
+                raise ValueError("Cannot handle %s" % data.schema[column])
+            by_params.setdefault((size, f), []).append(column)
+        sketches = {}
+        for (size, f), cols in by_params.items():  # one pass over the columns sharing sketch parameters
+            raws = engine.ctx().kll_sketch_columns([data[c].native() for c in cols], data.nrows, size, f)
+            for c, raw in zip(cols, raws):
+                sketches[c] = KLLState.fromBytes(raw)
         results = {}
         for a in analyzers:
             results[a] = a.calculateMetric(sketches[a.column], aggregateWith, saveStatesTo)

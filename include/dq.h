@@ -367,6 +367,15 @@ int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows,
 int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32_t sketch_size,
                       double shrinking_factor, uint8_t* state_out, int64_t capacity);
 
+/* The KLL extra pass over several columns of one table at once (R/KLLRunner.scala:91-112 sketches every KLL column
+ * in one pass over the partitions): column i's KLLState bytes, exactly those of dq_kll_sketch, go to
+ * state_out + (sum of sizes[0..i)) and sizes[i] receives their length. Returns the total length (nothing is written
+ * when it exceeds `capacity`: call again with a larger buffer) or a negative dq_status. The columns' compaction
+ * schedules are computed on parallel host threads and every column's kernels are queued on the stream with one host
+ * round trip for all of them. */
+int64_t dq_kll_sketch_columns(dq_ctx* ctx, const dq_column* columns, int32_t ncols, int64_t nrows, int32_t sketch_size,
+                              double shrinking_factor, uint8_t* state_out, int64_t capacity, int64_t* sizes);
+
 /* ColumnProfiler.castColumn (M/profiles/ColumnProfiler.scala:346-355): Spark 2.2 Cast of a column to LONG or
  * DOUBLE. STRING sources: UTF8String.toLong (no trimming, optional sign, digits, optional '.' + digits truncated,
  * overflow NULL) / java.lang.Double.parseDouble (correctly rounded); strings that do not parse become NULL.

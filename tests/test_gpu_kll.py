@@ -167,3 +167,25 @@ def test_sketch_large_properties():
     for i in (0, 9, 49, 89, 98):
         r = int(torch.searchsorted(srt, torch.tensor([qs[i]], dtype=torch.float64, device="cuda"))) / n
         assert abs(r - (i + 1) / 100) < 0.005
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_kll_sketch_columns_equals_per_column_sketches(device):
+    """dq_kll_sketch_columns (one call, parallel host schedules, one round trip) gives every column exactly the bytes
+    of its own dq_kll_sketch, and of the oracle: six columns of different types, null shares and lengths of their
+    non-NULL streams (0, a few, 1e5, 3e5 items)."""
+    n = 300_001
+    rng = np.random.default_rng(21)
+    cols = {"d": rng.normal(100.0, 15.0, n), "f": rng.random(n).astype(np.float32),
+            "l": rng.integers(-2 ** 50, 2 ** 50, n, dtype=np.int64), "i": rng.integers(-1000, 1000, n).astype(np.int32),
+            "none": rng.random(n), "few": rng.random(n)}
+    valid = {"d": rng.random(n) > 0.05, "f": None, "l": rng.random(n) > 0.5, "i": rng.random(n) > 0.9,
+             "none": np.zeros(n, dtype=bool), "few": rng.random(n) < 3e-5}
+    t = Table.from_arrays(cols, validity={k: v for k, v in valid.items() if v is not None})
+    if device:
+        t.to_device(0)
+    names = list(cols)
+    batch = engine.ctx().kll_sketch_columns([t[c].native() for c in names], t.nrows, 2048, 0.64)
+    for c, raw in zip(names, batch):
+        assert raw == gpu_bytes(t, c), c
+        assert raw == O.kll_state_bytes(non_null(cols[c], valid[c]).astype(np.float64), 2048, 0.64), c

@@ -1,5 +1,6 @@
-"""Cost of a `where` filter on the C2 suite (1e9 rows): the predicate pass reads the filter's column and writes two
-bitmaps before the scan. Prints the dq_scan HIP-event time without / with `where`, and a where-only Compliance."""
+"""Cost of a `where` filter on the C2 suite (1e9 rows). Prints the dq_scan HIP-event time without / with `where`
+(the filter produced by its own column's scan, DQ_WHERE_FUSED=1, and by where_masks_kernel with the filter column a
+consumer, DQ_WHERE_FUSED=0, interleaved), and a where-only Compliance."""
 import os
 import sys
 
@@ -29,7 +30,11 @@ for c in names:
 cases["c2_where_c4<0"] = cw
 cases["compliance_c4<0"] = [D.Compliance("neg", "c4 < 0")]
 cases["compliance_c4<0_or_c5>1"] = [D.Compliance("neg", "c4 < 0 OR c5 > 1")]
-for name, an in cases.items():
+runs = [(name, an, None) for name, an in cases.items()]
+runs += [("c2_where_c4<0 fused=%s" % f, cw, f) for f in ("1", "0", "1", "0")]
+for name, an, fused in runs:
+    if fused is not None:
+        os.environ["DQ_WHERE_FUSED"] = fused
     wl = bench.ScanWorkload(torch, N, D, ctx, t, an, stream, dev, 1, "nccl")
     _, ms, _ = bench.timed(torch, None, 1, 10, 2, stream, wl.step)
     print("%-26s %8.3f ms  %.3e rows/s" % (name, ms, rows / ms * 1e3), flush=True)
