@@ -200,39 +200,29 @@ __device__ __forceinline__ void kll_reg_sort(uint64_t (&v)[E]) {
     for (int r = 0; r < E; ++r) v[r] = w[r];
 }
 
-template <int T, int E>
-__global__ void __launch_bounds__(T)
-kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
-                   unsigned long long* __restrict__ minmax) {
-    constexpr int PAD = T * E;
-    __shared__ uint64_t k[PAD + T];
+// One merge round of the LDS merge sort: thread t's E keys (registers) are the sorted run it holds; runs of w keys are
+// merged pairwise. The thread finds its output window of the merged pair on the merge path (binary search on the
+// diagonal), loads the next E keys of both inputs at once (2E independent LDS reads, not a chain of E dependent ones)
+// and keeps the E smallest of them with a register network: min against the reversed B window (a bitonic half-cleaner:
+// the E smallest of two sorted windows) then a bitonic merge of those E. Equal keys are equal values, so which input a
+// tied key comes from does not matter. Out-of-range keys read as ~0 (no key is ~0: kll_key(NaN) = 0xfff8...).
+template <int E>
+__device__ __forceinline__ void kll_merge_round(uint64_t* k, uint64_t (&v)[E], int t, int w) {
     auto at = [](int i) { return i + i / E; };
-    const uint64_t sg = segs[blockIdx.x];
-    const uint64_t start = sg & ((1ull << 40) - 1);
-    const int len = (int)((sg >> 40) & 0x7FFF);
-    const int t = threadIdx.x;
-    const double* in = src + start;
-    uint64_t v[E];
 #pragma unroll
-    for (int r = 0; r < E; ++r) {
-        const int i = t * E + r;
-        v[r] = i < len ? kll_key(in[i]) : ~0ull;
+    for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
+    __syncthreads();
+    const int diag = E * (t & (2 * (w / E) - 1));  // offset inside the merged pair (w / E is a power of 2)
+    const int A = (t * E) - diag, B = A + w;
+    int lo = diag > w ? diag - w : 0, hi = diag < w ? diag : w;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (k[at(A + mid)] <= k[at(B + diag - 1 - mid)]) lo = mid + 1;
+        else hi = mid;
     }
-    kll_reg_sort<E>(v);
-    for (int w = E; w < PAD; w <<= 1) {
-#pragma unroll
-        for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
-        __syncthreads();
-        const int diag = E * (t & (2 * (w / E) - 1));  // offset inside the merged pair (w / E is a power of 2)
-        const int A = (t * E) - diag, B = A + w;
-        int lo = diag > w ? diag - w : 0, hi = diag < w ? diag : w;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (k[at(A + mid)] <= k[at(B + diag - 1 - mid)]) lo = mid + 1;
-            else hi = mid;
-        }
-        int ai = A + lo, bi = B + diag - lo;
-        const int aend = A + w, bend = B + w;
+    int ai = A + lo, bi = B + diag - lo;
+    const int aend = A + w, bend = B + w;
+    if constexpr ((E & (E - 1)) != 0) {  // E = 12: the sequential merge (the network below needs a power of two)
         uint64_t ah = ai < aend ? k[at(ai)] : ~0ull, bh = bi < bend ? k[at(bi)] : ~0ull;
 #pragma unroll
         for (int r = 0; r < E; ++r) {
@@ -248,7 +238,52 @@ kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ 
             }
         }
         __syncthreads();
+        return;
     }
+    uint64_t a[E], b[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        a[r] = ai + r < aend ? k[at(ai + r)] : ~0ull;
+        b[r] = bi + r < bend ? k[at(bi + r)] : ~0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const uint64_t x = a[r], y = b[E - 1 - r];
+        v[r] = x < y ? x : y;
+    }
+    // v is bitonic (non-increasing after non-decreasing): sort it ascending
+#pragma unroll
+    for (int stride = E / 2; stride > 0; stride >>= 1)
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            if ((r & stride) == 0) {
+                const uint64_t x = v[r], y = v[r + stride];
+                const bool sw = x > y;
+                v[r] = sw ? y : x;
+                v[r + stride] = sw ? x : y;
+            }
+    __syncthreads();
+}
+
+template <int T, int E>
+__global__ void __launch_bounds__(T)
+kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
+                   unsigned long long* __restrict__ minmax) {
+    constexpr int PAD = T * E;
+    __shared__ uint64_t k[PAD + T];
+    const uint64_t sg = segs[blockIdx.x];
+    const uint64_t start = sg & ((1ull << 40) - 1);
+    const int len = (int)((sg >> 40) & 0x7FFF);
+    const int t = threadIdx.x;
+    const double* in = src + start;
+    uint64_t v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int i = t * E + r;
+        v[r] = i < len ? kll_key(in[i]) : ~0ull;
+    }
+    kll_reg_sort<E>(v);
+    for (int w = E; w < PAD; w <<= 1) kll_merge_round<E>(k, v, t, w);
     // picks: sorted index i = t*E + r with i = offset + 2j, j < len/2
     const int half = len >> 1;
     const int off = (int)(sg >> 63);
@@ -303,36 +338,7 @@ kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict_
     uint64_t xk = ~0ull;
     if (t < XM && t < rx) xk = kll_key(in[P + t]);
     kll_reg_sort<E>(v);
-    for (int w = E; w < P; w <<= 1) {
-#pragma unroll
-        for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
-        __syncthreads();
-        const int diag = E * (t & (2 * (w / E) - 1));
-        const int A = (t * E) - diag, B = A + w;
-        int lo = diag > w ? diag - w : 0, hi = diag < w ? diag : w;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (k[at(A + mid)] <= k[at(B + diag - 1 - mid)]) lo = mid + 1;
-            else hi = mid;
-        }
-        int ai = A + lo, bi = B + diag - lo;
-        const int aend = A + w, bend = B + w;
-        uint64_t ah = ai < aend ? k[at(ai)] : ~0ull, bh = bi < bend ? k[at(bi)] : ~0ull;
-#pragma unroll
-        for (int r = 0; r < E; ++r) {
-            const bool takeA = bi >= bend || (ai < aend && ah <= bh);
-            if (takeA) {
-                v[r] = ah;
-                ++ai;
-                ah = ai < aend ? k[at(ai)] : ~0ull;
-            } else {
-                v[r] = bh;
-                ++bi;
-                bh = bi < bend ? k[at(bi)] : ~0ull;
-            }
-        }
-        __syncthreads();
-    }
+    for (int w = E; w < P; w <<= 1) kll_merge_round<E>(k, v, t, w);
     // the sorted main array in LDS (the extras' ranks) and the extras sorted by wave 0
 #pragma unroll
     for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
@@ -852,7 +858,28 @@ struct KColumnRun {
     int64_t ntail = 0;
     size_t pin_at = 0;          // this column's region of the pinned staging area
     double* hgat = nullptr;     // pinned: gathered final buffers, then the 2 min / max keys
+    struct Launch {
+        size_t level, first, count;
+        int cls;
+    };
+    std::vector<Launch> launches;  // compactions grouped per (level, kernel class)
 };
+
+// Runs work(i) for i < n on up to hardware-concurrency host threads (inline when n == 1).
+extern "C++" template <typename F>
+static void kll_parallel(int n, F work) {
+    if (n <= 1) {
+        if (n == 1) work(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int nth = std::min(n, std::max(1, (int)std::thread::hardware_concurrency()));
+    for (int w = 0; w < nth; ++w)
+        th.emplace_back([&, w]() {
+            for (int i = w; i < n; i += nth) work(i);
+        });
+    for (auto& x : th) x.join();
+}
 
 static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, int32_t sketch_size,
                             double shrinking_factor, std::vector<std::vector<uint8_t>>& states) {
@@ -934,18 +961,9 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
     }
     {
         std::vector<int> ok(ncols, 1);
-        auto work = [&](int i) { ok[i] = kll_schedule(run[i].n, sketch_size, shrinking_factor, run[i].sc, &run[i].events); };
-        if (ncols == 1) {
-            work(0);
-        } else {
-            std::vector<std::thread> th;
-            const int nth = std::min(ncols, std::max(1, (int)std::thread::hardware_concurrency()));
-            for (int w = 0; w < nth; ++w)
-                th.emplace_back([&, w]() {
-                    for (int i = w; i < ncols; i += nth) work(i);
-                });
-            for (auto& x : th) x.join();
-        }
+        kll_parallel(ncols, [&](int i) {
+            ok[i] = kll_schedule(run[i].n, sketch_size, shrinking_factor, run[i].sc, &run[i].events);
+        });
         for (int i = 0; i < ncols; ++i)
             if (!ok[i])
                 return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED,
@@ -964,6 +982,26 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
     }
     uint8_t* pin = static_cast<uint8_t*>(dq::ctx_pinned_buf(ctx, std::max<size_t>(pin_total, 16)));
     if (!pin) return DQ_ERR_OUT_OF_MEMORY;
+    // every column's descriptors grouped per (level, kernel class) straight into its pinned region, on the host threads
+    kll_parallel(ncols, [&](int i) {
+        KColumnRun& r = run[i];
+        const KllSchedule& sc = r.sc;
+        const size_t nlev = sc.levels.size();
+        uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin + r.pin_at);
+        size_t pos = 0;
+        std::vector<size_t> cursor(nlev * kKllAllClasses);
+        r.launches.clear();
+        for (size_t h = 0; h < nlev; ++h) {
+            const KllLevel& l = sc.levels[h];
+            for (int c = 0; c < kKllAllClasses; ++c) {
+                cursor[h * kKllAllClasses + c] = pos;
+                if (l.per_class[c]) r.launches.push_back({h, pos, (size_t)l.per_class[c], c});
+                pos += (size_t)l.per_class[c];
+            }
+        }
+        for (const uint64_t d : r.events)  // schedule order inside a group
+            hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
+    });
     const unsigned long long mm_init[2] = {~0ull, 0ull};
     for (KColumnRun& r : run) {
         KllSchedule& sc = r.sc;
@@ -990,28 +1028,11 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
         KllTail* htails = reinterpret_cast<KllTail*>(pin + r.pin_at + nseg_all * 8);
         r.hgat = reinterpret_cast<double*>(pin + r.pin_at + nseg_all * 8 + nlev * sizeof(KllTail));
 
-        // compactions grouped per (level, kernel class): one launch per group; the order inside a level is free
-        // because every compaction's input range and output slot are explicit
-        struct Launch {
-            size_t level, first, count;
-            int cls;
-        };
-        std::vector<Launch> launches;
-        size_t pos = 0;
-        std::vector<size_t> cursor(nlev * kKllAllClasses);
-        for (size_t h = 0; h < nlev; ++h) {
-            const KllLevel& l = sc.levels[h];
-            for (int c = 0; c < kKllAllClasses; ++c) {
-                cursor[h * kKllAllClasses + c] = pos;
-                if (l.per_class[c]) launches.push_back({h, pos, (size_t)l.per_class[c], c});
-                pos += (size_t)l.per_class[c];
-            }
-        }
-        for (const uint64_t d : r.events)  // grouped by (level, class), schedule order inside a group
-            hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
+        // one launch per (level, kernel class) group; the order inside a level is free because every compaction's
+        // input range and output slot are explicit
         if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, s));
         KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, s));
-        for (const Launch& L : launches) {  // a level that compacted always has a level above it
+        for (const KColumnRun::Launch& L : r.launches) {  // a level that compacted always has a level above it
             const size_t h = L.level;
             const double* src = h == 0 ? r.stream0 : dup + r.lbase[h];
             double* dst = dup + r.lbase[h + 1];

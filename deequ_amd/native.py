@@ -381,7 +381,7 @@ class Context:
         one call (parallel host schedules, one round trip)."""
         arr = (DqColumn * max(len(columns), 1))(*columns)
         sizes = np.zeros(max(len(columns), 1), dtype=np.int64)
-        cap = 1 << 18
+        cap = (1 << 18) * max(len(columns), 1)  # a default sketch's state is ~40 KB: one call, not a size probe + a rerun
         while True:
             buf = np.empty(cap, dtype=np.uint8)
             n = self.lib.dq_kll_sketch_columns(self.handle, arr, len(columns), int(nrows), int(sketch_size),
