@@ -88,6 +88,7 @@ struct KeySpec {
     int32_t string_null_is_value;  // Histogram on a string column: NULL == "NullValue"
     uint64_t seed;         // fingerprint seed (general path)
     const long long* weights;  // per-row counts (pre-aggregated (key, count) input), nullptr = 1 per row
+    uint64_t fp_mask;      // general-path fingerprint bits kept (~0; the collision tests narrow it: DQ_FREQ_FP_MASK)
 };
 
 // A group: 64-bit key and its 64-bit count (Spark counts with Long: a key seen >= 2^32 times is exact).
@@ -187,7 +188,7 @@ __device__ __forceinline__ bool row_key(const KeySpec& ks, int64_t r, uint64_t& 
         acc = mix64(acc + P64_1 * (uint64_t)(i + 1) + ch);
     }
     if (!any && !ks.include_nulls) return false;
-    h = acc == kEmpty ? kEmpty - 1 : acc;
+    h = (acc == kEmpty ? kEmpty - 1 : acc) & ks.fp_mask;
     return true;
 }
 
@@ -1095,6 +1096,124 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
     if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->overflow, 1ull);
 }
 
+// ---- small general tables: one fused pass -------------------------------------------------------------
+// When the sizing estimate puts a general-path table (string / multi-column keys, unweighted) in one region (bits = 0,
+// <= kRegionTarget distinct keys: the Histograms of low-cardinality columns the ColumnProfiler's third pass computes),
+// the extract-write / build / verify passes collapse into one: every workgroup takes a contiguous chunk of rows in
+// tiles, inserts each tile's fingerprints into its LDS table (count, smallest row), then checks each of the tile's rows
+// against its slot's representative while both rows are still cache-hot (rows arrive in order, so once a tile is
+// inserted a representative never changes again); the workgroup tables merge into region 0 with global atomics and
+// publish their representatives, which small_check_kernel compares with the final (smallest) one. Exact: a fingerprint
+// collision anywhere raises `mismatch` and the build reruns with a new seed; a full table raises `overflow` and the
+// build takes the regular path.
+constexpr int kSmallTile = 4 * kBuildBlock;
+constexpr int kSmallGrid = 256;
+
+__global__ void __launch_bounds__(kBuildBlock)
+small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
+                   unsigned long long* __restrict__ wg_keys, unsigned long long* __restrict__ wg_reps,
+                   Counters* __restrict__ ctr) {
+    __shared__ unsigned long long lkey[kRegion];
+    __shared__ unsigned int lcnt[kRegion];
+    __shared__ unsigned long long lrep[kRegion];
+    __shared__ unsigned long long red[kBuildBlock / 64];
+    __shared__ unsigned int lovf;
+    for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
+        lkey[i] = kEmpty;
+        lcnt[i] = 0;
+        lrep[i] = ~0ull;
+    }
+    if (threadIdx.x == 0) lovf = 0;
+    __syncthreads();
+    int64_t r0, r1;
+    chunk_of(nrows, r0, r1);
+    unsigned long long bad = 0;
+    bool ok = true;
+    for (int64_t t0 = r0; t0 < r1; t0 += kSmallTile) {
+        uint64_t h[4];
+        bool take[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t r = t0 + (int64_t)u * kBuildBlock + threadIdx.x;
+            bool ng = false;
+            h[u] = kEmpty;
+            take[u] = r < r1 && row_key(ks, r, h[u], ng) && !ng && h[u] != kEmpty;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (take[u])
+                ok &= lds_insert<unsigned int>(lkey, lcnt, lrep, h[u], (unsigned long long)(t0 + (int64_t)u * kBuildBlock +
+                                                                                    threadIdx.x), 1u, true);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!take[u]) continue;
+            const int64_t r = t0 + (int64_t)u * kBuildBlock + threadIdx.x;
+            unsigned int p = region_probe(h[u]);
+            for (int probe = 0; probe < kRegion && lkey[p] != h[u]; ++probe) p = (p + 1) & (kRegion - 1);
+            const unsigned long long rep = lrep[p];
+            if (lkey[p] != h[u] || (rep != (unsigned long long)r && !rows_equal(ks, r, (int64_t)rep))) ++bad;
+        }
+        __syncthreads();
+    }
+    if (!ok) lovf = 1;
+    __syncthreads();
+    // publish this workgroup's groups and merge them into region 0
+    bool mok = true;
+    for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
+        const unsigned long long key = lkey[i];
+        wg_keys[(uint64_t)blockIdx.x * kRegion + i] = key;
+        wg_reps[(uint64_t)blockIdx.x * kRegion + i] = lrep[i];
+        if (key == kEmpty) continue;
+        unsigned int p = region_probe(key);
+        bool done = false;
+        for (int probe = 0; probe < kRegion; ++probe) {
+            const unsigned long long prev = atomicCAS(&slots[p].key, kEmpty, key);
+            if (prev == kEmpty || prev == key) {
+                atomicAdd(&slots[p].count, (unsigned long long)lcnt[i]);
+                atomicMin(&reps[p], lrep[i]);
+                done = true;
+                break;
+            }
+            p = (p + 1) & (kRegion - 1);
+        }
+        mok &= done;
+    }
+    if (!mok) lovf = 1;
+    for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bad;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = 0;
+        for (int w = 0; w < kBuildBlock / 64; ++w) b += red[w];
+        if (b) atomicAdd(&ctr->mismatch, b);
+        if (lovf) atomicAdd(&ctr->overflow, 1ull);
+    }
+}
+
+// Every workgroup's representative of a group against the group's final (smallest-row) representative.
+__global__ void __launch_bounds__(kBuildBlock)
+small_check_kernel(KeySpec ks, const Slot* __restrict__ slots, const unsigned long long* __restrict__ reps,
+                   const unsigned long long* __restrict__ wg_keys, const unsigned long long* __restrict__ wg_reps,
+                   Counters* __restrict__ ctr) {
+    unsigned long long bad = 0;
+    for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
+        const unsigned long long key = wg_keys[(uint64_t)blockIdx.x * kRegion + i];
+        if (key == kEmpty) continue;
+        const unsigned long long wrep = wg_reps[(uint64_t)blockIdx.x * kRegion + i];
+        unsigned int p = region_probe(key);
+        int probe = 0;
+        for (; probe < kRegion && slots[p].key != key; ++probe) p = (p + 1) & (kRegion - 1);
+        if (probe == kRegion) {
+            ++bad;
+            continue;
+        }
+        const unsigned long long grep = reps[p];
+        if (grep != wrep && !rows_equal(ks, (int64_t)wrep, (int64_t)grep)) ++bad;
+    }
+    if (bad) atomicAdd(&ctr->mismatch, bad);
+}
+
 // ---- table scans ---------------------------------------------------------------------------------
 
 __global__ void __launch_bounds__(kFreqBlock)
@@ -1519,6 +1638,50 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     return DQ_OK;
 }
 
+// Small general tables (bits = 0): small_build_kernel + small_check_kernel, the table one region. *overflow sends the
+// caller to the regular path, *collision to a new seed.
+int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* overflow, bool* collision) {
+    hipStream_t s = dq::ctx_stream(ctx);
+    release_slots(t, ctx);
+    t->home = ctx;
+    t->slots_bytes = kRegion * sizeof(Slot);
+    t->reps_bytes = kRegion * sizeof(unsigned long long);
+    t->slots = (Slot*)dq::scratch_alloc(ctx, t->slots_bytes);
+    if (t->slots) t->reps = (unsigned long long*)dq::scratch_alloc(ctx, t->reps_bytes);
+    if (!t->slots || !t->reps) return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
+    t->cap = kRegion;
+    t->bits = 0;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(kSmallGrid, (nrows + kSmallTile - 1) / kSmallTile));
+    BuildItem* ditem = nullptr;
+    unsigned long long *wk = nullptr, *wr = nullptr;
+    FQ_HIP(ctx, buf.alloc((void**)&ditem, sizeof(BuildItem)));
+    FQ_HIP(ctx, buf.alloc((void**)&wk, (size_t)grid * kRegion * 8));
+    FQ_HIP(ctx, buf.alloc((void**)&wr, (size_t)grid * kRegion * 8));
+    const BuildItem it = {0ull, 0ull, 0u, 1u};  // split = 1: region_init clears region 0
+    FQ_HIP(ctx, hipMemcpyAsync(ditem, &it, sizeof(it), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(region_init_kernel, dim3(1), dim3(kFreqBlock), 0, s, ditem, 1, t->slots, t->reps);
+    hipLaunchKernelGGL(small_build_kernel, dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots, t->reps, wk, wr,
+                       t->ctr);
+    hipLaunchKernelGGL(small_check_kernel, dim3(grid), dim3(kBuildBlock), 0, s, t->ks, t->slots, t->reps, wk, wr, t->ctr);
+    FQ_HIP(ctx, hipGetLastError());
+    FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    FQ_HIP(ctx, hipStreamSynchronize(s));
+    t->pre_valid = 0;  // the summary scans the one region
+    if (getenv("DQ_DEBUG_FREQ"))
+        fprintf(stderr, "[freq small] rows=%lld grid=%d rows_taken=%llu ovf=%llu mis=%llu\n", (long long)nrows, grid,
+                t->host_ctr.num_rows, t->host_ctr.overflow, t->host_ctr.mismatch);
+    *overflow = t->host_ctr.overflow != 0;
+    *collision = t->host_ctr.mismatch != 0;
+    if (*overflow || *collision) {  // the caller rebuilds: clear the flags the rebuild reads
+        Counters c = t->host_ctr;
+        c.overflow = 0;
+        c.mismatch = 0;
+        FQ_HIP(ctx, hipMemcpyAsync(t->ctr, &c, sizeof(Counters), hipMemcpyHostToDevice, s));
+        FQ_HIP(ctx, hipStreamSynchronize(s));  // `c` lives on this stack frame
+    }
+    return DQ_OK;
+}
+
 // Radix-partition path (8 <= bits <= kMaxPartBits): rows -> 256 partitions (pass 1, fed by the count pass's
 // per-workgroup digit histograms) -> buckets (pass 2 on the next bits - 8 bits) -> regions.
 constexpr int kMaxPartBits = 20;
@@ -1816,6 +1979,17 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         if (getenv("DQ_DEBUG_FREQ"))
             fprintf(stderr, "[freq] rows=%lld n=%llu est=%.1f bits=%d\n", (long long)nrows, n, est, bits);
         bool collision = false;
+        if (general && !t->ks.weights && bits == 0 && n > 0 && !getenv("DQ_FREQ_NO_SMALL")) {
+            bool overflow = false;
+            const int rc = build_small(ctx, t, nrows, buf, &overflow, &collision);
+            if (rc != DQ_OK) return rc;
+            if (!overflow && !collision) return DQ_OK;
+            if (collision) {
+                t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
+                continue;
+            }
+            collision = false;  // a full table: the regular path below
+        }
         if (!no_partition && n > 0 && bits >= 8 && bits <= kMaxPartBits) {
             const int rc = build_partitioned(ctx, t, nrows, buf, xgrid, hist1, n, bits, &collision);
             if (rc != DQ_OK) return rc;
@@ -2393,6 +2567,8 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
     t->ks.string_null_is_value = (t->ks.include_nulls && nkeys == 1 && t->ks.cols[0].spark_type == DQ_TYPE_STRING);
     t->fast = t->ks.fast;
     t->ks.seed = 0x243F6A8885A308D3ULL;
+    t->ks.fp_mask = ~0ull;
+    if (const char* m = getenv("DQ_FREQ_FP_MASK")) t->ks.fp_mask = strtoull(m, nullptr, 0);
 
     FQ_HIP(ctx, hipMalloc(&t->ctr, sizeof(Counters)));
     int rc = build_table(ctx, t, nrows);

@@ -233,6 +233,16 @@ class FrequencyTable:
             return (self._decode_value(int(k)),)
         return self._key_of_row(int(k))
 
+    def _decode_many(self, keys):
+        """_decode over many keys; a representative-row table gathers every key column's cells in one batch."""
+        if self.key_kind() == N.FREQ_KEYS_VALUES:
+            return [(self._decode_value(int(k)),) for k in keys]
+        cols = [c.cells_at(keys) for c in self.key_columns]
+        out = []
+        for i in range(len(keys)):
+            out.append(tuple(GroupFloat(col[i]) if isinstance(col[i], float) else col[i] for col in cols))
+        return out
+
     def top(self, k):
         """[(key tuple, count)] of the k largest groups (NULL group included for Histogram)."""
         k = int(min(k, self.num_groups))
@@ -241,7 +251,8 @@ class FrequencyTable:
         n = self.ctx.lib.dq_freq_top(self.ctx.handle, self.handle, k, keys.ctypes.data, counts.ctypes.data)
         if n < 0:
             raise N.NativeError(int(n), "dq_freq_top: %s" % self.ctx.last_error())
-        out = [(self._decode(keys[i]), int(counts[i])) for i in range(n)]
+        dec = self._decode_many(keys[:n])
+        out = [(dec[i], int(counts[i])) for i in range(n)]
         nulls = self.summary(None)["null_count"]
         if nulls:
             out.append(((None,) * max(len(self.names), 1), int(nulls)))
@@ -256,7 +267,8 @@ class FrequencyTable:
         got = self.ctx.lib.dq_freq_export(self.ctx.handle, self.handle, n, keys.ctypes.data, counts.ctypes.data)
         if got < 0:
             raise N.NativeError(int(got), "dq_freq_export: %s" % self.ctx.last_error())
-        out = {self._decode(keys[i]): int(counts[i]) for i in range(got)}
+        dec = self._decode_many(keys[:got])
+        out = {dec[i]: int(counts[i]) for i in range(got)}
         nulls = self.summary(None)["null_count"]
         if nulls:
             out[(None,) * max(len(self.names), 1)] = int(nulls)

@@ -127,6 +127,49 @@ class Column:
             v = t[i:i + 1].cpu().numpy().astype(dt)[0]
         return self._decode_cell(v)
 
+    def cells_at(self, rows):
+        """The cells of `rows` (None for NULL) in one go: for a device-only column, one gather per buffer and one copy
+        back each (the representatives of a table's groups), instead of a device round trip per row."""
+        rows = np.asarray(rows, dtype=np.int64)
+        if len(rows) == 0:
+            return []
+        if not (self.values is None and self.device is not None):
+            return [self.value_at(int(r)) if self.valid_at(int(r)) else None for r in rows]
+        import torch
+        d = self.device
+        dev = d["values"].device
+        idx = torch.from_numpy(rows).to(dev)
+        if d.get("validity") is not None:
+            vb = d["validity"][idx >> 3].cpu().numpy()
+            valid = ((vb >> (rows & 7).astype(np.uint8)) & 1).astype(bool)
+        else:
+            valid = np.ones(len(rows), dtype=bool)
+        if self.spark_type == N.TYPE_STRING:
+            off = d["offsets"]
+            lo = off[idx].to(torch.int64)
+            hi = off[idx + 1].to(torch.int64)
+            lens = (hi - lo).cpu().numpy()
+            total = int(lens.sum())
+            if total:
+                starts = np.repeat(lo.cpu().numpy() - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)
+                pos = torch.from_numpy(starts + np.arange(total, dtype=np.int64)).to(dev)
+                data = d["values"][pos].cpu().numpy().tobytes()
+            else:
+                data = b""
+            out, at = [], 0
+            for ok, n in zip(valid, lens):
+                out.append(data[at:at + int(n)].decode("utf-8") if ok else None)
+                at += int(n)
+            return out
+        t = d["values"]
+        dt = np.dtype(NUMPY_OF[self.spark_type])
+        if str(t.dtype) == "torch.uint8" and dt.itemsize > 1:
+            pos = (idx[:, None] * dt.itemsize + torch.arange(dt.itemsize, device=dev)[None, :]).reshape(-1)
+            vals = t[pos].cpu().numpy().view(dt)
+        else:
+            vals = t[idx].cpu().numpy().astype(dt)
+        return [self._decode_cell(v) if ok else None for v, ok in zip(vals, valid)]
+
     def _decode_cell(self, v):
         if self.spark_type == N.TYPE_BOOLEAN:
             return bool(v)

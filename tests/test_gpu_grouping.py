@@ -8,6 +8,7 @@ import pytest
 
 import deequ_amd as D
 import deequ_amd.native as N
+from deequ_amd.native import NativeError
 from deequ_amd import engine
 from deequ_amd.table import Table, Column, pack_validity
 import oracle as O
@@ -239,3 +240,50 @@ def test_fast_build_equals_exact_build(case, monkeypatch):
         assert np.array_equal(kf, ke) and np.array_equal(cf, ce), case
         assert [c for _, c in fast.top(5)] == [c for _, c in exact.top(5)]
         del fast, exact
+
+
+def _freq_dict(t, cols, include_nulls=False, env=None):
+    import os
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        ft = engine.frequencies(t, cols, include_nulls=include_nulls)
+        return ft.to_dict(), ft.summary(None)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_small_table_path_equals_the_regular_path(device):
+    """Small general-path tables (<= ~2600 distinct string / multi-column keys) take the fused one-pass build
+    (small_build_kernel + small_check_kernel); its groups, counts, NULL handling (Histogram's "NullValue") and
+    summary equal the regular extract / build / verify path (DQ_FREQ_NO_SMALL=1) and the oracle, over 3e5 rows in
+    many workgroups (groups seen by several workgroups, representatives merged to the smallest row)."""
+    rng = np.random.default_rng(17)
+    n = 300_001
+    words = np.array(["w%d" % i for i in range(700)] + ["", "NullValue", "ü" * 3, "x" * 60], dtype=object)
+    s = [None if rng.random() < 0.05 else words[rng.integers(0, len(words))] for _ in range(n)]
+    k = [None if rng.random() < 0.1 else int(rng.integers(0, 3)) for _ in range(n)]
+    t = Table.from_pydict({"s": s, "k": k}, types={"s": "string", "k": "int"})
+    if device:
+        t.to_device(0)
+    for cols, nulls in ((["s"], True), (["s"], False), (["s", "k"], False), (["s", "k"], True)):
+        small, ssum = _freq_dict(t, cols, nulls)
+        regular, rsum = _freq_dict(t, cols, nulls, {"DQ_FREQ_NO_SMALL": "1"})
+        assert small == regular, cols
+        assert ssum == rsum, (cols, ssum, rsum)
+    _summary_vs_oracle(t, ["s", "k"])
+
+
+def test_fingerprint_collisions_are_never_merged():
+    """Fingerprints narrowed to 4 bits (DQ_FREQ_FP_MASK) collide on every seed: both the small path and the regular
+    path detect the collisions against the representatives and fail the build instead of merging groups."""
+    words = ["w%d" % i for i in range(40)]
+    t = Table.from_pydict({"s": [words[i % 40] for i in range(5000)]}, types={"s": "string"})
+    for extra in ({}, {"DQ_FREQ_NO_SMALL": "1"}):
+        with pytest.raises(NativeError):
+            _freq_dict(t, ["s"], False, dict(extra, DQ_FREQ_FP_MASK="0xF"))
