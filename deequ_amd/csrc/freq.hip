@@ -228,6 +228,7 @@ struct Counters {
     unsigned long long overflow;   // probe limit hit: rebuild bigger
     unsigned long long mismatch;   // general path verification: fingerprint collisions
     unsigned long long pad[3];
+    unsigned long long narrow_miss;  // fast path, narrow keys: 8-byte keys outside the 32-bit window
 };
 
 __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, unsigned long long* lds4) {
@@ -703,21 +704,26 @@ __device__ __forceinline__ uint64_t canonical_of(int elem, uint64_t raw) {
 // One tile already in registers (h, keep) -> LDS staging ordered by digit -> global runs reserved with atomics:
 // digit b's run goes to bucket k = bucket_of(b), at k * cap + atomicAdd(&gcursor[k], hist[b]), when it fits the
 // bucket's capacity; otherwise *lovf is raised and nothing more is written.
-template <int BINS, int TILE, typename BucketOf, typename CounterOf, typename Prefetch>
+// NARROW: the staged word is (digit << 32) | 32-bit payload and the payload is what goes out (narrow keys, below);
+// otherwise the staged word is the key itself, its digit (key >> shift) & mask.
+template <int BINS, int TILE, bool NARROW, typename BucketOf, typename CounterOf, typename Prefetch, typename OutT>
 __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / kFreqBlock], unsigned int keepm,
                                                      int shift, unsigned int mask, unsigned int* hist, unsigned int* start,
                                                      unsigned long long* cursor, unsigned long long* sh,
                                                      unsigned long long* __restrict__ gcursor, unsigned long long cap,
                                                      BucketOf bucket_of, CounterOf counter_of, unsigned int* lovf,
                                                      unsigned int* lbad,
-                                                     unsigned long long limit, unsigned long long* __restrict__ out_h,
+                                                     unsigned long long limit, OutT* __restrict__ out_h,
                                                      Prefetch prefetch) {
     constexpr int PER = TILE / kFreqBlock;
     static_assert(PER <= 32, "keep flags are one bit per key");
+    auto digit = [shift, mask](uint64_t v) {
+        return NARROW ? (unsigned int)(v >> 32) : (unsigned int)(v >> shift) & mask;
+    };
     unsigned int rank[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j)
-        rank[j] = ((keepm >> j) & 1u) ? atomicAdd(&hist[(unsigned int)(h[j] >> shift) & mask], 1u) : 0u;
+        rank[j] = ((keepm >> j) & 1u) ? atomicAdd(&hist[digit(h[j])], 1u) : 0u;
     __syncthreads();
     constexpr int RUN = BINS / kFreqBlock > 0 ? BINS / kFreqBlock : 1;
     __shared__ unsigned int wsum[kFreqBlock / 64];
@@ -763,15 +769,15 @@ __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / 
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         if (!((keepm >> j) & 1u)) continue;
-        sh[start[(unsigned int)(h[j] >> shift) & mask] + rank[j]] = h[j];
+        sh[start[digit(h[j])] + rank[j]] = h[j];
     }
     __syncthreads();
     if (!*lovf) {  // (uniform: read after the barrier that follows every write of the flag)
         for (unsigned int i = threadIdx.x; i < total; i += kFreqBlock) {
             const unsigned long long hv = sh[i];
-            const unsigned int d = (unsigned int)(hv >> shift) & mask;
+            const unsigned int d = digit(hv);
             const unsigned long long pos = cursor[d] + (i - start[d]);
-            if (pos < limit) out_h[pos] = hv;  // always true; a violated invariant is reported, never written
+            if (pos < limit) out_h[pos] = (OutT)hv;  // always true; a violated invariant is reported, never written
             else *lbad = 1u;
         }
     }
@@ -780,15 +786,32 @@ __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / 
     __syncthreads();
 }
 
+// Narrow keys: when every key's canonical value fits 32 bits around a base (keys of <= 4-byte columns always; 8-byte
+// integral keys when a sample of the column spans < 2^31), the partition buffers hold the 32-bit offset from the base
+// instead of the 64-bit mixed key, and pass 2 / the build re-derive the key as mix64(base + offset): the two partition
+// passes move 4 bytes per key instead of 8 in every write and every re-read. An 8-byte key outside the window raises
+// Counters::narrow_miss in pass 1 and the build restarts with 64-bit keys.
+struct NarrowKey {
+    unsigned long long base;
+    int sx;  // the offset is sign-extended (<= 4-byte signed columns)
+    int pad;
+};
+
+__device__ __forceinline__ uint64_t narrow_canon(const NarrowKey& nk, uint32_t p) {
+    return nk.base + (nk.sx ? (uint64_t)(int64_t)(int32_t)p : (uint64_t)p);
+}
+
 // Fast pass 1: rows -> 256 partitions x 8 XCD sub-regions of `cap` keys each (sub-region (d, x) at (8 d + x) * cap),
 // plus the side counters and the
 // sizing registers (per workgroup, reduced by sizing_reduce_kernel). W = the key column's cell width. The next
 // tile's cells are loaded while the current tile is scattered (after its reservation atomics returned).
-template <int TILE, int W>
+template <int TILE, int W, bool NARROW>
 __global__ void __launch_bounds__(kFreqBlock)
 partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long long cap,
-                       unsigned long long* __restrict__ gcursor, unsigned long long* __restrict__ out_h,
-                       uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr) {
+                       unsigned long long* __restrict__ gcursor, void* __restrict__ out,
+                       uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, NarrowKey nk) {
+    using OutT = typename std::conditional<NARROW, uint32_t, unsigned long long>::type;
+    OutT* __restrict__ out_h = static_cast<OutT*>(out);
     constexpr int PER = TILE / kFreqBlock;
     __shared__ unsigned int hist[kDigitBins], start[kDigitBins];
     __shared__ unsigned long long cursor[kDigitBins];
@@ -800,7 +823,7 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
     hist[threadIdx.x] = 0;
     if (threadIdx.x == 0) lovf = lbad = 0;
     __syncthreads();
-    unsigned long long taken = 0, sent = 0, nulls = 0;
+    unsigned long long taken = 0, sent = 0, nulls = 0, miss = 0;
     const int64_t ntiles = (nrows + TILE - 1) / TILE;
     const bool has_validity = c.validity != nullptr;
     // workgroups are dealt round-robin to the XCDs: each XCD's workgroups fill their own sub-region of every
@@ -822,13 +845,20 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t t0 = tile * TILE;
         uint64_t h[PER];
+        uint32_t pay[PER];
         unsigned int keepm = 0;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const int64_t r = t0 + (int64_t)j * kFreqBlock + threadIdx.x;
             const bool in = r < nrows;
             const bool valid = (vbyte[j] >> (r & 7)) & 1u;
-            h[j] = mix64(canonical_of<W>(c.elem, raw[j]));
+            const uint64_t canon = canonical_of<W>(c.elem, raw[j]);
+            h[j] = mix64(canon);
+            if (NARROW) {
+                const uint64_t off = canon - nk.base;
+                pay[j] = (uint32_t)off;
+                if (W == 8 && valid && (off >> 32)) ++miss;
+            }
             const bool keep = valid && h[j] != kEmpty;
             keepm |= (keep ? 1u : 0u) << j;
             taken += (valid || (in && include_nulls)) ? 1 : 0;
@@ -846,7 +876,11 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
             const unsigned int rank = (unsigned int)__clzll((long long)((h[j] << 10) | (1ull << 9))) + 1u;
             if (rank > regs[idx]) atomicMax(&regs[idx], rank);
         }
-        scatter_tile_reserve<kDigitBins, TILE>(h, keepm, 0, kDigitBins - 1, hist, start, cursor, sh, gcursor, cap,
+        if (NARROW) {
+#pragma unroll
+            for (int j = 0; j < PER; ++j) h[j] = ((h[j] & (kDigitBins - 1)) << 32) | pay[j];
+        }
+        scatter_tile_reserve<kDigitBins, TILE, NARROW>(h, keepm, 0, kDigitBins - 1, hist, start, cursor, sh, gcursor, cap,
                                                [xcd](int b) { return (unsigned long long)b * kXcds + xcd; },
                                                [xcd](int b) { return ((unsigned long long)b * kXcds + xcd) * kCursorStride; },
                                                &lovf, &lbad, cap * kDigitBins * kXcds, out_h, [&]() {
@@ -856,10 +890,12 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
     taken = block_sum_u64(taken, red);
     sent = block_sum_u64(sent, red);
     nulls = block_sum_u64(nulls, red);
+    if (NARROW && W == 8) miss = block_sum_u64(miss, red);
     if (threadIdx.x == 0) {
         if (taken) atomicAdd(&ctr->num_rows, taken);
         if (sent) atomicAdd(&ctr->sentinel, sent);
         if (nulls) atomicAdd(&ctr->nulls, nulls);
+        if (miss) atomicAdd(&ctr->narrow_miss, miss);
         if (lovf) atomicAdd(&ctr->pad[0], 1ull);
         if (lbad) atomicAdd(&ctr->pad[2], 1ull);
     }
@@ -877,11 +913,14 @@ struct FastItem {
 // Fast pass 2: per work item (a chunk of one partition), keys -> bucket part + 256 * (next bits), bucket k at
 // k * cap; its reservation counter is part * bins + b, so a partition's counters share lines only with each other.
 // The next tile is loaded before the current one is scattered.
-template <int BINS, int TILE>
+template <int BINS, int TILE, bool NARROW>
 __global__ void __launch_bounds__(kFreqBlock)
-scatter2_fast_kernel(const FastItem* __restrict__ items, const unsigned long long* __restrict__ in_h, unsigned int mask,
-                     unsigned long long cap, unsigned long long* __restrict__ gcursor, unsigned long long* __restrict__ out_h,
-                     Counters* __restrict__ ctr) {
+scatter2_fast_kernel(const FastItem* __restrict__ items, const void* __restrict__ in, unsigned int mask,
+                     unsigned long long cap, unsigned long long* __restrict__ gcursor, void* __restrict__ out,
+                     Counters* __restrict__ ctr, NarrowKey nk) {
+    using KeyT = typename std::conditional<NARROW, uint32_t, unsigned long long>::type;
+    const KeyT* __restrict__ in_h = static_cast<const KeyT*>(in);
+    KeyT* __restrict__ out_h = static_cast<KeyT*>(out);
     constexpr int PER = TILE / kFreqBlock;
     __shared__ unsigned int hist[BINS], start[BINS];
     __shared__ unsigned long long cursor[BINS];
@@ -892,22 +931,24 @@ scatter2_fast_kernel(const FastItem* __restrict__ items, const unsigned long lon
     if (threadIdx.x == 0) lovf = lbad = 0;
     __syncthreads();
     const unsigned long long part = it.part;
-    uint64_t nxt[PER];
+    KeyT nxt[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const unsigned long long i = it.begin + (unsigned long long)j * kFreqBlock + threadIdx.x;
-        nxt[j] = i < it.end ? __builtin_nontemporal_load(&in_h[i]) : kEmpty;
+        nxt[j] = i < it.end ? __builtin_nontemporal_load(&in_h[i]) : (KeyT)kEmpty;
     }
     for (unsigned long long t0 = it.begin; t0 < it.end; t0 += TILE) {
         uint64_t h[PER];
         unsigned int keepm = 0;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            h[j] = nxt[j];
+            // narrow: the digit comes from the re-derived key, the payload travels on
+            h[j] = NARROW ? ((((mix64(narrow_canon(nk, (uint32_t)nxt[j])) >> 8) & mask)) << 32) | (uint64_t)nxt[j]
+                          : (uint64_t)nxt[j];
             keepm |= (t0 + (unsigned long long)j * kFreqBlock + threadIdx.x < it.end ? 1u : 0u) << j;
         }
         const unsigned long long n0 = t0 + TILE;
-        scatter_tile_reserve<BINS, TILE>(h, keepm, 8, mask, hist, start, cursor, sh, gcursor, cap,
+        scatter_tile_reserve<BINS, TILE, NARROW>(h, keepm, 8, mask, hist, start, cursor, sh, gcursor, cap,
                                          [part](int b) { return part + (unsigned long long)kDigitBins * b; },
                                          [part, mask](int b) { return part * (mask + 1ull) + b; }, &lovf, &lbad,
                                          cap * kDigitBins * (mask + 1ull), out_h, [&]() {
@@ -915,7 +956,7 @@ scatter2_fast_kernel(const FastItem* __restrict__ items, const unsigned long lon
 #pragma unroll
                 for (int j = 0; j < PER; ++j) {
                     const unsigned long long i = n0 + (unsigned long long)j * kFreqBlock + threadIdx.x;
-                    nxt[j] = i < it.end ? __builtin_nontemporal_load(&in_h[i]) : kEmpty;
+                    nxt[j] = i < it.end ? __builtin_nontemporal_load(&in_h[i]) : (KeyT)kEmpty;
                 }
             }
         });
@@ -986,12 +1027,14 @@ __device__ __forceinline__ bool lds_insert(unsigned long long* lkey, C* lcnt, un
 // #groups, #(count == 1), max count, sum -(c/N) ln(c/N)) is folded into the build: a whole-bucket item knows its
 // region's final counts in LDS, so it writes its summary partial (parts[item]) and the table is never re-read for
 // the default N; a slice of a split bucket flags its partial (pad = 1) and the host scans the table instead.
-template <bool GENERAL, bool WEIGHTED>
+// NARROW: `hs` holds 32-bit narrow-key offsets (fast path), the key is mix64(base + offset).
+template <bool GENERAL, bool WEIGHTED, bool NARROW = false>
 __global__ void __launch_bounds__(kBuildBlock)
 build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
              const unsigned long long* __restrict__ rows, const long long* __restrict__ weights,
              Slot* __restrict__ slots, unsigned long long* __restrict__ reps, Counters* __restrict__ ctr,
-             SummaryPartial* __restrict__ parts, double n) {
+             SummaryPartial* __restrict__ parts, double n, NarrowKey nk) {
+    const uint32_t* __restrict__ hs32 = reinterpret_cast<const uint32_t*>(hs);
     using C = typename std::conditional<WEIGHTED, unsigned long long, unsigned int>::type;
     __shared__ unsigned long long lkey[kRegion];
     __shared__ C lcnt[kRegion];
@@ -1012,7 +1055,10 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u) {
             const unsigned long long j = j0 + (unsigned long long)u * kBuildBlock;
-            h[u] = j < it.end ? hs[j] : kEmpty;
+            if (NARROW)
+                h[u] = j < it.end ? mix64(narrow_canon(nk, hs32[j])) : kEmpty;
+            else
+                h[u] = j < it.end ? hs[j] : kEmpty;
             rw[u] = ((GENERAL || WEIGHTED) && j < it.end) ? rows[j] : 0ull;
         }
 #pragma unroll
@@ -1107,24 +1153,26 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
 // collision anywhere raises `mismatch` and the build reruns with a new seed; a full table raises `overflow` and the
 // build takes the regular path.
 constexpr int kSmallTile = 4 * kBuildBlock;
-constexpr int kSmallGrid = 256;
+constexpr int kSmallGrid = 768;  // 3 workgroups per CU with the 2048-slot table
 
+template <int LS>  // slots of the workgroup's LDS table
 __global__ void __launch_bounds__(kBuildBlock)
 small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
                    unsigned long long* __restrict__ wg_keys, unsigned long long* __restrict__ wg_reps,
                    Counters* __restrict__ ctr) {
-    __shared__ unsigned long long lkey[kRegion];
-    __shared__ unsigned int lcnt[kRegion];
-    __shared__ unsigned long long lrep[kRegion];
+    __shared__ unsigned long long lkey[LS];
+    __shared__ unsigned int lcnt[LS];
+    __shared__ unsigned long long lrep[LS];
     __shared__ unsigned long long red[kBuildBlock / 64];
     __shared__ unsigned int lovf;
-    for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
+    for (int i = threadIdx.x; i < LS; i += kBuildBlock) {
         lkey[i] = kEmpty;
         lcnt[i] = 0;
         lrep[i] = ~0ull;
     }
     if (threadIdx.x == 0) lovf = 0;
     __syncthreads();
+    auto start = [](uint64_t h) { return (unsigned int)(h >> 52) & (LS - 1); };
     int64_t r0, r1;
     chunk_of(nrows, r0, r1);
     unsigned long long bad = 0;
@@ -1140,17 +1188,30 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
             take[u] = r < r1 && row_key(ks, r, h[u], ng) && !ng && h[u] != kEmpty;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (take[u])
-                ok &= lds_insert<unsigned int>(lkey, lcnt, lrep, h[u], (unsigned long long)(t0 + (int64_t)u * kBuildBlock +
-                                                                                    threadIdx.x), 1u, true);
+        for (int u = 0; u < 4; ++u) {
+            if (!take[u]) continue;
+            const unsigned long long row = (unsigned long long)(t0 + (int64_t)u * kBuildBlock + threadIdx.x);
+            unsigned int p = start(h[u]);
+            bool done = false;
+            for (int probe = 0; probe < LS; ++probe) {
+                const unsigned long long prev = atomicCAS(&lkey[p], kEmpty, h[u]);
+                if (prev == kEmpty || prev == h[u]) {
+                    atomicAdd(&lcnt[p], 1u);
+                    atomicMin(&lrep[p], row);
+                    done = true;
+                    break;
+                }
+                p = (p + 1) & (LS - 1);
+            }
+            ok &= done;
+        }
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (!take[u]) continue;
             const int64_t r = t0 + (int64_t)u * kBuildBlock + threadIdx.x;
-            unsigned int p = region_probe(h[u]);
-            for (int probe = 0; probe < kRegion && lkey[p] != h[u]; ++probe) p = (p + 1) & (kRegion - 1);
+            unsigned int p = start(h[u]);
+            for (int probe = 0; probe < LS && lkey[p] != h[u]; ++probe) p = (p + 1) & (LS - 1);
             const unsigned long long rep = lrep[p];
             if (lkey[p] != h[u] || (rep != (unsigned long long)r && !rows_equal(ks, r, (int64_t)rep))) ++bad;
         }
@@ -1158,12 +1219,12 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
     }
     if (!ok) lovf = 1;
     __syncthreads();
-    // publish this workgroup's groups and merge them into region 0
+    // publish this workgroup's groups and merge them into region 0 (kRegion slots)
     bool mok = true;
     for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
-        const unsigned long long key = lkey[i];
+        const unsigned long long key = i < LS ? lkey[i] : kEmpty;
         wg_keys[(uint64_t)blockIdx.x * kRegion + i] = key;
-        wg_reps[(uint64_t)blockIdx.x * kRegion + i] = lrep[i];
+        wg_reps[(uint64_t)blockIdx.x * kRegion + i] = i < LS ? lrep[i] : ~0ull;
         if (key == kEmpty) continue;
         unsigned int p = region_probe(key);
         bool done = false;
@@ -1539,7 +1600,8 @@ struct DevBuf {  // scratch device buffers of one build (the context's scratch c
 // bucket. Returns DQ_OK with *overflow / *collision set from the device counters.
 int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, const unsigned long long* sorted,
                   const unsigned long long* srows, const std::vector<unsigned long long>& bstart,
-                  const std::vector<unsigned long long>& bcount, int bits, bool* overflow, bool* collision) {
+                  const std::vector<unsigned long long>& bcount, int bits, bool* overflow, bool* collision,
+                  const NarrowKey* narrow = nullptr) {
     hipStream_t s = dq::ctx_stream(ctx);
     const bool general = !t->fast;
     const bool weighted = t->ks.weights != nullptr;
@@ -1577,16 +1639,19 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     const double build_n = (double)t->host_ctr.num_rows;  // the count pass's numRows (copied before the build)
     if (general && weighted)
         hipLaunchKernelGGL((build_kernel<true, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n);
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     else if (general)
         hipLaunchKernelGGL((build_kernel<true, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n);
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     else if (weighted)
         hipLaunchKernelGGL((build_kernel<false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n);
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
+    else if (narrow)
+        hipLaunchKernelGGL((build_kernel<false, false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows,
+                           w, t->slots, t->reps, t->ctr, bparts, build_n, *narrow);
     else
         hipLaunchKernelGGL((build_kernel<false, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n);
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     FQ_HIP(ctx, hipGetLastError());
     if (general && nrows > 0) {
         const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
@@ -1640,7 +1705,7 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
 
 // Small general tables (bits = 0): small_build_kernel + small_check_kernel, the table one region. *overflow sends the
 // caller to the regular path, *collision to a new seed.
-int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* overflow, bool* collision) {
+int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf& buf, bool* overflow, bool* collision) {
     hipStream_t s = dq::ctx_stream(ctx);
     release_slots(t, ctx);
     t->home = ctx;
@@ -1660,8 +1725,13 @@ int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool*
     const BuildItem it = {0ull, 0ull, 0u, 1u};  // split = 1: region_init clears region 0
     FQ_HIP(ctx, hipMemcpyAsync(ditem, &it, sizeof(it), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(region_init_kernel, dim3(1), dim3(kFreqBlock), 0, s, ditem, 1, t->slots, t->reps);
-    hipLaunchKernelGGL(small_build_kernel, dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots, t->reps, wk, wr,
-                       t->ctr);
+    // a 2048-slot workgroup table (40 KB of LDS: 3 workgroups per CU instead of 1) when the estimate leaves it <= 5/8 full
+    if (est <= 1280.0)
+        hipLaunchKernelGGL((small_build_kernel<2048>), dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots, t->reps,
+                           wk, wr, t->ctr);
+    else
+        hipLaunchKernelGGL((small_build_kernel<kRegion>), dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots,
+                           t->reps, wk, wr, t->ctr);
     hipLaunchKernelGGL(small_check_kernel, dim3(grid), dim3(kBuildBlock), 0, s, t->ks, t->slots, t->reps, wk, wr, t->ctr);
     FQ_HIP(ctx, hipGetLastError());
     FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
@@ -1794,20 +1864,95 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
 // too small or too large for the two-pass bucketing.
 constexpr int64_t kFastMinRows = 1 << 24;
 
-int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* done) {
+// Signed min / max of the canonical values of a strided sample of an 8-byte integral key column (narrow-key choice).
+constexpr int kNarrowSample = 1 << 16;
+
+__global__ void __launch_bounds__(256)
+narrow_sample_kernel(KeyCol c, int64_t nrows, long long* __restrict__ out) {
+    __shared__ long long smin[256], smax[256];
+    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    const int64_t stride = nrows / kNarrowSample > 0 ? nrows / kNarrowSample : 1;
+    for (int64_t k = threadIdx.x; k < kNarrowSample && k * stride < nrows; k += 256) {
+        const int64_t r = k * stride;
+        if (c.validity && !((c.validity[r >> 3] >> (r & 7)) & 1u)) continue;
+        const long long v = static_cast<const long long*>(c.values)[r];
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    smin[threadIdx.x] = lo;
+    smax[threadIdx.x] = hi;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            smin[threadIdx.x] = smin[threadIdx.x + o] < smin[threadIdx.x] ? smin[threadIdx.x + o] : smin[threadIdx.x];
+            smax[threadIdx.x] = smax[threadIdx.x + o] > smax[threadIdx.x] ? smax[threadIdx.x + o] : smax[threadIdx.x];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = smin[0];
+        out[1] = smax[0];
+    }
+}
+
+// The narrow-key window for the fast path's key column (see NarrowKey), or false for 64-bit keys.
+bool choose_narrow(dq_ctx* ctx, const dq_freq_table* t, int64_t nrows, DevBuf& buf, NarrowKey* nk, int* rc) {
+    *rc = DQ_OK;
+    const KeyCol& c = t->ks.cols[0];
+    const ElemType elem = (ElemType)c.elem;
+    const int w = elem_size(elem);
+    if (getenv("DQ_FREQ_WIDE")) return false;
+    if (w <= 4) {  // the canonical value is the cell's 32 bits, sign-extended for the signed types
+        *nk = NarrowKey{0ull, (elem == ET_F32 || elem == ET_U8) ? 0 : 1, 0};
+        return true;
+    }
+    if (elem == ET_F64) return false;  // the bit patterns of doubles seldom share 32 high bits
+    hipStream_t s = dq::ctx_stream(ctx);
+    long long* d = nullptr;
+    if (buf.alloc((void**)&d, 2 * sizeof(long long)) != hipSuccess) {
+        *rc = dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "narrow-key sample allocation failed");
+        return false;
+    }
+    hipLaunchKernelGGL(narrow_sample_kernel, dim3(1), dim3(256), 0, s, c, nrows, d);
+    long long mm[2];
+    if (hipMemcpyAsync(mm, d, sizeof(mm), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        *rc = dq::ctx_fail(ctx, DQ_ERR_DEVICE, "narrow-key sample failed");
+        return false;
+    }
+    if (mm[0] > mm[1]) {  // no valid row in the sample
+        *nk = NarrowKey{0ull, 1, 0};
+        return true;
+    }
+    const unsigned long long range = (unsigned long long)mm[1] - (unsigned long long)mm[0];
+    if (range >= (1ull << 31)) return false;
+    // the window [base, base + 2^32) centred on the sample's range
+    *nk = NarrowKey{(unsigned long long)mm[0] - ((0xFFFFFFFFull - range) >> 1), 0, 0};
+    return true;
+}
+
+int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* done, bool allow_narrow = true) {
     *done = false;
     hipStream_t s = dq::ctx_stream(ctx);
     const int xgrid = scan_grid((uint64_t)nrows);
+    NarrowKey nk{0ull, 0, 0};
+    bool narrow = false;
+    if (allow_narrow) {
+        int rc = DQ_OK;
+        narrow = choose_narrow(ctx, t, nrows, buf, &nk, &rc);
+        if (rc != DQ_OK) return rc;
+    }
+    const size_t ksz = narrow ? 4 : 8;  // bytes per key in the partition buffers
     // pass 1: 256 partitions x 8 XCD sub-regions of cap1 keys (the expected share plus slack for hashing variance
     // and repeated keys)
     constexpr int kSub = kDigitBins * kXcds;
     const unsigned long long share = (unsigned long long)(nrows / kSub);
     const unsigned long long cap1 = share + share / 8 + 16384;
-    unsigned long long *gc1 = nullptr, *h1 = nullptr;
+    unsigned long long* gc1 = nullptr;
+    void* h1 = nullptr;
     unsigned int* regs = nullptr;
     uint8_t* regs_part = nullptr;
     FQ_HIP(ctx, buf.alloc((void**)&gc1, sizeof(unsigned long long) * kSub * kCursorStride));
-    FQ_HIP(ctx, buf.alloc((void**)&h1, cap1 * kSub * 8));
+    FQ_HIP(ctx, buf.alloc((void**)&h1, cap1 * kSub * ksz));
     FQ_HIP(ctx, buf.alloc((void**)&regs, kFastRegs * sizeof(unsigned int)));
     FQ_HIP(ctx, buf.alloc((void**)&regs_part, (size_t)kFastRegs * xgrid));
     FQ_HIP(ctx, hipMemsetAsync(gc1, 0, sizeof(unsigned long long) * kSub * kCursorStride, s));
@@ -1815,24 +1960,24 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
     const int inul = t->ks.include_nulls ? 1 : 0;
     // (measured: an 8 K-key pass-1 tile runs 8.1 ms against 6.1 ms for 4 K on C4 -- twice the registers)
+#define DQ_P1(W, N)                                                                                                   \
+    hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, W, N>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0], \
+                       nrows, inul, cap1, gc1, h1, regs_part, t->ctr, nk)
     switch (elem_size((ElemType)t->ks.cols[0].elem)) {
         case 8:
-            hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, 8>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
-                               nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+            if (narrow) DQ_P1(8, true); else DQ_P1(8, false);
             break;
         case 4:
-            hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, 4>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
-                               nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+            if (narrow) DQ_P1(4, true); else DQ_P1(4, false);
             break;
         case 2:
-            hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, 2>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
-                               nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+            if (narrow) DQ_P1(2, true); else DQ_P1(2, false);
             break;
         default:
-            hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, 1>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0],
-                               nrows, inul, cap1, gc1, h1, regs_part, t->ctr);
+            if (narrow) DQ_P1(1, true); else DQ_P1(1, false);
             break;
     }
+#undef DQ_P1
     hipLaunchKernelGGL(sizing_reduce_kernel, dim3(kFastRegs / 256, std::min(xgrid, 64)), dim3(256), 0, s,
                        (const uint8_t*)regs_part, xgrid, kFastRegs, regs);
     FQ_HIP(ctx, hipGetLastError());
@@ -1845,6 +1990,11 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     FQ_HIP(ctx, hipStreamSynchronize(s));
     if (t->host_ctr.pad[2]) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency fast build: run position out of range");
     if (t->host_ctr.pad[0]) return DQ_OK;  // a partition overflowed: the exact path
+    if (t->host_ctr.narrow_miss) {  // an 8-byte key outside the sampled window: again with 64-bit keys
+        if (getenv("DQ_DEBUG_FREQ"))
+            fprintf(stderr, "[freq fast] narrow window missed by %llu rows\n", t->host_ctr.narrow_miss);
+        return build_fast(ctx, t, nrows, buf, done, false);
+    }
     for (int q = 0; q < kSub; ++q) pcount[q] = pstrided[(size_t)q * kCursorStride];
     unsigned long long n = 0;
     for (unsigned long long c : pcount) n += c;
@@ -1852,14 +2002,15 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     int bits = 0;
     while (bits < 40 && est / (double)(1ull << bits) > (double)kRegionTarget) ++bits;
     if (getenv("DQ_DEBUG_FREQ"))
-        fprintf(stderr, "[freq fast] rows=%lld n=%llu est=%.1f bits=%d\n", (long long)nrows, n, est, bits);
+        fprintf(stderr, "[freq fast] rows=%lld n=%llu est=%.1f bits=%d narrow=%d\n", (long long)nrows, n, est, bits,
+                (int)narrow);
     if (bits < 8 || bits > kMaxPartBits) return DQ_OK;
     bits = std::max(bits, 9);  // a partition is 8 sub-regions: the second pass gathers them into buckets
-    unsigned long long* h2 = nullptr;
+    void* h2 = nullptr;
     size_t h2_bytes = 0;
     for (int grow = 0; grow < 8 && bits <= kMaxPartBits; ++grow, ++bits) {
         std::vector<unsigned long long> bstart, bcount;
-        const unsigned long long* sorted = h1;
+        const void* sorted = h1;
         {
             const int bins = 1 << (bits - 8);
             const uint64_t nb = 1ull << bits;
@@ -1889,19 +2040,22 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
             unsigned long long* gc2 = nullptr;
             FQ_HIP(ctx, buf.alloc((void**)&ditems, sizeof(FastItem) * std::max(nitems, 1)));
             FQ_HIP(ctx, buf.alloc((void**)&gc2, sizeof(unsigned long long) * nb));
-            if (cap2 * nb * 8 > h2_bytes) {
-                h2_bytes = cap2 * nb * 8;
+            if (cap2 * nb * ksz > h2_bytes) {
+                h2_bytes = cap2 * nb * ksz;
                 FQ_HIP(ctx, buf.alloc((void**)&h2, h2_bytes));
             }
             FQ_HIP(ctx, hipMemsetAsync(gc2, 0, sizeof(unsigned long long) * nb, s));
             if (nitems) FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), sizeof(FastItem) * nitems, hipMemcpyHostToDevice, s));
             const unsigned int mask = (unsigned int)bins - 1;
-            if (nitems && bins > kDigitBins)
-                hipLaunchKernelGGL((scatter2_fast_kernel<4096, kPartTile>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, h1,
-                                   mask, cap2, gc2, h2, t->ctr);
-            else if (nitems)
-                hipLaunchKernelGGL((scatter2_fast_kernel<kDigitBins, kPartTileFast>), dim3(nitems), dim3(kFreqBlock), 0, s,
-                                   ditems, h1, mask, cap2, gc2, h2, t->ctr);
+#define DQ_P2(B, T, N)                                                                                            \
+    hipLaunchKernelGGL((scatter2_fast_kernel<B, T, N>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, h1, mask, cap2, \
+                       gc2, h2, t->ctr, nk)
+            if (nitems && bins > kDigitBins) {
+                if (narrow) DQ_P2(4096, kPartTile, true); else DQ_P2(4096, kPartTile, false);
+            } else if (nitems) {
+                if (narrow) DQ_P2(kDigitBins, kPartTileFast, true); else DQ_P2(kDigitBins, kPartTileFast, false);
+            }
+#undef DQ_P2
             FQ_HIP(ctx, hipGetLastError());
             std::vector<unsigned long long> pb(nb);
             FQ_HIP(ctx, hipMemcpyAsync(pb.data(), gc2, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, s));
@@ -1918,7 +2072,8 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
             sorted = h2;
         }
         bool overflow = false, collision = false;
-        const int rc = build_regions(ctx, t, nrows, buf, sorted, nullptr, bstart, bcount, bits, &overflow, &collision);
+        const int rc = build_regions(ctx, t, nrows, buf, static_cast<const unsigned long long*>(sorted), nullptr, bstart,
+                                     bcount, bits, &overflow, &collision, narrow ? &nk : nullptr);
         if (rc != DQ_OK) return rc;
         if (!overflow) {
             *done = true;
@@ -1981,7 +2136,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         bool collision = false;
         if (general && !t->ks.weights && bits == 0 && n > 0 && !getenv("DQ_FREQ_NO_SMALL")) {
             bool overflow = false;
-            const int rc = build_small(ctx, t, nrows, buf, &overflow, &collision);
+            const int rc = build_small(ctx, t, nrows, est, buf, &overflow, &collision);
             if (rc != DQ_OK) return rc;
             if (!overflow && !collision) return DQ_OK;
             if (collision) {

@@ -27,6 +27,19 @@ def _order_key(v):
     return (0, v, 0 if math.copysign(1.0, v) < 0 else 1)  # -0.0 just below 0.0, above every negative
 
 
+def _sorted_java(items):
+    """sorted(items, key=_order_key) (a stable sort by Double.compare): on int64 keys that order like
+    Double.compare (the bits of a canonical NaN, sign-flipped for negatives) for more than a few items."""
+    if len(items) < 64:
+        return sorted(items, key=_order_key)
+    import numpy as np
+    a = np.asarray(items, dtype=np.float64)
+    b = a.view(np.int64).copy()
+    b[np.isnan(a)] = 0x7FF8000000000000
+    k = b ^ ((b >> 63) & 0x7FFFFFFFFFFFFFFF)
+    return a[np.argsort(k, kind="stable")].tolist()
+
+
 def _capacity(sketch_size, shrinking_factor, height):
     """QuantileNonSample.capacity (A/QuantileNonSample.scala:87-89)."""
     return 2 * (int(math.ceil(sketch_size * math.pow(shrinking_factor, height) / 2)) + 1)
@@ -49,7 +62,7 @@ class NonSampleCompactor:
         ln = items - items % 2
         if self.numOfCompress % 2 == 1:
             self.offset = 1 - self.offset
-        srt = sorted(self.buffer[:ln], key=_order_key)
+        srt = _sorted_java(self.buffer[:ln])
         output = srt[self.offset:ln:2]
         self.buffer = [self.buffer[items - 1]] if items % 2 == 1 else []
         self.numOfCompress += 1

@@ -285,12 +285,10 @@ class AnalysisRunner:
             return AnalyzerContext.empty()
         if isinstance(data, ChunkedTable):
             return AnalysisRunner._run_chunked(data, analyzers, aggregateWith, saveStatesWith)
-        allAnalyzers = []
-        for a in analyzers:  # VerificationSuite does not dedupe; the result map does
-            if a not in allAnalyzers:
-                allAnalyzers.append(a)
+        allAnalyzers = list(dict.fromkeys(analyzers))  # VerificationSuite does not dedupe; the result map does
         passed = [a for a in allAnalyzers if Preconditions.findFirstFailing(data.schema, a.preconditions()) is None]
-        failed = [a for a in allAnalyzers if a not in passed]
+        passed_set = set(passed)
+        failed = [a for a in allAnalyzers if a not in passed_set]
         preconditionFailures = AnalyzerContext(
             {a: a.toFailureMetric(Preconditions.findFirstFailing(data.schema, a.preconditions())) for a in failed})
         grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]
@@ -394,7 +392,8 @@ class AnalysisRunner:
             return AnalyzerContext.empty()
         analyzers = analysis.analyzers
         passed = [a for a in analyzers if Preconditions.findFirstFailing(schema, a.preconditions()) is None]
-        failed = [a for a in analyzers if a not in passed]
+        passed_set = set(passed)
+        failed = [a for a in analyzers if a not in passed_set]
         pre = AnalyzerContext({a: a.toFailureMetric(Preconditions.findFirstFailing(schema, a.preconditions()))
                                for a in failed})
         agg = InMemoryStateProvider()

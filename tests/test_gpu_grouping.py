@@ -201,15 +201,31 @@ def _sorted_pairs(ft):
     return k[o], c[o]
 
 
-@pytest.mark.parametrize("case", ["uniform", "repeats", "heavy_hitter", "nulls_nan_sentinel"])
+@pytest.mark.parametrize("case", ["uniform", "repeats", "heavy_hitter", "nulls_nan_sentinel", "narrow_window",
+                                  "narrow_outlier", "int32", "float32"])
 def test_fast_build_equals_exact_build(case, monkeypatch):
     """The fast build (fixed-capacity buckets, atomically reserved runs, no count pass; >= 2^24 rows) against the
     exactly-counted build on the same keys: identical groups, counts and summary. A heavy hitter overflows a
-    bucket and must take the exact path by itself."""
+    bucket and must take the exact path by itself. Narrow keys (32-bit offsets in the partition buffers): 8-byte
+    keys inside a sampled window (negative, far from zero), a key outside the window on a row the sample skips
+    (the build restarts with 64-bit keys), and 4-byte keys (always narrow)."""
     import torch
     n = 40_000_000
     rng = np.random.default_rng(7)
-    if case == "uniform":
+    if case == "narrow_window":
+        v = rng.integers(-5_000_000_000 - 2_000_000, -5_000_000_000, n, dtype=np.int64)
+    elif case == "narrow_outlier":
+        v = rng.integers(0, 2_000_000, n, dtype=np.int64)
+        v[12345] = 1 << 40  # not on the sample's stride (n / 65536 = 610)
+        v[777777] = -(1 << 40)
+    elif case == "int32":
+        v = rng.integers(-2 ** 31, 2 ** 31, n, dtype=np.int64).astype(np.int32)
+        v[::7] = rng.integers(-1000, 1000, len(v[::7]), dtype=np.int32)
+    elif case == "float32":
+        v = (rng.integers(-3_000_000, 3_000_000, n) / 4.0).astype(np.float32)
+        v[rng.random(n) < 0.01] = np.nan
+        v[rng.random(n) < 0.01] = -0.0
+    elif case == "uniform":
         v = rng.integers(0, 2 ** 62, n, dtype=np.int64)
         v[::1_000_003] = _value_mixing_to_all_ones()  # its mixed key is the EMPTY slot marker
     elif case == "repeats":
@@ -220,8 +236,10 @@ def test_fast_build_equals_exact_build(case, monkeypatch):
         v = rng.integers(-500_000, 500_000, n).astype(np.float64) / 8.0
         v[rng.random(n) < 0.01] = np.nan
         v[rng.random(n) < 0.01] = -0.0
-    valid = rng.random(n) > 0.02 if case == "nulls_nan_sentinel" else None
-    col = Column("k", N.TYPE_DOUBLE if v.dtype == np.float64 else N.TYPE_LONG, None, None, length=n)
+    valid = rng.random(n) > 0.02 if case in ("nulls_nan_sentinel", "narrow_window") else None
+    col = Column("k", {np.dtype(np.float64): N.TYPE_DOUBLE, np.dtype(np.int64): N.TYPE_LONG,
+                       np.dtype(np.int32): N.TYPE_INT, np.dtype(np.float32): N.TYPE_FLOAT}[v.dtype], None, None,
+                 length=n)
     col.device = {"values": torch.from_numpy(v).cuda()}
     if valid is not None:
         col.device["validity"] = torch.from_numpy(pack_validity(valid)).cuda()
