@@ -161,7 +161,7 @@ def bench_c3(torch, N, D, ctx, stream, dev, total, steps, dist=None, world=1, ra
     el, kms, _ = timed(torch, dist, world, steps, 1, stream, w.step)
     bpr = 3 * (8 + 1 / 8)
     ach = bpr * nrows / (kms * 1e-3) / 1e9
-    c3_traffic = committed_json("c3_traffic_*.json", nrows) if world == 1 else None
+    c3_traffic = committed_json("c3_traffic_*.json", nrows, need="traffic_bytes_per_call") if world == 1 else None
     return {"workload": "C3: ApproxCountDistinct(k) + Correlation(x, y) + Completeness(k), 3 cols x %d rows, 1%% nulls, "
                         "rows sharded over %d GPU(s), states all-gathered (RCCL) and folded in rank order"
                         % (total, world),
@@ -213,14 +213,13 @@ def bench_c4(torch, N, D, ctx, stream, dev, total, steps):
     table_bytes = 2 * 16 * distinct  # write + read of the 16-B slots of each group
     ach = (bpr * total + table_bytes) / (el / steps) / 1e9
     traffic = None
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "c4_traffic_*.json"))):
-        try:
-            d = json.load(open(path))
-        except (OSError, ValueError):
-            continue
-        if int(d.get("rows", -1)) == total:
-            traffic = (d["total_GB_per_call"], os.path.relpath(path, ROOT))
+    found = committed_json("c4_traffic_*.json", total, need="traffic_bytes_per_call")
+    if found:
+        traffic = (found[0]["traffic_bytes_per_call"] / 1e9, found[1])
+    else:  # the round-2 layout
+        found = committed_json("c4_traffic_*.json", total, need="total_GB_per_call")
+        if found:
+            traffic = (found[0]["total_GB_per_call"], found[1])
     return {"workload": "C4: computeFrequencies + Uniqueness/Distinctness/UniqueValueRatio/CountDistinct/Entropy "
                         "aggregation, 1e9 int64 keys, 1e8 distinct; closed forms exact",
             "value": total / (el / steps), "unit": "rows/s", "ms_per_step": el / steps * 1e3,
@@ -352,7 +351,7 @@ def bench_c5(torch, N, D, ctx, dev, rows, steps):
     types = {n: p.dataType for n, p in prof.profiles.items()}
     assert types["s_int"] == "Integral" and types["s_dec"] == "Fractional" and types["s_text0"] == "String", types
     ach = nbytes / el / 1e9
-    c5_traffic = committed_json("c5_traffic_*.json", rows)
+    c5_traffic = committed_json("c5_traffic_*.json", rows, need="traffic_bytes_per_call")
     passes = c5_pass_times(torch, D, t)
     return {"workload": "C5 shard: ColumnProfiler passes 1-3 (Completeness, ApproxCountDistinct, DataType; Min / Max / "
                         "Mean / StdDev / Sum / KLL on 13 numeric and cast numeric-string columns; exact histograms of "
@@ -618,16 +617,8 @@ def measured_traffic(rows_per_gpu):
     """HBM bytes per dq_scan call of this workload from the committed rocprofv3 PMC passes
     (tools/gpu_pmc.sh -> tools/pmc_traffic.py -> profiles/<round>/c2_traffic_*.json), in GB, or None
     when no PMC measurement of this exact shard size is committed."""
-    import glob
-    best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "c2_traffic_*.json"))):
-        try:
-            d = json.load(open(path))
-        except (OSError, ValueError):
-            continue
-        if int(d.get("rows", -1)) == rows_per_gpu:
-            best = (d["traffic_bytes_per_call"] / 1e9, os.path.relpath(path, ROOT))
-    return best
+    found = committed_json("c2_traffic_*.json", rows_per_gpu, need="traffic_bytes_per_call")
+    return (found[0]["traffic_bytes_per_call"] / 1e9, found[1]) if found else None
 
 
 def main():
@@ -721,7 +712,7 @@ def main():
         s10 = ScanWorkload(torch, N, D, ctx, table, suite10_analyzers(D, names), stream, dev, world, args.dist_backend)
         el, kms, st = timed(torch, dist, world, max(3, args.steps // 4), 1, stream, s10.step)
         ach = alg_bytes / (kms * 1e-3) / 1e9
-        s10_traffic = committed_json("suite10_traffic_*.json", nrows)
+        s10_traffic = committed_json("suite10_traffic_*.json", nrows, need="traffic_bytes_per_call")
         s10_valu = committed_json("suite10_sq_counters_*.json", None, need="runs")
         valu = None
         if s10_valu is not None and world == 1 and nrows == 1_000_000_000:
@@ -760,7 +751,7 @@ def main():
         el, kms, _ = timed(torch, dist, world, max(3, args.steps // 4), 1, stream, c2w.step)
         after = ctx.kernel_launches()
         ach = alg_bytes / (kms * 1e-3) / 1e9
-        c2w_traffic = committed_json("c2where_traffic_*.json", nrows)
+        c2w_traffic = committed_json("c2where_traffic_*.json", nrows, need="traffic_bytes_per_call")
         sec["c2_where"] = {
             "workload": "C2's 49 ops, every one under `where %s` (int64 column, 1%% nulls: ~50%% of the rows selected)" % w,
             "value": total / (el / max(3, args.steps // 4)), "unit": "rows/s",
