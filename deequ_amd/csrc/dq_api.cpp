@@ -260,6 +260,17 @@ int ctx_device(dq_ctx* ctx) { return ctx->device; }
 int ctx_cus(dq_ctx* ctx) { return ctx->cus; }
 int ctx_fail(dq_ctx* ctx, int code, const char* msg) { return fail(ctx, code, "%s", msg); }
 int ctx_num_subs(dq_ctx* ctx) { return (int)ctx->subs.size(); }
+// The context's side streams (created on first use) with its fork event and one join event per side stream; returns
+// their number, 0 when they cannot be created.
+int ctx_side_streams(dq_ctx* ctx, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join) {
+    if (ensure_side_streams(ctx) != DQ_OK) return 0;
+    for (int i = 0; i < dq_ctx::kSide; ++i) {
+        side[i] = ctx->side[i];
+        join[i] = ctx->join_ev[i];
+    }
+    *fork = ctx->fork_ev;
+    return dq_ctx::kSide;
+}
 dq_ctx* ctx_sub(dq_ctx* ctx, int i) { return ctx->subs[i]; }
 // The context's device arena / pinned staging buffer, grown to `bytes` (NULL + error set on failure).
 // Used by one call at a time (a ctx is not re-entrant); work queued on the ctx stream stays ordered.

@@ -1864,34 +1864,37 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
 // too small or too large for the two-pass bucketing.
 constexpr int64_t kFastMinRows = 1 << 24;
 
-// Signed min / max of the canonical values of a strided sample of an 8-byte integral key column (narrow-key choice).
+// Signed min / max of the canonical values of a strided sample of an 8-byte integral key column (narrow-key choice):
+// one sampled row per thread (no dependent load chain), block minima / maxima folded with 64-bit atomics.
 constexpr int kNarrowSample = 1 << 16;
 
 __global__ void __launch_bounds__(256)
 narrow_sample_kernel(KeyCol c, int64_t nrows, long long* __restrict__ out) {
-    __shared__ long long smin[256], smax[256];
-    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    __shared__ long long smin[4], smax[4];
     const int64_t stride = nrows / kNarrowSample > 0 ? nrows / kNarrowSample : 1;
-    for (int64_t k = threadIdx.x; k < kNarrowSample && k * stride < nrows; k += 256) {
-        const int64_t r = k * stride;
-        if (c.validity && !((c.validity[r >> 3] >> (r & 7)) & 1u)) continue;
-        const long long v = static_cast<const long long*>(c.values)[r];
-        lo = v < lo ? v : lo;
-        hi = v > hi ? v : hi;
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t r = k * stride;
+    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    if (r < nrows && (!c.validity || ((c.validity[r >> 3] >> (r & 7)) & 1u))) {
+        lo = hi = static_cast<const long long*>(c.values)[r];
     }
-    smin[threadIdx.x] = lo;
-    smax[threadIdx.x] = hi;
+    for (int o = 32; o > 0; o >>= 1) {
+        const long long l2 = __shfl_down(lo, o, 64), h2 = __shfl_down(hi, o, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        smin[threadIdx.x >> 6] = lo;
+        smax[threadIdx.x >> 6] = hi;
+    }
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) {
-            smin[threadIdx.x] = smin[threadIdx.x + o] < smin[threadIdx.x] ? smin[threadIdx.x + o] : smin[threadIdx.x];
-            smax[threadIdx.x] = smax[threadIdx.x + o] > smax[threadIdx.x] ? smax[threadIdx.x + o] : smax[threadIdx.x];
-        }
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
-        out[0] = smin[0];
-        out[1] = smax[0];
+        for (int w = 1; w < 4; ++w) {
+            lo = smin[w] < lo ? smin[w] : lo;
+            hi = smax[w] > hi ? smax[w] : hi;
+        }
+        atomicMin(&out[0], lo);
+        atomicMax(&out[1], hi);
     }
 }
 
@@ -1913,7 +1916,12 @@ bool choose_narrow(dq_ctx* ctx, const dq_freq_table* t, int64_t nrows, DevBuf& b
         *rc = dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "narrow-key sample allocation failed");
         return false;
     }
-    hipLaunchKernelGGL(narrow_sample_kernel, dim3(1), dim3(256), 0, s, c, nrows, d);
+    static const long long init[2] = {LLONG_MAX, LLONG_MIN};
+    if (hipMemcpyAsync(d, init, sizeof(init), hipMemcpyHostToDevice, s) != hipSuccess) {
+        *rc = dq::ctx_fail(ctx, DQ_ERR_DEVICE, "narrow-key sample failed");
+        return false;
+    }
+    hipLaunchKernelGGL(narrow_sample_kernel, dim3(kNarrowSample / 256), dim3(256), 0, s, c, nrows, d);
     long long mm[2];
     if (hipMemcpyAsync(mm, d, sizeof(mm), hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
         *rc = dq::ctx_fail(ctx, DQ_ERR_DEVICE, "narrow-key sample failed");

@@ -464,6 +464,7 @@ hipStream_t ctx_stream(dq_ctx* ctx);
 int ctx_device(dq_ctx* ctx);
 int ctx_fail(dq_ctx* ctx, int code, const char* msg);
 int ctx_num_subs(dq_ctx* ctx);
+int ctx_side_streams(dq_ctx* ctx, hipStream_t* side, hipEvent_t* fork, hipEvent_t* join);
 dq_ctx* ctx_sub(dq_ctx* ctx, int i);
 void* ctx_scratch(dq_ctx* ctx, size_t bytes);
 void* ctx_pinned_buf(dq_ctx* ctx, size_t bytes);
@@ -1003,7 +1004,23 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
             hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
     });
     const unsigned long long mm_init[2] = {~0ull, 0ull};
-    for (KColumnRun& r : run) {
+    // columns are independent: their compaction chains go round-robin onto the context's stream and its side streams
+    // (forked after the dense writes, joined before the read-back), so one column's small upper-level launches overlap
+    // another's instead of leaving the chip idle between them
+    hipStream_t cstreams[1 + 8] = {s};
+    hipEvent_t fork_ev = nullptr, join_ev[8] = {};
+    int nstreams = 1;
+    if (ncols > 1 && !getenv("DQ_KLL_SERIAL")) {
+        const int nside = dq::ctx_side_streams(ctx, cstreams + 1, &fork_ev, join_ev);
+        if (nside > 0) {
+            nstreams = 1 + std::min(nside, ncols - 1);
+            KL_HIP(ctx, hipEventRecord(fork_ev, s));
+            for (int j = 1; j < nstreams; ++j) KL_HIP(ctx, hipStreamWaitEvent(cstreams[j], fork_ev, 0));
+        }
+    }
+    for (int ci = 0; ci < ncols; ++ci) {
+        KColumnRun& r = run[ci];
+        hipStream_t cs = cstreams[ci % nstreams];
         KllSchedule& sc = r.sc;
         const size_t nlev = sc.levels.size(), nseg_all = r.events.size();
         r.lbase.assign(nlev, 0);
@@ -1030,13 +1047,13 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
 
         // one launch per (level, kernel class) group; the order inside a level is free because every compaction's
         // input range and output slot are explicit
-        if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, s));
-        KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, s));
+        if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, cs));
+        KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, cs));
         for (const KColumnRun::Launch& L : r.launches) {  // a level that compacted always has a level above it
             const size_t h = L.level;
             const double* src = h == 0 ? r.stream0 : dup + r.lbase[h];
             double* dst = dup + r.lbase[h + 1];
-            if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, s) != 0)
+            if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, cs) != 0)
                 return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
         }
         // final buffers: one gather, one read-back (completed by the single synchronisation below)
@@ -1047,11 +1064,15 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
             htails[h] = KllTail{(unsigned long long)(uintptr_t)src, (unsigned long long)l.len, at};
             at += (unsigned long long)l.len;
         }
-        KL_HIP(ctx, hipMemcpyAsync(dtails, htails, nlev * sizeof(KllTail), hipMemcpyHostToDevice, s));
-        if (r.ntail) hipLaunchKernelGGL(kll_gather_kernel, dim3((unsigned)nlev), dim3(256), 0, s, (const KllTail*)dtails, dgat);
+        KL_HIP(ctx, hipMemcpyAsync(dtails, htails, nlev * sizeof(KllTail), hipMemcpyHostToDevice, cs));
+        if (r.ntail) hipLaunchKernelGGL(kll_gather_kernel, dim3((unsigned)nlev), dim3(256), 0, cs, (const KllTail*)dtails, dgat);
         KL_HIP(ctx, hipGetLastError());
-        if (r.ntail) KL_HIP(ctx, hipMemcpyAsync(r.hgat, dgat, sizeof(double) * (size_t)r.ntail, hipMemcpyDeviceToHost, s));
-        KL_HIP(ctx, hipMemcpyAsync(r.hgat + r.ntail, dminmax, 16, hipMemcpyDeviceToHost, s));
+        if (r.ntail) KL_HIP(ctx, hipMemcpyAsync(r.hgat, dgat, sizeof(double) * (size_t)r.ntail, hipMemcpyDeviceToHost, cs));
+        KL_HIP(ctx, hipMemcpyAsync(r.hgat + r.ntail, dminmax, 16, hipMemcpyDeviceToHost, cs));
+    }
+    for (int j = 1; j < nstreams; ++j) {
+        KL_HIP(ctx, hipEventRecord(join_ev[j - 1], cstreams[j]));
+        KL_HIP(ctx, hipStreamWaitEvent(s, join_ev[j - 1], 0));
     }
     const auto t2 = std::chrono::steady_clock::now();
     KL_HIP(ctx, hipStreamSynchronize(s));
