@@ -411,8 +411,9 @@ int kll_class_of_slow(int len) {
         const int P = kKllXClasses[j].t * kKllXClasses[j].e;
         if (len >= P && len - P <= 64) return kKllNumClasses + j;
     }
+    static const bool no12 = getenv("DQ_KLL_NO_E12") != nullptr;  // A/B: padded power-of-two classes only
     for (int c = 0; c < kKllNumClasses; ++c)
-        if (kKllClasses[c].t * kKllClasses[c].e >= len) return c;
+        if (kKllClasses[c].t * kKllClasses[c].e >= len && !(no12 && kKllClasses[c].e == 12)) return c;
     return -1;
 }
 
@@ -949,13 +950,28 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
         for (int i = 0; i < ncols; ++i)
             if (!run[i].zero_copy) run[i].n = nrows > 0 ? (int64_t)htotals[i] : 0;
     }
+    // columns are independent: their compaction chains go round-robin onto the context's stream and its side streams
+    // (forked after the non-NULL counts, joined before the read-back): each column's dense write and compaction chain, so one column's small upper-level launches overlap
+    // another's instead of leaving the chip idle between them
+    hipStream_t cstreams[1 + 8] = {s};
+    hipEvent_t fork_ev = nullptr, join_ev[8] = {};
+    int nstreams = 1;
+    if (ncols > 1 && !getenv("DQ_KLL_SERIAL")) {
+        const int nside = dq::ctx_side_streams(ctx, cstreams + 1, &fork_ev, join_ev);
+        if (nside > 0) {
+            nstreams = 1 + std::min(nside, ncols - 1);
+            KL_HIP(ctx, hipEventRecord(fork_ev, s));
+            for (int j = 1; j < nstreams; ++j) KL_HIP(ctx, hipStreamWaitEvent(cstreams[j], fork_ev, 0));
+        }
+    }
     // dense level-0 streams go out while the host computes the (count-only) compaction schedules
     for (int i = 0; i < ncols; ++i) {
         KColumnRun& r = run[i];
         if (r.zero_copy || r.n <= 0) continue;
         double* dense = nullptr;
         KL_HIP(ctx, buf.alloc((void**)&dense, (size_t)r.n * 8));
-        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)r.ntiles), dim3(kKllStageBlock), 0, s, r.kc, nrows,
+        hipLaunchKernelGGL(kll_write_kernel, dim3((unsigned)r.ntiles), dim3(kKllStageBlock), 0, cstreams[i % nstreams],
+                           r.kc, nrows,
                            (const unsigned long long*)r.doffs, dense);
         KL_HIP(ctx, hipGetLastError());
         r.stream0 = dense;
@@ -1004,20 +1020,6 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
             hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
     });
     const unsigned long long mm_init[2] = {~0ull, 0ull};
-    // columns are independent: their compaction chains go round-robin onto the context's stream and its side streams
-    // (forked after the dense writes, joined before the read-back), so one column's small upper-level launches overlap
-    // another's instead of leaving the chip idle between them
-    hipStream_t cstreams[1 + 8] = {s};
-    hipEvent_t fork_ev = nullptr, join_ev[8] = {};
-    int nstreams = 1;
-    if (ncols > 1 && !getenv("DQ_KLL_SERIAL")) {
-        const int nside = dq::ctx_side_streams(ctx, cstreams + 1, &fork_ev, join_ev);
-        if (nside > 0) {
-            nstreams = 1 + std::min(nside, ncols - 1);
-            KL_HIP(ctx, hipEventRecord(fork_ev, s));
-            for (int j = 1; j < nstreams; ++j) KL_HIP(ctx, hipStreamWaitEvent(cstreams[j], fork_ev, 0));
-        }
-    }
     for (int ci = 0; ci < ncols; ++ci) {
         KColumnRun& r = run[ci];
         hipStream_t cs = cstreams[ci % nstreams];

@@ -3,7 +3,7 @@ dq_kll_sketch per column vs one dq_kll_sketch_columns call (parallel host schedu
 every column's compaction chain on one stream (DQ_KLL_SERIAL=1) and spread over the context's 4 streams; bytes compared,
 wall time per pass (device synchronised), interleaved rounds.
 
-    python tools/kll_ab.py [rows] [rounds]
+    python tools/kll_ab.py [rows] [rounds] [no12]
 """
 import os
 import sys
@@ -18,6 +18,8 @@ from deequ_amd import engine  # noqa: E402
 from deequ_amd.table import Column  # noqa: E402
 
 os.environ.setdefault("DQ_KLL_TIMING", "1")
+if len(sys.argv) > 3 and sys.argv[3] == "no12":  # padded power-of-two compaction classes only (read once per process)
+    os.environ["DQ_KLL_NO_E12"] = "1"
 rows = int(float(sys.argv[1])) if len(sys.argv) > 1 else 125_000_000
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 ctx = engine.ctx()
