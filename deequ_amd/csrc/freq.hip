@@ -152,6 +152,69 @@ __device__ __forceinline__ uint64_t canonical(const KeyCol& c, int64_t r) {
 
 __device__ __constant__ const uint8_t kNullValue[9] = {'N', 'u', 'l', 'l', 'V', 'a', 'l', 'u', 'e'};
 
+// Little-endian loads of string bytes through aligned dwords (a lane's byte-by-byte loads were the general path's
+// bottleneck); only dwords holding at least one byte of [p, p + n) are read, so nothing past a buffer is touched.
+__device__ __forceinline__ uint32_t dw_at(const uint8_t* a) { return *reinterpret_cast<const uint32_t*>(a); }
+
+__device__ __forceinline__ uint64_t dev_le64(const uint8_t* p) {  // 8 readable bytes at p
+    const uint8_t* a = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+    const int sh = (int)(p - a) * 8;
+    const uint32_t w0 = dw_at(a), w1 = dw_at(a + 4);
+    if (!sh) return (uint64_t)w0 | ((uint64_t)w1 << 32);
+    const uint32_t w2 = dw_at(a + 8);
+    const uint64_t lo = ((uint64_t)w1 << 32 | w0) >> sh, hi = ((uint64_t)w2 << 32 | w1) >> sh;
+    return (lo & 0xFFFFFFFFull) | (hi << 32);
+}
+
+__device__ __forceinline__ uint32_t dev_le32(const uint8_t* p) {  // 4 readable bytes at p
+    const uint8_t* a = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+    const int sh = (int)(p - a) * 8;
+    const uint32_t w0 = dw_at(a);
+    if (!sh) return w0;
+    return (uint32_t)((((uint64_t)dw_at(a + 4) << 32) | w0) >> sh);
+}
+
+// xxh_bytes (dq_common.h) with the loads above: the same hash.
+__device__ uint64_t dev_xxh_bytes(const uint8_t* p, int64_t len, uint64_t seed) {
+    const uint8_t* end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        const uint8_t* limit = end - 32;
+        uint64_t v1 = seed + P64_1 + P64_2, v2 = seed + P64_2, v3 = seed, v4 = seed - P64_1;
+        do {
+            v1 = xxh_round(v1, dev_le64(p));
+            v2 = xxh_round(v2, dev_le64(p + 8));
+            v3 = xxh_round(v3, dev_le64(p + 16));
+            v4 = xxh_round(v4, dev_le64(p + 24));
+            p += 32;
+        } while (p <= limit);
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = xxh_merge_round(h, v1);
+        h = xxh_merge_round(h, v2);
+        h = xxh_merge_round(h, v3);
+        h = xxh_merge_round(h, v4);
+    } else {
+        h = seed + P64_5;
+    }
+    h += (uint64_t)len;
+    while (p + 8 <= end) {
+        h ^= xxh_round(0, dev_le64(p));
+        h = rotl64(h, 27) * P64_1 + P64_4;
+        p += 8;
+    }
+    if (p + 4 <= end) {
+        h ^= (uint64_t)dev_le32(p) * P64_1;
+        h = rotl64(h, 23) * P64_2 + P64_3;
+        p += 4;
+    }
+    while (p < end) {
+        h ^= (uint64_t)(*p) * P64_5;
+        h = rotl64(h, 11) * P64_1;
+        ++p;
+    }
+    return xxh_fmix(h);
+}
+
 // Key of row r: returns false when the row does not take part (all key columns NULL, grouping
 // semantics); `null_group` = the row belongs to the fast path's NULL group (Histogram semantics).
 __device__ __forceinline__ bool row_key(const KeySpec& ks, int64_t r, uint64_t& h, bool& null_group) {
@@ -175,7 +238,7 @@ __device__ __forceinline__ bool row_key(const KeySpec& ks, int64_t r, uint64_t& 
             any = true;
             if (c.spark_type == DQ_TYPE_STRING) {
                 const int32_t o0 = c.offsets[r], o1 = c.offsets[r + 1];
-                ch = xxh_bytes(static_cast<const uint8_t*>(c.values) + o0, o1 - o0, ks.seed);
+                ch = dev_xxh_bytes(static_cast<const uint8_t*>(c.values) + o0, o1 - o0, ks.seed);
             } else {
                 ch = xxh_long(canonical(c, r), ks.seed);
             }
@@ -210,7 +273,14 @@ __device__ bool rows_equal(const KeySpec& ks, int64_t a, int64_t b) {
             if (va != vb) return false;
             if (!va) continue;
             if (la != lb) return false;
-            for (int k = 0; k < la; ++k)
+            int k = 0;
+            for (; k + 8 <= la; k += 8)
+                if (dev_le64(pa + k) != dev_le64(pb + k)) return false;
+            if (k + 4 <= la) {
+                if (dev_le32(pa + k) != dev_le32(pb + k)) return false;
+                k += 4;
+            }
+            for (; k < la; ++k)
                 if (pa[k] != pb[k]) return false;
         } else {
             if (va != vb) return false;

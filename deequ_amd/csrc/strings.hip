@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdlib.h>
+
+#include <algorithm>
 
 #include "dq_common.h"
 #include "dq_internal.h"
@@ -110,6 +113,24 @@ __device__ uint64_t xxh64_utf8(const uint8_t* data, int64_t o0, int64_t o1, uint
 
 enum DtClass : int { DT_NULL = 0, DT_FRACTIONAL = 1, DT_INTEGRAL = 2, DT_BOOLEAN = 3, DT_STRING = 4 };
 
+// First position in [i, o1) that is not an ASCII digit (o1 if none), four bytes per step: a byte b is a digit iff
+// t = b ^ 0x30 is < 10, i.e. neither t's bit 7 nor bit 7 of (t & 0x7F) + 0x76 is set (no carry crosses a byte).
+__device__ __forceinline__ int64_t skip_digits(const uint8_t* data, int64_t i, int64_t o1) {
+    while (i < o1) {
+        const int64_t a = i & ~(int64_t)3;
+        const int k = (int)(i - a);
+        const uint32_t t = (load_word(data, a) >> (8 * k)) ^ 0x30303030u;
+        const uint32_t nd = (((t & 0x7F7F7F7Fu) + 0x76767676u) | t) & 0x80808080u;
+        const int nb = (int)(o1 - i < 4 - k ? o1 - i : 4 - k);  // bytes of this word inside the string
+        if (nd) {
+            const int pos = __builtin_ctz(nd) >> 3;
+            if (pos < nb) return i + pos;
+        }
+        i += nb;
+    }
+    return o1;
+}
+
 // StatefulDataType's three full-match regexes over the UTF-8 bytes.
 __device__ int classify_string(const uint8_t* data, int64_t o0, int64_t o1) {
     int64_t i = o0;
@@ -118,19 +139,10 @@ __device__ int classify_string(const uint8_t* data, int64_t o0, int64_t o1) {
         if (c == '-' || c == '+') ++i;
     }
     if (i < o1 && byte_at(data, i) == ' ') ++i;
-    while (i < o1) {
-        const uint8_t c = byte_at(data, i);
-        if (c < '0' || c > '9') break;
-        ++i;
-    }
+    i = skip_digits(data, i, o1);
     if (i == o1) return DT_INTEGRAL;  // includes "" and a lone sign
     if (byte_at(data, i) == '.') {
-        ++i;
-        while (i < o1) {
-            const uint8_t c = byte_at(data, i);
-            if (c < '0' || c > '9') break;
-            ++i;
-        }
+        i = skip_digits(data, i + 1, o1);
         if (i == o1) return DT_FRACTIONAL;
     }
     const int64_t n = o1 - o0;
@@ -340,9 +352,13 @@ __global__ void finalize_strings_kernel(const StrOpMap* __restrict__ ops, int no
     }
 }
 
+// 4 workgroups per CU (DQ_STR_WG_PER_CU: 8, twice the resident waves, measured 2-3 % slower on the C5 string pass,
+// profiles/r03/strings_grid_ab_r03s.log).
 int string_scan_grid(int cus, int64_t nrows) {
+    const int per_cu = getenv("DQ_STR_WG_PER_CU") ? std::max(1, atoi(getenv("DQ_STR_WG_PER_CU"))) : 4;
     const int64_t want = (nrows + kBlock - 1) / kBlock;
-    return (int)(want < 1 ? 1 : (want < (int64_t)cus * 4 ? want : (int64_t)cus * 4));
+    const int64_t cap = (int64_t)cus * per_cu;
+    return (int)(want < 1 ? 1 : (want < cap ? want : cap));
 }
 
 void launch_string_scan(const StrSlot* slots, int nslots, int64_t nrows, int grid, int gstride, StrPartial* partials,

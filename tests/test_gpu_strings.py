@@ -66,6 +66,31 @@ def test_string_ops_match_oracle(device, where):
         [int(w) & 0xFFFFFFFFFFFFFFFF for w in O.expected_state(t, analyzers[3]).words]
 
 
+def test_datatype_digit_runs_match_oracle():
+    """DataType's digit runs are scanned four bytes at a time: strings of digits with the bytes next to '0'..'9'
+    ('/', ':'), signs, spaces, points and multi-byte characters at every offset and length 0-40."""
+    rng = np.random.default_rng(11)
+    alphabet = list("0123456789") * 4 + list("/:.-+ ") + ["°", "é", "٣"]
+    vals = []
+    for i in range(60_000):
+        k = int(rng.integers(0, 41))
+        body = "".join(alphabet[j] for j in rng.integers(0, len(alphabet), k))
+        r = rng.random()
+        if r < 0.3:
+            body = "".join(c for c in body if c.isdigit() and c.isascii())
+        elif r < 0.5:
+            d = "".join(c for c in body if c.isdigit() and c.isascii())
+            body = ("-" if rng.random() < 0.3 else "") + d[: len(d) // 2] + "." + d[len(d) // 2:]
+        vals.append(body)
+    t = Table([_column_from_pylist("s", "string", vals)])
+    t.to_device(0)
+    a = D.DataType("s")
+    got = run_states(t, [a])[0]
+    exp = O.expected_state(t, a)
+    fields = ("numNull", "numFractional", "numIntegral", "numBoolean", "numString")
+    assert [getattr(got, f) for f in fields] == [getattr(exp, f) for f in fields], (got, exp)
+
+
 def test_string_all_null_and_empty():
     t = Table([_column_from_pylist("s", "string", [None] * 100)])
     ctx = D.AnalysisRunner.onData(t).addAnalyzers(
