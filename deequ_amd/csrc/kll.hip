@@ -265,13 +265,33 @@ __device__ __forceinline__ void kll_merge_round(uint64_t* k, uint64_t (&v)[E], i
     __syncthreads();
 }
 
+// Batched launches (one launch per level and class over every column of a dq_kll_sketch_columns call): a descriptor's
+// bits 55-62 name its column, whose stream / next-level / min-max pointers for this level come from `cols`.
+struct KllColPtr {
+    const double* src;
+    double* dst;
+    unsigned long long* minmax;
+    unsigned long long pad;
+};
+
+template <typename S, typename D, typename M>
+__device__ __forceinline__ void kll_col_ptrs(const KllColPtr* cols, uint64_t sg, S& src, D& dst, M& minmax) {
+    if (cols) {
+        const KllColPtr cp = cols[(sg >> 55) & 0xFF];
+        src = cp.src;
+        dst = cp.dst;
+        minmax = cp.minmax;
+    }
+}
+
 template <int T, int E>
 __global__ void __launch_bounds__(T)
 kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
-                   unsigned long long* __restrict__ minmax) {
+                   unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols) {
     constexpr int PAD = T * E;
     __shared__ uint64_t k[PAD + T];
     const uint64_t sg = segs[blockIdx.x];
+    kll_col_ptrs(cols, sg, src, dst, minmax);
     const uint64_t start = sg & ((1ull << 40) - 1);
     const int len = (int)((sg >> 40) & 0x7FFF);
     const int t = threadIdx.x;
@@ -319,7 +339,7 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
 template <int T, int E>
 __global__ void __launch_bounds__(T)
 kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
-                     unsigned long long* __restrict__ minmax) {
+                     unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols) {
     constexpr int P = T * E;
     constexpr int XM = 64;
     static_assert(T >= XM, "wave 0 sorts the extras");
@@ -327,6 +347,7 @@ kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict_
     __shared__ uint64_t ex[XM];
     auto at = [](int i) { return i + i / E; };
     const uint64_t sg = segs[blockIdx.x];
+    kll_col_ptrs(cols, sg, src, dst, minmax);
     const uint64_t start = sg & ((1ull << 40) - 1);
     const int len = (int)((sg >> 40) & 0x7FFF);
     const int rx = len - P;  // 0..XM (host-checked)
@@ -428,11 +449,11 @@ int kll_class_of(int len) {
 }
 
 int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nseg, double* dst,
-                       unsigned long long* minmax, hipStream_t s) {
+                       unsigned long long* minmax, hipStream_t s, const KllColPtr* cols = nullptr) {
     if (nseg <= 0) return 0;
     switch (cls) {
 #define KLL_CASE(C, T, E) \
-    case C: hipLaunchKernelGGL((kll_compact_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax); break;
+    case C: hipLaunchKernelGGL((kll_compact_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols); break;
         KLL_CASE(0, 64, 4)
         KLL_CASE(1, 64, 8)
         KLL_CASE(2, 64, 12)
@@ -447,7 +468,8 @@ int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nse
         KLL_CASE(11, 1024, 16)
 #undef KLL_CASE
 #define KLL_XCASE(C, T, E) \
-    case C: hipLaunchKernelGGL((kll_compact_x_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax); break;
+    case C: \
+        hipLaunchKernelGGL((kll_compact_x_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols); break;
         KLL_XCASE(12, 64, 4)
         KLL_XCASE(13, 64, 8)
         KLL_XCASE(14, 128, 8)
@@ -956,7 +978,10 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
     hipStream_t cstreams[1 + 8] = {s};
     hipEvent_t fork_ev = nullptr, join_ev[8] = {};
     int nstreams = 1;
-    if (ncols > 1 && !getenv("DQ_KLL_SERIAL")) {
+    // several columns: one launch per (level, class) over all of them (below) unless DQ_KLL_PER_COLUMN asks for one
+    // launch chain per column (spread over the streams)
+    const bool batched = ncols > 1 && ncols <= 255 && !getenv("DQ_KLL_PER_COLUMN");
+    if (ncols > 1 && !batched && !getenv("DQ_KLL_SERIAL")) {
         const int nside = dq::ctx_side_streams(ctx, cstreams + 1, &fork_ev, join_ev);
         if (nside > 0) {
             nstreams = 1 + std::min(nside, ncols - 1);
@@ -988,89 +1013,193 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
     }
     const auto t1 = std::chrono::steady_clock::now();
 
-    // pinned staging for every column: [segment descriptors][level tails][gathered final buffers + min / max keys]
-    size_t pin_total = 0;
-    for (KColumnRun& r : run) {
-        const size_t nlev = r.sc.levels.size(), nseg = r.events.size();
-        r.ntail = 0;
-        for (const KllLevel& l : r.sc.levels) r.ntail += l.len;
-        r.pin_at = pin_total;
-        pin_total += (nseg * 8 + nlev * sizeof(KllTail) + (size_t)r.ntail * 8 + 16 + 255) / 256 * 256;
-    }
-    uint8_t* pin = static_cast<uint8_t*>(dq::ctx_pinned_buf(ctx, std::max<size_t>(pin_total, 16)));
-    if (!pin) return DQ_ERR_OUT_OF_MEMORY;
-    // every column's descriptors grouped per (level, kernel class) straight into its pinned region, on the host threads
-    kll_parallel(ncols, [&](int i) {
-        KColumnRun& r = run[i];
-        const KllSchedule& sc = r.sc;
-        const size_t nlev = sc.levels.size();
-        uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin + r.pin_at);
-        size_t pos = 0;
-        std::vector<size_t> cursor(nlev * kKllAllClasses);
-        r.launches.clear();
-        for (size_t h = 0; h < nlev; ++h) {
-            const KllLevel& l = sc.levels[h];
-            for (int c = 0; c < kKllAllClasses; ++c) {
-                cursor[h * kKllAllClasses + c] = pos;
-                if (l.per_class[c]) r.launches.push_back({h, pos, (size_t)l.per_class[c], c});
-                pos += (size_t)l.per_class[c];
+    if (batched) {
+        // every column's compactions grouped per (level, class, column): one launch per (level, class) covers all
+        // columns, so the upper levels' small per-column launches (a few workgroups each) become one wide launch
+        constexpr size_t NC = kKllAllClasses;
+        size_t maxlev = 0;
+        for (const KColumnRun& r : run) maxlev = std::max(maxlev, r.sc.levels.size());
+        std::vector<size_t> cnt(std::max<size_t>(maxlev * NC * ncols, 1), 0), first(cnt.size(), 0);
+        for (int i = 0; i < ncols; ++i)
+            for (size_t h = 0; h < run[i].sc.levels.size(); ++h)
+                for (size_t c = 0; c < NC; ++c) cnt[(h * NC + c) * ncols + i] = (size_t)run[i].sc.levels[h].per_class[c];
+        size_t nseg_all = 0;
+        for (size_t q = 0; q < cnt.size(); ++q) {
+            first[q] = nseg_all;
+            nseg_all += cnt[q];
+        }
+        // pinned: [descriptors][pointer tables, level-major][min / max init], then per column [tails][finals + min / max]
+        const size_t seg_bytes = (nseg_all * 8 + 255) / 256 * 256;
+        const size_t tab_bytes = (std::max<size_t>(maxlev, 1) * ncols * sizeof(KllColPtr) + 255) / 256 * 256;
+        const size_t mm_bytes = ((size_t)ncols * 16 + 255) / 256 * 256;
+        size_t pin_total = seg_bytes + tab_bytes + mm_bytes;
+        for (KColumnRun& r : run) {
+            const size_t nlev = r.sc.levels.size();
+            r.ntail = 0;
+            for (const KllLevel& l : r.sc.levels) r.ntail += l.len;
+            r.pin_at = pin_total;
+            pin_total += (nlev * sizeof(KllTail) + (size_t)r.ntail * 8 + 16 + 255) / 256 * 256;
+        }
+        uint8_t* pin = static_cast<uint8_t*>(dq::ctx_pinned_buf(ctx, pin_total));
+        if (!pin) return DQ_ERR_OUT_OF_MEMORY;
+        uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin);
+        KllColPtr* htab = reinterpret_cast<KllColPtr*>(pin + seg_bytes);
+        unsigned long long* hmm = reinterpret_cast<unsigned long long*>(pin + seg_bytes + tab_bytes);
+        kll_parallel(ncols, [&](int i) {
+            std::vector<size_t> cur(maxlev * NC);
+            for (size_t q = 0; q < cur.size(); ++q) cur[q] = first[q * ncols + i];
+            for (const uint64_t d : run[i].events) {  // the level bits give way to the column
+                const size_t h = (size_t)((d >> 55) & 0xFF);
+                const size_t c = (size_t)kll_class_of((int)((d >> 40) & 0x7FFF));
+                hsegs[cur[h * NC + c]++] = (d & ~(0xFFull << 55)) | ((uint64_t)i << 55);
+            }
+        });
+        uint8_t* gdev = nullptr;
+        KL_HIP(ctx, buf.alloc((void**)&gdev, seg_bytes + tab_bytes + mm_bytes));
+        const uint64_t* dsegs = reinterpret_cast<const uint64_t*>(gdev);
+        const KllColPtr* dtab = reinterpret_cast<const KllColPtr*>(gdev + seg_bytes);
+        unsigned long long* dmm = reinterpret_cast<unsigned long long*>(gdev + seg_bytes + tab_bytes);
+        std::vector<KllTail*> dtails(ncols);
+        std::vector<double*> dgats(ncols);
+        memset(htab, 0, tab_bytes);
+        for (int i = 0; i < ncols; ++i) {
+            KColumnRun& r = run[i];
+            const KllSchedule& sc = r.sc;
+            const size_t nlev = sc.levels.size();
+            r.lbase.assign(nlev, 0);
+            int64_t upper = 0;
+            for (size_t h = 1; h < nlev; ++h) {
+                r.lbase[h] = upper;
+                upper += sc.levels[h].arrived;
+            }
+            const size_t tail_off = ((size_t)upper * 8 + 255) / 256 * 256;
+            const size_t gat_off = tail_off + (nlev * sizeof(KllTail) + 255) / 256 * 256;
+            uint8_t* scratch = nullptr;
+            KL_HIP(ctx, buf.alloc((void**)&scratch, gat_off + (size_t)r.ntail * 8 + 256));
+            double* dup = reinterpret_cast<double*>(scratch);
+            dtails[i] = reinterpret_cast<KllTail*>(scratch + tail_off);
+            dgats[i] = reinterpret_cast<double*>(scratch + gat_off);
+            for (size_t h = 0; h < nlev; ++h)
+                htab[h * ncols + i] = KllColPtr{h == 0 ? r.stream0 : dup + r.lbase[h], h + 1 < nlev ? dup + r.lbase[h + 1] : nullptr,
+                                                h == 0 ? dmm + 2 * i : nullptr, 0ull};
+            hmm[2 * i] = ~0ull;
+            hmm[2 * i + 1] = 0ull;
+            KllTail* htails = reinterpret_cast<KllTail*>(pin + r.pin_at);
+            r.hgat = reinterpret_cast<double*>(pin + r.pin_at + nlev * sizeof(KllTail));
+            unsigned long long at = 0;
+            for (size_t h = 0; h < nlev; ++h) {
+                const KllLevel& l = sc.levels[h];
+                const double* src = (h == 0 ? r.stream0 : dup + r.lbase[h]) + l.pos;
+                htails[h] = KllTail{(unsigned long long)(uintptr_t)src, (unsigned long long)l.len, at};
+                at += (unsigned long long)l.len;
             }
         }
-        for (const uint64_t d : r.events)  // schedule order inside a group
-            hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
-    });
-    const unsigned long long mm_init[2] = {~0ull, 0ull};
-    for (int ci = 0; ci < ncols; ++ci) {
-        KColumnRun& r = run[ci];
-        hipStream_t cs = cstreams[ci % nstreams];
-        KllSchedule& sc = r.sc;
-        const size_t nlev = sc.levels.size(), nseg_all = r.events.size();
-        r.lbase.assign(nlev, 0);
-        int64_t upper = 0;
-        for (size_t h = 1; h < nlev; ++h) {
-            r.lbase[h] = upper;
-            upper += sc.levels[h].arrived;
+        KL_HIP(ctx, hipMemcpyAsync(gdev, pin, seg_bytes + tab_bytes + mm_bytes, hipMemcpyHostToDevice, s));
+        for (size_t h = 0; h < maxlev; ++h)
+            for (size_t c = 0; c < NC; ++c) {
+                size_t total = 0;
+                for (int i = 0; i < ncols; ++i) total += cnt[(h * NC + c) * ncols + i];
+                if (!total) continue;
+                if (launch_kll_compact((int)c, nullptr, dsegs + first[(h * NC + c) * ncols], (int)total, nullptr, nullptr, s,
+                                       dtab + h * ncols) != 0)
+                    return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
+            }
+        for (int i = 0; i < ncols; ++i) {
+            KColumnRun& r = run[i];
+            const size_t nlev = r.sc.levels.size();
+            KL_HIP(ctx, hipMemcpyAsync(dtails[i], pin + r.pin_at, nlev * sizeof(KllTail), hipMemcpyHostToDevice, s));
+            if (r.ntail)
+                hipLaunchKernelGGL(kll_gather_kernel, dim3((unsigned)nlev), dim3(256), 0, s, (const KllTail*)dtails[i], dgats[i]);
+            KL_HIP(ctx, hipGetLastError());
+            if (r.ntail)
+                KL_HIP(ctx, hipMemcpyAsync(r.hgat, dgats[i], sizeof(double) * (size_t)r.ntail, hipMemcpyDeviceToHost, s));
+            KL_HIP(ctx, hipMemcpyAsync(r.hgat + r.ntail, dmm + 2 * i, 16, hipMemcpyDeviceToHost, s));
         }
-        // device: [upper levels' streams][segment descriptors][min / max][level tails][gathered final buffers]
-        const size_t seg_off = ((size_t)upper * 8 + 255) / 256 * 256;
-        const size_t mm_off = seg_off + (nseg_all * 8 + 255) / 256 * 256;
-        const size_t tail_off = mm_off + 256;
-        const size_t gat_off = tail_off + (nlev * sizeof(KllTail) + 255) / 256 * 256;
-        uint8_t* scratch = nullptr;
-        KL_HIP(ctx, buf.alloc((void**)&scratch, gat_off + (size_t)r.ntail * 8 + 256));
-        double* dup = reinterpret_cast<double*>(scratch);
-        uint64_t* dsegs = reinterpret_cast<uint64_t*>(scratch + seg_off);
-        unsigned long long* dminmax = reinterpret_cast<unsigned long long*>(scratch + mm_off);
-        KllTail* dtails = reinterpret_cast<KllTail*>(scratch + tail_off);
-        double* dgat = reinterpret_cast<double*>(scratch + gat_off);
-        uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin + r.pin_at);
-        KllTail* htails = reinterpret_cast<KllTail*>(pin + r.pin_at + nseg_all * 8);
-        r.hgat = reinterpret_cast<double*>(pin + r.pin_at + nseg_all * 8 + nlev * sizeof(KllTail));
+    } else {
+        // pinned staging for every column: [segment descriptors][level tails][gathered final buffers + min / max keys]
+        size_t pin_total = 0;
+        for (KColumnRun& r : run) {
+            const size_t nlev = r.sc.levels.size(), nseg = r.events.size();
+            r.ntail = 0;
+            for (const KllLevel& l : r.sc.levels) r.ntail += l.len;
+            r.pin_at = pin_total;
+            pin_total += (nseg * 8 + nlev * sizeof(KllTail) + (size_t)r.ntail * 8 + 16 + 255) / 256 * 256;
+        }
+        uint8_t* pin = static_cast<uint8_t*>(dq::ctx_pinned_buf(ctx, std::max<size_t>(pin_total, 16)));
+        if (!pin) return DQ_ERR_OUT_OF_MEMORY;
+        // every column's descriptors grouped per (level, kernel class) straight into its pinned region, on the host threads
+        kll_parallel(ncols, [&](int i) {
+            KColumnRun& r = run[i];
+            const KllSchedule& sc = r.sc;
+            const size_t nlev = sc.levels.size();
+            uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin + r.pin_at);
+            size_t pos = 0;
+            std::vector<size_t> cursor(nlev * kKllAllClasses);
+            r.launches.clear();
+            for (size_t h = 0; h < nlev; ++h) {
+                const KllLevel& l = sc.levels[h];
+                for (int c = 0; c < kKllAllClasses; ++c) {
+                    cursor[h * kKllAllClasses + c] = pos;
+                    if (l.per_class[c]) r.launches.push_back({h, pos, (size_t)l.per_class[c], c});
+                    pos += (size_t)l.per_class[c];
+                }
+            }
+            for (const uint64_t d : r.events)  // schedule order inside a group
+                hsegs[cursor[(size_t)((d >> 55) & 0xFF) * kKllAllClasses + kll_class_of((int)((d >> 40) & 0x7FFF))]++] = d;
+        });
+        const unsigned long long mm_init[2] = {~0ull, 0ull};
+        for (int ci = 0; ci < ncols; ++ci) {
+            KColumnRun& r = run[ci];
+            hipStream_t cs = cstreams[ci % nstreams];
+            KllSchedule& sc = r.sc;
+            const size_t nlev = sc.levels.size(), nseg_all = r.events.size();
+            r.lbase.assign(nlev, 0);
+            int64_t upper = 0;
+            for (size_t h = 1; h < nlev; ++h) {
+                r.lbase[h] = upper;
+                upper += sc.levels[h].arrived;
+            }
+            // device: [upper levels' streams][segment descriptors][min / max][level tails][gathered final buffers]
+            const size_t seg_off = ((size_t)upper * 8 + 255) / 256 * 256;
+            const size_t mm_off = seg_off + (nseg_all * 8 + 255) / 256 * 256;
+            const size_t tail_off = mm_off + 256;
+            const size_t gat_off = tail_off + (nlev * sizeof(KllTail) + 255) / 256 * 256;
+            uint8_t* scratch = nullptr;
+            KL_HIP(ctx, buf.alloc((void**)&scratch, gat_off + (size_t)r.ntail * 8 + 256));
+            double* dup = reinterpret_cast<double*>(scratch);
+            uint64_t* dsegs = reinterpret_cast<uint64_t*>(scratch + seg_off);
+            unsigned long long* dminmax = reinterpret_cast<unsigned long long*>(scratch + mm_off);
+            KllTail* dtails = reinterpret_cast<KllTail*>(scratch + tail_off);
+            double* dgat = reinterpret_cast<double*>(scratch + gat_off);
+            uint64_t* hsegs = reinterpret_cast<uint64_t*>(pin + r.pin_at);
+            KllTail* htails = reinterpret_cast<KllTail*>(pin + r.pin_at + nseg_all * 8);
+            r.hgat = reinterpret_cast<double*>(pin + r.pin_at + nseg_all * 8 + nlev * sizeof(KllTail));
 
-        // one launch per (level, kernel class) group; the order inside a level is free because every compaction's
-        // input range and output slot are explicit
-        if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, cs));
-        KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, cs));
-        for (const KColumnRun::Launch& L : r.launches) {  // a level that compacted always has a level above it
-            const size_t h = L.level;
-            const double* src = h == 0 ? r.stream0 : dup + r.lbase[h];
-            double* dst = dup + r.lbase[h + 1];
-            if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, cs) != 0)
-                return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
+            // one launch per (level, kernel class) group; the order inside a level is free because every compaction's
+            // input range and output slot are explicit
+            if (nseg_all) KL_HIP(ctx, hipMemcpyAsync(dsegs, hsegs, nseg_all * 8, hipMemcpyHostToDevice, cs));
+            KL_HIP(ctx, hipMemcpyAsync(dminmax, mm_init, sizeof(mm_init), hipMemcpyHostToDevice, cs));
+            for (const KColumnRun::Launch& L : r.launches) {  // a level that compacted always has a level above it
+                const size_t h = L.level;
+                const double* src = h == 0 ? r.stream0 : dup + r.lbase[h];
+                double* dst = dup + r.lbase[h + 1];
+                if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, cs) != 0)
+                    return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
+            }
+            // final buffers: one gather, one read-back (completed by the single synchronisation below)
+            unsigned long long at = 0;
+            for (size_t h = 0; h < nlev; ++h) {
+                const KllLevel& l = sc.levels[h];
+                const double* src = (h == 0 ? r.stream0 : dup + r.lbase[h]) + l.pos;
+                htails[h] = KllTail{(unsigned long long)(uintptr_t)src, (unsigned long long)l.len, at};
+                at += (unsigned long long)l.len;
+            }
+            KL_HIP(ctx, hipMemcpyAsync(dtails, htails, nlev * sizeof(KllTail), hipMemcpyHostToDevice, cs));
+            if (r.ntail) hipLaunchKernelGGL(kll_gather_kernel, dim3((unsigned)nlev), dim3(256), 0, cs, (const KllTail*)dtails, dgat);
+            KL_HIP(ctx, hipGetLastError());
+            if (r.ntail) KL_HIP(ctx, hipMemcpyAsync(r.hgat, dgat, sizeof(double) * (size_t)r.ntail, hipMemcpyDeviceToHost, cs));
+            KL_HIP(ctx, hipMemcpyAsync(r.hgat + r.ntail, dminmax, 16, hipMemcpyDeviceToHost, cs));
         }
-        // final buffers: one gather, one read-back (completed by the single synchronisation below)
-        unsigned long long at = 0;
-        for (size_t h = 0; h < nlev; ++h) {
-            const KllLevel& l = sc.levels[h];
-            const double* src = (h == 0 ? r.stream0 : dup + r.lbase[h]) + l.pos;
-            htails[h] = KllTail{(unsigned long long)(uintptr_t)src, (unsigned long long)l.len, at};
-            at += (unsigned long long)l.len;
-        }
-        KL_HIP(ctx, hipMemcpyAsync(dtails, htails, nlev * sizeof(KllTail), hipMemcpyHostToDevice, cs));
-        if (r.ntail) hipLaunchKernelGGL(kll_gather_kernel, dim3((unsigned)nlev), dim3(256), 0, cs, (const KllTail*)dtails, dgat);
-        KL_HIP(ctx, hipGetLastError());
-        if (r.ntail) KL_HIP(ctx, hipMemcpyAsync(r.hgat, dgat, sizeof(double) * (size_t)r.ntail, hipMemcpyDeviceToHost, cs));
-        KL_HIP(ctx, hipMemcpyAsync(r.hgat + r.ntail, dminmax, 16, hipMemcpyDeviceToHost, cs));
     }
     for (int j = 1; j < nstreams; ++j) {
         KL_HIP(ctx, hipEventRecord(join_ev[j - 1], cstreams[j]));

@@ -1,6 +1,7 @@
 """KLL extra pass over the C5 shard's 10 numeric columns (5 % nulls) + 3 cast columns' worth of fp64 data: one
 dq_kll_sketch per column vs one dq_kll_sketch_columns call (parallel host schedules, one round trip), the latter with
-every column's compaction chain on one stream (DQ_KLL_SERIAL=1) and spread over the context's 4 streams; bytes compared,
+every column's compaction chain spread over the context's 4 streams (DQ_KLL_PER_COLUMN=1) and batched (one launch per
+level and class over all columns); bytes compared,
 wall time per pass (device synchronised), interleaved rounds.
 
     python tools/kll_ab.py [rows] [rounds] [no12]
@@ -43,14 +44,15 @@ for r in range(rounds + 1):
     single = [ctx.kll_sketch(x, rows, 2048, 0.64) for x in nat]
     ctx.synchronize()
     t1 = time.perf_counter()
-    os.environ["DQ_KLL_SERIAL"] = "1"
+    os.environ["DQ_KLL_PER_COLUMN"] = "1"  # one launch chain per column, spread over 4 streams
     serial = ctx.kll_sketch_columns(nat, rows, 2048, 0.64)
     ctx.synchronize()
-    del os.environ["DQ_KLL_SERIAL"]
+    del os.environ["DQ_KLL_PER_COLUMN"]
     t2 = time.perf_counter()
     batch = ctx.kll_sketch_columns(nat, rows, 2048, 0.64)
     ctx.synchronize()
     t3 = time.perf_counter()
     assert batch == single and serial == single, "batched KLL bytes differ"
-    print("round %d: 13 x dq_kll_sketch %.1f ms, dq_kll_sketch_columns one stream %.1f ms, on 4 streams %.1f ms "
+    print("round %d: 13 x dq_kll_sketch %.1f ms, dq_kll_sketch_columns per-column chains on 4 streams %.1f ms, "
+          "batched (one launch per level and class) %.1f ms "
           "(%d rows per column)" % (r, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, rows), flush=True)
