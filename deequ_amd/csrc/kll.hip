@@ -76,9 +76,20 @@ __device__ __forceinline__ bool kll_valid(const KllColumn& c, int64_t r) {
     return c.validity == nullptr || ((c.validity[r >> 6] >> (r & 63)) & 1ull);
 }
 
+// One column's NULL compaction: its tile counts, tile offsets and total (blockIdx.y of the count / scan launches).
+struct KllCountJob {
+    KllColumn c;
+    unsigned int* counts;
+    unsigned long long* offs;
+    unsigned long long* total;
+    double* dense;  // the dense level-0 stream (write pass), null when the column has no non-NULL value
+};
+
 // NULL compaction, pass 1: non-NULL rows per 2048-row tile.
 __global__ void __launch_bounds__(kKllStageBlock)
-kll_count_kernel(KllColumn c, int64_t nrows, unsigned int* __restrict__ tile_counts) {
+kll_count_kernel(const KllCountJob* __restrict__ jobs, int64_t nrows) {
+    const KllColumn c = jobs[blockIdx.y].c;
+    unsigned int* __restrict__ tile_counts = jobs[blockIdx.y].counts;
     __shared__ unsigned int red[kKllStageBlock / 64];
     const int64_t t = blockIdx.x;
     const int64_t r0 = t * kKllStageRows;
@@ -120,11 +131,42 @@ kll_write_kernel(KllColumn c, int64_t nrows, const unsigned long long* __restric
     }
 }
 
+// The same for every column of a batched sketch (blockIdx.y = job).
+__global__ void __launch_bounds__(kKllStageBlock)
+kll_write_jobs_kernel(const KllCountJob* __restrict__ jobs, int64_t nrows) {
+    const KllCountJob& j = jobs[blockIdx.y];
+    if (!j.dense) return;
+    __shared__ unsigned int wsum[kKllStageBlock / 64];
+    const KllColumn c = j.c;
+    const int64_t r0 = (int64_t)blockIdx.x * kKllStageRows;
+    unsigned long long base = j.offs[blockIdx.x];
+    double* __restrict__ out = j.dense;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t rb = r0; rb < r0 + kKllStageRows && rb < nrows; rb += kKllStageBlock) {
+        const int64_t r = rb + threadIdx.x;
+        const bool v = r < nrows && kll_valid(c, r);
+        const unsigned long long ball = __ballot(v);
+        const unsigned int before = (unsigned int)__popcll(ball & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[wave] = (unsigned int)__popcll(ball);
+        __syncthreads();
+        unsigned int wbase = 0, total = 0;
+        for (int w = 0; w < kKllStageBlock / 64; ++w) {
+            if (w < wave) wbase += wsum[w];
+            total += wsum[w];
+        }
+        if (v) out[base + wbase + before] = kll_load(c, r);
+        base += total;
+        __syncthreads();
+    }
+}
+
 // NULL compaction, between the passes: exclusive prefix of the tile counts (one workgroup) and the total, so only
 // the total travels to the host (the compaction schedule is a function of it).
 __global__ void __launch_bounds__(1024)
-kll_scan_kernel(const unsigned int* __restrict__ counts, int64_t ntiles, unsigned long long* __restrict__ offs,
-                unsigned long long* __restrict__ total) {
+kll_scan_kernel(const KllCountJob* __restrict__ jobs, int64_t ntiles) {
+    const unsigned int* __restrict__ counts = jobs[blockIdx.y].counts;
+    unsigned long long* __restrict__ offs = jobs[blockIdx.y].offs;
+    unsigned long long* __restrict__ total = jobs[blockIdx.y].total;
     __shared__ unsigned long long part[1024];
     const int t = threadIdx.x;
     const int64_t per = (ntiles + 1023) / 1024;
@@ -926,6 +968,8 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
     unsigned long long* dtotals = nullptr;
     KL_HIP(ctx, buf.alloc((void**)&dtotals, sizeof(unsigned long long) * std::max(ncols, 1)));
     int ncount = 0;
+    std::vector<KllCountJob> jobs;  // every NULL-compacted column's counts: one count and one scan launch for all
+    std::vector<int> job_col;
     for (int i = 0; i < ncols; ++i) {
         const dq_column* column = &columns[i];
         KColumnRun& r = run[i];
@@ -957,12 +1001,20 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
             unsigned int* dcounts = nullptr;
             KL_HIP(ctx, buf.alloc((void**)&dcounts, sizeof(unsigned int) * ntiles));
             KL_HIP(ctx, buf.alloc((void**)&r.doffs, sizeof(unsigned long long) * ntiles));
-            hipLaunchKernelGGL(kll_count_kernel, dim3((unsigned)ntiles), dim3(kKllStageBlock), 0, s, r.kc, nrows, dcounts);
-            hipLaunchKernelGGL(kll_scan_kernel, dim3(1), dim3(1024), 0, s, (const unsigned int*)dcounts, ntiles, r.doffs,
-                               dtotals + i);
-            KL_HIP(ctx, hipGetLastError());
+            jobs.push_back(KllCountJob{r.kc, dcounts, r.doffs, dtotals + i, nullptr});
+            job_col.push_back(i);
             ++ncount;
         }
+    }
+    if (ncount) {
+        KllCountJob* djobs = nullptr;
+        KL_HIP(ctx, buf.alloc((void**)&djobs, sizeof(KllCountJob) * jobs.size()));
+        KL_HIP(ctx, hipMemcpyAsync(djobs, jobs.data(), sizeof(KllCountJob) * jobs.size(), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(kll_count_kernel, dim3((unsigned)ntiles, (unsigned)jobs.size()), dim3(kKllStageBlock), 0, s,
+                           (const KllCountJob*)djobs, nrows);
+        hipLaunchKernelGGL(kll_scan_kernel, dim3(1, (unsigned)jobs.size()), dim3(1024), 0, s, (const KllCountJob*)djobs,
+                           ntiles);
+        KL_HIP(ctx, hipGetLastError());
     }
     if (ncount) {  // one round trip for every column's non-NULL count
         unsigned long long* htotals = static_cast<unsigned long long*>(dq::ctx_pinned_buf(ctx, 8 * (size_t)ncols));
@@ -989,8 +1041,22 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
             for (int j = 1; j < nstreams; ++j) KL_HIP(ctx, hipStreamWaitEvent(cstreams[j], fork_ev, 0));
         }
     }
-    // dense level-0 streams go out while the host computes the (count-only) compaction schedules
-    for (int i = 0; i < ncols; ++i) {
+    // dense level-0 streams go out while the host computes the (count-only) compaction schedules; batched: one launch
+    if (batched && !jobs.empty()) {
+        for (size_t j = 0; j < jobs.size(); ++j) {
+            KColumnRun& r = run[job_col[j]];
+            if (r.n <= 0) continue;
+            KL_HIP(ctx, buf.alloc((void**)&jobs[j].dense, (size_t)r.n * 8));
+            r.stream0 = jobs[j].dense;
+        }
+        KllCountJob* wjobs = nullptr;
+        KL_HIP(ctx, buf.alloc((void**)&wjobs, sizeof(KllCountJob) * jobs.size()));
+        KL_HIP(ctx, hipMemcpyAsync(wjobs, jobs.data(), sizeof(KllCountJob) * jobs.size(), hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(kll_write_jobs_kernel, dim3((unsigned)ntiles, (unsigned)jobs.size()), dim3(kKllStageBlock), 0, s,
+                           (const KllCountJob*)wjobs, nrows);
+        KL_HIP(ctx, hipGetLastError());
+    }
+    for (int i = 0; i < ncols && !batched; ++i) {
         KColumnRun& r = run[i];
         if (r.zero_copy || r.n <= 0) continue;
         double* dense = nullptr;
