@@ -371,8 +371,8 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
  * in one pass over the partitions): column i's KLLState bytes, exactly those of dq_kll_sketch, go to
  * state_out + (sum of sizes[0..i)) and sizes[i] receives their length. Returns the total length (nothing is written
  * when it exceeds `capacity`: call again with a larger buffer) or a negative dq_status. The columns' compaction
- * schedules are computed on parallel host threads and every column's kernels are queued on the stream with one host
- * round trip for all of them. */
+ * schedules are computed on parallel host threads; the NULL-compaction passes and every compaction level (per kernel
+ * class) are one launch each over all the columns, with one host round trip for all of them. */
 int64_t dq_kll_sketch_columns(dq_ctx* ctx, const dq_column* columns, int32_t ncols, int64_t nrows, int32_t sketch_size,
                               double shrinking_factor, uint8_t* state_out, int64_t capacity, int64_t* sizes);
 
