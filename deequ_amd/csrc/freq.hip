@@ -1229,23 +1229,23 @@ template <int LS>  // slots of the workgroup's LDS table
 __global__ void __launch_bounds__(kBuildBlock)
 small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
                    unsigned long long* __restrict__ wg_keys, unsigned long long* __restrict__ wg_reps,
-                   Counters* __restrict__ ctr) {
+                   Counters* __restrict__ ctr, int count_rows) {
     __shared__ unsigned long long lkey[LS];
     __shared__ unsigned int lcnt[LS];
     __shared__ unsigned long long lrep[LS];
     __shared__ unsigned long long red[kBuildBlock / 64];
-    __shared__ unsigned int lovf;
+    __shared__ unsigned int lovf, lfill;
     for (int i = threadIdx.x; i < LS; i += kBuildBlock) {
         lkey[i] = kEmpty;
         lcnt[i] = 0;
         lrep[i] = ~0ull;
     }
-    if (threadIdx.x == 0) lovf = 0;
+    if (threadIdx.x == 0) lovf = lfill = 0;
     __syncthreads();
     auto start = [](uint64_t h) { return (unsigned int)(h >> 52) & (LS - 1); };
     int64_t r0, r1;
     chunk_of(nrows, r0, r1);
-    unsigned long long bad = 0;
+    unsigned long long bad = 0, taken = 0;
     bool ok = true;
     for (int64_t t0 = r0; t0 < r1; t0 += kSmallTile) {
         uint64_t h[4];
@@ -1256,16 +1256,23 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
             bool ng = false;
             h[u] = kEmpty;
             take[u] = r < r1 && row_key(ks, r, h[u], ng) && !ng && h[u] != kEmpty;
+            taken += take[u] ? 1 : 0;
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (!take[u]) continue;
             const unsigned long long row = (unsigned long long)(t0 + (int64_t)u * kBuildBlock + threadIdx.x);
+            // past 3/4 full the table counts as overflowing (bounded probe chains when the guess was wrong)
+            if (*(volatile unsigned int*)&lfill > (unsigned int)(LS / 4 * 3)) {
+                ok = false;
+                continue;
+            }
             unsigned int p = start(h[u]);
             bool done = false;
             for (int probe = 0; probe < LS; ++probe) {
                 const unsigned long long prev = atomicCAS(&lkey[p], kEmpty, h[u]);
                 if (prev == kEmpty || prev == h[u]) {
+                    if (prev == kEmpty) atomicAdd(&lfill, 1u);
                     atomicAdd(&lcnt[p], 1u);
                     atomicMin(&lrep[p], row);
                     done = true;
@@ -1275,7 +1282,9 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
             }
             ok &= done;
         }
+        if (!ok) lovf = 1;
         __syncthreads();
+        if (lovf) break;  // a full table: the build goes elsewhere, stop reading rows (uniform: read after the barrier)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (!take[u]) continue;
@@ -1311,6 +1320,17 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
         mok &= done;
     }
     if (!mok) lovf = 1;
+    if (count_rows) {  // numRows when no sizing pass counted it (the optimistic small build)
+        for (int off = 32; off > 0; off >>= 1) taken += __shfl_down(taken, off, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = taken;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long t = 0;
+            for (int w = 0; w < kBuildBlock / 64; ++w) t += red[w];
+            if (t) atomicAdd(&ctr->num_rows, t);
+        }
+        __syncthreads();  // `red` is reused below
+    }
     for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bad;
     __syncthreads();
@@ -1775,8 +1795,10 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
 
 // Small general tables (bits = 0): small_build_kernel + small_check_kernel, the table one region. *overflow sends the
 // caller to the regular path, *collision to a new seed.
-int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf& buf, bool* overflow, bool* collision) {
+int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf& buf, bool* overflow, bool* collision,
+                bool count_rows = false) {
     hipStream_t s = dq::ctx_stream(ctx);
+    if (count_rows) FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
     release_slots(t, ctx);
     t->home = ctx;
     t->slots_bytes = kRegion * sizeof(Slot);
@@ -1798,10 +1820,10 @@ int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf
     // a 2048-slot workgroup table (40 KB of LDS: 3 workgroups per CU instead of 1) when the estimate leaves it <= 5/8 full
     if (est <= 1280.0)
         hipLaunchKernelGGL((small_build_kernel<2048>), dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots, t->reps,
-                           wk, wr, t->ctr);
+                           wk, wr, t->ctr, count_rows ? 1 : 0);
     else
         hipLaunchKernelGGL((small_build_kernel<kRegion>), dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots,
-                           t->reps, wk, wr, t->ctr);
+                           t->reps, wk, wr, t->ctr, count_rows ? 1 : 0);
     hipLaunchKernelGGL(small_check_kernel, dim3(grid), dim3(kBuildBlock), 0, s, t->ks, t->slots, t->reps, wk, wr, t->ctr);
     FQ_HIP(ctx, hipGetLastError());
     FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
@@ -1933,6 +1955,7 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
 // nothing that the exact path cannot redo, when a bucket overflows its capacity (heavy hitters) or the table is
 // too small or too large for the two-pass bucketing.
 constexpr int64_t kFastMinRows = 1 << 24;
+constexpr int64_t kOptimisticSmallRows = 1 << 22;  // below: the sizing pass is cheap, keep the sized path
 
 // Signed min / max of the canonical values of a strided sample of an 8-byte integral key column (narrow-key choice):
 // one sampled row per thread (no dependent load chain), block minima / maxima folded with 64-bit atomics.
@@ -2174,6 +2197,17 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         bool done = false;
         const int rc = build_fast(ctx, t, nrows, buf, &done);
         if (rc != DQ_OK || done) return rc;
+    }
+    // General keys, unweighted: try the one-pass small build first, without the sizing pass (a histogram column the
+    // ColumnProfiler sends here has <= 120 distinct values). A workgroup whose LDS table fills stops at once and the
+    // build takes the sized path below (the cost of a wrong guess: a few thousand rows per workgroup); a fingerprint
+    // collision also goes there (it re-seeds).
+    if (general && !t->ks.weights && nrows >= kOptimisticSmallRows && !getenv("DQ_FREQ_NO_SMALL") &&
+        !getenv("DQ_FREQ_NO_OPTIMISTIC")) {
+        bool overflow = false, collision = false;
+        const int rc = build_small(ctx, t, nrows, 0.0, buf, &overflow, &collision, true);
+        if (rc != DQ_OK) return rc;
+        if (!overflow && !collision) return DQ_OK;
     }
     for (int seed_attempt = 0; seed_attempt < 4; ++seed_attempt) {
         unsigned long long *hs = nullptr, *rows = nullptr, *bk = nullptr;

@@ -297,6 +297,27 @@ def test_small_table_path_equals_the_regular_path(device):
     _summary_vs_oracle(t, ["s", "k"])
 
 
+@pytest.mark.parametrize("distinct", [60, 3000, 1_000_000])
+def test_optimistic_small_build_equals_the_sized_path(distinct):
+    """General keys with >= 2^22 rows first try the one-pass small build without the sizing pass: it must equal the
+    sized path (DQ_FREQ_NO_OPTIMISTIC=1) when it succeeds (60 distinct strings), when the union of the workgroup
+    tables overflows the one region (3000) and when every workgroup's LDS table fills at once (1e6 distinct)."""
+    import pyarrow as pa
+    rng = np.random.default_rng(distinct)
+    n = 5_000_000
+    words = np.array(["v%07d" % i for i in range(distinct)], dtype=object)
+    idx = rng.integers(0, distinct, n)
+    valid = rng.random(n) > 0.03
+    arr = pa.array(words[idx], type=pa.string(), mask=~valid)
+    t = Table.from_arrow(pa.table({"s": arr, "k": pa.array(rng.integers(0, 2, n))}))
+    t.to_device(0)
+    for cols, nulls in ((["s"], True), (["s", "k"], False)):
+        opt, osum = _freq_dict(t, cols, nulls)
+        sized, ssum = _freq_dict(t, cols, nulls, {"DQ_FREQ_NO_OPTIMISTIC": "1"})
+        assert opt == sized, (distinct, cols)
+        assert osum == ssum, (distinct, cols, osum, ssum)
+
+
 def test_fingerprint_collisions_are_never_merged():
     """Fingerprints narrowed to 4 bits (DQ_FREQ_FP_MASK) collide on every seed: both the small path and the regular
     path detect the collisions against the representatives and fail the build instead of merging groups."""
