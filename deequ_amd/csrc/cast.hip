@@ -42,21 +42,46 @@ __device__ __forceinline__ int64_t java_d2l(double d) {
     return (int64_t)d;
 }
 
+// Bytes of one wave's 64 consecutive strings staged in LDS by coalesced dword loads (the parsers then read LDS, not
+// scattered HBM bytes); a longer range is parsed from HBM directly.
+constexpr int kCastStageWords = 512;
+
 template <bool STRING>
 __global__ void __launch_bounds__(kCastBlock)
 cast_kernel(CastSource c, int64_t nrows, int to_double, void* __restrict__ values_out,
             uint64_t* __restrict__ validity_out, unsigned int* __restrict__ slow_flag) {
+    __shared__ uint32_t stage[STRING ? kCastBlock / 64 : 1][STRING ? kCastStageWords : 1];
     const int64_t stride = (int64_t)gridDim.x * kCastBlock;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t base = (int64_t)blockIdx.x * kCastBlock; base < nrows; base += stride) {
         const int64_t r = base + threadIdx.x;
         bool ok = false;
         double d = 0.0;
         int64_t v = 0;
+        const uint8_t* sbase = nullptr;  // STRING: the staged copy of this wave's bytes, based at a0
+        int64_t a0 = 0;
+        if (STRING) {
+            const int64_t w0 = base + 64 * wave;
+            if (w0 < nrows) {
+                const int64_t wl = w0 + 64 < nrows ? w0 + 64 : nrows;
+                const int64_t b0 = c.offsets[w0], b1 = c.offsets[wl];
+                a0 = b0 & ~(int64_t)3;
+                const int64_t nwords = (b1 - a0 + 3) >> 2;  // dwords holding [b0, b1): nothing past the last byte
+                if (nwords <= kCastStageWords) {
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(c.bytes + a0);
+                    for (int64_t i = lane; i < nwords; i += 64) stage[wave][i] = src[i];
+                    sbase = reinterpret_cast<const uint8_t*>(&stage[wave][0]);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
         if (r < nrows && (c.validity == nullptr || ((c.validity[r >> 6] >> (r & 63)) & 1ull))) {
             if (STRING) {
                 const int32_t o = c.offsets[r];
                 const int len = c.offsets[r + 1] - o;
-                const uint8_t* s = c.bytes + o;
+                const uint8_t* s = sbase ? sbase + (o - a0) : c.bytes + o;
                 if (to_double) {
                     bool slow = false;
                     ok = java_parse_double(s, len, d, slow);
@@ -93,6 +118,7 @@ cast_kernel(CastSource c, int64_t nrows, int to_double, void* __restrict__ value
         }
         const unsigned long long ball = __ballot(ok);
         if ((threadIdx.x & 63) == 0 && r < nrows) validity_out[r >> 6] = ball;
+        if (STRING) __builtin_amdgcn_wave_barrier();  // every lane's parse done before the next group's staging
     }
 }
 
