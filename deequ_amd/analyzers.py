@@ -110,6 +110,10 @@ def merge(*states):
     return out
 
 
+# Placeholder result of an analyzer whose state went to a states-only provider (see Analyzer.calculateMetric).
+STATE_ONLY = DoubleMetric(Entity.Dataset, "StateOnly", "*", Success(0.0))
+
+
 # ---- Analyzer base classes (A/Analyzer.scala:56-197) ---------------------------------------------
 class Analyzer:
     _fields = ()
@@ -162,11 +166,15 @@ class Analyzer:
             return self.toFailureMetric(e)
 
     def calculateMetric(self, state, aggregateWith=None, saveStatesWith=None):
-        """A/Analyzer.scala:107-128."""
+        """A/Analyzer.scala:107-128. A states-only provider (the row chunks of a ChunkedTable, whose states are merged
+        before any metric) takes the state and no metric is computed (STATE_ONLY: not even the empty-state failure,
+        which only the merged state decides)."""
         loaded = aggregateWith.load(self) if aggregateWith is not None else None
         to_use = merge(state, loaded)
         if to_use is not None and saveStatesWith is not None:
             saveStatesWith.persist(self, to_use)
+        if getattr(saveStatesWith, "states_only", False):
+            return STATE_ONLY
         return self.computeMetricFrom(to_use)
 
     def aggregateStateTo(self, sourceA, sourceB, target):

@@ -8,7 +8,7 @@ import os
 from . import native as N
 from . import engine
 from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer,
-                        FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies)
+                        FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies, STATE_ONLY)
 from .expr import compile_predicate
 from .metrics import DoubleMetric, Success, UnsupportedOnDevice
 from .table import ChunkedTable
@@ -313,10 +313,12 @@ class AnalysisRunner:
         """A ChunkedTable: every chunk runs the analysis (its scan, grouping and KLL passes on the GPU) and persists
         its states in memory; the chunk states (and the states of `aggregateWith`) then merge in chunk order through
         runOnAggregatedStates — Spark's partial aggregates of one `agg` over the partitions, merged by the same
-        State.sum. An analyzer that failed on any chunk keeps that chunk's failure metric."""
+        State.sum. An analyzer whose state computation failed on any chunk (an exception, not an empty state) keeps
+        that chunk's failure metric."""
         providers, failures = [], {}
         for chunk in data.chunks:
             p = InMemoryStateProvider()
+            p.states_only = True  # states only: no per-chunk metric (an empty chunk state is no failure)
             res = AnalysisRunner.doAnalysisRun(chunk, analyzers, saveStatesWith=p)
             for a, m in res.metricMap.items():
                 if not m.value.isSuccess and a not in failures:
@@ -326,7 +328,15 @@ class AnalysisRunner:
             providers.append(aggregateWith)
         merged = AnalysisRunner.runOnAggregatedStates(data.schema, Analysis(list(analyzers)), providers,
                                                       saveStatesWith)
-        return merged + AnalyzerContext(failures)
+        # no chunk had a state (every chunk empty for it): the metric of an empty state, as one run over all rows
+        empty = {}
+        for a in dict.fromkeys(analyzers):
+            if a not in merged.metricMap and a not in failures:
+                try:
+                    empty[a] = a.computeMetricFrom(None)
+                except Exception as e:
+                    empty[a] = a.toFailureMetric(e)
+        return merged + AnalyzerContext(empty) + AnalyzerContext(failures)
 
     @staticmethod
     def _runScanningAnalyzers(data, analyzers, aggregateWith=None, saveStatesTo=None):
@@ -375,6 +385,9 @@ class AnalysisRunner:
 
     @staticmethod
     def _runAnalyzersForParticularGrouping(freq, analyzers, saveStatesTo=None):
+        if getattr(saveStatesTo, "states_only", False):  # a row chunk: the merged state computes the metrics
+            saveStatesTo.persist(analyzers[0], freq)
+            return AnalyzerContext({a: STATE_ONLY for a in analyzers})
         results = {}
         for a in analyzers:
             try:

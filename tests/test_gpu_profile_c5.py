@@ -148,3 +148,33 @@ def _check_profile(t, prof, exp):
             for k, v in p.histogram.values.items():
                 assert v.ratio == e["histogram"][k] / ROWS
     assert seen_hist >= 5 and seen_numeric_string == 3
+
+
+def test_chunked_run_with_an_all_null_chunk_equals_the_whole_table():
+    """A column that is NULL on every row of one chunk: that chunk's empty states are no failure -- the merged state
+    decides (as Spark's partial aggregates do); a column NULL everywhere fails on both sides the same way."""
+    rng = np.random.default_rng(5)
+    n = 30_000
+    x = [None if (i < 12_000 or rng.random() < 0.1) else float(rng.normal()) for i in range(n)]
+    k = [int(v) for v in rng.integers(0, 50, n)]
+    z = [None] * n
+    data = {"x": x, "k": k, "z": z}
+    types = {"x": "double", "k": "long", "z": "double"}
+    full = Table.from_pydict(data, types=types).to_device()
+    cuts = [0, 12_000, 20_000, n]
+    chunks = [Table.from_pydict({c: v[a:b] for c, v in data.items()}, types=types).to_device()
+              for a, b in zip(cuts, cuts[1:])]
+    ct = D.ChunkedTable(chunks)
+    an = [D.Mean("x"), D.Minimum("x"), D.StandardDeviation("x"), D.Completeness("x"), D.ApproxCountDistinct("x"),
+          D.Uniqueness(["x"]), D.KLLSketch("x"), D.Mean("z"), D.Sum("k"), D.Size()]
+    want = D.AnalysisRunner.onData(full).addAnalyzers(an).run()
+    got = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in an:
+        w, g = want.metric(a).value, got.metric(a).value
+        assert w.isSuccess == g.isSuccess, (a, w, g)
+        if not w.isSuccess:
+            continue
+        if isinstance(a, D.KLLSketch):
+            assert sum(b.count for b in g.get().buckets) == sum(b.count for b in w.get().buckets), a
+        else:
+            assert _close(g.get(), w.get()), (a, g.get(), w.get())
