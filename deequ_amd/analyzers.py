@@ -440,10 +440,9 @@ class PatternMatch(StandardScanShareableAnalyzer):
         return self.pattern_
 
     def addOps(self, batch):
-        col = batch.data[self.column] if self.column in batch.col_index else None
-        if col is not None and col.spark_type in (N.TYPE_DECIMAL, N.TYPE_DATE, N.TYPE_TIMESTAMP):
-            raise UnsupportedOnDevice(
-                "PatternMatch over %s: the GPU engine does not format this type as a string" % col.type_name)
+        # regexp_extract casts a non-string column to STRING (Spark's implicit cast): the device formats every cell
+        # as Cast(x AS STRING) does — Java toString of numerics, BigDecimal.toString of decimals, "yyyy-MM-dd" of
+        # dates and "yyyy-MM-dd HH:mm:ss[.ffffff]" of timestamps in a UTC session time zone (regex.hip)
         p = batch.regex_predicate(self.column, self.pattern_)
         return [batch.add_op(N.OP_COMPLIANCE, where=self.where, predicate_index=p)]
 
@@ -714,8 +713,12 @@ class FrequenciesAndNumRows:
         if isinstance(f, engine.FrequencyTable):
             return f
         if self._device is None and isinstance(f, G.BlockParts):
-            table, counts = f.device_table()
-            self._device = engine.frequencies(table, f.names, False, weights=counts)
+            splits = f.split_by_key()
+            tables = []
+            for s in splits:
+                table, counts = s.device_table()
+                tables.append(engine.frequencies(table, s.names, False, weights=counts))
+            self._device = tables[0] if len(tables) == 1 else SplitFrequencies(tables, f.names)
         elif self._device is None and isinstance(f, G.GroupBlock):
             self._device = engine.frequencies(f.table(), f.names, False, weights=f.counts)
         if self._device is None and isinstance(f, engine.PairFrequencies):
@@ -738,6 +741,31 @@ class FrequenciesAndNumRows:
                 ent = float(-(p * np.log(p)).sum())
             return {"num_groups": len(counts), "num_unique": int((counts == 1).sum()), "entropy": ent}
         return self.device_table().summary(n)
+
+
+class SplitFrequencies:
+    """A merged string / multi-column state too large for one device build (its key bytes reach the int32 Arrow
+    offsets): weighted tables over key-disjoint splits of its groups (groups.BlockParts.split_by_key). A key lives in
+    exactly one split, so the fused aggregation over the whole table (A/GroupingAnalyzers.scala:83-120) is the sum
+    of the splits' (groups, unique groups, entropy terms), as in the multi-device union of dq_open_devices."""
+
+    def __init__(self, tables, names):
+        self.tables = list(tables)
+        self.names = list(names)
+        self.source = None  # no single source table: MutualInformation's marginals need the joint groups in one
+
+    def key_kind(self):
+        return self.tables[0].key_kind()
+
+    def summary(self, entropy_rows=None):
+        parts = [t.summary(entropy_rows) for t in self.tables]
+        return {"num_rows": sum(p["num_rows"] for p in parts), "num_groups": sum(p["num_groups"] for p in parts),
+                "num_unique": sum(p["num_unique"] for p in parts),
+                "entropy": math.fsum(p["entropy"] for p in parts), "entropy_rows": parts[0]["entropy_rows"],
+                "max_count": max(p["max_count"] for p in parts), "null_count": sum(p["null_count"] for p in parts)}
+
+    def export_raw(self):
+        raise ValueError("a split frequency state has no single source table to export representative rows from")
 
 
 def _block_from_dict(freq, like):
@@ -936,15 +964,34 @@ class Histogram(Analyzer):
 
     def computeStateFrom(self, data):
         if self.binningUdf is not None:
-            # The binning UDF is an arbitrary host function: apply it to the key column, then group.
-            from .table import Table, _column_from_pylist
-            vals = data[self.column].to_pylist()
-            binned = [self.binningUdf(None if v is None else _spark_string(v, data[self.column])) for v in vals]
-            t = Table([_column_from_pylist(self.column, "string", binned)])
-            table = engine.frequencies(t, [self.column], include_nulls=True)
-        else:
-            table = engine.frequencies(data, [self.column], include_nulls=True)
+            return FrequenciesAndNumRows(self.binned_counts(data), data.count(), [self.column])
+        table = engine.frequencies(data, [self.column], include_nulls=True)
         return FrequenciesAndNumRows(table, data.count(), [self.column])
+
+    def binned_counts(self, data):
+        """`data.withColumn(column, bin(col(column))).select(col(column).cast(StringType)).na.fill("NullValue")
+        .groupBy(column).count()` (A/Histogram.scala:59-65) without a per-row Python call: the column's groups are
+        counted on the GPU, the UDF runs once per DISTINCT value (and once for NULL, as a Scala UDF over an object
+        type sees the nulls), and the bins add the groups' counts — exact for any deterministic UDF. The UDF receives
+        the column's value (str, int, float, ...), as a Spark UDF receives the Scala value. {(bin label,): count}."""
+        ft = engine.frequencies(data, [self.column], include_nulls=False)
+        return self.bin_groups(((k[0], c) for k, c in ft.to_dict().items()), data.count() - ft.num_rows)
+
+    def bin_groups(self, groups, null_rows):
+        """(value, count) groups of the raw column + its NULL rows -> {(bin label,): count}: the UDF's result cast to
+        STRING, NULL filled with "NullValue", counts added per bin."""
+        bins = {}
+
+        def add(value, count):
+            label = self.binningUdf(value)
+            label = Histogram.NullFieldReplacement if label is None else (
+                label if isinstance(label, str) else _spark_string(label))
+            bins[(label,)] = bins.get((label,), 0) + int(count)
+        for v, c in groups:
+            add(float(v) if isinstance(v, float) else v, c)
+        if null_rows:
+            add(None, null_rows)
+        return bins
 
     def computeMetricFrom(self, state):
         if state is None:

@@ -418,6 +418,13 @@ int64_t dq_scan_kernel_launches(const dq_ctx* ctx, int32_t kernel) {
     return n;
 }
 
+int64_t dq_freq_path_count(const dq_ctx* ctx, int32_t path) {
+    if (!ctx || path < 0 || path >= DQ_FREQ_PATH_COUNT) return -1;
+    int64_t n = ctx->freq_paths[path];
+    for (const dq_ctx* sub : ctx->subs) n += sub->freq_paths[path];
+    return n;
+}
+
 int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const dq_op* ops, int nops,
             const dq_predicate* preds, int npreds, dq_state* out, uint32_t flags) {
     if (!ctx) return DQ_ERR_INVALID_ARGUMENT;
@@ -529,9 +536,11 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 pr.consts[k].str_offset + pr.consts[k].str_len > pr.strings_len)
                 return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: malformed REGEX program", p);
             const int t = columns[c].spark_type;
-            if (!(t == DQ_TYPE_STRING || t == DQ_TYPE_BOOLEAN || t == DQ_TYPE_BYTE || t == DQ_TYPE_SHORT ||
-                  t == DQ_TYPE_INT || t == DQ_TYPE_LONG || t == DQ_TYPE_FLOAT || t == DQ_TYPE_DOUBLE))
+            if (t < DQ_TYPE_BOOLEAN || t > DQ_TYPE_DECIMAL)
                 return fail(ctx, DQ_ERR_UNSUPPORTED, "predicate %d: PatternMatch over this column type is not supported", p);
+            if (t == DQ_TYPE_DECIMAL && (columns[c].decimal_scale < 0 || columns[c].decimal_scale > 18))
+                return fail(ctx, DQ_ERR_UNSUPPORTED, "predicate %d: PatternMatch over a DECIMAL of scale %d", p,
+                            columns[c].decimal_scale);
             col_used[c] = 1;
             continue;
         }

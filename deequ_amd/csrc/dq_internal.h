@@ -271,6 +271,7 @@ struct dq_ctx {
     std::map<int, int> occupancy;  // launch shape -> workgroups per CU
     int64_t scan_launches = 0;
     int64_t kernel_launches[DQ_KERNEL_COUNT] = {};  // by dq_scan_kernel
+    int64_t freq_paths[DQ_FREQ_PATH_COUNT] = {};     // by dq_freq_path
     // Released device scratch of the grouping builds (multi-GB partition buffers and tables), re-used in stream
     // order instead of a hipMalloc / hipFree pair per call; bounded, freed at dq_close and on allocation failure.
     struct CachedBlock {

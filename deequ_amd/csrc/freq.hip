@@ -299,6 +299,7 @@ struct Counters {
     unsigned long long mismatch;   // general path verification: fingerprint collisions
     unsigned long long pad[3];
     unsigned long long narrow_miss;  // fast path, narrow keys: 8-byte keys outside the 32-bit window
+    unsigned long long spilled;      // fast path: keys past a full bucket, appended to the spill buffer
 };
 
 __device__ __forceinline__ unsigned long long block_sum_u64(unsigned long long v, unsigned long long* lds4) {
@@ -771,19 +772,28 @@ __device__ __forceinline__ uint64_t canonical_of(int elem, uint64_t raw) {
     return elem == ET_U8 ? (raw ? 1ull : 0ull) : (uint64_t)(int64_t)(int8_t)(uint8_t)raw;
 }
 
+// Keys that do not fit their bucket (a key repeated more often than a bucket's slack: NaN, 0, a default value) go
+// to one spill buffer as full 64-bit keys, reserved per wave; the build inserts them into the finished table with
+// global atomics (spill_insert_kernel). Only a full spill buffer sends the build to the exactly-counted path.
+struct Spill {
+    unsigned long long* keys;
+    unsigned long long cap;
+    unsigned long long* count;  // Counters::spilled
+};
+
 // One tile already in registers (h, keep) -> LDS staging ordered by digit -> global runs reserved with atomics:
-// digit b's run goes to bucket k = bucket_of(b), at k * cap + atomicAdd(&gcursor[k], hist[b]), when it fits the
-// bucket's capacity; otherwise *lovf is raised and nothing more is written.
+// digit b's run goes to bucket k = bucket_of(b), at k * cap + atomicAdd(&gcursor[k], hist[b]); the part of a run past
+// the bucket's capacity is spilled (to_key(staged word) into `sp`), and a full spill buffer raises *lovf.
 // NARROW: the staged word is (digit << 32) | 32-bit payload and the payload is what goes out (narrow keys, below);
 // otherwise the staged word is the key itself, its digit (key >> shift) & mask.
-template <int BINS, int TILE, bool NARROW, typename BucketOf, typename CounterOf, typename Prefetch, typename OutT>
+template <int BINS, int TILE, bool NARROW, typename BucketOf, typename CounterOf, typename Prefetch, typename OutT,
+          typename ToKey>
 __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / kFreqBlock], unsigned int keepm,
                                                      int shift, unsigned int mask, unsigned int* hist, unsigned int* start,
                                                      unsigned long long* cursor, unsigned long long* sh,
                                                      unsigned long long* __restrict__ gcursor, unsigned long long cap,
                                                      BucketOf bucket_of, CounterOf counter_of, unsigned int* lovf,
-                                                     unsigned int* lbad,
-                                                     unsigned long long limit, OutT* __restrict__ out_h,
+                                                     const Spill& sp, ToKey to_key, OutT* __restrict__ out_h,
                                                      Prefetch prefetch) {
     constexpr int PER = TILE / kFreqBlock;
     static_assert(PER <= 32, "keep flags are one bit per key");
@@ -827,7 +837,6 @@ __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / 
             if (hb) {
                 const unsigned long long k = bucket_of(b0 + b);
                 const unsigned long long at = atomicAdd(&gcursor[counter_of(b0 + b)], (unsigned long long)hb);
-                if (at + hb > cap) *lovf = 1u;
                 cursor[b0 + b] = k * cap + at;
             }
         }
@@ -843,12 +852,25 @@ __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / 
     }
     __syncthreads();
     if (!*lovf) {  // (uniform: read after the barrier that follows every write of the flag)
+        const unsigned int lane = threadIdx.x & 63;
         for (unsigned int i = threadIdx.x; i < total; i += kFreqBlock) {
             const unsigned long long hv = sh[i];
             const unsigned int d = digit(hv);
             const unsigned long long pos = cursor[d] + (i - start[d]);
-            if (pos < limit) out_h[pos] = (OutT)hv;  // always true; a violated invariant is reported, never written
-            else *lbad = 1u;
+            const bool fits = pos < (bucket_of(d) + 1) * cap;
+            if (fits) out_h[pos] = (OutT)hv;
+            const unsigned long long sm = __ballot(!fits);
+            if (sm) {  // wave-uniform: one reservation per wave for its spilled keys
+                const int leader = __ffsll((long long)sm) - 1;
+                unsigned long long base = 0;
+                if ((int)lane == leader) base = atomicAdd(sp.count, (unsigned long long)__popcll(sm));
+                base = __shfl(base, leader, 64);
+                if (!fits) {
+                    const unsigned long long at = base + __popcll(sm & ((1ull << lane) - 1ull));
+                    if (at < sp.cap) sp.keys[at] = to_key(hv);
+                    else *lovf = 1u;
+                }
+            }
         }
     }
     __syncthreads();
@@ -879,7 +901,7 @@ template <int TILE, int W, bool NARROW>
 __global__ void __launch_bounds__(kFreqBlock)
 partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long long cap,
                        unsigned long long* __restrict__ gcursor, void* __restrict__ out,
-                       uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, NarrowKey nk) {
+                       uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, NarrowKey nk, Spill sp) {
     using OutT = typename std::conditional<NARROW, uint32_t, unsigned long long>::type;
     OutT* __restrict__ out_h = static_cast<OutT*>(out);
     constexpr int PER = TILE / kFreqBlock;
@@ -888,10 +910,10 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
     __shared__ unsigned long long sh[TILE];
     __shared__ unsigned int regs[kFastRegs];
     __shared__ unsigned long long red[kFreqBlock / 64];
-    __shared__ unsigned int lovf, lbad;
+    __shared__ unsigned int lovf;
     for (int i = threadIdx.x; i < kFastRegs; i += kFreqBlock) regs[i] = 0;
     hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) lovf = lbad = 0;
+    if (threadIdx.x == 0) lovf = 0;
     __syncthreads();
     unsigned long long taken = 0, sent = 0, nulls = 0, miss = 0;
     const int64_t ntiles = (nrows + TILE - 1) / TILE;
@@ -953,7 +975,9 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
         scatter_tile_reserve<kDigitBins, TILE, NARROW>(h, keepm, 0, kDigitBins - 1, hist, start, cursor, sh, gcursor, cap,
                                                [xcd](int b) { return (unsigned long long)b * kXcds + xcd; },
                                                [xcd](int b) { return ((unsigned long long)b * kXcds + xcd) * kCursorStride; },
-                                               &lovf, &lbad, cap * kDigitBins * kXcds, out_h, [&]() {
+                                               &lovf, sp, [nk](uint64_t v) {
+                                                   return NARROW ? mix64(narrow_canon(nk, (uint32_t)v)) : v;
+                                               }, out_h, [&]() {
             if (next < ntiles) load(next);
         });
     }
@@ -967,7 +991,6 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
         if (nulls) atomicAdd(&ctr->nulls, nulls);
         if (miss) atomicAdd(&ctr->narrow_miss, miss);
         if (lovf) atomicAdd(&ctr->pad[0], 1ull);
-        if (lbad) atomicAdd(&ctr->pad[2], 1ull);
     }
     for (int i = threadIdx.x; i < kFastRegs / 4; i += kFreqBlock) {
         const unsigned int w = regs[4 * i] | (regs[4 * i + 1] << 8) | (regs[4 * i + 2] << 16) | (regs[4 * i + 3] << 24);
@@ -982,12 +1005,14 @@ struct FastItem {
 
 // Fast pass 2: per work item (a chunk of one partition), keys -> bucket part + 256 * (next bits), bucket k at
 // k * cap; its reservation counter is part * bins + b, so a partition's counters share lines only with each other.
-// The next tile is loaded before the current one is scattered.
+// The next tile is loaded before the current one is scattered. Two workgroups per CU (69.6 KB of LDS each) need
+// <= 256 VGPRs: the 64-bit 8192-key tile sits at 252-258, and one register over halves the occupancy (r03: C4's
+// pass 2 went from 4.2 to 5.1 ms when the NARROW template pushed it to 258), hence the explicit bound.
 template <int BINS, int TILE, bool NARROW>
-__global__ void __launch_bounds__(kFreqBlock)
+__global__ void __launch_bounds__(kFreqBlock, BINS <= kDigitBins ? 2 : 1)
 scatter2_fast_kernel(const FastItem* __restrict__ items, const void* __restrict__ in, unsigned int mask,
                      unsigned long long cap, unsigned long long* __restrict__ gcursor, void* __restrict__ out,
-                     Counters* __restrict__ ctr, NarrowKey nk) {
+                     Counters* __restrict__ ctr, NarrowKey nk, Spill sp) {
     using KeyT = typename std::conditional<NARROW, uint32_t, unsigned long long>::type;
     const KeyT* __restrict__ in_h = static_cast<const KeyT*>(in);
     KeyT* __restrict__ out_h = static_cast<KeyT*>(out);
@@ -995,10 +1020,10 @@ scatter2_fast_kernel(const FastItem* __restrict__ items, const void* __restrict_
     __shared__ unsigned int hist[BINS], start[BINS];
     __shared__ unsigned long long cursor[BINS];
     __shared__ unsigned long long sh[TILE];
-    __shared__ unsigned int lovf, lbad;
+    __shared__ unsigned int lovf;
     const FastItem it = items[blockIdx.x];
     for (int b = threadIdx.x; b < BINS; b += kFreqBlock) hist[b] = 0;
-    if (threadIdx.x == 0) lovf = lbad = 0;
+    if (threadIdx.x == 0) lovf = 0;
     __syncthreads();
     const unsigned long long part = it.part;
     KeyT nxt[PER];
@@ -1020,8 +1045,10 @@ scatter2_fast_kernel(const FastItem* __restrict__ items, const void* __restrict_
         const unsigned long long n0 = t0 + TILE;
         scatter_tile_reserve<BINS, TILE, NARROW>(h, keepm, 8, mask, hist, start, cursor, sh, gcursor, cap,
                                          [part](int b) { return part + (unsigned long long)kDigitBins * b; },
-                                         [part, mask](int b) { return part * (mask + 1ull) + b; }, &lovf, &lbad,
-                                         cap * kDigitBins * (mask + 1ull), out_h, [&]() {
+                                         [part, mask](int b) { return part * (mask + 1ull) + b; }, &lovf, sp,
+                                         [nk](uint64_t v) {
+                                             return NARROW ? mix64(narrow_canon(nk, (uint32_t)v)) : v;
+                                         }, out_h, [&]() {
             if (n0 < it.end) {
 #pragma unroll
                 for (int j = 0; j < PER; ++j) {
@@ -1032,7 +1059,6 @@ scatter2_fast_kernel(const FastItem* __restrict__ items, const void* __restrict_
         });
     }
     if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->pad[1], 1ull);
-    if (threadIdx.x == 0 && lbad) atomicAdd(&ctr->pad[2], 1ull);
 }
 
 struct SummaryPartial {
@@ -1210,6 +1236,54 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
         __syncthreads();
     }
     if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->overflow, 1ull);
+}
+
+// Spilled keys of the fast build (a bucket's share of a heavily repeated key past its slack) into the finished table:
+// each workgroup aggregates a chunk of the spill in an LDS table (a heavy key becomes one (key, count) entry) and adds
+// the entries to their regions with global compare-and-swap + add (the split-bucket merge of build_kernel). Region r
+// of a key is its low `bits` bits, its probe start the top bits, as in every other build. A full region (or a full
+// LDS table, whose key is then added on its own) raises Counters::overflow: the build grows, as for any overflow.
+constexpr int kSpillChunk = 16384;
+
+__device__ __forceinline__ bool region_add(Slot* __restrict__ slots, int bits, unsigned long long h,
+                                           unsigned long long c) {
+    Slot* region = slots + (h & ((1ull << bits) - 1ull)) * (unsigned long long)kRegion;
+    unsigned int p = region_probe(h);
+    for (int probe = 0; probe < kRegion; ++probe) {
+        const unsigned long long prev = atomicCAS(&region[p].key, kEmpty, h);
+        if (prev == kEmpty || prev == h) {
+            atomicAdd(&region[p].count, c);
+            return true;
+        }
+        p = (p + 1) & (kRegion - 1);
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(kBuildBlock)
+spill_insert_kernel(const unsigned long long* __restrict__ spill, unsigned long long nspill, Slot* __restrict__ slots,
+                    int bits, Counters* __restrict__ ctr) {
+    __shared__ unsigned long long lkey[kRegion];
+    __shared__ unsigned int lcnt[kRegion];
+    bool ok = true;
+    for (unsigned long long c0 = (unsigned long long)blockIdx.x * kSpillChunk; c0 < nspill;
+         c0 += (unsigned long long)gridDim.x * kSpillChunk) {
+        for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
+            lkey[i] = kEmpty;
+            lcnt[i] = 0;
+        }
+        __syncthreads();
+        const unsigned long long c1 = c0 + kSpillChunk < nspill ? c0 + kSpillChunk : nspill;
+        for (unsigned long long j = c0 + threadIdx.x; j < c1; j += kBuildBlock) {
+            const unsigned long long h = spill[j];
+            if (!lds_insert<unsigned int>(lkey, lcnt, nullptr, h, 0ull, 1u, false)) ok &= region_add(slots, bits, h, 1ull);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < kRegion; i += kBuildBlock)
+            if (lkey[i] != kEmpty) ok &= region_add(slots, bits, lkey[i], (unsigned long long)lcnt[i]);
+        __syncthreads();
+    }
+    if (!ok) atomicAdd(&ctr->overflow, 1ull);
 }
 
 // ---- small general tables: one fused pass -------------------------------------------------------------
@@ -1691,7 +1765,8 @@ struct DevBuf {  // scratch device buffers of one build (the context's scratch c
 int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, const unsigned long long* sorted,
                   const unsigned long long* srows, const std::vector<unsigned long long>& bstart,
                   const std::vector<unsigned long long>& bcount, int bits, bool* overflow, bool* collision,
-                  const NarrowKey* narrow = nullptr) {
+                  const NarrowKey* narrow = nullptr, const unsigned long long* spill = nullptr,
+                  unsigned long long nspill = 0) {
     hipStream_t s = dq::ctx_stream(ctx);
     const bool general = !t->fast;
     const bool weighted = t->ks.weights != nullptr;
@@ -1743,6 +1818,11 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
         hipLaunchKernelGGL((build_kernel<false, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
                            t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     FQ_HIP(ctx, hipGetLastError());
+    if (nspill) {
+        const int grid = (int)std::min<unsigned long long>((nspill + kSpillChunk - 1) / kSpillChunk, 2048);
+        hipLaunchKernelGGL(spill_insert_kernel, dim3(grid), dim3(kBuildBlock), 0, s, spill, nspill, t->slots, bits, t->ctr);
+        FQ_HIP(ctx, hipGetLastError());
+    }
     if (general && nrows > 0) {
         const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
         hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots, t->reps, bits,
@@ -1754,7 +1834,7 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     FQ_HIP(ctx, hipStreamSynchronize(s));
     // the fused summary, folded in item order (deterministic) unless a split bucket needs the table scan
     t->pre_valid = 0;
-    if (t->host_ctr.overflow == 0 && t->host_ctr.mismatch == 0) {
+    if (t->host_ctr.overflow == 0 && t->host_ctr.mismatch == 0 && nspill == 0) {  // spilled keys: the table scan
         bool all = true;
         unsigned long long groups = 0, unique = 0, maxc = 0;
         double ent = 0.0, comp = 0.0;
@@ -1817,6 +1897,7 @@ int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf
     const BuildItem it = {0ull, 0ull, 0u, 1u};  // split = 1: region_init clears region 0
     FQ_HIP(ctx, hipMemcpyAsync(ditem, &it, sizeof(it), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(region_init_kernel, dim3(1), dim3(kFreqBlock), 0, s, ditem, 1, t->slots, t->reps);
+    ctx->freq_paths[DQ_FREQ_PATH_SMALL]++;
     // a 2048-slot workgroup table (40 KB of LDS: 3 workgroups per CU instead of 1) when the estimate leaves it <= 5/8 full
     if (est <= 1280.0)
         hipLaunchKernelGGL((small_build_kernel<2048>), dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots, t->reps,
@@ -2056,6 +2137,10 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     FQ_HIP(ctx, buf.alloc((void**)&h1, cap1 * kSub * ksz));
     FQ_HIP(ctx, buf.alloc((void**)&regs, kFastRegs * sizeof(unsigned int)));
     FQ_HIP(ctx, buf.alloc((void**)&regs_part, (size_t)kFastRegs * xgrid));
+    // spill buffer: room for a quarter of the rows past full buckets (heavily repeated keys); more sends the build to
+    // the exactly-counted path
+    Spill sp{nullptr, (unsigned long long)nrows / 4 + (1ull << 20), &t->ctr->spilled};
+    FQ_HIP(ctx, buf.alloc((void**)&sp.keys, sp.cap * sizeof(unsigned long long)));
     FQ_HIP(ctx, hipMemsetAsync(gc1, 0, sizeof(unsigned long long) * kSub * kCursorStride, s));
     FQ_HIP(ctx, hipMemsetAsync(regs, 0, kFastRegs * sizeof(unsigned int), s));
     FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
@@ -2063,7 +2148,8 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     // (measured: an 8 K-key pass-1 tile runs 8.1 ms against 6.1 ms for 4 K on C4 -- twice the registers)
 #define DQ_P1(W, N)                                                                                                   \
     hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, W, N>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0], \
-                       nrows, inul, cap1, gc1, h1, regs_part, t->ctr, nk)
+                       nrows, inul, cap1, gc1, h1, regs_part, t->ctr, nk, sp)
+    ctx->freq_paths[narrow ? DQ_FREQ_PATH_FAST_NARROW : DQ_FREQ_PATH_FAST]++;
     switch (elem_size((ElemType)t->ks.cols[0].elem)) {
         case 8:
             if (narrow) DQ_P1(8, true); else DQ_P1(8, false);
@@ -2089,14 +2175,15 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
                                hipMemcpyDeviceToHost, s));
     FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
     FQ_HIP(ctx, hipStreamSynchronize(s));
-    if (t->host_ctr.pad[2]) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency fast build: run position out of range");
-    if (t->host_ctr.pad[0]) return DQ_OK;  // a partition overflowed: the exact path
+    if (t->host_ctr.pad[0]) return DQ_OK;  // the spill buffer overflowed: the exact path
     if (t->host_ctr.narrow_miss) {  // an 8-byte key outside the sampled window: again with 64-bit keys
         if (getenv("DQ_DEBUG_FREQ"))
             fprintf(stderr, "[freq fast] narrow window missed by %llu rows\n", t->host_ctr.narrow_miss);
         return build_fast(ctx, t, nrows, buf, done, false);
     }
-    for (int q = 0; q < kSub; ++q) pcount[q] = pstrided[(size_t)q * kCursorStride];
+    // a sub-region's reservations past its capacity went to the spill buffer
+    for (int q = 0; q < kSub; ++q) pcount[q] = std::min(pstrided[(size_t)q * kCursorStride], cap1);
+    const unsigned long long spilled1 = t->host_ctr.spilled;
     unsigned long long n = 0;
     for (unsigned long long c : pcount) n += c;
     const double est = n ? 8.0 * hll_raw_estimate(hregs) : 0.0;  // the sketch holds a 1/8 sample of the keys
@@ -2146,11 +2233,13 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
                 FQ_HIP(ctx, buf.alloc((void**)&h2, h2_bytes));
             }
             FQ_HIP(ctx, hipMemsetAsync(gc2, 0, sizeof(unsigned long long) * nb, s));
+            // a retry with more buckets keeps pass 1's spilled keys and drops the previous pass 2's
+            FQ_HIP(ctx, hipMemcpyAsync(&t->ctr->spilled, &spilled1, sizeof(spilled1), hipMemcpyHostToDevice, s));
             if (nitems) FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), sizeof(FastItem) * nitems, hipMemcpyHostToDevice, s));
             const unsigned int mask = (unsigned int)bins - 1;
 #define DQ_P2(B, T, N)                                                                                            \
     hipLaunchKernelGGL((scatter2_fast_kernel<B, T, N>), dim3(nitems), dim3(kFreqBlock), 0, s, ditems, h1, mask, cap2, \
-                       gc2, h2, t->ctr, nk)
+                       gc2, h2, t->ctr, nk, sp)
             if (nitems && bins > kDigitBins) {
                 if (narrow) DQ_P2(4096, kPartTile, true); else DQ_P2(4096, kPartTile, false);
             } else if (nitems) {
@@ -2162,22 +2251,24 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
             FQ_HIP(ctx, hipMemcpyAsync(pb.data(), gc2, sizeof(unsigned long long) * nb, hipMemcpyDeviceToHost, s));
             FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
             FQ_HIP(ctx, hipStreamSynchronize(s));
-            if (t->host_ctr.pad[2]) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "frequency fast build: run position out of range");
-            if (t->host_ctr.pad[1]) return DQ_OK;  // a bucket overflowed: the exact path
+            if (t->host_ctr.pad[1]) return DQ_OK;  // the spill buffer overflowed: the exact path
             bstart.resize(nb);
             bcount.resize(nb);
             for (uint64_t k = 0; k < nb; ++k) {
                 bstart[k] = k * cap2;
-                bcount[k] = pb[(k & (kDigitBins - 1)) * (uint64_t)bins + (k >> 8)];
+                bcount[k] = std::min(pb[(k & (kDigitBins - 1)) * (uint64_t)bins + (k >> 8)], cap2);
             }
             sorted = h2;
         }
         bool overflow = false, collision = false;
+        const unsigned long long nspill = std::min(t->host_ctr.spilled, sp.cap);
         const int rc = build_regions(ctx, t, nrows, buf, static_cast<const unsigned long long*>(sorted), nullptr, bstart,
-                                     bcount, bits, &overflow, &collision, narrow ? &nk : nullptr);
+                                     bcount, bits, &overflow, &collision, narrow ? &nk : nullptr, sp.keys, nspill);
         if (rc != DQ_OK) return rc;
         if (!overflow) {
             *done = true;
+            ctx->freq_paths[DQ_FREQ_PATH_FAST_DONE]++;
+            if (nspill) ctx->freq_paths[DQ_FREQ_PATH_FAST_SPILL]++;
             return DQ_OK;
         }
     }
@@ -2207,7 +2298,10 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         bool overflow = false, collision = false;
         const int rc = build_small(ctx, t, nrows, 0.0, buf, &overflow, &collision, true);
         if (rc != DQ_OK) return rc;
-        if (!overflow && !collision) return DQ_OK;
+        if (!overflow && !collision) {
+            ctx->freq_paths[DQ_FREQ_PATH_SMALL_OPTIMISTIC]++;
+            return DQ_OK;
+        }
     }
     for (int seed_attempt = 0; seed_attempt < 4; ++seed_attempt) {
         unsigned long long *hs = nullptr, *rows = nullptr, *bk = nullptr;
@@ -2222,6 +2316,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         FQ_HIP(ctx, hipMemsetAsync(bk, 0, 2 * sizeof(unsigned long long) * xgrid, s));
         FQ_HIP(ctx, hipMemsetAsync(regs, 0, kSizingRegs * sizeof(unsigned int), s));
         FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
+        ctx->freq_paths[DQ_FREQ_PATH_EXACT]++;
         if (nrows > 0) {
             hipLaunchKernelGGL(extract_count_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows, bk, regs_part,
                                t->ctr, hist1, kPartTile);
@@ -2258,12 +2353,14 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
             collision = false;  // a full table: the regular path below
         }
         if (!no_partition && n > 0 && bits >= 8 && bits <= kMaxPartBits) {
+            ctx->freq_paths[DQ_FREQ_PATH_PARTITIONED]++;
             const int rc = build_partitioned(ctx, t, nrows, buf, xgrid, hist1, n, bits, &collision);
             if (rc != DQ_OK) return rc;
             if (!collision) return DQ_OK;
             t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
             continue;
         }
+        ctx->freq_paths[DQ_FREQ_PATH_SORTED]++;
         FQ_HIP(ctx, buf.alloc((void**)&hs, n_alloc * 8));
         if (general) FQ_HIP(ctx, buf.alloc((void**)&rows, n_alloc * 8));
         if (nrows > 0) {

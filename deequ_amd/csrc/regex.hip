@@ -249,6 +249,113 @@ __device__ int format_long(int64_t v, uint8_t* buf) {
     return n;
 }
 
+// Spark 2.2's Cast(decimal AS STRING) = Decimal.toString = java.math.BigDecimal.toString of the unscaled Long at
+// the column scale: plain notation while the adjusted exponent (digits - 1 - scale) is >= -6, scientific below
+// ("1E-7", "0E-7", "1.5E-8"); scale >= 0 for every Spark DecimalType, so no "E+".
+__device__ int format_decimal(int64_t unscaled, int scale, uint8_t* buf) {
+    uint8_t d[20];
+    uint64_t m = unscaled < 0 ? (uint64_t)0 - (uint64_t)unscaled : (uint64_t)unscaled;
+    int k = 0;
+    do {
+        d[k++] = (uint8_t)('0' + m % 10);
+        m /= 10;
+    } while (m);  // d[k-1] is the most significant digit
+    int n = 0;
+    if (unscaled < 0) buf[n++] = '-';
+    const int adjusted = k - 1 - scale;
+    if (adjusted >= -6) {
+        if (scale == 0) {
+            for (int i = k - 1; i >= 0; --i) buf[n++] = d[i];
+        } else if (k > scale) {
+            for (int i = k - 1; i >= scale; --i) buf[n++] = d[i];
+            buf[n++] = '.';
+            for (int i = scale - 1; i >= 0; --i) buf[n++] = d[i];
+        } else {
+            buf[n++] = '0';
+            buf[n++] = '.';
+            for (int i = 0; i < scale - k; ++i) buf[n++] = '0';
+            for (int i = k - 1; i >= 0; --i) buf[n++] = d[i];
+        }
+        return n;
+    }
+    buf[n++] = d[k - 1];
+    if (k > 1) {
+        buf[n++] = '.';
+        for (int i = k - 2; i >= 0; --i) buf[n++] = d[i];
+    }
+    buf[n++] = 'E';
+    buf[n++] = '-';
+    return n + format_long(-(int64_t)adjusted, buf + n);
+}
+
+__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b) {
+    const int64_t q = a / b;
+    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
+// The civil date of a day number (days since 1970-01-01) as java.text.SimpleDateFormat prints it with its default
+// GregorianCalendar: Gregorian from 1582-10-15 (Julian Day 2299161), the Julian calendar before the cutover
+// (E. G. Richards' day-number conversions). `year` is the year of era (1 BC prints as 1: "yyyy" shows no era).
+__device__ void civil_from_days(int64_t days, int64_t* year, int* month, int* day) {
+    const int64_t J = days + 2440588;
+    int64_t f = J + 1401;
+    if (J >= 2299161) f += floor_div(floor_div(4 * J + 274277, 146097) * 3, 4) - 38;
+    const int64_t e = 4 * f + 3;
+    const int64_t g = floor_div(e - floor_div(e, 1461) * 1461, 4);
+    const int64_t h = 5 * g + 2;
+    *day = (int)(floor_div(h - floor_div(h, 153) * 153, 5) + 1);
+    *month = (int)((floor_div(h, 153) + 2) % 12 + 1);
+    const int64_t y = floor_div(e, 1461) - 4716 + (12 + 2 - *month) / 12;  // astronomical year
+    *year = y >= 1 ? y : 1 - y;
+}
+
+__device__ __forceinline__ int put2(int v, uint8_t* b) {
+    b[0] = (uint8_t)('0' + v / 10);
+    b[1] = (uint8_t)('0' + v % 10);
+    return 2;
+}
+
+// "yyyy-MM-dd" (at least four year digits, more when needed).
+__device__ int format_date_days(int64_t days, uint8_t* buf) {
+    int64_t y;
+    int mo, d;
+    civil_from_days(days, &y, &mo, &d);
+    int n = 0;
+    for (int64_t p = 1000; p > y && p > 1; p /= 10) buf[n++] = '0';
+    n += format_long(y, buf + n);
+    buf[n++] = '-';
+    n += put2(mo, buf + n);
+    buf[n++] = '-';
+    return n + put2(d, buf + n);
+}
+
+// Spark 2.2's Cast(timestamp AS STRING) (DateTimeUtils.timestampToString) in a UTC session time zone:
+// "yyyy-MM-dd HH:mm:ss" of the floored second, then java.sql.Timestamp.toString's fraction (the microseconds as
+// nanoseconds, trailing zeros dropped) unless it is ".0".
+__device__ int format_timestamp_utc(int64_t micros, uint8_t* buf) {
+    const int64_t secs = floor_div(micros, 1000000);
+    const int64_t frac = micros - secs * 1000000;
+    const int64_t days = floor_div(secs, 86400);
+    const int64_t sod = secs - days * 86400;
+    int n = format_date_days(days, buf);
+    buf[n++] = ' ';
+    n += put2((int)(sod / 3600), buf + n);
+    buf[n++] = ':';
+    n += put2((int)(sod / 60 % 60), buf + n);
+    buf[n++] = ':';
+    n += put2((int)(sod % 60), buf + n);
+    if (frac) {
+        buf[n++] = '.';
+        int64_t f = frac, div = 100000;
+        while (f) {
+            buf[n++] = (uint8_t)('0' + f / div);
+            f %= div;
+            div /= 10;
+        }
+    }
+    return n;
+}
+
 }  // namespace
 
 __global__ void __launch_bounds__(256)
@@ -292,6 +399,18 @@ regex_match_kernel(PredColumn col, const int32_t* __restrict__ image, int64_t nr
                     s = buf;
                     break;
                 }
+                case DQ_TYPE_DECIMAL:
+                    n = format_decimal(static_cast<const int64_t*>(col.values)[row], col.decimal_scale, buf);
+                    s = buf;
+                    break;
+                case DQ_TYPE_DATE:
+                    n = format_date_days(static_cast<const int32_t*>(col.values)[row], buf);
+                    s = buf;
+                    break;
+                case DQ_TYPE_TIMESTAMP:
+                    n = format_timestamp_utc(static_cast<const int64_t*>(col.values)[row], buf);
+                    s = buf;
+                    break;
                 default: {
                     int64_t v;
                     switch (col.spark_type) {

@@ -385,9 +385,10 @@ class DistributedAnalysisRunner:
         by_cols = {}
         for a in passed:
             if isinstance(a, Histogram) and a.binningUdf is not None:
-                # the binning UDF is a host function of this process; the sharded path groups raw keys
-                results[a] = a.toFailureMetric(UnsupportedOnDevice(
-                    "Histogram with a binningUdf is not supported by the multi-GPU runner"))
+                try:
+                    results[a] = self._binned_histogram(shard, a)
+                except Exception as e:
+                    results[a] = a.toFailureMetric(wrap_if_necessary(e))
                 continue
             if isinstance(a, MutualInformation):
                 try:
@@ -409,6 +410,24 @@ class DistributedAnalysisRunner:
             for a in group:
                 results[a] = self._grouping_metric(a, freq)
         return AnalyzerContext(results)
+
+    def _binned_histogram(self, shard, a):
+        """Histogram with a binningUdf: every rank bins its shard's distinct values (the UDF is a deterministic host
+        function of the value, so a value lands in the same bin on every rank) and the per-rank bin counts add up —
+        the same (bin, count) table as binning the whole column (A/Histogram.scala:59-65)."""
+        import json
+        def binned():
+            block = self.local.group_block(shard, [a.column], False)
+            groups = ((k[0], c) for k, c in zip(block.keys(), block.counts.tolist()))
+            return a.bin_groups(groups, shard.count() - block.num_rows)
+        local = self._local_step(binned)
+        blob = json.dumps([[k[0], int(c)] for k, c in local.items()]).encode()
+        bins = {}
+        for b in self.ex.all_gather_blobs(blob):
+            for label, c in json.loads(b.decode()):
+                bins[(label,)] = bins.get((label,), 0) + c
+        rows = self.ex.all_reduce_i64([shard.count()])[0]
+        return a.computeMetricFrom(FrequenciesAndNumRows(bins, rows, [a.column]))
 
     def _local_step(self, fn):
         """Run one piece of per-rank compute, then agree on it: every rank returns its result, or every rank

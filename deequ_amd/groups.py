@@ -70,6 +70,9 @@ def _string_hashes_span(values, start, end):
 
 
 _HASH_SLICE_BYTES = 1 << 24
+# A device string column carries int32 Arrow offsets: a merged block whose key bytes reach this is built in
+# key-disjoint splits (BlockParts.split_by_key). Module-level so tests can inject a small limit.
+STRING_KEY_LIMIT = 2 ** 31 - 1
 
 
 def string_hashes(values, offsets, slice_bytes=None):
@@ -294,12 +297,48 @@ class BlockParts(GroupBlock):
     def schema(self):
         return list(self._schema)
 
+    def key_bytes(self):
+        """The largest total of UTF-8 key bytes over this block's string key columns (0 without string keys)."""
+        most = 0
+        for i, (_, t, _, _) in enumerate(self._schema):
+            if t == N.TYPE_STRING:
+                most = max(most, sum(int(p.columns[i].offsets[p.columns[i].length]) - int(p.columns[i].offsets[0])
+                                     for p in self.parts))
+        return most
+
+    def split_by_key(self, limit=None):
+        """The groups split into key-disjoint BlockParts (by a hash of the whole key, so every copy of a key lands
+        in the same split), each with fewer than `limit` string key bytes per column: one weighted build per split
+        stays within the int32 Arrow offsets of a device string column. One split when the block already fits."""
+        limit = int(limit or STRING_KEY_LIMIT)
+        total = self.key_bytes()
+        if total < limit:
+            return [self]
+        k = max(2, -(-total * 5 // (4 * limit)))
+        while True:
+            splits = [[] for _ in range(k)]
+            for p in self.parts:
+                own = (key_hashes(p.columns) >> np.uint64(32)) % np.uint64(k)
+                for s in range(k):
+                    rows = np.flatnonzero(own == s)
+                    if len(rows):
+                        splits[s].append(p.subset(rows))
+            out = [BlockParts(s, self._schema) for s in splits]
+            if all(b.key_bytes() < limit for b in out):
+                return out
+            k *= 2
+            if k > 4096:
+                raise ValueError("string group keys do not split under the int32 Arrow offsets")
+
     def device_table(self):
         """(deequ_amd.table.Table of device columns, device int64 counts): each part's buffers copied into its
         slice of the device buffers, string offsets rebased on the device."""
         import torch
         dev = torch.device("cuda", torch.cuda.current_device())
         n = self.size
+        if self.key_bytes() >= STRING_KEY_LIMIT:
+            raise ValueError("string group keys of %d bytes exceed the int32 Arrow offsets of one device column "
+                             "(split_by_key first)" % self.key_bytes())
         cols = []
         for i, (name, t, prec, scale) in enumerate(self._schema):
             parts = [b.columns[i] for b in self.parts]
@@ -312,11 +351,11 @@ class BlockParts(GroupBlock):
                 off[0] = 0
                 at, base = 0, 0
                 for p in parts:
-                    o = np.asarray(p.offsets, dtype=np.int32)[:p.length + 1]
+                    o = np.asarray(p.offsets, dtype=np.int64)[:p.length + 1]
                     a, b = int(o[0]), int(o[-1])
-                    data[base:base + b - a].copy_(torch.from_numpy(np.asarray(p.values, dtype=np.uint8)[a:b]))
-                    po = torch.from_numpy(np.ascontiguousarray(o[1:])).to(dev)
-                    off[at + 1:at + 1 + p.length] = po - a + base
+                    data[base:base + b - a].copy_(_host_tensor(np.asarray(p.values, dtype=np.uint8)[a:b]))
+                    po = _host_tensor(o[1:]).to(dev)  # int64 on the device: the rebase cannot wrap
+                    off[at + 1:at + 1 + p.length] = (po - a + base).to(torch.int32)
                     at += p.length
                     base += b - a
                 d["values"], d["offsets"] = data, off
@@ -325,25 +364,47 @@ class BlockParts(GroupBlock):
                 vals = torch.empty(max(n, 1), dtype=torch.from_numpy(np.zeros(1, dtype=dt)).dtype, device=dev)
                 at = 0
                 for p in parts:
-                    vals[at:at + p.length].copy_(torch.from_numpy(np.ascontiguousarray(np.asarray(p.values)[:p.length])))
+                    vals[at:at + p.length].copy_(_host_tensor(np.asarray(p.values)[:p.length]))
                     at += p.length
                 d["values"] = vals
             if any(p.validity is not None for p in parts):
-                valid = np.concatenate([unpack_validity(p.validity, p.length) for p in parts])
-                if not valid.all():
-                    bits = pack_validity(valid)
-                    m = np.zeros((n + 63) // 64 * 8, dtype=np.uint8)
-                    m[:len(bits)] = bits
-                    d["validity"] = torch.from_numpy(m).to(dev)
+                d["validity"] = _device_validity(parts, n, dev)
             c.device = d
             cols.append(c)
         counts = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         at = 0
         for p in self.parts:
-            counts[at:at + p.size].copy_(torch.from_numpy(np.ascontiguousarray(p.counts)))
+            counts[at:at + p.size].copy_(_host_tensor(p.counts))
             at += p.size
         torch.cuda.synchronize()
         return Table(cols), counts[:n]
+
+
+def _host_tensor(a):
+    """A CPU tensor over a numpy array, copied only when the array is read-only or strided (np.frombuffer views of
+    persisted / received bytes are read-only, and torch.from_numpy warns on those)."""
+    import torch
+    return torch.from_numpy(np.require(a, requirements=["C", "W"]))
+
+
+def _device_validity(parts, n, dev):
+    """The validity bitmaps of several columns joined on the device: each part's packed bits (LSB first) unpacked
+    to one byte per row in its slice, then repacked into one bitmap padded to whole 64-bit words."""
+    import torch
+    valid = torch.ones(max(n, 1), dtype=torch.uint8, device=dev)
+    shifts = torch.arange(8, dtype=torch.uint8, device=dev)
+    at = 0
+    for p in parts:
+        if p.validity is not None and p.length:
+            packed = _host_tensor(np.asarray(p.validity, dtype=np.uint8)[:(p.length + 7) // 8]).to(dev)
+            bits = (packed.unsqueeze(1) >> shifts) & 1
+            valid[at:at + p.length] = bits.reshape(-1)[:p.length]
+        at += p.length
+    words = (n + 63) // 64
+    rows = torch.zeros(words * 64, dtype=torch.uint8, device=dev)
+    rows[:n] = valid[:n]
+    return (rows.reshape(-1, 8) << shifts).sum(dim=1, dtype=torch.uint8) if n else \
+        torch.zeros(8, dtype=torch.uint8, device=dev)
 
 
 def concat(blocks, schema):

@@ -46,6 +46,7 @@ SYNTH_STR_CAT50, SYNTH_STR_BOOL, SYNTH_STR_CAT100, SYNTH_STR_INT, SYNTH_STR_DEC,
 HLL_NUM_WORDS = 52
 
 # dq_scan_kernel, in enum order
+FREQ_PATHS = ("fast", "fast_narrow", "fast_done", "exact", "partitioned", "sorted", "small", "small_optimistic", "fast_spill")
 SCAN_KERNELS = ("striped", "striped_heavy", "heavy8", "heavy8_full", "bits", "pred_simple", "pred_vm", "regex",
                 "strings", "where_fused", "where_masks")
 
@@ -57,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts", "dq_synth_strings",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
-    "dq_scan_streamed", "dq_scan_kernel_launches", "dq_kll_sketch_columns",
+    "dq_scan_streamed", "dq_scan_kernel_launches", "dq_freq_path_count", "dq_kll_sketch_columns",
 )
 
 
@@ -174,6 +175,7 @@ def load_library(path=None):
                                 c_uint32]),
             "dq_scan_launch_count": (c_int64, [c_void_p]),
             "dq_scan_kernel_launches": (c_int64, [c_void_p, ctypes.c_int32]),
+            "dq_freq_path_count": (c_int64, [c_void_p, ctypes.c_int32]),
             "dq_state_merge": (c_int, [c_void_p, c_void_p, c_void_p]),
             "dq_state_fold": (c_int, [c_void_p, c_int, c_int, c_void_p]),
             "dq_hll_count": (ctypes.c_double, [c_void_p]),
@@ -320,6 +322,10 @@ class Context:
     def kernel_launches(self):
         """{kernel name: launches so far} of the scan path (dq_scan_kernel_launches)."""
         return {name: int(self.lib.dq_scan_kernel_launches(self.handle, i)) for i, name in enumerate(SCAN_KERNELS)}
+
+    def freq_paths(self):
+        """{grouping build path: count so far} (dq_freq_path_count): which build produced the tables."""
+        return {name: int(self.lib.dq_freq_path_count(self.handle, i)) for i, name in enumerate(FREQ_PATHS)}
 
     def scan(self, columns, nrows, ops, preds, out_device_ptr=None):
         """Run dq_scan. `columns`: list of DqColumn, `ops`: list of DqOp, `preds`: list of DqPredicate.

@@ -314,7 +314,10 @@ class AnalysisRunner:
         its states in memory; the chunk states (and the states of `aggregateWith`) then merge in chunk order through
         runOnAggregatedStates — Spark's partial aggregates of one `agg` over the partitions, merged by the same
         State.sum. An analyzer whose state computation failed on any chunk (an exception, not an empty state) keeps
-        that chunk's failure metric."""
+        that chunk's failure metric. A grouping-column set with no state on any chunk (its frequencies failed on every
+        chunk) does not reach the merge (the reference's findStateForParticularGrouping would require one): it keeps
+        the chunk failure metrics."""
+        analyzers = list(dict.fromkeys(analyzers))  # one state per analyzer: the merge adds each loader's state once
         providers, failures = [], {}
         for chunk in data.chunks:
             p = InMemoryStateProvider()
@@ -326,8 +329,16 @@ class AnalysisRunner:
             providers.append(p)
         if aggregateWith is not None:
             providers.append(aggregateWith)
-        merged = AnalysisRunner.runOnAggregatedStates(data.schema, Analysis(list(analyzers)), providers,
-                                                      saveStatesWith)
+        by_cols = {}
+        for a in analyzers:
+            if isinstance(a, GroupingAnalyzer):
+                by_cols.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
+        stateless = set()
+        for group in by_cols.values():
+            if not any(p.load(a) is not None for p in providers for a in group):
+                stateless.update(group)
+        merged = AnalysisRunner.runOnAggregatedStates(
+            data.schema, Analysis([a for a in analyzers if a not in stateless]), providers, saveStatesWith)
         # no chunk had a state (every chunk empty for it): the metric of an empty state, as one run over all rows
         empty = {}
         for a in dict.fromkeys(analyzers):

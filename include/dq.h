@@ -267,6 +267,22 @@ typedef enum dq_scan_kernel {
 } dq_scan_kernel;
 int64_t dq_scan_kernel_launches(const dq_ctx* ctx, int32_t kernel);
 
+/* Which grouping build produced the frequency tables of this context so far (all devices of a multi-device
+ * context), so a test can prove which path it checked against the oracle (tests/test_gpu_grouping_oracle.py). */
+typedef enum dq_freq_path {
+    DQ_FREQ_PATH_FAST = 0,              /* fast build pass 1 (partition1_fast) over 64-bit keys                */
+    DQ_FREQ_PATH_FAST_NARROW = 1,       /* fast build pass 1 over 32-bit offsets around a sampled base         */
+    DQ_FREQ_PATH_FAST_DONE = 2,         /* fast builds that produced their table (no exact-path fallback)      */
+    DQ_FREQ_PATH_EXACT = 3,             /* exactly-counted path (extract_count + digit histograms)             */
+    DQ_FREQ_PATH_PARTITIONED = 4,       /* exact path: radix partition passes (partition1 / scatter2)          */
+    DQ_FREQ_PATH_SORTED = 5,            /* exact path: keys sorted on the bucket bits                          */
+    DQ_FREQ_PATH_SMALL = 6,             /* one-pass small builds launched (sized or optimistic)                */
+    DQ_FREQ_PATH_SMALL_OPTIMISTIC = 7,  /* optimistic small builds (no sizing pass) that produced their table  */
+    DQ_FREQ_PATH_FAST_SPILL = 8,        /* fast builds whose full buckets spilled keys (inserted after the build) */
+    DQ_FREQ_PATH_COUNT = 9
+} dq_freq_path;
+int64_t dq_freq_path_count(const dq_ctx* ctx, int32_t path);
+
 /* Semigroup merge of two states of the same op kind (State.sum, per analyzer file);
  * also used for the rank-ordered fold after the RCCL all-gather. */
 int dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out);

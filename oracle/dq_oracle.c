@@ -868,3 +868,77 @@ int64_t oracle_count_keys(const int64_t* keys, int64_t n, int64_t* table, uint8_
     }
     return groups;
 }
+
+/* count(*) GROUP BY one fixed-width key column, the grouping step of FrequencyBasedAnalyzer.computeFrequencies
+ * (analyzers/GroupingAnalyzers.scala:53-79: `data.select(cols).where(atLeastOne non-null).groupBy(cols).count()`)
+ * for a single column, restated as a sort + run length over the canonical 64-bit keys: integral values
+ * sign-extended, FLOAT / DOUBLE bit patterns with every NaN mapped to Java's canonical NaN and -0.0 kept apart
+ * from 0.0 — Spark 2.2 groups rows on the binary UnsafeRow of the key (there is no NormalizeFloatingNumbers rule
+ * before Spark 3.0), whose float cells are written through floatToIntBits / doubleToLongBits: NaN is canonical,
+ * -0.0 is not. NULL rows are not grouped
+ * (their count is returned in *null_rows). `valid`: LSB-first bitmap, NULL = every row valid. On return keys[0..g)
+ * holds the distinct canonical keys in ascending unsigned order and counts[0..g) their Long counts; the return
+ * value is g. keys / counts must hold n entries; scratch is n 64-bit words. */
+int64_t oracle_group_counts(int spark_type, const void* values, const uint8_t* valid, int64_t n, int64_t* keys,
+                            int64_t* counts, uint64_t* scratch, int64_t* null_rows) {
+    const uint8_t* v = (const uint8_t*)values;
+    const int w = elem_size(spark_type);
+    uint64_t* a = (uint64_t*)keys;
+    int64_t m = 0, nulls = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (valid && !((valid[i >> 3] >> (i & 7)) & 1)) {
+            ++nulls;
+            continue;
+        }
+        const uint8_t* p = v + i * w;
+        uint64_t k;
+        if (spark_type == T_DOUBLE) {
+            double d;
+            memcpy(&d, p, 8);
+            if (d != d) k = 0x7ff8000000000000ULL; else memcpy(&k, p, 8);
+        } else if (spark_type == T_FLOAT) {
+            float f;
+            uint32_t u;
+            memcpy(&f, p, 4);
+            if (f != f) u = 0x7fc00000u; else memcpy(&u, p, 4);
+            k = u;
+        } else {
+            k = (uint64_t)as_i64(spark_type, p);
+        }
+        a[m++] = k;
+    }
+    *null_rows = nulls;
+    /* LSD radix sort, 16-bit digits; a digit every key shares is skipped */
+    uint64_t* src = a;
+    uint64_t* dst = scratch;
+    static int64_t hist[65536];
+    for (int shift = 0; shift < 64; shift += 16) {
+        memset(hist, 0, sizeof(hist));
+        for (int64_t i = 0; i < m; ++i) hist[(src[i] >> shift) & 0xFFFF]++;
+        int single = 0;
+        for (int d = 0; d < 65536; ++d)
+            if (hist[d] == m) single = 1;
+        if (single) continue;
+        int64_t at = 0;
+        for (int d = 0; d < 65536; ++d) {
+            const int64_t c = hist[d];
+            hist[d] = at;
+            at += c;
+        }
+        for (int64_t i = 0; i < m; ++i) dst[hist[(src[i] >> shift) & 0xFFFF]++] = src[i];
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+    }
+    if (src != a) memcpy(a, src, (size_t)m * 8);
+    int64_t g = 0;
+    for (int64_t i = 0; i < m;) {
+        int64_t j = i + 1;
+        while (j < m && a[j] == a[i]) ++j;
+        a[g] = a[i];
+        counts[g] = j - i;
+        ++g;
+        i = j;
+    }
+    return g;
+}

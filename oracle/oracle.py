@@ -106,8 +106,40 @@ def lib():
                                                 ctypes.POINTER(OracleGenPred), ctypes.c_int,
                                                 ctypes.POINTER(OracleGenPred), ctypes.POINTER(OracleGenCol),
                                                 ctypes.POINTER(OracleGenCorr), ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_group_counts.restype = ctypes.c_int64
+        L.oracle_group_counts.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_int64)]
         _lib = L
     return _lib
+
+
+def group_counts_raw(spark_type, values, validity, nrows):
+    """count(*) GROUP BY one fixed-width key column from its raw Arrow buffers (values, LSB-first validity bitmap
+    or None) in C (oracle_group_counts, A/GroupingAnalyzers.scala:53-79): (canonical keys as uint64 ascending,
+    int64 counts, NULL rows). Canonical: integers sign-extended, FLOAT / DOUBLE bits with NaN canonical."""
+    vals = np.ascontiguousarray(values)
+    n = int(nrows)
+    keys = np.empty(max(n, 1), dtype=np.int64)
+    counts = np.empty(max(n, 1), dtype=np.int64)
+    scratch = np.empty(max(n, 1), dtype=np.uint64)
+    nulls = ctypes.c_int64(0)
+    vb = None if validity is None else np.ascontiguousarray(validity, dtype=np.uint8)
+    g = lib().oracle_group_counts(int(spark_type), vals.ctypes.data, None if vb is None else vb.ctypes.data, n,
+                                  keys.ctypes.data, counts.ctypes.data, scratch.ctypes.data, ctypes.byref(nulls))
+    return keys[:g].view(np.uint64).copy(), counts[:g].copy(), int(nulls.value)
+
+
+def group_summary_from_counts(counts, num_rows):
+    """The fused aggregation of A/GroupingAnalyzers.scala:83-120 over a table's counts: groups, groups seen once,
+    and the entropy terms -(c/N) ln(c/N) summed exactly (math.fsum over the distinct counts' multiplicities)."""
+    c = np.asarray(counts, dtype=np.int64)
+    vals, mult = np.unique(c, return_counts=True)
+    terms = []
+    for v, m in zip(vals.tolist(), mult.tolist()):
+        p = v / num_rows
+        terms.append(-m * p * math.log(p))
+    return {"num_groups": int(len(c)), "num_unique": int((c == 1).sum()), "entropy": math.fsum(terms) if terms else 0.0}
 
 
 # ---- raw helpers ---------------------------------------------------------------------------------
@@ -1148,9 +1180,55 @@ def spark_cast_to_string(col, i):
     if t == T_DECIMAL:
         return java_bigdecimal_to_string(int(v), col.decimal_scale)
     if t == T_DATE:
-        import datetime
-        return (datetime.date(1970, 1, 1) + datetime.timedelta(days=int(v))).isoformat()
-    return "1970-01-01 00:00:00"  # timestamps: any "yyyy-MM-dd HH:mm:ss" text classifies as String
+        return java_date_to_string(int(v))
+    return java_timestamp_to_string_utc(int(v))
+
+
+def _java_civil(days):
+    """(year of era, month, day) of a day number (days since 1970-01-01) in java.util.GregorianCalendar's hybrid
+    calendar, the one java.text.SimpleDateFormat prints with: Gregorian from 1582-10-15, Julian before (Java's
+    published cutover; restated with Python's proleptic-Gregorian date arithmetic and the Julian leap rule, not
+    with the device's day-number formulas)."""
+    import datetime
+    if days >= -141427:  # 1582-10-15 and later: Gregorian
+        shift = 0
+        if days > 2932896:  # past 9999-12-31 (Python's date range): whole 400-year Gregorian cycles of 146097 days
+            shift = (days - 2932896) // 146097 + 1
+        d = datetime.date(1970, 1, 1) + datetime.timedelta(days=days - 146097 * shift)
+        return d.year + 400 * shift, d.month, d.day
+    # Julian calendar: whole 4-year cycles of 1461 days counted from Julian 0001-01-01 (day -719164), then the year
+    # inside the cycle (the fourth year is the leap year) and the month from cumulative month lengths
+    off = days + 719164
+    cycles, rem = divmod(off, 1461)
+    yin = min(rem // 365, 3)
+    y = 1 + 4 * cycles + yin
+    doy = rem - 365 * yin
+    leap = y % 4 == 0
+    m = 1
+    for ml in (31, 29 if leap else 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31):
+        if doy < ml:
+            break
+        doy -= ml
+        m += 1
+    return (y if y >= 1 else 1 - y), m, doy + 1
+
+
+def java_date_to_string(days):
+    """Spark 2.2 Cast(date AS STRING) = DateTimeUtils.dateToString: SimpleDateFormat("yyyy-MM-dd")."""
+    y, m, d = _java_civil(days)
+    return "%04d-%02d-%02d" % (y, m, d)
+
+
+def java_timestamp_to_string_utc(micros):
+    """Spark 2.2 Cast(timestamp AS STRING) = DateTimeUtils.timestampToString in a UTC session time zone:
+    SimpleDateFormat("yyyy-MM-dd HH:mm:ss") of the floored second, plus java.sql.Timestamp.toString's fraction
+    (nanoseconds with trailing zeros dropped) unless it is ".0". Other session time zones: parity unpinned."""
+    secs, frac = divmod(micros, 1_000_000)
+    days, sod = divmod(secs, 86400)
+    out = "%s %02d:%02d:%02d" % (java_date_to_string(days), sod // 3600, sod // 60 % 60, sod % 60)
+    if frac:
+        out += "." + ("%06d" % frac).rstrip("0")
+    return out
 
 
 def java_bigdecimal_to_string(unscaled, scale):

@@ -146,12 +146,28 @@ def full_table(n=3000, seed=0):
         validity={"x": rng.random(n) > 0.1, "k": rng.random(n) > 0.05})
 
 
+class _BinK:
+    """A binning UDF over the LONG column k (NULL rows included, as a Scala UDF over an object type sees them):
+    strings, an int (cast to "1") and None (filled with "NullValue")."""
+
+    def __call__(self, v):
+        if v is None:
+            return "missing"
+        return "low" if v < 50 else (1 if v < 100 else None)
+
+    def __repr__(self):
+        return "binK"
+
+
+BIN_K = _BinK()  # one instance per process: the analyzer's identity (Histogram equality compares the UDF object)
+
+
 def analyzers():
     return [D.Size(), D.Completeness("x"), D.Mean("x"), D.Sum("k"), D.Minimum("y"), D.Maximum("k"),
             D.StandardDeviation("x"), D.Correlation("x", "y"), D.ApproxCountDistinct("k"),
             D.Compliance("big", "x > 5", "k < 150"), D.Mean("y", "k > 20"),
             D.Uniqueness(["k"]), D.Distinctness(["k"]), D.Entropy("k"), D.CountDistinct(["k"]),
-            D.UniqueValueRatio(["k"]), D.Histogram("d", None, 10), D.Uniqueness(["d"]),
+            D.UniqueValueRatio(["k"]), D.Histogram("d", None, 10), D.Uniqueness(["d"]), D.Histogram("k", BIN_K, 10),
             D.ApproxQuantile("x", 0.5), D.ApproxQuantile("y", 0.9, 0.05), D.ApproxQuantiles("y", [0.1, 0.5]),
             D.KLLSketch("x", D.KLLParameters(64, 0.64, 10)), D.KLLSketch("k")]
 
@@ -219,6 +235,15 @@ def test_distributed_runner_matches_single_table_oracle(world):
     for a in analyzers():
         name = type(a).__name__
         g = got[repr(a)]
+        if name == "Histogram" and a.binningUdf is not None:
+            # A/Histogram.scala:59-65: the UDF over every row of the whole table, its result cast to string
+            bins = {}
+            for (v,), c in O.frequencies(t, [a.column], include_nulls=True)[0].items():
+                lab = a.binningUdf(v)
+                lab = "NullValue" if lab is None else str(lab)
+                bins[lab] = bins.get(lab, 0) + c
+            assert g == (len(bins), sorted(bins.items())), (g, bins)
+            continue
         if name == "Histogram":
             freq, _ = O.frequencies(t, [a.column], include_nulls=True)
             assert g[0] == len(freq)
@@ -301,7 +326,7 @@ def _failing_worker(rank, world, port, q):
         mask[rank * per:min(t.nrows, (rank + 1) * per)] = True
         runner = D.distributed.DistributedAnalysisRunner(local=FailingOnRankOne(rank))
         analyzers = [D.Size(), D.Mean("x"), D.KLLSketch("x"), D.Uniqueness(["k"]),
-                     D.Histogram("d", lambda s: s[:1])]
+                     D.Histogram("d", lambda v: None if v is None else str(int(v)))]
         ctx = runner.run(t.select_rows(mask), analyzers)
         out = {(repr(a) if a.__class__.__name__ != "Histogram" else "Histogram"):
                (ctx.metric(a).value.isFailure, str(ctx.metric(a).value.failed) if ctx.metric(a).value.isFailure else None)
@@ -331,7 +356,7 @@ def test_one_failing_rank_fails_every_rank_without_hanging(world):
     assert any(k.startswith("KLLSketch") and v[0] and "rank 1 failed" in v[1] for k, v in got.items())
     assert got["Uniqueness(List(k))"][0] and "rank 1 failed" in got["Uniqueness(List(k))"][1]
     hist = got["Histogram"]
-    assert hist[0] and "binningUdf" in hist[1]
+    assert hist[0] and "rank 1 failed" in hist[1]
 
 
 def mixed_table(n=2400, seed=3):

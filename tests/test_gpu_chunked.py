@@ -1,0 +1,90 @@
+"""ChunkedTable runs (row chunks whose states merge through runOnAggregatedStates, R/AnalysisRunner.scala:385-460)
+against the single-table run: duplicated analyzers, a grouping that fails on every chunk, and merged string states
+built in key-disjoint splits."""
+import numpy as np
+import pytest
+
+import deequ_amd as D
+from deequ_amd import groups as G
+from deequ_amd import runners
+from deequ_amd.table import Table
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b):
+    return a == b or abs(a - b) <= 1e-12 * max(1.0, abs(b))
+
+
+def _data(n=20_000, seed=3):
+    rng = np.random.default_rng(seed)
+    s = [None if rng.random() < 0.05 else "v%d" % int(v) for v in rng.integers(0, 3000, n)]
+    k = [int(v) for v in rng.integers(0, 500, n)]
+    x = [None if rng.random() < 0.1 else float(v) for v in rng.normal(size=n)]
+    return {"s": s, "k": k, "x": x}, {"s": "string", "k": "long", "x": "double"}
+
+
+def _chunked(data, types, cuts):
+    full = Table.from_pydict(data, types=types).to_device()
+    chunks = [Table.from_pydict({c: v[a:b] for c, v in data.items()}, types=types).to_device()
+              for a, b in zip(cuts, cuts[1:])]
+    return full, D.ChunkedTable(chunks)
+
+
+def test_duplicated_analyzers_merge_once():
+    """VerificationSuite does not dedupe its constraints' analyzers (M/VerificationSuite.scala): two constraints on
+    one Size or one Uniqueness must not add each chunk's state twice."""
+    data, types = _data()
+    full, ct = _chunked(data, types, [0, 7_000, 13_000, 20_000])
+    an = [D.Size(), D.Size(), D.Uniqueness(["s"]), D.Uniqueness(["s"]), D.Sum("k"), D.Sum("k"), D.Entropy("k"),
+          D.CountDistinct(["s", "k"]), D.CountDistinct(["s", "k"])]
+    want = D.AnalysisRunner.onData(full).addAnalyzers(an).run()
+    got = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in an:
+        w, g = want.metric(a).value.get(), got.metric(a).value.get()
+        assert _close(g, w), (a, g, w)
+    assert got.metric(D.Size()).value.get() == 20_000
+
+
+def test_grouping_failing_on_every_chunk_returns_failure_metrics(monkeypatch):
+    """A grouping whose frequencies fail on every chunk keeps the chunk failure metrics; the other analyzers of the
+    run still succeed (no 'requirement failed' from the merge)."""
+    data, types = _data()
+    _, ct = _chunked(data, types, [0, 10_000, 20_000])
+    real = runners.computeFrequencies
+
+    def failing(table, cols, *args, **kw):
+        if list(cols) == ["s"]:
+            raise RuntimeError("injected grouping failure")
+        return real(table, cols, *args, **kw)
+
+    monkeypatch.setattr(runners, "computeFrequencies", failing)
+    an = [D.Size(), D.Uniqueness(["s"]), D.Distinctness(["s"]), D.Entropy("k"), D.Mean("x")]
+    got = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in (D.Uniqueness(["s"]), D.Distinctness(["s"])):
+        v = got.metric(a).value
+        assert not v.isSuccess, a
+    assert got.metric(D.Size()).value.get() == 20_000
+    assert got.metric(D.Entropy("k")).value.isSuccess and got.metric(D.Mean("x")).value.isSuccess
+
+
+def test_merged_string_state_split_under_the_offset_limit(monkeypatch):
+    """A merged string / multi-column state whose key bytes reach the int32 Arrow offsets is built in key-disjoint
+    splits (the limit injected small here): the metrics equal the single-table run, with NULL keys and validity
+    joined on the device."""
+    data, types = _data(60_000, seed=9)
+    full, ct = _chunked(data, types, [0, 25_000, 41_000, 60_000])
+    an = [D.Uniqueness(["s"]), D.Distinctness(["s", "k"]), D.UniqueValueRatio(["s"]), D.CountDistinct(["s", "k"]),
+          D.Entropy("s")]
+    want = D.AnalysisRunner.onData(full).addAnalyzers(an).run()
+    monkeypatch.setattr(G, "STRING_KEY_LIMIT", 4096)
+    got = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in an:
+        w, g = want.metric(a).value.get(), got.metric(a).value.get()
+        assert _close(g, w), (a, g, w)
+    # the merged state really was split
+    st = D.Uniqueness(["s", "k"]).computeStateFrom(ct.chunks[0]).sum(
+        D.Uniqueness(["s", "k"]).computeStateFrom(ct.chunks[1]))
+    assert isinstance(st.frequencies, G.BlockParts)
+    assert len(st.frequencies.split_by_key()) > 1
+    assert isinstance(st.device_table(), D.analyzers.SplitFrequencies)

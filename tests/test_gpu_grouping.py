@@ -326,3 +326,41 @@ def test_fingerprint_collisions_are_never_merged():
     for extra in ({}, {"DQ_FREQ_NO_SMALL": "1"}):
         with pytest.raises(NativeError):
             _freq_dict(t, ["s"], False, dict(extra, DQ_FREQ_FP_MASK="0xF"))
+
+
+def test_histogram_binning_udf_per_distinct_value(kats):
+    """Histogram(column, binningUdf) (A/Histogram.scala:59-65: the UDF over the column, its result cast to string,
+    NULL filled with "NullValue", then the group-by): the reference's own case (AnalyzerTests.scala:227-245, a/b ->
+    Value1, the rest -> Value2 over dfMissing.att1) and a 2e6-row LONG column against the oracle's per-row binning. The
+    UDF runs once per distinct value (+ once for NULL), not once per row."""
+    t = table_from_fixture(kats["fixtures"]["dfMissing"])
+    calls = []
+
+    def binner(v):
+        calls.append(v)
+        return "Value1" if v in ("a", "b") else "Value2"
+    h = D.Histogram("att1", binner).calculate(t).value.get()
+    assert h.numberOfBins == 2 and set(h.values) == {"Value1", "Value2"}
+    rng = np.random.default_rng(4)
+    n = 2_000_000
+    v = rng.integers(0, 1000, n).astype(np.int64)
+    valid = rng.random(n) > 0.02
+    t = Table.from_arrays({"v": v}, validity={"v": valid})
+    calls.clear()
+
+    def bin2(x):
+        calls.append(x)
+        if x is None:
+            return None  # -> "NullValue"
+        return "lo" if x < 300 else (7 if x < 900 else None)
+    h = D.Histogram("v", bin2, 10).calculate(t).value.get()
+    assert len(calls) <= 1001
+    want = {}
+    for x, ok in zip(v.tolist(), valid.tolist()):
+        lab = bin2(x if ok else None)
+        lab = "NullValue" if lab is None else str(lab)
+        want[lab] = want.get(lab, 0) + 1
+    assert h.numberOfBins == len(want)
+    assert {k: d.absolute for k, d in h.values.items()} == want
+    for k, d in h.values.items():
+        assert d.ratio == want[k] / n

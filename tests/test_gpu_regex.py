@@ -107,3 +107,48 @@ def test_pattern_match_over_double_and_float_columns():
     for a, g in zip(analyzers, got):
         exp = O.expected_state(t, a)
         assert g == exp, (a.column, a.pattern, g, exp)
+
+
+def test_pattern_match_over_decimal_date_and_timestamp_columns():
+    """regexp_extract over a DECIMAL / DATE / TIMESTAMP column casts it to STRING first (Spark's implicit cast,
+    A/PatternMatch.scala:46-48): BigDecimal.toString at the column scale (scientific below an adjusted exponent of
+    -6), SimpleDateFormat's "yyyy-MM-dd" in the Julian/Gregorian hybrid calendar (dates before 1582-10-15 print in the
+    Julian calendar, 1 BC as 0001), "yyyy-MM-dd HH:mm:ss" + Timestamp.toString's fraction for timestamps, UTC session
+    time zone. Each special value is matched against its exact oracle string (anchored, escaped), so one wrong digit
+    fails; broad patterns run over random values. Java's calendar cutover and BigDecimal notation are restated from
+    their published behaviour (parity unpinned by the reference's own tests); other time zones are out of scope."""
+    import re
+    rng = np.random.default_rng(21)
+    n = 20000
+    dec = rng.integers(-10 ** 12, 10 ** 12, n).astype(np.int64)
+    dec[:12] = [0, 1, -1, 5, 15, 100000, 123456789, -9223372036854775807, 9223372036854775807, 10, 99, 1000001]
+    days = rng.integers(-800_000, 3_000_000, n).astype(np.int32)
+    days[:12] = [0, -1, -141427, -141428, -141429, -719162, -719163, -719528, 2932896, 2932897, 19000, -100]
+    micros = rng.integers(-10 ** 17, 10 ** 17, n).astype(np.int64)
+    micros[:12] = [0, 1, -1, 1_500_000, -1_500_000, 1234567890123456, -62135596800000000, 86_399_999_999, 10,
+                   120_000, -12_219_292_800_000_001, 253402300799999999]
+    micros[12:2000] = micros[12:2000] // 1_000_000 * 1_000_000  # whole seconds: no fraction
+    valid = rng.random(n) > 0.03
+    valid[:12] = True
+    cols = [Column("d2", "decimal", dec, pack_validity(valid), decimal_precision=18, decimal_scale=2),
+            Column("d9", "decimal", dec, pack_validity(valid), decimal_precision=18, decimal_scale=9),
+            Column("d0", "decimal", dec, pack_validity(valid), decimal_precision=18, decimal_scale=0),
+            Column("dt", "date", days, pack_validity(valid)),
+            Column("ts", "timestamp", micros, pack_validity(valid))]
+    t = Table(cols)
+    analyzers = []
+    for c in cols:
+        for i in range(12):
+            s = O.spark_cast_to_string(t[c.name], i)
+            analyzers.append(D.PatternMatch(c.name, "^" + re.escape(s) + "$"))
+    analyzers += [D.PatternMatch(c, p) for c in ("d2", "d9", "d0") for p in (r"E-\d+$", r"^-?0\.0", r"\.\d{2}$",
+                                                                             r"^-?\d+$")]
+    analyzers += [D.PatternMatch("dt", p) for p in (r"^\d{4}-\d{2}-\d{2}$", r"^\d{5,}", r"-02-29$", r"^0")]
+    analyzers += [D.PatternMatch("ts", p) for p in (r"^\d{4}-\d{2}-\d{2} \d{2}:\d{2}:\d{2}$", r"\.\d{1,6}$",
+                                                    r"0$", r" 23:59:59", r"^\d{6}")]
+    got = states(t, analyzers)
+    for a, g in zip(analyzers, got):
+        exp = O.expected_state(t, a)
+        assert g == exp, (a.column, a.pattern, g, exp)
+    for a, g in zip(analyzers[:60], got[:60]):
+        assert g.numMatches >= 1, (a.column, a.pattern)  # the exact rendering of the special value itself

@@ -195,3 +195,35 @@ def test_histogram_identity_and_tostring():
     assert repr(D.ApproxQuantile("c", 0.5, 1e-4)) == "ApproxQuantile(c,0.5,1.0E-4)"
     ctx_keys = {D.Histogram("c", f): 1, D.Histogram("c", g): 2}
     assert ctx_keys[D.Histogram("c", g)] == 2
+
+
+def test_split_by_key_keeps_keys_together_under_the_offset_limit():
+    """A merged string state past the int32 Arrow offsets is built in key-disjoint splits: every copy of
+    a key lands in one split, the counts are preserved and each split stays under the (injected) byte limit."""
+    import numpy as np
+    import deequ_amd.native as N
+    from deequ_amd import groups as G
+    from deequ_amd.table import Column, pack_validity
+
+    def block(keys, counts, valid):
+        data = b"".join(k.encode() for k in keys)
+        off = np.zeros(len(keys) + 1, dtype=np.int64)
+        np.cumsum([len(k.encode()) for k in keys], out=off[1:])
+        col = Column("s", N.TYPE_STRING, np.frombuffer(data, np.uint8), pack_validity(np.array(valid)),
+                     off.astype(np.int32), length=len(keys))
+        return G.GroupBlock([col, Column("k", N.TYPE_LONG, np.arange(len(keys), dtype=np.int64) % 3, None)],
+                            np.array(counts, dtype=np.int64))
+
+    keys = ["key-%05d" % i for i in range(400)]
+    a = block(keys[:300], range(1, 301), [i % 17 != 0 for i in range(300)])
+    b = block(keys[200:], range(1, 201), [i % 13 != 0 for i in range(200)])
+    parts = G.BlockParts([a, b], a.schema())
+    assert parts.split_by_key(limit=10 ** 9) == [parts]
+    splits = parts.split_by_key(limit=1000)
+    assert len(splits) > 1 and all(s.key_bytes() < 1000 for s in splits)
+    assert sum(s.size for s in splits) == parts.size
+    assert sum(int(s.counts.sum()) for s in splits) == int(parts.counts.sum())
+    owner = {}
+    for i, s in enumerate(splits):
+        for key in s.keys():
+            assert owner.setdefault(key, i) == i, key  # a key never spans two splits
