@@ -737,10 +737,14 @@ scatter2_kernel(const Pass2Item* __restrict__ items, const unsigned long long* _
 // (extract_count -> partition1 -> count2 / scan2 / scatter2).
 
 constexpr int kFastRegs = 1024;  // sizing HLL registers of the fast pass 1 (1 KB per workgroup; sizing only)
+constexpr int kSketchBits = 9;   // the sizing sketch samples the keys whose low 9 mixed bits are zero (1 / 512)
 // Pass-1 run cursors, one per 128-byte line: every workgroup of the chip reserves on the same 256 counters, and
 // atomics on one line serialise (16 counters to a line would be 16-way contention on top of the reservation's).
 constexpr int kCursorStride = 16;
 constexpr int kXcds = 8;  // MI355X: 8 XCDs, workgroup i runs on XCD i % 8
+// (r04: splitting each (partition, XCD) sub-region 4 or 8 ways by workgroup, so fewer workgroups share a reservation
+// counter, made pass 1 4.6 -> 5.1-5.2 ms on C4, profiles/r04/c4_split_ab_r04j.txt; one sub-region per XCD stays.)
+constexpr int kP1Sub = kXcds;  // sub-regions per partition
 
 // Raw bits of a W-byte cell, loaded without any branch on the element type (a runtime switch around the load
 // would put a wait after every load: one row in flight per lane); canonical_of() converts after the loads.
@@ -775,6 +779,8 @@ __device__ __forceinline__ uint64_t canonical_of(int elem, uint64_t raw) {
 // Keys that do not fit their bucket (a key repeated more often than a bucket's slack: NaN, 0, a default value) go
 // to one spill buffer as full 64-bit keys, reserved per wave; the build inserts them into the finished table with
 // global atomics (spill_insert_kernel). Only a full spill buffer sends the build to the exactly-counted path.
+constexpr unsigned long long kPosMask = (1ull << 48) - 1ull;  // partition-buffer positions (2^48 keys)
+
 struct Spill {
     unsigned long long* keys;
     unsigned long long cap;
@@ -837,7 +843,11 @@ __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / 
             if (hb) {
                 const unsigned long long k = bucket_of(b0 + b);
                 const unsigned long long at = atomicAdd(&gcursor[counter_of(b0 + b)], (unsigned long long)hb);
-                cursor[b0 + b] = k * cap + at;
+                // staged index i of this digit lands at (k cap + at - start) + i while i < start + fit; both halves in
+                // one LDS word (positions < 2^48, staged indices < 2^16), so a key needs one read to place itself
+                const unsigned long long fit = at >= cap ? 0ull : (cap - at < hb ? cap - at : (unsigned long long)hb);
+                const unsigned long long rel = (k * cap + at - (unsigned long long)(run - hb)) & kPosMask;
+                cursor[b0 + b] = rel | ((unsigned long long)(run - hb + fit) << 48);
             }
         }
     }
@@ -855,10 +865,9 @@ __device__ __forceinline__ void scatter_tile_reserve(const uint64_t (&h)[TILE / 
         const unsigned int lane = threadIdx.x & 63;
         for (unsigned int i = threadIdx.x; i < total; i += kFreqBlock) {
             const unsigned long long hv = sh[i];
-            const unsigned int d = digit(hv);
-            const unsigned long long pos = cursor[d] + (i - start[d]);
-            const bool fits = pos < (bucket_of(d) + 1) * cap;
-            if (fits) out_h[pos] = (OutT)hv;
+            const unsigned long long cw = cursor[digit(hv)];
+            const bool fits = i < (unsigned int)(cw >> 48);
+            if (fits) out_h[(cw + i) & kPosMask] = (OutT)hv;
             const unsigned long long sm = __ballot(!fits);
             if (sm) {  // wave-uniform: one reservation per wave for its spilled keys
                 const int leader = __ffsll((long long)sm) - 1;
@@ -894,14 +903,93 @@ __device__ __forceinline__ uint64_t narrow_canon(const NarrowKey& nk, uint32_t p
 }
 
 // Fast pass 1: rows -> 256 partitions x 8 XCD sub-regions of `cap` keys each (sub-region (d, x) at (8 d + x) * cap),
-// plus the side counters and the
-// sizing registers (per workgroup, reduced by sizing_reduce_kernel). W = the key column's cell width. The next
-// tile's cells are loaded while the current tile is scattered (after its reservation atomics returned).
-template <int TILE, int W, bool NARROW>
-__global__ void __launch_bounds__(kFreqBlock)
+// plus the side counters and the sizing registers (per workgroup, reduced by sizing_reduce_kernel). W = the key
+// column's cell width, FLT = FLOAT / DOUBLE cells (NaN canonical). The next tile's cells are loaded while the current
+// tile is scattered (after its reservation atomics returned). (r04: lane-contiguous rows — 16 consecutive cells per
+// lane as 16-byte loads at a 128-byte lane stride, the validity one 16-bit load — cut the VALU work but made the pass
+// 4.8 -> 5.4 ms: 64 lines per load instruction; the coalesced layout stays.)
+typedef int fq_v4i __attribute__((ext_vector_type(4)));
+typedef int fq_v2i __attribute__((ext_vector_type(2)));
+
+template <int W, bool FLT>
+__device__ __forceinline__ uint64_t canonical_cell(uint64_t raw) {
+    if (W == 8) {
+        if (FLT) {
+            const bool nan = (raw & 0x7FFFFFFFFFFFFFFFull) > 0x7FF0000000000000ull;
+            return nan ? 0x7ff8000000000000ull : raw;
+        }
+        return raw;
+    }
+    if (W == 4) {
+        if (FLT) {
+            const bool nan = (raw & 0x7FFFFFFFu) > 0x7F800000u;
+            return nan ? 0x7fc00000ull : raw;
+        }
+        return (uint64_t)(int64_t)(int32_t)(uint32_t)raw;
+    }
+    if (W == 2) return (uint64_t)(int64_t)(int16_t)(uint16_t)raw;
+    return FLT ? (raw ? 1ull : 0ull) : (uint64_t)(int64_t)(int8_t)(uint8_t)raw;  // W = 1: FLT marks BOOLEAN
+}
+
+// The lane's PER = 16 rows of tile t0 (row t0 + 256 j + tid: a wave's loads are 64 consecutive cells, coalesced): raw
+// cells and the validity word (bit j = row j's). A full tile takes buffer loads (the tile base in SGPRs, the row
+// offset j in the scalar offset: no per-row address arithmetic); the last, partial tile reads row by row.
+template <int W>
+__device__ __forceinline__ void p1_load(const KeyCol& c, int64_t t0, int64_t nrows, uint64_t (&raw)[16],
+                                        unsigned int& vword) {
+    constexpr int TILE = 16 * kFreqBlock;
+    const int64_t rem = nrows - t0;
+    const int tid = (int)threadIdx.x;
+    if (rem >= TILE) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(static_cast<const char*>(c.values) + t0 * W), (short)0, TILE * W, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int so = j * kFreqBlock * W;
+            if (W == 8) {
+                const fq_v2i x = __builtin_amdgcn_raw_buffer_load_b64(r, tid * 8, so, 0);
+                raw[j] = ((uint64_t)(uint32_t)x.y << 32) | (uint32_t)x.x;
+            } else if (W == 4) {
+                raw[j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, tid * 4, so, 0);
+            } else if (W == 2) {
+                raw[j] = (uint16_t)__builtin_amdgcn_raw_buffer_load_b16(r, tid * 2, so, 0);
+            } else {
+                raw[j] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(r, tid, so, 0);
+            }
+        }
+        if (c.validity) {
+            const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(c.validity + (t0 >> 3)), (short)0, TILE / 8, 0x00020000);
+            const unsigned int sh = (unsigned int)tid & 7u;
+            unsigned int w = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const unsigned int b = (unsigned int)__builtin_amdgcn_raw_buffer_load_b8(rv, tid >> 3, j * (kFreqBlock / 8), 0);
+                w |= ((b >> sh) & 1u) << j;
+            }
+            vword = w;
+        } else {
+            vword = 0xFFFFu;
+        }
+        return;
+    }
+    vword = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int64_t r = t0 + (int64_t)j * kFreqBlock + tid;
+        const bool in = r < nrows;
+        raw[j] = in ? load_bits<W>(c.values, r) : 0ull;
+        const bool ok = in && (!c.validity || ((c.validity[r >> 3] >> (r & 7)) & 1u));
+        vword |= (ok ? 1u : 0u) << j;
+    }
+}
+
+template <int TILE, int W, bool NARROW, bool FLT>
+__global__ void __launch_bounds__(kFreqBlock)  // 41 KB of LDS: 3 workgroups per CU (wide keys: 167 VGPRs fit)
 partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long long cap,
                        unsigned long long* __restrict__ gcursor, void* __restrict__ out,
                        uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, NarrowKey nk, Spill sp) {
+    static_assert(TILE == 16 * kFreqBlock, "16 rows per lane");
     using OutT = typename std::conditional<NARROW, uint32_t, unsigned long long>::type;
     OutT* __restrict__ out_h = static_cast<OutT*>(out);
     constexpr int PER = TILE / kFreqBlock;
@@ -915,55 +1003,57 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
     hist[threadIdx.x] = 0;
     if (threadIdx.x == 0) lovf = 0;
     __syncthreads();
-    unsigned long long taken = 0, sent = 0, nulls = 0, miss = 0;
+    // per-lane counts (a lane sees nrows / (grid x 256) rows: 32 bits), widened once at the end
+    unsigned int taken = 0, sent = 0, nulls = 0, miss = 0;
     const int64_t ntiles = (nrows + TILE - 1) / TILE;
-    const bool has_validity = c.validity != nullptr;
     // workgroups are dealt round-robin to the XCDs: each XCD's workgroups fill their own sub-region of every
     // partition, so a reservation counter is shared by 1/8 of the chip (and stays with one XCD's traffic)
     const unsigned int xcd = blockIdx.x % kXcds;
     uint64_t raw[PER];
-    unsigned int vbyte[PER];  // the validity byte holding the row's bit (0xFF without a bitmap)
-    auto load = [&](int64_t tl) {
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const int64_t r = tl * TILE + (int64_t)j * kFreqBlock + threadIdx.x;
-            const bool in = r < nrows;
-            raw[j] = in ? load_bits<W>(c.values, r) : 0ull;
-            vbyte[j] = !in ? 0u : (has_validity ? (unsigned int)c.validity[r >> 3] : 0xFFu);
-        }
-    };
+    unsigned int vword = 0;
     int64_t tile = blockIdx.x;
-    if (tile < ntiles) load(tile);
+    if (tile < ntiles) p1_load<W>(c, tile * TILE, nrows, raw, vword);
     for (; tile < ntiles; tile += gridDim.x) {
         const int64_t t0 = tile * TILE;
         uint64_t h[PER];
         uint32_t pay[PER];
-        unsigned int keepm = 0;
+        // row masks: valid (rows past the end read as invalid), EMPTY-colliding, narrow-window misses; the counters
+        // take their popcounts once per tile
+        const unsigned int vm = vword;
+        unsigned int em = 0, mm = 0;
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            const int64_t r = t0 + (int64_t)j * kFreqBlock + threadIdx.x;
-            const bool in = r < nrows;
-            const bool valid = (vbyte[j] >> (r & 7)) & 1u;
-            const uint64_t canon = canonical_of<W>(c.elem, raw[j]);
+            const uint64_t canon = canonical_cell<W, FLT>(raw[j]);
             h[j] = mix64(canon);
+            em |= (h[j] == kEmpty ? 1u : 0u) << j;
             if (NARROW) {
                 const uint64_t off = canon - nk.base;
                 pay[j] = (uint32_t)off;
-                if (W == 8 && valid && (off >> 32)) ++miss;
+                if (W == 8) mm |= ((off >> 32) != 0 ? 1u : 0u) << j;
             }
-            const bool keep = valid && h[j] != kEmpty;
-            keepm |= (keep ? 1u : 0u) << j;
-            taken += (valid || (in && include_nulls)) ? 1 : 0;
-            nulls += (in && !valid && include_nulls) ? 1 : 0;
-            sent += (valid && h[j] == kEmpty) ? 1 : 0;
+        }
+        const unsigned int keepm = vm & ~em;
+        sent += __popc(vm & em);
+        if (NARROW && W == 8) miss += __popc(mm & vm);
+        if (include_nulls) {  // Histogram: the NULL rows in range count (as the NULL group)
+            const int64_t lrem = nrows - t0 - (int64_t)threadIdx.x;  // row t0 + 256 j + tid is in range iff 256 j < lrem
+            unsigned int inm = 0;
+#pragma unroll
+            for (int j = 0; j < PER; ++j) inm |= ((int64_t)j * kFreqBlock < lrem ? 1u : 0u) << j;
+            nulls += __popc(inm & ~vm);
+            taken += __popc(inm);
+        } else {
+            taken += __popc(vm);
         }
         const int64_t next = tile + gridDim.x;
-        // the sizing sketch sees the keys whose low 3 bits are zero: a 1/8 sample of the distinct keys (each key is
-        // in or out on every row), scaled back by 8 on the host. The sample bits must lie below every bit a rank can
-        // reach (a forced-zero run inside the rank field would inflate the maxima, and the estimate with them).
+        // the sizing sketch sees the keys whose low kSketchBits bits are zero: a 1/512 sample of the distinct keys
+        // (each key is in or out on every row), scaled back on the host. A sparse sample leaves the block below
+        // unexecuted by most waves (its instructions run whenever one lane of 64 qualifies). The sample bits lie below
+        // every bit a rank can reach but the last 9 of 54 (a forced-zero run inside the rank field would inflate the
+        // maxima; reaching it needs 45 zero bits first).
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
-            if (!((keepm >> j) & 1u) || (h[j] & 7u)) continue;
+            if (!((keepm >> j) & 1u) || (h[j] & ((1u << kSketchBits) - 1u))) continue;
             const unsigned int idx = (unsigned int)(h[j] >> 54);
             const unsigned int rank = (unsigned int)__clzll((long long)((h[j] << 10) | (1ull << 9))) + 1u;
             if (rank > regs[idx]) atomicMax(&regs[idx], rank);
@@ -973,23 +1063,23 @@ partition1_fast_kernel(KeyCol c, int64_t nrows, int include_nulls, unsigned long
             for (int j = 0; j < PER; ++j) h[j] = ((h[j] & (kDigitBins - 1)) << 32) | pay[j];
         }
         scatter_tile_reserve<kDigitBins, TILE, NARROW>(h, keepm, 0, kDigitBins - 1, hist, start, cursor, sh, gcursor, cap,
-                                               [xcd](int b) { return (unsigned long long)b * kXcds + xcd; },
-                                               [xcd](int b) { return ((unsigned long long)b * kXcds + xcd) * kCursorStride; },
+                                               [xcd](int b) { return (unsigned long long)b * kP1Sub + xcd; },
+                                               [xcd](int b) { return ((unsigned long long)b * kP1Sub + xcd) * kCursorStride; },
                                                &lovf, sp, [nk](uint64_t v) {
                                                    return NARROW ? mix64(narrow_canon(nk, (uint32_t)v)) : v;
                                                }, out_h, [&]() {
-            if (next < ntiles) load(next);
+            if (next < ntiles) p1_load<W>(c, next * TILE, nrows, raw, vword);
         });
     }
-    taken = block_sum_u64(taken, red);
-    sent = block_sum_u64(sent, red);
-    nulls = block_sum_u64(nulls, red);
-    if (NARROW && W == 8) miss = block_sum_u64(miss, red);
+    const unsigned long long wtaken = block_sum_u64(taken, red);
+    const unsigned long long wsent = block_sum_u64(sent, red);
+    const unsigned long long wnulls = block_sum_u64(nulls, red);
+    const unsigned long long wmiss = (NARROW && W == 8) ? block_sum_u64(miss, red) : 0ull;
     if (threadIdx.x == 0) {
-        if (taken) atomicAdd(&ctr->num_rows, taken);
-        if (sent) atomicAdd(&ctr->sentinel, sent);
-        if (nulls) atomicAdd(&ctr->nulls, nulls);
-        if (miss) atomicAdd(&ctr->narrow_miss, miss);
+        if (wtaken) atomicAdd(&ctr->num_rows, wtaken);
+        if (wsent) atomicAdd(&ctr->sentinel, wsent);
+        if (wnulls) atomicAdd(&ctr->nulls, wnulls);
+        if (wmiss) atomicAdd(&ctr->narrow_miss, wmiss);
         if (lovf) atomicAdd(&ctr->pad[0], 1ull);
     }
     for (int i = threadIdx.x; i < kFastRegs / 4; i += kFreqBlock) {
@@ -1157,6 +1247,8 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
                 h[u] = j < it.end ? hs[j] : kEmpty;
             rw[u] = ((GENERAL || WEIGHTED) && j < it.end) ? rows[j] : 0ull;
         }
+        // (r04: issuing the 8 keys' compare-and-swaps before looking at any result made the C4 build 3.1 -> 4.1 ms,
+        // profiles/r04/c4_split_ab_r04j.txt; one key at a time stays)
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u)
             if (h[u] != kEmpty)
@@ -1217,13 +1309,14 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
         for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
             const unsigned long long h = lkey[i];
             if (h == kEmpty) continue;
+            const unsigned long long cnt = (unsigned long long)lcnt[i];
             unsigned int p = region_probe(h);
             bool done = false;
             for (int probe = 0; probe < kRegion; ++probe) {
                 Slot* sl = region + p;
                 const unsigned long long prev = atomicCAS(&sl->key, kEmpty, h);
                 if (prev == kEmpty || prev == h) {
-                    atomicAdd(&sl->count, (unsigned long long)lcnt[i]);
+                    atomicAdd(&sl->count, cnt);
                     if (GENERAL) atomicMin(&rrep[p], lrep[i]);
                     done = true;
                     break;
@@ -2126,7 +2219,7 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     const size_t ksz = narrow ? 4 : 8;  // bytes per key in the partition buffers
     // pass 1: 256 partitions x 8 XCD sub-regions of cap1 keys (the expected share plus slack for hashing variance
     // and repeated keys)
-    constexpr int kSub = kDigitBins * kXcds;
+    constexpr int kSub = kDigitBins * kP1Sub;
     const unsigned long long share = (unsigned long long)(nrows / kSub);
     const unsigned long long cap1 = share + share / 8 + 16384;
     unsigned long long* gc1 = nullptr;
@@ -2146,23 +2239,30 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
     const int inul = t->ks.include_nulls ? 1 : 0;
     // (measured: an 8 K-key pass-1 tile runs 8.1 ms against 6.1 ms for 4 K on C4 -- twice the registers)
-#define DQ_P1(W, N)                                                                                                   \
-    hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, W, N>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks.cols[0], \
-                       nrows, inul, cap1, gc1, h1, regs_part, t->ctr, nk, sp)
+#define DQ_P1(W, N, F)                                                                                              \
+    hipLaunchKernelGGL((partition1_fast_kernel<kP1TileFast, W, N, F>), dim3(xgrid), dim3(kFreqBlock), 0, s,            \
+                       t->ks.cols[0], nrows, inul, cap1, gc1, h1, regs_part, t->ctr, nk, sp)
     ctx->freq_paths[narrow ? DQ_FREQ_PATH_FAST_NARROW : DQ_FREQ_PATH_FAST]++;
-    switch (elem_size((ElemType)t->ks.cols[0].elem)) {
-        case 8:
-            if (narrow) DQ_P1(8, true); else DQ_P1(8, false);
-            break;
-        case 4:
-            if (narrow) DQ_P1(4, true); else DQ_P1(4, false);
-            break;
-        case 2:
-            if (narrow) DQ_P1(2, true); else DQ_P1(2, false);
-            break;
-        default:
-            if (narrow) DQ_P1(1, true); else DQ_P1(1, false);
-            break;
+    {
+        const ElemType e1 = (ElemType)t->ks.cols[0].elem;
+        const bool flt = e1 == ET_F64 || e1 == ET_F32 || e1 == ET_U8;  // NaN canonical / BOOLEAN 0-1
+        switch (elem_size(e1)) {
+            case 8:
+                if (flt) { if (narrow) DQ_P1(8, true, true); else DQ_P1(8, false, true); }
+                else { if (narrow) DQ_P1(8, true, false); else DQ_P1(8, false, false); }
+                break;
+            case 4:
+                if (flt) { if (narrow) DQ_P1(4, true, true); else DQ_P1(4, false, true); }
+                else { if (narrow) DQ_P1(4, true, false); else DQ_P1(4, false, false); }
+                break;
+            case 2:
+                if (narrow) DQ_P1(2, true, false); else DQ_P1(2, false, false);
+                break;
+            default:
+                if (flt) { if (narrow) DQ_P1(1, true, true); else DQ_P1(1, false, true); }
+                else { if (narrow) DQ_P1(1, true, false); else DQ_P1(1, false, false); }
+                break;
+        }
     }
 #undef DQ_P1
     hipLaunchKernelGGL(sizing_reduce_kernel, dim3(kFastRegs / 256, std::min(xgrid, 64)), dim3(256), 0, s,
@@ -2186,7 +2286,7 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
     const unsigned long long spilled1 = t->host_ctr.spilled;
     unsigned long long n = 0;
     for (unsigned long long c : pcount) n += c;
-    const double est = n ? 8.0 * hll_raw_estimate(hregs) : 0.0;  // the sketch holds a 1/8 sample of the keys
+    const double est = n ? (double)(1u << kSketchBits) * hll_raw_estimate(hregs) : 0.0;  // a 1/512 sample of the keys
     int bits = 0;
     while (bits < 40 && est / (double)(1ull << bits) > (double)kRegionTarget) ++bits;
     if (getenv("DQ_DEBUG_FREQ"))
@@ -2210,8 +2310,8 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
             for (int q = 0; q < kSub; ++q) {
                 const unsigned long long base = (unsigned long long)q * cap1;
                 for (unsigned long long x = 0; x < pcount[q]; x += kPass2Item)
-                    by_part[q / kXcds].push_back(FastItem{base + x, base + std::min<unsigned long long>(pcount[q], x + kPass2Item),
-                                                          (unsigned int)(q / kXcds), 0u});
+                    by_part[q / kP1Sub].push_back(FastItem{base + x, base + std::min<unsigned long long>(pcount[q], x + kPass2Item),
+                                                           (unsigned int)(q / kP1Sub), 0u});
             }
             std::vector<FastItem> items;
             for (size_t round = 0;; ++round) {

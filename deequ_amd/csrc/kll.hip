@@ -131,32 +131,45 @@ kll_write_kernel(KllColumn c, int64_t nrows, const unsigned long long* __restric
     }
 }
 
-// The same for every column of a batched sketch (blockIdx.y = job).
+// The same for every column of a batched sketch (blockIdx.y = job). Each thread loads its 8 rows of the tile at once
+// (rows t + 256 q: every load instruction coalesced), the ballots of all 8 row groups go to LDS together, and one
+// barrier later every value knows its dense position: one round trip per tile instead of one per 256 rows.
 __global__ void __launch_bounds__(kKllStageBlock)
 kll_write_jobs_kernel(const KllCountJob* __restrict__ jobs, int64_t nrows) {
     const KllCountJob& j = jobs[blockIdx.y];
     if (!j.dense) return;
-    __shared__ unsigned int wsum[kKllStageBlock / 64];
+    constexpr int Q = kKllStageRows / kKllStageBlock, NW = kKllStageBlock / 64;
+    __shared__ unsigned int wc[Q * NW];
     const KllColumn c = j.c;
     const int64_t r0 = (int64_t)blockIdx.x * kKllStageRows;
-    unsigned long long base = j.offs[blockIdx.x];
-    double* __restrict__ out = j.dense;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t rb = r0; rb < r0 + kKllStageRows && rb < nrows; rb += kKllStageBlock) {
-        const int64_t r = rb + threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    double x[Q];
+    unsigned long long bal[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int64_t r = r0 + (int64_t)q * kKllStageBlock + t;
         const bool v = r < nrows && kll_valid(c, r);
-        const unsigned long long ball = __ballot(v);
-        const unsigned int before = (unsigned int)__popcll(ball & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[wave] = (unsigned int)__popcll(ball);
-        __syncthreads();
-        unsigned int wbase = 0, total = 0;
-        for (int w = 0; w < kKllStageBlock / 64; ++w) {
-            if (w < wave) wbase += wsum[w];
-            total += wsum[w];
+        x[q] = v ? kll_load(c, r) : 0.0;
+        bal[q] = __ballot(v);
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) wc[q * NW + wave] = (unsigned int)__popcll(bal[q]);
+    }
+    __syncthreads();
+    unsigned long long at = j.offs[blockIdx.x];
+    double* __restrict__ out = j.dense;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        unsigned int wq = 0, tq = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const unsigned int n = wc[q * NW + w];
+            wq += w < wave ? n : 0u;
+            tq += n;
         }
-        if (v) out[base + wbase + before] = kll_load(c, r);
-        base += total;
-        __syncthreads();
+        if ((bal[q] >> lane) & 1ull) out[at + wq + (unsigned int)__popcll(bal[q] & ((1ull << lane) - 1ull))] = x[q];
+        at += tq;
     }
 }
 
@@ -310,11 +323,134 @@ __device__ __forceinline__ void kll_merge_round(uint64_t* k, uint64_t (&v)[E], i
 // Batched launches (one launch per level and class over every column of a dq_kll_sketch_columns call): a descriptor's
 // bits 55-62 name its column, whose stream / next-level / min-max pointers for this level come from `cols`.
 struct KllColPtr {
-    const double* src;
+    const double* src;          // the level's stream; null at level 0 of a column read in place (below)
     double* dst;
     unsigned long long* minmax;
-    unsigned long long pad;
+    // level 0 read in place: the raw column and its NULL-compaction tile offsets (kll_count / kll_scan)
+    KllColumn raw;
+    const unsigned long long* offs;
+    int64_t ntiles, nrows;
 };
+
+// ---- level 0 in place -----------------------------------------------------------------------------------------------
+// A level-0 compaction consumes the dense stream of the column's non-NULL values [start, start + L). Instead of writing
+// that stream out (8 B written and re-read per value), the compaction reads the raw column: kll_locate_kernel turns each
+// level-0 descriptor's dense range into a row range once (tile offsets + a select inside the tile), and the workgroup
+// stages the range's non-NULL values into its LDS image in dense order (ballot prefixes), then sorts as before.
+
+// Row of the d-th non-NULL value (d < the column's non-NULL count): the last tile whose offset is <= d, then the
+// (d - offset)-th set validity bit of that tile.
+__device__ int64_t kll_row_of(const KllColPtr& cp, uint64_t d) {
+    if (!cp.raw.validity) return (int64_t)d;
+    int64_t lo = 0, hi = cp.ntiles - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (cp.offs[mid] <= d) lo = mid;
+        else hi = mid - 1;
+    }
+    uint64_t need = d - cp.offs[lo];
+    const int64_t w0 = lo * (kKllStageRows / 64), wend = (cp.nrows + 63) >> 6;
+    for (int64_t w = w0; w < w0 + kKllStageRows / 64 && w < wend; ++w) {
+        uint64_t bits = cp.raw.validity[w];
+        if (w == wend - 1 && (cp.nrows & 63)) bits &= (1ull << (cp.nrows & 63)) - 1ull;
+        const uint64_t c = (uint64_t)__popcll(bits);
+        if (need < c) {
+            for (uint64_t k = 0; k < need; ++k) bits &= bits - 1ull;  // drop the lowest `need` set bits
+            return (w << 6) + (__ffsll((long long)bits) - 1);
+        }
+        need -= c;
+    }
+    return cp.nrows;  // not reached for d below the non-NULL count
+}
+
+__global__ void __launch_bounds__(256)
+kll_locate_kernel(const uint64_t* __restrict__ segs, int n, const KllColPtr* __restrict__ cols,
+                  unsigned long long* __restrict__ rows) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t sg = segs[i];
+    const KllColPtr cp = cols[(sg >> 55) & 0xFF];
+    if (cp.src) return;  // a column read as a stream (zero copy)
+    const uint64_t start = sg & ((1ull << 40) - 1);
+    const uint32_t len = (uint32_t)((sg >> 40) & 0x7FFF);
+    rows[2 * i] = (unsigned long long)kll_row_of(cp, start);
+    rows[2 * i + 1] = len ? (unsigned long long)kll_row_of(cp, start + len - 1) + 1ull : rows[2 * i];
+}
+
+// Stages the non-NULL values of rows [r0, r1) (exactly `len` of them) as order keys, in row order: place(pos, key).
+// Each thread loads RM rows per chunk at once (rows r0 + q T + t: coalesced), the chunk's ballots give every value its
+// dense position, one barrier pair per chunk of RM * T rows.
+template <int T, bool RAWBITS = false, typename Place>
+__device__ __forceinline__ void kll_stage_rows(const KllColumn& c, int64_t r0, int64_t r1, unsigned int* wc,
+                                               Place place) {
+    constexpr int RM = 8, NW = T / 64, NE = RM * NW;  // NE <= 128: (chunk row, wave) counts
+    static_assert(NE <= 128, "two scan entries per lane of wave 0");
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    unsigned int base = 0;
+    for (int64_t c0 = r0; c0 < r1; c0 += (int64_t)RM * T) {
+        uint64_t key[RM];
+        uint64_t bal[RM];
+#pragma unroll
+        for (int q = 0; q < RM; ++q) {
+            const int64_t r = c0 + (int64_t)q * T + t;
+            const bool v = r < r1 && kll_valid(c, r);
+            const double x = v ? kll_load(c, r) : 0.0;
+            key[q] = RAWBITS ? (uint64_t)__double_as_longlong(x) : kll_key(x);
+            bal[q] = __ballot(v);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < RM; ++q) wc[q * NW + wave] = (unsigned int)__popcll(bal[q]);
+        }
+        __syncthreads();
+        // wave 0: exclusive prefix of the counts in (chunk row, wave) order, written back in place; the chunk total in
+        // wc[NE]
+        if (wave == 0) {
+            const unsigned int a0 = lane < NE ? wc[lane] : 0u, b0 = lane + 64 < NE ? wc[lane + 64] : 0u;
+            unsigned int a = a0, b = b0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int x = __shfl_up(a, o, 64), y = __shfl_up(b, o, 64);
+                if (lane >= o) {
+                    a += x;
+                    b += y;
+                }
+            }
+            const unsigned int ta = __shfl(a, 63, 64), tb = __shfl(b, 63, 64);
+            if (lane < NE) wc[lane] = a - a0;
+            if (lane + 64 < NE) wc[lane + 64] = ta + b - b0;
+            if (lane == 0) wc[NE] = ta + tb;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < RM; ++q)
+            if ((bal[q] >> lane) & 1ull)
+                place(base + wc[q * NW + wave] + (unsigned int)__popcll(bal[q] & ((1ull << lane) - 1ull)), key[q]);
+        base += wc[NE];
+        __syncthreads();
+    }
+}
+
+// Level 0 read in place: its final buffer (the non-NULL values [pos, pos + len) that no compaction consumed) written
+// out densely for the gather, one workgroup per column (blockIdx.x = job).
+struct KllTail0Job {
+    const KllColPtr* col;  // device pointer to the column's level-0 KllColPtr
+    unsigned long long pos, len;
+    double* out;
+};
+__global__ void __launch_bounds__(256)
+kll_tail0_kernel(const KllTail0Job* __restrict__ jobs) {
+    const KllTail0Job j = jobs[blockIdx.x];
+    const KllColPtr cp = *j.col;
+    __shared__ long long r0s;
+    __shared__ unsigned int wc[8 * 4 + 1];
+    if (threadIdx.x == 0) r0s = j.len ? (long long)kll_row_of(cp, j.pos) : cp.nrows;
+    __syncthreads();
+    // exactly `len` non-NULL values remain from that row to the end of the column
+    kll_stage_rows<256, true>(cp.raw, (int64_t)r0s, cp.nrows, wc, [&](unsigned int pos, uint64_t bits) {
+        if (pos < j.len) j.out[pos] = __longlong_as_double((long long)bits);  // the values as loaded (NaN payloads)
+    });
+}
 
 template <typename S, typename D, typename M>
 __device__ __forceinline__ void kll_col_ptrs(const KllColPtr* cols, uint64_t sg, S& src, D& dst, M& minmax) {
@@ -329,20 +465,33 @@ __device__ __forceinline__ void kll_col_ptrs(const KllColPtr* cols, uint64_t sg,
 template <int T, int E>
 __global__ void __launch_bounds__(T)
 kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
-                   unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols) {
+                   unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols,
+                   const unsigned long long* __restrict__ rows) {
     constexpr int PAD = T * E;
     __shared__ uint64_t k[PAD + T];
+    __shared__ unsigned int wc[8 * (T / 64) + 1];
     const uint64_t sg = segs[blockIdx.x];
     kll_col_ptrs(cols, sg, src, dst, minmax);
     const uint64_t start = sg & ((1ull << 40) - 1);
     const int len = (int)((sg >> 40) & 0x7FFF);
     const int t = threadIdx.x;
-    const double* in = src + start;
     uint64_t v[E];
+    if (rows && !src) {  // level 0 read in place: stage the range's values in dense order (uniform branch)
+        auto at = [](int i) { return i + i / E; };
+        kll_stage_rows<T>(cols[(sg >> 55) & 0xFF].raw, (int64_t)rows[2 * blockIdx.x], (int64_t)rows[2 * blockIdx.x + 1],
+                          wc, [&](unsigned int pos, uint64_t key) { if ((int)pos < len) k[at((int)pos)] = key; });
 #pragma unroll
-    for (int r = 0; r < E; ++r) {
-        const int i = t * E + r;
-        v[r] = i < len ? kll_key(in[i]) : ~0ull;
+        for (int r = 0; r < E; ++r) {
+            const int i = t * E + r;
+            v[r] = i < len ? k[at(i)] : ~0ull;
+        }
+    } else {
+        const double* in = src + start;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int i = t * E + r;
+            v[r] = i < len ? kll_key(in[i]) : ~0ull;
+        }
     }
     kll_reg_sort<E>(v);
     for (int w = E; w < PAD; w <<= 1) kll_merge_round<E>(k, v, t, w);
@@ -381,12 +530,14 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
 template <int T, int E>
 __global__ void __launch_bounds__(T)
 kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
-                     unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols) {
+                     unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols,
+                     const unsigned long long* __restrict__ rows) {
     constexpr int P = T * E;
     constexpr int XM = 64;
     static_assert(T >= XM, "wave 0 sorts the extras");
     __shared__ uint64_t k[P + T];
     __shared__ uint64_t ex[XM];
+    __shared__ unsigned int wc[8 * (T / 64) + 1];
     auto at = [](int i) { return i + i / E; };
     const uint64_t sg = segs[blockIdx.x];
     kll_col_ptrs(cols, sg, src, dst, minmax);
@@ -394,12 +545,24 @@ kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict_
     const int len = (int)((sg >> 40) & 0x7FFF);
     const int rx = len - P;  // 0..XM (host-checked)
     const int t = threadIdx.x;
-    const double* in = src + start;
     uint64_t v[E];
-#pragma unroll
-    for (int r = 0; r < E; ++r) v[r] = kll_key(in[t * E + r]);
     uint64_t xk = ~0ull;
-    if (t < XM && t < rx) xk = kll_key(in[P + t]);
+    if (rows && !src) {  // level 0 read in place (see kll_compact_kernel)
+        kll_stage_rows<T>(cols[(sg >> 55) & 0xFF].raw, (int64_t)rows[2 * blockIdx.x], (int64_t)rows[2 * blockIdx.x + 1],
+                          wc, [&](unsigned int pos, uint64_t key) {
+                              if ((int)pos < P) k[at((int)pos)] = key;
+                              else if ((int)pos < len) ex[pos - P] = key;
+                          });
+#pragma unroll
+        for (int r = 0; r < E; ++r) v[r] = k[at(t * E + r)];
+        if (t < XM && t < rx) xk = ex[t];
+        __syncthreads();  // every extra read before wave 0 sorts them back into ex[]
+    } else {
+        const double* in = src + start;
+#pragma unroll
+        for (int r = 0; r < E; ++r) v[r] = kll_key(in[t * E + r]);
+        if (t < XM && t < rx) xk = kll_key(in[P + t]);
+    }
     kll_reg_sort<E>(v);
     for (int w = E; w < P; w <<= 1) kll_merge_round<E>(k, v, t, w);
     // the sorted main array in LDS (the extras' ranks) and the extras sorted by wave 0
@@ -491,11 +654,12 @@ int kll_class_of(int len) {
 }
 
 int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nseg, double* dst,
-                       unsigned long long* minmax, hipStream_t s, const KllColPtr* cols = nullptr) {
+                       unsigned long long* minmax, hipStream_t s, const KllColPtr* cols = nullptr,
+                       const unsigned long long* rows = nullptr) {
     if (nseg <= 0) return 0;
     switch (cls) {
 #define KLL_CASE(C, T, E) \
-    case C: hipLaunchKernelGGL((kll_compact_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols); break;
+    case C: hipLaunchKernelGGL((kll_compact_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols, rows); break;
         KLL_CASE(0, 64, 4)
         KLL_CASE(1, 64, 8)
         KLL_CASE(2, 64, 12)
@@ -511,7 +675,7 @@ int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nse
 #undef KLL_CASE
 #define KLL_XCASE(C, T, E) \
     case C: \
-        hipLaunchKernelGGL((kll_compact_x_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols); break;
+        hipLaunchKernelGGL((kll_compact_x_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols, rows); break;
         KLL_XCASE(12, 64, 4)
         KLL_XCASE(13, 64, 8)
         KLL_XCASE(14, 128, 8)
@@ -1032,7 +1196,12 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
     int nstreams = 1;
     // several columns: one launch per (level, class) over all of them (below) unless DQ_KLL_PER_COLUMN asks for one
     // launch chain per column (spread over the streams)
-    const bool batched = ncols > 1 && ncols <= 255 && !getenv("DQ_KLL_PER_COLUMN");
+    const bool batched = ncols >= 1 && ncols <= 255 && !getenv("DQ_KLL_PER_COLUMN");
+    // batched: level 0 of a NULL-compacted column can be read in place by its compactions (DQ_KLL_INPLACE=1: no dense
+    // stream, 8 B written and re-read per value less). Measured slower end to end on the C5 shard (profiles/r04/
+    // c5_kll_ab_r04k.txt: the staging adds ~15 % to every level-0 compaction, and those run after the host schedule,
+    // while the dense write overlaps it), so the dense stream stays the default.
+    const bool inplace = batched && getenv("DQ_KLL_INPLACE") != nullptr;
     if (ncols > 1 && !batched && !getenv("DQ_KLL_SERIAL")) {
         const int nside = dq::ctx_side_streams(ctx, cstreams + 1, &fork_ev, join_ev);
         if (nside > 0) {
@@ -1042,7 +1211,7 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
         }
     }
     // dense level-0 streams go out while the host computes the (count-only) compaction schedules; batched: one launch
-    if (batched && !jobs.empty()) {
+    if (batched && !inplace && !jobs.empty()) {
         for (size_t j = 0; j < jobs.size(); ++j) {
             KColumnRun& r = run[job_col[j]];
             if (r.n <= 0) continue;
@@ -1122,6 +1291,10 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
         });
         uint8_t* gdev = nullptr;
         KL_HIP(ctx, buf.alloc((void**)&gdev, seg_bytes + tab_bytes + mm_bytes));
+        // level 0 in place: (first row, end row) per descriptor, filled for level 0 by kll_locate_kernel
+        unsigned long long* drows = nullptr;
+        if (inplace) KL_HIP(ctx, buf.alloc((void**)&drows, std::max<size_t>(nseg_all, 1) * 16));
+        std::vector<KllTail0Job> tail0;
         const uint64_t* dsegs = reinterpret_cast<const uint64_t*>(gdev);
         const KllColPtr* dtab = reinterpret_cast<const KllColPtr*>(gdev + seg_bytes);
         unsigned long long* dmm = reinterpret_cast<unsigned long long*>(gdev + seg_bytes + tab_bytes);
@@ -1147,7 +1320,14 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
             dgats[i] = reinterpret_cast<double*>(scratch + gat_off);
             for (size_t h = 0; h < nlev; ++h)
                 htab[h * ncols + i] = KllColPtr{h == 0 ? r.stream0 : dup + r.lbase[h], h + 1 < nlev ? dup + r.lbase[h + 1] : nullptr,
-                                                h == 0 ? dmm + 2 * i : nullptr, 0ull};
+                                                h == 0 ? dmm + 2 * i : nullptr, r.kc, r.doffs, r.ntiles, nrows};
+            const bool raw0 = r.stream0 == nullptr && r.n > 0;  // level 0 read in place
+            double* tail0_buf = nullptr;
+            if (raw0 && sc.levels[0].len > 0) {
+                KL_HIP(ctx, buf.alloc((void**)&tail0_buf, (size_t)sc.levels[0].len * 8));
+                tail0.push_back(KllTail0Job{dtab + i, (unsigned long long)sc.levels[0].pos,
+                                            (unsigned long long)sc.levels[0].len, tail0_buf});
+            }
             hmm[2 * i] = ~0ull;
             hmm[2 * i + 1] = 0ull;
             KllTail* htails = reinterpret_cast<KllTail*>(pin + r.pin_at);
@@ -1155,19 +1335,35 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
             unsigned long long at = 0;
             for (size_t h = 0; h < nlev; ++h) {
                 const KllLevel& l = sc.levels[h];
-                const double* src = (h == 0 ? r.stream0 : dup + r.lbase[h]) + l.pos;
+                const double* src = h == 0 ? (raw0 ? tail0_buf : r.stream0 + l.pos) : dup + r.lbase[h] + l.pos;
                 htails[h] = KllTail{(unsigned long long)(uintptr_t)src, (unsigned long long)l.len, at};
                 at += (unsigned long long)l.len;
             }
         }
         KL_HIP(ctx, hipMemcpyAsync(gdev, pin, seg_bytes + tab_bytes + mm_bytes, hipMemcpyHostToDevice, s));
+        if (inplace) {
+            // level 0's descriptors are the first NC * ncols groups (level-major): their row ranges, then the final
+            // level-0 buffers of the columns read in place
+            const size_t n0 = maxlev > 1 ? first[NC * ncols] : nseg_all;
+            if (n0)
+                hipLaunchKernelGGL(kll_locate_kernel, dim3((unsigned)((n0 + 255) / 256)), dim3(256), 0, s, dsegs, (int)n0,
+                                   dtab, drows);
+            if (!tail0.empty()) {
+                KllTail0Job* dt0 = nullptr;
+                KL_HIP(ctx, buf.alloc((void**)&dt0, tail0.size() * sizeof(KllTail0Job)));
+                KL_HIP(ctx, hipMemcpyAsync(dt0, tail0.data(), tail0.size() * sizeof(KllTail0Job), hipMemcpyHostToDevice, s));
+                hipLaunchKernelGGL(kll_tail0_kernel, dim3((unsigned)tail0.size()), dim3(256), 0, s, (const KllTail0Job*)dt0);
+            }
+            KL_HIP(ctx, hipGetLastError());
+        }
         for (size_t h = 0; h < maxlev; ++h)
             for (size_t c = 0; c < NC; ++c) {
                 size_t total = 0;
                 for (int i = 0; i < ncols; ++i) total += cnt[(h * NC + c) * ncols + i];
                 if (!total) continue;
-                if (launch_kll_compact((int)c, nullptr, dsegs + first[(h * NC + c) * ncols], (int)total, nullptr, nullptr, s,
-                                       dtab + h * ncols) != 0)
+                const size_t f = first[(h * NC + c) * ncols];
+                if (launch_kll_compact((int)c, nullptr, dsegs + f, (int)total, nullptr, nullptr, s, dtab + h * ncols,
+                                       h == 0 && inplace ? drows + 2 * f : nullptr) != 0)
                     return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
             }
         for (int i = 0; i < ncols; ++i) {

@@ -1160,6 +1160,36 @@ __device__ __forceinline__ uint32_t cmp_hits8(const double (&xd)[8], const uint6
     return h;
 }
 
+// The same count over the whole wave (wave-uniform): each compare is one v_cmp into a lane mask whose popcount the
+// scalar unit adds, instead of a compare plus a per-lane add with carry for every value.
+template <bool F>
+__device__ __forceinline__ uint32_t cmp_hits8_wave(const double (&xd)[8], const uint64_t (&xi)[8], int op, double y,
+                                                   int64_t yi) {
+    uint32_t h = 0;
+#define DQ_CMPW(expr) _Pragma("unroll") for (int k = 0; k < 8; ++k) h += (uint32_t)__popcll(__ballot(expr)); break;
+    if (F) {
+        switch (op) {
+            case DQ_P_EQ: DQ_CMPW(xd[k] == y)
+            case DQ_P_NE: DQ_CMPW(!(xd[k] == y))
+            case DQ_P_LT: DQ_CMPW(xd[k] < y)
+            case DQ_P_LE: DQ_CMPW(xd[k] <= y)
+            case DQ_P_GT: DQ_CMPW(!(xd[k] <= y))
+            default: DQ_CMPW(!(xd[k] < y))
+        }
+    } else {
+        switch (op) {
+            case DQ_P_EQ: DQ_CMPW((int64_t)xi[k] == yi)
+            case DQ_P_NE: DQ_CMPW((int64_t)xi[k] != yi)
+            case DQ_P_LT: DQ_CMPW((int64_t)xi[k] < yi)
+            case DQ_P_LE: DQ_CMPW((int64_t)xi[k] <= yi)
+            case DQ_P_GT: DQ_CMPW((int64_t)xi[k] > yi)
+            default: DQ_CMPW((int64_t)xi[k] >= yi)
+        }
+    }
+#undef DQ_CMPW
+    return h;
+}
+
 // XXH64 hashLong (seed 42) of a long (or of doubleToLongBits) up to the final multiply's high word (see hll_idx_rank);
 // returns that word: idx = g >> 23, rank field t = g << 9.
 __device__ __forceinline__ uint32_t xxh_long_ghi(uint64_t lv) {
@@ -1404,7 +1434,9 @@ __device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, cons
         double s1 = 0.0, s2 = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const double d = mul_raw(xd[k] - c0, one_if(row_mask(m, k)));
+            // xd holds 0.0 on masked rows: xd - c0 f is exactly the rounded deviation on valid rows and 0 on masked
+            // ones, one fma instead of a subtract and a multiply
+            const double d = __builtin_fma(-c0, one_if(row_mask(m, k)), xd[k]);
             s1 += d;
             s2 = __builtin_fma(d, d, s2);
         }
@@ -1422,7 +1454,18 @@ __device__ __forceinline__ void heavy_col_rows(typename HAccOf<F>::type& a, cons
         }
         hmoments_merge(a.n, a.mean, a.m2, cnt, mb, m2b);
     }
-    if (FULL || hc.pred) a.pt += cmp_hits8<F>(xd, xi, hc.op, hc.y, hc.yi) - hc.zhit * (8u - cnt);
+    if (FULL) {
+        // the tile loop runs with every lane active: the wave's hits go to lane 0's partial (the lane partials are
+        // summed at the end); masked rows hold 0 and hit when `0 <op> c` does (zhit): taken off per wave
+        uint32_t w = cmp_hits8_wave<F>(xd, xi, hc.op, hc.y, hc.yi);
+        if (hc.zhit) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w -= (uint32_t)__popcll(__ballot(!((m >> k) & 1u)));
+        }
+        if ((threadIdx.x & 63) == 0) a.pt += w;
+    } else if (hc.pred) {
+        a.pt += cmp_hits8<F>(xd, xi, hc.op, hc.y, hc.yi) - hc.zhit * (8u - cnt);
+    }
     else if (c.pred_kind != FP_NONE) a.pt += fused_pred_count<F>(c, v, m);  // NaN constant / mixed kinds
     a.n += cnt;
     if (FULL || hc.hll) {

@@ -236,21 +236,26 @@ scan_strings_kernel(const StrSlot* __restrict__ slots, int nslots, int64_t nrows
         int64_t n = 0, mn = INT64_MAX, mx = INT64_MIN;
         int64_t dt[5] = {0, 0, 0, 0, 0};
         const int64_t stride = (int64_t)gridDim.x * kBlock;
-        // wave-uniform loop over groups of 64 consecutive rows (lane = row within the group)
-        for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < nrows; base += stride) {
-            const int64_t row = base + lane;
+        const int64_t base0 = (int64_t)blockIdx.x * kBlock + wave * 64;
+        auto row_on = [&](int64_t b) {  // validity (and `where`) of row b + lane
+            const int64_t row = b + lane;
             bool on = row < nrows;
             if (on) {
                 on = s.validity == nullptr || ((s.validity[row >> 6] >> (row & 63)) & 1ull);
                 if (s.where_t) on = on && ((s.where_t[row >> 6] >> (row & 63)) & 1ull);
             }
-            n += on ? 1 : 0;
-            if (str) {
+            return on;
+        };
+        // (r04: software-pipelining this loop — the next group's words and the group after's offsets in registers while
+        // the current group is hashed — made the C5 string pass 25 % slower, profiles/r04/c5_ab_r04g.txt)
+        if (str) {
+            for (int64_t base = base0; base < nrows; base += stride) {
+                const int64_t row = base + lane;
+                const bool on = row_on(base);
+                n += on ? 1 : 0;
                 const int64_t last = base + 64 < nrows ? base + 64 : nrows;
                 const int64_t b0 = s.offsets[base], b1 = s.offsets[last];
                 const int64_t a0 = b0 & ~(int64_t)3;
-                // staged bytes: [a0, b1 + 12) — le64_at reads up to 12 bytes past a string's end (the buffer has
-                // >= 16 readable bytes past the column's last string)
                 const int64_t nwords = (b1 + 12 - a0 + 3) >> 2;
                 if (nwords <= kStrStageWords) {
                     for (int64_t i = lane; i < nwords; i += 64) stage[wave][i] = load_word(s.data, a0 + 4 * i);
@@ -262,14 +267,16 @@ scan_strings_kernel(const StrSlot* __restrict__ slots, int nslots, int64_t nrows
                         string_row(s, reinterpret_cast<const uint8_t*>(&stage[wave][0]), o0, o1, want_hll, mn, mx, dt,
                                    regs);
                     }
-                    // the next group's staging writes after every lane's reads of this one (LDS keeps a wave's
-                    // accesses in order)
                     __builtin_amdgcn_wave_barrier();
                 } else if (on) {
                     string_row(s, s.data, s.offsets[row], s.offsets[row + 1], want_hll, mn, mx, dt, regs);
                 }
-            } else if (on && (s.flags & SF_DTYPE)) {
-                dt[numeric_class(s, row)] += 1;
+            }
+        } else {
+            for (int64_t b = base0; b < nrows; b += stride) {
+                const bool on = row_on(b);
+                n += on ? 1 : 0;
+                if (on && (s.flags & SF_DTYPE)) dt[numeric_class(s, b + lane)] += 1;
             }
         }
         // wave64 tree, then the 4 waves in a fixed order

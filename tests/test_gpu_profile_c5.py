@@ -178,3 +178,64 @@ def test_chunked_run_with_an_all_null_chunk_equals_the_whole_table():
             assert sum(b.count for b in g.get().buckets) == sum(b.count for b in w.get().buckets), a
         else:
             assert _close(g.get(), w.get()), (a, g.get(), w.get())
+
+
+def test_c5_chunked_shard_at_scale_against_oracle():
+    """The 2.5e8-row C5 shard bench.py times (two 1.25e8-row chunks, ChunkedTable) profiled by the full ColumnProfiler,
+    checked against the oracle at that size (it was checked only by the bench's property asserts).
+    The 10 numeric columns are regenerated row by row by the oracle's streamed suite (same counter-based generators
+    and validity): completeness and min / max exact, integral sums exact, fp64 sum / mean / stdDev within 1e-12 of the
+    exact values, approximateNumDistinctValues from bit-exact HLL registers, KLL bucket weights = non-NULL count. The
+    10 string columns: completeness exact and the HLL estimate from the oracle's XXH64 registers over the device bytes."""
+    import torch
+    import bench
+    import deequ_amd.native as N
+    from deequ_amd import engine
+    rows = 250_000_000
+    t, _ = bench.c5_shard(torch, N, engine.ctx(), torch.device("cuda", 0), rows)
+    assert len(t.chunks) == 2
+    prof = D.ColumnProfiler.profile(t)
+    assert prof.numRecords == rows
+    specs = []
+    for j, (name, kind) in enumerate(bench.C5_NUMERIC):
+        specs.append(dict(name=name, kind=kind, spark_type=O.T_DOUBLE if kind in (1, 2, 3, 6, 7) else O.T_LONG,
+                          seed=0xC5000000 + j, vseed=0xC5200000 + j, permille=50, hll=1))
+    cols, _ = O.generated_suite(specs, 0, rows)
+    for sp, o in zip(specs, cols):
+        p = prof.profiles[sp["name"]]
+        n = o["n"]
+        assert p.completeness == n / rows, sp["name"]
+        assert p.approximateNumDistinctValues == int(O.hll_count(o["words"])), sp["name"]
+        assert isinstance(p, D.NumericColumnProfile), sp["name"]
+        if sp["spark_type"] == O.T_LONG:
+            assert (p.minimum, p.maximum) == (float(o["imin"]), float(o["imax"])), sp["name"]
+            assert p.sum == float(o["isum"]), sp["name"]
+        else:
+            assert (p.minimum, p.maximum) == (o["dmin"], o["dmax"]), sp["name"]
+            if sp["kind"] == 1:  # dyadic values: every partial sum is exact
+                assert p.sum == o["ex_sum"], sp["name"]
+            else:
+                assert _close(p.sum, o["ex_sum"]), (sp["name"], p.sum, o["ex_sum"])
+        sigma = math.sqrt(o["ex_m2"] / n)
+        # the mean against max(|mean|, sigma), as the C2 bars (a zero-mean column has no relative scale of its own)
+        assert abs(p.mean - o["ex_mean"]) <= 1e-12 * max(abs(o["ex_mean"]), sigma), (sp["name"], p.mean, o["ex_mean"])
+        assert _close(p.stdDev, sigma), (sp["name"], p.stdDev, sigma)
+        assert sum(b.count for b in p.kll.buckets) == n, sp["name"]
+    # string columns: completeness and HLL registers over the device bytes, chunk by chunk
+    for name, _ in bench.C5_STRINGS:
+        regs = np.zeros(512, dtype=np.uint8)
+        valid_total = 0
+        for ch in t.chunks:
+            c = ch[name]
+            off = c.device["offsets"].cpu().numpy()
+            data = c.device["values"].cpu().numpy()
+            bits = c.device["validity"].cpu().numpy()
+            mask = np.unpackbits(bits, bitorder="little")[:c.length].astype(np.uint8)
+            valid_total += int(mask.sum())
+            O.lib().oracle_hll_strings(data.ctypes.data, off.ctypes.data, mask.ctypes.data, c.length, regs.ctypes.data)
+            del data, off
+        p = prof.profiles[name]
+        assert p.completeness == valid_total / rows, name
+        words = np.zeros(52, dtype=np.int64)
+        O.lib().oracle_hll_pack(regs.ctypes.data, words.ctypes.data)
+        assert p.approximateNumDistinctValues == int(O.hll_count([int(w) for w in words])), name

@@ -13,6 +13,7 @@ import sys
 
 def main():
     fn, pat = sys.argv[1], sys.argv[2]
+    min_depth = int(sys.argv[3]) if len(sys.argv) > 3 else 2
     lines = open(fn).read().splitlines()
     start = [i for i, l in enumerate(lines) if re.match(pat, l)][0]
     end = start + 1
@@ -30,13 +31,15 @@ def main():
             continue
         cur[1].append(s)
     for name, ins, hdr in blocks:
-        if "Depth=2" not in hdr and "Depth=3" not in hdr:
+        depth = int(hdr.split("Depth=")[1].split()[0]) if "Depth=" in hdr else 0
+        if depth < min_depth:
             continue
         c = collections.Counter(i.split()[0] for i in ins)
         valu = sum(n for k, n in c.items() if k.startswith("v_"))
         ds = sum(n for k, n in c.items() if k.startswith("ds_"))
         br = [i.split()[0] + " " + i.split()[-1] for i in ins if i.startswith(("s_cbranch", "s_branch"))]
-        print("%-12s %4d instr  valu %4d  ds %2d  %s" % (name, len(ins), valu, ds, " ".join(br)))
+        glob = sum(n for k, n in c.items() if k.startswith(("global_", "buffer_")))
+        print("%-12s d%d %4d instr  valu %4d  ds %2d  mem %2d  %s" % (name, depth, len(ins), valu, ds, glob, " ".join(br)))
 
 
 if __name__ == "__main__":
