@@ -261,12 +261,29 @@ __device__ __forceinline__ void kll_reg_sort(uint64_t (&v)[E]) {
 // and keeps the E smallest of them with a register network: min against the reversed B window (a bitonic half-cleaner:
 // the E smallest of two sorted windows) then a bitonic merge of those E. Equal keys are equal values, so which input a
 // tied key comes from does not matter. Out-of-range keys read as ~0 (no key is ~0: kll_key(NaN) = 0xfff8...).
+// A round whose merged pairs (2w keys = 2w / E threads) lie inside one wave synchronises that wave only: each wave reads
+// just its own part of the LDS image until the first block-wide round (DQ_KLL_BLOCK_ROUNDS=1 builds the block-barrier
+// form for A/B).
+#ifndef DQ_KLL_BLOCK_ROUNDS
+#define DQ_KLL_BLOCK_ROUNDS 0
+#endif
+__device__ __forceinline__ void kll_round_sync(bool wave_local) {
+    if (wave_local && !DQ_KLL_BLOCK_ROUNDS) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 template <int E>
 __device__ __forceinline__ void kll_merge_round(uint64_t* k, uint64_t (&v)[E], int t, int w) {
     auto at = [](int i) { return i + i / E; };
+    const bool wave_local = 2 * w <= 64 * E;
 #pragma unroll
     for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
-    __syncthreads();
+    kll_round_sync(wave_local);
     const int diag = E * (t & (2 * (w / E) - 1));  // offset inside the merged pair (w / E is a power of 2)
     const int A = (t * E) - diag, B = A + w;
     int lo = diag > w ? diag - w : 0, hi = diag < w ? diag : w;
@@ -292,7 +309,7 @@ __device__ __forceinline__ void kll_merge_round(uint64_t* k, uint64_t (&v)[E], i
                 bh = bi < bend ? k[at(bi)] : ~0ull;
             }
         }
-        __syncthreads();
+        kll_round_sync(wave_local);
         return;
     }
     uint64_t a[E], b[E];
@@ -317,7 +334,132 @@ __device__ __forceinline__ void kll_merge_round(uint64_t* k, uint64_t (&v)[E], i
                 v[r] = sw ? y : x;
                 v[r + stride] = sw ? x : y;
             }
+    kll_round_sync(wave_local);
+}
+
+// ---- levels above 0: merge the natural runs --------------------------------------------------------------------------
+// Level h >= 1's stream is the concatenation of level h-1's pick runs, each sorted (a compaction emits the alternate
+// items of its sorted range in order). A compaction range of such a level therefore holds a few maximal non-decreasing
+// runs (the level's odd leftover, the tail of one pick run, the head of the next) rather than L unsorted items. The
+// workgroup finds the descents (one ballot per wave, one barrier); with at most kKllMaxRuns runs it merges them in
+// <= 2 merge-path rounds (a sequential E-step merge per thread, since run lengths are arbitrary) instead of the register
+// sort + log2(T) rounds; a range with more descents takes the full sort. The sorted result is the same sequence either
+// way (sorting keys is unique), so the picks do not depend on which path ran.
+constexpr int kKllMaxRuns = 4;
+
+struct KllRunScratch {
+    int cnt[16];                 // per wave: descents in its keys (or 1 << 20: too many)
+    int pos[16][kKllMaxRuns];    // their positions, in order
+};
+
+// One round over up to two (A, B) pairs tiling [0, n): pair j merges [ps[j], pm[j]) with [pm[j], ps[j + 1]). Thread t
+// produces sorted positions [tE, tE + E) of the round's output into v.
+template <int E>
+__device__ __forceinline__ void kll_merge_pairs(const uint64_t* k, uint64_t (&v)[E], int o, int np, const int (&ps)[3],
+                                                const int (&pm)[2]) {
+    auto at = [](int i) { return i + i / E; };
+    int j = (np > 1 && o >= ps[1]) ? 1 : 0;
+    int ai, bi, aend, bend;
+    {
+        const int a0 = ps[j], b0 = pm[j];
+        aend = pm[j];
+        bend = ps[j + 1];
+        const int diag = o - a0, la = aend - a0, lb = bend - b0;
+        int lo = diag > lb ? diag - lb : 0, hi = diag < la ? diag : la;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (k[at(a0 + mid)] <= k[at(b0 + diag - 1 - mid)]) lo = mid + 1;
+            else hi = mid;
+        }
+        ai = a0 + lo;
+        bi = b0 + diag - lo;
+    }
+    uint64_t ah = ai < aend ? k[at(ai)] : ~0ull, bh = bi < bend ? k[at(bi)] : ~0ull;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        if (o + r == bend && j + 1 < np) {  // this thread's window runs into the next pair: merge it from its start
+            ++j;
+            ai = ps[j];
+            aend = pm[j];
+            bi = pm[j];
+            bend = ps[j + 1];
+            ah = ai < aend ? k[at(ai)] : ~0ull;
+            bh = bi < bend ? k[at(bi)] : ~0ull;
+        }
+        const bool takeA = bi >= bend || (ai < aend && ah <= bh);
+        if (takeA) {
+            v[r] = ah;
+            ++ai;
+            ah = ai < aend ? k[at(ai)] : ~0ull;
+        } else {
+            v[r] = bh;
+            ++bi;
+            bh = bi < bend ? k[at(bi)] : ~0ull;
+        }
+    }
+}
+
+// v = keys [tE, tE + E) of the range in stream order (n = T * E of them, padding ~0 at the end), vprev = key tE - 1.
+// Returns false (uniformly) when the range has more than kKllMaxRuns natural runs; otherwise v is sorted as by the
+// full merge sort. Ends with a barrier after its last LDS read of k.
+template <int T, int E>
+__device__ bool kll_natural_sort(uint64_t* k, uint64_t (&v)[E], int t, uint64_t vprev, KllRunScratch& rs) {
+    constexpr int n = T * E;
+    constexpr int NW = T / 64;
+    auto at = [](int i) { return i + i / E; };
+    const int lane = t & 63, wave = t >> 6;
+    int nd = 0, p = 0;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const bool d = r == 0 ? (t > 0 && v[0] < vprev) : v[r] < v[r - 1];
+        p = (d && nd == 0) ? t * E + r : p;
+        nd += d ? 1 : 0;
+    }
+    const uint64_t m = __ballot(nd > 0);
+    const bool many = __ballot(nd > 1) != 0 || __popcll(m) > kKllMaxRuns - 1;
+    if (!many && nd == 1) rs.pos[wave][__popcll(m & ((1ull << lane) - 1))] = p;
+    if (lane == 0) rs.cnt[wave] = many ? 1 << 20 : (int)__popcll(m);
     __syncthreads();
+    int total = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) total += rs.cnt[w];
+    if (total > kKllMaxRuns - 1) return false;
+    if (total == 0) return true;  // already sorted
+    static_assert(kKllMaxRuns == 4, "run starts below are three registers");
+    int s[kKllMaxRuns + 1] = {0, n, n, n, n};  // static indices only (no scratch)
+    int c = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+#pragma unroll
+        for (int i = 0; i < kKllMaxRuns - 1; ++i)
+            if (i < rs.cnt[w]) {
+                const int q = rs.pos[w][i];
+                s[1] = c == 0 ? q : s[1];
+                s[2] = c == 1 ? q : s[2];
+                s[3] = c == 2 ? q : s[3];
+                ++c;
+            }
+    const int R = total + 1;
+    // round 1: runs (0, 1) and (2, 3); round 2 (R >= 3): the two results
+#pragma unroll
+    for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
+    __syncthreads();
+    {
+        const int ps[3] = {0, s[2], n};
+        const int pm[2] = {s[1], R == 4 ? s[3] : n};
+        kll_merge_pairs<E>(k, v, t * E, R >= 3 ? 2 : 1, ps, pm);
+    }
+    __syncthreads();
+    if (R >= 3) {
+#pragma unroll
+        for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
+        __syncthreads();
+        const int ps[3] = {0, n, n};
+        const int pm[2] = {s[2], n};
+        kll_merge_pairs<E>(k, v, t * E, 1, ps, pm);
+        __syncthreads();
+    }
+    return true;
 }
 
 // Batched launches (one launch per level and class over every column of a dq_kll_sketch_columns call): a descriptor's
@@ -466,9 +608,10 @@ template <int T, int E>
 __global__ void __launch_bounds__(T)
 kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
                    unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols,
-                   const unsigned long long* __restrict__ rows) {
+                   const unsigned long long* __restrict__ rows, int runs) {
     constexpr int PAD = T * E;
     __shared__ uint64_t k[PAD + T];
+    __shared__ KllRunScratch rsc;
     __shared__ unsigned int wc[8 * (T / 64) + 1];
     const uint64_t sg = segs[blockIdx.x];
     kll_col_ptrs(cols, sg, src, dst, minmax);
@@ -476,6 +619,7 @@ kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ 
     const int len = (int)((sg >> 40) & 0x7FFF);
     const int t = threadIdx.x;
     uint64_t v[E];
+    bool sorted = false;
     if (rows && !src) {  // level 0 read in place: stage the range's values in dense order (uniform branch)
         auto at = [](int i) { return i + i / E; };
         kll_stage_rows<T>(cols[(sg >> 55) & 0xFF].raw, (int64_t)rows[2 * blockIdx.x], (int64_t)rows[2 * blockIdx.x + 1],
@@ -492,9 +636,16 @@ kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ 
             const int i = t * E + r;
             v[r] = i < len ? kll_key(in[i]) : ~0ull;
         }
+        if (runs) {  // a level above 0: its range is a few sorted runs (uniform branch)
+            const int ip = t * E - 1;
+            const uint64_t vprev = ip >= 0 && ip < len ? kll_key(in[ip]) : ~0ull;
+            sorted = kll_natural_sort<T, E>(k, v, t, vprev, rsc);
+        }
     }
-    kll_reg_sort<E>(v);
-    for (int w = E; w < PAD; w <<= 1) kll_merge_round<E>(k, v, t, w);
+    if (!sorted) {
+        kll_reg_sort<E>(v);
+        for (int w = E; w < PAD; w <<= 1) kll_merge_round<E>(k, v, t, w);
+    }
     // picks: sorted index i = t*E + r with i = offset + 2j, j < len/2
     const int half = len >> 1;
     const int off = (int)(sg >> 63);
@@ -518,10 +669,13 @@ kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ 
     }
 }
 
-// Compactions of L = P + rx items with P = T*E a power of two and 0 <= rx <= 64 (the schedule's L sit just above
+// Compactions of L = P + rx items with P = T*E a power of two and 0 <= rx <= kll_xm(T) (the schedule's L sit just above
 // powers of two: 2060, 1030, 516, 258, ...): the first P items take the exact-size merge sort above, the rx newest
-// ones are sorted by wave 0 (bitonic over lanes) and merged by rank — a main item moves up by the extras strictly
-// below it, an extra lands after the main items <= it — instead of padding the range to 1.5x in a larger class.
+// ones are sorted apart (wave 0's bitonic over lanes up to 64 of them, else a rank pass: 13.5 % of C5's level-0
+// compactions have 65-256 extras, which the padded 3072 class sorted at 2.3x the cost) and merged by rank — a main item
+// moves up by the extras strictly below it, an extra lands after the main items <= it.
+__host__ __device__ constexpr int kll_xm(int T) { return T < 256 ? T : 256; }
+
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
     const int lo = __shfl_xor((int)(uint32_t)x, m, 64), hi = __shfl_xor((int)(uint32_t)(x >> 32), m, 64);
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
@@ -531,13 +685,13 @@ template <int T, int E>
 __global__ void __launch_bounds__(T)
 kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
                      unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols,
-                     const unsigned long long* __restrict__ rows) {
+                     const unsigned long long* __restrict__ rows, int runs) {
     constexpr int P = T * E;
-    constexpr int XM = 64;
-    static_assert(T >= XM, "wave 0 sorts the extras");
+    constexpr int XM = kll_xm(T);
     __shared__ uint64_t k[P + T];
     __shared__ uint64_t ex[XM];
     __shared__ unsigned int wc[8 * (T / 64) + 1];
+    __shared__ KllRunScratch rsc;
     auto at = [](int i) { return i + i / E; };
     const uint64_t sg = segs[blockIdx.x];
     kll_col_ptrs(cols, sg, src, dst, minmax);
@@ -547,6 +701,7 @@ kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict_
     const int t = threadIdx.x;
     uint64_t v[E];
     uint64_t xk = ~0ull;
+    bool sorted = false;
     if (rows && !src) {  // level 0 read in place (see kll_compact_kernel)
         kll_stage_rows<T>(cols[(sg >> 55) & 0xFF].raw, (int64_t)rows[2 * blockIdx.x], (int64_t)rows[2 * blockIdx.x + 1],
                           wc, [&](unsigned int pos, uint64_t key) {
@@ -562,22 +717,38 @@ kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict_
 #pragma unroll
         for (int r = 0; r < E; ++r) v[r] = kll_key(in[t * E + r]);
         if (t < XM && t < rx) xk = kll_key(in[P + t]);
+        if (runs) sorted = kll_natural_sort<T, E>(k, v, t, t > 0 ? kll_key(in[t * E - 1]) : 0ull, rsc);
     }
-    kll_reg_sort<E>(v);
-    for (int w = E; w < P; w <<= 1) kll_merge_round<E>(k, v, t, w);
+    if (!sorted) {
+        kll_reg_sort<E>(v);
+        for (int w = E; w < P; w <<= 1) kll_merge_round<E>(k, v, t, w);
+    }
     // the sorted main array in LDS (the extras' ranks) and the extras sorted by wave 0
 #pragma unroll
     for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
-    if (t < XM) {
+    if (rx <= 64) {  // wave 0: bitonic over its lanes (rx is uniform)
+        if (t < 64) {
 #pragma unroll
-        for (int size = 2; size <= XM; size <<= 1)
+            for (int size = 2; size <= 64; size <<= 1)
 #pragma unroll
-            for (int stride = size >> 1; stride > 0; stride >>= 1) {
-                const uint64_t y = shfl_xor_u64(xk, stride);
-                const bool keep_min = ((t & stride) == 0) == ((t & size) == 0);
-                xk = keep_min ? (y < xk ? y : xk) : (y > xk ? y : xk);
+                for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                    const uint64_t y = shfl_xor_u64(xk, stride);
+                    const bool keep_min = ((t & stride) == 0) == ((t & size) == 0);
+                    xk = keep_min ? (y < xk ? y : xk) : (y > xk ? y : xk);
+                }
+            ex[t] = xk;
+        }
+    } else {  // up to XM extras: each one's rank among them (ties by arrival), one pass over LDS broadcasts
+        if (t < rx) ex[t] = xk;
+        __syncthreads();
+        int rk = 0;
+        if (t < rx)
+            for (int j = 0; j < rx; ++j) {
+                const uint64_t y = ex[j];
+                rk += (y < xk || (y == xk && j < t)) ? 1 : 0;
             }
-        ex[t] = xk;
+        __syncthreads();
+        if (t < rx) ex[rk] = xk;
     }
     __syncthreads();
     const int half = len >> 1;
@@ -635,7 +806,7 @@ constexpr int kKllAllClasses = kKllNumClasses + kKllNumXClasses;
 int kll_class_of_slow(int len) {
     for (int j = kKllNumXClasses - 1; j >= 0; --j) {
         const int P = kKllXClasses[j].t * kKllXClasses[j].e;
-        if (len >= P && len - P <= 64) return kKllNumClasses + j;
+        if (len >= P && len - P <= kll_xm(kKllXClasses[j].t)) return kKllNumClasses + j;
     }
     static const bool no12 = getenv("DQ_KLL_NO_E12") != nullptr;  // A/B: padded power-of-two classes only
     for (int c = 0; c < kKllNumClasses; ++c)
@@ -654,12 +825,14 @@ int kll_class_of(int len) {
 }
 
 int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nseg, double* dst,
-                       unsigned long long* minmax, hipStream_t s, const KllColPtr* cols = nullptr,
+                       unsigned long long* minmax, hipStream_t s, int level, const KllColPtr* cols = nullptr,
                        const unsigned long long* rows = nullptr) {
+    const bool no_runs = getenv("DQ_KLL_NO_RUNS") != nullptr;  // A/B and tests: the full sort at every level
+    const int runs = level > 0 && !no_runs ? 1 : 0;
     if (nseg <= 0) return 0;
     switch (cls) {
 #define KLL_CASE(C, T, E) \
-    case C: hipLaunchKernelGGL((kll_compact_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols, rows); break;
+    case C: hipLaunchKernelGGL((kll_compact_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols, rows, runs); break;
         KLL_CASE(0, 64, 4)
         KLL_CASE(1, 64, 8)
         KLL_CASE(2, 64, 12)
@@ -675,7 +848,7 @@ int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nse
 #undef KLL_CASE
 #define KLL_XCASE(C, T, E) \
     case C: \
-        hipLaunchKernelGGL((kll_compact_x_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols, rows); break;
+        hipLaunchKernelGGL((kll_compact_x_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols, rows, runs); break;
         KLL_XCASE(12, 64, 4)
         KLL_XCASE(13, 64, 8)
         KLL_XCASE(14, 128, 8)
@@ -1362,7 +1535,7 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
                 for (int i = 0; i < ncols; ++i) total += cnt[(h * NC + c) * ncols + i];
                 if (!total) continue;
                 const size_t f = first[(h * NC + c) * ncols];
-                if (launch_kll_compact((int)c, nullptr, dsegs + f, (int)total, nullptr, nullptr, s, dtab + h * ncols,
+                if (launch_kll_compact((int)c, nullptr, dsegs + f, (int)total, nullptr, nullptr, s, (int)h, dtab + h * ncols,
                                        h == 0 && inplace ? drows + 2 * f : nullptr) != 0)
                     return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
             }
@@ -1445,7 +1618,7 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
                 const size_t h = L.level;
                 const double* src = h == 0 ? r.stream0 : dup + r.lbase[h];
                 double* dst = dup + r.lbase[h + 1];
-                if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, cs) != 0)
+                if (launch_kll_compact(L.cls, src, dsegs + L.first, (int)L.count, dst, h == 0 ? dminmax : nullptr, cs, (int)h) != 0)
                     return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: compaction launch failed");
             }
             // final buffers: one gather, one read-back (completed by the single synchronisation below)

@@ -108,6 +108,26 @@ def test_sketch_specials_and_device_columns():
     check(rng.normal(size=n), None, device=True)
 
 
+@pytest.mark.parametrize("shape", ["ascending", "descending", "sawtooth", "few_values", "normal"])
+@pytest.mark.parametrize("size,f", [(2048, 0.64), (64, 0.64), (16, 0.5)])
+def test_sketch_run_shapes(shape, size, f, monkeypatch):
+    """Compactions above level 0 merge the natural runs of their range (kll.hip kll_natural_sort, <= 4 runs) and fall
+    back to the full sort beyond that: inputs whose level-0 ranges are already sorted / reversed / periodic / mostly
+    ties give every run count, against the oracle; the natural path equals the full sort (DQ_KLL_NO_RUNS)."""
+    n = 400_003
+    rng = np.random.default_rng(len(shape) * 1000 + size)
+    x = {"ascending": np.arange(n, dtype=np.float64),
+         "descending": -np.arange(n, dtype=np.float64),
+         "sawtooth": (np.arange(n) % 3001).astype(np.float64),
+         "few_values": rng.integers(0, 4, n).astype(np.float64),
+         "normal": rng.normal(size=n)}[shape]
+    got = check(x, None, size, f)
+    valid = rng.random(n) > 0.1
+    check(x, valid, size, f, device=True)
+    monkeypatch.setenv("DQ_KLL_NO_RUNS", "1")  # read at every compaction launch
+    assert got == check(x, None, size, f)
+
+
 def test_sketch_all_null_and_min_max_quirk():
     x = np.arange(100, dtype=np.float64)
     raw = check(x, np.zeros(100, dtype=bool))

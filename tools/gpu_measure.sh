@@ -15,6 +15,8 @@ for cfg in $CFGS; do
     c4) cmd="$R/tools/bench_configs.py --config c4 --steps 3" ;;
     c5) cmd="$R/tools/c5_shard.py 2.5e8 1" ;;
     s10) cmd="$R/tools/bench_configs.py --config suite10 --steps 3" ;;
+    c3) cmd="$R/tools/bench_configs.py --config c3 --steps 3" ;;
+    c2where) cmd="$R/tools/bench_configs.py --config c2where --steps 3" ;;
     *) echo "unknown $cfg"; exit 2 ;;
   esac
   for c in FETCH_SIZE WRITE_SIZE; do
