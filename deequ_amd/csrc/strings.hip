@@ -161,7 +161,7 @@ __device__ int classify_string(const uint8_t* data, int64_t o0, int64_t o1) {
 //   (STRING) otherwise; decimal -> BigDecimal.toString: scale 0 -> digits (INTEGRAL), otherwise
 //   plain with a point (FRACTIONAL) unless the adjusted exponent is < -6 (scientific, STRING);
 //   date / timestamp -> "yyyy-MM-dd..." (STRING).
-__device__ int numeric_class(const StrSlot& s, int64_t row) {
+__device__ __forceinline__ int numeric_class(const StrSlot& s, int64_t row) {
     switch (s.spark_type) {
         case DQ_TYPE_BOOLEAN: return DT_BOOLEAN;
         case DQ_TYPE_BYTE: case DQ_TYPE_SHORT: case DQ_TYPE_INT: case DQ_TYPE_LONG: return DT_INTEGRAL;
@@ -218,12 +218,213 @@ __device__ __forceinline__ void string_row(const StrSlot& s, const uint8_t* data
 // each lane's scattered byte / dword loads); ranges longer than this are read from HBM directly.
 constexpr int kStrStageWords = 512;
 
+// ---- the staged form: 32-bit byte positions into the wave's LDS words -----------------------------------------------
+// The same ops as above over a staged range (< 2 KiB, so positions are 32-bit: the int64 position arithmetic of the
+// HBM form doubles every add / compare), unaligned words assembled with one v_alignbyte each, the string's first word
+// held for the sign / space / boolean tests, and the 1-3 byte hash tail taken from one word. The stage holds >= 12
+// bytes past the range, so a word read past a string's end stays inside it.
+__device__ __forceinline__ uint32_t st_word(const uint32_t* st, int p) {  // bytes p .. p + 3
+    const int a = p >> 2;
+    return __builtin_amdgcn_alignbyte(st[a + 1], st[a], (uint32_t)(p & 3));
+}
+__device__ __forceinline__ uint64_t st_dword(const uint32_t* st, int p) {  // bytes p .. p + 7
+    const int a = p >> 2;
+    const uint32_t sh = (uint32_t)(p & 3), w0 = st[a], w1 = st[a + 1], w2 = st[a + 2];
+    return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+
+__device__ __forceinline__ int st_utf8_length(const uint32_t* st, int o0, int o1) {
+    int cont = 0;
+    for (int w = o0 & ~3; w < o1; w += 4) {
+        const uint32_t x = st[w >> 2];
+        uint32_t mask = 0xFFFFFFFFu;
+        if (w < o0) mask &= 0xFFFFFFFFu << (8 * (o0 - w));
+        if (w + 4 > o1) mask &= 0xFFFFFFFFu >> (8 * (w + 4 - o1));
+        cont += __popc(x & ~(x << 1) & 0x80808080u & mask);
+    }
+    return (o1 - o0) - cont;
+}
+
+__device__ __forceinline__ uint64_t st_xxh64(const uint32_t* st, int o0, int o1, uint64_t seed) {
+    const int len = o1 - o0;
+    int p = o0;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = seed + P64_1 + P64_2, v2 = seed + P64_2, v3 = seed, v4 = seed - P64_1;
+        const int limit = o1 - 32;
+        do {
+            v1 = xxh_round(v1, st_dword(st, p));
+            v2 = xxh_round(v2, st_dword(st, p + 8));
+            v3 = xxh_round(v3, st_dword(st, p + 16));
+            v4 = xxh_round(v4, st_dword(st, p + 24));
+            p += 32;
+        } while (p <= limit);
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = xxh_merge_round(h, v1);
+        h = xxh_merge_round(h, v2);
+        h = xxh_merge_round(h, v3);
+        h = xxh_merge_round(h, v4);
+    } else {
+        h = seed + P64_5;
+    }
+    h += (uint64_t)len;
+    while (p + 8 <= o1) {
+        h ^= xxh_round(0, st_dword(st, p));
+        h = rotl64(h, 27) * P64_1 + P64_4;
+        p += 8;
+    }
+    if (p + 4 <= o1) {
+        h ^= (uint64_t)st_word(st, p) * P64_1;
+        h = rotl64(h, 23) * P64_2 + P64_3;
+        p += 4;
+    }
+    if (p < o1) {  // 1-3 bytes, from one word
+        uint32_t w = st_word(st, p);
+        const int r = o1 - p;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (i < r) {
+                h ^= (uint64_t)(w & 0xFFu) * P64_5;
+                h = rotl64(h, 11) * P64_1;
+                w >>= 8;
+            }
+    }
+    return xxh_fmix(h);
+}
+
+__device__ __forceinline__ int st_skip_digits(const uint32_t* st, int i, int o1) {
+    while (i < o1) {
+        const int k = i & 3;
+        const uint32_t t = (st[i >> 2] >> (8 * k)) ^ 0x30303030u;
+        const uint32_t nd = (((t & 0x7F7F7F7Fu) + 0x76767676u) | t) & 0x80808080u;
+        const int nb = o1 - i < 4 - k ? o1 - i : 4 - k;
+        if (nd) {
+            const int pos = __builtin_ctz(nd) >> 3;
+            if (pos < nb) return i + pos;
+        }
+        i += nb;
+    }
+    return o1;
+}
+
+__device__ __forceinline__ int st_classify(const uint32_t* st, int o0, int o1) {
+    const int n = o1 - o0;
+    const uint32_t w = st_word(st, o0);  // the first 4 bytes (garbage past n)
+    const uint32_t c0 = w & 0xFFu;
+    const int sgn = (n > 0 && (c0 == '-' || c0 == '+')) ? 1 : 0;
+    const int sp = (n > sgn && ((w >> (8 * sgn)) & 0xFFu) == ' ') ? 1 : 0;
+    int i = st_skip_digits(st, o0 + sgn + sp, o1);
+    if (i == o1) return DT_INTEGRAL;  // includes "" and a lone sign
+    if (((st[i >> 2] >> (8 * (i & 3))) & 0xFFu) == '.') {
+        i = st_skip_digits(st, i + 1, o1);
+        if (i == o1) return DT_FRACTIONAL;
+    }
+    if (n == 4 && w == 0x65757274u) return DT_BOOLEAN;                                          // "true"
+    if (n == 5 && w == 0x736C6166u && ((st[(o0 + 4) >> 2] >> (8 * ((o0 + 4) & 3))) & 0xFFu) == 'e')  // "false"
+        return DT_BOOLEAN;
+    return DT_STRING;
+}
+
+// dt[c] += 1 with static indices only (a dynamic index into the register array would put it in scratch)
+__device__ __forceinline__ void dt_add(int64_t (&dt)[5], int c) {
+#pragma unroll
+    for (int k = 1; k < 5; ++k) dt[k] += c == k ? 1 : 0;
+}
+
+template <bool LEN, bool DT, bool HLL>
+__device__ __forceinline__ void st_string_row(const uint32_t* st, int o0, int o1, int64_t& mn, int64_t& mx,
+                                              int64_t (&dt)[5], uint32_t* regs) {
+    if constexpr (LEN) {
+        const int64_t len = st_utf8_length(st, o0, o1);
+        mn = len < mn ? len : mn;
+        mx = len > mx ? len : mx;
+    }
+    if constexpr (DT) dt_add(dt, st_classify(st, o0, o1));
+    if constexpr (HLL) {
+        const uint64_t x = st_xxh64(st, o0, o1, SPARK_HLL_SEED);
+        atomicMax(&regs[hll_index(x)], hll_rank(x));
+    }
+}
+
+// One slot's string rows, kStrR groups of 64 consecutive rows per wave and step (lane L takes rows base + 64 j + L): all
+// their offsets and validity words are loaded first, then the step's whole byte range is staged in the wave's LDS words
+// by buffer loads issued 8 per lane at a time (out-of-range words read as 0), so one step costs two dependent memory
+// round trips for 64 kStrR rows instead of two per 64. Ranges longer than the stage are read from HBM per lane.
+#ifndef DQ_STR_R
+#define DQ_STR_R 4
+#endif
+constexpr int kStrR = DQ_STR_R;
+
+template <bool LEN, bool DT, bool HLL>
+__device__ __forceinline__ void string_groups(const uint8_t* __restrict__ data, const int32_t* __restrict__ offsets,
+                                              const uint64_t* __restrict__ validity, const uint64_t* __restrict__ where_t,
+                                              int64_t nrows, int64_t base0, int64_t stride, int lane, uint32_t* stage,
+                                              int64_t& n, int64_t& mn, int64_t& mx, int64_t (&dt)[5], uint32_t* regs) {
+    constexpr int G = 64 * kStrR;
+    for (int64_t base = base0; base < nrows; base += stride) {
+        const int64_t last = base + G < nrows ? base + G : nrows;
+        const int64_t b0 = offsets[base], b1 = offsets[last];
+        bool on[kStrR];
+        int32_t o[kStrR], e[kStrR];
+#pragma unroll
+        for (int j = 0; j < kStrR; ++j) {
+            const int64_t row = base + 64 * j + lane;
+            bool v = row < nrows;
+            if (v) {
+                v = validity == nullptr || ((validity[row >> 6] >> (row & 63)) & 1ull);
+                if (where_t) v = v && ((where_t[row >> 6] >> (row & 63)) & 1ull);
+            }
+            on[j] = v;
+            o[j] = row < nrows ? offsets[row] : 0;
+            e[j] = row < nrows ? offsets[row + 1] : 0;
+            n += v ? 1 : 0;
+        }
+        const int64_t a0 = b0 & ~(int64_t)3;
+        const int nwords = (int)((b1 + 12 - a0 + 3) >> 2);
+        if (nwords <= kStrR * kStrStageWords) {
+            const __amdgpu_buffer_rsrc_t r =
+                __builtin_amdgcn_make_buffer_rsrc((void*)(data + a0), (short)0, nwords * 4, 0x00020000);
+            for (int i0 = 0; i0 < nwords; i0 += 64 * 8) {
+                uint32_t w[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    w[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (i0 + 64 * u + lane) * 4, 0, 0);
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (i0 + 64 * u + lane < nwords) stage[i0 + 64 * u + lane] = w[u];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < kStrR; ++j)
+                if (on[j]) st_string_row<LEN, DT, HLL>(stage, (int)(o[j] - a0), (int)(e[j] - a0), mn, mx, dt, regs);
+            __builtin_amdgcn_wave_barrier();
+        } else {
+#pragma unroll
+            for (int j = 0; j < kStrR; ++j)
+                if (on[j]) {
+                    if constexpr (LEN) {
+                        const int64_t len = utf8_length(data, o[j], e[j]);
+                        mn = len < mn ? len : mn;
+                        mx = len > mx ? len : mx;
+                    }
+                    if constexpr (DT) dt_add(dt, classify_string(data, o[j], e[j]));
+                    if constexpr (HLL) {
+                        const uint64_t x = xxh64_utf8(data, o[j], e[j], SPARK_HLL_SEED);
+                        atomicMax(&regs[hll_index(x)], hll_rank(x));
+                    }
+                }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kBlock)
 scan_strings_kernel(const StrSlot* __restrict__ slots, int nslots, int64_t nrows, int gstride,
                     StrPartial* __restrict__ partials, uint8_t* __restrict__ hll_partials) {
     __shared__ uint32_t regs[kHllRegs];
     __shared__ StrPartial red[kBlock / 64];
-    __shared__ uint32_t stage[kBlock / 64][kStrStageWords];
+    __shared__ uint32_t stage[kBlock / 64][kStrR * kStrStageWords];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int si = 0; si < nslots; ++si) {
         const StrSlot s = slots[si];
@@ -249,34 +450,23 @@ scan_strings_kernel(const StrSlot* __restrict__ slots, int nslots, int64_t nrows
         // (r04: software-pipelining this loop — the next group's words and the group after's offsets in registers while
         // the current group is hashed — made the C5 string pass 25 % slower, profiles/r04/c5_ab_r04g.txt)
         if (str) {
-            for (int64_t base = base0; base < nrows; base += stride) {
-                const int64_t row = base + lane;
-                const bool on = row_on(base);
-                n += on ? 1 : 0;
-                const int64_t last = base + 64 < nrows ? base + 64 : nrows;
-                const int64_t b0 = s.offsets[base], b1 = s.offsets[last];
-                const int64_t a0 = b0 & ~(int64_t)3;
-                const int64_t nwords = (b1 + 12 - a0 + 3) >> 2;
-                if (nwords <= kStrStageWords) {
-                    for (int64_t i = lane; i < nwords; i += 64) stage[wave][i] = load_word(s.data, a0 + 4 * i);
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    if (on) {
-                        const int64_t o0 = s.offsets[row] - a0, o1 = s.offsets[row + 1] - a0;
-                        string_row(s, reinterpret_cast<const uint8_t*>(&stage[wave][0]), o0, o1, want_hll, mn, mx, dt,
-                                   regs);
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                } else if (on) {
-                    string_row(s, s.data, s.offsets[row], s.offsets[row + 1], want_hll, mn, mx, dt, regs);
-                }
+            const int fl = ((s.flags & SF_LEN) ? 1 : 0) | ((s.flags & SF_DTYPE) ? 2 : 0) | (want_hll ? 4 : 0);
+            const int64_t sbase0 = ((int64_t)blockIdx.x * (kBlock / 64) + wave) * (64 * kStrR);
+            const int64_t sstride = (int64_t)gridDim.x * kBlock * kStrR;
+            switch (fl) {  // the slot's ops as template flags: no per-row flag tests
+#define DQ_STR_CASE(F) \
+    case F: string_groups<(F & 1) != 0, (F & 2) != 0, (F & 4) != 0>(s.data, s.offsets, s.validity, s.where_t, nrows, \
+                                                                    sbase0, sstride, lane, stage[wave], n, mn, mx, dt, regs); \
+        break;
+                DQ_STR_CASE(0) DQ_STR_CASE(1) DQ_STR_CASE(2) DQ_STR_CASE(3)
+                DQ_STR_CASE(4) DQ_STR_CASE(5) DQ_STR_CASE(6) DQ_STR_CASE(7)
+#undef DQ_STR_CASE
             }
         } else {
             for (int64_t b = base0; b < nrows; b += stride) {
                 const bool on = row_on(b);
                 n += on ? 1 : 0;
-                if (on && (s.flags & SF_DTYPE)) dt[numeric_class(s, b + lane)] += 1;
+                if (on && (s.flags & SF_DTYPE)) dt_add(dt, numeric_class(s, b + lane));
             }
         }
         // wave64 tree, then the 4 waves in a fixed order
@@ -363,7 +553,7 @@ __global__ void finalize_strings_kernel(const StrOpMap* __restrict__ ops, int no
 // profiles/r03/strings_grid_ab_r03s.log).
 int string_scan_grid(int cus, int64_t nrows) {
     const int per_cu = getenv("DQ_STR_WG_PER_CU") ? std::max(1, atoi(getenv("DQ_STR_WG_PER_CU"))) : 4;
-    const int64_t want = (nrows + kBlock - 1) / kBlock;
+    const int64_t want = (nrows + (int64_t)kBlock * kStrR - 1) / ((int64_t)kBlock * kStrR);
     const int64_t cap = (int64_t)cus * per_cu;
     return (int)(want < 1 ? 1 : (want < cap ? want : cap));
 }

@@ -87,6 +87,7 @@ class QuantileNonSample:
             self.curNumOfCompactors = int(curNumOfCompactors)
             self.compactorActualSize = int(compactorActualSize)
             self.compactorTotalSize = int(compactorTotalSize)
+        self._np_levels = None  # the buffers as float64 arrays (read paths); dropped by every mutation
 
     def copy(self):
         return QuantileNonSample(self.sketchSize, self.shrinkingFactor, [c.copy() for c in self.compactors],
@@ -96,11 +97,13 @@ class QuantileNonSample:
         return _capacity(self.sketchSize, self.shrinkingFactor, height)
 
     def expand(self):
+        self._np_levels = None
         self.compactors.append(NonSampleCompactor())
         self.curNumOfCompactors = len(self.compactors)
         self.compactorTotalSize = self.getCompactorCapacityCount()
 
     def reconstruct(self, sketchSize, shrinkingFactor, data):
+        self._np_levels = None
         self.sketchSize, self.shrinkingFactor = int(sketchSize), float(shrinkingFactor)
         self.compactors = [NonSampleCompactor(buffer=list(d)) for d in data]
         self.curNumOfCompactors = len(data)
@@ -112,12 +115,14 @@ class QuantileNonSample:
 
     def update(self, item):
         """QuantileNonSample.update (host-side restatement; the GPU runs this loop for real data)."""
+        self._np_levels = None
         self.compactors[0].buffer.append(float(item))
         self.compactorActualSize += 1
         if self.compactorActualSize > self.compactorTotalSize:
             self.condense()
 
     def condense(self):
+        self._np_levels = None
         for height in range(len(self.compactors)):
             if len(self.compactors[height].buffer) >= self.capacity(height):
                 if height + 1 >= self.curNumOfCompactors:
@@ -147,10 +152,16 @@ class QuantileNonSample:
             out.extend((v, w) for v in c.buffer)
         return out
 
+    def _levels(self):
+        import numpy as np
+        if self._np_levels is None:
+            self._np_levels = [np.asarray(c.buffer, dtype=np.float64) for c in self.compactors]
+        return self._np_levels
+
     def _output_arrays(self):
         import numpy as np
-        items = np.concatenate([np.asarray(c.buffer, dtype=np.float64)
-                                for c in self.compactors[:self.curNumOfCompactors]] or [np.zeros(0)])
+        lv = self._levels()
+        items = np.concatenate(lv[:self.curNumOfCompactors] or [np.zeros(0)])
         weights = np.concatenate([np.full(len(c.buffer), 1 << i, dtype=np.int64)
                                   for i, c in enumerate(self.compactors[:self.curNumOfCompactors])] or
                                  [np.zeros(0, dtype=np.int64)])
@@ -204,16 +215,18 @@ class QuantileNonSample:
         order = np.argsort(key, kind="stable")
         ts, c = t[order], np.cumsum(w[order])
         total = int(c[-1])
-        res = [float(ts[0])] * (q - 1)
-        i = 0
-        for curq in range(1, q):
-            if i >= n:
-                break
-            thresh = curq * total // q
-            if thresh > 0:
-                i = max(i, int(np.searchsorted(c, thresh, side="left")) + 1)
-            res[curq - 1] = float(ts[min(i, n - 1)])
-        return res
+        if q < 2:
+            return []
+        # the walk, vectorised: i_k = max(i_{k-1}, searchsorted(c, thresh_k) + 1) for thresh_k > 0 (the thresholds
+        # rise, so a running maximum); entries whose walk has already passed the last item keep ts[0]
+        curq = np.arange(1, q, dtype=np.int64)
+        thresh = (curq * total) // q if total < (1 << 62) // max(q, 1) else \
+            np.array([k * total // q for k in range(1, q)], dtype=object).astype(np.int64)
+        step = np.where(thresh > 0, np.searchsorted(c, thresh, side="left") + 1, 0)
+        i = np.maximum.accumulate(step)
+        prev = np.concatenate([[0], i[:-1]])
+        res = np.where(prev < n, ts[np.minimum(i, n - 1)], ts[0])
+        return [float(x) for x in res]
 
     def getCompactorItemsCount(self):
         return sum(len(c.buffer) for c in self.compactors[:self.curNumOfCompactors])
@@ -234,14 +247,18 @@ class QuantileNonSample:
     def deserialize(data, off=0):
         size, f, cur, actual, total, ncomp = struct.unpack_from(">idiiii", data, off)
         off += 28
-        comps = []
+        import numpy as np
+        comps, levels = [], []
         for _ in range(ncomp):
             nc, o, ln = struct.unpack_from(">iii", data, off)
             off += 12
-            buf = list(struct.unpack_from(">%dd" % ln, data, off))
+            arr = np.frombuffer(data, dtype=">f8", count=ln, offset=off).astype(np.float64)
             off += 8 * ln
-            comps.append(NonSampleCompactor(nc, o, buf))
-        return QuantileNonSample(size, f, comps, cur, actual, total)
+            comps.append(NonSampleCompactor(nc, o, arr.tolist()))
+            levels.append(arr)
+        q = QuantileNonSample(size, f, comps, cur, actual, total)
+        q._np_levels = levels
+        return q
 
 
 def _java_min(a, b):
@@ -260,20 +277,47 @@ def _java_max(a, b):
 class KLLState:
     """A/KLLSketch.scala:32-67."""
 
-    def __init__(self, qSketch, globalMax, globalMin):
-        self.qSketch, self.globalMax, self.globalMin = qSketch, float(globalMax), float(globalMin)
+    def __init__(self, qSketch, globalMax, globalMin, raw=None):
+        self._q, self.globalMax, self.globalMin = qSketch, float(globalMax), float(globalMin)
+        self._raw = raw  # the serialized state this one was read from (the sketch is parsed on first use)
+
+    @property
+    def qSketch(self):
+        if self._q is None:
+            self._q = QuantileNonSample.deserialize(self._raw, 16)
+        return self._q
+
+    @qSketch.setter
+    def qSketch(self, q):
+        self._q, self._raw = q, None
 
     def sum(self, other):
+        """KLLState.sum (A/KLLSketch.scala:49-54) through the library's merge (dq_kll_merge_states): the same
+        QuantileNonSample.merge + condense as `self.qSketch.merge(other.qSketch)` below, without the Python list work
+        (13 columns x chunk merges sat between the C5 profiler's passes)."""
+        from .native import kll_merge_states
+        return KLLState.fromBytes(kll_merge_states(self.toBytes(), other.toBytes()))
+
+    def sum_restated(self, other):
+        """KLLState.sum over the Python QuantileNonSample (the library's merge is checked against it)."""
         return KLLState(self.qSketch.merge(other.qSketch), _java_max(self.globalMax, other.globalMax),
                         _java_min(self.globalMin, other.globalMin))
 
     @staticmethod
     def fromBytes(data):
         mn, mx = struct.unpack_from(">dd", data, 0)
-        return KLLState(QuantileNonSample.deserialize(data, 16), mx, mn)
+        off = 16 + 28  # the layout is checked now (headers only), as an eager parse would
+        ncomp = struct.unpack_from(">i", data, 40)[0]
+        for _ in range(ncomp):
+            off += 12 + 8 * struct.unpack_from(">i", data, off + 8)[0]
+        if off > len(data):
+            raise struct.error("KLLState bytes truncated")
+        return KLLState(None, mx, mn, raw=bytes(data))
 
     def toBytes(self):
         """StatefulKLLSketch.toBytes layout (C/StatefulKLLSketch.scala:86-92): min, max, sketch."""
+        if self._q is None:
+            return self._raw
         return struct.pack(">dd", self.globalMin, self.globalMax) + self.qSketch.serialize()
 
     def __eq__(self, other):
@@ -317,15 +361,18 @@ class BucketValue:
 class BucketDistribution:
     """M/metrics/KLLMetric.scala:26-96."""
 
-    def __init__(self, buckets, parameters, data):
+    def __init__(self, buckets, parameters, data, _levels=None):
         self.buckets, self.parameters, self.data = list(buckets), [float(p) for p in parameters], \
             [list(d) for d in data]
+        self._levels = _levels  # `data` as float64 arrays when the sketch had them
 
     def computePercentiles(self):
         # parameters = (shrinkingFactor, sketchSize) but are read back as (sketchSize, shrinkingFactor); the
         # quantiles depend only on `data`, so the swap (kept from the reference) is harmless.
         q = QuantileNonSample(int(self.parameters[0]), self.parameters[1])
         q.reconstruct(int(self.parameters[0]), self.parameters[1], self.data)
+        if self._levels is not None and len(self._levels) == len(self.data):
+            q._np_levels = self._levels
         return q.quantiles(100)
 
     def __getitem__(self, key):
@@ -397,4 +444,5 @@ def bucket_distribution(state, numberOfBuckets):
         else:
             cnt = int(ex_high[i]) - int(ex_low[i])
         buckets.append(BucketValue(lows[i], highs[i], cnt))
-    return BucketDistribution(buckets, [sk.shrinkingFactor, float(sk.sketchSize)], sk.getCompactorItems())
+    return BucketDistribution(buckets, [sk.shrinkingFactor, float(sk.sketchSize)], sk.getCompactorItems(),
+                              _levels=list(sk._levels()))

@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts", "dq_synth_strings",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
     "dq_scan_streamed", "dq_scan_kernel_launches", "dq_freq_path_count", "dq_kll_sketch_columns",
+    "dq_kll_merge_states",
 )
 
 
@@ -193,6 +194,7 @@ def load_library(path=None):
                                         c_int64]),
             "dq_kll_sketch_columns": (c_int64, [c_void_p, c_void_p, ctypes.c_int32, c_int64, ctypes.c_int32,
                                                 ctypes.c_double, c_void_p, c_int64, c_void_p]),
+            "dq_kll_merge_states": (c_int64, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64]),
             "dq_cast_column": (c_int, [c_void_p, c_void_p, c_int64, ctypes.c_int32, c_void_p, c_void_p]),
             "dq_synth_column": (c_int, [c_void_p, ctypes.c_int32, ctypes.c_uint64, c_int64, c_int64, c_void_p]),
             "dq_synth_freq_keys": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p]),
@@ -228,6 +230,20 @@ def hll_count(words):
     lib = load_library()
     arr = (ctypes.c_int64 * HLL_NUM_WORDS)(*[int(np.int64(np.uint64(w & 0xFFFFFFFFFFFFFFFF))) for w in words])
     return lib.dq_hll_count(arr)
+
+
+def kll_merge_states(a, b):
+    """dq_kll_merge_states: KLLState.sum of two serialized KLLStates (host-side, C-ABI)."""
+    lib = load_library()
+    cap = len(a) + len(b) + 64
+    while True:
+        out = ctypes.create_string_buffer(cap)
+        n = lib.dq_kll_merge_states(a, len(a), b, len(b), out, cap)
+        if n < 0:
+            raise NativeError(int(n), "dq_kll_merge_states: malformed KLLState bytes")
+        if n <= cap:
+            return out.raw[:n]
+        cap = int(n)
 
 
 def spark_hash64(spark_type, value):

@@ -392,6 +392,13 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
 int64_t dq_kll_sketch_columns(dq_ctx* ctx, const dq_column* columns, int32_t ncols, int64_t nrows, int32_t sketch_size,
                               double shrinking_factor, uint8_t* state_out, int64_t capacity, int64_t* sizes);
 
+/* KLLState.sum of two serialized KLLState byte strings (A/KLLSketch.scala:49-54: QuantileNonSample.merge,
+ * A/QuantileNonSample.scala:218-234, then condense until the sketch fits; java max / min of the extremes) — the
+ * partition sketches of KLLRunner's treeReduce (R/KLLRunner.scala:104-112) and the row chunks of a chunked table.
+ * Host only (no context, no device). Writes the merged state to `out` when it fits in `capacity` and returns its
+ * length, or DQ_ERR_INVALID_ARGUMENT for malformed input. */
+int64_t dq_kll_merge_states(const uint8_t* a, int64_t na, const uint8_t* b, int64_t nb, uint8_t* out, int64_t capacity);
+
 /* ColumnProfiler.castColumn (M/profiles/ColumnProfiler.scala:346-355): Spark 2.2 Cast of a column to LONG or
  * DOUBLE. STRING sources: UTF8String.toLong (no trimming, optional sign, digits, optional '.' + digits truncated,
  * overflow NULL) / java.lang.Double.parseDouble (correctly rounded); strings that do not parse become NULL.

@@ -75,6 +75,25 @@ def test_merge_conserves_weight_and_capacity():
     assert KLLState.fromBytes(O.kll_state_bytes(a, 128, 0.64)) == sa
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_library_merge_equals_the_restated_merge(seed):
+    """KLLState.sum goes through the library (dq_kll_merge_states, host only): byte-equal to the Python
+    QuantileNonSample.merge + condense restatement over sketches of unequal depth, NaN / +-0.0 / ties and small
+    sketch sizes (many condense rounds), in both argument orders."""
+    rng = np.random.default_rng(seed)
+    size, f = [(2048, 0.64), (64, 0.64), (16, 0.5), (128, 0.9)][seed % 4]
+    pool = np.concatenate([rng.normal(0, 10, 40), [0.0, -0.0, np.nan, np.inf, -np.inf, 1.5, 1.5]])
+    na, nb = [(50_000, 3_000), (0, 7), (20_000, 20_000), (1, 1)][seed // 2 % 4]
+    a = rng.choice(pool, na) if seed % 3 else rng.normal(size=na)
+    b = rng.choice(pool, nb)
+    sa = KLLState.fromBytes(O.kll_state_bytes(a, size, f))
+    sb = KLLState.fromBytes(O.kll_state_bytes(b, size, f))
+    for x, y in ((sa, sb), (sb, sa)):
+        got = x.sum(y).toBytes()
+        exp = KLLState.fromBytes(x.toBytes()).sum_restated(KLLState.fromBytes(y.toBytes())).toBytes()
+        assert got == exp
+
+
 def test_quantiles_rank_error_is_small():
     rng = np.random.default_rng(12)
     v = rng.random(200000)
