@@ -347,9 +347,10 @@ __device__ __forceinline__ void kll_merge_round(uint64_t* k, uint64_t (&v)[E], i
 // way (sorting keys is unique), so the picks do not depend on which path ran.
 constexpr int kKllMaxRuns = 4;
 
+template <int NW>
 struct KllRunScratch {
-    int cnt[16];                 // per wave: descents in its keys (or 1 << 20: too many)
-    int pos[16][kKllMaxRuns];    // their positions, in order
+    int cnt[NW];                       // per wave: descents in its keys (or 1 << 20: too many)
+    int pos[NW][kKllMaxRuns - 1];      // their positions, in order
 };
 
 // One round over up to two (A, B) pairs tiling [0, n): pair j merges [ps[j], pm[j]) with [pm[j], ps[j + 1]). Thread t
@@ -403,7 +404,7 @@ __device__ __forceinline__ void kll_merge_pairs(const uint64_t* k, uint64_t (&v)
 // Returns false (uniformly) when the range has more than kKllMaxRuns natural runs; otherwise v is sorted as by the
 // full merge sort. Ends with a barrier after its last LDS read of k.
 template <int T, int E>
-__device__ bool kll_natural_sort(uint64_t* k, uint64_t (&v)[E], int t, uint64_t vprev, KllRunScratch& rs) {
+__device__ bool kll_natural_sort(uint64_t* k, uint64_t (&v)[E], int t, uint64_t vprev, KllRunScratch<T / 64>& rs) {
     constexpr int n = T * E;
     constexpr int NW = T / 64;
     auto at = [](int i) { return i + i / E; };
@@ -611,7 +612,7 @@ kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ 
                    const unsigned long long* __restrict__ rows, int runs) {
     constexpr int PAD = T * E;
     __shared__ uint64_t k[PAD + T];
-    __shared__ KllRunScratch rsc;
+    __shared__ KllRunScratch<T / 64> rsc;
     __shared__ unsigned int wc[8 * (T / 64) + 1];
     const uint64_t sg = segs[blockIdx.x];
     kll_col_ptrs(cols, sg, src, dst, minmax);
@@ -674,6 +675,8 @@ kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ 
 // ones are sorted apart (wave 0's bitonic over lanes up to 64 of them, else a rank pass: 13.5 % of C5's level-0
 // compactions have 65-256 extras, which the padded 3072 class sorted at 2.3x the cost) and merged by rank — a main item
 // moves up by the extras strictly below it, an extra lands after the main items <= it.
+// (224, which keeps the 2048-key class at 20.4 KB of LDS for 8 workgroups per CU instead of 7, measured the same:
+// profiles/r04/c5_kll_ab_r04ab.txt)
 __host__ __device__ constexpr int kll_xm(int T) { return T < 256 ? T : 256; }
 
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t x, int m) {
@@ -691,7 +694,7 @@ kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict_
     __shared__ uint64_t k[P + T];
     __shared__ uint64_t ex[XM];
     __shared__ unsigned int wc[8 * (T / 64) + 1];
-    __shared__ KllRunScratch rsc;
+    __shared__ KllRunScratch<T / 64> rsc;
     auto at = [](int i) { return i + i / E; };
     const uint64_t sg = segs[blockIdx.x];
     kll_col_ptrs(cols, sg, src, dst, minmax);
@@ -799,6 +802,8 @@ constexpr KllClass kKllClasses[] = {{64, 4},   {64, 8},   {64, 12},   {64, 16}, 
 constexpr int kKllNumClasses = sizeof(kKllClasses) / sizeof(kKllClasses[0]);
 
 // Exact-size classes of kll_compact_x_kernel: P = 256 << j (T, E), for L in [P, P + 64].
+// (the 2048-key class as 128 threads x 16 keys: 3 % less time in its own launches, but its 128 extras send twice as many
+// compactions to the padded 3072 class; no gain overall, profiles/r04/c5_kll_ab_r04ab.txt)
 constexpr KllClass kKllXClasses[] = {{64, 4}, {64, 8}, {128, 8}, {256, 8}, {512, 8}, {1024, 8}, {1024, 16}};
 constexpr int kKllNumXClasses = sizeof(kKllXClasses) / sizeof(kKllXClasses[0]);
 constexpr int kKllAllClasses = kKllNumClasses + kKllNumXClasses;
@@ -989,7 +994,10 @@ void put_be32(std::vector<uint8_t>& o, int32_t v) {
     for (int i = 3; i >= 0; --i) o.push_back((uint8_t)((uint32_t)v >> (8 * i)));
 }
 void put_be64(std::vector<uint8_t>& o, uint64_t v) {
-    for (int i = 7; i >= 0; --i) o.push_back((uint8_t)(v >> (8 * i)));
+    const uint64_t be = __builtin_bswap64(v);
+    const size_t at = o.size();
+    o.resize(at + 8);
+    memcpy(o.data() + at, &be, 8);
 }
 void put_f64(std::vector<uint8_t>& o, double d) {
     uint64_t u;
@@ -1023,16 +1031,17 @@ struct KState {
 
 uint32_t get_be32(const uint8_t* p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
 double get_f64(const uint8_t* p) {
-    uint64_t u = 0;
-    for (int i = 0; i < 8; ++i) u = (u << 8) | p[i];
+    uint64_t u;
+    memcpy(&u, p, 8);
+    u = __builtin_bswap64(u);
     double d;
     memcpy(&d, &u, 8);
     return d;
 }
 
-bool kll_parse(const std::vector<uint8_t>& b, KState& s) {
+bool kll_parse(const uint8_t* b, size_t nb, KState& s) {
     size_t at = 0;
-    auto need = [&](size_t n) { return at + n <= b.size(); };
+    auto need = [&](size_t n) { return at + n <= nb; };
     if (!need(16 + 28)) return false;
     s.gmin = get_f64(&b[0]);
     s.gmax = get_f64(&b[8]);
@@ -1062,6 +1071,9 @@ bool kll_parse(const std::vector<uint8_t>& b, KState& s) {
 
 void kll_serialize(const KState& s, std::vector<uint8_t>& o) {
     o.clear();
+    size_t need = 16 + 28;
+    for (const KComp& c : s.c) need += 12 + 8 * c.buf.size();
+    o.reserve(need);
     put_f64(o, s.gmin);
     put_f64(o, s.gmax);
     put_be32(o, s.sketch);
@@ -1098,6 +1110,41 @@ void kll_expand(KState& s) {
 // every item skipped (a comparison sort with the key computed per compare made the chunk merges of the C5 profiler
 // ~1 ms per column).
 void kll_sort_stable(const double* v, size_t n, std::vector<double>& out) {
+    // a buffer above level 0 is a concatenation of sorted pick runs: with few natural runs, stable pairwise merges
+    size_t runs = 1;
+    for (size_t i = 1; i < n && runs <= 16; ++i) runs += host_key(v[i]) < host_key(v[i - 1]) ? 1 : 0;
+    if (n > 1 && runs <= 16) {
+        std::vector<uint64_t> k(n), k2(n);
+        std::vector<uint32_t> ix(n), ix2(n);
+        std::vector<size_t> bnd{0};
+        for (size_t i = 0; i < n; ++i) {
+            k[i] = host_key(v[i]);
+            ix[i] = (uint32_t)i;
+            if (i && k[i] < k[i - 1]) bnd.push_back(i);
+        }
+        bnd.push_back(n);
+        while (bnd.size() > 2) {  // merge runs (0, 1), (2, 3), ...: ties from the earlier run first (stable)
+            std::vector<size_t> nb{0};
+            for (size_t r = 0; r + 1 < bnd.size(); r += 2) {
+                const size_t a0 = bnd[r], a1 = bnd[r + 1], b1 = r + 2 < bnd.size() ? bnd[r + 2] : a1;
+                size_t i = a0, j = a1, o = a0;
+                while (i < a1 && j < b1) {
+                    const bool takeB = k[j] < k[i];
+                    k2[o] = takeB ? k[j] : k[i];
+                    ix2[o++] = takeB ? ix[j++] : ix[i++];
+                }
+                for (; i < a1; ++i, ++o) { k2[o] = k[i]; ix2[o] = ix[i]; }
+                for (; j < b1; ++j, ++o) { k2[o] = k[j]; ix2[o] = ix[j]; }
+                nb.push_back(b1);
+            }
+            k.swap(k2);
+            ix.swap(ix2);
+            bnd.swap(nb);
+        }
+        out.resize(n);
+        for (size_t i = 0; i < n; ++i) out[i] = v[ix[i]];
+        return;
+    }
     std::vector<uint64_t> k(n), k2(n);
     std::vector<uint32_t> ix(n), ix2(n);
     for (size_t i = 0; i < n; ++i) {
@@ -1181,7 +1228,7 @@ int64_t dq_kll_merge_states(const uint8_t* a, int64_t na, const uint8_t* b, int6
                             int64_t capacity) {
     if (!a || !b || na < 0 || nb < 0 || capacity < 0 || (capacity > 0 && !out)) return DQ_ERR_INVALID_ARGUMENT;
     KState x, y;
-    if (!kll_parse(std::vector<uint8_t>(a, a + na), x) || !kll_parse(std::vector<uint8_t>(b, b + nb), y))
+    if (!kll_parse(a, (size_t)na, x) || !kll_parse(b, (size_t)nb, y))
         return DQ_ERR_INVALID_ARGUMENT;
     if (!kll_merge(x, y)) return DQ_ERR_INVALID_ARGUMENT;
     std::vector<uint8_t> o;
@@ -1226,10 +1273,10 @@ int64_t dq_kll_sketch(dq_ctx* ctx, const dq_column* column, int64_t nrows, int32
     for (int i = 0; i < nsub; ++i)
         if (rc[i] < 0) return dq::ctx_fail(ctx, (int)rc[i], "dq_kll_sketch: a device's partition failed");
     KState acc;
-    if (!kll_parse(parts[0], acc)) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: malformed partition state");
+    if (!kll_parse(parts[0].data(), parts[0].size(), acc)) return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: malformed partition state");
     for (int i = 1; i < nsub; ++i) {
         KState b;
-        if (!kll_parse(parts[i], b) || !kll_merge(acc, b))
+        if (!kll_parse(parts[i].data(), parts[i].size(), b) || !kll_merge(acc, b))
             return dq::ctx_fail(ctx, DQ_ERR_DEVICE, "dq_kll_sketch: partition merge failed");
     }
     std::vector<uint8_t> o;

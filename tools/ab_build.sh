@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B libraries: tools/ab_build.sh NAME [extra hipcc flags...] — libdq.so with freq.hip / strings.hip / scan.hip / kll.hip compiled with the
-# given -D flags (or from a git revision: FREQ_REV / STR_REV / SCAN_REV / KLL_REV), into tools/ab/NAME.so (select with DQ_LIBRARY).
+# given -D flags (or from a git revision: FREQ_REV / STR_REV / SCAN_REV / KLL_REV; CAST_SRC=path for cast.hip), into tools/ab/NAME.so (select with DQ_LIBRARY).
 set -eu
 cd "$(dirname "$0")/../deequ_amd/csrc"
 NAME=$1; shift
@@ -14,9 +14,10 @@ for f in dq_api.cpp host_algebra.cpp multi.cpp scan.hip predicate.hip synth.hip 
   if [ "$f" = strings.hip ] && [ -n "${STR_REV:-}" ]; then git show "$STR_REV:deequ_amd/csrc/strings.hip" > _ab_rev_strings.hip; src=_ab_rev_strings.hip; fi
   if [ "$f" = scan.hip ] && [ -n "${SCAN_REV:-}" ]; then git show "$SCAN_REV:deequ_amd/csrc/scan.hip" > _ab_rev_scan.hip; src=_ab_rev_scan.hip; fi
   if [ "$f" = kll.hip ] && [ -n "${KLL_REV:-}" ]; then git show "$KLL_REV:deequ_amd/csrc/kll.hip" > _ab_rev_kll.hip; src=_ab_rev_kll.hip; fi
-  case $f in freq.hip|strings.hip|scan.hip|kll.hip) /opt/rocm/bin/hipcc $FLAGS "$@" -I. -x hip -c $src -o $OUT/$NAME.build/$f.o ;; *) cp build/$f.o $OUT/$NAME.build/$f.o ;; esac
+  if [ "$f" = cast.hip ] && [ -n "${CAST_SRC:-}" ]; then cp "$CAST_SRC" _ab_src_cast.hip; src=_ab_src_cast.hip; fi
+  case $f in freq.hip|strings.hip|scan.hip|kll.hip|cast.hip) /opt/rocm/bin/hipcc $FLAGS "$@" -I. -x hip -c $src -o $OUT/$NAME.build/$f.o ;; *) cp build/$f.o $OUT/$NAME.build/$f.o ;; esac
   objs="$objs $OUT/$NAME.build/$f.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/$NAME.so $objs -ldl
-rm -rf $OUT/$NAME.build _ab_rev_freq.hip _ab_rev_strings.hip _ab_rev_scan.hip _ab_rev_kll.hip
+rm -rf $OUT/$NAME.build _ab_rev_freq.hip _ab_rev_strings.hip _ab_rev_scan.hip _ab_rev_kll.hip _ab_src_cast.hip
 echo built $OUT/$NAME.so
