@@ -119,8 +119,12 @@ class Analyzer:
     _fields = ()
 
     def _key(self):
-        return (type(self).__name__,) + tuple(
-            tuple(v) if isinstance(v, list) else v for v in (getattr(self, f) for f in self._fields))
+        k = self.__dict__.get("_cached_key")  # analyzers are values: fields are not changed after construction
+        if k is None:
+            k = (type(self).__name__,) + tuple(
+                tuple(v) if isinstance(v, list) else v for v in (getattr(self, f) for f in self._fields))
+            self.__dict__["_cached_key"] = k
+        return k
 
     def __eq__(self, other):
         return type(self) is type(other) and self._key() == other._key()

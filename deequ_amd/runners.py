@@ -9,6 +9,7 @@ from . import native as N
 from . import engine
 from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer,
                         FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies, STATE_ONLY)
+from .analyzers import merge as merge_states
 from .expr import compile_predicate
 from .metrics import DoubleMetric, Success, UnsupportedOnDevice
 from .table import ChunkedTable
@@ -421,7 +422,27 @@ class AnalysisRunner:
         pre = AnalyzerContext({a: a.toFailureMetric(Preconditions.findFirstFailing(schema, a.preconditions()))
                                for a in failed})
         agg = InMemoryStateProvider()
+        # KLL states fold through the library's merge (a ctypes call that releases the GIL): the columns' folds run on
+        # a thread pool, each in loader order as below; every other state folds in place
+        kll = [a for a in passed if isinstance(a, KLLSketch)] if len(stateLoaders) > 1 else []
+        if len(kll) < 2:
+            kll = []
+        if kll:
+            from concurrent.futures import ThreadPoolExecutor
+
+            def fold(a):
+                st = None
+                for loader in stateLoaders:
+                    st = merge_states(st, loader.load(a))
+                return st
+            with ThreadPoolExecutor(max_workers=min(8, len(kll))) as ex:
+                for a, st in zip(kll, ex.map(fold, kll)):
+                    if st is not None:
+                        agg.persist(a, st)
+        kll_set = set(kll)
         for a in passed:
+            if a in kll_set:
+                continue
             for loader in stateLoaders:
                 a.aggregateStateTo(agg, loader, agg)
         grouping = [a for a in passed if isinstance(a, GroupingAnalyzer)]

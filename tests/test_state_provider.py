@@ -142,6 +142,33 @@ def test_run_on_aggregated_states_from_two_persisted_partitions(tmp_path):
     assert merged.numRows == 5 and merged.as_dict() == {("a",): 3, ("b",): 1, ("c",): 1}
 
 
+def test_run_on_aggregated_states_folds_kll_sketches_in_loader_order():
+    """runOnAggregatedStates folds the KLL states of several columns on a thread pool (the library merge releases the
+    GIL): each column's metric equals the one of its states summed in loader order by the restated Python merge."""
+    import numpy as np
+    import oracle as O
+    from deequ_amd.kll import KLLState, bucket_distribution
+    from deequ_amd.runners import InMemoryStateProvider
+    rng = np.random.default_rng(4)
+    names = ["c%d" % i for i in range(5)]
+    loaders = [InMemoryStateProvider() for _ in range(3)]
+    raw = {}
+    for n in names:
+        for j, p in enumerate(loaders):
+            b = O.kll_state_bytes(rng.normal(j, 1 + j, 20_000 + 1000 * j), 256, 0.64)
+            raw[(n, j)] = b
+            p.persist(D.KLLSketch(n, D.KLLParameters(256, 0.64, 10)), KLLState.fromBytes(b))
+    schema = D.Table.from_pydict({n: [1.0] for n in names}).schema
+    for ncols in (5, 1):  # several KLL columns (the thread pool) and one (folded in place)
+        an = [D.KLLSketch(n, D.KLLParameters(256, 0.64, 10)) for n in names[:ncols]]
+        ctx = AnalysisRunner.runOnAggregatedStates(schema, Analysis(an + [D.Size()]), loaders)
+        for a, n in zip(an, names):
+            exp = KLLState.fromBytes(raw[(n, 0)])
+            for j in (1, 2):
+                exp = exp.sum_restated(KLLState.fromBytes(raw[(n, j)]))
+            assert ctx.metric(a).value.get() == bucket_distribution(exp, 10)
+
+
 def test_float_grouping_keys_merge_bitwise_across_persisted_states(tmp_path):
     """Frequencies of a double grouping column loaded from disk join the in-memory state with Spark's
     grouping equality (bitwise, NaN canonical, -0.0 != 0.0): repeated values merge, -0.0 and 0.0 stay
