@@ -85,24 +85,26 @@ struct KllCountJob {
     double* dense;  // the dense level-0 stream (write pass), null when the column has no non-NULL value
 };
 
-// NULL compaction, pass 1: non-NULL rows per 2048-row tile.
+// NULL compaction, pass 1: non-NULL rows per 2048-row tile, from the validity words (32 per tile): one lane per word
+// (a population count of the word's bits below nrows), a wave covers two tiles, a workgroup eight. (The per-row form —
+// every lane testing its rows' bits through 64-bit word loads — took 1.36 ms per 1.25e8-row chunk of 13 columns.)
+constexpr int kKllCountTilesPerBlock = kKllStageBlock / 32;
 __global__ void __launch_bounds__(kKllStageBlock)
-kll_count_kernel(const KllCountJob* __restrict__ jobs, int64_t nrows) {
+kll_count_kernel(const KllCountJob* __restrict__ jobs, int64_t nrows, int64_t ntiles) {
     const KllColumn c = jobs[blockIdx.y].c;
     unsigned int* __restrict__ tile_counts = jobs[blockIdx.y].counts;
-    __shared__ unsigned int red[kKllStageBlock / 64];
-    const int64_t t = blockIdx.x;
-    const int64_t r0 = t * kKllStageRows;
+    const int64_t t = (int64_t)blockIdx.x * kKllCountTilesPerBlock + (threadIdx.x >> 5);  // this lane's tile
+    const int64_t w = t * (kKllStageRows / 64) + (threadIdx.x & 31);                       // its validity word
+    const int64_t r0 = w * 64;
     unsigned int cnt = 0;
-    for (int64_t r = r0 + threadIdx.x; r < r0 + kKllStageRows && r < nrows; r += kKllStageBlock) cnt += kll_valid(c, r);
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned int s = 0;
-        for (int w = 0; w < kKllStageBlock / 64; ++w) s += red[w];
-        tile_counts[t] = s;
+    if (t < ntiles && r0 < nrows) {
+        const uint64_t bits = c.validity ? c.validity[w] : ~0ull;
+        const uint64_t in = nrows - r0 >= 64 ? ~0ull : ((1ull << (nrows - r0)) - 1ull);
+        cnt = (unsigned int)__popcll(bits & in);
     }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 32);
+    if ((threadIdx.x & 31) == 0 && t < ntiles) tile_counts[t] = cnt;
 }
 
 // NULL compaction, pass 2: non-NULL values as doubles, in row order, from each tile's offset.
@@ -1437,8 +1439,10 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
         KllCountJob* djobs = nullptr;
         KL_HIP(ctx, buf.alloc((void**)&djobs, sizeof(KllCountJob) * jobs.size()));
         KL_HIP(ctx, hipMemcpyAsync(djobs, jobs.data(), sizeof(KllCountJob) * jobs.size(), hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(kll_count_kernel, dim3((unsigned)ntiles, (unsigned)jobs.size()), dim3(kKllStageBlock), 0, s,
-                           (const KllCountJob*)djobs, nrows);
+        hipLaunchKernelGGL(kll_count_kernel,
+                           dim3((unsigned)((ntiles + kKllCountTilesPerBlock - 1) / kKllCountTilesPerBlock),
+                                (unsigned)jobs.size()),
+                           dim3(kKllStageBlock), 0, s, (const KllCountJob*)djobs, nrows, (int64_t)ntiles);
         hipLaunchKernelGGL(kll_scan_kernel, dim3(1, (unsigned)jobs.size()), dim3(1024), 0, s, (const KllCountJob*)djobs,
                            ntiles);
         KL_HIP(ctx, hipGetLastError());
