@@ -1984,7 +1984,7 @@ __global__ void __launch_bounds__(kBlock)
 scan_bits_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__ group, int ngroup, int64_t nrows,
                  int64_t ntiles, int gstride, SlotPartial* __restrict__ partials) {
     __shared__ SlotPartial red[kBlock / 64];
-    constexpr int kWordsPerTile = kTileRows / 64;
+    (void)ntiles;
     const int64_t nwords_total = (nrows + 63) >> 6;
     for (int gi = 0; gi < ngroup; ++gi) {
         const int s = group[gi];
@@ -1992,10 +1992,10 @@ scan_bits_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__
         const uint8_t* vb = reinterpret_cast<const uint8_t*>(sd.bits_valid);
         SlotPartial acc;
         slot_init(acc);
-        for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-            for (int i = threadIdx.x; i < kWordsPerTile; i += kBlock) {
-                const int64_t w = t * kWordsPerTile + i;
-                if (w >= nwords_total) break;
+        // every lane of the grid takes bitmap words in turn (a 2048-row tile is only 32 words: a tile per workgroup
+        // left 7 of its 8 waves idle)
+        for (int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x; w < nwords_total; w += (int64_t)gridDim.x * kBlock) {
+            {
                 const int64_t base = w << 6;
                 const int64_t nin = nrows - base;
                 const uint64_t range = nin >= 64 ? ~0ull : ((1ull << nin) - 1ull);
