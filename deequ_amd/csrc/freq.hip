@@ -1389,10 +1389,105 @@ spill_insert_kernel(const unsigned long long* __restrict__ spill, unsigned long 
 // publish their representatives, which small_check_kernel compares with the final (smallest) one. Exact: a fingerprint
 // collision anywhere raises `mismatch` and the build reruns with a new seed; a full table raises `overflow` and the
 // build takes the regular path.
+// One string key column (the Histograms of the profiler's third pass): a key of <= 15 bytes is held exactly as two
+// words (bytes 0-7, bytes 8-14 | length << 56), so a row is verified against its group's representative by comparing
+// words with the representative's copy in LDS instead of re-reading both rows' bytes from HBM (half the kernel's time).
+// A NULL row of a grouping is one marker, a NULL row of a Histogram the bytes of "NullValue" (string_null_is_value),
+// a longer key the "long" marker (verified through rows_equal).
+constexpr uint64_t kTupleNull = ~0ull, kTupleLong = ~0ull - 1;
+__device__ __forceinline__ bool short_key_tuple(const KeySpec& ks, int64_t r, uint64_t& b0, uint64_t& b1) {
+    const KeyCol& c = ks.cols[0];
+    if (!is_valid(c, r)) {
+        if (ks.string_null_is_value) {  // "NullValue"
+            b0 = 0x756C61566C6C754EULL;
+            b1 = 0x65ull | (9ull << 56);
+        } else {
+            b0 = b1 = kTupleNull;
+        }
+        return true;
+    }
+    const int32_t o0 = c.offsets[r], len = c.offsets[r + 1] - o0;
+    if (len > 15) {
+        b0 = b1 = kTupleLong;
+        return false;
+    }
+    const uint8_t* p = static_cast<const uint8_t*>(c.values) + o0;
+    const uint8_t* a = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(p - a);
+    const int ndw = (int)((sh + (uint32_t)len + 3) >> 2);  // only dwords holding bytes of [p, p + len): <= 5
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w[k] = k < ndw ? dw_at(a + 4 * k) : 0u;
+    uint64_t x0 = (uint64_t)__builtin_amdgcn_alignbyte(w[1], w[0], sh) |
+                  ((uint64_t)__builtin_amdgcn_alignbyte(w[2], w[1], sh) << 32);
+    uint64_t x1 = (uint64_t)__builtin_amdgcn_alignbyte(w[3], w[2], sh) |
+                  ((uint64_t)__builtin_amdgcn_alignbyte(w[4], w[3], sh) << 32);
+    if (len < 8) {
+        x0 &= len ? (~0ull >> (64 - 8 * len)) : 0ull;
+        x1 = 0;
+    } else {
+        x1 &= len > 8 ? (~0ull >> (64 - 8 * (len - 8))) : 0ull;
+    }
+    b0 = x0;
+    b1 = x1 | ((uint64_t)len << 56);
+    return true;
+}
+
+// XXH64 (seed) of a <= 15-byte key held as short_key_tuple words: the same value as dev_xxh_bytes over its bytes.
+__device__ __forceinline__ uint64_t xxh_short_words(uint64_t b0, uint64_t b1, uint64_t seed) {
+    const int len = (int)(b1 >> 56);
+    uint64_t w0 = b0, w1 = b1 & 0x00FFFFFFFFFFFFFFull;  // the key's bytes 0-7 and 8-14
+    uint64_t h = seed + P64_5 + (uint64_t)len;
+    int rest = len;
+    if (rest >= 8) {
+        h ^= xxh_round(0, w0);
+        h = rotl64(h, 27) * P64_1 + P64_4;
+        w0 = w1;
+        w1 = 0;
+        rest -= 8;
+    }
+    if (rest >= 4) {
+        h ^= (uint64_t)(uint32_t)w0 * P64_1;
+        h = rotl64(h, 23) * P64_2 + P64_3;
+        w0 >>= 32;
+        rest -= 4;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        if (i < rest) {
+            h ^= (w0 & 0xFFull) * P64_5;
+            h = rotl64(h, 11) * P64_1;
+            w0 >>= 8;
+        }
+    return xxh_fmix(h);
+}
+
+// row_key for one string key column that also returns the key's words (short_key_tuple): one set of loads per row.
+__device__ __forceinline__ bool row_key_str1(const KeySpec& ks, int64_t r, uint64_t& h, uint64_t& b0, uint64_t& b1,
+                                             bool& is_short) {
+    const KeyCol& c = ks.cols[0];
+    is_short = short_key_tuple(ks, r, b0, b1);
+    uint64_t ch;
+    bool any = true;
+    if (b0 == kTupleNull && b1 == kTupleNull) {  // NULL row of a grouping
+        ch = 0x6A09E667F3BCC909ULL;
+        any = false;
+    } else if (is_short) {  // valid, or "NullValue" for a Histogram's NULL row
+        ch = xxh_short_words(b0, b1, ks.seed);
+    } else {
+        const int32_t o0 = c.offsets[r], o1 = c.offsets[r + 1];
+        ch = dev_xxh_bytes(static_cast<const uint8_t*>(c.values) + o0, o1 - o0, ks.seed);
+    }
+    const uint64_t acc = mix64(ks.seed + P64_1 * 1ull + ch);
+    if (!any && !ks.include_nulls) return false;
+    h = (acc == kEmpty ? kEmpty - 1 : acc) & ks.fp_mask;
+    return true;
+}
+
 constexpr int kSmallTile = 4 * kBuildBlock;
 constexpr int kSmallGrid = 768;  // 3 workgroups per CU with the 2048-slot table
 
-template <int LS>  // slots of the workgroup's LDS table
+template <int LS, bool STR1 = false>  // slots of the workgroup's LDS table; STR1: one string key column
 __global__ void __launch_bounds__(kBuildBlock)
 small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
                    unsigned long long* __restrict__ wg_keys, unsigned long long* __restrict__ wg_reps,
@@ -1400,6 +1495,7 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
     __shared__ unsigned long long lkey[LS];
     __shared__ unsigned int lcnt[LS];
     __shared__ unsigned long long lrep[LS];
+    __shared__ unsigned long long lb0[STR1 ? LS : 1], lb1[STR1 ? LS : 1];  // the representative's key words (STR1)
     __shared__ unsigned long long red[kBuildBlock / 64];
     __shared__ unsigned int lovf, lfill;
     for (int i = threadIdx.x; i < LS; i += kBuildBlock) {
@@ -1417,16 +1513,24 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
     for (int64_t t0 = r0; t0 < r1; t0 += kSmallTile) {
         uint64_t h[4];
         bool take[4];
+        uint64_t kb0[STR1 ? 4 : 1], kb1[STR1 ? 4 : 1];
+        bool kshort[STR1 ? 4 : 1];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int64_t r = t0 + (int64_t)u * kBuildBlock + threadIdx.x;
             bool ng = false;
             h[u] = kEmpty;
-            take[u] = r < r1 && row_key(ks, r, h[u], ng) && !ng && h[u] != kEmpty;
+            if constexpr (STR1) {
+                take[u] = r < r1 && row_key_str1(ks, r, h[u], kb0[u], kb1[u], kshort[u]) && h[u] != kEmpty;
+            } else {
+                take[u] = r < r1 && row_key(ks, r, h[u], ng) && !ng && h[u] != kEmpty;
+            }
             taken += take[u] ? 1 : 0;
         }
+        unsigned int pu[4];  // each row's slot, kept for the verification
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
+            pu[u] = 0;
             if (!take[u]) continue;
             const unsigned long long row = (unsigned long long)(t0 + (int64_t)u * kBuildBlock + threadIdx.x);
             // past 3/4 full the table counts as overflowing (bounded probe chains when the guess was wrong)
@@ -1447,19 +1551,41 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
                 }
                 p = (p + 1) & (LS - 1);
             }
+            pu[u] = p;
             ok &= done;
         }
         if (!ok) lovf = 1;
         __syncthreads();
         if (lovf) break;  // a full table: the build goes elsewhere, stop reading rows (uniform: read after the barrier)
+        if constexpr (STR1) {  // each group's representative row (new in this tile) publishes its key words
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t r = t0 + (int64_t)u * kBuildBlock + threadIdx.x;
+                if (take[u] && lkey[pu[u]] == h[u] && lrep[pu[u]] == (unsigned long long)r) {
+                    lb0[pu[u]] = kb0[u];
+                    lb1[pu[u]] = kb1[u];
+                }
+            }
+            __syncthreads();
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (!take[u]) continue;
             const int64_t r = t0 + (int64_t)u * kBuildBlock + threadIdx.x;
-            unsigned int p = start(h[u]);
-            for (int probe = 0; probe < LS && lkey[p] != h[u]; ++probe) p = (p + 1) & (LS - 1);
+            const unsigned int p = pu[u];
             const unsigned long long rep = lrep[p];
-            if (lkey[p] != h[u] || (rep != (unsigned long long)r && !rows_equal(ks, r, (int64_t)rep))) ++bad;
+            if (lkey[p] != h[u]) {
+                ++bad;
+            } else if (rep != (unsigned long long)r) {
+                bool same;
+                if constexpr (STR1) {
+                    if (kshort[u] && lb1[p] != kTupleLong) same = lb0[p] == kb0[u] && lb1[p] == kb1[u];
+                    else same = rows_equal(ks, r, (int64_t)rep);
+                } else {
+                    same = rows_equal(ks, r, (int64_t)rep);
+                }
+                if (!same) ++bad;
+            }
         }
         __syncthreads();
     }
@@ -1981,7 +2107,12 @@ int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf
     if (!t->slots || !t->reps) return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
     t->cap = kRegion;
     t->bits = 0;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(kSmallGrid, (nrows + kSmallTile - 1) / kSmallTile));
+    // one string key column and a table the estimate leaves <= 5/8 full at 1024 slots (the profiler's Histograms, or the
+    // optimistic try with no estimate): 1024 slots + the representatives' key words, 36 KB of LDS (4 workgroups per CU)
+    const bool str1 = t->ks.ncols == 1 && t->ks.cols[0].spark_type == DQ_TYPE_STRING && est <= 640.0 &&
+                      !getenv("DQ_SMALL_NO_STR1");
+    const int grid = (int)std::max<int64_t>(
+        1, std::min<int64_t>(str1 ? kSmallGrid / 3 * 4 : kSmallGrid, (nrows + kSmallTile - 1) / kSmallTile));
     BuildItem* ditem = nullptr;
     unsigned long long *wk = nullptr, *wr = nullptr;
     FQ_HIP(ctx, buf.alloc((void**)&ditem, sizeof(BuildItem)));
@@ -1991,8 +2122,11 @@ int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf
     FQ_HIP(ctx, hipMemcpyAsync(ditem, &it, sizeof(it), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(region_init_kernel, dim3(1), dim3(kFreqBlock), 0, s, ditem, 1, t->slots, t->reps);
     ctx->freq_paths[DQ_FREQ_PATH_SMALL]++;
+    if (str1)
+        hipLaunchKernelGGL((small_build_kernel<1024, true>), dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots,
+                           t->reps, wk, wr, t->ctr, count_rows ? 1 : 0);
     // a 2048-slot workgroup table (40 KB of LDS: 3 workgroups per CU instead of 1) when the estimate leaves it <= 5/8 full
-    if (est <= 1280.0)
+    else if (est <= 1280.0)
         hipLaunchKernelGGL((small_build_kernel<2048>), dim3(grid), dim3(kBuildBlock), 0, s, t->ks, nrows, t->slots, t->reps,
                            wk, wr, t->ctr, count_rows ? 1 : 0);
     else

@@ -199,3 +199,41 @@ def test_optimistic_small_build_against_oracle(distinct):
     got = ft.to_dict()
     want = {("v%07d" % int(k),): int(c) for k, c in zip(okeys.view(np.int64), ocounts)}
     assert got == want
+
+
+@pytest.mark.parametrize("n", [200_000, 5_000_000])
+@pytest.mark.parametrize("include_nulls", [False, True])
+def test_small_build_one_string_column_short_and_long_keys(n, include_nulls, monkeypatch):
+    """The small build of one string key column holds keys of <= 15 bytes as two words (hashed from them and verified
+    against the representative's words in LDS); longer keys go through the byte path. Keys of every length 0-40, the
+    literal "NullValue" (a Histogram groups NULL rows with it) and NULLs, at the sized (2e5 rows) and the optimistic
+    (5e6 rows) small build: the groups equal a Python count and the byte-path build (DQ_SMALL_NO_STR1)."""
+    import collections
+    import pyarrow as pa
+    rng = np.random.default_rng(n + include_nulls)
+    base = ["", "a", "NullValue", "NullValu", "NullValuee", "x" * 15, "y" * 16, "z" * 40, "é" * 5, "é" * 8]
+    words = np.array(base + ["w%d-%s" % (i, "q" * int(i % 37)) for i in range(290)], dtype=object)
+    idx = rng.integers(0, len(words), n)
+    valid = rng.random(n) > 0.03
+    t = Table.from_arrow(pa.table({"s": pa.array(words[idx], type=pa.string(), mask=~valid)}))
+    t.to_device(0)
+    before = engine.ctx().freq_paths()
+    got = engine.frequencies(t, ["s"], include_nulls).to_dict()
+    paths = _paths_delta(before)
+    assert paths.get("small_optimistic" if n >= 1 << 22 else "small", 0) >= 1, paths
+    monkeypatch.setenv("DQ_SMALL_NO_STR1", "1")
+    ref = engine.frequencies(t, ["s"], include_nulls).to_dict()
+    assert got == ref
+    exp = collections.Counter()
+    for w, v in zip(words[idx], valid):
+        if v:
+            exp[(w,)] += 1
+        elif include_nulls:
+            exp[(None,)] += 1
+    assert sum(got.values()) == sum(exp.values())
+    if include_nulls:  # NULL rows and "NullValue" rows are one group (the Histogram's NullFieldReplacement)
+        nv = exp.pop((None,), 0) + exp.pop(("NullValue",), 0)
+        gnv = got.get((None,), 0) + got.get(("NullValue",), 0)
+        assert gnv == nv
+        got = {k: c for k, c in got.items() if k not in ((None,), ("NullValue",))}
+    assert got == dict(exp)
