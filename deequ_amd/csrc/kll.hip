@@ -339,6 +339,86 @@ __device__ __forceinline__ void kll_merge_round(uint64_t* k, uint64_t (&v)[E], i
     kll_round_sync(wave_local);
 }
 
+// ---- the first merge rounds across lanes (E = 8) ---------------------------------------------------------------------
+#ifndef DQ_KLL_DPP
+#define DQ_KLL_DPP 2  // 0: every round through LDS; 1: w = 8-32 across lanes; 2: also w = 64
+#endif
+// Merging runs of w = 8 * 2^M keys held by 2^M consecutive lanes needs no LDS: a bitonic merge whose first stage pairs
+// lane t's key r with lane t ^ (2^(M+1) - 1)'s key 7 - r (the mirror: the partner run read backwards), then halves
+// between lanes t ^ 2^s (same r), then the lane's 8 keys in registers. Partners are DPP lane swizzles (quad_perm /
+// row_half_mirror): M = 0, 1, 2 cover w = 8, 16, 32, three of the eight rounds of a 2048-key sort, without their LDS
+// writes, reads, merge-path searches and wave barriers. The result is the same sorted sequence.
+template <int CTRL>
+__device__ __forceinline__ uint64_t kll_dpp64(uint64_t x) {
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Every key of v against the same-index key of the partner lane (REV: the partner's keys reversed); the lower lane
+// of the pair keeps the minima.
+template <int CTRL, bool REV>
+__device__ __forceinline__ void kll_dpp_stage(uint64_t (&v)[8], bool lower) {
+    uint64_t b[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) b[r] = kll_dpp64<CTRL>(v[r]);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const uint64_t x = v[r], y = b[REV ? 7 - r : r];
+        v[r] = (x < y) == lower ? x : y;
+    }
+}
+
+__device__ __forceinline__ void kll_bitonic8(uint64_t (&v)[8]) {  // a bitonic 8 in registers, ascending
+#pragma unroll
+    for (int stride = 4; stride > 0; stride >>= 1)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            if ((r & stride) == 0) {
+                const uint64_t x = v[r], y = v[r + stride];
+                const bool sw = x > y;
+                v[r] = sw ? y : x;
+                v[r + stride] = sw ? x : y;
+            }
+}
+
+// Rounds w = 8, 16, 32 of the merge sort of kll_compact_*: thread t's 8 sorted keys in, the sorted 64-key run of its
+// 8-lane group out.
+__device__ __forceinline__ void kll_dpp_rounds(uint64_t (&v)[8], int t) {
+    constexpr int kXor1 = 0xB1, kXor2 = 0x4E, kRev4 = 0x1B, kRev8 = 0x141;  // quad_perm [1,0,3,2] / [2,3,0,1] / [3,2,1,0], row_half_mirror
+    kll_dpp_stage<kXor1, true>(v, (t & 1) == 0);  // w = 8: lanes t, t ^ 1
+    kll_bitonic8(v);
+    kll_dpp_stage<kRev4, true>(v, (t & 2) == 0);  // w = 16: lanes t, t ^ 3 mirrored, then t ^ 1
+    kll_dpp_stage<kXor1, false>(v, (t & 1) == 0);
+    kll_bitonic8(v);
+    kll_dpp_stage<kRev8, true>(v, (t & 4) == 0);  // w = 32: lanes t, 7 - t mirrored, then t ^ 2, t ^ 1
+    kll_dpp_stage<kXor2, false>(v, (t & 2) == 0);
+    kll_dpp_stage<kXor1, false>(v, (t & 1) == 0);
+    kll_bitonic8(v);
+#if DQ_KLL_DPP >= 2
+    constexpr int kRev16 = 0x140, kShl4 = 0x104, kShr4 = 0x114;  // row_mirror, row_shl:4, row_shr:4
+    kll_dpp_stage<kRev16, true>(v, (t & 8) == 0);  // w = 64: lanes t, 15 - t mirrored, then t ^ 4 (two row shifts),
+    {                                              // t ^ 2, t ^ 1
+        const bool lo4 = (t & 4) == 0;
+        uint64_t b[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint64_t up = kll_dpp64<kShl4>(v[r]), dn = kll_dpp64<kShr4>(v[r]);
+            b[r] = lo4 ? up : dn;
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const uint64_t x = v[r], y = b[r];
+            v[r] = (x < y) == lo4 ? x : y;
+        }
+    }
+    kll_dpp_stage<kXor2, false>(v, (t & 2) == 0);
+    kll_dpp_stage<kXor1, false>(v, (t & 1) == 0);
+    kll_bitonic8(v);
+#endif
+}
+
+
 // ---- levels above 0: merge the natural runs --------------------------------------------------------------------------
 // Level h >= 1's stream is the concatenation of level h-1's pick runs, each sorted (a compaction emits the alternate
 // items of its sorted range in order). A compaction range of such a level therefore holds a few maximal non-decreasing
@@ -647,7 +727,12 @@ kll_compact_kernel(const double* __restrict__ src, const uint64_t* __restrict__ 
     }
     if (!sorted) {
         kll_reg_sort<E>(v);
-        for (int w = E; w < PAD; w <<= 1) kll_merge_round<E>(k, v, t, w);
+        int w0 = E;
+        if constexpr (E == 8 && DQ_KLL_DPP) {
+            kll_dpp_rounds(v, t);
+            w0 = DQ_KLL_DPP >= 2 ? 128 : 64;
+        }
+        for (int w = w0; w < PAD; w <<= 1) kll_merge_round<E>(k, v, t, w);
     }
     // picks: sorted index i = t*E + r with i = offset + 2j, j < len/2
     const int half = len >> 1;
@@ -726,7 +811,12 @@ kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict_
     }
     if (!sorted) {
         kll_reg_sort<E>(v);
-        for (int w = E; w < P; w <<= 1) kll_merge_round<E>(k, v, t, w);
+        int w0 = E;
+        if constexpr (E == 8 && DQ_KLL_DPP) {
+            kll_dpp_rounds(v, t);
+            w0 = DQ_KLL_DPP >= 2 ? 128 : 64;
+        }
+        for (int w = w0; w < P; w <<= 1) kll_merge_round<E>(k, v, t, w);
     }
     // the sorted main array in LDS (the extras' ranks) and the extras sorted by wave 0
 #pragma unroll
@@ -955,10 +1045,13 @@ bool kll_schedule(int64_t n, int sketch_size, double f, KllSchedule& sc, std::ve
     sc.actual = 0;
     uint64_t full = 0;  // bit h: levels[h].len >= cap[h]
     int64_t rem = n;
+    events.reserve((size_t)(n / 900 + 64));
     while (rem > 0) {
         KllLevel& l0 = sc.levels[0];
+        // the updates until condense next compacts: past `total`, and (no level full) until level 0 fills — one jump
+        // per compaction (condense without a full level changes nothing but the counts)
         int64_t k = std::max<int64_t>(1, sc.total - sc.actual + 1);
-        if (sc.actual > sc.total && full == 0) k = std::max<int64_t>(k, cap[0] - l0.len);
+        if (full == 0) k = std::max<int64_t>(k, cap[0] - l0.len);
         k = std::min<int64_t>(rem, k);
         l0.len += k;
         l0.arrived += k;
@@ -1503,6 +1596,7 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
         KL_HIP(ctx, hipGetLastError());
         r.stream0 = dense;
     }
+    const auto t0b = std::chrono::steady_clock::now();
     {
         std::vector<int> ok(ncols, 1);
         kll_parallel(ncols, [&](int i) {
@@ -1742,9 +1836,9 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
         };
         size_t nseg = 0;
         for (const KColumnRun& r : run) nseg += r.events.size();
-        fprintf(stderr, "[dq_kll_sketch] columns=%d rows=%lld compactions=%zu counts+schedules %.2f ms, staging+launch %.2f ms, "
-                "device %.2f ms\n", ncols, (long long)nrows, nseg, ms(t0, t1), ms(t1, t2),
-                ms(t2, std::chrono::steady_clock::now()));
+        fprintf(stderr, "[dq_kll_sketch] columns=%d rows=%lld compactions=%zu counts %.2f ms, schedules %.2f ms, "
+                "staging+launch %.2f ms, device %.2f ms\n", ncols, (long long)nrows, nseg, ms(t0, t0b), ms(t0b, t1),
+                ms(t1, t2), ms(t2, std::chrono::steady_clock::now()));
     }
 
     for (int i = 0; i < ncols; ++i) {
