@@ -12,6 +12,7 @@ The metrics repository / result reuse and the JSON file output of the runner are
 """
 import json
 import math
+import os
 
 import numpy as np
 
@@ -136,6 +137,10 @@ class GenericColumnStatistics:
         return merged[column]
 
 
+# schema types whose pass-2 cast is the identity (integers -> LONG, FLOAT / DOUBLE -> DOUBLE: _cast_column)
+_IDENTITY_CAST_TYPES = ("ByteType", "ShortType", "IntegerType", "LongType", "FloatType", "DoubleType")
+
+
 def _cast_column(data, name, to_type):
     """ColumnProfiler.castColumn (:346-355) on the GPU. Casts that cannot change a value are skipped:
     integer -> LONG, FLOAT / DOUBLE -> DOUBLE (every pass-2 analyzer casts its input to double or sums
@@ -192,6 +197,14 @@ class ColumnProfiler:
                 first += [Completeness(name), ApproxCountDistinct(name), DataType(name)]
             else:
                 first += [Completeness(name), ApproxCountDistinct(name)]
+        # A column whose schema type is an integer or floating type is numeric whatever pass 1 finds, and its pass-2
+        # cast is the identity (_cast_column), so its pass-2 statistics are the same analyzers over the same values:
+        # they join pass 1's scan (one read of the column instead of two); its KLL sketch stays in pass 2.
+        early = [name for name in relevant
+                 if name not in predefinedTypes and schema[name] in _IDENTITY_CAST_TYPES and
+                 not os.environ.get("DQ_PROFILE_NO_EARLY_STATS")]
+        for name in early:
+            first += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
         res1 = passes.run(data, first + [Size()])
         generic = ColumnProfiler._extract_generic(relevant, schema, res1, predefinedTypes)
 
@@ -204,10 +217,14 @@ class ColumnProfiler:
                  for name in numeric}
         casted = _cast_table(passes, data, casts)
         second = []
+        early_set = set(early)
         for name in numeric:
-            second += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name),
-                       KLLSketch(name, kllParameters)]
+            if name not in early_set:
+                second += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
+            second += [KLLSketch(name, kllParameters)]
         res2 = passes.run(casted, second) if second else None
+        if early and res2 is not None:
+            res2 = res1 + res2
         stats = ColumnProfiler._extract_numeric(res2, numeric, kllParameters)
 
         # ---- pass 3 ------------------------------------------------------------------------------
