@@ -37,6 +37,11 @@ DQ_PARSE_FN double parse_bits_double(uint64_t u) {
     c.u = u;
     return c.d;
 }
+DQ_PARSE_FN uint64_t parse_double_bits(double d) {
+    union { uint64_t u; double d; } c;
+    c.d = d;
+    return c.u;
+}
 DQ_PARSE_FN uint64_t parse_umulhi64(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return __umul64hi(a, b);
@@ -232,7 +237,14 @@ DQ_PARSE_FN bool java_parse_double(const uint8_t* s, int n, double& out, bool& s
         if (!(i + 1 == n && (s[i] == 'd' || s[i] == 'D' || s[i] == 'f' || s[i] == 'F'))) return false;
     }
     uint64_t bits = 0;
-    if (w != 0) {
+    if (w != 0 && !trunc && w <= (1ull << 53) && exp_adj >= -22 && exp_adj <= 22) {
+        // Clinger's fast path: w and 10^|e| (<= 10^22 = 2^22 * 5^22, 5^22 < 2^53) are exact doubles, so one IEEE
+        // multiplication or division is the correctly rounded result, as Double.parseDouble's
+        double p = 1.0;
+        for (int k = 0; k < (exp_adj < 0 ? -exp_adj : exp_adj); ++k) p *= 10.0;
+        const double d = exp_adj < 0 ? (double)w / p : (double)w * p;
+        bits = parse_double_bits(d);
+    } else if (w != 0) {
         const AdjustedMantissa a = el_compute_float(exp_adj, w);
         if (trunc) {
             const AdjustedMantissa b = el_compute_float(exp_adj, w + 1);
