@@ -1035,53 +1035,71 @@ constexpr int kKllMaxLevels = 64;
 // compactions go to the caller's buffer (~145k entries for 1e8 items).
 bool kll_schedule(int64_t n, int sketch_size, double f, KllSchedule& sc, std::vector<uint64_t>* out) {
     std::vector<uint64_t>& events = *out;
-    events.clear();
     sc.segs = &events;
     int64_t cap[kKllMaxLevels + 1];
     for (int h = 0; h <= kKllMaxLevels; ++h) cap[h] = kll_capacity(sketch_size, f, h);
-    sc.levels.assign(1, KllLevel());
-    sc.levels.reserve(kKllMaxLevels + 1);
-    sc.total = cap[0];
-    sc.actual = 0;
-    uint64_t full = 0;  // bit h: levels[h].len >= cap[h]
+    // the levels as plain arrays in the loop (one compaction per iteration), copied into sc.levels at the end
+    int64_t len[kKllMaxLevels + 1] = {0}, pos[kKllMaxLevels + 1] = {0}, arrived[kKllMaxLevels + 1] = {0};
+    int32_t ncomp[kKllMaxLevels + 1] = {0}, offset[kKllMaxLevels + 1] = {0};
+    std::vector<int64_t> per_class((size_t)(kKllMaxLevels + 1) * 32, 0);
+    int nlev = 1;
+    int64_t total = cap[0], actual = 0;
+    uint64_t full = 0;  // bit h: len[h] >= cap[h]
     int64_t rem = n;
-    events.reserve((size_t)(n / 900 + 64));
+    events.resize((size_t)(n / 512 + 1024));
+    uint64_t* ev = events.data();
+    size_t ne = 0;
     while (rem > 0) {
-        KllLevel& l0 = sc.levels[0];
         // the updates until condense next compacts: past `total`, and (no level full) until level 0 fills — one jump
         // per compaction (condense without a full level changes nothing but the counts)
-        int64_t k = std::max<int64_t>(1, sc.total - sc.actual + 1);
-        if (full == 0) k = std::max<int64_t>(k, cap[0] - l0.len);
+        int64_t k = std::max<int64_t>(1, total - actual + 1);
+        if (full == 0) k = std::max<int64_t>(k, cap[0] - len[0]);
         k = std::min<int64_t>(rem, k);
-        l0.len += k;
-        l0.arrived += k;
-        sc.actual += k;
+        len[0] += k;
+        arrived[0] += k;
+        actual += k;
         rem -= k;
-        if (l0.len >= cap[0]) full |= 1ull;
-        if (sc.actual <= sc.total || full == 0) continue;
+        if (len[0] >= cap[0]) full |= 1ull;
+        if (actual <= total || full == 0) continue;
         const int h = __builtin_ctzll(full);
-        if (h + 1 >= (int)sc.levels.size()) {
-            if ((int)sc.levels.size() >= kKllMaxLevels) return false;
-            sc.levels.push_back(KllLevel());
-            sc.total += cap[sc.levels.size() - 1];
+        if (h + 1 >= nlev) {
+            if (nlev >= kKllMaxLevels) return false;
+            ++nlev;
+            total += cap[nlev - 1];
         }
-        KllLevel& lv = sc.levels[h];
-        const int64_t items = lv.len;
-        const int64_t L = items - items % 2;
+        const int64_t items = len[h];
+        const int64_t L = items & ~(int64_t)1;
         if (L > kKllMaxPad) return false;
-        if (lv.ncomp % 2 == 1) lv.offset = 1 - lv.offset;
-        KllLevel& up = sc.levels[h + 1];
-        events.push_back(kll_desc((uint64_t)lv.pos, (uint32_t)L, (uint32_t)lv.offset) | ((uint64_t)h << 55));
-        ++lv.per_class[kll_class_of((int)L)];
-        lv.pos += L;
-        lv.len = items % 2;
+        const int32_t off = offset[h] ^ (ncomp[h] & 1);  // the offset flips on odd compaction counts
+        offset[h] = off;
+        if (ne == events.size()) {
+            events.resize(events.size() * 2);
+            ev = events.data();
+        }
+        ev[ne++] = kll_desc((uint64_t)pos[h], (uint32_t)L, (uint32_t)off) | ((uint64_t)h << 55);
+        ++per_class[(size_t)h * 32 + kll_class_of((int)L)];
+        pos[h] += L;
+        len[h] = items & 1;
         full &= ~(1ull << h);
-        up.len += L / 2;
-        up.arrived += L / 2;
-        if (up.len >= cap[h + 1]) full |= 1ull << (h + 1);
-        lv.ncomp += 1;
-        sc.actual -= L / 2;  // = the sum of buffer lengths, as getCompactorItemsCount recomputes it
+        len[h + 1] += L >> 1;
+        arrived[h + 1] += L >> 1;
+        if (len[h + 1] >= cap[h + 1]) full |= 1ull << (h + 1);
+        ncomp[h] += 1;
+        actual -= L >> 1;  // = the sum of buffer lengths, as getCompactorItemsCount recomputes it
     }
+    events.resize(ne);
+    sc.levels.assign(nlev, KllLevel());
+    for (int h = 0; h < nlev; ++h) {
+        KllLevel& l = sc.levels[h];
+        l.len = len[h];
+        l.ncomp = ncomp[h];
+        l.offset = offset[h];
+        l.pos = pos[h];
+        l.arrived = arrived[h];
+        for (int c = 0; c < 32; ++c) l.per_class[c] = per_class[(size_t)h * 32 + c];
+    }
+    sc.total = total;
+    sc.actual = actual;
     return true;
 }
 
