@@ -731,19 +731,12 @@ class FrequenciesAndNumRows:
 
     def summary(self, entropy_rows=None):
         n = self.numRows if entropy_rows is None else entropy_rows
-        if isinstance(self.frequencies, (dict, engine.PairFrequencies)):
-            if isinstance(self.frequencies, engine.PairFrequencies):
-                pf = self.frequencies
-                counts = pf.counts.astype(np.float64)
-                if pf.null_count:
-                    counts = np.append(counts, float(pf.null_count))
-            else:
-                counts = np.fromiter(self.frequencies.values(), dtype=np.float64, count=len(self.frequencies))
-            ent = 0.0
-            if len(counts):
-                p = counts / n
-                ent = float(-(p * np.log(p)).sum())
-            return {"num_groups": len(counts), "num_unique": int((counts == 1).sum()), "entropy": ent}
+        if isinstance(self.frequencies, dict):
+            # a small host-built state (the reference's KAT-sized inputs): the device summary's exact fixed-point sum
+            counts = list(self.frequencies.values())
+            fx = sum(N.fx_of(-(c / n) * math.log(c / n)) for c in counts) if n else 0
+            return {"num_groups": len(counts), "num_unique": sum(1 for c in counts if c == 1),
+                    "entropy": N.fx_to_float(fx), "entropy_fx": fx}
         return self.device_table().summary(n)
 
 
@@ -763,9 +756,12 @@ class SplitFrequencies:
 
     def summary(self, entropy_rows=None):
         parts = [t.summary(entropy_rows) for t in self.tables]
+        fx = sum(p["entropy_fx"] for p in parts)  # exact: the same bits as one table over all the groups
+        finite = all(math.isfinite(p["entropy"]) for p in parts)
         return {"num_rows": sum(p["num_rows"] for p in parts), "num_groups": sum(p["num_groups"] for p in parts),
                 "num_unique": sum(p["num_unique"] for p in parts),
-                "entropy": math.fsum(p["entropy"] for p in parts), "entropy_rows": parts[0]["entropy_rows"],
+                "entropy": N.fx_to_float(fx) if finite else float("nan"), "entropy_fx": fx,
+                "entropy_rows": parts[0]["entropy_rows"],
                 "max_count": max(p["max_count"] for p in parts), "null_count": sum(p["null_count"] for p in parts)}
 
     def export_raw(self):

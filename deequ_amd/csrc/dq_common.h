@@ -157,4 +157,44 @@ DQ_HD uint64_t splitmix64(uint64_t seed, uint64_t i) {
     return z ^ (z >> 31);
 }
 
+// ---- exact, order-free sums of fp64 terms (entropy / MutualInformation) ------------------------------
+// A Spark `sum` over the groups' terms (A/Entropy.scala:28-42, A/MutualInformation.scala:66-90) has no defined
+// order; a GPU table's slot order is decided by atomics, so any fp fold over slots is run-to-run and
+// geometry dependent. Each term is instead rounded once to a signed 128-bit fixed-point integer of
+// kFxBits fraction bits and the integers are added (associative, exact), so every build / launch
+// geometry / device split of the same groups gives the same bits. |term| < 2^22 (an entropy term is
+// <= 1/e, a MutualInformation term <= ln(2^63) < 44); the rounding error is <= 2^-105 per term.
+constexpr int kFxBits = 104;
+typedef __int128 fx128;
+
+DQ_HD fx128 fx_of(double t) {
+    union { double d; uint64_t u; } c;
+    c.d = t;
+    const int e = (int)((c.u >> 52) & 0x7ff);
+    const uint64_t m = (c.u & ((1ull << 52) - 1)) | (e ? (1ull << 52) : 0ull);
+    const int sh = (e ? e : 1) - 1075 + kFxBits;
+    fx128 v;
+    if (sh >= 0)
+        v = (fx128)m << (sh < 74 ? sh : 74);  // callers keep |t| < 2^22 (sh <= 73); clamp defensively
+    else if (sh > -64)
+        v = (fx128)((m + (1ull << (-sh - 1))) >> -sh);  // round half up (in magnitude)
+    else
+        v = 0;
+    return (c.u >> 63) ? -v : v;
+}
+
+// fx128 -> double: one correctly rounded integer conversion, then an exact power-of-two scale.
+inline double fx_to_double(fx128 v) {
+    const double d = (double)v;
+    return d * (1.0 / 20282409603651670423947251286016.0);  // 2^-104
+}
+
+#if !defined(DQ_HOST_ONLY)
+__device__ __forceinline__ fx128 fx_shfl_down(fx128 v, int off) {
+    const unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
+    const unsigned long long l2 = __shfl_down(lo, off, 64), h2 = __shfl_down(hi, off, 64);
+    return (fx128)(((unsigned __int128)h2 << 64) | l2);
+}
+#endif
+
 }  // namespace dq

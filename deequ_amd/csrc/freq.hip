@@ -64,7 +64,15 @@ constexpr int kP1TileFast = 4096;
 constexpr int kPartTileFast = 8192;// second pass, fast path: 32 per lane, so a tile's 256 per-digit runs average 256 B
                                    // (measured: scatter2 5.85 -> 4.88 ms on C4; partition1 slows down at 8192)
 constexpr int kPass2Item = 65536;  // keys per work item of the second partition pass
-constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (fixed: deterministic partials)
+constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (upper bound: the scratch is sized for it)
+
+// Grid of the summary / MutualInformation table scans. The sums are exact fixed point (SummaryPartial), so any
+// grid gives the same bits; DQ_FREQ_SUMMARY_GRID (1..kScanBlocks) changes it to prove that (tests/).
+int summary_grid() {
+    const char* e = getenv("DQ_FREQ_SUMMARY_GRID");
+    const int v = e ? atoi(e) : kScanBlocks;
+    return v >= 1 && v <= kScanBlocks ? v : kScanBlocks;
+}
 constexpr int kRegion = 4096;      // slots per bucket region (the LDS table of one workgroup)
 // Distinct keys per bucket the bucket count aims at (load <= ~0.63). rocPRIM sorts 8 bits per pass
 // on gfx950, so 1e8 distinct keys take b = 16 (2 passes) rather than 17 (3 passes). (Measured on C4: a
@@ -1151,20 +1159,56 @@ scatter2_fast_kernel(const FastItem* __restrict__ items, const void* __restrict_
     if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->pad[1], 1ull);
 }
 
+// Grouping summary partial. `ent` is the exact fixed-point sum of the entropy (or MutualInformation) terms
+// (dq_common.h fx_of): integer adds, so the fold is the same for any slot order, workgroup split or device split.
 struct SummaryPartial {
-    unsigned long long groups, unique, maxc, pad;
-    double ent, comp;
+    unsigned long long groups, unique, maxc;
+    unsigned int pad;        // build partials: 1 = this region needs the table scan
+    unsigned int nonfinite;  // terms that were inf / NaN (the metric is then NaN, as a Spark double sum)
+    fx128 ent;
 };
 
-// Kahan-compensated fold of two summary partials (fixed order: a then b).
-__device__ __forceinline__ void summary_merge(SummaryPartial& a, const SummaryPartial& b) {
+__host__ __device__ __forceinline__ void summary_merge(SummaryPartial& a, const SummaryPartial& b) {
     a.groups += b.groups;
     a.unique += b.unique;
     a.maxc = b.maxc > a.maxc ? b.maxc : a.maxc;
-    const double y = b.ent - (a.comp + b.comp);
-    const double t = a.ent + y;
-    a.comp = (t - a.ent) - y;
-    a.ent = t;
+    a.nonfinite += b.nonfinite;
+    a.ent += b.ent;
+}
+
+// Adds one term to a partial: rounded once to fixed point, or counted as non-finite.
+__device__ __forceinline__ void summary_add_term(SummaryPartial& p, double term) {
+    if (__builtin_isfinite(term) && fabs(term) < 4194304.0)
+        p.ent += fx_of(term);
+    else
+        p.nonfinite++;
+}
+
+// -(c/N) ln(c/N): the one definition of an entropy term (A/Entropy.scala:28-42), used by every kernel below.
+__device__ __forceinline__ double entropy_term(unsigned long long c, double n) {
+    const double q = (double)c / n;
+    return -q * log(q);
+}
+
+__device__ __forceinline__ SummaryPartial summary_shfl_down(const SummaryPartial& p, int off) {
+    SummaryPartial o;
+    o.groups = __shfl_down(p.groups, off, 64);
+    o.unique = __shfl_down(p.unique, off, 64);
+    o.maxc = __shfl_down(p.maxc, off, 64);
+    o.pad = __shfl_down(p.pad, off, 64);
+    o.nonfinite = __shfl_down(p.nonfinite, off, 64);
+    o.ent = fx_shfl_down(p.ent, off);
+    return o;
+}
+
+// Entropy terms of the side groups the host keeps outside the table (the fast path's EMPTY-colliding value,
+// Histogram's NULL group), computed by the same device code as the table's terms.
+__global__ void side_terms_kernel(unsigned long long c0, unsigned long long c1, double n, SummaryPartial* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    SummaryPartial p = {0, 0, 0, 0, 0, 0};
+    if (c0) summary_add_term(p, entropy_term(c0, n));
+    if (c1) summary_add_term(p, entropy_term(c1, n));
+    *out = p;
 }
 
 struct BuildItem {
@@ -1259,7 +1303,7 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
     Slot* region = slots + (uint64_t)it.bucket * kRegion;
     unsigned long long* rrep = GENERAL ? reps + (uint64_t)it.bucket * kRegion : nullptr;
     if (!it.split) {
-        SummaryPartial p = {0, 0, 0, 0, 0.0, 0.0};
+        SummaryPartial p = {0, 0, 0, 0, 0, 0};
         for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
             Slot sl;
             sl.key = lkey[i];
@@ -1271,25 +1315,13 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
             p.groups++;
             p.unique += c == 1;
             p.maxc = c > p.maxc ? c : p.maxc;
-            if (n > 0) {
-                const double q = (double)c / n;
-                const double term = -q * log(q);
-                const double y = term - p.comp;
-                const double t = p.ent + y;
-                p.comp = (t - p.ent) - y;
-                p.ent = t;
-            }
+            if (n > 0) summary_add_term(p, entropy_term(c, n));
         }
         if (parts) {
             __shared__ SummaryPartial wred[kBuildBlock / 64];
             const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
             for (int off = 32; off > 0; off >>= 1) {
-                SummaryPartial o;
-                o.groups = __shfl_down(p.groups, off, 64);
-                o.unique = __shfl_down(p.unique, off, 64);
-                o.maxc = __shfl_down(p.maxc, off, 64);
-                o.ent = __shfl_down(p.ent, off, 64);
-                o.comp = __shfl_down(p.comp, off, 64);
+                const SummaryPartial o = summary_shfl_down(p, off);
                 if (lane < off) summary_merge(p, o);
             }
             if (lane == 0) wred[wave] = p;
@@ -1302,7 +1334,7 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
         }
     } else {
         if (parts && threadIdx.x == 0) {
-            SummaryPartial z = {0, 0, 0, 1, 0.0, 0.0};  // pad = 1: this region needs the table scan
+            SummaryPartial z = {0, 0, 0, 1, 0, 0};  // pad = 1: this region needs the table scan
             parts[blockIdx.x] = z;
         }
         bool mok = true;
@@ -1666,36 +1698,19 @@ summary_kernel(const Slot* __restrict__ slots, uint64_t cap, double n, SummaryPa
     const uint64_t chunk = (cap + gridDim.x - 1) / gridDim.x;
     const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t b1 = b0 + chunk < cap ? b0 + chunk : cap;
-    SummaryPartial p = {0, 0, 0, 0, 0.0, 0.0};
+    SummaryPartial p = {0, 0, 0, 0, 0, 0};
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += kFreqBlock) {
         const unsigned long long c = slots[i].count;
         if (c == 0) continue;
         p.groups++;
         p.unique += c == 1;
         p.maxc = c > p.maxc ? c : p.maxc;
-        if (n > 0) {
-            const double q = (double)c / n;
-            const double term = -q * log(q);
-            const double y = term - p.comp;  // Kahan
-            const double t = p.ent + y;
-            p.comp = (t - p.ent) - y;
-            p.ent = t;
-        }
+        if (n > 0) summary_add_term(p, entropy_term(c, n));
     }
     red[threadIdx.x] = p;
     __syncthreads();
     for (int s = kFreqBlock / 2; s > 0; s >>= 1) {
-        if (threadIdx.x < s) {
-            SummaryPartial& a = red[threadIdx.x];
-            const SummaryPartial& b = red[threadIdx.x + s];
-            a.groups += b.groups;
-            a.unique += b.unique;
-            a.maxc = b.maxc > a.maxc ? b.maxc : a.maxc;
-            const double y = b.ent - (a.comp + b.comp);
-            const double t = a.ent + y;
-            a.comp = (t - a.ent) - y;
-            a.ent = t;
-        }
+        if (threadIdx.x < s) summary_merge(red[threadIdx.x], red[threadIdx.x + s]);
         __syncthreads();
     }
     if (threadIdx.x == 0) out[blockIdx.x] = red[0];
@@ -1799,8 +1814,8 @@ __device__ __forceinline__ unsigned long long lookup_count(const LookupTable& T,
     return 0;
 }
 
-// sum over joint groups with both keys non-NULL of (pxy/N) ln((pxy/N) / ((px/N)(py/N))), per-workgroup Kahan
-// partials over fixed slot chunks (folded in order on the host: deterministic)
+// sum over joint groups with both keys non-NULL of (pxy/N) ln((pxy/N) / ((px/N)(py/N))): every term rounded once to
+// fixed point and the integers added (SummaryPartial), so the sum does not depend on the joint table's slot order
 __global__ void __launch_bounds__(kFreqBlock)
 mi_kernel(const Slot* __restrict__ slots, const unsigned long long* __restrict__ reps, uint64_t cap, KeySpec jks,
           LookupTable X, LookupTable Y, double n, SummaryPartial* __restrict__ out) {
@@ -1808,7 +1823,7 @@ mi_kernel(const Slot* __restrict__ slots, const unsigned long long* __restrict__
     const uint64_t chunk = (cap + gridDim.x - 1) / gridDim.x;
     const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t b1 = b0 + chunk < cap ? b0 + chunk : cap;
-    SummaryPartial p = {0, 0, 0, 0, 0.0, 0.0};
+    SummaryPartial p = {0, 0, 0, 0, 0, 0};
     for (uint64_t i = b0 + threadIdx.x; i < b1; i += kFreqBlock) {
         const unsigned long long c = slots[i].count;
         if (c == 0) continue;
@@ -1816,25 +1831,13 @@ mi_kernel(const Slot* __restrict__ slots, const unsigned long long* __restrict__
         if (!is_valid(jks.cols[0], r) || !is_valid(jks.cols[1], r)) continue;
         const double px = (double)lookup_count(X, r), py = (double)lookup_count(Y, r);
         const double pxy = (double)c / n;
-        const double term = pxy * log(pxy / ((px / n) * (py / n)));
         p.groups++;
-        const double yk = term - p.comp;
-        const double t = p.ent + yk;
-        p.comp = (t - p.ent) - yk;
-        p.ent = t;
+        summary_add_term(p, pxy * log(pxy / ((px / n) * (py / n))));
     }
     red[threadIdx.x] = p;
     __syncthreads();
     for (int st = kFreqBlock / 2; st > 0; st >>= 1) {
-        if (threadIdx.x < st) {
-            SummaryPartial& a = red[threadIdx.x];
-            const SummaryPartial& b = red[threadIdx.x + st];
-            a.groups += b.groups;
-            const double yk = b.ent - (a.comp + b.comp);
-            const double t = a.ent + yk;
-            a.comp = (t - a.ent) - yk;
-            a.ent = t;
-        }
+        if (threadIdx.x < st) summary_merge(red[threadIdx.x], red[threadIdx.x + st]);
         __syncthreads();
     }
     if (threadIdx.x == 0) out[blockIdx.x] = red[0];
@@ -1891,7 +1894,8 @@ struct dq_freq_table {
     int pre_valid = 0;
     int64_t pre_n = -1;
     unsigned long long pre_groups = 0, pre_unique = 0, pre_maxc = 0;
-    double pre_ent = 0.0, pre_comp = 0.0;
+    fx128 pre_ent = 0;
+    unsigned int pre_nonfinite = 0;
     int32_t key_type = 0;   // Spark type of the (single) key column, or of the canonical keys of a pair-built table
     int64_t num_rows_override = -1;  // tables built from (key, count) pairs carry the caller's numRows
     int64_t src_rows = -1;  // rows of the source columns (dq_frequencies_ex), -1 for pair-built / merged tables
@@ -2051,30 +2055,24 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     std::vector<SummaryPartial> hparts(items.size());
     FQ_HIP(ctx, hipMemcpyAsync(hparts.data(), bparts, items.size() * sizeof(SummaryPartial), hipMemcpyDeviceToHost, s));
     FQ_HIP(ctx, hipStreamSynchronize(s));
-    // the fused summary, folded in item order (deterministic) unless a split bucket needs the table scan
+    // the fused summary (exact fixed-point terms: any fold order gives the same bits) unless a split bucket needs
+    // the table scan
     t->pre_valid = 0;
     if (t->host_ctr.overflow == 0 && t->host_ctr.mismatch == 0 && nspill == 0) {  // spilled keys: the table scan
         bool all = true;
-        unsigned long long groups = 0, unique = 0, maxc = 0;
-        double ent = 0.0, comp = 0.0;
+        SummaryPartial acc = {0, 0, 0, 0, 0, 0};
         for (const SummaryPartial& p : hparts) {
             if (p.pad) { all = false; break; }
-            groups += p.groups;
-            unique += p.unique;
-            maxc = std::max(maxc, p.maxc);
-            const double y = (p.ent - p.comp) - comp;
-            const double tt = ent + y;
-            comp = (tt - ent) - y;
-            ent = tt;
+            summary_merge(acc, p);
         }
         if (all) {
             t->pre_valid = 1;
             t->pre_n = (int64_t)build_n;
-            t->pre_groups = groups;
-            t->pre_unique = unique;
-            t->pre_maxc = maxc;
-            t->pre_ent = ent;
-            t->pre_comp = comp;
+            t->pre_groups = acc.groups;
+            t->pre_unique = acc.unique;
+            t->pre_maxc = acc.maxc;
+            t->pre_ent = acc.ent;
+            t->pre_nonfinite = acc.nonfinite;
         }
     }
     if (getenv("DQ_DEBUG_FREQ"))
@@ -3188,11 +3186,12 @@ int dq_freq_key_kind(const dq_freq_table* t) { return !t ? -1 : (t->fast ? DQ_FR
 int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows, dq_freq_summary* out) {
     if (!ctx || !t || !out) return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_freq_summarize: invalid arguments");
     if (!t->parts.empty()) {
-        // union of disjoint per-device tables: counts add, entropy terms (global N) folded in device order
+        // union of disjoint per-device tables: counts add, the exact entropy sums (global N) add
         const int64_t n = entropy_rows > 0 ? entropy_rows : t->total_rows;
         dq_freq_summary acc;
         memset(&acc, 0, sizeof(acc));
-        double comp = 0.0;
+        fx128 ent = 0;
+        bool nonfinite = false;
         for (size_t i = 0; i < t->parts.size(); ++i) {
             dq_freq_summary p;
             const int rc = dq_freq_summarize(t->part_ctx[i], t->parts[i], n, &p);
@@ -3201,13 +3200,14 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
             acc.num_unique += p.num_unique;
             acc.max_count = std::max(acc.max_count, p.max_count);
             acc.null_count += p.null_count;
-            const double yk = p.entropy - comp;
-            const double tt = acc.entropy + yk;
-            comp = (tt - acc.entropy) - yk;
-            acc.entropy = tt;
+            ent += (fx128)(((unsigned __int128)(uint64_t)p.entropy_fx_hi << 64) | p.entropy_fx_lo);
+            nonfinite |= !std::isfinite(p.entropy);
         }
         acc.num_rows = t->total_rows;
         acc.entropy_rows = n;
+        acc.entropy = nonfinite ? NAN : fx_to_double(ent);
+        acc.entropy_fx_lo = (uint64_t)ent;
+        acc.entropy_fx_hi = (int64_t)(ent >> 64);
         *out = acc;
         return DQ_OK;
     }
@@ -3219,51 +3219,50 @@ int dq_freq_summarize(dq_ctx* ctx, const dq_freq_table* t, int64_t entropy_rows,
         *out = t->cached;
         return DQ_OK;
     }
-    unsigned long long groups = 0, unique = 0, maxc = 0;
-    double ent = 0.0, comp = 0.0;
-    auto add_term = [&](double term) {
-        const double y = term - comp;
-        const double tt = ent + y;
-        comp = (tt - ent) - y;
-        ent = tt;
-    };
-    if (t->pre_valid && t->pre_n == n) {  // folded into the build: no table scan
-        groups = t->pre_groups;
-        unique = t->pre_unique;
-        maxc = t->pre_maxc;
-        ent = t->pre_ent;
-        comp = t->pre_comp;
+    SummaryPartial acc = {0, 0, 0, 0, 0, 0};
+    if (t->pre_valid && t->pre_n == n && !getenv("DQ_FREQ_NO_FUSED_SUMMARY")) {  // folded into the build: no scan
+        acc.groups = t->pre_groups;
+        acc.unique = t->pre_unique;
+        acc.maxc = t->pre_maxc;
+        acc.ent = t->pre_ent;
+        acc.nonfinite = t->pre_nonfinite;
     } else {
         SummaryPartial* parts = (SummaryPartial*)t->scratch;
-        hipLaunchKernelGGL(summary_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->cap, (double)n, parts);
+        const int grid = summary_grid();
+        hipLaunchKernelGGL(summary_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->slots, t->cap, (double)n, parts);
         FQ_HIP(ctx, hipGetLastError());
-        std::vector<SummaryPartial> hp(kScanBlocks);
-        FQ_HIP(ctx, hipMemcpyAsync(hp.data(), parts, sizeof(SummaryPartial) * kScanBlocks, hipMemcpyDeviceToHost, s));
+        std::vector<SummaryPartial> hp(grid);
+        FQ_HIP(ctx, hipMemcpyAsync(hp.data(), parts, sizeof(SummaryPartial) * grid, hipMemcpyDeviceToHost, s));
         FQ_HIP(ctx, hipStreamSynchronize(s));
-        for (const SummaryPartial& p : hp) {
-            groups += p.groups;
-            unique += p.unique;
-            maxc = std::max(maxc, p.maxc);
-            add_term(p.ent - p.comp);
-        }
+        for (const SummaryPartial& p : hp) summary_merge(acc, p);
     }
-    // side groups: the fast path's EMPTY-colliding value and (Histogram) the NULL group
-    for (unsigned long long extra : {t->host_ctr.sentinel, t->host_ctr.nulls}) {
+    // side groups: the fast path's EMPTY-colliding value and (Histogram) the NULL group; their terms come from the
+    // device's entropy_term like every other group's, so a group's term does not depend on where it is kept
+    const unsigned long long side[2] = {t->host_ctr.sentinel, t->host_ctr.nulls};
+    for (unsigned long long extra : side) {
         if (!extra) continue;
-        groups += 1;
-        unique += extra == 1;
-        maxc = std::max(maxc, extra);
-        if (n > 0) {
-            const double q = (double)extra / (double)n;
-            add_term(-q * log(q));
-        }
+        acc.groups += 1;
+        acc.unique += extra == 1;
+        acc.maxc = std::max(acc.maxc, extra);
+    }
+    if (n > 0 && (side[0] || side[1])) {
+        SummaryPartial* d = (SummaryPartial*)t->scratch;
+        hipLaunchKernelGGL(side_terms_kernel, dim3(1), dim3(64), 0, s, side[0], side[1], (double)n, d);
+        FQ_HIP(ctx, hipGetLastError());
+        SummaryPartial hs;
+        FQ_HIP(ctx, hipMemcpyAsync(&hs, d, sizeof(hs), hipMemcpyDeviceToHost, s));
+        FQ_HIP(ctx, hipStreamSynchronize(s));
+        acc.ent += hs.ent;
+        acc.nonfinite += hs.nonfinite;
     }
     out->num_rows = table_rows;
-    out->num_groups = (int64_t)groups;
-    out->num_unique = (int64_t)unique;
-    out->entropy = ent;
+    out->num_groups = (int64_t)acc.groups;
+    out->num_unique = (int64_t)acc.unique;
+    out->entropy = acc.nonfinite ? NAN : fx_to_double(acc.ent);
+    out->entropy_fx_lo = (uint64_t)acc.ent;
+    out->entropy_fx_hi = (int64_t)(acc.ent >> 64);
     out->entropy_rows = n;
-    out->max_count = (int64_t)maxc;
+    out->max_count = (int64_t)acc.maxc;
     out->null_count = (int64_t)t->host_ctr.nulls;
     dq_freq_table* mt = const_cast<dq_freq_table*>(t);
     mt->cached = *out;
@@ -3615,23 +3614,17 @@ int mi_tables(dq_ctx* ctx, const dq_freq_table* joint, const dq_freq_table* x, c
     Y.bits = y->bits;
     const int64_t n = joint->num_rows_override >= 0 ? joint->num_rows_override : (int64_t)joint->host_ctr.num_rows;
     SummaryPartial* parts = (SummaryPartial*)joint->scratch;
-    hipLaunchKernelGGL(mi_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, joint->slots, joint->reps, joint->cap,
+    const int grid = summary_grid();
+    hipLaunchKernelGGL(mi_kernel, dim3(grid), dim3(kFreqBlock), 0, s, joint->slots, joint->reps, joint->cap,
                        joint->ks, X, Y, (double)n, parts);
     FQ_HIP(ctx, hipGetLastError());
-    std::vector<SummaryPartial> hp(kScanBlocks);
-    FQ_HIP(ctx, hipMemcpyAsync(hp.data(), parts, sizeof(SummaryPartial) * kScanBlocks, hipMemcpyDeviceToHost, s));
+    std::vector<SummaryPartial> hp(grid);
+    FQ_HIP(ctx, hipMemcpyAsync(hp.data(), parts, sizeof(SummaryPartial) * grid, hipMemcpyDeviceToHost, s));
     FQ_HIP(ctx, hipStreamSynchronize(s));
-    unsigned long long groups = 0;
-    double sum = 0.0, comp = 0.0;
-    for (const SummaryPartial& p : hp) {
-        groups += p.groups;
-        const double yk = (p.ent - p.comp) - comp;
-        const double tt = sum + yk;
-        comp = (tt - sum) - yk;
-        sum = tt;
-    }
-    *mi = sum;
-    *present = groups > 0 ? 1 : 0;  // sum over zero joined rows is NULL (A/MutualInformation.scala:82-86)
+    SummaryPartial acc = {0, 0, 0, 0, 0, 0};
+    for (const SummaryPartial& p : hp) summary_merge(acc, p);
+    *mi = acc.nonfinite ? NAN : fx_to_double(acc.ent);
+    *present = acc.groups > 0 ? 1 : 0;  // sum over zero joined rows is NULL (A/MutualInformation.scala:82-86)
     return DQ_OK;
 }
 }  // namespace

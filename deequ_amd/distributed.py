@@ -64,14 +64,13 @@ def owner_ranks(torch, keys, world):
     return torch.remainder((z >> 32) & 0xFFFFFFFF, world)
 
 
-def kahan_fold(values):
-    s, c = 0.0, 0.0
-    for v in values:
-        y = v - c
-        t = s + y
-        c = (t - s) - y
-        s = t
-    return s
+_M64 = (1 << 64) - 1
+
+
+def _i64(v):
+    """A 64-bit pattern as a signed int64 (for an int64 tensor)."""
+    v &= _M64
+    return v - (1 << 64) if v >> 63 else v
 
 
 class Exchange:
@@ -111,6 +110,14 @@ class Exchange:
         t = self.torch.tensor(values, dtype=self.torch.int64, device=self.device)
         self.dist.all_reduce(t, group=self.group)
         return [int(v) for v in t.cpu().tolist()]
+
+    def all_gather_i64(self, values):
+        """A fixed-length int64 vector of every rank, in rank order."""
+        t = self.torch.tensor(values, dtype=self.torch.int64, device=self.device)
+        out = self.torch.empty(self.world * len(values), dtype=self.torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+        flat = [int(v) for v in out.cpu().tolist()]
+        return [flat[r * len(values):(r + 1) * len(values)] for r in range(self.world)]
 
     def all_gather_f64(self, value):
         t = self.torch.tensor([value], dtype=self.torch.float64, device=self.device)
@@ -281,7 +288,11 @@ class DistributedFrequencies:
         if n not in self._summary:
             s = self.runner._local_step(lambda: self.local.table_summary(self.table, n))
             groups, unique = self.ex.all_reduce_i64([s["num_groups"], s["num_unique"]])
-            ent = kahan_fold(self.ex.all_gather_f64(s["entropy"]))
+            # the ranks' exact fixed-point entropy sums add exactly: the same bits for any world size
+            fx = s["entropy_fx"]
+            rows = self.ex.all_gather_i64([_i64(fx & _M64), _i64(fx >> 64), 0 if math.isfinite(s["entropy"]) else 1])
+            total = sum(((hi << 64) | (lo & _M64)) for lo, hi, _ in rows)
+            ent = N.fx_to_float(total) if not any(bad for _, _, bad in rows) else float("nan")
             self._summary[n] = {"num_rows": self.num_rows, "num_groups": groups, "num_unique": unique,
                                 "entropy": ent}
         return self._summary[n]

@@ -212,7 +212,7 @@ class FrequencyTable:
         self.ctx.check(rc, "dq_freq_summarize")
         return {"num_rows": out.num_rows, "num_groups": out.num_groups, "num_unique": out.num_unique,
                 "entropy": out.entropy, "entropy_rows": out.entropy_rows, "max_count": out.max_count,
-                "null_count": out.null_count}
+                "null_count": out.null_count, "entropy_fx": N.fx_value(out.entropy_fx_lo, out.entropy_fx_hi)}
 
     def key_kind(self):
         return self.ctx.lib.dq_freq_key_kind(self.handle)

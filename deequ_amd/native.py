@@ -131,7 +131,34 @@ class DqState(ctypes.Structure):
 class DqFreqSummary(ctypes.Structure):
     _fields_ = [("num_rows", ctypes.c_int64), ("num_groups", ctypes.c_int64), ("num_unique", ctypes.c_int64),
                 ("entropy", ctypes.c_double), ("entropy_rows", ctypes.c_int64), ("max_count", ctypes.c_int64),
-                ("null_count", ctypes.c_int64)]
+                ("null_count", ctypes.c_int64), ("entropy_fx_lo", ctypes.c_uint64), ("entropy_fx_hi", ctypes.c_int64)]
+
+
+def fx_value(lo, hi):
+    """The exact fixed-point entropy sum of a dq_freq_summary (2^-104 units) as a Python int."""
+    return (int(hi) << 64) | int(lo)
+
+
+def fx_of(t):
+    """dq_common.h fx_of: a double rounded once to signed fixed point of 2^-104 units (round half up in magnitude)."""
+    import struct
+    u = struct.unpack("<Q", struct.pack("<d", float(t)))[0]
+    e = (u >> 52) & 0x7FF
+    m = (u & ((1 << 52) - 1)) | ((1 << 52) if e else 0)
+    sh = (e if e else 1) - 1075 + 104
+    if sh >= 0:
+        v = m << min(sh, 74)
+    elif sh > -64:
+        v = (m + (1 << (-sh - 1))) >> -sh
+    else:
+        v = 0
+    return -v if u >> 63 else v
+
+
+def fx_to_float(v):
+    """dq_common.h fx_to_double: one correctly rounded conversion (Python's int / float true division of an int by a
+    power of two rounds correctly), then an exact scale."""
+    return v / float(1 << 104) if abs(v) < (1 << 1000) else float("nan")
 
 
 class DqFreqOptions(ctypes.Structure):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 1
+#define DQ_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------------------------------
  * Status codes
@@ -191,6 +191,12 @@ typedef struct dq_freq_summary {
     int64_t entropy_rows;  /* the N used for `entropy`                                                 */
     int64_t max_count;
     int64_t null_count;    /* DQ_FREQ_INCLUDE_NULLS: rows whose keys are all NULL (one extra group)  */
+    /* `entropy` exactly as the order-free sum it was rounded from: each group's term rounded once to
+     * a signed 128-bit integer of 2^-104 units, the integers added. entropy ==
+     * (double)(hi:lo) * 2^-104. Parts of a sharded table (disjoint groups) add these, not `entropy`,
+     * so any split of the same groups gives the same bits. */
+    uint64_t entropy_fx_lo;
+    int64_t entropy_fx_hi;
 } dq_freq_summary;
 
 /* ---------------------------------------------------------------------------------------------

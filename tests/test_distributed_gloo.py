@@ -80,9 +80,10 @@ class OracleLocal:
 
     def table_summary(self, table, n):
         counts = list(table.values())
-        ent = math.fsum(-(c / n) * math.log(c / n) for c in counts) if counts and n else 0.0
-        return {"num_groups": len(counts), "num_unique": sum(1 for c in counts if c == 1), "entropy": ent,
-                "num_rows": sum(counts)}
+        # the device summary's contract: each term rounded once to 2^-104 fixed point, the integers added
+        fx = sum(N.fx_of(-(c / n) * math.log(c / n)) for c in counts) if counts and n else 0
+        return {"num_groups": len(counts), "num_unique": sum(1 for c in counts if c == 1),
+                "entropy": N.fx_to_float(fx), "entropy_fx": fx, "num_rows": sum(counts)}
 
     def top_block(self, table, block, k):
         items = sorted(table.items(), key=lambda kv: -kv[1])[:k]

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     assert set(decl) == set(N.EXPORTED_SYMBOLS), set(decl) ^ set(N.EXPORTED_SYMBOLS)
     for s in decl:
         assert hasattr(lib, s), s
-    assert lib.dq_abi_version() == 1
+    assert lib.dq_abi_version() == 2
 
 
 def test_struct_sizes_match_header_layout():
