@@ -3,9 +3,14 @@
 One step = one AnalysisRunner scan pass of the suite over the rank's row shard (49 ops: Size +
 {Completeness, Mean, Sum, Minimum, Maximum, StandardDeviation} over 8 columns: 4 fp64 + 4 int64,
 1 % nulls), the RCCL all-gather of the per-rank states (N > 1) and the rank-ordered
-semigroup fold of those states on the host. Rows are sharded contiguously across ranks (strong
-scaling over the 1e9-row table). Inputs are generated in HBM by the counter-based splitmix64
-generators before timing.
+semigroup fold of those states on the host. Rows are independent partitions (Spark partitions feeding one
+`data.agg`, R/AnalysisRunner.scala:313), so the default is weak scaling: every rank scans its own 1e9-row shard
+of one N x 1e9-row table and `value` counts the rows of all ranks (`--scaling strong` splits 1e9 rows instead).
+Inputs are generated in HBM by the counter-based splitmix64 generators before timing.
+
+`--gpus N` without a launcher starts N rank processes itself (spawn_ranks); under torch.distributed.run the
+ranks come from RANK / LOCAL_RANK / WORLD_SIZE. N > 1 runs on RCCL (nccl); `--dist-backend gloo
+--device-override 0` rehearses N ranks on one GPU.
 
 The same JSON line carries `secondary` measurements of the other BASELINE workloads, each timed the
 same way (its own steps, HIP events on the scan stream, its own roofline):
@@ -18,7 +23,7 @@ same way (its own steps, HIP events on the scan stream, its own roofline):
   c2_host_streamed  the C2 suite over pinned host columns streamed through HBM (dq_scan_streamed): the
            end-to-end rate including the host link, never the headline value (N = 1).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--no-secondary]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--scaling weak|strong] [--no-secondary]
 """
 import argparse
 import ctypes
@@ -621,6 +626,65 @@ def measured_traffic(rows_per_gpu):
     return (found[0]["traffic_bytes_per_call"] / 1e9, found[1]) if found else None
 
 
+def spawn_ranks(args):
+    """`--gpus N` without a launcher: start N rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set, rendezvous on 127.0.0.1), forward rank 0's stdout, and return the first failing exit status. The
+    parent makes no GPU call (it never touches torch.cuda), so the children are fresh processes on their GPUs; if one
+    rank fails the others are stopped (by PID) instead of waiting in a collective."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    out0 = []
+    import threading
+    reader = threading.Thread(target=lambda: out0.extend(procs[0].stdout.read().decode().splitlines()))
+    reader.start()
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+        if p.returncode and not rc:
+            rc = p.returncode
+    reader.join()
+    for line in out0:
+        print(line, flush=True)
+    return rc
+
+
+def launch_check(args, world, rank):
+    """--launch-check: the launcher plumbing without any GPU call (CPU tests): gloo rendezvous, one all-reduce, rank 0
+    prints {"n_gpus": world, ...}."""
+    import torch
+    import torch.distributed as dist
+    assert world == args.gpus, (world, args.gpus)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        t = torch.tensor([rank + 1], dtype=torch.int64)
+        dist.all_reduce(t)
+        ranks_sum = int(t.item())
+        dist.destroy_process_group()
+    else:
+        ranks_sum = 1
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_sum": ranks_sum,
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -633,16 +697,32 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="only the headline C2 line")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
     ap.add_argument("--device-override", type=int, default=None, help="run every rank on this GPU (rehearsal)")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                    help="weak: every rank scans its own --rows-row shard (rows are independent partitions, the only "
+                         "exchange is the all-gather of the fixed-size states); strong: --rows split over the ranks")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        return launch_check(args, world, rank)
+    if world != args.gpus:
+        sys.exit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
+        assert dist.get_world_size() == args.gpus
+        # the measured multi-GPU path is RCCL over xGMI; gloo only as an explicit one-GPU rehearsal
+        assert dist.get_backend() == args.dist_backend and (args.dist_backend == "nccl" or
+                                                             args.device_override is not None), \
+            "multi-GPU bench runs on RCCL (nccl); gloo needs --device-override (rehearsal)"
     if args.device_override is not None:
         local = args.device_override
     torch.cuda.set_device(local)
@@ -660,7 +740,7 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
-    total = int(args.rows)
+    total = int(args.rows) * (world if args.scaling == "weak" else 1)
     # contiguous shards, aligned to the 2048-row tile
     per = (total + world - 1) // world
     per = (per + 2047) // 2048 * 2048
@@ -690,14 +770,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64+i64",
         "data": "synthetic (counter-based splitmix64 columns generated in HBM, SURVEY.md §8d)",
         "config": {"workload": "C2 fused scan suite: Size + {Completeness, Mean, Sum, Minimum, Maximum, "
                                "StandardDeviation} x 8 cols (4 fp64 + 4 int64, 1% nulls) = 49 ops",
                    "rows": total, "rows_per_gpu": nrows, "columns": len(names), "ops": c2.nops,
-                   "parallelism": "rows sharded dp%d + RCCL all-gather of states" % world},
+                   "parallelism": "rows sharded dp%d + %s all-gather of states"
+                                  % (world, "RCCL" if args.dist_backend == "nccl" else args.dist_backend),
+                   "dist_backend": args.dist_backend if world > 1 else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBPS, "traffic": traffic[0] if traffic else None,
                      "traffic_unit": "GB per dq_scan call (HBM FETCH+WRITE from rocprofv3 PMC, %s)"
