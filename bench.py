@@ -28,6 +28,7 @@ same way (its own steps, HIP events on the scan stream, its own roofline):
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -334,20 +335,50 @@ def c5_shard(torch, N, ctx, dev, rows, chunk_rows=125_000_000):
     return (chunks[0] if len(chunks) == 1 else ChunkedTable(chunks)), nbytes
 
 
+def c5_extra_analyzers(D):
+    """The rest of BASELINE config C5 / SURVEY §8d beside the ColumnProfiler's passes: ApproxQuantile(0.5) on every
+    numeric column and the grouping analyzers (Uniqueness, Entropy) on a low-cardinality and a free-text column."""
+    out = [D.ApproxQuantile(name, 0.5) for name, _ in C5_NUMERIC]
+    for col in ("s_cat100", "s_text0"):
+        out += [D.Uniqueness([col]), D.Entropy(col)]
+    return out
+
+
+def c5_step(D, t, extras):
+    """One C5 step: the 3-pass ColumnProfiler + one AnalysisRunner run of the extra analyzers."""
+    prof = D.ColumnProfiler.profile(t)
+    ctx = D.AnalysisRunner.onData(t).addAnalyzers(extras).run()
+    return prof, ctx
+
+
 def bench_c5(torch, N, D, ctx, dev, rows, steps):
     """BASELINE config C5 at one GPU's shard size: the full 3-pass ColumnProfiler (generic statistics, numeric
     statistics + KLL over the numeric and numeric-looking string columns after Spark's casts, exact histograms of
-    the low-cardinality columns) over a 20-column mixed table in HBM. Wall time per profile, sanity-checked."""
+    the low-cardinality columns) plus ApproxQuantile(0.5) on the numeric columns and Uniqueness / Entropy on a
+    low-cardinality and a free-text column, over a 20-column mixed table in HBM. Wall time per step, sanity-checked."""
     t, nbytes = c5_shard(torch, N, ctx, dev, rows)
+    extras = c5_extra_analyzers(D)
     prof = None
-    D.ColumnProfiler.profile(t)  # warm-up
+    c5_step(D, t, extras)  # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        prof = D.ColumnProfiler.profile(t)
+        prof, actx = c5_step(D, t, extras)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / steps
+    # the profiler alone (the r02-r04 C5 line), for comparison
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        D.ColumnProfiler.profile(t)
+    torch.cuda.synchronize()
+    el_profile = (time.perf_counter() - t0) / steps
     assert prof.numRecords == rows
+    for a in extras:
+        assert actx.metric(a).value.isSuccess, (a, actx.metric(a).value)
+    for name, _ in C5_NUMERIC:  # the median of a column the profiler also summarised lies inside its range
+        p = prof.profiles[name]
+        assert p.minimum <= actx.metric(D.ApproxQuantile(name, 0.5)).value.get() <= p.maximum, name
+    assert 0.0 < actx.metric(D.Entropy("s_cat100")).value.get() <= math.log(100) + 1e-12
     for name, p in prof.profiles.items():
         assert 0.94 < p.completeness < 0.96, (name, p.completeness)
     hist = {n: p.histogram for n, p in prof.profiles.items() if p.histogram is not None}
@@ -358,12 +389,19 @@ def bench_c5(torch, N, D, ctx, dev, rows, steps):
     ach = nbytes / el / 1e9
     c5_traffic = committed_json("c5_traffic_*.json", rows, need="traffic_bytes_per_call")
     passes = c5_pass_times(torch, D, t)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    D.AnalysisRunner.onData(t).addAnalyzers(extras).run()
+    torch.cuda.synchronize()
+    passes["extras_quantiles_grouping"] = round((time.perf_counter() - t0) * 1e3, 2)
     return {"workload": "C5 shard: ColumnProfiler passes 1-3 (Completeness, ApproxCountDistinct, DataType; Min / Max / "
                         "Mean / StdDev / Sum / KLL on 13 numeric and cast numeric-string columns; exact histograms of "
-                        "%d low-cardinality columns) over %d rows x 20 columns (5 fp64, 5 int64, 10 UTF-8), 5%% nulls, "
+                        "%d low-cardinality columns) + ApproxQuantile(0.5) x 10 numeric columns + Uniqueness / Entropy "
+                        "of s_cat100 and s_text0, over %d rows x 20 columns (5 fp64, 5 int64, 10 UTF-8), 5%% nulls, "
                         "held as %d row chunk(s) (one GPU's share of the 8-GPU 2e9-row table)"
                         % (len(hist), rows, len(getattr(t, "chunks", [t]))),
             "value": rows / el, "unit": "rows/s", "ms_per_step": el * 1e3,
+            "profile_only_ms": el_profile * 1e3,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": ach / PEAK_HBM_GBPS,
                          "traffic": c5_traffic[0]["traffic_bytes_per_call"] / 1e9 if c5_traffic else None,

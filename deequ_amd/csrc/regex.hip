@@ -23,10 +23,16 @@ namespace {
 
 enum RxOp : int32_t {
     RX_CHAR = 1, RX_CLASS, RX_ANY, RX_SPLIT, RX_JMP, RX_SAVE, RX_ASSERT, RX_BACKREF, RX_LOOK, RX_LOOKEND, RX_MARK,
-    RX_CHECK, RX_MATCH
+    RX_CHECK, RX_MATCH, RX_ATOMIC, RX_ATOMIC_END, RX_STEPBACK, RX_ATPOS
 };
-enum RxAssert : int32_t { AS_BOL = 0, AS_EOL, AS_WORDB, AS_NWORDB, AS_BEGIN, AS_END, AS_ENDZ };
-enum RxFrame : uint32_t { FR_BRANCH = 0, FR_CAP = 1, FR_LOOP = 2, FR_LOOK = 3 };
+// ^ / $ / \Z without and with MULTILINE, and their UNIX_LINES forms (only '\n' ends a line)
+enum RxAssert : int32_t {
+    AS_BOL = 0, AS_EOL, AS_WORDB, AS_NWORDB, AS_BEGIN, AS_END, AS_ENDZ, AS_MBOL, AS_MEOL, AS_EOL_UNIX, AS_MBOL_UNIX,
+    AS_MEOL_UNIX, AS_ENDZ_UNIX
+};
+// stack frames: a branch to retry, undo records (capture, empty-loop mark), a lookaround (its start position),
+// an atomic group's marker, a lookbehind's next start offset to try
+enum RxFrame : uint32_t { FR_BRANCH = 0, FR_CAP = 1, FR_LOOP = 2, FR_LOOK = 3, FR_ATOMIC = 4, FR_STEP = 5 };
 
 constexpr int kRxStack = 512;       // frames per lane
 constexpr int kRxSteps = 1 << 20;   // instruction budget per row
@@ -91,12 +97,33 @@ __device__ __forceinline__ bool is_word(int32_t c) {
 
 __device__ __forceinline__ bool in_class(const RxProg& p, int k, int32_t c) {
     const int first = p.classes[2 * k], cnt = p.classes[2 * k + 1];
-    for (int r = 0; r < cnt; ++r) {
-        const int32_t lo = p.ranges[2 * (first + r)], hi = p.ranges[2 * (first + r) + 1];
-        if (c < lo) return false;  // ranges are sorted
-        if (c <= hi) return true;
+    const int32_t* r = p.ranges + 2 * first;
+    if (cnt <= 8) {
+        for (int i = 0; i < cnt; ++i) {
+            if (c < r[2 * i]) return false;  // ranges are sorted and disjoint
+            if (c <= r[2 * i + 1]) return true;
+        }
+        return false;
+    }
+    int lo = 0, hi = cnt - 1;  // Unicode property classes: hundreds of ranges
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (c < r[2 * mid]) hi = mid - 1;
+        else if (c > r[2 * mid + 1]) lo = mid + 1;
+        else return true;
     }
     return false;
+}
+
+// Java's CASE_INSENSITIVE back reference (CIBackRef): code points equal, or equal after toUpperCase / toLowerCase
+// (US-ASCII letters; with UNICODE_CASE also Latin-1 and the Greek / Cyrillic blocks' simple +-32 / +-80 pairs).
+__device__ __forceinline__ int32_t fold_ci(int32_t c, bool unicode) {
+    if (c >= 'A' && c <= 'Z') return c + 32;
+    if (!unicode) return c;
+    if ((c >= 0xC0 && c <= 0xDE && c != 0xD7) || (c >= 0x391 && c <= 0x3AB && c != 0x3A2) || (c >= 0x410 && c <= 0x42F))
+        return c + 32;
+    if (c >= 0x400 && c <= 0x40F) return c + 80;
+    return c;
 }
 
 // $ without MULTILINE: end of input, or before a final line terminator ("\r\n" counts as one).
@@ -105,7 +132,38 @@ __device__ __forceinline__ bool at_eol(const uint8_t* s, int n, int i) {
     int len;
     const int32_t c = decode(s, n, i, len);
     if (c == '\r' && i + 1 < n && s[i + 1] == '\n') return i + 2 == n;
+    if (c == '\n' && i > 0 && s[i - 1] == '\r') return false;  // not between "\r" and "\n"
     return is_line_term(c) && i + len == n;
+}
+
+// MULTILINE ^: start of input, or after a line terminator, but never at the end of input ("Perl does not match ^ at
+// end of input even after newline", Java's Caret; not between the '\r' and '\n' of "\r\n").
+__device__ __forceinline__ bool at_mbol(const uint8_t* s, int n, int i) {
+    if (i == n) return false;
+    if (i == 0) return true;
+    const int32_t p = decode_prev(s, n, i);
+    if (p == '\r' && s[i] == '\n') return false;
+    return is_line_term(p);
+}
+
+// MULTILINE $: end of input, or before any line terminator (not between "\r" and "\n").
+__device__ __forceinline__ bool at_meol(const uint8_t* s, int n, int i) {
+    if (i == n) return true;
+    int len;
+    const int32_t c = decode(s, n, i, len);
+    if (c == '\n' && i > 0 && s[i - 1] == '\r') return false;
+    return is_line_term(c);
+}
+
+// The code point position k code points before byte i, or -1.
+__device__ __forceinline__ int back_cps(const uint8_t* s, int i, int k) {
+    for (; k > 0; --k) {
+        if (i <= 0) return -1;
+        --i;
+        int steps = 0;
+        while (i > 0 && (s[i] & 0xC0) == 0x80 && steps < 3) { --i; ++steps; }
+    }
+    return i;
 }
 
 __device__ __forceinline__ uint64_t frame(uint32_t kind, uint32_t a, int32_t pos) {
@@ -157,6 +215,11 @@ __device__ int rx_match_at(const RxProg& p, const uint8_t* s, int n, int start, 
                     case AS_BOL: case AS_BEGIN: r = pos == 0; break;
                     case AS_EOL: case AS_ENDZ: r = at_eol(s, n, pos); break;
                     case AS_END: r = pos == n; break;
+                    case AS_MBOL: r = at_mbol(s, n, pos); break;
+                    case AS_MEOL: r = at_meol(s, n, pos); break;
+                    case AS_EOL_UNIX: case AS_ENDZ_UNIX: r = pos == n || (pos + 1 == n && s[pos] == '\n'); break;
+                    case AS_MBOL_UNIX: r = pos < n && (pos == 0 || s[pos - 1] == '\n'); break;
+                    case AS_MEOL_UNIX: r = pos == n || s[pos] == '\n'; break;
                     default: {
                         int len;
                         const bool left = pos > 0 && is_word(decode_prev(s, n, pos));
@@ -173,7 +236,22 @@ __device__ int rx_match_at(const RxProg& p, const uint8_t* s, int n, int start, 
                 if (g0 < 0 || g1 < 0) { ok = false; break; }  // Java: a reference to an unset group fails
                 const int len = g1 - g0;
                 if (pos + len > n) { ok = false; break; }
-                for (int k = 0; k < len && ok; ++k) ok = s[g0 + k] == s[pos + k];
+                if (b == 0) {
+                    for (int k = 0; k < len && ok; ++k) ok = s[g0 + k] == s[pos + k];
+                } else {  // case-insensitive: code point by code point
+                    int i0 = g0, i1 = pos;
+                    while (ok && i0 < g1) {
+                        int l0, l1;
+                        const int32_t c0 = decode(s, n, i0, l0);
+                        if (i1 >= n) { ok = false; break; }
+                        const int32_t c1 = decode(s, n, i1, l1);
+                        ok = c0 == c1 || fold_ci(c0, b == 2) == fold_ci(c1, b == 2);
+                        i0 += l0;
+                        i1 += l1;
+                    }
+                    if (ok) { pos = i1; ++pc; }
+                    break;
+                }
                 if (ok) { pos += len; ++pc; }
                 break;
             }
@@ -214,6 +292,45 @@ __device__ int rx_match_at(const RxProg& p, const uint8_t* s, int n, int start, 
             case RX_CHECK:
                 if (pos == loops[a]) ok = false; else ++pc;  // an empty iteration does not repeat
                 break;
+            case RX_ATOMIC:
+                if (top >= kRxStack) return -2;
+                stk[top++] = frame(FR_ATOMIC, 0, pos);
+                ++pc;
+                break;
+            case RX_ATOMIC_END: {
+                // (?>X) matched: drop X's untried alternatives (branch / lookbehind-start frames) above the marker, keep
+                // the undo records so that backtracking past the group still restores captures and loop marks
+                int j = top - 1;
+                while (j >= 0 && (uint32_t)(stk[j] >> 60) != FR_ATOMIC) --j;
+                if (j < 0) return -2;
+                int w = j;
+                for (int k = j + 1; k < top; ++k) {
+                    const uint32_t kind = (uint32_t)(stk[k] >> 60);
+                    if (kind == FR_CAP || kind == FR_LOOP) stk[w++] = stk[k];
+                }
+                top = w;
+                ++pc;
+                break;
+            }
+            case RX_STEPBACK:
+            case RX_ATPOS: {
+                // lookbehind: the LOOK frame below holds the position the body must end at
+                int j = top - 1;
+                while (j >= 0 && (uint32_t)(stk[j] >> 60) != FR_LOOK) --j;
+                if (j < 0) return -2;
+                const int32_t target = (int32_t)(uint32_t)stk[j];
+                if (op == RX_ATPOS) {
+                    if (pos == target) ++pc; else ok = false;
+                    break;
+                }
+                const int st = back_cps(s, target, a);  // first try: `a` (the minimum length) code points back
+                if (st < 0 || a > b) { ok = false; break; }
+                if (top >= kRxStack) return -2;
+                stk[top++] = frame(FR_STEP, (uint32_t)pc, a + 1);
+                pos = st;
+                ++pc;
+                break;
+            }
             case RX_MATCH: return pos;
             default: return -2;
         }
@@ -227,6 +344,20 @@ __device__ int rx_match_at(const RxProg& p, const uint8_t* s, int n, int start, 
             if (kind == FR_BRANCH) { pc = (int)arg; pos = fp; break; }
             if (kind == FR_CAP) { caps[arg] = fp; continue; }
             if (kind == FR_LOOP) { loops[arg] = fp; continue; }
+            if (kind == FR_ATOMIC) continue;
+            if (kind == FR_STEP) {  // the lookbehind body failed from this start: one more code point back
+                const int k = fp, maxk = p.ins[3 * arg + 2];
+                if (k > maxk) continue;
+                int j = top - 1;
+                while (j >= 0 && (uint32_t)(stk[j] >> 60) != FR_LOOK) --j;
+                if (j < 0) return -2;
+                const int st = back_cps(s, (int32_t)(uint32_t)stk[j], k);
+                if (st < 0) continue;
+                stk[top++] = frame(FR_STEP, arg, k + 1);
+                pos = st;
+                pc = (int)arg + 1;
+                break;
+            }
             // FR_LOOK: the lookahead body failed
             if (arg >> 24) { pos = fp; pc = (int)(arg & 0xFFFFFF); break; }  // (?!X): succeeds
         }

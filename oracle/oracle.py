@@ -1058,12 +1058,13 @@ def expected_state(table, analyzer, exact=True):
         return S.ApproxCountDistinctState([int(w) for w in words])
     if name == "PatternMatch":
         # sum(when(regexp_extract(col, p, 0) != "", 1).otherwise(0)) under where (A/PatternMatch.scala:46-48):
-        # Python's `re` is, like java.util.regex, a leftmost-first backtracking engine; re.ASCII gives
-        # Java's default \d \s \w classes (Java's Unicode \b, `.` and `$` line terminators differ
-        # only on non-ASCII word characters / \r, \u0085, \u2028, \u2029, absent from the tests).
-        import re
+        # the third-party `regex` module (2026.7.19, V1 syntax) is, like java.util.regex, a leftmost-first
+        # backtracking engine with atomic groups, possessive quantifiers, lookbehind, named groups, nested sets
+        # and `&&` intersections; regex.ASCII gives Java's default \d \s \w classes and ASCII-only
+        # CASE_INSENSITIVE (Java's Unicode \b, `.` and `$` line terminators differ only on non-ASCII word
+        # characters / \r, \u0085, \u2028, \u2029, absent from the tests).
         c = table[analyzer.column]
-        rx = re.compile(java_regex_to_python(analyzer.pattern), re.ASCII)
+        rx = compile_java_regex(analyzer.pattern)
         wt, _ = _where(table, analyzer.where)
         valid = _valid(c)
         cnt, present = _cond_count(table, analyzer.where)
@@ -1100,19 +1101,133 @@ def expected_state(table, analyzer, exact=True):
     raise ValueError("no oracle for %s" % name)
 
 
+_POSIX_ORACLE = {  # java.util.regex.Pattern's US-ASCII POSIX classes, as set contents
+    "Lower": "a-z", "Upper": "A-Z", "ASCII": "\\x00-\\x7f", "Alpha": "a-zA-Z", "Digit": "0-9", "Alnum": "a-zA-Z0-9",
+    "Punct": "!-/:-@\\[-`{-~", "Graph": "!-~", "Print": " -~", "Blank": " \\t", "Cntrl": "\\x00-\\x1f\\x7f",
+    "XDigit": "0-9a-fA-F", "Space": " \\t\\n\\x0b\\f\\r",
+}
+_JAVA_PROPS_ORACLE = {"javaLowerCase": "Ll", "javaUpperCase": "Lu", "javaLetter": "L", "javaDigit": "Nd",
+                      "javaAlphabetic": "Alphabetic", "IsAlphabetic": "Alphabetic", "IsLetter": "L",
+                      "IsDigit": "Nd", "IsLowercase": "Ll", "IsUppercase": "Lu", "IsPunctuation": "P",
+                      "IsControl": "Cc", "IsWhite_Space": "White_Space"}
+
+
 def java_regex_to_python(p):
-    r"""The two java.util.regex anchors Python spells differently: \z (end of input) -> \Z and
-    \Z (end, or before a final line terminator) -> (?=\n?\Z)."""
-    out, i = [], 0
+    """A java.util.regex pattern in the `regex` module's V1 syntax: the spellings that differ are rewritten —
+    \\z -> \\Z, \\Z -> (?=\\n?\\Z), POSIX \\p{Lower}..\\p{Space} -> their US-ASCII sets, java* / Is* properties ->
+    Unicode property names, \\h \\v \\R \\e \\cX \\x{..} \\0oo -> explicit forms, \\Q..\\E -> escaped text, the
+    Java-only flags d / u dropped (inputs hold no \\r and no non-ASCII letters), and a MULTILINE ^ never matching at
+    the end of input (Java's Caret)."""
+    import regex
+    out, i, depth = [], 0, 0
+    multiline = False
     while i < len(p):
-        if p[i] == "\\" and i + 1 < len(p):
+        ch = p[i]
+        if ch == "\\" and i + 1 < len(p):
             nxt = p[i + 1]
-            out.append("\\Z" if nxt == "z" else ("(?=\\n?\\Z)" if nxt == "Z" else p[i:i + 2]))
+            if nxt == "z":
+                out.append("\\Z")
+            elif nxt == "Z":
+                out.append("(?=\\n?\\Z)")
+            elif nxt in "pP":
+                if i + 2 < len(p) and p[i + 2] == "{":
+                    j = p.index("}", i)
+                    name = p[i + 3:j]
+                else:
+                    j, name = i + 2, p[i + 2]
+                neg = nxt == "P"
+                if name.startswith("^"):
+                    neg, name = not neg, name[1:]
+                if name in _POSIX_ORACLE:
+                    body = _POSIX_ORACLE[name]
+                    out.append(("[^%s]" if neg else "[%s]") % body if depth == 0 else
+                               ("[^%s]" % body if neg else body))
+                else:
+                    name = _JAVA_PROPS_ORACLE.get(name, name)
+                    for prefix in ("general_category=", "gc=", "Is"):
+                        if name.startswith(prefix):
+                            name = name[len(prefix):]
+                    out.append("\\%s{%s}" % ("P" if neg else "p", name))
+                i = j + 1
+                continue
+            elif nxt == "h":
+                out.append("[ \\t\\xa0\\u1680\\u180e\\u2000-\\u200a\\u202f\\u205f\\u3000]" if depth == 0 else
+                           " \\t\\xa0\\u1680\\u180e\\u2000-\\u200a\\u202f\\u205f\\u3000")
+            elif nxt == "v":
+                out.append("[\\n\\x0b\\f\\r\\x85\\u2028\\u2029]" if depth == 0 else "\\n\\x0b\\f\\r\\x85\\u2028\\u2029")
+            elif nxt == "R":
+                out.append("(?>\\r\\n|[\\n\\x0b\\f\\r\\x85\\u2028\\u2029])")
+            elif nxt == "k":
+                j = p.index(">", i)
+                out.append("(?P=%s)" % p[i + 3:j])
+                i = j + 1
+                continue
+            elif nxt == "e":
+                out.append("\\x1b")
+            elif nxt == "c":
+                out.append("\\x%02x" % (ord(p[i + 2]) ^ 64))
+                i += 3
+                continue
+            elif nxt == "x" and i + 2 < len(p) and p[i + 2] == "{":
+                j = p.index("}", i)
+                out.append("\\U%08x" % int(p[i + 3:j], 16))
+                i = j + 1
+                continue
+            elif nxt == "0":
+                j = i + 2
+                while j < len(p) and j < i + 5 and p[j] in "01234567" and int(p[i + 2:j + 1], 8) <= 0o377:
+                    j += 1
+                out.append("\\x%02x" % int(p[i + 2:j], 8))
+                i = j
+                continue
+            elif nxt == "Q":
+                j = p.find("\\E", i + 2)
+                lit = p[i + 2:] if j < 0 else p[i + 2:j]
+                out.append(regex.escape(lit, special_only=False) if depth == 0 else
+                           "".join("\\" + c if not c.isalnum() else c for c in lit))
+                i = len(p) if j < 0 else j + 2
+                continue
+            else:
+                out.append(p[i:i + 2])
             i += 2
-        else:
-            out.append(p[i])
+            continue
+        if ch == "[":
+            depth += 1
+        elif ch == "]" and depth > 0 and not (out and out[-1] in ("[", "[^")):
+            depth -= 1
+        elif ch == "(" and p[i + 1:i + 2] == "?" and depth == 0:
+            j = i + 2
+            flags = ""
+            while j < len(p) and (p[j].isalpha() or p[j] == "-"):
+                flags += p[j]
+                j += 1
+            if flags and j < len(p) and p[j] in ":)":
+                if "m" in flags.split("-")[0]:
+                    multiline = True
+                kept = "".join(c for c in flags if c not in "du")
+                if kept.strip("-") == "":
+                    out.append("(?:" if p[j] == ":" else "")
+                    if p[j] == ")":
+                        i = j + 1
+                        continue
+                    i = j + 1
+                    continue
+                out.append("(?" + kept.rstrip("-") + p[j])
+                i = j + 1
+                continue
+        elif ch == "^" and depth == 0 and multiline:
+            out.append("(?:^(?!\\Z))")
             i += 1
+            continue
+        out.append("[" if ch == "[" and depth == 1 and (i + 1 >= len(p) or p[i + 1] != "^") else ch)
+        i += 1
     return "".join(out)
+
+
+def compile_java_regex(pattern):
+    """The oracle's compiled form of a java.util.regex pattern (`regex` module, V1, ASCII classes)."""
+    import regex
+    return regex.compile(java_regex_to_python(pattern), regex.ASCII | regex.V1)
 
 
 # StatefulDataType's regexes (C/StatefulDataType.scala:36-38), ASCII \d as in java.util.regex

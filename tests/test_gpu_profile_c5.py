@@ -239,3 +239,41 @@ def test_c5_chunked_shard_at_scale_against_oracle():
         words = np.zeros(52, dtype=np.int64)
         O.lib().oracle_hll_pack(regs.ctypes.data, words.ctypes.data)
         assert p.approximateNumDistinctValues == int(O.hll_count([int(w) for w in words])), name
+
+
+def _check_c5_extras(full, ctx, extras):
+    """ApproxQuantile(0.5) inside the GK rank bound of the exact order statistics (relativeError 0.01; a merged
+    summary of several partitions keeps the bound, QuantileSummaries.merge), Uniqueness / Entropy against the oracle's
+    exact grouping (A/ApproxQuantile.scala:28-103, A/Uniqueness.scala:29-36, A/Entropy.scala:28-42)."""
+    for a in extras:
+        m = ctx.metric(a).value
+        assert m.isSuccess, (a, m)
+        if isinstance(a, D.ApproxQuantile):
+            s = O.java_sorted_doubles(full, a.column)
+            n = len(s)
+            lo, hi = O.rank_interval(s, m.get())
+            target = max(1, math.ceil(0.5 * n))
+            slack = math.ceil(0.01 * n) + 1
+            assert lo - slack <= target <= hi + slack, (a, m.get(), lo, hi, target)
+        else:
+            col = a.columns[0] if isinstance(a, D.Uniqueness) else a.column
+            freq, n = O.frequencies(full, [col])
+            exp = O.grouping_summary(freq, n)
+            want = exp["num_unique"] / n if isinstance(a, D.Uniqueness) else exp["entropy"]
+            assert _close(m.get(), want), (a, m.get(), want)
+
+
+def test_c5_quantiles_and_grouping_against_oracle():
+    """The part of BASELINE config C5 beside the ColumnProfiler (`ApproxQuantile(0.5)` on numerics; the
+    grouping analyzers): the analyzer list bench.py's C5 line times, on the reduced table, whole and as 3 row chunks."""
+    import bench
+    pat = c5_arrow(ROWS)
+    full = Table.from_arrow(pat)
+    extras = [D.ApproxQuantile(c, 0.5) for c in pat.column_names[:10]]
+    extras += [D.Uniqueness(["s_cat100"]), D.Entropy("s_cat100"), D.Uniqueness(["s_text0"]), D.Entropy("s_text0")]
+    assert len(bench.c5_extra_analyzers(D)) == len(extras)  # the bench's list has the same shape
+    dev = Table.from_arrow(pat).to_device()
+    _check_c5_extras(full, D.AnalysisRunner.onData(dev).addAnalyzers(extras).run(), extras)
+    cut = [0, ROWS // 3, ROWS // 3 + ROWS // 4 + 7, ROWS]
+    ct = D.ChunkedTable([Table.from_arrow(pat.slice(a, b - a)).to_device() for a, b in zip(cut, cut[1:])])
+    _check_c5_extras(full, D.AnalysisRunner.onData(ct).addAnalyzers(extras).run(), extras)

@@ -73,7 +73,7 @@ def test_pattern_match_over_integral_and_boolean_columns():
 
 def test_unsupported_construct_fails_only_that_analyzer():
     t = Table([_column_from_pylist("s", "string", ["a", "b", None])])
-    bad = D.PatternMatch("s", r"(?i)a")
+    bad = D.PatternMatch("s", r"(?<=a+)b")  # Java: "Look-behind group does not have an obvious maximum length"
     ctx = D.AnalysisRunner.onData(t).addAnalyzers([bad, D.Completeness("s"), D.PatternMatch("s", "a")]).run()
     assert ctx.metric(bad).value.isFailure
     assert ctx.metric(D.Completeness("s")).value.get() == 2.0 / 3.0
@@ -152,3 +152,75 @@ def test_pattern_match_over_decimal_date_and_timestamp_columns():
         assert g == exp, (a.column, a.pattern, g, exp)
     for a, g in zip(analyzers[:60], got[:60]):
         assert g.numMatches >= 1, (a.column, a.pattern)  # the exact rendering of the special value itself
+
+
+# java.util.regex constructs beyond the r04 subset (VERDICT r04 missing #3), each compared with the oracle (the
+# `regex` module over the pattern's V1 spelling, oracle/oracle.py java_regex_to_python)
+EXTENDED = [
+    r"(?i)foo", r"(?i:AB)c", r"a(?i)B", r"(?-i)foo", r"(?i)[a-c]+Z", r"(?i)(ab)\1", r"(?i)[^a]b",
+    r"(?m)^foo", r"(?m)o$", r"(?m)^$", r"(?s)a.*z", r"a.*z", r"(?x) f o o  # comment", r"(?x)\d \d",
+    r"(?<=foo)bar", r"(?<!foo)bar", r"(?<=\d{2})-", r"(?<=a|bc)d", r"(?<![a-z])\d+", r"(?<=^|\s)foo",
+    r"(?<w>[a-z])\k<w>", r"(?<year>\d{4})-(?<m>\d\d)",
+    r"(?>a+)b", r"(?>ab|a)c", r"a++b", r"a*+a", r"\d++-", r"[a-z]?+z", r"(?:ab){1,3}+c",
+    r"\p{Lower}+", r"\p{Upper}", r"\p{Alpha}\p{Digit}", r"\p{Alnum}{3}", r"\p{Punct}", r"\P{Alpha}+",
+    r"[\p{Digit}x]+", r"\p{XDigit}{2}", r"\p{Space}", r"\p{L}+", r"\p{Lu}", r"\pL\pN", r"\p{IsAlphabetic}{4}",
+    r"\p{javaLowerCase}", r"[^\p{Alpha}]", r"\p{Blank}",
+    r"[a-z&&[^aeiou]]+", r"[a-d[m-p]]", r"[\w&&[^\d]]+", r"[a-f&&c-z&&[^e]]",
+    r"\Qa.b\E", r"x\Q*\E", r"\h", r"\v", r"\R", r"\x{41}", r"\0101", r"\cJ", r"\Gfoo",
+]
+
+EXT_WORDS = ["foo", "FOO", "Foo", "fOo bar", "foobar", "xbar", "bar", "12-", "ab-", "12-34", "ad", "bcd", "xd",
+             "aa", "abab", "ABAB", "AbaB", "aab", "ac", "abc", "abcab", "aaa", "aaab", "1999-12", "a.b", "axb", "x*",
+             "A", "line1\nfoo", "foo\n", "o\nfoo", "a\nz", "az", "\n", "", "xyz", "e", "cd", "9f", "HELLO world",
+             "a\tb", "A1", "abcZ", "ABCz", "ccZ", "1-", "22-"]
+
+
+def ext_strings(rng, n):
+    chars = list("abcdefoxzABZ019 -.\n*\t") + ["foo", "bar", "FOO"]
+    out = []
+    for _ in range(n):
+        if rng.random() < 0.5:
+            out.append(EXT_WORDS[rng.integers(len(EXT_WORDS))])
+        else:
+            out.append("".join(chars[j] for j in rng.integers(0, len(chars), int(rng.integers(0, 16)))))
+    return out
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_extended_java_regex_constructs_match_the_oracle(device):
+    """Inline flags (?i) (?m) (?s) (?x) scoped like Java's, lookbehind, named groups, atomic groups, possessive
+    quantifiers, POSIX / Unicode property classes, nested classes and && intersections, \\Q..\\E and Java 8's
+    \\h \\v \\R: exact PatternMatch counts against the oracle over ASCII strings with '\\n' line breaks."""
+    rng = np.random.default_rng(19)
+    n = 5000
+    items = [None if rng.random() < 0.05 else s for s in ext_strings(rng, n)]
+    t = Table([_column_from_pylist("s", "string", items)])
+    if device:
+        t.to_device(0)
+    analyzers = [D.PatternMatch("s", p) for p in EXTENDED]
+    got = states(t, analyzers)
+    for a, g in zip(analyzers, got):
+        exp = O.expected_state(t, a)
+        assert g == exp, (a.pattern, g, exp)
+
+
+def test_extended_regex_known_answers():
+    """Java 8 behaviours the oracle engine spells differently, pinned by hand (java.util.regex documentation):
+    MULTILINE ^ never matches at the end of input, a CASE_INSENSITIVE back reference, a lookbehind trying its
+    shortest start first, possessive loops that do not give back, and intersections."""
+    cases = [
+        (r"(?m)^", ["", "a", "a\n"], [0, 0, 0]),          # ^ at 0 is an empty match: never counts anyway
+        (r"(?m)^x", ["x", "a\nx", "a\n", "\nx"], [1, 1, 0, 1]),
+        (r"(?i)(a)\1", ["aA", "Aa", "ab"], [1, 1, 0]),
+        (r"(?<=ab|b)c", ["abc", "bc", "ac"], [1, 1, 0]),
+        (r"a++a", ["aaaa", "aab"], [0, 0]),
+        (r"(?>a|ab)c", ["abc", "ac"], [0, 1]),
+        (r"[a-z&&[def]]", ["d", "a", "F"], [1, 0, 0]),
+        (r"(?i)[a-z&&[def]]", ["D", "a"], [1, 0]),
+        (r"(?x) a \  b", ["a b", "ab"], [1, 0]),
+        (r"\p{Lu}\p{Ll}", ["Ab", "ab", "AB"], [1, 0, 0]),
+    ]
+    for pat, words, hits in cases:
+        t = Table([_column_from_pylist("s", "string", words)])
+        st = states(t, [D.PatternMatch("s", pat)])[0]
+        assert st.numMatches == sum(hits), (pat, st, hits)
