@@ -560,10 +560,21 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                 depth -= arg;
             } else if (op == DQ_P_COALESCE) {
                 depth -= arg - 1;
+            } else if (op == DQ_P_CASE) {
+                if (arg < 2) return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: CASE without WHEN", p);
+                depth -= arg - 1;  // 2 * #WHEN + has ELSE operands -> 1
+            } else if (op == DQ_P_SUBSTR) {
+                depth -= 2;
             } else if (op == DQ_P_NOT || op == DQ_P_IS_NULL || op == DQ_P_IS_NOT_NULL || op == DQ_P_NEG ||
                        op == DQ_P_LIKE || op == DQ_P_LENGTH || op == DQ_P_CAST_DOUBLE || op == DQ_P_CAST_LONG ||
-                       op == DQ_P_CAST_STRING_NUM) {
+                       op == DQ_P_CAST_STRING_NUM || op == DQ_P_RLIKE || op == DQ_P_LOWER || op == DQ_P_UPPER ||
+                       op == DQ_P_TRIM || op == DQ_P_ISNAN || op == DQ_P_ABS || op == DQ_P_YEAR || op == DQ_P_MONTH ||
+                       op == DQ_P_DAY) {
                 if (op == DQ_P_LIKE && (arg < 0 || arg >= pr.n_consts)) return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: bad LIKE pattern", p);
+                if (op == DQ_P_RLIKE &&
+                    (arg < 0 || arg >= pr.n_consts || pr.consts[arg].tag != DQ_V_STRING || pr.consts[arg].str_len < 32 ||
+                     (pr.consts[arg].str_offset & 3) || pr.consts[arg].str_offset + pr.consts[arg].str_len > pr.strings_len))
+                    return fail(ctx, DQ_ERR_PREDICATE, "predicate %d: malformed RLIKE program", p);
             } else {
                 --depth;
             }
@@ -1154,9 +1165,12 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
                     launch_pred_simple(ps, (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p], ctx->stream);
                     ctx->kernel_launches[DQ_KERNEL_PRED_SIMPLE]++;
                 } else {
-                    launch_predicate((const PredProgram*)pprog[p], (const PredColumn*)pcols, nrows, pwords, pt[p], pn[p],
-                                     ctx->stream);
+                    bool rx = false;
+                    for (int k = 0; k + 1 < pr.code_len; k += 2) rx |= pr.code[k] == DQ_P_RLIKE;
+                    launch_predicate((const PredProgram*)pprog[p], rx, rx_status + p, (const PredColumn*)pcols, nrows,
+                                     pwords, pt[p], pn[p], ctx->stream);
                     ctx->kernel_launches[DQ_KERNEL_PRED_VM]++;
+                    any_regex |= rx;
                 }
                 DQ_HIP(ctx, hipGetLastError());
             }

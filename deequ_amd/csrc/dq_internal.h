@@ -343,7 +343,9 @@ void launch_pred_simple(const PredSimple& prog, const PredColumn* cols_dev, int6
 // counts into partials[wslot * gstride + block] for `grid` blocks.
 void launch_where_masks(const WhereOut* wo_dev, const PredSimple& prog, const PredColumn* cols_dev, int64_t nrows,
                         int64_t padded_words, SlotPartial* partials, int wslot, int gstride, int grid, hipStream_t s);
-void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
+// rx: the program holds RLIKE (the kernel variant with the regex engine; a value past its backtracking budget sets
+// *status).
+void launch_predicate(const PredProgram* prog_dev, bool rx, int32_t* status, const PredColumn* cols_dev, int64_t nrows,
                       int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s);
 int string_scan_grid(int cus, int64_t nrows);
 void launch_string_scan(const StrSlot* slots, int nslots, int64_t nrows, int grid, int gstride, StrPartial* partials,

@@ -13,6 +13,8 @@
 #include "dq_common.h"
 #include "dq_internal.h"
 #include "dq_parse.h"
+#include "java_dtoa.h"
+#include "rx_engine.h"
 
 namespace dq {
 
@@ -25,6 +27,7 @@ struct Val {
     double d;      // DOUBLE
     const uint8_t* s;
     int32_t slen;
+    int32_t xf;    // STRING read through lower() / upper(): 0 none, 1 lower, 2 upper (rx::case_map)
 };
 
 __device__ __forceinline__ Val vnull() {
@@ -35,6 +38,7 @@ __device__ __forceinline__ Val vnull() {
     v.d = 0.0;
     v.s = nullptr;
     v.slen = 0;
+    v.xf = 0;
     return v;
 }
 __device__ __forceinline__ Val vbool(bool b) {
@@ -138,22 +142,56 @@ __device__ int cmp_bytes(const uint8_t* a, int na, const uint8_t* b, int nb) {
     return na < nb ? -1 : (na > nb ? 1 : 0);
 }
 
+// Binary (UTF-8 byte) order of two strings, each possibly read through lower() / upper(): UTF-8 preserves code point
+// order, so the mapped code point sequences compare like their encodings.
+__device__ int cmp_str(const Val& a, const Val& b) {
+    if (a.xf == 0 && b.xf == 0) return cmp_bytes(a.s, a.slen, b.s, b.slen);
+    int i = 0, j = 0;
+    while (i < a.slen && j < b.slen) {
+        int la, lb;
+        const int32_t ca = rx::decode_xf(a.s, a.slen, i, la, a.xf), cb = rx::decode_xf(b.s, b.slen, j, lb, b.xf);
+        if (ca != cb) return ca < cb ? -1 : 1;
+        i += la;
+        j += lb;
+    }
+    return (i < a.slen) ? 1 : ((j < b.slen) ? -1 : 0);
+}
+
+// The bytes of a string value for the numeric parsers: a transformed value is mapped into `buf` (numbers are ASCII;
+// a longer value is parsed as stored -- it cannot be a number whose parse depends on letter case).
+__device__ __forceinline__ const uint8_t* str_bytes(const Val& v, uint8_t (&buf)[64], int& n) {
+    n = v.slen;
+    if (v.xf == 0 || v.slen > 64) return v.s;
+    for (int k = 0; k < v.slen; ++k) {
+        const uint8_t c = v.s[k];
+        buf[k] = c < 0x80 ? (uint8_t)rx::case_map(c, v.xf) : c;
+    }
+    return buf;
+}
+
+__device__ bool parse_double_v(const Val& v, double& out) {
+    uint8_t buf[64];
+    int n;
+    const uint8_t* p = str_bytes(v, buf, n);
+    return parse_double(p, n, out);
+}
+
 // Coerce a string operand against a numeric one the way Spark 2.x PromoteStrings does
 // (string -> double). Returns false when the string does not parse (comparison is NULL).
 __device__ bool compare(const Val& a, const Val& b, int& c) {
     if (a.tag == DQ_V_STRING && b.tag == DQ_V_STRING) {
-        c = cmp_bytes(a.s, a.slen, b.s, b.slen);
+        c = cmp_str(a, b);
         return true;
     }
     if (a.tag == DQ_V_STRING || b.tag == DQ_V_STRING) {
         double x, y;
         if (a.tag == DQ_V_STRING) {
-            if (!parse_double(a.s, a.slen, x)) return false;
+            if (!parse_double_v(a, x)) return false;
         } else {
             x = as_double(a);
         }
         if (b.tag == DQ_V_STRING) {
-            if (!parse_double(b.s, b.slen, y)) return false;
+            if (!parse_double_v(b, y)) return false;
         } else {
             y = as_double(b);
         }
@@ -207,6 +245,47 @@ __device__ bool like_match(const uint8_t* s, int ns, const uint8_t* p, int np) {
     return pi == np;
 }
 
+// LIKE over a value read through lower() / upper(): code point by code point ('_' = one character, '%' = any run,
+// '\\' escapes), backtracking to the last '%' like like_match.
+__device__ bool like_match_xf(const uint8_t* s, int ns, int xf, const uint8_t* p, int np) {
+    int si = 0, pi = 0, star_p = -1, star_s = 0;
+    while (si < ns) {
+        int ls;
+        const int32_t c = rx::decode_xf(s, ns, si, ls, xf);
+        if (pi < np && p[pi] == '%') {
+            star_p = ++pi;
+            star_s = si;
+            continue;
+        }
+        if (pi < np) {
+            const bool esc = p[pi] == '\\' && pi + 1 < np;
+            int lp;
+            const int32_t pc = rx::decode(p, np, esc ? pi + 1 : pi, lp);
+            if (!esc && pc == '_') {
+                si += ls;
+                pi += 1;
+                continue;
+            }
+            if (pc == c) {
+                si += ls;
+                pi += (esc ? 1 : 0) + lp;
+                continue;
+            }
+        }
+        if (star_p >= 0) {
+            pi = star_p;
+            int l0;
+            rx::decode(s, ns, star_s, l0);
+            star_s += l0;
+            si = star_s;
+            continue;
+        }
+        return false;
+    }
+    while (pi < np && p[pi] == '%') ++pi;
+    return pi == np;
+}
+
 __device__ __forceinline__ int utf8_chars(const uint8_t* s, int n) {
     int c = 0;
     for (int i = 0; i < n; ++i) c += (s[i] & 0xC0) != 0x80;
@@ -251,12 +330,12 @@ __device__ Val arith(int op, const Val& a, const Val& b) {
     Val x = a, y = b;
     if (x.tag == DQ_V_STRING) {
         double d;
-        if (!parse_double(x.s, x.slen, d)) return vnull();
+        if (!parse_double_v(x, d)) return vnull();
         x = vdouble(d);
     }
     if (y.tag == DQ_V_STRING) {
         double d;
-        if (!parse_double(y.s, y.slen, d)) return vnull();
+        if (!parse_double_v(y, d)) return vnull();
         y = vdouble(d);
     }
     const bool integral = x.tag != DQ_V_DOUBLE && y.tag != DQ_V_DOUBLE;
@@ -282,22 +361,60 @@ __device__ Val arith(int op, const Val& a, const Val& b) {
     }
 }
 
+// Spark 2.2 DateTimeUtils.getYear / getMonth / getDayOfMonth of a day number (days since 1970-01-01): the
+// proleptic Gregorian civil date of the day number, shifted back 10 days on or before 1582-10-04 (day -141428)
+// as getYearAndDayInYear does for the Julian-to-Gregorian gap.
+__device__ void spark_ymd(int64_t days, int64_t& y, int& m, int& d) {
+    if (days <= -141428) days -= 10;
+    const int64_t z = days + 719468;  // H. Hinnant's days_from_civil inverse
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+    const int64_t doe = z - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const int64_t mp = (5 * doy + 2) / 153;
+    d = (int)(doy - (153 * mp + 2) / 5 + 1);
+    m = (int)(mp < 10 ? mp + 3 : mp - 9);
+    y = yoe + era * 400 + (m <= 2 ? 1 : 0);
+}
+
+// Spark's Cast(x AS STRING) of a non-string operand of RLIKE into buf (rx_engine.h formatters, java_dtoa.h).
+__device__ int value_string(const Val& v, int spark_type, int scale, uint8_t* buf) {
+    if (v.tag == DQ_V_BOOL) {
+        const char* t = v.i ? "true" : "false";
+        const int n = v.i ? 4 : 5;
+        for (int k = 0; k < n; ++k) buf[k] = (uint8_t)t[k];
+        return n;
+    }
+    if (v.tag == DQ_V_DOUBLE) return spark_type == DQ_TYPE_FLOAT ? java_float_to_chars((float)v.d, buf)
+                                                                 : java_double_to_chars(v.d, buf);
+    if (spark_type == DQ_TYPE_DATE) return rx::format_date_days(v.i, buf);
+    if (spark_type == DQ_TYPE_TIMESTAMP) return rx::format_timestamp_utc(v.i, buf);
+    return rx::format_long(v.i, buf);
+}
+
 }  // namespace
 
+// RX: the program holds RLIKE (each lane then carries the regex engine's backtracking stack).
+template <bool RX>
 __global__ void __launch_bounds__(256)
 predicate_kernel(const PredProgram* __restrict__ progp, const PredColumn* __restrict__ cols, int64_t nrows,
-                 int64_t padded_words, uint64_t* __restrict__ out_t, uint64_t* __restrict__ out_nn) {
+                 int64_t padded_words, uint64_t* __restrict__ out_t, uint64_t* __restrict__ out_nn,
+                 int32_t* __restrict__ status) {
     const PredProgram prog = *progp;
     const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool t = false, nn = false;
     if (row < nrows) {
         Val st[kPredStack];
+        int st_type[kPredStack];  // Spark type of a value loaded straight from a column (RLIKE's string cast), else 0
         int sp = 0;
         for (int pc = 0; pc + 1 < prog.code_len; pc += 2) {
             const int op = prog.code[pc];
             const int arg = prog.code[pc + 1];
             switch (op) {
-                case DQ_P_COL: st[sp++] = load_col(cols[arg], row); break;
+                case DQ_P_COL:
+                    st_type[sp] = cols[arg].spark_type;
+                    st[sp++] = load_col(cols[arg], row);
+                    break;
                 case DQ_P_CONST: {
                     const dq_const k = prog.consts[arg];
                     Val v = vnull();
@@ -307,10 +424,11 @@ predicate_kernel(const PredProgram* __restrict__ progp, const PredColumn* __rest
                     v.d = k.f64;
                     v.s = prog.strings + k.str_offset;
                     v.slen = k.str_len;
+                    st_type[sp] = 0;
                     st[sp++] = v;
                     break;
                 }
-                case DQ_P_NULL: st[sp++] = vnull(); break;
+                case DQ_P_NULL: st_type[sp] = 0; st[sp++] = vnull(); break;
                 case DQ_P_EQ: case DQ_P_NE: case DQ_P_LT: case DQ_P_LE: case DQ_P_GT: case DQ_P_GE: {
                     const Val b = st[--sp];
                     const Val a = st[--sp];
@@ -414,10 +532,150 @@ predicate_kernel(const PredProgram* __restrict__ progp, const PredColumn* __rest
                     const Val a = st[sp - 1];
                     if (!a.null && a.tag == DQ_V_STRING) {
                         const dq_const k = prog.consts[arg];
-                        st[sp - 1] = vbool(like_match(a.s, a.slen, prog.strings + k.str_offset, k.str_len));
+                        st[sp - 1] = vbool(a.xf ? like_match_xf(a.s, a.slen, a.xf, prog.strings + k.str_offset, k.str_len)
+                                                : like_match(a.s, a.slen, prog.strings + k.str_offset, k.str_len));
                     } else {
                         st[sp - 1] = vnull();
                     }
+                    break;
+                }
+                case DQ_P_RLIKE: {
+                    // str RLIKE regex = Pattern.compile(regex).matcher(str).find(): any match, also an empty one
+                    const Val a = st[sp - 1];
+                    if (a.null) break;
+                    if (RX) {
+                        const dq_const k = prog.consts[arg];
+                        const int32_t* image = reinterpret_cast<const int32_t*>(prog.strings + k.str_offset);
+                        rx::RxProg rp;
+                        rp.ninstr = image[1];
+                        rp.anchored = image[6];
+                        rp.ins = image + 8;
+                        rp.classes = rp.ins + 3 * rp.ninstr;
+                        rp.ranges = rp.classes + 2 * image[2];
+                        uint8_t buf[40];
+                        const uint8_t* sv = a.s;
+                        int n = a.slen, xf = a.xf;
+                        if (a.tag != DQ_V_STRING) {
+                            n = value_string(a, st_type[sp - 1], 0, buf);
+                            sv = buf;
+                            xf = 0;
+                        }
+                        uint64_t stk[rx::kRxStack];
+                        bool found = false;
+                        for (int start = 0; start <= n;) {
+                            const int end = rx::rx_match_at(rp, sv, n, start, stk, xf);
+                            if (end == -2) {
+                                atomicOr(status, 1);
+                                break;
+                            }
+                            if (end >= 0) {
+                                found = true;
+                                break;
+                            }
+                            if (rp.anchored || start == n) break;
+                            int len;
+                            rx::decode(sv, n, start, len);
+                            start += len;
+                        }
+                        st[sp - 1] = vbool(found);
+                    }
+                    st_type[sp - 1] = 0;
+                    break;
+                }
+                case DQ_P_LOWER: case DQ_P_UPPER: {
+                    Val& a = st[sp - 1];
+                    // a number / boolean's string form has no letters to map: the value stands (a comparison with it
+                    // coerces the same way)
+                    if (!a.null && a.tag == DQ_V_STRING) a.xf = op == DQ_P_LOWER ? 1 : 2;
+                    st_type[sp - 1] = 0;
+                    break;
+                }
+                case DQ_P_TRIM: {  // Spark 2.2 UTF8String.trim / trimLeft / trimRight: ASCII spaces (0x20) only
+                    Val& a = st[sp - 1];
+                    if (!a.null && a.tag == DQ_V_STRING) {
+                        if (arg != 2) while (a.slen > 0 && a.s[0] == ' ') { ++a.s; --a.slen; }
+                        if (arg != 1) while (a.slen > 0 && a.s[a.slen - 1] == ' ') --a.slen;
+                    }  // a number's string form has no spaces to trim
+                    st_type[sp - 1] = 0;
+                    break;
+                }
+                case DQ_P_SUBSTR: {  // substring(str, pos, len): UTF8String.substringSQL (1-based, 0 = 1, < 0 from the end)
+                    const Val ln = st[--sp];
+                    const Val ps = st[--sp];
+                    Val& a = st[sp - 1];
+                    st_type[sp - 1] = 0;
+                    if (a.null || ps.null || ln.null || a.tag != DQ_V_STRING) { a = vnull(); break; }
+                    const int64_t pos = ps.tag == DQ_V_DOUBLE ? (int64_t)ps.d : ps.i;
+                    const int64_t length = ln.tag == DQ_V_DOUBLE ? (int64_t)ln.d : ln.i;
+                    const int64_t nch = utf8_chars(a.s, a.slen);
+                    const int64_t start = pos > 0 ? pos - 1 : (pos < 0 ? nch + pos : 0);
+                    const int64_t until = length >= 2147483647 ? nch : start + length;
+                    if (until <= start || start >= a.slen) { a.slen = 0; break; }
+                    int i = 0;
+                    int64_t c = 0;
+                    while (i < a.slen && c < start) { int l; rx::decode(a.s, a.slen, i, l); i += l; ++c; }
+                    int j = i;
+                    while (j < a.slen && c < until) { int l; rx::decode(a.s, a.slen, j, l); j += l; ++c; }
+                    a.s += i;
+                    a.slen = j - i;
+                    break;
+                }
+                case DQ_P_CASE: {  // CASE WHEN c1 THEN v1 ... [ELSE e] END: arg = 2 * #WHEN + has ELSE
+                    const int nw = arg >> 1, has_else = arg & 1;
+                    const int base = sp - 2 * nw - has_else;
+                    Val r = has_else ? st[sp - 1] : vnull();
+                    int rt = has_else ? st_type[sp - 1] : 0;
+                    for (int k = 0; k < nw; ++k) {
+                        const Val& c = st[base + 2 * k];
+                        if (!c.null && (c.tag == DQ_V_DOUBLE ? c.d != 0.0 : c.i != 0)) {
+                            r = st[base + 2 * k + 1];
+                            rt = st_type[base + 2 * k + 1];
+                            break;
+                        }
+                    }
+                    sp = base;
+                    st_type[sp] = rt;
+                    st[sp++] = r;
+                    break;
+                }
+                case DQ_P_ISNAN: {  // IsNaN: never NULL (FALSE for NULL), a string operand cast to double
+                    const Val a = st[sp - 1];
+                    bool r = false;
+                    if (!a.null) {
+                        if (a.tag == DQ_V_DOUBLE) r = a.d != a.d;
+                        else if (a.tag == DQ_V_STRING) { double d; r = parse_double_v(a, d) && d != d; }
+                    }
+                    st[sp - 1] = vbool(r);
+                    st_type[sp - 1] = 0;
+                    break;
+                }
+                case DQ_P_ABS: {
+                    Val& a = st[sp - 1];
+                    if (!a.null) {
+                        if (a.tag == DQ_V_STRING) { double d; a = parse_double_v(a, d) ? vdouble(fabs(d)) : vnull(); }
+                        else if (a.tag == DQ_V_DOUBLE) a.d = fabs(a.d);
+                        else if (a.i < 0) a.i = (int64_t)(0ull - (uint64_t)a.i);  // Long.MinValue stays (Math.abs)
+                    }
+                    break;
+                }
+                case DQ_P_NANVL: {  // nanvl(a, b): b when a is NaN, else a (NULL in -> NULL out)
+                    const Val b = st[--sp];
+                    const Val a = st[sp - 1];
+                    if (a.null || b.null) st[sp - 1] = vnull();
+                    else if (a.tag == DQ_V_DOUBLE && a.d != a.d) st[sp - 1] = b;
+                    st_type[sp - 1] = 0;
+                    break;
+                }
+                case DQ_P_YEAR: case DQ_P_MONTH: case DQ_P_DAY: {  // arg: 0 = DATE (days), 1 = TIMESTAMP (micros, UTC)
+                    Val& a = st[sp - 1];
+                    st_type[sp - 1] = 0;
+                    if (a.null) break;
+                    if (a.tag != DQ_V_LONG) { a = vnull(); break; }
+                    const int64_t days = arg == 1 ? rx::floor_div(a.i, 86400000000ll) : a.i;
+                    int64_t y;
+                    int m, d;
+                    spark_ymd(days, y, m, d);
+                    a = vlong(op == DQ_P_YEAR ? y : (op == DQ_P_MONTH ? m : d));
                     break;
                 }
                 case DQ_P_LENGTH: {
@@ -452,6 +710,7 @@ predicate_kernel(const PredProgram* __restrict__ progp, const PredColumn* __rest
                 }
                 default: break;
             }
+            if (op != DQ_P_COL && op != DQ_P_CASE && sp > 0) st_type[sp - 1] = op == DQ_P_COALESCE ? st_type[sp - 1] : 0;
         }
         if (sp > 0) {
             const Val r = st[sp - 1];
@@ -790,12 +1049,16 @@ void launch_pred_simple(const PredSimple& prog, const PredColumn* cols_dev, int6
                        padded_words, out_t, out_nn);
 }
 
-void launch_predicate(const PredProgram* prog_dev, const PredColumn* cols_dev, int64_t nrows,
+void launch_predicate(const PredProgram* prog_dev, bool rx, int32_t* status, const PredColumn* cols_dev, int64_t nrows,
                       int64_t padded_words, uint64_t* out_t, uint64_t* out_nn, hipStream_t s) {
     const int64_t rows = padded_words * 64;
     const int64_t blocks = (rows + 255) / 256;
-    hipLaunchKernelGGL(predicate_kernel, dim3((unsigned)blocks), dim3(256), 0, s, prog_dev, cols_dev, nrows,
-                       padded_words, out_t, out_nn);
+    if (rx)
+        hipLaunchKernelGGL(predicate_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, prog_dev, cols_dev, nrows,
+                           padded_words, out_t, out_nn, status);
+    else
+        hipLaunchKernelGGL(predicate_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, prog_dev, cols_dev, nrows,
+                           padded_words, out_t, out_nn, status);
 }
 
 }  // namespace dq

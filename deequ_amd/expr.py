@@ -2,11 +2,14 @@
 
 deequ passes `where` filters and Compliance predicates as Spark SQL expression strings
 (`expr(...)` in A/Analyzer.scala:409-432 and A/Compliance.scala:49-52; generated ones in
-M/checks/Check.scala:594-943). This module parses the subset those produce — comparisons, IN,
-IS [NOT] NULL, LIKE, BETWEEN, AND/OR/NOT, arithmetic, COALESCE, LENGTH, CAST — resolving column
-names against the table schema exactly like Spark's analyzer would: an unknown column raises
-(Spark's AnalysisException), which the runner turns into a failure of every shareable analyzer
-of the batch (R/AnalysisRunner.scala:320-323).
+M/checks/Check.scala:594-943). This module parses Spark SQL's scalar expression language over one row —
+comparisons (= == != <> < <= > >= <=>), IN, IS [NOT] NULL, [NOT] LIKE, [NOT] RLIKE / REGEXP (java.util.regex
+through deequ_amd/regex.py), [NOT] BETWEEN, AND / OR / NOT, + - * / %, CASE WHEN .. THEN .. [ELSE ..] END (searched
+and simple forms), CAST, DATE 'yyyy-MM-dd' literals and the functions coalesce / nvl / ifnull, if, isnull /
+isnotnull, isnan, nanvl, abs, length, lower / lcase, upper / ucase, trim / ltrim / rtrim, substring / substr,
+year / month / dayofmonth / day — resolving column names against the table schema exactly like Spark's analyzer
+would: an unknown column raises (Spark's AnalysisException), which the runner turns into a failure of every
+shareable analyzer of the batch (R/AnalysisRunner.scala:320-323). Anything else raises PredicateSyntaxError.
 """
 import ctypes
 import re
@@ -33,7 +36,8 @@ _TOKEN = re.compile(r"""
   | (?P<id>[A-Za-z_][A-Za-z0-9_.]*)
 """, re.VERBOSE)
 
-_KEYWORDS = {"AND", "OR", "NOT", "IS", "NULL", "IN", "LIKE", "TRUE", "FALSE", "BETWEEN", "CAST", "AS"}
+_KEYWORDS = {"AND", "OR", "NOT", "IS", "NULL", "IN", "LIKE", "TRUE", "FALSE", "BETWEEN", "CAST", "AS", "RLIKE",
+             "REGEXP", "CASE", "WHEN", "THEN", "ELSE", "END", "DATE"}
 
 
 def _tokenize(text):
@@ -126,7 +130,8 @@ class _Parser:
             op = {"==": "=", "<>": "!="}.get(t[1], t[1])
             return _Node("cmp", left, self.add(), value=op)
         negate = False
-        if t == ("kw", "NOT") and self.peek(1)[0] == "kw" and self.peek(1)[1] in ("IN", "LIKE", "BETWEEN"):
+        if t == ("kw", "NOT") and self.peek(1)[0] == "kw" and self.peek(1)[1] in ("IN", "LIKE", "BETWEEN", "RLIKE",
+                                                                                   "REGEXP"):
             self.take()
             negate = True
             t = self.peek()
@@ -147,6 +152,12 @@ class _Parser:
             if pat[0] != "str":
                 raise PredicateSyntaxError("LIKE needs a string literal pattern in %r" % self.text)
             n = _Node("like", left, value=pat[1])
+            return _Node("not", n) if negate else n
+        if self.accept("kw", "RLIKE") or self.accept("kw", "REGEXP"):
+            pat = self.take()
+            if pat[0] != "str":
+                raise PredicateSyntaxError("RLIKE needs a string literal pattern in %r" % self.text)
+            n = _Node("rlike", left, value=pat[1])
             return _Node("not", n) if negate else n
         if self.accept("kw", "BETWEEN"):
             lo = self.add()
@@ -195,6 +206,13 @@ class _Parser:
             return _Node("const", value=("bool", val == "TRUE"))
         if kind == "kw" and val == "NULL":
             return _Node("null")
+        if kind == "kw" and val == "DATE":  # DATE 'yyyy-MM-dd' literal: days since the epoch (a DATE column's value)
+            lit = self.take()
+            if lit[0] != "str":
+                raise PredicateSyntaxError("DATE needs a string literal in %r" % self.text)
+            return _Node("const", value=("long", _date_days(lit[1], self.text)))
+        if kind == "kw" and val == "CASE":
+            return self._case()
         if kind == "kw" and val == "CAST":
             self.expect("op", "(")
             e = self.or_()
@@ -223,20 +241,66 @@ class _Parser:
                     while self.accept("op", ","):
                         args.append(self.or_())
                     self.expect("op", ")")
-                if fname == "coalesce":
-                    return _Node("coalesce", *args)
-                if fname in ("length", "char_length", "character_length") and len(args) == 1:
-                    return _Node("length", args[0])
-                if fname in ("isnull",) and len(args) == 1:
-                    return _Node("isnull", args[0])
-                if fname in ("isnotnull",) and len(args) == 1:
-                    return _Node("isnotnull", args[0])
-                if fname == "abs" and len(args) == 1:
-                    a = args[0]
-                    return _Node("coalesce", _Node("abs", a))
-                raise PredicateSyntaxError("unsupported function %s in %r" % (val, self.text))
+                n = self._function(fname, args)
+                if n is None:
+                    raise PredicateSyntaxError("unsupported function %s/%d in %r" % (val, len(args), self.text))
+                return n
             return _Node("col", value=val)
         raise PredicateSyntaxError("unexpected %r in %r" % (val, self.text))
+
+
+    _UNARY = {"length": "length", "char_length": "length", "character_length": "length", "isnull": "isnull",
+              "isnotnull": "isnotnull", "isnan": "isnan", "abs": "abs", "lower": "lower", "lcase": "lower",
+              "upper": "upper", "ucase": "upper", "trim": "trim", "ltrim": "ltrim", "rtrim": "rtrim", "year": "year",
+              "month": "month", "dayofmonth": "day", "day": "day"}
+
+    def _function(self, fname, args):
+        if fname == "coalesce" and args:
+            return _Node("coalesce", *args)
+        if fname in ("nvl", "ifnull") and len(args) == 2:
+            return _Node("coalesce", *args)
+        if fname == "if" and len(args) == 3:  # if(c, a, b) = CASE WHEN c THEN a ELSE b END
+            return _Node("case", args[0], args[1], args[2], value=(1, True))
+        if fname == "nanvl" and len(args) == 2:
+            return _Node("nanvl", *args)
+        if fname in ("substring", "substr") and len(args) in (2, 3):
+            if len(args) == 2:
+                args.append(_Node("const", value=("long", 2147483647)))
+            return _Node("substr", *args)
+        if fname in self._UNARY and len(args) == 1:
+            return _Node(self._UNARY[fname], args[0])
+        return None
+
+    def _case(self):
+        """CASE [x] WHEN w THEN v ... [ELSE e] END; the simple form's WHEN w means x = w."""
+        subject = None
+        if self.peek() != ("kw", "WHEN"):
+            subject = self.or_()
+        parts = []
+        while self.accept("kw", "WHEN"):
+            cond = self.or_()
+            if subject is not None:
+                cond = _Node("cmp", subject, cond, value="=")
+            self.expect("kw", "THEN")
+            parts += [cond, self.or_()]
+        if not parts:
+            raise PredicateSyntaxError("CASE without WHEN in %r" % self.text)
+        has_else = self.accept("kw", "ELSE")
+        if has_else:
+            parts.append(self.or_())
+        self.expect("kw", "END")
+        return _Node("case", *parts, value=(len(parts) // 2, has_else))
+
+
+def _date_days(text, where):
+    """DATE 'yyyy-MM-dd' as days since 1970-01-01 (proleptic Gregorian, Spark's DateTimeUtils.stringToDate for dates
+    after the 1582 cutover)."""
+    import datetime
+    m = re.fullmatch(r"\s*(\d{4})-(\d{1,2})-(\d{1,2})\s*", text)
+    if not m:
+        raise PredicateSyntaxError("bad DATE literal %r in %r" % (text, where))
+    d = datetime.date(int(m.group(1)), int(m.group(2)), int(m.group(3)))
+    return (d - datetime.date(1970, 1, 1)).days
 
 
 class CompiledPredicate:
@@ -266,10 +330,32 @@ _CMP = {"=": N.P_EQ, "!=": N.P_NE, "<": N.P_LT, "<=": N.P_LE, ">": N.P_GT, ">=":
 _ARITH = {"+": N.P_ADD, "-": N.P_SUB, "*": N.P_MUL, "/": N.P_DIV, "%": N.P_MOD}
 
 
-def compile_predicate(text, column_index):
-    """`column_index`: name -> index into the batch's column list. Returns CompiledPredicate."""
+def compile_predicate(text, column_index, column_types=None):
+    """`column_index`: name -> index into the batch's column list; `column_types`: name -> Spark type (for the
+    functions whose meaning depends on it: year / month / day of a DATE or a TIMESTAMP). Returns CompiledPredicate."""
     tree = _Parser(text).parse()
     code, consts, strings, used = [], [], bytearray(), []
+    column_types = column_types or {}
+
+    def resolve(name):
+        if name in column_index:
+            return name
+        # Spark resolves identifiers case-insensitively by default.
+        matches = [c for c in column_index if c.lower() == name.lower()]
+        if len(matches) != 1:
+            raise UnresolvedColumnError("cannot resolve '`%s`' given input columns: [%s]"
+                                        % (name, ", ".join(column_index)))
+        return matches[0]
+
+    def blob_const(image):
+        """A STRING constant holding a binary image, 4-byte aligned in the pool (regex programs)."""
+        while len(strings) % 4:
+            strings.append(0)
+        c = N.DqConst()
+        c.tag, c.str_offset, c.str_len = N.V_STRING, len(strings), len(image)
+        strings.extend(image)
+        consts.append(c)
+        return len(consts) - 1
 
     def const(kind, v):
         c = N.DqConst()
@@ -289,14 +375,7 @@ def compile_predicate(text, column_index):
     def emit(n):
         k = n.kind
         if k == "col":
-            name = n.value
-            if name not in column_index:
-                # Spark resolves identifiers case-insensitively by default.
-                matches = [c for c in column_index if c.lower() == name.lower()]
-                if len(matches) != 1:
-                    raise UnresolvedColumnError("cannot resolve '`%s`' given input columns: [%s]"
-                                                % (name, ", ".join(column_index)))
-                name = matches[0]
+            name = resolve(n.value)
             code.extend([N.P_COL, column_index[name]])
             used.append(name)
         elif k == "const":
@@ -332,9 +411,37 @@ def compile_predicate(text, column_index):
         elif k == "neg":
             emit(n.children[0])
             code.extend([N.P_NEG, 0])
-        elif k == "abs":
-            # abs(x) = CASE WHEN x < 0 THEN -x ELSE x END, as coalesce-free postfix: not needed by deequ
-            raise PredicateSyntaxError("abs() is not supported")
+        elif k in ("abs", "isnan", "lower", "upper"):
+            emit(n.children[0])
+            code.extend([{"abs": N.P_ABS, "isnan": N.P_ISNAN, "lower": N.P_LOWER, "upper": N.P_UPPER}[k], 0])
+        elif k in ("trim", "ltrim", "rtrim"):
+            emit(n.children[0])
+            code.extend([N.P_TRIM, {"trim": 0, "ltrim": 1, "rtrim": 2}[k]])
+        elif k == "nanvl":
+            emit(n.children[0])
+            emit(n.children[1])
+            code.extend([N.P_NANVL, 0])
+        elif k == "substr":
+            for ch in n.children:
+                emit(ch)
+            code.extend([N.P_SUBSTR, 0])
+        elif k == "case":
+            nwhen, has_else = n.value
+            for ch in n.children:
+                emit(ch)
+            code.extend([N.P_CASE, 2 * nwhen + (1 if has_else else 0)])
+        elif k == "rlike":
+            from .regex import compile_regex
+            emit(n.children[0])
+            code.extend([N.P_RLIKE, blob_const(compile_regex(n.value).to_bytes())])
+        elif k in ("year", "month", "day"):
+            child = n.children[0]
+            ty = column_types.get(resolve(child.value)) if child.kind == "col" else None
+            if ty not in (N.TYPE_DATE, N.TYPE_TIMESTAMP):
+                raise PredicateSyntaxError("%s() needs a DATE or TIMESTAMP column in %r" % (k, text))
+            emit(child)
+            code.extend([{"year": N.P_YEAR, "month": N.P_MONTH, "day": N.P_DAY}[k],
+                         1 if ty == N.TYPE_TIMESTAMP else 0])
         elif k == "like":
             emit(n.children[0])
             code.extend([N.P_LIKE, const("string", n.value)])

@@ -37,6 +37,7 @@ P_EQ, P_NE, P_LT, P_LE, P_GT, P_GE, P_EQ_NULLSAFE = 10, 11, 12, 13, 14, 15, 16
 P_AND, P_OR, P_NOT, P_IS_NULL, P_IS_NOT_NULL, P_IN, P_COALESCE = 20, 21, 22, 23, 24, 25, 26
 P_ADD, P_SUB, P_MUL, P_DIV, P_MOD, P_NEG = 30, 31, 32, 33, 34, 35
 P_LIKE, P_LENGTH, P_CAST_DOUBLE, P_CAST_LONG, P_CAST_STRING_NUM, P_REGEX = 40, 41, 42, 43, 44, 45
+P_RLIKE, P_LOWER, P_UPPER, P_TRIM, P_CASE, P_ISNAN, P_ABS, P_SUBSTR, P_YEAR, P_MONTH, P_DAY, P_NANVL = range(46, 58)
 V_BOOL, V_LONG, V_DOUBLE, V_STRING = 1, 2, 3, 4
 
 SYNTH_DYADIC, SYNTH_UNIFORM, SYNTH_NORMAL, SYNTH_INT32R, SYNTH_KEY30, SYNTH_GAUSS01, SYNTH_GAUSS_CORR = range(1, 8)
@@ -46,7 +47,8 @@ SYNTH_STR_CAT50, SYNTH_STR_BOOL, SYNTH_STR_CAT100, SYNTH_STR_INT, SYNTH_STR_DEC,
 HLL_NUM_WORDS = 52
 
 # dq_scan_kernel, in enum order
-FREQ_PATHS = ("fast", "fast_narrow", "fast_done", "exact", "partitioned", "sorted", "small", "small_optimistic", "fast_spill")
+FREQ_PATHS = ("fast", "fast_narrow", "fast_done", "exact", "partitioned", "sorted", "small", "small_optimistic", "fast_spill",
+              "fast_windowed")
 SCAN_KERNELS = ("striped", "striped_heavy", "heavy8", "heavy8_full", "bits", "pred_simple", "pred_vm", "regex",
                 "strings", "where_fused", "where_masks")
 

@@ -45,9 +45,18 @@ class ScanBatch:
 
     def predicate(self, text):
         if text not in self.pred_index:
-            self.preds.append(compile_predicate(text, self.col_index))
+            self.preds.append(compile_predicate(text, self.col_index, self._column_types()))
             self.pred_index[text] = len(self.preds) - 1
         return self.pred_index[text]
+
+    def _column_types(self):
+        types = {}
+        for n in self.names:
+            try:
+                types[n] = self.data[n].spark_type
+            except (KeyError, TypeError, AttributeError):
+                pass
+        return types
 
     def regex_predicate(self, column, pattern):
         """PatternMatch's `regexp_extract(col, pattern, 0) != ""` as the [COL, REGEX] program."""

@@ -99,7 +99,19 @@ typedef enum dq_pred_opcode {
      * TRUE when the first Matcher.find() match of the value's string form is non-empty, FALSE
      * otherwise, also for NULL (`when(regexp_extract(..) != "", 1).otherwise(0)`). Only as the whole
      * program [COL c, REGEX k], over STRING / integral / BOOLEAN columns. */
-    DQ_P_REGEX = 45
+    DQ_P_REGEX = 45,
+    /* str RLIKE regex (Spark RLike: Pattern.compile(regex).matcher(str).find(), any match): arg = index of a STRING
+     * constant holding a compiled regex program (as DQ_P_REGEX); 1 operand, a non-string one as its Spark string
+     * cast. NULL in -> NULL. */
+    DQ_P_RLIKE = 46,
+    DQ_P_LOWER = 47, DQ_P_UPPER = 48,  /* lower(str) / upper(str): simple Unicode case mappings                 */
+    DQ_P_TRIM = 49,      /* arg 0 trim, 1 ltrim, 2 rtrim (ASCII spaces, Spark 2.2 UTF8String.trim)                 */
+    DQ_P_CASE = 50,      /* CASE WHEN c1 THEN v1 .. [ELSE e] END: arg = 2 * #WHEN + has ELSE; operands c1 v1 .. [e] */
+    DQ_P_ISNAN = 51,     /* isnan(x): never NULL                                                                  */
+    DQ_P_ABS = 52,
+    DQ_P_SUBSTR = 53,    /* substring(str, pos, len): 3 operands, UTF8String.substringSQL                          */
+    DQ_P_YEAR = 54, DQ_P_MONTH = 55, DQ_P_DAY = 56, /* arg 0: DATE days, 1: TIMESTAMP micros (UTC session zone)  */
+    DQ_P_NANVL = 57      /* nanvl(a, b): 2 operands                                                               */
 } dq_pred_opcode;
 
 typedef enum dq_value_tag { DQ_V_BOOL = 1, DQ_V_LONG = 2, DQ_V_DOUBLE = 3, DQ_V_STRING = 4 } dq_value_tag;
@@ -285,7 +297,8 @@ typedef enum dq_freq_path {
     DQ_FREQ_PATH_SMALL = 6,             /* one-pass small builds launched (sized or optimistic)                */
     DQ_FREQ_PATH_SMALL_OPTIMISTIC = 7,  /* optimistic small builds (no sizing pass) that produced their table  */
     DQ_FREQ_PATH_FAST_SPILL = 8,        /* fast builds whose full buckets spilled keys (inserted after the build) */
-    DQ_FREQ_PATH_COUNT = 9
+    DQ_FREQ_PATH_FAST_WINDOWED = 9,     /* fast builds whose pass 2 + build ran window by window (cache-resident) */
+    DQ_FREQ_PATH_COUNT = 10
 } dq_freq_path;
 int64_t dq_freq_path_count(const dq_ctx* ctx, int32_t path);
 

@@ -606,7 +606,8 @@ class OracleParser:
         if tok[0] == "op" and tok[1] in self._CMP:
             return True
         w = self._word()
-        return w in ("IS", "IN", "LIKE", "BETWEEN") or (w == "NOT" and self._word(1) in ("IN", "LIKE", "BETWEEN"))
+        return w in ("IS", "IN", "LIKE", "BETWEEN", "RLIKE", "REGEXP") or \
+            (w == "NOT" and self._word(1) in ("IN", "LIKE", "BETWEEN", "RLIKE", "REGEXP"))
 
     def _predicate(self, left):
         tok = self._peek()
@@ -640,6 +641,11 @@ class OracleParser:
             if pat[0] != "str":
                 raise ValueError("oracle parser: LIKE pattern must be a string literal")
             node = PNode("like", left, value=pat[1])
+        elif w in ("RLIKE", "REGEXP"):
+            pat = self._next()
+            if pat[0] != "str":
+                raise ValueError("oracle parser: RLIKE pattern must be a string literal")
+            node = PNode("rlike", left, value=pat[1])
         else:  # BETWEEN lo AND hi
             lo = self._arith(0)
             if self._word() != "AND":
@@ -688,6 +694,30 @@ class OracleParser:
             return PNode("const", value=("bool", up == "TRUE"))
         if up == "NULL":
             return PNode("null")
+        if up == "DATE" and self._peek()[0] == "str":
+            import datetime
+            y, m, d = (int(x) for x in self._next()[1].strip().split("-"))
+            return PNode("const", value=("long", (datetime.date(y, m, d) - datetime.date(1970, 1, 1)).days))
+        if up == "CASE":
+            subject = None if self._word() == "WHEN" else self._expr(0)
+            parts = []
+            while self._word() == "WHEN":
+                self._next()
+                cond = self._expr(0)
+                if subject is not None:
+                    cond = PNode("cmp", subject, cond, value="=")
+                if self._word() != "THEN":
+                    raise ValueError("oracle parser: CASE WHEN without THEN")
+                self._next()
+                parts.append((cond, self._expr(0)))
+            other = None
+            if self._word() == "ELSE":
+                self._next()
+                other = self._expr(0)
+            if self._word() != "END":
+                raise ValueError("oracle parser: CASE without END")
+            self._next()
+            return PNode("case", value=(parts, other))
         if up == "CAST":
             self._expect_op("(")
             inner = self._expr(0)
@@ -724,6 +754,17 @@ class OracleParser:
                 return PNode("isnull", args[0])
             if f == "isnotnull":
                 return PNode("isnotnull", args[0])
+            if f in ("nvl", "ifnull"):
+                return PNode("coalesce", *args)
+            if f == "if":
+                return PNode("case", value=([(args[0], args[1])], args[2]))
+            if f in ("substring", "substr"):
+                return PNode("substr", *args)
+            unary = {"isnan": "isnan", "abs": "abs", "lower": "lower", "lcase": "lower", "upper": "upper",
+                     "ucase": "upper", "trim": "trim", "ltrim": "ltrim", "rtrim": "rtrim", "year": "year",
+                     "month": "month", "dayofmonth": "day", "day": "day", "nanvl": "nanvl"}
+            if f in unary:
+                return PNode(unary[f], *args)
             raise ValueError("oracle parser: function %s" % f)
         return PNode("col", value=val)
 
@@ -863,7 +904,89 @@ def _eval(node, row):
             return int(float(a)) if isinstance(a, str) else int(a)
         except ValueError:
             return None
+    if k == "case":
+        parts, other = node.value
+        for cond, val in parts:
+            c = _eval(cond, row)
+            if c is True or (c is not None and not isinstance(c, bool) and c != 0):
+                return _eval(val, row)
+        return None if other is None else _eval(other, row)
+    if k == "rlike":
+        # Spark RLike: Pattern.compile(p).matcher(str).find() -- any match, even an empty one
+        a = _eval(node.children[0], row)
+        if a is None:
+            return None
+        text = a if isinstance(a, str) else ("true" if a is True else "false" if a is False else str(a))
+        return compile_java_regex(node.value).search(text) is not None
+    if k in ("lower", "upper"):
+        a = _eval(node.children[0], row)
+        return a if not isinstance(a, str) else (a.lower() if k == "lower" else a.upper())
+    if k in ("trim", "ltrim", "rtrim"):  # Spark 2.2 UTF8String.trim*: ASCII spaces only
+        a = _eval(node.children[0], row)
+        if not isinstance(a, str):
+            return a
+        return a.strip(" ") if k == "trim" else (a.lstrip(" ") if k == "ltrim" else a.rstrip(" "))
+    if k == "substr":
+        # UTF8String.substringSQL(pos, len): one-based, 0 = the first character, negative from the end
+        vals = [_eval(c, row) for c in node.children]
+        if any(v is None for v in vals):
+            return None
+        s, pos = vals[0], int(vals[1])
+        length = int(vals[2]) if len(vals) > 2 else 2 ** 31 - 1
+        n = len(s)
+        start = pos - 1 if pos > 0 else (n + pos if pos < 0 else 0)
+        until = n if length == 2 ** 31 - 1 else start + length
+        if until <= start or start >= len(s.encode()):
+            return ""
+        return s[max(start, 0):max(until, 0)]
+    if k == "isnan":
+        a = _eval(node.children[0], row)
+        if a is None:
+            return False
+        try:
+            return math.isnan(float(a))
+        except ValueError:
+            return False
+    if k == "abs":
+        a = _eval(node.children[0], row)
+        if isinstance(a, str):
+            try:
+                return abs(float(a))
+            except ValueError:
+                return None
+        return None if a is None else abs(a)
+    if k == "nanvl":
+        a, b = _eval(node.children[0], row), _eval(node.children[1], row)
+        if a is None or b is None:
+            return None
+        return b if isinstance(a, float) and math.isnan(a) else a
+    if k in ("year", "month", "day"):
+        # Spark 2.2 DateTimeUtils.getYear / getMonth / getDayOfMonth: the proleptic Gregorian date of the day number,
+        # 10 days earlier on or before 1582-10-04; a TIMESTAMP's day in the UTC session zone
+        import datetime
+        a = _eval(node.children[0], row)
+        if a is None:
+            return None
+        days = a // 86400000000 if node.value == T_TIMESTAMP else a
+        if days <= -141428:
+            days -= 10
+        d = datetime.date(1970, 1, 1) + datetime.timedelta(days=days)
+        return {"year": d.year, "month": d.month, "day": d.day}[k]
     raise ValueError(k)
+
+
+def _annotate_types(node, table):
+    """year / month / day of a column: the column's Spark type decides DATE (days) or TIMESTAMP (micros)."""
+    if node.kind in ("year", "month", "day") and node.children and node.children[0].kind == "col":
+        node.value = table[node.children[0].value].spark_type
+    for c in node.children:
+        _annotate_types(c, table)
+    if node.kind == "case":
+        for cond, val in node.value[0]:
+            _annotate_types(cond, table)
+            _annotate_types(val, table)
+        if node.value[1] is not None:
+            _annotate_types(node.value[1], table)
 
 
 _MASKS = weakref.WeakKeyDictionary()  # table -> {predicate text: masks} (tables are not mutated by the tests)
@@ -876,6 +999,7 @@ def predicate_masks(table, text):
     if text in memo:
         return memo[text]
     tree = OracleParser(text).parse()
+    _annotate_types(tree, table)
     cols = {n: _pylist(table[n]) for n in table.columns}
     t = np.zeros(table.nrows, dtype=bool)
     nn = np.zeros(table.nrows, dtype=bool)

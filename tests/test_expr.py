@@ -102,3 +102,52 @@ def test_oracle_parser_reference_truth_tables(kats):
         assert got == k["expected"], k
         seen += 1
     assert seen >= 3
+
+
+# Spark SQL beyond the predicates Check.scala generates (VERDICT r04 missing #4): CASE WHEN, RLIKE, string and date
+# functions, isnan / nanvl / abs, DATE literals. Compiled programs here; GPU parity against the oracle in
+# tests/test_gpu_pred_surface.py.
+SURFACE = ["CASE WHEN att1 > 1 THEN 'big' WHEN att1 = 1 THEN 'one' ELSE 'small' END = 'big'",
+           "CASE att1 WHEN 1 THEN TRUE WHEN 2 THEN FALSE END", "if(att1 > 2, att2, -1) >= 0",
+           "item RLIKE '^[0-9]+$'", "item NOT RLIKE '\\\\.'", "item REGEXP '(?i)IT'", "lower(item) = 'it''s'",
+           "upper(item) LIKE 'IT%'", "trim(item) = '1'", "ltrim(item) <> rtrim(item)", "substring(item, 2) = '1'",
+           "substr(item, -1, 1) = '5'", "isnan(att1)", "nanvl(att1, 0) > 1", "abs(att1 - 3) <= 1",
+           "nvl(att1, 0) + ifnull(att2, 0) > 3", "lcase(item) = ucase(item)", "length(trim(item)) = 1"]
+
+
+def test_sql_surface_compiles():
+    from deequ_amd.expr import compile_predicate
+    for text in SURFACE:
+        p = compile_predicate(text, COLS)
+        assert len(p._code) % 2 == 0 and len(p._code) > 0, text
+    p = compile_predicate("item RLIKE 'a+'", COLS)
+    ops = list(p._code[0::2])
+    assert N.P_RLIKE in ops
+    k = p._code[list(p._code[0::2]).index(N.P_RLIKE) * 2 + 1]
+    assert p._consts[k].str_offset % 4 == 0 and p._consts[k].str_len >= 32  # an aligned regex program image
+    with pytest.raises(PredicateSyntaxError):
+        compile_predicate("year(att1) = 2020", COLS, {"att1": N.TYPE_LONG})  # year() of a non-date column
+    d = compile_predicate("year(d) = 2020 AND d >= DATE '2020-02-01'", dict(COLS, d=3),
+                          {"d": N.TYPE_DATE})
+    assert N.P_YEAR in list(d._code[0::2])
+
+
+def test_sql_surface_oracle_known_answers():
+    """The oracle's evaluation of the new forms against hand-computed Spark 2.2 results (three-valued logic: a NULL
+    input gives NULL, isnan(NULL) is FALSE, CASE without a matching WHEN and without ELSE is NULL)."""
+    import oracle as O
+    rows = [({"item": " 12 ", "att1": 2, "att2": None}, {
+        "trim(item) = '12'": True, "ltrim(item) = '12 '": True, "rtrim(item) = ' 12'": True,
+        "substring(item, 2, 2) = '12'": True, "substring(item, -2, 1) = '2'": True, "substring(item, 0, 2) = ' 1'": True,
+        "item RLIKE '\\\\d{2}'": True, "item RLIKE '^\\\\d'": False, "item RLIKE ''": True,
+        "CASE WHEN att2 > 1 THEN 1 END = 1": None, "CASE WHEN att2 > 1 THEN 1 ELSE 2 END = 2": True,
+        "CASE att1 WHEN 2 THEN 'two' ELSE 'other' END = 'two'": True, "if(att2 IS NULL, 1, 0) = 1": True,
+        "isnan(att2)": False, "nanvl(att2, 1) = 1": None, "abs(att1 - 5) = 3": True,
+        "upper(item) = ' 12 '": True, "nvl(att2, 7) = 7": True}),
+        ({"item": "AbC", "att1": float("nan"), "att2": 3}, {
+            "lower(item) = 'abc'": True, "upper(item) LIKE 'AB_'": True, "item RLIKE '(?i)abc'": True,
+            "item RLIKE 'abc'": False, "isnan(att1)": True, "nanvl(att1, 5) = 5": True, "att1 > 1e308": True})]
+    for row, cases in rows:
+        for text, want in cases.items():
+            got = O._eval(O.OracleParser(text).parse(), row)
+            assert got == want, (text, row, got, want)
