@@ -447,8 +447,17 @@ class PatternMatch(StandardScanShareableAnalyzer):
         # regexp_extract casts a non-string column to STRING (Spark's implicit cast): the device formats every cell
         # as Cast(x AS STRING) does — Java toString of numerics, BigDecimal.toString of decimals, "yyyy-MM-dd" of
         # dates and "yyyy-MM-dd HH:mm:ss[.ffffff]" of timestamps in a UTC session time zone (regex.hip)
+        col = batch.data[self.column] if self.column in batch.col_index else None
+        tz = getattr(col, "tz", None)
+        if col is not None and col.spark_type == N.TYPE_TIMESTAMP and tz not in UTC_ZONES:
+            # Spark formats timestamps in the session time zone; the device formats in UTC only
+            raise UnsupportedOnDevice("PatternMatch over TIMESTAMP column %s in time zone %s: the device formats "
+                                      "timestamps in a UTC session time zone only" % (self.column, tz))
         p = batch.regex_predicate(self.column, self.pattern_)
         return [batch.add_op(N.OP_COMPLIANCE, where=self.where, predicate_index=p)]
+
+
+UTC_ZONES = (None, "UTC", "Etc/UTC", "GMT", "Etc/GMT", "Z", "+00:00", "-00:00", "Zulu", "Universal")
 
 
 class Patterns:
@@ -722,7 +731,7 @@ class FrequenciesAndNumRows:
             for s in splits:
                 table, counts = s.device_table()
                 tables.append(engine.frequencies(table, s.names, False, weights=counts))
-            self._device = tables[0] if len(tables) == 1 else SplitFrequencies(tables, f.names)
+            self._device = tables[0] if len(tables) == 1 else SplitFrequencies(tables, f.names, splits)
         elif self._device is None and isinstance(f, G.GroupBlock):
             self._device = engine.frequencies(f.table(), f.names, False, weights=f.counts)
         if self._device is None and isinstance(f, engine.PairFrequencies):
@@ -746,9 +755,10 @@ class SplitFrequencies:
     exactly one split, so the fused aggregation over the whole table (A/GroupingAnalyzers.scala:83-120) is the sum
     of the splits' (groups, unique groups, entropy terms), as in the multi-device union of dq_open_devices."""
 
-    def __init__(self, tables, names):
+    def __init__(self, tables, names, splits=None):
         self.tables = list(tables)
         self.names = list(names)
+        self.splits = list(splits) if splits is not None else None  # the BlockParts each table was built over
         self.source = None  # no single source table: MutualInformation's marginals need the joint groups in one
 
     def key_kind(self):
@@ -766,6 +776,21 @@ class SplitFrequencies:
 
     def export_raw(self):
         raise ValueError("a split frequency state has no single source table to export representative rows from")
+
+    def distinct_block(self):
+        """The aggregated groups as one GroupBlock: each split's (representative row, count) pairs taken from that
+        split's own key columns and concatenated -- the splits are key-disjoint, so the groups stay distinct (the
+        persisted form of a merged state, state_provider._block_table)."""
+        from . import groups as G
+        if self.splits is None:
+            raise ValueError("a split frequency state without its splits' key columns")
+        blocks = []
+        for blk, table in zip(self.splits, self.tables):
+            keys, counts = table.export_raw()
+            blocks.append(G.GroupBlock([G.take(c, keys) for c in blk.columns], counts))
+        out = G.concat(blocks, self.splits[0].schema())
+        out.distinct = True
+        return out
 
 
 def _block_from_dict(freq, like):
@@ -949,11 +974,15 @@ class Histogram(Analyzer):
     _fields = ("column", "binningUdf", "maxDetailBins")
 
     def _key(self):
-        udf = None if self.binningUdf is None else ("udf", id(self.binningUdf))
+        udf = None if self.binningUdf is None else ("udf", id(self.binningUdf), self.udfInputAsString)
         return (type(self).__name__, self.column, udf, self.maxDetailBins)
 
-    def __init__(self, column, binningUdf=None, maxDetailBins=MaximumAllowedDetailBins):
+    def __init__(self, column, binningUdf=None, maxDetailBins=MaximumAllowedDetailBins, udfInputAsString=False):
+        """`binningUdf` receives each value as the column's type (int, float, Decimal, date, str), as a typed Scala
+        UDF does. `udfInputAsString=True` hands it the value's Spark string form instead, as Spark's implicit cast
+        does for a UDF declared over String on a non-string column (NULL stays None either way)."""
         self.column, self.binningUdf, self.maxDetailBins = column, binningUdf, maxDetailBins
+        self.udfInputAsString = bool(udfInputAsString)
 
     def preconditions(self):
         def param_check(_):
@@ -975,9 +1004,10 @@ class Histogram(Analyzer):
         type sees the nulls), and the bins add the groups' counts — exact for any deterministic UDF. The UDF receives
         the column's value (str, int, float, ...), as a Spark UDF receives the Scala value. {(bin label,): count}."""
         ft = engine.frequencies(data, [self.column], include_nulls=False)
-        return self.bin_groups(((k[0], c) for k, c in ft.to_dict().items()), data.count() - ft.num_rows)
+        col = data[self.column] if self.udfInputAsString else None
+        return self.bin_groups(((k[0], c) for k, c in ft.to_dict().items()), data.count() - ft.num_rows, col)
 
-    def bin_groups(self, groups, null_rows):
+    def bin_groups(self, groups, null_rows, string_column=None):
         """(value, count) groups of the raw column + its NULL rows -> {(bin label,): count}: the UDF's result cast to
         STRING, NULL filled with "NullValue", counts added per bin."""
         bins = {}
@@ -988,7 +1018,10 @@ class Histogram(Analyzer):
                 label if isinstance(label, str) else _spark_string(label))
             bins[(label,)] = bins.get((label,), 0) + int(count)
         for v, c in groups:
-            add(float(v) if isinstance(v, float) else v, c)
+            v = float(v) if isinstance(v, float) else v
+            if self.udfInputAsString and v is not None and not isinstance(v, str):
+                v = _spark_string(v, string_column)
+            add(v, c)
         if null_rows:
             add(None, null_rows)
         return bins

@@ -1110,7 +1110,7 @@ template <int BINS, int TILE, bool NARROW>
 __global__ void __launch_bounds__(kFreqBlock, BINS <= kDigitBins ? 2 : 1)
 scatter2_fast_kernel(const FastItem* __restrict__ items, const void* __restrict__ in, unsigned int mask,
                      unsigned long long cap, unsigned long long* __restrict__ gcursor, void* __restrict__ out,
-                     Counters* __restrict__ ctr, NarrowKey nk, Spill sp, int windowed = 0, unsigned int p0 = 0) {
+                     Counters* __restrict__ ctr, NarrowKey nk, Spill sp) {
     using KeyT = typename std::conditional<NARROW, uint32_t, unsigned long long>::type;
     const KeyT* __restrict__ in_h = static_cast<const KeyT*>(in);
     KeyT* __restrict__ out_h = static_cast<KeyT*>(out);
@@ -1141,12 +1141,8 @@ scatter2_fast_kernel(const FastItem* __restrict__ items, const void* __restrict_
             keepm |= (t0 + (unsigned long long)j * kFreqBlock + threadIdx.x < it.end ? 1u : 0u) << j;
         }
         const unsigned long long n0 = t0 + TILE;
-        // bucket part + 256 b at (part + 256 b) * cap; windowed: the window buffer's run (part - p0) * bins + b
         scatter_tile_reserve<BINS, TILE, NARROW>(h, keepm, 8, mask, hist, start, cursor, sh, gcursor, cap,
-                                         [part, windowed, p0, mask](int b) {
-                                             return windowed ? (part - p0) * (mask + 1ull) + b
-                                                             : part + (unsigned long long)kDigitBins * b;
-                                         },
+                                         [part](int b) { return part + (unsigned long long)kDigitBins * b; },
                                          [part, mask](int b) { return part * (mask + 1ull) + b; }, &lovf, sp,
                                          [nk](uint64_t v) {
                                              return NARROW ? mix64(narrow_canon(nk, (uint32_t)v)) : v;
@@ -1221,26 +1217,6 @@ struct BuildItem {
     unsigned int split;             // 1: the bucket is split over several items (merge with atomics)
 };
 
-// The build items of one window of the fast path (build_fast, windowed): workgroup i builds bucket
-// (p0 + i / bins) + 256 * (i % bins) from its pass-2 run at i * cap2 of the window buffer, the run's length read from
-// the pass-2 reservation counter (clipped to cap2: the rest was spilled) -- no host round trip between the passes.
-struct WinItems {
-    const unsigned long long* gc2;  // pass-2 reservation counters, part * bins + b
-    unsigned long long cap2;
-    unsigned int p0, bins;
-};
-
-__device__ __forceinline__ BuildItem win_item(const WinItems& w, unsigned int i) {
-    const unsigned int part = w.p0 + i / w.bins, b = i % w.bins;
-    const unsigned long long n = w.gc2[(unsigned long long)part * w.bins + b];
-    BuildItem it;
-    it.begin = (unsigned long long)i * w.cap2;
-    it.end = it.begin + (n < w.cap2 ? n : w.cap2);
-    it.bucket = part + (unsigned int)kDigitBins * b;
-    it.split = 0;
-    return it;
-}
-
 __global__ void region_init_kernel(const BuildItem* __restrict__ items, int nitems, Slot* __restrict__ slots,
                                    unsigned long long* __restrict__ reps) {
     const BuildItem it = items[blockIdx.x];
@@ -1287,14 +1263,14 @@ __global__ void __launch_bounds__(kBuildBlock)
 build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
              const unsigned long long* __restrict__ rows, const long long* __restrict__ weights,
              Slot* __restrict__ slots, unsigned long long* __restrict__ reps, Counters* __restrict__ ctr,
-             SummaryPartial* __restrict__ parts, double n, NarrowKey nk, WinItems win = WinItems{}) {
+             SummaryPartial* __restrict__ parts, double n, NarrowKey nk) {
     const uint32_t* __restrict__ hs32 = reinterpret_cast<const uint32_t*>(hs);
     using C = typename std::conditional<WEIGHTED, unsigned long long, unsigned int>::type;
     __shared__ unsigned long long lkey[kRegion];
     __shared__ C lcnt[kRegion];
     __shared__ unsigned long long lrep[GENERAL ? kRegion : 1];
     __shared__ unsigned int lovf;
-    const BuildItem it = items ? items[blockIdx.x] : win_item(win, blockIdx.x);
+    const BuildItem it = items[blockIdx.x];
     for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
         lkey[i] = kEmpty;
         lcnt[i] = 0;
@@ -2361,145 +2337,6 @@ bool choose_narrow(dq_ctx* ctx, const dq_freq_table* t, int64_t nrows, DevBuf& b
     return true;
 }
 
-// Windowed second pass + build (r05): the 256 first-level partitions are taken `wp` at a time; one window's pass-2
-// runs (wp x bins buckets, ~31 MB per partition at C4's size) are written to one window buffer and the window's
-// buckets are built right after, while those runs are still in the 256 MB Infinity Cache, so the pass-2 write and
-// the build's re-read of the keys stay on die instead of crossing HBM twice. Every window reuses
-// the same buffer. Build items come from the pass-2 counters on the device (WinItems); the host syncs once, after
-// the last window.
-constexpr int kWindowParts = 2;
-constexpr unsigned long long kPass2ItemWin = 16384;  // smaller pass-2 items: a window alone must fill the chip
-
-int window_parts() {
-    const char* e = getenv("DQ_FREQ_WINDOW_PARTS");
-    const int v = e ? atoi(e) : kWindowParts;
-    return (v >= 1 && v <= kDigitBins && kDigitBins % v == 0) ? v : kWindowParts;
-}
-
-int build_fast_windowed(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, const void* h1,
-                        unsigned long long cap1, const std::vector<unsigned long long>& pcount,
-                        unsigned long long spilled1, const Spill& sp, bool narrow, const NarrowKey& nk, int bits,
-                        size_t ksz, bool* done) {
-    hipStream_t s = dq::ctx_stream(ctx);
-    const int wp = window_parts();
-    unsigned long long n = 0;
-    for (unsigned long long c : pcount) n += c;
-    void* h2 = nullptr;
-    size_t h2_bytes = 0;
-    for (int grow = 0; grow < 8 && bits <= kMaxPartBits; ++grow, ++bits) {
-        const int bins = 1 << (bits - 8);
-        const uint64_t nb = 1ull << bits;
-        const unsigned long long per = n / nb;
-        const unsigned long long cap2 = per + per / 4 + 2048;
-        // items in partition order; window w = partitions [w wp, (w + 1) wp)
-        std::vector<FastItem> items;
-        std::vector<int> first(kDigitBins / wp + 1, 0);
-        for (int p = 0; p < kDigitBins; ++p) {
-            if (p % wp == 0) first[p / wp] = (int)items.size();
-            for (int x = 0; x < kP1Sub; ++x) {
-                const int q = p * kP1Sub + x;
-                const unsigned long long base = (unsigned long long)q * cap1;
-                for (unsigned long long o = 0; o < pcount[q]; o += kPass2ItemWin)
-                    items.push_back(FastItem{base + o, base + std::min<unsigned long long>(pcount[q], o + kPass2ItemWin),
-                                             (unsigned int)p, 0u});
-            }
-        }
-        first[kDigitBins / wp] = (int)items.size();
-        FastItem* ditems = nullptr;
-        unsigned long long* gc2 = nullptr;
-        SummaryPartial* bparts = nullptr;
-        FQ_HIP(ctx, buf.alloc((void**)&ditems, sizeof(FastItem) * std::max<size_t>(items.size(), 1)));
-        FQ_HIP(ctx, buf.alloc((void**)&gc2, sizeof(unsigned long long) * nb));
-        FQ_HIP(ctx, buf.alloc((void**)&bparts, sizeof(SummaryPartial) * nb));
-        const size_t need = (size_t)cap2 * wp * bins * ksz;
-        if (need > h2_bytes) {
-            h2_bytes = need;
-            FQ_HIP(ctx, buf.alloc((void**)&h2, h2_bytes));
-        }
-        FQ_HIP(ctx, hipMemsetAsync(gc2, 0, sizeof(unsigned long long) * nb, s));
-        FQ_HIP(ctx, hipMemcpyAsync(&t->ctr->spilled, &spilled1, sizeof(spilled1), hipMemcpyHostToDevice, s));
-        if (!items.empty())
-            FQ_HIP(ctx, hipMemcpyAsync(ditems, items.data(), sizeof(FastItem) * items.size(), hipMemcpyHostToDevice, s));
-        // the table: every region is written whole by its bucket's build (no split items on this path)
-        const uint64_t cap = nb * kRegion;
-        release_slots(t, ctx);
-        t->home = ctx;
-        t->slots_bytes = cap * sizeof(Slot);
-        t->reps_bytes = 0;
-        t->slots = (Slot*)dq::scratch_alloc(ctx, t->slots_bytes);
-        if (!t->slots) return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
-        t->cap = cap;
-        t->bits = bits;
-        const double build_n = (double)t->host_ctr.num_rows;
-        const unsigned int mask = (unsigned int)bins - 1;
-        for (int w = 0; w < kDigitBins / wp; ++w) {
-            const int ni = first[w + 1] - first[w];
-            const unsigned int p0 = (unsigned int)(w * wp);
-#define DQ_P2W(B, T, N)                                                                                           \
-    hipLaunchKernelGGL((scatter2_fast_kernel<B, T, N>), dim3(ni), dim3(kFreqBlock), 0, s, ditems + first[w], h1, mask, \
-                       cap2, gc2, h2, t->ctr, nk, sp, 1, p0)
-            if (ni && bins > kDigitBins) {
-                if (narrow) DQ_P2W(4096, kPartTile, true); else DQ_P2W(4096, kPartTile, false);
-            } else if (ni) {
-                if (narrow) DQ_P2W(kDigitBins, kPartTileFast, true); else DQ_P2W(kDigitBins, kPartTileFast, false);
-            }
-#undef DQ_P2W
-            const WinItems wi{gc2, cap2, p0, (unsigned int)bins};
-            if (narrow)
-                hipLaunchKernelGGL((build_kernel<false, false, true>), dim3(wp * bins), dim3(kBuildBlock), 0, s, nullptr,
-                                   static_cast<const unsigned long long*>(h2), nullptr, nullptr, t->slots, nullptr,
-                                   t->ctr, bparts + (size_t)w * wp * bins, build_n, nk, wi);
-            else
-                hipLaunchKernelGGL((build_kernel<false, false>), dim3(wp * bins), dim3(kBuildBlock), 0, s, nullptr,
-                                   static_cast<const unsigned long long*>(h2), nullptr, nullptr, t->slots, nullptr,
-                                   t->ctr, bparts + (size_t)w * wp * bins, build_n, NarrowKey{}, wi);
-        }
-        FQ_HIP(ctx, hipGetLastError());
-        FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-        FQ_HIP(ctx, hipStreamSynchronize(s));
-        if (t->host_ctr.pad[1]) return DQ_OK;  // the spill buffer overflowed: the exact path
-        const unsigned long long nspill = std::min(t->host_ctr.spilled, sp.cap);
-        if (nspill) {
-            const int grid = (int)std::min<unsigned long long>((nspill + kSpillChunk - 1) / kSpillChunk, 2048);
-            hipLaunchKernelGGL(spill_insert_kernel, dim3(grid), dim3(kBuildBlock), 0, s, sp.keys, nspill, t->slots, bits,
-                               t->ctr);
-            FQ_HIP(ctx, hipGetLastError());
-        }
-        std::vector<SummaryPartial> hparts(nb);
-        FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
-        FQ_HIP(ctx, hipMemcpyAsync(hparts.data(), bparts, nb * sizeof(SummaryPartial), hipMemcpyDeviceToHost, s));
-        FQ_HIP(ctx, hipStreamSynchronize(s));
-        t->pre_valid = 0;
-        if (t->host_ctr.overflow == 0 && nspill == 0) {  // spilled keys: the summary scans the table
-            SummaryPartial acc = {0, 0, 0, 0, 0, 0};
-            for (const SummaryPartial& p : hparts) summary_merge(acc, p);
-            t->pre_valid = 1;
-            t->pre_n = (int64_t)build_n;
-            t->pre_groups = acc.groups;
-            t->pre_unique = acc.unique;
-            t->pre_maxc = acc.maxc;
-            t->pre_ent = acc.ent;
-            t->pre_nonfinite = acc.nonfinite;
-        }
-        if (getenv("DQ_DEBUG_FREQ"))
-            fprintf(stderr, "[freq fast windowed] rows=%lld bits=%d wp=%d items=%zu spilled=%llu ovf=%llu\n",
-                    (long long)nrows, bits, wp, items.size(), nspill, t->host_ctr.overflow);
-        if (t->host_ctr.overflow == 0) {
-            *done = true;
-            ctx->freq_paths[DQ_FREQ_PATH_FAST_DONE]++;
-            ctx->freq_paths[DQ_FREQ_PATH_FAST_WINDOWED]++;
-            if (nspill) ctx->freq_paths[DQ_FREQ_PATH_FAST_SPILL]++;
-            return DQ_OK;
-        }
-        Counters c = t->host_ctr;  // a region overflowed: again with more buckets
-        c.overflow = 0;
-        c.mismatch = 0;
-        FQ_HIP(ctx, hipMemcpyAsync(t->ctr, &c, sizeof(Counters), hipMemcpyHostToDevice, s));
-        FQ_HIP(ctx, hipStreamSynchronize(s));
-    }
-    return DQ_OK;
-}
-
 int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* done, bool allow_narrow = true) {
     *done = false;
     hipStream_t s = dq::ctx_stream(ctx);
@@ -2589,8 +2426,6 @@ int build_fast(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, bool* 
                 (int)narrow);
     if (bits < 8 || bits > kMaxPartBits) return DQ_OK;
     bits = std::max(bits, 9);  // a partition is 8 sub-regions: the second pass gathers them into buckets
-    if (!getenv("DQ_FREQ_NO_WINDOW"))
-        return build_fast_windowed(ctx, t, nrows, buf, h1, cap1, pcount, spilled1, sp, narrow, nk, bits, ksz, done);
     void* h2 = nullptr;
     size_t h2_bytes = 0;
     for (int grow = 0; grow < 8 && bits <= kMaxPartBits; ++grow, ++bits) {

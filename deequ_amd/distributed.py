@@ -430,7 +430,8 @@ class DistributedAnalysisRunner:
         def binned():
             block = self.local.group_block(shard, [a.column], False)
             groups = ((k[0], c) for k, c in zip(block.keys(), block.counts.tolist()))
-            return a.bin_groups(groups, shard.count() - block.num_rows)
+            col = shard[a.column] if getattr(a, "udfInputAsString", False) else None
+            return a.bin_groups(groups, shard.count() - block.num_rows, col)
         local = self._local_step(binned)
         blob = json.dumps([[k[0], int(c)] for k, c in local.items()]).encode()
         bins = {}

@@ -300,8 +300,15 @@ class KLLState:
         """KLLState.sum (A/KLLSketch.scala:49-54) through the library's merge (dq_kll_merge_states): the same
         QuantileNonSample.merge + condense as `self.qSketch.merge(other.qSketch)` below, without the Python list work
         (13 columns x chunk merges sat between the C5 profiler's passes)."""
-        from .native import kll_merge_states
-        return KLLState.fromBytes(kll_merge_states(self.toBytes(), other.toBytes()))
+        from .native import kll_merge_states, NativeError
+        try:
+            return KLLState.fromBytes(kll_merge_states(self.toBytes(), other.toBytes()))
+        except (OSError, NativeError) as e:
+            if isinstance(e, NativeError) and "malformed" in str(e):
+                raise
+            # the merge is host-only state algebra: without a loadable libdq.so (a host with no ROCm runtime merging
+            # persisted states, runOnAggregatedStates) the restated merge gives the same bytes
+            return self.sum_restated(other)
 
     def sum_restated(self, other):
         """KLLState.sum over the Python QuantileNonSample (the library's merge is checked against it)."""

@@ -47,8 +47,7 @@ SYNTH_STR_CAT50, SYNTH_STR_BOOL, SYNTH_STR_CAT100, SYNTH_STR_INT, SYNTH_STR_DEC,
 HLL_NUM_WORDS = 52
 
 # dq_scan_kernel, in enum order
-FREQ_PATHS = ("fast", "fast_narrow", "fast_done", "exact", "partitioned", "sorted", "small", "small_optimistic", "fast_spill",
-              "fast_windowed")
+FREQ_PATHS = ("fast", "fast_narrow", "fast_done", "exact", "partitioned", "sorted", "small", "small_optimistic", "fast_spill")
 SCAN_KERNELS = ("striped", "striped_heavy", "heavy8", "heavy8_full", "bits", "pred_simple", "pred_vm", "regex",
                 "strings", "where_fused", "where_masks")
 

@@ -298,8 +298,11 @@ def _block_table(state):
     f = state.frequencies
     if isinstance(f, G.GroupBlock) and not getattr(f, "distinct", False):
         ft = state.device_table()
-        keys, counts = ft.export_raw()
-        f = G.GroupBlock([G.take(c, keys) for c in f.columns], counts)
+        if hasattr(ft, "distinct_block"):  # a merged state past the int32 offsets: key-disjoint split builds
+            f = ft.distinct_block()
+        else:
+            keys, counts = ft.export_raw()
+            f = G.GroupBlock([G.take(c, keys) for c in f.columns], counts)
     elif not isinstance(f, G.GroupBlock):
         if not isinstance(f, engine.FrequencyTable) or f.key_kind() == N.FREQ_KEYS_VALUES:
             return None

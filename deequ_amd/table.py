@@ -75,6 +75,7 @@ class Column:
             length = len(offsets) - 1 if self.spark_type == N.TYPE_STRING else len(values)
         self.length = int(length)
         self.device = None  # dict of torch tensors once resident in HBM
+        self.tz = None  # TIMESTAMP: the Arrow column's time zone (None = naive, read as the UTC session zone)
 
     @property
     def type_name(self):
@@ -265,7 +266,9 @@ def _column_from_arrow(name, arr, pa):
     if pa.types.is_timestamp(t):
         us = arr.cast(pa.timestamp("us", tz=t.tz), safe=False) if t.unit != "us" else arr
         vals = np.frombuffer(us.buffers()[1], dtype=np.int64)[us.offset:us.offset + n]
-        return Column(name, N.TYPE_TIMESTAMP, vals, validity)
+        col = Column(name, N.TYPE_TIMESTAMP, vals, validity)
+        col.tz = t.tz
+        return col
     spark = {pa.int8(): N.TYPE_BYTE, pa.int16(): N.TYPE_SHORT, pa.int32(): N.TYPE_INT, pa.int64(): N.TYPE_LONG,
              pa.float32(): N.TYPE_FLOAT, pa.float64(): N.TYPE_DOUBLE, pa.date32(): N.TYPE_DATE}.get(t)
     if spark is None:

@@ -297,8 +297,7 @@ typedef enum dq_freq_path {
     DQ_FREQ_PATH_SMALL = 6,             /* one-pass small builds launched (sized or optimistic)                */
     DQ_FREQ_PATH_SMALL_OPTIMISTIC = 7,  /* optimistic small builds (no sizing pass) that produced their table  */
     DQ_FREQ_PATH_FAST_SPILL = 8,        /* fast builds whose full buckets spilled keys (inserted after the build) */
-    DQ_FREQ_PATH_FAST_WINDOWED = 9,     /* fast builds whose pass 2 + build ran window by window (cache-resident) */
-    DQ_FREQ_PATH_COUNT = 10
+    DQ_FREQ_PATH_COUNT = 9
 } dq_freq_path;
 int64_t dq_freq_path_count(const dq_ctx* ctx, int32_t path);
 

@@ -88,3 +88,23 @@ def test_merged_string_state_split_under_the_offset_limit(monkeypatch):
     assert isinstance(st.frequencies, G.BlockParts)
     assert len(st.frequencies.split_by_key()) > 1
     assert isinstance(st.device_table(), D.analyzers.SplitFrequencies)
+
+
+def test_split_merged_state_persists_and_loads_back(monkeypatch, tmp_path):
+    """a merged string / multi-column state built as key-disjoint splits (the int32 offset limit injected
+    small) persists through HdfsStateProvider as its distinct groups and loads back to the same metrics
+    (A/StateProvider.scala:187-262 layouts; FrequenciesAndNumRows.sum, A/GroupingAnalyzers.scala:127-147)."""
+    data, types = _data(40_000, seed=13)
+    full, ct = _chunked(data, types, [0, 17_000, 40_000])
+    monkeypatch.setattr(G, "STRING_KEY_LIMIT", 4096)
+    a = D.Uniqueness(["s", "k"])
+    st = a.computeStateFrom(ct.chunks[0]).sum(a.computeStateFrom(ct.chunks[1]))
+    assert isinstance(st.device_table(), D.analyzers.SplitFrequencies)
+    want = a.computeMetricFrom(st).value.get()
+    provider = D.HdfsStateProvider(None, str(tmp_path / "split"))
+    provider.persist(a, st)
+    back = provider.load(a)
+    assert back.numRows == st.numRows
+    assert _close(a.computeMetricFrom(back).value.get(), want)
+    full_state = a.computeStateFrom(full)
+    assert _close(a.computeMetricFrom(full_state).value.get(), want)

@@ -364,3 +364,20 @@ def test_histogram_binning_udf_per_distinct_value(kats):
     assert {k: d.absolute for k, d in h.values.items()} == want
     for k, d in h.values.items():
         assert d.ratio == want[k] / n
+
+
+def test_histogram_binning_udf_string_input():
+    """Histogram(..., udfInputAsString=True): the UDF sees the Spark string form of a non-string column's values (as a
+    Scala UDF declared over String does through Spark's implicit cast) -- a first-character binning of DOUBLE values
+    counts "1.0", "1.5", "10.25" together."""
+    vals = [1.0, 1.5, 10.25, 2.0, None, 2.5, 1.0]
+    t = Table.from_pydict({"x": vals}, types={"x": "double"})
+    seen = []
+
+    def first(s):
+        seen.append(s)
+        return None if s is None else s[:1]
+    h = D.Histogram("x", first, udfInputAsString=True).calculate(t).value.get()
+    assert {k: d.absolute for k, d in h.values.items()} == {"1": 4, "2": 2, "NullValue": 1}
+    assert all(v is None or isinstance(v, str) for v in seen)
+    assert "1.0" in seen and "10.25" in seen
