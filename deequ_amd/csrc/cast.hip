@@ -217,6 +217,8 @@ static int cast_single(dq_ctx* ctx, const dq_column* column, int64_t nrows, int3
     CA_HIP(ctx, hipSetDevice(dq::ctx_device(ctx)));
     hipStream_t s = dq::ctx_stream(ctx);
     CBuffers buf;
+    if (column->flags & DQ_COL_OFFSETS64)
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_cast_column: int64 string offsets are for the grouping builds only");
     dq::CastSource c;
     memset(&c, 0, sizeof(c));
     c.elem = is_string ? dq::ET_NONE : dq::elem_of(t);

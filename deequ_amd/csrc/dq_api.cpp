@@ -24,6 +24,29 @@
 #include "dq_common.h"
 #include "dq_internal.h"
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+namespace {
+// DQ_SEGV_TRACE=1: a host-side fault of the library prints its native backtrace (addresses into libdq.so, resolved
+// with addr2line against the same build) before the process dies -- the host code's equivalent of a GPU printf.
+void dq_segv_trace(int sig) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "[dq] fatal signal, native backtrace:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+struct DqSegvTrace {
+    DqSegvTrace() {
+        if (getenv("DQ_SEGV_TRACE")) signal(SIGSEGV, dq_segv_trace);
+    }
+} dq_segv_trace_init;
+}  // namespace
+
 
 using namespace dq;
 
@@ -468,6 +491,8 @@ int dq_scan(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, con
             return fail(ctx, DQ_ERR_UNSUPPORTED, "column %d: unknown spark type %d", c, col.spark_type);
         if (col.spark_type == DQ_TYPE_STRING && nrows > 0 && !col.offsets)
             return fail(ctx, DQ_ERR_INVALID_ARGUMENT, "string column %d without offsets", c);
+        if (col.flags & DQ_COL_OFFSETS64)
+            return fail(ctx, DQ_ERR_UNSUPPORTED, "column %d: int64 string offsets are for the grouping builds only", c);
         if (col.spark_type == DQ_TYPE_DECIMAL && (col.decimal_precision > 18 || col.decimal_scale < 0 || col.decimal_scale > 18))
             return fail(ctx, DQ_ERR_UNSUPPORTED, "column %d: decimal precision > 18 unsupported", c);
         if ((col.flags & DQ_COL_DEVICE) && nrows > 0) {

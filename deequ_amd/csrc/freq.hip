@@ -84,9 +84,24 @@ struct KeyCol {
     const void* values;
     const uint8_t* validity;
     const int32_t* offsets;
+    const int64_t* offsets64;  // DQ_COL_OFFSETS64: int64 offsets instead (a column past 2^31 bytes)
     int32_t spark_type;
     int32_t elem;
 };
+
+// Row r's UTF-8 bytes of a string key column: start pointer and length.
+__host__ __device__ __forceinline__ const uint8_t* str_span(const KeyCol& c, int64_t r, int& len) {
+    int64_t o0, o1;
+    if (c.offsets64) {
+        o0 = c.offsets64[r];
+        o1 = c.offsets64[r + 1];
+    } else {
+        o0 = c.offsets[r];
+        o1 = c.offsets[r + 1];
+    }
+    len = (int)(o1 - o0);
+    return static_cast<const uint8_t*>(c.values) + o0;
+}
 
 struct KeySpec {
     KeyCol cols[kMaxKeys];
@@ -245,8 +260,9 @@ __device__ __forceinline__ bool row_key(const KeySpec& ks, int64_t r, uint64_t& 
         if (is_valid(c, r)) {
             any = true;
             if (c.spark_type == DQ_TYPE_STRING) {
-                const int32_t o0 = c.offsets[r], o1 = c.offsets[r + 1];
-                ch = dev_xxh_bytes(static_cast<const uint8_t*>(c.values) + o0, o1 - o0, ks.seed);
+                int len;
+                const uint8_t* p = str_span(c, r, len);
+                ch = dev_xxh_bytes(p, len, ks.seed);
             } else {
                 ch = xxh_long(canonical(c, r), ks.seed);
             }
@@ -272,10 +288,10 @@ __device__ bool rows_equal(const KeySpec& ks, int64_t a, int64_t b) {
             const uint8_t* pa;
             const uint8_t* pb;
             int la, lb;
-            if (va) { pa = static_cast<const uint8_t*>(c.values) + c.offsets[a]; la = c.offsets[a + 1] - c.offsets[a]; }
+            if (va) { pa = str_span(c, a, la); }
             else if (ks.string_null_is_value) { pa = kNullValue; la = 9; va = true; }
             else { pa = nullptr; la = 0; }
-            if (vb) { pb = static_cast<const uint8_t*>(c.values) + c.offsets[b]; lb = c.offsets[b + 1] - c.offsets[b]; }
+            if (vb) { pb = str_span(c, b, lb); }
             else if (ks.string_null_is_value) { pb = kNullValue; lb = 9; vb = true; }
             else { pb = nullptr; lb = 0; }
             if (va != vb) return false;
@@ -1438,12 +1454,12 @@ __device__ __forceinline__ bool short_key_tuple(const KeySpec& ks, int64_t r, ui
         }
         return true;
     }
-    const int32_t o0 = c.offsets[r], len = c.offsets[r + 1] - o0;
+    int len;
+    const uint8_t* p = str_span(c, r, len);
     if (len > 15) {
         b0 = b1 = kTupleLong;
         return false;
     }
-    const uint8_t* p = static_cast<const uint8_t*>(c.values) + o0;
     const uint8_t* a = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(p - a);
     const int ndw = (int)((sh + (uint32_t)len + 3) >> 2);  // only dwords holding bytes of [p, p + len): <= 5
@@ -1507,8 +1523,9 @@ __device__ __forceinline__ bool row_key_str1(const KeySpec& ks, int64_t r, uint6
     } else if (is_short) {  // valid, or "NullValue" for a Histogram's NULL row
         ch = xxh_short_words(b0, b1, ks.seed);
     } else {
-        const int32_t o0 = c.offsets[r], o1 = c.offsets[r + 1];
-        ch = dev_xxh_bytes(static_cast<const uint8_t*>(c.values) + o0, o1 - o0, ks.seed);
+        int len;
+        const uint8_t* p = str_span(c, r, len);
+        ch = dev_xxh_bytes(p, len, ks.seed);
     }
     const uint64_t acc = mix64(ks.seed + P64_1 * 1ull + ch);
     if (!any && !ks.include_nulls) return false;
@@ -2975,8 +2992,8 @@ int multi_frequencies_general(dq_ctx* ctx, const dq_column* columns, int ncols, 
 int multi_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
                       int nkeys, const dq_freq_options* opt, dq_freq_table** out) {
     for (int c = 0; c < ncols; ++c)
-        if (columns[c].flags & DQ_COL_DEVICE)
-            return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "multi-device grouping takes host columns");
+        if (columns[c].flags & (DQ_COL_DEVICE | DQ_COL_OFFSETS64))
+            return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "multi-device grouping takes host columns with int32 offsets");
     if (opt->weights)
         return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "multi-device grouping: weighted input takes a one-device context");
     for (int k = 0; k < nkeys; ++k)
@@ -3110,13 +3127,20 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
         KeyCol& kc = t->ks.cols[i];
         kc.spark_type = col.spark_type;
         kc.elem = elem_of(col.spark_type);
+        const bool off64 = col.spark_type == DQ_TYPE_STRING && (col.flags & DQ_COL_OFFSETS64);
+        kc.offsets64 = nullptr;
         if (col.flags & DQ_COL_DEVICE) {
             kc.values = col.values;
             kc.validity = col.validity;
-            kc.offsets = col.offsets;
+            kc.offsets = off64 ? nullptr : col.offsets;
+            kc.offsets64 = off64 ? reinterpret_cast<const int64_t*>(col.offsets) : nullptr;
         } else {
             // stage host buffers (kept alive with the table: rows are re-read by verify / export)
-            size_t vbytes = col.spark_type == DQ_TYPE_STRING ? (nrows ? (size_t)col.offsets[nrows] : 0)
+            const int64_t send = (!nrows || col.spark_type != DQ_TYPE_STRING)
+                                     ? 0
+                                     : (off64 ? reinterpret_cast<const int64_t*>(col.offsets)[nrows]
+                                              : (int64_t)col.offsets[nrows]);
+            size_t vbytes = col.spark_type == DQ_TYPE_STRING ? (size_t)send
                                                               : (size_t)nrows * std::max(1, elem_size(kc.elem));
             void* v = nullptr;
             FQ_HIP(ctx, hipMalloc(&v, vbytes + 16));
@@ -3132,11 +3156,13 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
                 kc.validity = (const uint8_t*)vd;
             }
             if (col.spark_type == DQ_TYPE_STRING) {
+                const size_t ow = off64 ? 8 : 4;
                 void* od = nullptr;
-                FQ_HIP(ctx, hipMalloc(&od, ((size_t)nrows + 1) * 4));
+                FQ_HIP(ctx, hipMalloc(&od, ((size_t)nrows + 1) * ow));
                 staged.push_back(od);
-                FQ_HIP(ctx, hipMemcpyAsync(od, col.offsets, ((size_t)nrows + 1) * 4, hipMemcpyHostToDevice, s));
-                kc.offsets = (const int32_t*)od;
+                FQ_HIP(ctx, hipMemcpyAsync(od, col.offsets, ((size_t)nrows + 1) * ow, hipMemcpyHostToDevice, s));
+                kc.offsets = off64 ? nullptr : (const int32_t*)od;
+                kc.offsets64 = off64 ? (const int64_t*)od : nullptr;
             }
         }
         if (kc.elem == ET_NONE && kc.spark_type != DQ_TYPE_STRING) {
@@ -3740,6 +3766,7 @@ extern "C" int dq_partition_keys(dq_ctx* ctx, const dq_column* column, int64_t n
     c.values = column->values;
     c.validity = column->validity;
     c.offsets = nullptr;
+    c.offsets64 = nullptr;
     c.spark_type = column->spark_type;
     c.elem = elem_of(column->spark_type);
     unsigned long long* dev = nullptr;

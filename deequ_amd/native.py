@@ -23,6 +23,7 @@ TYPE_BOOLEAN, TYPE_BYTE, TYPE_SHORT, TYPE_INT, TYPE_LONG, TYPE_FLOAT, TYPE_DOUBL
     TYPE_DATE, TYPE_TIMESTAMP, TYPE_DECIMAL = range(1, 12)
 
 COL_DEVICE = 0x1
+COL_OFFSETS64 = 0x2  # STRING: int64 offsets (dq_frequencies only)
 SCAN_OUT_DEVICE = 0x1
 FREQ_INCLUDE_NULLS = 0x1
 FREQ_KEYS_VALUES, FREQ_KEYS_ROWS = 0, 1

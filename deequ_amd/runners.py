@@ -328,6 +328,17 @@ class AnalysisRunner:
         chunk) does not reach the merge (the reference's findStateForParticularGrouping would require one): it keeps
         the chunk failure metrics."""
         analyzers = list(dict.fromkeys(analyzers))  # one state per analyzer: the merge adds each loader's state once
+        # grouping analyzers: one frequency table over the whole shard (the chunks' key columns concatenated where
+        # they live, int64 string offsets) instead of per-chunk tables merged through host memory -- the same
+        # groups as Spark's shuffle of the partitions' partial counts (R/AnalysisRunner.scala:259-287)
+        grouping = [a for a in analyzers if isinstance(a, GroupingAnalyzer)]
+        whole = AnalyzerContext.empty()
+        if grouping and len(data.chunks) > 1:
+            cols = sorted({c for a in grouping for c in a.groupingColumns() if c in data})
+            whole = AnalysisRunner.doAnalysisRun(data.concat(cols), grouping, aggregateWith, saveStatesWith)
+            analyzers = [a for a in analyzers if not isinstance(a, GroupingAnalyzer)]
+            if not analyzers:
+                return whole
         providers, failures = [], {}
         for chunk in data.chunks:
             p = InMemoryStateProvider()
@@ -357,7 +368,7 @@ class AnalysisRunner:
                     empty[a] = a.computeMetricFrom(None)
                 except Exception as e:
                     empty[a] = a.toFailureMetric(e)
-        return merged + AnalyzerContext(empty) + AnalyzerContext(failures)
+        return merged + AnalyzerContext(empty) + AnalyzerContext(failures) + whole
 
     @staticmethod
     def _runScanningAnalyzers(data, analyzers, aggregateWith=None, saveStatesTo=None):

@@ -188,12 +188,12 @@ class Column:
         c.decimal_precision = self.decimal_precision
         c.decimal_scale = self.decimal_scale
         if self.device is not None:
-            c.flags = N.COL_DEVICE
+            c.flags = N.COL_DEVICE | (N.COL_OFFSETS64 if getattr(self, "offsets64", False) else 0)
             c.values = self.device["values"].data_ptr() if self.device.get("values") is not None else None
             c.validity = self.device["validity"].data_ptr() if self.device.get("validity") is not None else None
             c.offsets = self.device["offsets"].data_ptr() if self.device.get("offsets") is not None else None
         else:
-            c.flags = 0
+            c.flags = N.COL_OFFSETS64 if getattr(self, "offsets64", False) else 0
             c.values = self.values.ctypes.data if self.values is not None and len(self.values) else None
             c.validity = self.validity.ctypes.data if self.validity is not None else None
             c.offsets = self.offsets.ctypes.data if self.offsets is not None else None
@@ -486,6 +486,15 @@ class ChunkedTable:
     def count(self):
         return self.nrows
 
+    def concat(self, names):
+        """The named columns of every chunk as one Table, concatenated where the chunks live (HBM when every chunk is
+        device-resident, else host memory): a string column's offsets become int64 (Arrow large_string,
+        DQ_COL_OFFSETS64) so its bytes may pass 2^31. The grouping builds take it whole, so a grouping over the shard
+        is one frequency table (not per-chunk tables merged through host memory)."""
+        on_device = all(all(c[n].device is not None for n in names) for c in self.chunks)
+        cols = [(_concat_device if on_device else _concat_host)([c[n] for c in self.chunks]) for n in names]
+        return Table(cols)
+
 
 def _infer_py_type(items):
     nn = [x for x in items if x is not None]
@@ -540,3 +549,72 @@ def _csv_field_type(x):
     if x.lower() in ("true", "false"):
         return N.TYPE_BOOLEAN
     return N.TYPE_STRING
+
+
+def _concat_host(parts):
+    """Host columns of consecutive chunks as one column (int64 string offsets)."""
+    first = parts[0]
+    n = sum(p.length for p in parts)
+    valid = np.concatenate([unpack_validity(p.validity, p.length) for p in parts]) if parts else np.zeros(0, bool)
+    validity = None if valid.all() else pack_validity(valid)
+    if first.spark_type == N.TYPE_STRING:
+        offs, datas, base = [np.zeros(1, dtype=np.int64)], [], 0
+        for p in parts:
+            o = np.asarray(p.offsets, dtype=np.int64)[:p.length + 1]
+            datas.append(np.asarray(p.values, dtype=np.uint8)[int(o[0]):int(o[-1])])
+            offs.append(o[1:] - o[0] + base)
+            base += int(o[-1] - o[0])
+        col = Column(first.name, N.TYPE_STRING, np.concatenate(datas) if datas else np.zeros(0, np.uint8), validity,
+                     np.concatenate(offs), length=n)
+        col.offsets64 = True
+        return col
+    vals = np.concatenate([np.asarray(p.values)[:p.length] for p in parts])
+    return Column(first.name, first.spark_type, vals, validity, decimal_precision=first.decimal_precision,
+                  decimal_scale=first.decimal_scale, length=n)
+
+
+def _device_valid_bits(col, torch):
+    """One bool per row of a device column's validity (all True without a bitmap)."""
+    d = col.device
+    dev = d["values"].device
+    if d.get("validity") is None:
+        return torch.ones(col.length, dtype=torch.bool, device=dev)
+    v = d["validity"][:(col.length + 7) // 8]
+    bits = (v.unsqueeze(1) >> torch.arange(8, device=dev, dtype=torch.uint8)) & 1
+    return bits.reshape(-1)[:col.length].bool()
+
+
+def _concat_device(parts):
+    """Device columns of consecutive chunks as one device column: values / UTF-8 bytes copied in HBM, validity bits
+    re-packed at the chunk boundaries, string offsets rebased into int64."""
+    import torch
+    first = parts[0]
+    dev = first.device["values"].device
+    n = sum(p.length for p in parts)
+    col = Column(first.name, first.spark_type, None, None, decimal_precision=first.decimal_precision,
+                 decimal_scale=first.decimal_scale, length=n)
+    d = {}
+    if any(p.device.get("validity") is not None for p in parts):
+        bits = torch.cat([_device_valid_bits(p, torch) for p in parts])
+        nb = (n + 63) // 64 * 64
+        padded = torch.zeros(max(nb, 64), dtype=torch.uint8, device=dev)
+        padded[:n] = bits.to(torch.uint8)
+        w = (1 << torch.arange(8, device=dev, dtype=torch.int32))
+        d["validity"] = (padded.reshape(-1, 8).to(torch.int32) * w).sum(dim=1).to(torch.uint8)
+    if first.spark_type == N.TYPE_STRING:
+        offs, datas, base = [torch.zeros(1, dtype=torch.int64, device=dev)], [], 0
+        for p in parts:
+            o = p.device["offsets"][:p.length + 1].to(torch.int64)
+            o0, o1 = int(o[0].item()), int(o[-1].item())
+            datas.append(p.device["values"][o0:o1])
+            offs.append(o[1:] - o0 + base)
+            base += o1 - o0
+        datas.append(torch.zeros(16, dtype=torch.uint8, device=dev))  # read-past padding of the dword loads
+        d["values"] = torch.cat(datas)
+        d["offsets"] = torch.cat(offs)
+        col.offsets64 = True
+    else:
+        width = np.dtype(NUMPY_OF[first.spark_type]).itemsize
+        d["values"] = torch.cat([p.device["values"].reshape(-1).view(torch.uint8)[:p.length * width] for p in parts])
+    col.device = d
+    return col

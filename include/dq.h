@@ -63,6 +63,10 @@ typedef enum dq_spark_type {
 } dq_spark_type;
 
 #define DQ_COL_DEVICE 0x1u /* values/validity/offsets are device pointers on the ctx's GPU */
+/* STRING: `offsets` points to length + 1 int64 offsets (Arrow large_string) -- a column whose UTF-8 bytes pass
+ * 2^31, e.g. the row chunks of a shard concatenated in HBM for one grouping build. Accepted by dq_frequencies(_ex)
+ * only; every other entry point fails such a column with DQ_ERR_UNSUPPORTED. */
+#define DQ_COL_OFFSETS64 0x2u
 
 typedef struct dq_column {
     int32_t spark_type;        /* dq_spark_type                                               */
