@@ -1640,16 +1640,28 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
     }
     if (!ok) lovf = 1;
     __syncthreads();
-    // publish this workgroup's groups and merge them into region 0 (kRegion slots)
+    // A full table (here or, already, in another workgroup) discards the build: raise `overflow` now and skip the
+    // merge, so an optimistic try over many distinct keys does not probe a full region 0 with every workgroup's
+    // groups (kRegion global CAS probes per key).
+    __shared__ unsigned int lskip;
+    if (threadIdx.x == 0) {
+        if (lovf) atomicAdd(&ctr->overflow, 1ull);
+        lskip = lovf || *(volatile unsigned long long*)&ctr->overflow != 0;
+    }
+    __syncthreads();
+    const bool skip = lskip != 0;
+    // publish this workgroup's groups and merge them into region 0 (kRegion slots; a probe chain past
+    // kMergeProbes counts as a full region)
+    constexpr int kMergeProbes = 512;
     bool mok = true;
     for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
-        const unsigned long long key = i < LS ? lkey[i] : kEmpty;
+        const unsigned long long key = i < LS && !skip ? lkey[i] : kEmpty;
         wg_keys[(uint64_t)blockIdx.x * kRegion + i] = key;
-        wg_reps[(uint64_t)blockIdx.x * kRegion + i] = i < LS ? lrep[i] : ~0ull;
+        wg_reps[(uint64_t)blockIdx.x * kRegion + i] = i < LS && !skip ? lrep[i] : ~0ull;
         if (key == kEmpty) continue;
         unsigned int p = region_probe(key);
         bool done = false;
-        for (int probe = 0; probe < kRegion; ++probe) {
+        for (int probe = 0; probe < kMergeProbes; ++probe) {
             const unsigned long long prev = atomicCAS(&slots[p].key, kEmpty, key);
             if (prev == kEmpty || prev == key) {
                 atomicAdd(&slots[p].count, (unsigned long long)lcnt[i]);
@@ -1661,7 +1673,10 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
         }
         mok &= done;
     }
-    if (!mok) lovf = 1;
+    __shared__ unsigned int lmfail;
+    if (threadIdx.x == 0) lmfail = 0;
+    __syncthreads();
+    if (!mok) lmfail = 1;
     if (count_rows) {  // numRows when no sizing pass counted it (the optimistic small build)
         for (int off = 32; off > 0; off >>= 1) taken += __shfl_down(taken, off, 64);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = taken;
@@ -1680,7 +1695,7 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
         unsigned long long b = 0;
         for (int w = 0; w < kBuildBlock / 64; ++w) b += red[w];
         if (b) atomicAdd(&ctr->mismatch, b);
-        if (lovf) atomicAdd(&ctr->overflow, 1ull);
+        if (lmfail && !lovf) atomicAdd(&ctr->overflow, 1ull);
     }
 }
 

@@ -57,7 +57,7 @@ EXPORTED_SYMBOLS = (
     "dq_abi_version", "dq_open", "dq_close", "dq_last_error", "dq_set_stream", "dq_synchronize", "dq_scan",
     "dq_scan_launch_count", "dq_state_merge", "dq_state_fold", "dq_hll_count", "dq_spark_hash64", "dq_frequencies",
     "dq_freq_summarize", "dq_freq_key_kind", "dq_freq_top", "dq_freq_export", "dq_freq_free", "dq_partition_keys",
-    "dq_quantile_summary", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
+    "dq_quantile_summary", "dq_quantile_summaries", "dq_kll_sketch", "dq_cast_column", "dq_synth_column", "dq_synth_freq_keys",
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts", "dq_synth_strings",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
     "dq_scan_streamed", "dq_scan_kernel_launches", "dq_freq_path_count", "dq_kll_sketch_columns",
@@ -219,6 +219,8 @@ def load_library(path=None):
             "dq_partition_keys": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
             "dq_quantile_summary": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_double, c_int64, c_void_p,
                                               c_void_p, c_void_p]),
+            "dq_quantile_summaries": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p,
+                                              c_void_p, c_void_p, c_void_p]),
             "dq_kll_sketch": (c_int64, [c_void_p, c_void_p, c_int64, ctypes.c_int32, ctypes.c_double, c_void_p,
                                         c_int64]),
             "dq_kll_sketch_columns": (c_int64, [c_void_p, c_void_p, ctypes.c_int32, c_int64, ctypes.c_int32,
@@ -413,6 +415,34 @@ class Context:
         if ns < 0:
             self.check(int(ns), "dq_quantile_summary")
         return vals[:ns].copy(), ranks[:ns].copy(), int(count.value)
+
+    def quantile_summaries(self, requests):
+        """dq_quantile_summaries: requests = [(parts, relative_error)], parts = the DqColumns of one column's
+        consecutive row ranges; returns [(values, ranks, n)] per request, as quantile_summary over the parts
+        concatenated."""
+        if not requests:
+            return []
+        parts, begin, rels, cap = [], [0], [], 2
+        for cols, rel in requests:
+            parts.extend(cols)
+            begin.append(len(parts))
+            rels.append(float(rel))
+            rows = sum(int(c.length) for c in cols)
+            cap = max(cap, rows if rel <= 0.0 else min(rows, int(2.0 / rel) + 8))
+        nreq = len(requests)
+        part_arr = (DqColumn * len(parts))(*parts)
+        begin_arr = np.asarray(begin, dtype=np.int32)
+        rel_arr = np.asarray(rels, dtype=np.float64)
+        vals = np.empty(nreq * cap, dtype=np.float64)
+        ranks = np.empty(nreq * cap, dtype=np.int64)
+        counts = np.zeros(nreq, dtype=np.int64)
+        nsamp = np.zeros(nreq, dtype=np.int64)
+        rc = self.lib.dq_quantile_summaries(self.handle, part_arr, begin_arr.ctypes.data, nreq, rel_arr.ctypes.data,
+                                            cap, vals.ctypes.data, ranks.ctypes.data, counts.ctypes.data,
+                                            nsamp.ctypes.data)
+        self.check(rc, "dq_quantile_summaries")
+        return [(vals[r * cap:r * cap + nsamp[r]].copy(), ranks[r * cap:r * cap + nsamp[r]].copy(), int(counts[r]))
+                for r in range(nreq)]
 
     def kll_sketch(self, column, nrows, sketch_size, shrinking_factor):
         """dq_kll_sketch: the KLLState bytes of one partition holding the column's rows in order."""

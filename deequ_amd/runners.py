@@ -8,7 +8,8 @@ import os
 from . import native as N
 from . import engine
 from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer,
-                        FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies, STATE_ONLY)
+                        FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies, STATE_ONLY,
+                        ApproxQuantile, ApproxQuantiles)
 from .analyzers import merge as merge_states
 from .expr import compile_predicate
 from .metrics import DoubleMetric, Success, UnsupportedOnDevice
@@ -127,13 +128,13 @@ class ScanBatch:
                 res.extend(got)
         if self.quantile_reqs:
             from .quantiles import PercentileDigest, DEFAULT_HEAD_SIZE
-            res.quantiles = []
+            # below the head-buffer size Spark's digest is a function of the sorted values: get all of them (rank
+            # spacing 1) and rebuild Spark's own summary; above it, a bounded summary. Every request in one call.
             small = self.data.nrows < DEFAULT_HEAD_SIZE
-            for column, rel in self.quantile_reqs:
-                # below the head-buffer size Spark's digest is a function of the sorted values: get all
-                # of them (rank spacing 1) and rebuild Spark's own summary; above it, a bounded summary
-                vals, ranks, n = engine.ctx().quantile_summary(self.data[column].native(), self.data.nrows,
-                                                               0.0 if small else rel)
+            got = engine.ctx().quantile_summaries(
+                [(self.data[column].native_parts(), 0.0 if small else rel) for column, rel in self.quantile_reqs])
+            res.quantiles = []
+            for (column, rel), (vals, ranks, n) in zip(self.quantile_reqs, got):
                 if small:
                     res.quantiles.append(PercentileDigest.spark_single_partition(rel, vals))
                 else:
@@ -337,6 +338,16 @@ class AnalysisRunner:
             cols = sorted({c for a in grouping for c in a.groupingColumns() if c in data})
             whole = AnalysisRunner.doAnalysisRun(data.concat(cols), grouping, aggregateWith, saveStatesWith)
             analyzers = [a for a in analyzers if not isinstance(a, GroupingAnalyzer)]
+            if not analyzers:
+                return whole
+        # ApproxQuantile(s): one summary per column over every chunk (dq_quantile_summaries reads the chunks as
+        # parts), the exact order statistics of the shard -- a GK summary inside the same rank bound as the merge of
+        # per-partition digests (QuantileSummaries.merge)
+        quant = [a for a in analyzers if isinstance(a, (ApproxQuantile, ApproxQuantiles))]
+        if quant and len(data.chunks) > 1:
+            cols = sorted({a.column for a in quant if a.column in data})
+            whole = whole + AnalysisRunner.doAnalysisRun(data.parted(cols), quant, aggregateWith, saveStatesWith)
+            analyzers = [a for a in analyzers if not isinstance(a, (ApproxQuantile, ApproxQuantiles))]
             if not analyzers:
                 return whole
         providers, failures = [], {}

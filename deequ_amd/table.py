@@ -199,6 +199,28 @@ class Column:
             c.offsets = self.offsets.ctypes.data if self.offsets is not None else None
         return c
 
+    def native_parts(self):
+        """The column as consecutive row ranges for the ABIs that take parts (dq_quantile_summaries)."""
+        return [self.native()]
+
+
+class PartedColumn(Column):
+    """A column of a ChunkedTable seen as its chunks' columns in row order, read where they lie (no concatenation):
+    only the ABIs that take parts accept it (dq_quantile_summaries)."""
+
+    def __init__(self, parts):
+        first = parts[0]
+        super().__init__(first.name, first.spark_type, None, None, decimal_precision=first.decimal_precision,
+                         decimal_scale=first.decimal_scale, length=sum(p.length for p in parts))
+        self.parts = list(parts)
+        self.tz = first.tz
+
+    def native(self):
+        raise TypeError("column %s is held as %d chunks: only a per-part ABI reads it" % (self.name, len(self.parts)))
+
+    def native_parts(self):
+        return [p.native() for p in self.parts]
+
 
 def _column_from_pylist(name, spark_type, items):
     t = spark_type_of(spark_type)
@@ -498,6 +520,11 @@ class ChunkedTable:
             # the copies run on torch's stream, the builds that read them on the context's own stream
             torch.cuda.current_stream().synchronize()
         return Table(cols)
+
+    def parted(self, names):
+        """The named columns as PartedColumns over the chunks (no copy): the ApproxQuantile summaries of the shard
+        read every chunk in one dq_quantile_summaries call."""
+        return Table([PartedColumn([c[n] for c in self.chunks]) for n in names])
 
 
 def _infer_py_type(items):

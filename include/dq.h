@@ -394,6 +394,18 @@ int dq_freq_row_counts(dq_ctx* ctx, const dq_freq_table* table, int64_t* counts,
 int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows, double relative_error,
                             int64_t max_samples, double* values_out, int64_t* ranks_out, int64_t* count_out);
 
+/* Several ApproxQuantile summaries at once — the ApproxQuantile(s) analyzers of one analysis run over one shard,
+ * each column given as one or more consecutive row ranges ("parts": the chunks of a ChunkedTable, read where they
+ * lie, no concatenation). Request r summarises parts[part_begin[r] .. part_begin[r+1]) (same type; each part's own
+ * `length` rows) at relative_error[r]: values_out / ranks_out + r * max_samples receive exactly the samples
+ * dq_quantile_summary returns for those parts concatenated, counts_out[r] = n, samples_out[r] = their number.
+ * One host round trip for all requests (A/ApproxQuantile.scala:28-103 via the runner's batched aggregation,
+ * R/AnalysisRunner.scala:289-336). A multi-device context takes one part per request. Returns 0 or a negative
+ * dq_status. */
+int dq_quantile_summaries(dq_ctx* ctx, const dq_column* parts, const int32_t* part_begin, int nreq,
+                          const double* relative_error, int64_t max_samples, double* values_out, int64_t* ranks_out,
+                          int64_t* counts_out, int64_t* samples_out);
+
 /* KLLSketch (A/KLLSketch.scala:82-176) as KLLRunner.computeKLLSketchesInExtraPass builds it
  * (R/KLLRunner.scala:91-179): replaces the per-row QuantileNonSample.update loop of sketchPartitions for ONE
  * partition whose non-NULL values (cast to double) arrive in row order. Writes the KLLState bytes

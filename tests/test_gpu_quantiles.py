@@ -149,3 +149,98 @@ def test_approx_quantile_large_within_rank_bound():
             target = max(1, math.ceil(q * n))
             slack = math.ceil(rel * n) + 1
             assert lo - slack <= target <= hi + slack, (rel, q, got)
+
+
+def _split(col, cuts):
+    """Column -> consecutive row-range parts at `cuts` (host buffers sliced, validity re-packed per part)."""
+    from deequ_amd.table import unpack_validity
+    valid = unpack_validity(col.validity, col.length)
+    out, lo = [], 0
+    for hi in list(cuts) + [col.length]:
+        v = valid[lo:hi]
+        out.append(Column(col.name, col.spark_type, np.ascontiguousarray(col.values[lo:hi]),
+                          None if v.all() else pack_validity(v), decimal_precision=col.decimal_precision,
+                          decimal_scale=col.decimal_scale, length=hi - lo))
+        lo = hi
+    return out
+
+
+def _batched_table():
+    rng = np.random.default_rng(21)
+    n = 250_003
+    x = rng.normal(size=n)
+    k = rng.integers(0, n, 3000)
+    x[k[:700]] = np.nan
+    x[k[700:1400]] = -0.0
+    x[k[1400:2100]] = 0.0
+    x[k[2100:2500]] = np.inf
+    x[k[2500:]] = -np.inf
+    cols = {"f64": x, "i64": rng.integers(-(2 ** 62), 2 ** 62, n, dtype=np.int64),
+            "f32": rng.lognormal(0, 3, n).astype(np.float32), "i8": rng.integers(-128, 128, n).astype(np.int8),
+            "dup": np.where(rng.random(n) < 0.6, 1.5, rng.random(n))}
+    valid = {c: rng.random(n) > 0.05 for c in cols}
+    valid["i8"] = np.ones(n, dtype=bool)
+    t = Table.from_arrays(cols, validity=valid)
+    dec = Column("dec", "DecimalType", rng.integers(-10 ** 12, 10 ** 12, n, dtype=np.int64), decimal_precision=15,
+                 decimal_scale=4)
+    return Table(list(t.columns.values()) + [dec])
+
+
+@pytest.mark.parametrize("device", [False, True])
+def test_summaries_batched_parts_exact(device):
+    """dq_quantile_summaries over several columns, each in parts (an empty part included), in one call: every
+    request's samples equal the oracle's order statistics of the parts concatenated, bit for bit."""
+    t = _batched_table()
+    n = t.nrows
+    cuts = [77_777, 77_777, 190_001]
+    reqs, expect, keep = [], [], []
+    for i, (name, rel) in enumerate([("f64", 0.01), ("i64", 0.001), ("f32", 0.25), ("i8", 0.01), ("dup", 0.01),
+                                     ("dec", 0.002), ("f64", 0.05)]):
+        parts = _split(t[name], cuts if i % 2 == 0 else cuts[2:])
+        if device:
+            for p in parts:
+                Table([p]).to_device(0)
+        keep.append(parts)  # the part buffers stay alive through the call
+        reqs.append(([p.native() for p in parts], rel))
+        expect.append((name, rel))
+    got = engine.ctx().quantile_summaries(reqs)
+    for (name, rel), (vals, ranks, cnt) in zip(expect, got):
+        s = O.java_sorted_doubles(t, name)
+        assert cnt == len(s)
+        exp_r = O.summary_ranks(cnt, rel)
+        assert np.array_equal(ranks, exp_r), name
+        assert np.array_equal(vals.view(np.uint64), s[exp_r - 1].view(np.uint64)), (name, rel)
+    assert n == 250_003
+
+
+def test_summaries_batched_sort_path_and_empty():
+    """relative_error 0 (every rank: the sort path) beside a selected request and an all-NULL one."""
+    rng = np.random.default_rng(8)
+    x = rng.normal(size=9000)
+    y = rng.integers(0, 50, 9000).astype(np.float64)
+    t = Table.from_arrays({"x": x, "y": y, "z": x}, validity={"z": np.zeros(9000, dtype=bool)})
+    px, py, pz = _split(t["x"], [3000]), _split(t["y"], [1, 8999]), _split(t["z"], [4500])
+    got = engine.ctx().quantile_summaries([([p.native() for p in px], 0.0), ([p.native() for p in py], 0.01),
+                                           ([p.native() for p in pz], 0.01)])
+    for name, rel, (vals, ranks, cnt) in [("x", 0.0, got[0]), ("y", 0.01, got[1])]:
+        s = O.java_sorted_doubles(t, name)
+        exp_r = O.summary_ranks(cnt, rel)
+        assert cnt == 9000 and np.array_equal(ranks, exp_r)
+        assert np.array_equal(vals.view(np.uint64), s[exp_r - 1].view(np.uint64)), name
+    assert got[2][2] == 0 and len(got[2][0]) == 0
+
+
+def test_approx_quantile_chunked_equals_whole():
+    """ApproxQuantile(s) over a ChunkedTable read the chunks as parts: the same digest, so the same answers, as one
+    run over the whole table (above the 50000-row head size)."""
+    from deequ_amd.table import ChunkedTable
+    t = _batched_table()
+    cuts = [60_000, 150_000]
+    pf, pi, pd = (_split(t[c], cuts) for c in ("f64", "i64", "dec"))
+    ct = ChunkedTable([Table([pf[i], pi[i], pd[i]]) for i in range(3)])
+    an = [D.ApproxQuantile("f64", 0.5), D.ApproxQuantile("i64", 0.9, 0.001), D.ApproxQuantiles("dec", [0.1, 0.5]),
+          D.Size()]
+    whole = D.AnalysisRunner.onData(t).addAnalyzers(an).run()
+    parted = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in an:
+        assert parted.metric(a).value.get() == whole.metric(a).value.get(), a
