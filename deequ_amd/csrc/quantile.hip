@@ -162,26 +162,25 @@ __host__ __device__ inline int q_tree_sorted_index(int i) {
     return ((2 * p + 1) << (11 - d)) - 1;
 }
 
-// bucket = number of splitters <= key (0..4095) and the largest splitter <= key (the predecessor: the last node the
-// descent went right at), kQRowsPerLane descents interleaved.
+// bucket = number of splitters <= key (0..4095), kQRowsPerLane descents interleaved; then the largest splitter <= key
+// (sorted splitter b - 1, bucket b's lower bound) read from its tree node: tracking it through the descent kept one
+// compare mask per level and row live and spilled them.
 __device__ __forceinline__ void q_tree_search(const uint64_t* tree, const uint64_t (&k)[kQRowsPerLane],
                                               uint32_t (&b)[kQRowsPerLane], uint64_t (&lo)[kQRowsPerLane]) {
 #pragma unroll
-    for (int j = 0; j < kQRowsPerLane; ++j) {
-        b[j] = 0;
-        lo[j] = 0;
-    }
+    for (int j = 0; j < kQRowsPerLane; ++j) b[j] = 0;
 #pragma unroll
     for (int level = 0; level < 12; ++level)
 #pragma unroll
-        for (int j = 0; j < kQRowsPerLane; ++j) {
-            const uint64_t node = tree[b[j]];
-            const bool ge = node <= k[j];
-            lo[j] = ge ? node : lo[j];
-            b[j] = 2 * b[j] + 1 + (ge ? 1u : 0u);
-        }
+        for (int j = 0; j < kQRowsPerLane; ++j) b[j] = 2 * b[j] + 1 + (tree[b[j]] <= k[j] ? 1u : 0u);
 #pragma unroll
-    for (int j = 0; j < kQRowsPerLane; ++j) b[j] -= kQBuckets - 1;
+    for (int j = 0; j < kQRowsPerLane; ++j) {
+        b[j] -= kQBuckets - 1;
+        // sorted index s = b - 1 sits at level d = 11 - ctz(s + 1), position (s + 1) >> (12 - d) in the level
+        const uint32_t s1 = b[j] ? b[j] : 1u;  // b = 0 has no lower splitter (lo unused)
+        const uint32_t tz = (uint32_t)__builtin_ctz(s1);
+        lo[j] = tree[((1u << (11 - tz)) - 1) + (s1 >> (tz + 1))];
+    }
 }
 
 // Pass 2 body: bucket counts and counts of keys equal to the bucket's lower splitter, over the rows

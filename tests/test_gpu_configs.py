@@ -247,7 +247,10 @@ def test_compound_compliance_parity_at_scale():
     mean_w = D.Mean("c3", w)
     before = engine.ctx().kernel_launches()
     st = _states(table, [comp, compw, mean_w, D.Size(w)])
-    print("\nlaunches:", _launch_delta(before))
+    launches = _launch_delta(before)
+    # one fused pass: the compound Compliance predicates run as simple predicates (`pred_simple`), the compound
+    # `where` as consumer masks (`where_masks`), Mean(c3) on the striped kernel and Size(where) on the bitmap kernel
+    assert launches == {"striped": 1, "bits": 1, "pred_simple": 1, "where_masks": 1}, launches
     del table
     pred = ("or", [(4, "<", 0), (5, ">", 1)])
     cols, _, cnt = O.generated_suite(specs, 0, WHERE_ROWS, preds=[pred])
