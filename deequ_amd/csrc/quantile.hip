@@ -41,6 +41,7 @@ namespace dq {
 constexpr int kQBuckets = 4096;          // buckets; kQBuckets - 1 splitters + a +inf sentinel
 constexpr int kQSample = 65536;          // stratified sample size
 constexpr int kQBlock = 256;
+constexpr int kQHistBlock = 1024;      // the batched histogram pass: 32 waves per CU at its 64 KB of LDS
 constexpr int kQRowsPerLane = 8;         // independent loads / tree descents in flight per lane
 constexpr uint32_t kQNoTarget = 0xFFFFFFFFu;
 
@@ -185,10 +186,13 @@ __device__ __forceinline__ void q_tree_search(const uint64_t* tree, const uint64
 
 // Pass 2 body: bucket counts and counts of keys equal to the bucket's lower splitter, over the rows
 // this block takes of a column (block `blk` of `nblk` striding the rows); `splitters` in tree order.
+// With `bid`, each row's bucket is also recorded (kQBidNull for NULL, kQBidEq | b for a copy of bucket b's lower
+// splitter, else b), so the compaction streams these 2-byte ids instead of searching the tree again.
+constexpr uint16_t kQBidNull = 0xFFFF, kQBidEq = 0x8000;
 template <int ET>
 __device__ __forceinline__ void q_hist_rows(const QColumn& c, int64_t nrows, const uint64_t* __restrict__ splitters,
                                             unsigned long long* __restrict__ hist, unsigned long long* __restrict__ eq,
-                                            int64_t blk, int64_t nblk) {
+                                            int64_t blk, int64_t nblk, uint16_t* __restrict__ bid = nullptr) {
     __shared__ uint64_t spl[kQBuckets];
     __shared__ uint32_t h[kQBuckets];
     __shared__ uint32_t e[kQBuckets];
@@ -208,9 +212,14 @@ __device__ __forceinline__ void q_hist_rows(const QColumn& c, int64_t nrows, con
         q_tree_search(spl, k, b, lo);
 #pragma unroll
         for (int j = 0; j < kQRowsPerLane; ++j) {
+            const bool is_eq = v[j] && b[j] > 0 && lo[j] == k[j];
+            if (bid) {
+                const int64_t r = base + (int64_t)j * blockDim.x;
+                if (r < nrows) bid[r] = !v[j] ? kQBidNull : (uint16_t)(b[j] | (is_eq ? kQBidEq : 0));
+            }
             if (!v[j]) continue;
             atomicAdd(&h[b[j]], 1u);
-            if (b[j] > 0 && lo[j] == k[j]) atomicAdd(&e[b[j]], 1u);
+            if (is_eq) atomicAdd(&e[b[j]], 1u);
         }
     }
     __syncthreads();
@@ -274,6 +283,7 @@ struct QPart {
     QColumn qc;
     int64_t nrows;
     int64_t row0;
+    int64_t bid_off;  // first of its rows' bucket ids in the id buffer
     int32_t req;
     int32_t pad;
 };
@@ -325,12 +335,13 @@ q_splitters_kernel(const uint64_t* __restrict__ sorted, const unsigned int* __re
 
 // Histogram of every part (blockIdx.y) into its request's hist / eq (2 * kQBuckets counters per request).
 template <int ET>
-__global__ void __launch_bounds__(kQBlock)
+__global__ void __launch_bounds__(kQHistBlock)
 q_hist_multi_kernel(const QPart* __restrict__ parts, const uint64_t* __restrict__ spl,
-                    unsigned long long* __restrict__ hist) {
+                    unsigned long long* __restrict__ hist, uint16_t* __restrict__ bid) {
     const QPart p = parts[blockIdx.y];
     unsigned long long* h = hist + (size_t)p.req * 2 * kQBuckets;
-    q_hist_rows<ET>(p.qc, p.nrows, spl + (size_t)p.req * kQBuckets, h, h + kQBuckets, blockIdx.x, gridDim.x);
+    q_hist_rows<ET>(p.qc, p.nrows, spl + (size_t)p.req * kQBuckets, h, h + kQBuckets, blockIdx.x, gridDim.x,
+                    bid ? bid + p.bid_off : nullptr);
 }
 
 // Compaction of every part into its request's bucket segments (cursors are absolute candidate offsets).
@@ -342,6 +353,40 @@ q_compact_multi_kernel(const QPart* __restrict__ parts, const uint64_t* __restri
     const QPart p = parts[blockIdx.y];
     q_compact_rows<ET>(p.qc, p.nrows, spl + (size_t)p.req * kQBuckets, target + (size_t)p.req * kQBuckets,
                    cursor + (size_t)p.req * kQBuckets, cand, blockIdx.x, gridDim.x);
+}
+
+// Compaction from the recorded bucket ids: a row is read again only when its bucket is a target (a few % of rows).
+template <int ET>
+__global__ void __launch_bounds__(kQBlock)
+q_compact_bid_kernel(const QPart* __restrict__ parts, const uint16_t* __restrict__ bid,
+                     const uint32_t* __restrict__ target, unsigned long long* __restrict__ cursor,
+                     uint64_t* __restrict__ cand) {
+    __shared__ uint8_t tg[kQBuckets];
+    const QPart p = parts[blockIdx.y];
+    const uint32_t* tgt = target + (size_t)p.req * kQBuckets;
+    unsigned long long* cur = cursor + (size_t)p.req * kQBuckets;
+    for (int i = threadIdx.x; i < kQBuckets; i += blockDim.x) tg[i] = tgt[i] != kQNoTarget ? 1 : 0;
+    __syncthreads();
+    const uint16_t* ids = bid + p.bid_off;
+    const int64_t nrows = p.nrows;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * kQRowsPerLane;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x * kQRowsPerLane + threadIdx.x; base < nrows; base += stride) {
+        uint16_t id[kQRowsPerLane];
+#pragma unroll
+        for (int j = 0; j < kQRowsPerLane; ++j) {
+            const int64_t r = base + (int64_t)j * blockDim.x;
+            id[j] = r < nrows ? q_gload<uint16_t>(ids, r) : kQBidNull;
+        }
+#pragma unroll
+        for (int j = 0; j < kQRowsPerLane; ++j) {
+            if (id[j] & kQBidEq) continue;  // NULL (0xFFFF) or a copy of the lower splitter
+            if (!tg[id[j]]) continue;
+            const int64_t r = base + (int64_t)j * blockDim.x;
+            const uint64_t key = order_key(q_raw_value<ET>(p.qc, q_load_raw<ET>(p.qc.values, r)));
+            const unsigned long long pos = atomicAdd(&cur[id[j]], 1ull);
+            cand[pos] = key;
+        }
+    }
 }
 
 // One order statistic: the k-th smallest (1-based) of cand[lo, lo + cnt), all known to lie in [lo_key, hi_key];
@@ -834,6 +879,7 @@ int dq_quantile_summaries(dq_ctx* ctx, const dq_column* parts, const int32_t* pa
     // ---- part table (host parts staged into scratch) ------------------------------------------------
     std::vector<QPart> qp(nparts);
     std::vector<int64_t> req_rows(nreq, 0);
+    int64_t total_rows = 0;
     for (int r = 0; r < nreq; ++r) {
         int64_t at = 0;
         for (int p = part_begin[r]; p < part_begin[r + 1]; ++p) {
@@ -845,6 +891,7 @@ int dq_quantile_summaries(dq_ctx* ctx, const dq_column* parts, const int32_t* pa
             q.qc.pow10 = pow(10.0, (double)q.qc.decimal_scale);
             q.nrows = c.length;
             q.row0 = at;
+            q.bid_off = total_rows + at;
             q.req = r;
             at += c.length;
             if (c.flags & DQ_COL_DEVICE) {
@@ -868,6 +915,7 @@ int dq_quantile_summaries(dq_ctx* ctx, const dq_column* parts, const int32_t* pa
         }
         if (at >= (1LL << 46)) return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_quantile_summaries: too many rows");
         req_rows[r] = at;
+        total_rows += at;
     }
     QPart* dparts;
     int32_t* dbegin;
@@ -916,11 +964,11 @@ int dq_quantile_summaries(dq_ctx* ctx, const dq_column* parts, const int32_t* pa
     const int64_t lanes_needed = (max_part + kQRowsPerLane - 1) / kQRowsPerLane;
     // one resident round of workgroups over all parts: 2 per CU in the histogram pass (64 KB of LDS), 3 in the
     // compaction (48 KB)
-    auto part_grid = [&](int per_cu) {
-        return (int)std::max<int64_t>(1, std::min<int64_t>((lanes_needed + kQBlock - 1) / kQBlock,
+    auto part_grid = [&](int per_cu, int block) {
+        return (int)std::max<int64_t>(1, std::min<int64_t>((lanes_needed + block - 1) / block,
                                                            (int64_t)dq::ctx_cus(ctx) * per_cu / nparts));
     };
-    const int gx = part_grid(2), gxc = part_grid(3);
+    const int gx = part_grid(2, kQHistBlock), gxc = part_grid(3, kQBlock), gxb = part_grid(8, kQBlock);
     // the parts grouped by element type: one launch per type present (blockIdx.y = part of that type)
     std::vector<QPart> typed(qp);
     std::stable_sort(typed.begin(), typed.end(), [](const QPart& a, const QPart& b) { return a.qc.elem < b.qc.elem; });
@@ -934,10 +982,12 @@ int dq_quantile_summaries(dq_ctx* ctx, const dq_column* parts, const int32_t* pa
         type_runs.emplace_back(i, j - i);
         i = j;
     }
+    // every row's bucket id (2 B a row) for the compaction; without room for it the compaction searches again
+    uint16_t* dbid = getenv("DQ_Q_NO_BID") ? nullptr : (uint16_t*)scr.get(sizeof(uint16_t) * (size_t)std::max<int64_t>(total_rows, 1));
     for (auto& tr : type_runs) {
         Q_ET_DISPATCH(typed[tr.first].qc.elem,
-                      hipLaunchKernelGGL(q_hist_multi_kernel<E>, dim3(gx, tr.second), dim3(kQBlock), 0, s,
-                                         (const QPart*)(dtyped + tr.first), (const uint64_t*)dtree, dhist));
+                      hipLaunchKernelGGL(q_hist_multi_kernel<E>, dim3(gx, tr.second), dim3(kQHistBlock), 0, s,
+                                         (const QPart*)(dtyped + tr.first), (const uint64_t*)dtree, dhist, dbid));
         QS_HIP(ctx, hipGetLastError());
     }
     std::vector<unsigned long long> hist((size_t)nreq * 2 * kQBuckets);
@@ -1039,10 +1089,16 @@ int dq_quantile_summaries(dq_ctx* ctx, const dq_column* parts, const int32_t* pa
     QS_HIP(ctx, hipMemcpyAsync(dtarget, target.data(), sizeof(uint32_t) * target.size(), hipMemcpyHostToDevice, s));
     QS_HIP(ctx, hipMemcpyAsync(dcursor, cursor.data(), sizeof(unsigned long long) * cursor.size(), hipMemcpyHostToDevice, s));
     for (auto& tr : type_runs) {
-        Q_ET_DISPATCH(typed[tr.first].qc.elem,
-                      hipLaunchKernelGGL(q_compact_multi_kernel<E>, dim3(gxc, tr.second), dim3(kQBlock), 0, s,
-                                         (const QPart*)(dtyped + tr.first), (const uint64_t*)dtree,
-                                         (const uint32_t*)dtarget, dcursor, dcand));
+        if (dbid)
+            Q_ET_DISPATCH(typed[tr.first].qc.elem,
+                          hipLaunchKernelGGL(q_compact_bid_kernel<E>, dim3(gxb, tr.second), dim3(kQBlock), 0, s,
+                                             (const QPart*)(dtyped + tr.first), (const uint16_t*)dbid,
+                                             (const uint32_t*)dtarget, dcursor, dcand))
+        else
+            Q_ET_DISPATCH(typed[tr.first].qc.elem,
+                          hipLaunchKernelGGL(q_compact_multi_kernel<E>, dim3(gxc, tr.second), dim3(kQBlock), 0, s,
+                                             (const QPart*)(dtyped + tr.first), (const uint64_t*)dtree,
+                                             (const uint32_t*)dtarget, dcursor, dcand))
         QS_HIP(ctx, hipGetLastError());
     }
 
