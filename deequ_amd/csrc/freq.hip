@@ -1282,7 +1282,7 @@ __global__ void __launch_bounds__(kBuildBlock)
 build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
              const unsigned long long* __restrict__ rows, const long long* __restrict__ weights,
              Slot* __restrict__ slots, unsigned long long* __restrict__ reps, Counters* __restrict__ ctr,
-             SummaryPartial* __restrict__ parts, double n, NarrowKey nk) {
+             SummaryPartial* __restrict__ parts, double n, NarrowKey nk, KeySpec ks, int verify) {
     const uint32_t* __restrict__ hs32 = reinterpret_cast<const uint32_t*>(hs);
     using C = typename std::conditional<WEIGHTED, unsigned long long, unsigned int>::type;
     __shared__ unsigned long long lkey[kRegion];
@@ -1319,6 +1319,35 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
     }
     if (!ok) lovf = 1;
     __syncthreads();
+    if constexpr (GENERAL) {
+        // The verification of a whole bucket (`verify`: no bucket of the build is split) while its table is in LDS:
+        // every row other than its group's representative (the smallest row) is compared with it byte for byte —
+        // instead of a pass over all rows that re-hashes each key and probes the table in HBM (verify_kernel).
+        if (verify && !it.split && !lovf) {
+            unsigned long long bad = 0;
+            for (unsigned long long j0 = it.begin + threadIdx.x; j0 < it.end; j0 += kStep) {
+#pragma unroll 4
+                for (int u = 0; u < kBuildUnroll; ++u) {
+                    const unsigned long long j = j0 + (unsigned long long)u * kBuildBlock;
+                    if (j >= it.end) break;
+                    const unsigned long long h = hs[j], row = rows[j];
+                    unsigned int p = region_probe(h);
+                    for (int probe = 0; probe < kRegion && lkey[p] != h; ++probe) p = (p + 1) & (kRegion - 1);
+                    const unsigned long long rep = lrep[p];
+                    if (rep != row && !rows_equal(ks, (int64_t)row, (int64_t)rep)) ++bad;
+                }
+            }
+            __shared__ unsigned long long vred[kBuildBlock / 64];
+            for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+            if ((threadIdx.x & 63) == 0) vred[threadIdx.x >> 6] = bad;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned long long b = 0;
+                for (int w = 0; w < kBuildBlock / 64; ++w) b += vred[w];
+                if (b) atomicAdd(&ctr->mismatch, b);
+            }
+        }
+    }
     Slot* region = slots + (uint64_t)it.bucket * kRegion;
     unsigned long long* rrep = GENERAL ? reps + (uint64_t)it.bucket * kRegion : nullptr;
     if (!it.split) {
@@ -1380,6 +1409,47 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
         __syncthreads();
     }
     if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->overflow, 1ull);
+}
+
+// The rows of split buckets (several work items merged into one region with atomics), verified once the table is
+// final: each item's (key, row) pairs from the partition buffers against the region's representative.
+__global__ void __launch_bounds__(kBuildBlock)
+verify_items_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
+                    const unsigned long long* __restrict__ rows, const Slot* __restrict__ slots,
+                    const unsigned long long* __restrict__ reps, KeySpec ks, Counters* __restrict__ ctr) {
+    __shared__ unsigned long long vred[kBuildBlock / 64];
+    const BuildItem it = items[blockIdx.x];
+    const Slot* region = slots + (uint64_t)it.bucket * kRegion;
+    const unsigned long long* rrep = reps + (uint64_t)it.bucket * kRegion;
+    unsigned long long bad = 0;
+    for (unsigned long long j = it.begin + threadIdx.x; j < it.end; j += kBuildBlock) {
+        const unsigned long long h = hs[j], row = rows[j];
+        unsigned int p = region_probe(h);
+        bool found = false;
+        for (int probe = 0; probe < kRegion; ++probe) {
+            const unsigned long long k = region[p].key;
+            if (k == h) {
+                found = true;
+                break;
+            }
+            if (k == kEmpty) break;
+            p = (p + 1) & (kRegion - 1);
+        }
+        if (!found) {
+            ++bad;
+            continue;
+        }
+        const unsigned long long rep = rrep[p];
+        if (rep != row && !rows_equal(ks, (int64_t)row, (int64_t)rep)) ++bad;
+    }
+    for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+    if ((threadIdx.x & 63) == 0) vred[threadIdx.x >> 6] = bad;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = 0;
+        for (int w = 0; w < kBuildBlock / 64; ++w) b += vred[w];
+        if (b) atomicAdd(&ctr->mismatch, b);
+    }
 }
 
 // Spilled keys of the fast build (a bucket's share of a heavily repeated key past its slack) into the finished table:
@@ -2060,28 +2130,44 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     SummaryPartial* bparts = nullptr;
     FQ_HIP(ctx, buf.alloc((void**)&bparts, items.size() * sizeof(SummaryPartial)));
     const double build_n = (double)t->host_ctr.num_rows;  // the count pass's numRows (copied before the build)
+    // general keys: whole buckets are verified inside the build, the rows of split buckets by verify_items_kernel
+    // after it (DQ_FREQ_VERIFY_PASS: the row pass over every row instead)
+    std::vector<BuildItem> split_items;
+    for (const BuildItem& bi : items)
+        if (bi.split) split_items.push_back(bi);
+    const int verify_in_build = general && !getenv("DQ_FREQ_VERIFY_PASS") ? 1 : 0;
+    const KeySpec vks = general ? t->ks : KeySpec{};
     if (general && weighted)
         hipLaunchKernelGGL((build_kernel<true, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{}, vks, verify_in_build);
     else if (general)
         hipLaunchKernelGGL((build_kernel<true, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{}, vks, verify_in_build);
     else if (weighted)
         hipLaunchKernelGGL((build_kernel<false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{}, vks, verify_in_build);
     else if (narrow)
         hipLaunchKernelGGL((build_kernel<false, false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows,
-                           w, t->slots, t->reps, t->ctr, bparts, build_n, *narrow);
+                           w, t->slots, t->reps, t->ctr, bparts, build_n, *narrow, vks, 0);
     else
         hipLaunchKernelGGL((build_kernel<false, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{}, vks, verify_in_build);
     FQ_HIP(ctx, hipGetLastError());
     if (nspill) {
         const int grid = (int)std::min<unsigned long long>((nspill + kSpillChunk - 1) / kSpillChunk, 2048);
         hipLaunchKernelGGL(spill_insert_kernel, dim3(grid), dim3(kBuildBlock), 0, s, spill, nspill, t->slots, bits, t->ctr);
         FQ_HIP(ctx, hipGetLastError());
     }
-    if (general && nrows > 0) {
+    if (verify_in_build && !split_items.empty()) {
+        BuildItem* dsplit = nullptr;
+        FQ_HIP(ctx, buf.alloc((void**)&dsplit, split_items.size() * sizeof(BuildItem)));
+        FQ_HIP(ctx, hipMemcpyAsync(dsplit, split_items.data(), split_items.size() * sizeof(BuildItem),
+                                   hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(verify_items_kernel, dim3((unsigned int)split_items.size()), dim3(kBuildBlock), 0, s, dsplit,
+                           sorted, srows, t->slots, t->reps, t->ks, t->ctr);
+        FQ_HIP(ctx, hipGetLastError());
+    }
+    if (general && nrows > 0 && !verify_in_build) {
         const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
         hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots, t->reps, bits,
                            t->ctr);

@@ -617,7 +617,8 @@ def _device_valid_bits(col, torch):
 
 def _concat_device(parts):
     """Device columns of consecutive chunks as one device column: values / UTF-8 bytes copied in HBM, validity bits
-    re-packed at the chunk boundaries, string offsets rebased into int64."""
+    re-packed at the chunk boundaries (byte-wise when every chunk but the last holds a multiple of 8 rows), string
+    offsets rebased into int64 in place in the output."""
     import torch
     first = parts[0]
     dev = first.device["values"].device
@@ -626,23 +627,48 @@ def _concat_device(parts):
                  decimal_scale=first.decimal_scale, length=n)
     d = {}
     if any(p.device.get("validity") is not None for p in parts):
-        bits = torch.cat([_device_valid_bits(p, torch) for p in parts])
-        nb = (n + 63) // 64 * 64
-        padded = torch.zeros(max(nb, 64), dtype=torch.uint8, device=dev)
-        padded[:n] = bits.to(torch.uint8)
-        w = (1 << torch.arange(8, device=dev, dtype=torch.int32))
-        d["validity"] = (padded.reshape(-1, 8).to(torch.int32) * w).sum(dim=1).to(torch.uint8)
+        nwords = max((n + 63) // 64, 1)
+        if all(p.length % 8 == 0 for p in parts[:-1]):
+            out = torch.zeros(nwords * 8, dtype=torch.uint8, device=dev)
+            at = 0
+            for p in parts:
+                nb = (p.length + 7) // 8
+                v = p.device.get("validity")
+                if v is None:
+                    out[at:at + nb] = 0xFF
+                    if p.length % 8:
+                        out[at + nb - 1] = (1 << (p.length % 8)) - 1
+                else:
+                    out[at:at + nb].copy_(v[:nb])
+                    if p.length % 8:  # bits past the chunk's last row read as NULL
+                        out[at + nb - 1] &= (1 << (p.length % 8)) - 1
+                at += nb
+            d["validity"] = out
+        else:
+            bits = torch.cat([_device_valid_bits(p, torch) for p in parts])
+            padded = torch.zeros(nwords * 64, dtype=torch.uint8, device=dev)
+            padded[:n] = bits.to(torch.uint8)
+            w = (1 << torch.arange(8, device=dev, dtype=torch.int32))
+            d["validity"] = (padded.reshape(-1, 8).to(torch.int32) * w).sum(dim=1).to(torch.uint8)
     if first.spark_type == N.TYPE_STRING:
-        offs, datas, base = [torch.zeros(1, dtype=torch.int64, device=dev)], [], 0
+        spans = []
         for p in parts:
-            o = p.device["offsets"][:p.length + 1].to(torch.int64)
-            o0, o1 = int(o[0].item()), int(o[-1].item())
-            datas.append(p.device["values"][o0:o1])
-            offs.append(o[1:] - o0 + base)
+            o = p.device["offsets"]
+            spans.append((int(o[0].item()), int(o[p.length].item())))
+        total = sum(b - a for a, b in spans)
+        data = torch.empty(total + 16, dtype=torch.uint8, device=dev)  # + read-past padding of the dword loads
+        data[total:] = 0
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        offs[0] = 0
+        at, base = 0, 0
+        for p, (o0, o1) in zip(parts, spans):
+            data[base:base + o1 - o0].copy_(p.device["values"][o0:o1])
+            seg = offs[at + 1:at + 1 + p.length]
+            seg.copy_(p.device["offsets"][1:p.length + 1])
+            seg.add_(base - o0)
+            at += p.length
             base += o1 - o0
-        datas.append(torch.zeros(16, dtype=torch.uint8, device=dev))  # read-past padding of the dword loads
-        d["values"] = torch.cat(datas)
-        d["offsets"] = torch.cat(offs)
+        d["values"], d["offsets"] = data, offs
         col.offsets64 = True
     else:
         width = np.dtype(NUMPY_OF[first.spark_type]).itemsize

@@ -108,3 +108,39 @@ def test_split_merged_state_persists_and_loads_back(monkeypatch, tmp_path):
     assert _close(a.computeMetricFrom(back).value.get(), want)
     full_state = a.computeStateFrom(full)
     assert _close(a.computeMetricFrom(full_state).value.get(), want)
+
+
+@pytest.mark.parametrize("lengths", [(4096, 8, 1000), (1001, 77, 3), (64, 0, 129)])
+def test_device_concat_equals_host_concat(lengths):
+    """ChunkedTable.concat in HBM (byte-wise validity when chunk lengths are multiples of 8, else bit repacking; int64
+    string offsets rebased in place) equals the host concatenation bit for bit, chunks with and without NULLs."""
+    import torch
+    from deequ_amd.table import ChunkedTable, unpack_validity
+    rng = np.random.default_rng(sum(lengths))
+    chunks = []
+    for i, n in enumerate(lengths):
+        words = ["w%d" % rng.integers(0, 50) * int(rng.integers(0, 3)) for _ in range(n)]
+        s = [None if (i != 1 and rng.random() < 0.2) else w for w in words]
+        x = [None if (i == 0 and rng.random() < 0.3) else float(v) for v in rng.normal(size=n)]
+        chunks.append(Table.from_pydict({"s": s, "x": x}, types={"s": "string", "x": "double"}))
+    host = ChunkedTable(chunks).concat(["s", "x"])
+    for c in chunks:
+        c.to_device(0)
+    dev = ChunkedTable(chunks).concat(["s", "x"])
+    n = sum(lengths)
+    for name in ("s", "x"):
+        hc, dc = host[name], dev[name]
+        hv = unpack_validity(hc.validity, n)
+        dvb = dc.device.get("validity")
+        dv = np.ones(n, dtype=bool) if dvb is None else unpack_validity(dvb.cpu().numpy(), n)
+        assert np.array_equal(hv, dv), name
+        if dvb is not None:
+            assert len(dvb) % 8 == 0
+        if name == "s":
+            assert np.array_equal(dc.device["offsets"].cpu().numpy(), np.asarray(hc.offsets, dtype=np.int64))
+            data = dc.device["values"].cpu().numpy()
+            assert bytes(data[:len(hc.values)]) == bytes(hc.values) and not data[len(hc.values):].any()
+        else:
+            got = dc.device["values"].cpu().numpy().view(np.float64)
+            assert np.array_equal(got[hv], np.asarray(hc.values)[hv])
+    torch.cuda.synchronize()
