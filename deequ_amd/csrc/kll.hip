@@ -1575,11 +1575,12 @@ static int kll_sketch_batch(dq_ctx* ctx, const dq_column* columns, int ncols, in
     // several columns: one launch per (level, class) over all of them (below) unless DQ_KLL_PER_COLUMN asks for one
     // launch chain per column (spread over the streams)
     const bool batched = ncols >= 1 && ncols <= 255 && !getenv("DQ_KLL_PER_COLUMN");
-    // batched: level 0 of a NULL-compacted column can be read in place by its compactions (DQ_KLL_INPLACE=1: no dense
-    // stream, 8 B written and re-read per value less). Measured slower end to end on the C5 shard (profiles/r04/
-    // c5_kll_ab_r04k.txt: the staging adds ~15 % to every level-0 compaction, and those run after the host schedule,
-    // while the dense write overlaps it), so the dense stream stays the default.
-    const bool inplace = batched && getenv("DQ_KLL_INPLACE") != nullptr;
+    // batched: level 0 of a NULL-compacted column is read in place by its compactions (no dense stream: 8 B written and
+    // re-read per value less; DQ_KLL_DENSE=1 writes the dense stream first). r04 measured in place slower end to end
+    // (profiles/r04/c5_kll_ab_r04k.txt: the compactions waited for the host schedule that the dense write overlapped);
+    // since the schedule automaton runs on plain arrays the two are equal in time on the C5 shard (r05: 125.1 vs
+    // 126.9 ms a profile, profiles/r05/c5_kll_inplace_ab_r05ah.txt) and in place moves ~50 GB less, so it is the default.
+    const bool inplace = batched && getenv("DQ_KLL_DENSE") == nullptr;
     if (ncols > 1 && !batched && !getenv("DQ_KLL_SERIAL")) {
         const int nside = dq::ctx_side_streams(ctx, cstreams + 1, &fork_ev, join_ev);
         if (nside > 0) {

@@ -213,10 +213,10 @@ def test_kll_sketch_columns_equals_per_column_sketches(device):
 
 @pytest.mark.parametrize("null_share", [0.0, 0.05, 0.99])
 def test_level0_in_place_equals_the_dense_stream(null_share, monkeypatch):
-    """Level-0 compactions reading the raw column in place (DQ_KLL_INPLACE=1: the range's row span located from the
-    NULL-compaction tile offsets, its non-NULL values staged in dense order) instead of the written-out dense stream (the
-    default): the KLLState bytes are equal for an int64 column, a float column and a double column with NULLs, including
-    a 99 %-NULL column whose compactions span many staging chunks; the small case also equals the oracle."""
+    """Level-0 compactions reading the raw column in place (the default: the range's row span located from the
+    NULL-compaction tile offsets, its non-NULL values staged in dense order) instead of the written-out dense stream
+    (DQ_KLL_DENSE=1): the KLLState bytes are equal for an int64 column, a float column and a double column with NULLs,
+    including a 99 %-NULL column whose compactions span many staging chunks; the small case also equals the oracle."""
     rng = np.random.default_rng(int(null_share * 100) + 7)
     n = 3_000_000
     cols = {"l": rng.integers(-10 ** 9, 10 ** 9, n), "f": rng.normal(size=n).astype(np.float32),
@@ -225,9 +225,10 @@ def test_level0_in_place_equals_the_dense_stream(null_share, monkeypatch):
     t = Table.from_arrays(cols, validity=valid)
     t.to_device(0)
     names = list(cols)
-    dense = engine.ctx().kll_sketch_columns([t[c].native() for c in names], t.nrows, 2048, 0.64)
-    monkeypatch.setenv("DQ_KLL_INPLACE", "1")
     inplace = engine.ctx().kll_sketch_columns([t[c].native() for c in names], t.nrows, 2048, 0.64)
+    monkeypatch.setenv("DQ_KLL_DENSE", "1")
+    dense = engine.ctx().kll_sketch_columns([t[c].native() for c in names], t.nrows, 2048, 0.64)
+    monkeypatch.delenv("DQ_KLL_DENSE")
     assert inplace == dense
     small = Table.from_arrays({c: v[:200_000] for c, v in cols.items()}, validity={c: v[:200_000] for c, v in valid.items()})
     for c in names:

@@ -1,0 +1,25 @@
+"""K full C5 steps (the 3-pass ColumnProfiler + the extra analyzers) on the 2.5e8-row shard, for PMC passes:
+python tools/c5_steps.py [rows] [K] — one progress line per step (the generators run first and are excluded by
+tools/pmc_traffic.py --all-engine)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+import bench
+import deequ_amd as D
+import deequ_amd.native as N
+from deequ_amd import engine
+
+rows = int(float(sys.argv[1])) if len(sys.argv) > 1 else 250_000_000
+k = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+t, _ = bench.c5_shard(torch, N, engine.ctx(), torch.device("cuda", 0), rows)
+extras = bench.c5_extra_analyzers(D)
+print("table ready", flush=True)
+for i in range(k):
+    t0 = time.perf_counter()
+    bench.c5_step(D, t, extras)
+    torch.cuda.synchronize()
+    print("step %d %.1f ms" % (i, (time.perf_counter() - t0) * 1e3), flush=True)
