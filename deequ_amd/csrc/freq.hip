@@ -383,7 +383,7 @@ __device__ __forceinline__ void chunk_of(int64_t nrows, int64_t& r0, int64_t& r1
 __global__ void __launch_bounds__(kFreqBlock)
 extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__ block_keep,
                      uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, unsigned int* __restrict__ hist1,
-                     int tile_rows) {
+                     int tile_rows, unsigned long long* __restrict__ hrow) {
     __shared__ unsigned int lds[kSizingRegs];
     __shared__ unsigned int dh[kDigitBins];
     __shared__ unsigned long long red[kFreqBlock / 64];
@@ -407,6 +407,12 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
             hv[u] = 0;
             ok[u] = r < r1 && row_key(ks, r, hv[u], ngv[u]);
         }
+        if (hrow)  // each row's key for the partition pass (kEmpty: the row takes no part in the table)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = rb + (int64_t)u * kFreqBlock;
+                if (r < r1) hrow[r] = ok[u] && !ngv[u] ? hv[u] : kEmpty;
+            }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if (!ok[u]) continue;
@@ -614,7 +620,7 @@ template <bool GENERAL, int TILE>
 __global__ void __launch_bounds__(kFreqBlock)
 partition1_kernel(KeySpec ks, int64_t nrows, const unsigned long long* __restrict__ off1,
                   const unsigned long long* __restrict__ totals, unsigned long long* __restrict__ out_h,
-                  unsigned long long* __restrict__ out_r) {
+                  unsigned long long* __restrict__ out_r, const unsigned long long* __restrict__ hrow) {
     constexpr int PER = TILE / kFreqBlock;
     __shared__ unsigned int hist[kDigitBins], start[kDigitBins];
     __shared__ unsigned long long cursor[kDigitBins];
@@ -651,10 +657,15 @@ partition1_kernel(KeySpec ks, int64_t nrows, const unsigned long long* __restric
                 rw[j] = 0;
                 continue;
             }
+            rw[j] = (unsigned long long)r;
+            if (hrow) {  // the keys the count pass wrote: no second read and hash of the key columns
+                h[j] = r < r1 ? hrow[r] : kEmpty;
+                keep[j] = h[j] != kEmpty;
+                continue;
+            }
             bool ng = false;
             h[j] = 0;
             keep[j] = r < r1 && row_key(ks, r, h[j], ng) && !ng && h[j] != kEmpty;
-            rw[j] = (unsigned long long)r;
         }
         scatter_tile<kDigitBins, GENERAL, TILE>(h, rw, keep, 0, kDigitBins - 1, hist, start, cursor, sh, sr, out_h, out_r);
     }
@@ -1282,7 +1293,7 @@ __global__ void __launch_bounds__(kBuildBlock)
 build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
              const unsigned long long* __restrict__ rows, const long long* __restrict__ weights,
              Slot* __restrict__ slots, unsigned long long* __restrict__ reps, Counters* __restrict__ ctr,
-             SummaryPartial* __restrict__ parts, double n, NarrowKey nk, KeySpec ks, int verify) {
+             SummaryPartial* __restrict__ parts, double n, NarrowKey nk) {
     const uint32_t* __restrict__ hs32 = reinterpret_cast<const uint32_t*>(hs);
     using C = typename std::conditional<WEIGHTED, unsigned long long, unsigned int>::type;
     __shared__ unsigned long long lkey[kRegion];
@@ -1319,35 +1330,6 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
     }
     if (!ok) lovf = 1;
     __syncthreads();
-    if constexpr (GENERAL) {
-        // The verification of a whole bucket (`verify`: no bucket of the build is split) while its table is in LDS:
-        // every row other than its group's representative (the smallest row) is compared with it byte for byte —
-        // instead of a pass over all rows that re-hashes each key and probes the table in HBM (verify_kernel).
-        if (verify && !it.split && !lovf) {
-            unsigned long long bad = 0;
-            for (unsigned long long j0 = it.begin + threadIdx.x; j0 < it.end; j0 += kStep) {
-#pragma unroll 4
-                for (int u = 0; u < kBuildUnroll; ++u) {
-                    const unsigned long long j = j0 + (unsigned long long)u * kBuildBlock;
-                    if (j >= it.end) break;
-                    const unsigned long long h = hs[j], row = rows[j];
-                    unsigned int p = region_probe(h);
-                    for (int probe = 0; probe < kRegion && lkey[p] != h; ++probe) p = (p + 1) & (kRegion - 1);
-                    const unsigned long long rep = lrep[p];
-                    if (rep != row && !rows_equal(ks, (int64_t)row, (int64_t)rep)) ++bad;
-                }
-            }
-            __shared__ unsigned long long vred[kBuildBlock / 64];
-            for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
-            if ((threadIdx.x & 63) == 0) vred[threadIdx.x >> 6] = bad;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                unsigned long long b = 0;
-                for (int w = 0; w < kBuildBlock / 64; ++w) b += vred[w];
-                if (b) atomicAdd(&ctr->mismatch, b);
-            }
-        }
-    }
     Slot* region = slots + (uint64_t)it.bucket * kRegion;
     unsigned long long* rrep = GENERAL ? reps + (uint64_t)it.bucket * kRegion : nullptr;
     if (!it.split) {
@@ -1411,43 +1393,58 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
     if (threadIdx.x == 0 && lovf) atomicAdd(&ctr->overflow, 1ull);
 }
 
-// The rows of split buckets (several work items merged into one region with atomics), verified once the table is
-// final: each item's (key, row) pairs from the partition buffers against the region's representative.
-__global__ void __launch_bounds__(kBuildBlock)
+// General keys, verified once the table is final: each work item's (key, row) pairs from the partition buffers
+// against their region's representative (the group's smallest row), byte for byte unless the row is the representative.
+constexpr int kVerifyBlock = 512;
+constexpr int kVerifyRows = 4;  // rows per lane and step, their loads and first probes issued together
+__global__ void __launch_bounds__(kVerifyBlock)
 verify_items_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
                     const unsigned long long* __restrict__ rows, const Slot* __restrict__ slots,
                     const unsigned long long* __restrict__ reps, KeySpec ks, Counters* __restrict__ ctr) {
-    __shared__ unsigned long long vred[kBuildBlock / 64];
+    __shared__ unsigned long long vred[kVerifyBlock / 64];
     const BuildItem it = items[blockIdx.x];
     const Slot* region = slots + (uint64_t)it.bucket * kRegion;
     const unsigned long long* rrep = reps + (uint64_t)it.bucket * kRegion;
     unsigned long long bad = 0;
-    for (unsigned long long j = it.begin + threadIdx.x; j < it.end; j += kBuildBlock) {
-        const unsigned long long h = hs[j], row = rows[j];
-        unsigned int p = region_probe(h);
-        bool found = false;
-        for (int probe = 0; probe < kRegion; ++probe) {
-            const unsigned long long k = region[p].key;
-            if (k == h) {
-                found = true;
-                break;
+    constexpr unsigned long long kStep = (unsigned long long)kVerifyBlock * kVerifyRows;
+    for (unsigned long long j0 = it.begin + threadIdx.x; j0 < it.end; j0 += kStep) {
+        unsigned long long h[kVerifyRows], row[kVerifyRows], rep[kVerifyRows];
+        unsigned int p[kVerifyRows];
+        bool in[kVerifyRows];
+#pragma unroll
+        for (int u = 0; u < kVerifyRows; ++u) {
+            const unsigned long long j = j0 + (unsigned long long)u * kVerifyBlock;
+            in[u] = j < it.end;
+            h[u] = in[u] ? hs[j] : kEmpty;
+            row[u] = in[u] ? rows[j] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kVerifyRows; ++u) {
+            p[u] = region_probe(h[u]);
+            // the group's slot: most keys sit at their first probe position
+            unsigned long long k = in[u] ? region[p[u]].key : h[u];
+            for (int probe = 0; in[u] && k != h[u] && probe < kRegion; ++probe) {
+                if (k == kEmpty) {
+                    in[u] = false;
+                    ++bad;  // a key missing from the table
+                    break;
+                }
+                p[u] = (p[u] + 1) & (kRegion - 1);
+                k = region[p[u]].key;
             }
-            if (k == kEmpty) break;
-            p = (p + 1) & (kRegion - 1);
         }
-        if (!found) {
-            ++bad;
-            continue;
-        }
-        const unsigned long long rep = rrep[p];
-        if (rep != row && !rows_equal(ks, (int64_t)row, (int64_t)rep)) ++bad;
+#pragma unroll
+        for (int u = 0; u < kVerifyRows; ++u) rep[u] = in[u] ? rrep[p[u]] : row[u];
+#pragma unroll
+        for (int u = 0; u < kVerifyRows; ++u)
+            if (rep[u] != row[u] && !rows_equal(ks, (int64_t)row[u], (int64_t)rep[u])) ++bad;
     }
     for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
     if ((threadIdx.x & 63) == 0) vred[threadIdx.x >> 6] = bad;
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long b = 0;
-        for (int w = 0; w < kBuildBlock / 64; ++w) b += vred[w];
+        for (int w = 0; w < kVerifyBlock / 64; ++w) b += vred[w];
         if (b) atomicAdd(&ctr->mismatch, b);
     }
 }
@@ -1821,6 +1818,30 @@ summary_kernel(const Slot* __restrict__ slots, uint64_t cap, double n, SummaryPa
     if (threadIdx.x == 0) out[blockIdx.x] = red[0];
 }
 
+// The summary partial of one region (blockIdx.x -> bucket) of the table.
+__global__ void __launch_bounds__(kFreqBlock)
+region_summary_kernel(const unsigned int* __restrict__ buckets, const Slot* __restrict__ slots, double n,
+                      SummaryPartial* __restrict__ out) {
+    __shared__ SummaryPartial red[kFreqBlock];
+    const Slot* region = slots + (uint64_t)buckets[blockIdx.x] * kRegion;
+    SummaryPartial p = {0, 0, 0, 0, 0, 0};
+    for (int i = threadIdx.x; i < kRegion; i += kFreqBlock) {
+        const unsigned long long c = region[i].count;
+        if (c == 0) continue;
+        p.groups++;
+        p.unique += c == 1;
+        p.maxc = c > p.maxc ? c : p.maxc;
+        if (n > 0) summary_add_term(p, entropy_term(c, n));
+    }
+    red[threadIdx.x] = p;
+    __syncthreads();
+    for (int st = kFreqBlock / 2; st > 0; st >>= 1) {
+        if (threadIdx.x < st) summary_merge(red[threadIdx.x], red[threadIdx.x + st]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
 // Radix-select step: histogram of 11-bit digit `shift` of counts whose higher bits equal `prefix`.
 __global__ void __launch_bounds__(kFreqBlock)
 digit_hist_kernel(const Slot* __restrict__ slots, uint64_t cap, int shift, unsigned long long prefix_mask,
@@ -2130,44 +2151,39 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     SummaryPartial* bparts = nullptr;
     FQ_HIP(ctx, buf.alloc((void**)&bparts, items.size() * sizeof(SummaryPartial)));
     const double build_n = (double)t->host_ctr.num_rows;  // the count pass's numRows (copied before the build)
-    // general keys: whole buckets are verified inside the build, the rows of split buckets by verify_items_kernel
-    // after it (DQ_FREQ_VERIFY_PASS: the row pass over every row instead)
-    std::vector<BuildItem> split_items;
-    for (const BuildItem& bi : items)
-        if (bi.split) split_items.push_back(bi);
-    const int verify_in_build = general && !getenv("DQ_FREQ_VERIFY_PASS") ? 1 : 0;
-    const KeySpec vks = general ? t->ks : KeySpec{};
+    // general keys: every row is verified against its group's representative by verify_items_kernel, one workgroup
+    // per work item reading the item's (key, row) pairs from the partition buffers with the item's region L2-resident
+    // (DQ_FREQ_VERIFY_PASS: a pass over the rows instead, re-hashing each key). r05: comparing inside the build while
+    // the table is in LDS cost more (build 7.4 -> 16.7 ms on the C5 text column: the random row reads stall the
+    // build's few resident workgroups).
+    const int verify_by_items = general && !getenv("DQ_FREQ_VERIFY_PASS") ? 1 : 0;
     if (general && weighted)
         hipLaunchKernelGGL((build_kernel<true, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{}, vks, verify_in_build);
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     else if (general)
         hipLaunchKernelGGL((build_kernel<true, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{}, vks, verify_in_build);
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     else if (weighted)
         hipLaunchKernelGGL((build_kernel<false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{}, vks, verify_in_build);
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     else if (narrow)
         hipLaunchKernelGGL((build_kernel<false, false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows,
-                           w, t->slots, t->reps, t->ctr, bparts, build_n, *narrow, vks, 0);
+                           w, t->slots, t->reps, t->ctr, bparts, build_n, *narrow);
     else
         hipLaunchKernelGGL((build_kernel<false, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
-                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{}, vks, verify_in_build);
+                           t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     FQ_HIP(ctx, hipGetLastError());
     if (nspill) {
         const int grid = (int)std::min<unsigned long long>((nspill + kSpillChunk - 1) / kSpillChunk, 2048);
         hipLaunchKernelGGL(spill_insert_kernel, dim3(grid), dim3(kBuildBlock), 0, s, spill, nspill, t->slots, bits, t->ctr);
         FQ_HIP(ctx, hipGetLastError());
     }
-    if (verify_in_build && !split_items.empty()) {
-        BuildItem* dsplit = nullptr;
-        FQ_HIP(ctx, buf.alloc((void**)&dsplit, split_items.size() * sizeof(BuildItem)));
-        FQ_HIP(ctx, hipMemcpyAsync(dsplit, split_items.data(), split_items.size() * sizeof(BuildItem),
-                                   hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(verify_items_kernel, dim3((unsigned int)split_items.size()), dim3(kBuildBlock), 0, s, dsplit,
-                           sorted, srows, t->slots, t->reps, t->ks, t->ctr);
+    if (verify_by_items && nitems > 0) {
+        hipLaunchKernelGGL(verify_items_kernel, dim3((unsigned int)nitems), dim3(kVerifyBlock), 0, s,
+                           (const BuildItem*)ditems, sorted, srows, t->slots, t->reps, t->ks, t->ctr);
         FQ_HIP(ctx, hipGetLastError());
     }
-    if (general && nrows > 0 && !verify_in_build) {
+    if (general && nrows > 0 && !verify_by_items) {
         const int grid = (int)std::min<int64_t>((nrows + kFreqBlock - 1) / kFreqBlock, 8192);
         hipLaunchKernelGGL(verify_kernel, dim3(grid), dim3(kFreqBlock), 0, s, t->ks, nrows, t->slots, t->reps, bits,
                            t->ctr);
@@ -2182,9 +2198,33 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     if (t->host_ctr.overflow == 0 && t->host_ctr.mismatch == 0 && nspill == 0) {  // spilled keys: the table scan
         bool all = true;
         SummaryPartial acc = {0, 0, 0, 0, 0, 0};
-        for (const SummaryPartial& p : hparts) {
-            if (p.pad) { all = false; break; }
-            summary_merge(acc, p);
+        std::vector<unsigned int> split_buckets;
+        for (size_t i = 0; i < hparts.size(); ++i) {
+            if (hparts[i].pad) {
+                split_buckets.push_back(items[i].bucket);
+                continue;
+            }
+            summary_merge(acc, hparts[i]);
+        }
+        std::sort(split_buckets.begin(), split_buckets.end());
+        split_buckets.erase(std::unique(split_buckets.begin(), split_buckets.end()), split_buckets.end());
+        if (!split_buckets.empty() && !getenv("DQ_FREQ_SPLIT_SCAN")) {
+            // the regions of split buckets (merged with atomics) scanned on their own, not the whole table
+            unsigned int* dsb = nullptr;
+            SummaryPartial* dsp = nullptr;
+            const size_t nsb = split_buckets.size();
+            FQ_HIP(ctx, buf.alloc((void**)&dsb, nsb * sizeof(unsigned int)));
+            FQ_HIP(ctx, buf.alloc((void**)&dsp, nsb * sizeof(SummaryPartial)));
+            FQ_HIP(ctx, hipMemcpyAsync(dsb, split_buckets.data(), nsb * sizeof(unsigned int), hipMemcpyHostToDevice, s));
+            hipLaunchKernelGGL(region_summary_kernel, dim3((unsigned int)nsb), dim3(kFreqBlock), 0, s,
+                               (const unsigned int*)dsb, (const Slot*)t->slots, build_n, dsp);
+            FQ_HIP(ctx, hipGetLastError());
+            std::vector<SummaryPartial> hsp(nsb);
+            FQ_HIP(ctx, hipMemcpyAsync(hsp.data(), dsp, nsb * sizeof(SummaryPartial), hipMemcpyDeviceToHost, s));
+            FQ_HIP(ctx, hipStreamSynchronize(s));
+            for (const SummaryPartial& p : hsp) summary_merge(acc, p);
+        } else if (!split_buckets.empty()) {
+            all = false;
         }
         if (all) {
             t->pre_valid = 1;
@@ -2276,7 +2316,7 @@ int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf
 constexpr int kMaxPartBits = 20;
 
 int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, int xgrid, const unsigned int* hist1,
-                      unsigned long long n, int bits, bool* collision) {
+                      unsigned long long n, int bits, bool* collision, const unsigned long long* hrow = nullptr) {
     hipStream_t s = dq::ctx_stream(ctx);
     const bool general = !t->fast || t->ks.weights != nullptr;  // carry row indices (representatives / weights)
     const size_t n_alloc = (size_t)std::max<unsigned long long>(n, 1);
@@ -2288,10 +2328,11 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
     hipLaunchKernelGGL(digit_scan_kernel, dim3(kDigitBins), dim3(256), 0, s, hist1, xgrid, kDigitBins, off1, totals);
     if (general)
         hipLaunchKernelGGL((partition1_kernel<true, kPartTile>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
-                           (const unsigned long long*)off1, (const unsigned long long*)totals, h1, r1);
+                           (const unsigned long long*)off1, (const unsigned long long*)totals, h1, r1, hrow);
     else
         hipLaunchKernelGGL((partition1_kernel<false, kPartTile>), dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows,
-                           (const unsigned long long*)off1, (const unsigned long long*)totals, h1, r1);
+                           (const unsigned long long*)off1, (const unsigned long long*)totals, h1, r1,
+                           (const unsigned long long*)nullptr);
     FQ_HIP(ctx, hipGetLastError());
     std::vector<unsigned long long> tot(kDigitBins), pbegin(kDigitBins + 1, 0);
     FQ_HIP(ctx, hipMemcpyAsync(tot.data(), totals, sizeof(unsigned long long) * kDigitBins, hipMemcpyDeviceToHost, s));
@@ -2646,10 +2687,12 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
     // ColumnProfiler sends here has <= 120 distinct values). A workgroup whose LDS table fills stops at once and the
     // build takes the sized path below (the cost of a wrong guess: a few thousand rows per workgroup); a fingerprint
     // collision also goes there (it re-seeds).
+    bool many_keys = false;  // the optimistic small build overflowed: a large table, its keys worth keeping per row
     if (general && !t->ks.weights && nrows >= kOptimisticSmallRows && !getenv("DQ_FREQ_NO_SMALL") &&
         !getenv("DQ_FREQ_NO_OPTIMISTIC")) {
         bool overflow = false, collision = false;
         const int rc = build_small(ctx, t, nrows, 0.0, buf, &overflow, &collision, true);
+        many_keys = overflow;
         if (rc != DQ_OK) return rc;
         if (!overflow && !collision) {
             ctx->freq_paths[DQ_FREQ_PATH_SMALL_OPTIMISTIC]++;
@@ -2669,10 +2712,14 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         FQ_HIP(ctx, hipMemsetAsync(bk, 0, 2 * sizeof(unsigned long long) * xgrid, s));
         FQ_HIP(ctx, hipMemsetAsync(regs, 0, kSizingRegs * sizeof(unsigned int), s));
         FQ_HIP(ctx, hipMemsetAsync(t->ctr, 0, sizeof(Counters), s));
+        // general keys of a large table: the count pass writes every row's key and the partition pass reads it back
+        // (8 B a row instead of reading and hashing the key columns twice)
+        unsigned long long* hrow = nullptr;
+        if (general && many_keys && !getenv("DQ_FREQ_NO_HROW")) FQ_HIP(ctx, buf.alloc((void**)&hrow, n_alloc * 8));
         ctx->freq_paths[DQ_FREQ_PATH_EXACT]++;
         if (nrows > 0) {
             hipLaunchKernelGGL(extract_count_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows, bk, regs_part,
-                               t->ctr, hist1, kPartTile);
+                               t->ctr, hist1, kPartTile, hrow);
             hipLaunchKernelGGL(sizing_reduce_kernel, dim3(kSizingRegs / 256, std::min(xgrid, 64)), dim3(256), 0, s,
                                (const uint8_t*)regs_part, xgrid, kSizingRegs, regs);
         }
@@ -2707,7 +2754,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         }
         if (!no_partition && n > 0 && bits >= 8 && bits <= kMaxPartBits) {
             ctx->freq_paths[DQ_FREQ_PATH_PARTITIONED]++;
-            const int rc = build_partitioned(ctx, t, nrows, buf, xgrid, hist1, n, bits, &collision);
+            const int rc = build_partitioned(ctx, t, nrows, buf, xgrid, hist1, n, bits, &collision, hrow);
             if (rc != DQ_OK) return rc;
             if (!collision) return DQ_OK;
             t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
