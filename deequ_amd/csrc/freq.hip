@@ -380,10 +380,50 @@ __device__ __forceinline__ void chunk_of(int64_t nrows, int64_t& r0, int64_t& r1
     if (r0 > nrows) r0 = nrows;
 }
 
+// One string key column: a key of <= 15 bytes as two exact words (see the small build below).
+constexpr uint64_t kTupleNull = ~0ull, kTupleLong = ~0ull - 1;
+__device__ __forceinline__ bool short_key_tuple(const KeySpec& ks, int64_t r, uint64_t& b0, uint64_t& b1) {
+    const KeyCol& c = ks.cols[0];
+    if (!is_valid(c, r)) {
+        if (ks.string_null_is_value) {  // "NullValue"
+            b0 = 0x756C61566C6C754EULL;
+            b1 = 0x65ull | (9ull << 56);
+        } else {
+            b0 = b1 = kTupleNull;
+        }
+        return true;
+    }
+    int len;
+    const uint8_t* p = str_span(c, r, len);
+    if (len > 15) {
+        b0 = b1 = kTupleLong;
+        return false;
+    }
+    const uint8_t* a = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(p - a);
+    const int ndw = (int)((sh + (uint32_t)len + 3) >> 2);  // only dwords holding bytes of [p, p + len): <= 5
+    uint32_t w[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) w[k] = k < ndw ? dw_at(a + 4 * k) : 0u;
+    uint64_t x0 = (uint64_t)__builtin_amdgcn_alignbyte(w[1], w[0], sh) |
+                  ((uint64_t)__builtin_amdgcn_alignbyte(w[2], w[1], sh) << 32);
+    uint64_t x1 = (uint64_t)__builtin_amdgcn_alignbyte(w[3], w[2], sh) |
+                  ((uint64_t)__builtin_amdgcn_alignbyte(w[4], w[3], sh) << 32);
+    if (len < 8) {
+        x0 &= len ? (~0ull >> (64 - 8 * len)) : 0ull;
+        x1 = 0;
+    } else {
+        x1 &= len > 8 ? (~0ull >> (64 - 8 * (len - 8))) : 0ull;
+    }
+    b0 = x0;
+    b1 = x1 | ((uint64_t)len << 56);
+    return true;
+}
+
 __global__ void __launch_bounds__(kFreqBlock)
 extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__ block_keep,
                      uint8_t* __restrict__ regs_part, Counters* __restrict__ ctr, unsigned int* __restrict__ hist1,
-                     int tile_rows, unsigned long long* __restrict__ hrow) {
+                     int tile_rows, unsigned long long* __restrict__ hrow, unsigned long long* __restrict__ tup) {
     __shared__ unsigned int lds[kSizingRegs];
     __shared__ unsigned int dh[kDigitBins];
     __shared__ unsigned long long red[kFreqBlock / 64];
@@ -412,6 +452,17 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
             for (int u = 0; u < U; ++u) {
                 const int64_t r = rb + (int64_t)u * kFreqBlock;
                 if (r < r1) hrow[r] = ok[u] && !ngv[u] ? hv[u] : kEmpty;
+            }
+        if (tup)  // one string key column: each row's key as two exact words (kTupleLong past 15 bytes) for the checks
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = rb + (int64_t)u * kFreqBlock;
+                if (r < r1 && ok[u] && !ngv[u]) {
+                    uint64_t b0, b1;
+                    short_key_tuple(ks, r, b0, b1);
+                    tup[2 * r] = b0;
+                    tup[2 * r + 1] = b1;
+                }
             }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1400,7 +1451,8 @@ constexpr int kVerifyRows = 4;  // rows per lane and step, their loads and first
 __global__ void __launch_bounds__(kVerifyBlock)
 verify_items_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
                     const unsigned long long* __restrict__ rows, const Slot* __restrict__ slots,
-                    const unsigned long long* __restrict__ reps, KeySpec ks, Counters* __restrict__ ctr) {
+                    const unsigned long long* __restrict__ reps, KeySpec ks, Counters* __restrict__ ctr,
+                    const unsigned long long* __restrict__ tup) {
     __shared__ unsigned long long vred[kVerifyBlock / 64];
     const BuildItem it = items[blockIdx.x];
     const Slot* region = slots + (uint64_t)it.bucket * kRegion;
@@ -1435,6 +1487,27 @@ verify_items_kernel(const BuildItem* __restrict__ items, const unsigned long lon
         }
 #pragma unroll
         for (int u = 0; u < kVerifyRows; ++u) rep[u] = in[u] ? rrep[p[u]] : row[u];
+        if (tup) {  // 16-byte tuples of keys <= 15 bytes: equal tuples <=> equal keys; longer keys compare bytes
+            uint64_t a0[kVerifyRows], a1[kVerifyRows], c0[kVerifyRows], c1[kVerifyRows];
+#pragma unroll
+            for (int u = 0; u < kVerifyRows; ++u) {
+                const bool need = rep[u] != row[u];
+                a0[u] = need ? tup[2 * row[u]] : 0;
+                a1[u] = need ? tup[2 * row[u] + 1] : 0;
+                c0[u] = need ? tup[2 * rep[u]] : 0;
+                c1[u] = need ? tup[2 * rep[u] + 1] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kVerifyRows; ++u) {
+                if (rep[u] == row[u]) continue;
+                if (a1[u] != kTupleLong && c1[u] != kTupleLong) {
+                    if (a0[u] != c0[u] || a1[u] != c1[u]) ++bad;
+                } else if (!rows_equal(ks, (int64_t)row[u], (int64_t)rep[u])) {
+                    ++bad;
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int u = 0; u < kVerifyRows; ++u)
             if (rep[u] != row[u] && !rows_equal(ks, (int64_t)row[u], (int64_t)rep[u])) ++bad;
@@ -1512,44 +1585,7 @@ spill_insert_kernel(const unsigned long long* __restrict__ spill, unsigned long 
 // words with the representative's copy in LDS instead of re-reading both rows' bytes from HBM (half the kernel's time).
 // A NULL row of a grouping is one marker, a NULL row of a Histogram the bytes of "NullValue" (string_null_is_value),
 // a longer key the "long" marker (verified through rows_equal).
-constexpr uint64_t kTupleNull = ~0ull, kTupleLong = ~0ull - 1;
-__device__ __forceinline__ bool short_key_tuple(const KeySpec& ks, int64_t r, uint64_t& b0, uint64_t& b1) {
-    const KeyCol& c = ks.cols[0];
-    if (!is_valid(c, r)) {
-        if (ks.string_null_is_value) {  // "NullValue"
-            b0 = 0x756C61566C6C754EULL;
-            b1 = 0x65ull | (9ull << 56);
-        } else {
-            b0 = b1 = kTupleNull;
-        }
-        return true;
-    }
-    int len;
-    const uint8_t* p = str_span(c, r, len);
-    if (len > 15) {
-        b0 = b1 = kTupleLong;
-        return false;
-    }
-    const uint8_t* a = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(p - a);
-    const int ndw = (int)((sh + (uint32_t)len + 3) >> 2);  // only dwords holding bytes of [p, p + len): <= 5
-    uint32_t w[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) w[k] = k < ndw ? dw_at(a + 4 * k) : 0u;
-    uint64_t x0 = (uint64_t)__builtin_amdgcn_alignbyte(w[1], w[0], sh) |
-                  ((uint64_t)__builtin_amdgcn_alignbyte(w[2], w[1], sh) << 32);
-    uint64_t x1 = (uint64_t)__builtin_amdgcn_alignbyte(w[3], w[2], sh) |
-                  ((uint64_t)__builtin_amdgcn_alignbyte(w[4], w[3], sh) << 32);
-    if (len < 8) {
-        x0 &= len ? (~0ull >> (64 - 8 * len)) : 0ull;
-        x1 = 0;
-    } else {
-        x1 &= len > 8 ? (~0ull >> (64 - 8 * (len - 8))) : 0ull;
-    }
-    b0 = x0;
-    b1 = x1 | ((uint64_t)len << 56);
-    return true;
-}
+// (kTupleNull / kTupleLong / short_key_tuple: defined before extract_count_kernel, which also writes them)
 
 // XXH64 (seed) of a <= 15-byte key held as short_key_tuple words: the same value as dev_xxh_bytes over its bytes.
 __device__ __forceinline__ uint64_t xxh_short_words(uint64_t b0, uint64_t b1, uint64_t seed) {
@@ -2115,7 +2151,7 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
                   const unsigned long long* srows, const std::vector<unsigned long long>& bstart,
                   const std::vector<unsigned long long>& bcount, int bits, bool* overflow, bool* collision,
                   const NarrowKey* narrow = nullptr, const unsigned long long* spill = nullptr,
-                  unsigned long long nspill = 0) {
+                  unsigned long long nspill = 0, const unsigned long long* tup = nullptr) {
     hipStream_t s = dq::ctx_stream(ctx);
     const bool general = !t->fast;
     const bool weighted = t->ks.weights != nullptr;
@@ -2180,7 +2216,7 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     }
     if (verify_by_items && nitems > 0) {
         hipLaunchKernelGGL(verify_items_kernel, dim3((unsigned int)nitems), dim3(kVerifyBlock), 0, s,
-                           (const BuildItem*)ditems, sorted, srows, t->slots, t->reps, t->ks, t->ctr);
+                           (const BuildItem*)ditems, sorted, srows, t->slots, t->reps, t->ks, t->ctr, tup);
         FQ_HIP(ctx, hipGetLastError());
     }
     if (general && nrows > 0 && !verify_by_items) {
@@ -2316,7 +2352,8 @@ int build_small(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, double est, DevBuf
 constexpr int kMaxPartBits = 20;
 
 int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, int xgrid, const unsigned int* hist1,
-                      unsigned long long n, int bits, bool* collision, const unsigned long long* hrow = nullptr) {
+                      unsigned long long n, int bits, bool* collision, const unsigned long long* hrow = nullptr,
+                      const unsigned long long* tup = nullptr) {
     hipStream_t s = dq::ctx_stream(ctx);
     const bool general = !t->fast || t->ks.weights != nullptr;  // carry row indices (representatives / weights)
     const size_t n_alloc = (size_t)std::max<unsigned long long>(n, 1);
@@ -2411,7 +2448,8 @@ int build_partitioned(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf,
             srows = r2;
         }
         bool overflow = false;
-        const int rc = build_regions(ctx, t, nrows, buf, sorted, srows, bstart, bcount, bits, &overflow, collision);
+        const int rc = build_regions(ctx, t, nrows, buf, sorted, srows, bstart, bcount, bits, &overflow, collision,
+                                     nullptr, nullptr, 0, tup);
         if (rc != DQ_OK) return rc;
         if (!overflow) return DQ_OK;
     }
@@ -2716,10 +2754,15 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         // (8 B a row instead of reading and hashing the key columns twice)
         unsigned long long* hrow = nullptr;
         if (general && many_keys && !getenv("DQ_FREQ_NO_HROW")) FQ_HIP(ctx, buf.alloc((void**)&hrow, n_alloc * 8));
+        // one string key column: its rows as two-word tuples too, so the verification compares 16-byte tuples
+        // instead of both rows' offsets and bytes
+        unsigned long long* tup = nullptr;
+        if (hrow && t->ks.ncols == 1 && t->ks.cols[0].spark_type == DQ_TYPE_STRING && !getenv("DQ_FREQ_NO_TUPLES"))
+            FQ_HIP(ctx, buf.alloc((void**)&tup, n_alloc * 16));
         ctx->freq_paths[DQ_FREQ_PATH_EXACT]++;
         if (nrows > 0) {
             hipLaunchKernelGGL(extract_count_kernel, dim3(xgrid), dim3(kFreqBlock), 0, s, t->ks, nrows, bk, regs_part,
-                               t->ctr, hist1, kPartTile, hrow);
+                               t->ctr, hist1, kPartTile, hrow, tup);
             hipLaunchKernelGGL(sizing_reduce_kernel, dim3(kSizingRegs / 256, std::min(xgrid, 64)), dim3(256), 0, s,
                                (const uint8_t*)regs_part, xgrid, kSizingRegs, regs);
         }
@@ -2754,7 +2797,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         }
         if (!no_partition && n > 0 && bits >= 8 && bits <= kMaxPartBits) {
             ctx->freq_paths[DQ_FREQ_PATH_PARTITIONED]++;
-            const int rc = build_partitioned(ctx, t, nrows, buf, xgrid, hist1, n, bits, &collision, hrow);
+            const int rc = build_partitioned(ctx, t, nrows, buf, xgrid, hist1, n, bits, &collision, hrow, tup);
             if (rc != DQ_OK) return rc;
             if (!collision) return DQ_OK;
             t->ks.seed = mix64(t->ks.seed + 0x9E3779B97F4A7C15ULL);
