@@ -216,7 +216,10 @@ __device__ __forceinline__ void string_row(const StrSlot& s, const uint8_t* data
 
 // Bytes of one wave's 64 consecutive strings staged in LDS (coalesced dword loads of the whole byte range instead of
 // each lane's scattered byte / dword loads); ranges longer than this are read from HBM directly.
-constexpr int kStrStageWords = 512;
+#ifndef DQ_STR_STAGE
+#define DQ_STR_STAGE 512
+#endif
+constexpr int kStrStageWords = DQ_STR_STAGE;
 
 // ---- the staged form: 32-bit byte positions into the wave's LDS words -----------------------------------------------
 // The same ops as above over a staged range (< 2 KiB, so positions are 32-bit: the int64 position arithmetic of the
