@@ -19,7 +19,10 @@ t, _ = bench.c5_shard(torch, N, engine.ctx(), torch.device("cuda", 0), rows)
 extras = bench.c5_extra_analyzers(D)
 print("table ready", flush=True)
 for i in range(k):
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
+    m0 = time.monotonic_ns()
     bench.c5_step(D, t, extras)
     torch.cuda.synchronize()
-    print("step %d %.1f ms" % (i, (time.perf_counter() - t0) * 1e3), flush=True)
+    print("step %d %.1f ms monotonic_ns %d %d" % (i, (time.perf_counter() - t0) * 1e3, m0, time.monotonic_ns()),
+          flush=True)
