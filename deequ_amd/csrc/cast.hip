@@ -60,6 +60,15 @@ cast_kernel(CastSource c, int64_t nrows, int to_double, void* __restrict__ value
         int64_t v = 0;
         const uint8_t* sbase = nullptr;  // STRING: the staged copy of this wave's bytes, based at a0
         int64_t a0 = 0;
+        // the row's validity and (STRING) its offsets, loaded before the staging: with the wave's range bounds they
+        // are one memory round trip, not a third one after the stage's barrier
+        const bool rin = r < nrows;
+        const bool rvalid = rin && (c.validity == nullptr || ((c.validity[r >> 6] >> (r & 63)) & 1ull));
+        int32_t ro = 0, rlen = 0;
+        if (STRING && rin) {
+            ro = c.offsets[r];
+            rlen = c.offsets[r + 1] - ro;
+        }
         if (STRING) {
             const int64_t w0 = base + 64 * wave;
             if (w0 < nrows) {
@@ -77,10 +86,10 @@ cast_kernel(CastSource c, int64_t nrows, int to_double, void* __restrict__ value
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         }
-        if (r < nrows && (c.validity == nullptr || ((c.validity[r >> 6] >> (r & 63)) & 1ull))) {
+        if (rvalid) {
             if (STRING) {
-                const int32_t o = c.offsets[r];
-                const int len = c.offsets[r + 1] - o;
+                const int32_t o = ro;
+                const int len = rlen;
                 const uint8_t* s = sbase ? sbase + (o - a0) : c.bytes + o;
                 if (to_double) {
                     bool slow = false;
