@@ -216,6 +216,9 @@ __device__ __forceinline__ void string_row(const StrSlot& s, const uint8_t* data
 
 // Bytes of one wave's 64 consecutive strings staged in LDS (coalesced dword loads of the whole byte range instead of
 // each lane's scattered byte / dword loads); ranges longer than this are read from HBM directly.
+#ifndef DQ_STR_B128
+#define DQ_STR_B128 1
+#endif
 #ifndef DQ_STR_STAGE
 #define DQ_STR_STAGE 512
 #endif
@@ -387,6 +390,31 @@ __device__ __forceinline__ void string_groups(const uint8_t* __restrict__ data, 
         if (nwords <= kStrR * kStrStageWords) {
             const __amdgpu_buffer_rsrc_t r =
                 __builtin_amdgcn_make_buffer_rsrc((void*)(data + a0), (short)0, nwords * 4, 0x00020000);
+#if DQ_STR_B128
+            // 16-byte loads and LDS stores (two per lane per 512 words instead of eight 4-byte ones); words past the
+            // range read as 0 (the buffer's size) and the stage holds whole 512-word blocks
+            // (a load straddling the range end is split into dword loads, so no load crosses the buffer's size)
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            for (int i0 = 0; i0 < nwords; i0 += 64 * 8) {
+                u32x4 w[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int c = i0 + 4 * (64 * u + lane);
+                    if (c + 4 <= nwords) {
+                        w[u] = __builtin_amdgcn_raw_buffer_load_b128(r, c * 4, 0, 0);
+                    } else {
+                        w[u] = u32x4{0u, 0u, 0u, 0u};
+                        for (int k = 0; k < 3; ++k)
+                            if (c + k < nwords) w[u][k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(r, (c + k) * 4, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int c = i0 + 4 * (64 * u + lane);
+                    if (c < nwords) *reinterpret_cast<u32x4*>(&stage[c]) = w[u];
+                }
+            }
+#else
             for (int i0 = 0; i0 < nwords; i0 += 64 * 8) {
                 uint32_t w[8];
 #pragma unroll
@@ -396,6 +424,7 @@ __device__ __forceinline__ void string_groups(const uint8_t* __restrict__ data, 
                 for (int u = 0; u < 8; ++u)
                     if (i0 + 64 * u + lane < nwords) stage[i0 + 64 * u + lane] = w[u];
             }
+#endif
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -427,7 +456,7 @@ scan_strings_kernel(const StrSlot* __restrict__ slots, int nslots, int64_t nrows
                     StrPartial* __restrict__ partials, uint8_t* __restrict__ hll_partials) {
     __shared__ uint32_t regs[kHllRegs];
     __shared__ StrPartial red[kBlock / 64];
-    __shared__ uint32_t stage[kBlock / 64][kStrR * kStrStageWords];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kBlock / 64][kStrR * kStrStageWords];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (int si = 0; si < nslots; ++si) {
         const StrSlot s = slots[si];
