@@ -1,6 +1,8 @@
 """Device selection and the frequency-table handle (the GPU side of computeFrequencies)."""
+import contextlib
 import ctypes
 import os
+import threading
 
 import numpy as np
 
@@ -20,8 +22,25 @@ def device():
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
+_local = threading.local()
+
+
 def ctx():
-    return N.context(device())
+    """This thread's context: the process-wide one of the device, unless `using_context` set another."""
+    c = getattr(_local, "ctx", None)
+    return c if c is not None else N.context(device())
+
+
+@contextlib.contextmanager
+def using_context(context):
+    """Run this thread's engine calls on `context` (a second context of the device has its own stream and scratch,
+    so work on it may proceed while another thread drives the first)."""
+    prev = getattr(_local, "ctx", None)
+    _local.ctx = context
+    try:
+        yield context
+    finally:
+        _local.ctx = prev
 
 
 class GroupFloat(float):

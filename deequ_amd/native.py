@@ -520,6 +520,17 @@ class Context:
 _contexts = {}
 
 
+def aux_context(device=0):
+    """A second cached single-device context of `device` (its own stream and scratch cache): work a helper thread
+    overlaps with the main context's, e.g. the ColumnProfiler's histogram pass beside its numeric pass."""
+    key = ("aux", device)
+    ctx = _contexts.get(key)
+    if ctx is None:
+        ctx = Context(device)
+        _contexts[key] = ctx
+    return ctx
+
+
 def context(device=0):
     """Process-wide cached context for a device. DQ_DEVICES="0,1,..." makes it one multi-device context over
     those GPUs (every host-column scan / grouping of the runner is then row-sharded across them)."""

@@ -13,6 +13,7 @@ The metrics repository / result reuse and the JSON file output of the runner are
 import json
 import math
 import os
+import threading
 
 import numpy as np
 
@@ -208,6 +209,19 @@ class ColumnProfiler:
         res1 = passes.run(data, first + [Size()])
         generic = ColumnProfiler._extract_generic(relevant, schema, res1, predefinedTypes)
 
+        # pass 3's columns depend on pass 1 only: on this process's GPU its histogram builds run on a second context
+        # (own stream) in a helper thread while this thread casts, scans and aggregates pass 2 (the host aggregation
+        # of pass 2 otherwise leaves the GPU idle); DQ_PROFILE_SERIAL=1 runs the passes one after the other
+        targets = [c for c, cnt in generic.approximateNumDistincts.items()
+                   if schema[c] in _HISTOGRAM_TYPES and
+                   generic.typeOf(c) in (DataTypeInstances.String, DataTypeInstances.Boolean,
+                                         DataTypeInstances.Integral, DataTypeInstances.Fractional) and
+                   cnt <= lowCardinalityHistogramThreshold]
+        pending = None
+        if targets and type(passes) is LocalPasses and not os.environ.get("DQ_PROFILE_SERIAL") and \
+                not os.environ.get("DQ_DEVICES"):
+            pending = _histograms_beside(passes, data, targets)
+
         # ---- pass 2 ------------------------------------------------------------------------------
         if printStatusUpdates:
             print("### PROFILING: Computing numeric column statistics in pass (2/3)...")
@@ -230,12 +244,10 @@ class ColumnProfiler:
         # ---- pass 3 ------------------------------------------------------------------------------
         if printStatusUpdates:
             print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3)...")
-        targets = [c for c, cnt in generic.approximateNumDistincts.items()
-                   if schema[c] in _HISTOGRAM_TYPES and
-                   generic.typeOf(c) in (DataTypeInstances.String, DataTypeInstances.Boolean,
-                                         DataTypeInstances.Integral, DataTypeInstances.Fractional) and
-                   cnt <= lowCardinalityHistogramThreshold]
-        histograms = passes.histograms(data, targets) if targets else {}
+        if pending is not None:
+            histograms = pending.result()
+        else:
+            histograms = passes.histograms(data, targets) if targets else {}
 
         profiles = {}
         for name in relevant:
@@ -307,6 +319,36 @@ class ColumnProfiler:
                 values[k] = DistributionValue(int(c), c / total)
             out[name] = Distribution(values, len(values))
         return out
+
+
+class _Pending:
+    """A helper thread's result (its exception re-raised by result())."""
+
+    def __init__(self, fn):
+        self.value, self.error = None, None
+        self.thread = threading.Thread(target=self._run, args=(fn,), daemon=True)
+        self.thread.start()
+
+    def _run(self, fn):
+        try:
+            self.value = fn()
+        except BaseException as e:  # handed to the caller
+            self.error = e
+
+    def result(self):
+        self.thread.join()
+        if self.error is not None:
+            raise self.error
+        return self.value
+
+
+def _histograms_beside(passes, data, targets):
+    from . import engine
+
+    def run():
+        with engine.using_context(N.aux_context(engine.device())):
+            return passes.histograms(data, targets)
+    return _Pending(run)
 
 
 def _cast_table(passes, data, casts):
