@@ -478,7 +478,9 @@ class Context:
             cap = int(n)
 
     def cast_column(self, column, nrows, to_type, values_dev_ptr, validity_dev_ptr):
-        """dq_cast_column: Spark Cast(column -> long | double) into caller-owned device buffers."""
+        """dq_cast_column: Spark Cast(column -> long | double) into caller-owned device buffers (torch's queued work
+        on them, e.g. a zero fill, completes first: the cast runs on the context's stream)."""
+        self._after_torch_stream()
         self.check(self.lib.dq_cast_column(self.handle, ctypes.byref(column), int(nrows), int(to_type),
                                             ctypes.c_void_p(values_dev_ptr), ctypes.c_void_p(validity_dev_ptr)),
                    "dq_cast_column")
@@ -520,10 +522,11 @@ class Context:
 _contexts = {}
 
 
-def aux_context(device=0):
-    """A second cached single-device context of `device` (its own stream and scratch cache): work a helper thread
-    overlaps with the main context's, e.g. the ColumnProfiler's histogram pass beside its numeric pass."""
-    key = ("aux", device)
+def aux_context(device=0, slot="aux"):
+    """Another cached single-device context of `device` (its own stream and scratch cache), one per `slot`: work a
+    helper thread overlaps with the main context's (the ColumnProfiler's histogram pass beside its numeric pass, a
+    run's grouping builds beside its scans)."""
+    key = ("aux", device, slot)
     ctx = _contexts.get(key)
     if ctx is None:
         ctx = Context(device)

@@ -13,7 +13,6 @@ The metrics repository / result reuse and the JSON file output of the runner are
 import json
 import math
 import os
-import threading
 
 import numpy as np
 
@@ -218,9 +217,8 @@ class ColumnProfiler:
                                          DataTypeInstances.Integral, DataTypeInstances.Fractional) and
                    cnt <= lowCardinalityHistogramThreshold]
         pending = None
-        if targets and type(passes) is LocalPasses and not os.environ.get("DQ_PROFILE_SERIAL") and \
-                not os.environ.get("DQ_DEVICES"):
-            pending = _histograms_beside(passes, data, targets)
+        if targets and type(passes) is LocalPasses and not os.environ.get("DQ_PROFILE_SERIAL"):
+            pending = _histograms_beside(passes, data, targets)  # None: the passes stay on this thread
 
         # ---- pass 2 ------------------------------------------------------------------------------
         if printStatusUpdates:
@@ -321,34 +319,9 @@ class ColumnProfiler:
         return out
 
 
-class _Pending:
-    """A helper thread's result (its exception re-raised by result())."""
-
-    def __init__(self, fn):
-        self.value, self.error = None, None
-        self.thread = threading.Thread(target=self._run, args=(fn,), daemon=True)
-        self.thread.start()
-
-    def _run(self, fn):
-        try:
-            self.value = fn()
-        except BaseException as e:  # handed to the caller
-            self.error = e
-
-    def result(self):
-        self.thread.join()
-        if self.error is not None:
-            raise self.error
-        return self.value
-
-
 def _histograms_beside(passes, data, targets):
-    from . import engine
-
-    def run():
-        with engine.using_context(N.aux_context(engine.device())):
-            return passes.histograms(data, targets)
-    return _Pending(run)
+    from .runners import _beside
+    return _beside(lambda: passes.histograms(data, targets), "hist")
 
 
 def _cast_table(passes, data, casts):

@@ -4,6 +4,7 @@ driving the MI355X engine. The scan-shareable analyzers of a run become ONE dq_s
 pass over HBM), exactly where the reference issues one `data.agg(...)` Spark job."""
 import json
 import os
+import threading
 
 from . import native as N
 from . import engine
@@ -21,6 +22,40 @@ def stream_chunk_rows():
     (copy of the next chunk overlapped with the scan of the current one) instead of being staged whole."""
     v = os.environ.get("DQ_STREAM_CHUNK_ROWS")
     return int(float(v)) if v else 0
+
+
+class _Pending:
+    """A helper thread's result (its exception re-raised by result())."""
+
+    def __init__(self, fn):
+        self.value, self.error = None, None
+        self.thread = threading.Thread(target=self._run, args=(fn,), daemon=True)
+        self.thread.start()
+
+    def _run(self, fn):
+        try:
+            self.value = fn()
+        except BaseException as e:  # handed to the caller
+            self.error = e
+
+    def result(self):
+        self.thread.join()
+        if self.error is not None:
+            raise self.error
+        return self.value
+
+
+def _beside(fn, slot):
+    """Run fn in a helper thread on a second context of this thread's device (own stream and scratch), or None when
+    the work must stay on this thread (DQ_RUN_SERIAL, a multi-device context, or already on a helper context)."""
+    if os.environ.get("DQ_RUN_SERIAL") or os.environ.get("DQ_DEVICES") or getattr(engine._local, "ctx", None):
+        return None
+    aux = N.aux_context(engine.device(), slot)
+
+    def run():
+        with engine.using_context(aux):
+            return fn()
+    return _Pending(run)
 
 
 class ScanResult(list):
@@ -306,17 +341,24 @@ class AnalysisRunner:
         allScanning = [a for a in passed if not isinstance(a, GroupingAnalyzer)]
         kllAnalyzers = [a for a in allScanning if isinstance(a, KLLSketch)]
         scanning = [a for a in allScanning if not isinstance(a, KLLSketch)]
+        def run_grouping():
+            grouped = AnalyzerContext.empty()
+            by_cols = {}
+            for a in grouping:
+                by_cols.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
+            for cols, group in by_cols.items():
+                _, metrics = AnalysisRunner._runGroupingAnalyzers(data, list(cols), group, aggregateWith,
+                                                                  saveStatesWith)
+                grouped = grouped + metrics
+            return grouped
+        # the grouping builds and the scanning / KLL passes read the table independently: the builds run on a second
+        # context in a helper thread meanwhile (Spark runs them as separate jobs)
+        pending = _beside(run_grouping, "group") if grouping and (scanning or kllAnalyzers) else None
         kllMetrics = AnalyzerContext.empty()
         if kllAnalyzers:
             kllMetrics = KLLRunner.computeKLLSketchesInExtraPass(data, kllAnalyzers, aggregateWith, saveStatesWith)
         nonGrouped = AnalysisRunner._runScanningAnalyzers(data, scanning, aggregateWith, saveStatesWith)
-        grouped = AnalyzerContext.empty()
-        by_cols = {}
-        for a in grouping:
-            by_cols.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
-        for cols, group in by_cols.items():
-            _, metrics = AnalysisRunner._runGroupingAnalyzers(data, list(cols), group, aggregateWith, saveStatesWith)
-            grouped = grouped + metrics
+        grouped = pending.result() if pending is not None else run_grouping()
         return preconditionFailures + nonGrouped + grouped + kllMetrics
 
     @staticmethod
@@ -334,10 +376,17 @@ class AnalysisRunner:
         # groups as Spark's shuffle of the partitions' partial counts (R/AnalysisRunner.scala:259-287)
         grouping = [a for a in analyzers if isinstance(a, GroupingAnalyzer)]
         whole = AnalyzerContext.empty()
+        grouping_pending = None
         if grouping and len(data.chunks) > 1:
             cols = sorted({c for a in grouping for c in a.groupingColumns() if c in data})
-            whole = AnalysisRunner.doAnalysisRun(data.concat(cols), grouping, aggregateWith, saveStatesWith)
             analyzers = [a for a in analyzers if not isinstance(a, GroupingAnalyzer)]
+
+            def run_grouping():
+                return AnalysisRunner.doAnalysisRun(data.concat(cols), grouping, aggregateWith, saveStatesWith)
+            # beside the other analyzers' passes, on a second context (see doAnalysisRun)
+            grouping_pending = _beside(run_grouping, "group") if analyzers else None
+            if grouping_pending is None:
+                whole = run_grouping()
             if not analyzers:
                 return whole
         # ApproxQuantile(s): one summary per column over every chunk (dq_quantile_summaries reads the chunks as
@@ -349,7 +398,7 @@ class AnalysisRunner:
             whole = whole + AnalysisRunner.doAnalysisRun(data.parted(cols), quant, aggregateWith, saveStatesWith)
             analyzers = [a for a in analyzers if not isinstance(a, (ApproxQuantile, ApproxQuantiles))]
             if not analyzers:
-                return whole
+                return whole + (grouping_pending.result() if grouping_pending is not None else AnalyzerContext.empty())
         providers, failures = [], {}
         for chunk in data.chunks:
             p = InMemoryStateProvider()
@@ -379,6 +428,8 @@ class AnalysisRunner:
                     empty[a] = a.computeMetricFrom(None)
                 except Exception as e:
                     empty[a] = a.toFailureMetric(e)
+        if grouping_pending is not None:
+            whole = whole + grouping_pending.result()
         return merged + AnalyzerContext(empty) + AnalyzerContext(failures) + whole
 
     @staticmethod
