@@ -399,11 +399,24 @@ class AnalysisRunner:
             analyzers = [a for a in analyzers if not isinstance(a, (ApproxQuantile, ApproxQuantiles))]
             if not analyzers:
                 return whole + (grouping_pending.result() if grouping_pending is not None else AnalyzerContext.empty())
+        def run_chunks(indices):
+            out = {}
+            for i in indices:
+                p = InMemoryStateProvider()
+                p.states_only = True  # states only: no per-chunk metric (an empty chunk state is no failure)
+                out[i] = (p, AnalysisRunner.doAnalysisRun(data.chunks[i], analyzers, saveStatesWith=p))
+            return out
+        # the chunks' runs are independent until the merge: the odd chunks run on a second context in a helper thread
+        # while this thread runs the even ones, so one chunk's host work (KLL schedules, state extraction) overlaps
+        # the other's kernels
+        nchunks = len(data.chunks)
+        odd = _beside(lambda: run_chunks(range(1, nchunks, 2)), "chunk") if nchunks > 1 else None
+        done = run_chunks(range(0, nchunks, 2) if odd is not None else range(nchunks))
+        if odd is not None:
+            done.update(odd.result())
         providers, failures = [], {}
-        for chunk in data.chunks:
-            p = InMemoryStateProvider()
-            p.states_only = True  # states only: no per-chunk metric (an empty chunk state is no failure)
-            res = AnalysisRunner.doAnalysisRun(chunk, analyzers, saveStatesWith=p)
+        for i in range(nchunks):  # chunk order: the merge and the first failure seen are those of a serial run
+            p, res = done[i]
             for a, m in res.metricMap.items():
                 if not m.value.isSuccess and a not in failures:
                     failures[a] = m
