@@ -376,18 +376,28 @@ class AnalysisRunner:
         # groups as Spark's shuffle of the partitions' partial counts (R/AnalysisRunner.scala:259-287)
         grouping = [a for a in analyzers if isinstance(a, GroupingAnalyzer)]
         whole = AnalyzerContext.empty()
-        grouping_pending = None
+        grouping_pending = []
         if grouping and len(data.chunks) > 1:
-            cols = sorted({c for a in grouping for c in a.groupingColumns() if c in data})
             analyzers = [a for a in analyzers if not isinstance(a, GroupingAnalyzer)]
-
-            def run_grouping():
-                return AnalysisRunner.doAnalysisRun(data.concat(cols), grouping, aggregateWith, saveStatesWith)
-            # beside the other analyzers' passes, on a second context (see doAnalysisRun)
-            grouping_pending = _beside(run_grouping, "group") if analyzers else None
-            if grouping_pending is None:
-                whole = run_grouping()
+            by_set = {}
+            for a in grouping:
+                by_set.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
+            sets = list(by_set.items())
+            # each grouping-column set on its own helper context (at most three; the rest, or the last set when
+            # nothing else runs, on this thread), beside the other analyzers' passes (see doAnalysisRun)
+            for k, (cset, group) in enumerate(sets):
+                def run_set(cset=cset, group=group):
+                    cols = [c for c in cset if c in data]
+                    return AnalysisRunner.doAnalysisRun(data.concat(cols), group, aggregateWith, saveStatesWith)
+                last_here = not analyzers and k == len(sets) - 1
+                h = None if last_here or k >= 3 else _beside(run_set, "group%d" % k)
+                if h is None:
+                    whole = whole + run_set()
+                else:
+                    grouping_pending.append(h)
             if not analyzers:
+                for h in grouping_pending:
+                    whole = whole + h.result()
                 return whole
         # ApproxQuantile(s): one summary per column over every chunk (dq_quantile_summaries reads the chunks as
         # parts), the exact order statistics of the shard -- a GK summary inside the same rank bound as the merge of
@@ -398,7 +408,9 @@ class AnalysisRunner:
             whole = whole + AnalysisRunner.doAnalysisRun(data.parted(cols), quant, aggregateWith, saveStatesWith)
             analyzers = [a for a in analyzers if not isinstance(a, (ApproxQuantile, ApproxQuantiles))]
             if not analyzers:
-                return whole + (grouping_pending.result() if grouping_pending is not None else AnalyzerContext.empty())
+                for h in grouping_pending:
+                    whole = whole + h.result()
+                return whole
         def run_chunks(indices):
             out = {}
             for i in indices:
@@ -441,8 +453,8 @@ class AnalysisRunner:
                     empty[a] = a.computeMetricFrom(None)
                 except Exception as e:
                     empty[a] = a.toFailureMetric(e)
-        if grouping_pending is not None:
-            whole = whole + grouping_pending.result()
+        for h in grouping_pending:
+            whole = whole + h.result()
         return merged + AnalyzerContext(empty) + AnalyzerContext(failures) + whole
 
     @staticmethod
