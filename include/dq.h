@@ -12,7 +12,11 @@
  *     holds a message. A failed dq_scan fails EVERY op of the batch, mirroring the catch-all in
  *     runScanningAnalyzers (R/AnalysisRunner.scala:320-323).
  *   - A dq_ctx from dq_open is bound to one GPU; one from dq_open_devices spans several GPUs of the node. A ctx
- *     is not re-entrant: one driver thread per ctx, one ctx per process/rank.
+ *     is not re-entrant: one driver thread per ctx. Several contexts of one GPU (each its own stream, scratch
+ *     cache and pinned staging) may be driven by different threads at once: independent passes of one analysis
+ *     then overlap on the device (the Python host runs grouping builds, histogram builds and the odd row chunks of
+ *     a shard on helper contexts this way). Inputs are read-only to every context; a buffer one context's stream
+ *     writes must not be read by another before that stream is synchronised.
  *   - States are returned in native byte order (little-endian on x86/MI355X hosts) with the
  *     field order of the reference's HdfsStateProvider layouts (A/StateProvider.scala:187-262).
  *
