@@ -42,7 +42,10 @@ constexpr int kQBuckets = 4096;          // buckets; kQBuckets - 1 splitters + a
 constexpr int kQSample = 65536;          // stratified sample size
 constexpr int kQBlock = 256;
 constexpr int kQHistBlock = 1024;      // the batched histogram pass: 32 waves per CU at its 64 KB of LDS
-constexpr int kQRowsPerLane = 8;         // independent loads / tree descents in flight per lane
+#ifndef DQ_Q_ROWS
+#define DQ_Q_ROWS 8
+#endif
+constexpr int kQRowsPerLane = DQ_Q_ROWS;  // independent loads / tree descents in flight per lane
 constexpr uint32_t kQNoTarget = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint64_t q_f64_bits(double d) { return (uint64_t)__double_as_longlong(d); }

@@ -15,7 +15,7 @@ for f in dq_api.cpp host_algebra.cpp multi.cpp scan.hip predicate.hip synth.hip 
   if [ "$f" = scan.hip ] && [ -n "${SCAN_REV:-}" ]; then git show "$SCAN_REV:deequ_amd/csrc/scan.hip" > _ab_rev_scan.hip; src=_ab_rev_scan.hip; fi
   if [ "$f" = kll.hip ] && [ -n "${KLL_REV:-}" ]; then git show "$KLL_REV:deequ_amd/csrc/kll.hip" > _ab_rev_kll.hip; src=_ab_rev_kll.hip; fi
   if [ "$f" = cast.hip ] && [ -n "${CAST_SRC:-}" ]; then cp "$CAST_SRC" _ab_src_cast.hip; src=_ab_src_cast.hip; fi
-  case $f in freq.hip|strings.hip|scan.hip|kll.hip|cast.hip) /opt/rocm/bin/hipcc $FLAGS "$@" -I. -x hip -c $src -o $OUT/$NAME.build/$f.o ;; *) cp build/$f.o $OUT/$NAME.build/$f.o ;; esac
+  case $f in freq.hip|strings.hip|scan.hip|kll.hip|cast.hip|quantile.hip) /opt/rocm/bin/hipcc $FLAGS "$@" -I. -x hip -c $src -o $OUT/$NAME.build/$f.o ;; *) cp build/$f.o $OUT/$NAME.build/$f.o ;; esac
   objs="$objs $OUT/$NAME.build/$f.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/$NAME.so $objs -ldl
