@@ -341,24 +341,33 @@ class AnalysisRunner:
         allScanning = [a for a in passed if not isinstance(a, GroupingAnalyzer)]
         kllAnalyzers = [a for a in allScanning if isinstance(a, KLLSketch)]
         scanning = [a for a in allScanning if not isinstance(a, KLLSketch)]
-        def run_grouping():
-            grouped = AnalyzerContext.empty()
-            by_cols = {}
-            for a in grouping:
-                by_cols.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
-            for cols, group in by_cols.items():
-                _, metrics = AnalysisRunner._runGroupingAnalyzers(data, list(cols), group, aggregateWith,
-                                                                  saveStatesWith)
-                grouped = grouped + metrics
-            return grouped
-        # the grouping builds and the scanning / KLL passes read the table independently: the builds run on a second
-        # context in a helper thread meanwhile (Spark runs them as separate jobs)
-        pending = _beside(run_grouping, "group") if grouping and (scanning or kllAnalyzers) else None
+        by_cols = {}
+        for a in grouping:
+            by_cols.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
+        sets = list(by_cols.items())
+
+        def run_set(cols, group):
+            _, metrics = AnalysisRunner._runGroupingAnalyzers(data, list(cols), group, aggregateWith, saveStatesWith)
+            return metrics
+        # the grouping builds (one per grouping-column set) and the scanning / KLL passes read the table independently:
+        # each set's build runs on its own helper context meanwhile (Spark runs them as separate jobs; at most three
+        # helpers, the rest -- or the last set when nothing else runs -- on this thread)
+        others = bool(scanning or kllAnalyzers)
+        helpers, here = [], []
+        for k, (cols, group) in enumerate(sets):
+            h = None
+            if k < 3 and (others or k < len(sets) - 1):
+                h = _beside(lambda cols=cols, group=group: run_set(cols, group), "group%d" % k)
+            (here.append((cols, group)) if h is None else helpers.append(h))
         kllMetrics = AnalyzerContext.empty()
         if kllAnalyzers:
             kllMetrics = KLLRunner.computeKLLSketchesInExtraPass(data, kllAnalyzers, aggregateWith, saveStatesWith)
         nonGrouped = AnalysisRunner._runScanningAnalyzers(data, scanning, aggregateWith, saveStatesWith)
-        grouped = pending.result() if pending is not None else run_grouping()
+        grouped = AnalyzerContext.empty()
+        for cols, group in here:
+            grouped = grouped + run_set(cols, group)
+        for h in helpers:
+            grouped = grouped + h.result()
         return preconditionFailures + nonGrouped + grouped + kllMetrics
 
     @staticmethod
