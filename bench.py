@@ -3,9 +3,10 @@
 One step = one AnalysisRunner scan pass of the suite over the rank's row shard (49 ops: Size +
 {Completeness, Mean, Sum, Minimum, Maximum, StandardDeviation} over 8 columns: 4 fp64 + 4 int64,
 1 % nulls), the RCCL all-gather of the per-rank states (N > 1) and the rank-ordered
-semigroup fold of those states on the host. Rows are independent partitions (Spark partitions feeding one
-`data.agg`, R/AnalysisRunner.scala:313), so the default is weak scaling: every rank scans its own 1e9-row shard
-of one N x 1e9-row table and `value` counts the rows of all ranks (`--scaling strong` splits 1e9 rows instead).
+semigroup fold of those states on the host. BASELINE's configuration is one synthetic 1B-row table at 1/2/4/8 GPUs
+(Spark partitions of one table feeding one `data.agg`, R/AnalysisRunner.scala:313), so the default is strong
+scaling: the 1e9 rows are split into contiguous 2048-row-aligned shards over the N ranks and `value` = 1e9 rows /
+the max-over-ranks step time (`--scaling weak` gives every rank its own --rows-row shard of an N x --rows table).
 Inputs are generated in HBM by the counter-based splitmix64 generators before timing.
 
 `--gpus N` without a launcher starts N rank processes itself (spawn_ranks); under torch.distributed.run the
@@ -123,6 +124,19 @@ def timed(torch, dist, world, steps, warmup, stream, step):
     return elapsed, kernel_ms, res
 
 
+def shard_plan(rows, world, rank, scaling):
+    """(total rows of the job, first row of this rank's shard, rows of the shard): strong scaling splits `rows` over
+    the ranks, weak scaling gives every rank `rows` of a world x rows table; contiguous shards aligned to the
+    2048-row tile."""
+    if scaling == "weak":
+        return int(rows) * world, rank * int(rows), int(rows)
+    total = int(rows)
+    per = (total + world - 1) // world
+    per = (per + 2047) // 2048 * 2048
+    row0 = min(rank * per, total)
+    return total, row0, max(0, min(total, row0 + per) - row0)
+
+
 def build_shard(torch, N, ctx, row0, nrows, dev):
     from deequ_amd.table import Table, Column
     cols = []
@@ -145,10 +159,7 @@ def bench_c3(torch, N, D, ctx, stream, dev, total, steps, dist=None, world=1, ra
     contiguously over the ranks (2048-row aligned); per step the fused scan of the shard, the RCCL all-gather of the
     states and their rank-ordered fold (HLL registers max-merged, CorrelationState Chan-merged)."""
     from deequ_amd.table import Table, Column
-    per = (total + world - 1) // world
-    per = (per + 2047) // 2048 * 2048
-    row0 = min(rank * per, total)
-    nrows = max(0, min(total, row0 + per) - row0)
+    _, row0, nrows = shard_plan(total, world, rank, "strong")
     cols = []
     for name, kind, seed, vseed, st in (("k", N.SYNTH_KEY30, 0xC3000001, 0xC3000101, N.TYPE_LONG),
                                         ("x", N.SYNTH_GAUSS01, 0xC3000002, 0xC3000102, N.TYPE_DOUBLE),
@@ -248,10 +259,7 @@ def bench_c4_dist(torch, N, D, dev, total, steps, dist, world, rank):
     from deequ_amd.distributed import DistributedAnalysisRunner
     from deequ_amd.table import Table, Column
     distinct = total // 10
-    per = (total + world - 1) // world
-    per = (per + 2047) // 2048 * 2048
-    row0 = min(rank * per, total)
-    nrows = max(0, min(total, row0 + per) - row0)
+    _, row0, nrows = shard_plan(total, world, rank, "strong")
     ctx = engine.ctx()
     keys = torch.empty(max(nrows, 1), dtype=torch.int64, device=dev)
     ctx.synth_freq_keys(total, distinct, row0, nrows, keys.data_ptr())
@@ -298,17 +306,19 @@ C5_STRINGS = [("s_cat50", 101), ("s_bool", 102), ("s_cat100", 103), ("s_int", 10
               ("s_text0", 107), ("s_text1", 107), ("s_text2", 107), ("s_text3", 107)]
 
 
-def c5_shard(torch, N, ctx, dev, rows, chunk_rows=125_000_000):
+def c5_shard(torch, N, ctx, dev, rows, chunk_rows=125_000_000, only=None):
     """One GPU's shard of BASELINE config C5 generated in HBM: 5 fp64 + 5 int64 columns (the C2 generators) and 10
     UTF-8 string columns (3 low-cardinality, 3 numeric-looking, 4 free text 1-20 characters), 5 % nulls each. A
     shard above `chunk_rows` rows is held as row chunks (ChunkedTable): one string column's bytes of the 2.5e8-row
-    shard exceed its int32 Arrow offsets."""
+    shard exceed its int32 Arrow offsets. `only`: generate just these columns (same values and validity)."""
     from deequ_amd.table import ChunkedTable, Table, Column
     chunks, nbytes = [], 0
     for r0 in range(0, rows, chunk_rows):
         n = min(chunk_rows, rows - r0)
         cols = []
         for j, (name, kind) in enumerate(C5_NUMERIC):
+            if only is not None and name not in only:
+                continue
             dt = torch.float64 if kind in (1, 2, 3, 6, 7) else torch.int64
             v = torch.empty(n, dtype=dt, device=dev)
             ctx.synth_column(kind, 0xC5000000 + j, r0, n, v.data_ptr())
@@ -317,6 +327,8 @@ def c5_shard(torch, N, ctx, dev, rows, chunk_rows=125_000_000):
             cols.append(c)
             nbytes += 8 * n
         for j, (name, kind) in enumerate(C5_STRINGS):
+            if only is not None and name not in only:
+                continue
             off = torch.empty(n + 1, dtype=torch.int32, device=dev)
             total = ctx.synth_strings(kind, 0xC5100000 + j, r0, n, off.data_ptr())
             data = torch.zeros(total + 16, dtype=torch.uint8, device=dev)
@@ -325,9 +337,10 @@ def c5_shard(torch, N, ctx, dev, rows, chunk_rows=125_000_000):
             c.device = {"values": data, "offsets": off}
             cols.append(c)
             nbytes += total + 4 * n
-        for j, c in enumerate(cols):
+        index = {name: j for j, (name, _) in enumerate(C5_NUMERIC + C5_STRINGS)}
+        for c in cols:
             m = torch.zeros((n + 63) // 64 * 8, dtype=torch.uint8, device=dev)
-            ctx.synth_validity(0xC5200000 + j, r0, n, 50, m.data_ptr())
+            ctx.synth_validity(0xC5200000 + index[c.name], r0, n, 50, m.data_ptr())
             c.device["validity"] = m
             nbytes += n / 8
         chunks.append(Table(cols))
@@ -718,9 +731,11 @@ def launch_check(args, world, rank):
         dist.destroy_process_group()
     else:
         ranks_sum = 1
+    total, _, nrows = shard_plan(args.rows, world, rank, args.scaling)
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_sum": ranks_sum,
-                          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}), flush=True)
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "config": {"rows": total, "rows_per_gpu": nrows, "scaling": args.scaling}}), flush=True)
 
 
 def main():
@@ -735,9 +750,9 @@ def main():
     ap.add_argument("--no-secondary", action="store_true", help="only the headline C2 line")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL over xGMI) or gloo (rehearsal on one GPU)")
     ap.add_argument("--device-override", type=int, default=None, help="run every rank on this GPU (rehearsal)")
-    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                    help="weak: every rank scans its own --rows-row shard (rows are independent partitions, the only "
-                         "exchange is the all-gather of the fixed-size states); strong: --rows split over the ranks")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="strong",
+                    help="strong (default, BASELINE's 1B-row table at 1/2/4/8 GPUs): --rows split over the ranks; "
+                         "weak: every rank scans its own --rows-row shard of a world x --rows table")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -778,12 +793,7 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
-    total = int(args.rows) * (world if args.scaling == "weak" else 1)
-    # contiguous shards, aligned to the 2048-row tile
-    per = (total + world - 1) // world
-    per = (per + 2047) // 2048 * 2048
-    row0 = min(rank * per, total)
-    nrows = max(0, min(total, row0 + per) - row0)
+    total, row0, nrows = shard_plan(args.rows, world, rank, args.scaling)
     table = build_shard(torch, N, ctx, row0, nrows, dev)
     names = list(table.columns)
     bytes_per_row = sum(8 + 1.0 / 8 for _ in names)  # values + validity bit, per column
@@ -814,7 +824,7 @@ def main():
         "data": "synthetic (counter-based splitmix64 columns generated in HBM, SURVEY.md §8d)",
         "config": {"workload": "C2 fused scan suite: Size + {Completeness, Mean, Sum, Minimum, Maximum, "
                                "StandardDeviation} x 8 cols (4 fp64 + 4 int64, 1% nulls) = 49 ops",
-                   "rows": total, "rows_per_gpu": nrows, "columns": len(names), "ops": c2.nops,
+                   "rows": total, "rows_per_gpu": nrows, "scaling": args.scaling, "columns": len(names), "ops": c2.nops,
                    "parallelism": "rows sharded dp%d + %s all-gather of states"
                                   % (world, "RCCL" if args.dist_backend == "nccl" else args.dist_backend),
                    "dist_backend": args.dist_backend if world > 1 else None},

@@ -306,39 +306,89 @@ void* ctx_pinned_buf(dq_ctx* ctx, size_t bytes) {
 
 constexpr size_t kScratchCacheCap = size_t(48) << 30;  // idle bytes kept for re-use
 
-void scratch_trim(dq_ctx* ctx) {
-    if (ctx->scratch_free.empty()) return;
-    (void)hipSetDevice(ctx->device);
-    for (const dq_ctx::CachedBlock& b : ctx->scratch_free) {
-        (void)hipStreamSynchronize(b.stream);
+// Every open single-device context, so an allocation that fails can release the idle scratch of the device's
+// other contexts (helper contexts keep their caches between runs).
+std::mutex g_ctx_mu;
+std::vector<dq_ctx*> g_ctxs;
+
+void register_ctx(dq_ctx* ctx) {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    g_ctxs.push_back(ctx);
+}
+
+void unregister_ctx(dq_ctx* ctx) {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), ctx), g_ctxs.end());
+}
+
+void free_blocks(int device, const std::vector<dq_ctx::CachedBlock>& blocks) {
+    if (blocks.empty()) return;
+    (void)hipSetDevice(device);
+    for (const dq_ctx::CachedBlock& b : blocks) {
+        (void)hipStreamSynchronize(b.stream);  // its last use was queued there
         (void)hipFree(b.ptr);
     }
-    ctx->scratch_free.clear();
-    ctx->scratch_cached = 0;
+}
+
+// Take the cached blocks beyond keep_bytes (oldest first) out of the cache under its lock.
+std::vector<dq_ctx::CachedBlock> take_blocks(dq_ctx* ctx, size_t keep_bytes) {
+    std::vector<dq_ctx::CachedBlock> out;
+    std::lock_guard<std::mutex> g(ctx->scratch_mu);
+    size_t i = 0;
+    while (ctx->scratch_cached > keep_bytes && i < ctx->scratch_free.size()) {
+        out.push_back(ctx->scratch_free[i]);
+        ctx->scratch_cached -= ctx->scratch_free[i].bytes;
+        ++i;
+    }
+    ctx->scratch_free.erase(ctx->scratch_free.begin(), ctx->scratch_free.begin() + i);
+    return out;
+}
+
+void scratch_trim(dq_ctx* ctx, size_t keep_bytes) { free_blocks(ctx->device, take_blocks(ctx, keep_bytes)); }
+
+// Release the idle scratch of the device's other contexts (an allocation of `ctx` failed).
+void trim_device_peers(dq_ctx* ctx) {
+    std::vector<dq_ctx::CachedBlock> blocks;
+    {
+        std::lock_guard<std::mutex> g(g_ctx_mu);
+        for (dq_ctx* o : g_ctxs) {
+            if (o == ctx || o->device != ctx->device) continue;
+            std::vector<dq_ctx::CachedBlock> b = take_blocks(o, 0);
+            blocks.insert(blocks.end(), b.begin(), b.end());
+        }
+    }
+    free_blocks(ctx->device, blocks);
 }
 
 void* scratch_alloc(dq_ctx* ctx, size_t bytes) {
     bytes = std::max<size_t>(bytes, 256);
-    int best = -1;
-    for (int i = 0; i < (int)ctx->scratch_free.size(); ++i) {
-        const size_t b = ctx->scratch_free[i].bytes;
-        if (b >= bytes && b <= 2 * bytes && (best < 0 || b < ctx->scratch_free[best].bytes)) best = i;
-    }
-    if (best >= 0) {
-        dq_ctx::CachedBlock blk = ctx->scratch_free[best];
-        ctx->scratch_free.erase(ctx->scratch_free.begin() + best);
-        ctx->scratch_cached -= blk.bytes;
-        // last used on another stream (dq_set_stream since): that work must be done before this stream reuses it
-        if (blk.stream != ctx->stream && hipStreamSynchronize(blk.stream) != hipSuccess) {
-            (void)hipFree(blk.ptr);
-            return nullptr;
+    {
+        std::unique_lock<std::mutex> g(ctx->scratch_mu);
+        int best = -1;
+        for (int i = 0; i < (int)ctx->scratch_free.size(); ++i) {
+            const size_t b = ctx->scratch_free[i].bytes;
+            if (b >= bytes && b <= 2 * bytes && (best < 0 || b < ctx->scratch_free[best].bytes)) best = i;
         }
-        return blk.ptr;
+        if (best >= 0) {
+            dq_ctx::CachedBlock blk = ctx->scratch_free[best];
+            ctx->scratch_free.erase(ctx->scratch_free.begin() + best);
+            ctx->scratch_cached -= blk.bytes;
+            g.unlock();
+            // last used on another stream (dq_set_stream since): that work must be done before this stream reuses it
+            if (blk.stream != ctx->stream && hipStreamSynchronize(blk.stream) != hipSuccess) {
+                (void)hipFree(blk.ptr);
+                return nullptr;
+            }
+            return blk.ptr;
+        }
     }
     void* p = nullptr;
     if (hipMalloc(&p, bytes) == hipSuccess) return p;
     (void)hipGetLastError();
     scratch_trim(ctx);  // the cache may hold what this allocation needs
+    if (hipMalloc(&p, bytes) == hipSuccess) return p;
+    (void)hipGetLastError();
+    trim_device_peers(ctx);  // then the idle caches of the device's other contexts
     if (hipMalloc(&p, bytes) == hipSuccess) return p;
     (void)hipGetLastError();
     return nullptr;
@@ -347,16 +397,12 @@ void* scratch_alloc(dq_ctx* ctx, size_t bytes) {
 void scratch_release(dq_ctx* ctx, void* ptr, size_t bytes) {
     if (!ptr) return;
     bytes = std::max<size_t>(bytes, 256);
-    ctx->scratch_free.push_back(dq_ctx::CachedBlock{ptr, bytes, ctx->stream});
-    ctx->scratch_cached += bytes;
-    while (ctx->scratch_cached > kScratchCacheCap && !ctx->scratch_free.empty()) {
-        // release the oldest block (its stream's queued work first)
-        dq_ctx::CachedBlock b = ctx->scratch_free.front();
-        ctx->scratch_free.erase(ctx->scratch_free.begin());
-        ctx->scratch_cached -= b.bytes;
-        (void)hipStreamSynchronize(b.stream);
-        (void)hipFree(b.ptr);
+    {
+        std::lock_guard<std::mutex> g(ctx->scratch_mu);
+        ctx->scratch_free.push_back(dq_ctx::CachedBlock{ptr, bytes, ctx->stream});
+        ctx->scratch_cached += bytes;
     }
+    scratch_trim(ctx, kScratchCacheCap);  // beyond the cap: the oldest blocks (their stream's queued work first)
 }
 }  // namespace dq
 
@@ -389,6 +435,7 @@ dq_ctx* dq_open(int device, int* status) {
         return nullptr;
     }
     ctx->stream = ctx->own_stream;
+    register_ctx(ctx);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ctx->cus = prop.multiProcessorCount;
@@ -401,6 +448,7 @@ void dq_close(dq_ctx* ctx) {
     if (!ctx->subs.empty()) close_subs(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    unregister_ctx(ctx);
     scratch_trim(ctx);
     if (ctx->arena) (void)hipFree(ctx->arena);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -419,6 +467,12 @@ int dq_set_stream(dq_ctx* ctx, void* stream) {
     if (!ctx) return DQ_ERR_INVALID_ARGUMENT;
     ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
     return DQ_OK;
+}
+
+void dq_scratch_trim(dq_ctx* ctx, int64_t keep_bytes) {
+    if (!ctx) return;
+    for (dq_ctx* sub : ctx->subs) dq_scratch_trim(sub, keep_bytes);
+    scratch_trim(ctx, (size_t)std::max<int64_t>(keep_bytes, 0));
 }
 
 int dq_synchronize(dq_ctx* ctx) {

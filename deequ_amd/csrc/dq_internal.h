@@ -245,6 +245,7 @@ inline int rows_per_load_of(int e) {
 
 #ifdef __cplusplus
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 // The context behind the C-ABI. A single-device context owns one stream, a device arena and pinned staging;
@@ -279,8 +280,9 @@ struct dq_ctx {
         size_t bytes;
         hipStream_t stream;  // the stream of its last use
     };
-    std::vector<CachedBlock> scratch_free;
+    std::vector<CachedBlock> scratch_free;  // guarded by scratch_mu: a table may be freed from another thread
     size_t scratch_cached = 0;
+    std::mutex scratch_mu;
     // multi-device
     std::vector<dq_ctx*> subs;   // one per device (empty: single-device context)
     std::vector<int> devices;
@@ -295,7 +297,8 @@ namespace dq {
 void* scratch_alloc(dq_ctx* ctx, size_t bytes);
 // Hand a block back to the cache (its last use was queued on the ctx stream).
 void scratch_release(dq_ctx* ctx, void* ptr, size_t bytes);
-void scratch_trim(dq_ctx* ctx);
+// Release the cached blocks beyond keep_bytes (oldest first).
+void scratch_trim(dq_ctx* ctx, size_t keep_bytes = 0);
 
 // Context accessors for the .hip translation units (dq_api.cpp).
 hipStream_t ctx_stream(dq_ctx* ctx);

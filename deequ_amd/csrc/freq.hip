@@ -321,7 +321,7 @@ struct Counters {
     unsigned long long nulls;      // fast path + include_nulls: NULL rows
     unsigned long long overflow;   // probe limit hit: rebuild bigger
     unsigned long long mismatch;   // general path verification: fingerprint collisions
-    unsigned long long pad[3];
+    unsigned long long pad[3];     // [0] [1] fast path spill overflow; [2] general count pass: string keys > 15 bytes
     unsigned long long narrow_miss;  // fast path, narrow keys: 8-byte keys outside the 32-bit window
     unsigned long long spilled;      // fast path: keys past a full bucket, appended to the spill buffer
 };
@@ -430,7 +430,7 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
     for (int i = threadIdx.x; i < kSizingRegs; i += kFreqBlock) lds[i] = 0;
     for (int i = threadIdx.x; i < kDigitBins; i += kFreqBlock) dh[i] = 0;
     __syncthreads();
-    unsigned long long taken = 0, sent = 0, nulls = 0, kept = 0;
+    unsigned long long taken = 0, sent = 0, nulls = 0, kept = 0, longk = 0;
     constexpr int U = 4;  // rows in flight per lane
     // tiles of kPartTile rows interleaved over the workgroups (tile g, g + G, ...): all workgroups stream
     // through one narrow address window, as the partition scatter that replays the same tiles does
@@ -462,6 +462,7 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
                     short_key_tuple(ks, r, b0, b1);
                     tup[2 * r] = b0;
                     tup[2 * r + 1] = b1;
+                    longk += b1 == kTupleLong;
                 }
             }
 #pragma unroll
@@ -484,11 +485,13 @@ extract_count_kernel(KeySpec ks, int64_t nrows, unsigned long long* __restrict__
     sent = block_sum_u64(sent, red);
     nulls = block_sum_u64(nulls, red);
     kept = block_sum_u64(kept, red);
+    if (tup) longk = block_sum_u64(longk, red);
     if (threadIdx.x == 0) {
         block_keep[blockIdx.x] = kept;
         if (taken) atomicAdd(&ctr->num_rows, taken);
         if (sent) atomicAdd(&ctr->sentinel, sent);
         if (nulls) atomicAdd(&ctr->nulls, nulls);
+        if (longk) atomicAdd(&ctr->pad[2], longk);
     }
     // this workgroup's sizing registers, one byte each; sizing_reduce_kernel takes the max over workgroups
     // (a global atomicMax per register per workgroup contends on 4096 addresses)
@@ -2244,6 +2247,7 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
         }
         std::sort(split_buckets.begin(), split_buckets.end());
         split_buckets.erase(std::unique(split_buckets.begin(), split_buckets.end()), split_buckets.end());
+        if (!split_buckets.empty()) ctx->freq_paths[DQ_FREQ_PATH_SPLIT_BUCKETS]++;
         if (!split_buckets.empty() && !getenv("DQ_FREQ_SPLIT_SCAN")) {
             // the regions of split buckets (merged with atomics) scanned on their own, not the whole table
             unsigned int* dsb = nullptr;
@@ -2773,6 +2777,7 @@ int build_table(dq_ctx* ctx, dq_freq_table* t, int64_t nrows) {
         FQ_HIP(ctx, hipMemcpyAsync(hkeep.data(), bk, sizeof(unsigned long long) * xgrid, hipMemcpyDeviceToHost, s));
         FQ_HIP(ctx, hipMemcpyAsync(&t->host_ctr, t->ctr, sizeof(Counters), hipMemcpyDeviceToHost, s));
         FQ_HIP(ctx, hipStreamSynchronize(s));
+        if (tup && t->host_ctr.pad[2]) ctx->freq_paths[DQ_FREQ_PATH_LONG_TUPLES]++;
         unsigned long long n = 0;
         for (int g = 0; g < xgrid; ++g) {
             hoff[g] = n;
@@ -3884,7 +3889,9 @@ void dq_freq_free(dq_ctx* ctx, dq_freq_table* t) {
         return;
     }
     (void)hipSetDevice(t->device);
-    (void)hipDeviceSynchronize();
+    // every call on a table returns after its stream's work (or hands device pairs to the caller's stream order);
+    // the slots go back to the context's cache in its stream order
+    (void)hipStreamSynchronize(dq::ctx_stream(ctx));
     free_table_buffers(t, ctx);
     delete t;
 }

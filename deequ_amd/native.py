@@ -48,7 +48,8 @@ SYNTH_STR_CAT50, SYNTH_STR_BOOL, SYNTH_STR_CAT100, SYNTH_STR_INT, SYNTH_STR_DEC,
 HLL_NUM_WORDS = 52
 
 # dq_scan_kernel, in enum order
-FREQ_PATHS = ("fast", "fast_narrow", "fast_done", "exact", "partitioned", "sorted", "small", "small_optimistic", "fast_spill")
+FREQ_PATHS = ("fast", "fast_narrow", "fast_done", "exact", "partitioned", "sorted", "small", "small_optimistic", "fast_spill",
+              "split_buckets", "long_tuples")
 SCAN_KERNELS = ("striped", "striped_heavy", "heavy8", "heavy8_full", "bits", "pred_simple", "pred_vm", "regex",
                 "strings", "where_fused", "where_masks")
 
@@ -61,7 +62,7 @@ EXPORTED_SYMBOLS = (
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts", "dq_synth_strings",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
     "dq_scan_streamed", "dq_scan_kernel_launches", "dq_freq_path_count", "dq_kll_sketch_columns",
-    "dq_kll_merge_states",
+    "dq_kll_merge_states", "dq_scratch_trim",
 )
 
 
@@ -201,6 +202,7 @@ def load_library(path=None):
             "dq_last_error": (ctypes.c_char_p, [c_void_p]),
             "dq_set_stream": (c_int, [c_void_p, c_void_p]),
             "dq_synchronize": (c_int, [c_void_p]),
+            "dq_scratch_trim": (None, [c_void_p, c_int64]),
             "dq_scan": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                 c_uint32]),
             "dq_scan_launch_count": (c_int64, [c_void_p]),
@@ -485,13 +487,14 @@ class Context:
                                             ctypes.c_void_p(values_dev_ptr), ctypes.c_void_p(validity_dev_ptr)),
                    "dq_cast_column")
 
-    @staticmethod
-    def _after_torch_stream():
+    def _after_torch_stream(self):
         """The generators run on the context's stream; a buffer torch just allocated and filled (torch.zeros) on its
-        own stream must be complete before they write into it."""
+        own stream must be complete before they write into it. The stream is this thread's current stream of the
+        context's device (explicitly: a helper thread starts on device 0)."""
         torch = sys.modules.get("torch")
         if torch is not None and torch.cuda.is_initialized():
-            torch.cuda.current_stream().synchronize()
+            for d in self.devices:
+                torch.cuda.current_stream(int(d)).synchronize()
 
     def synth_column(self, kind, seed, row0, nrows, dev_ptr):
         self._after_torch_stream()
@@ -520,17 +523,53 @@ class Context:
 
 
 _contexts = {}
+_aux_lock = threading.Lock()
+_aux_pool = {}     # (device, slot) -> [Context, ...]
+_aux_leased = set()  # id() of the aux contexts a helper thread drives right now
+
+
+def lease_aux_context(device=0, slot="aux"):
+    """A single-device context of `device` (its own stream and scratch cache) for one helper thread: the cached
+    context of `slot` unless another thread holds it (dq.h: calls on one ctx are not re-entrant), else another one of
+    the slot's pool. Return it with release_aux_context. Helper work overlaps the main context's (the
+    ColumnProfiler's histogram pass beside its numeric pass, a run's grouping builds beside its scans)."""
+    key = (int(device), slot)
+    with _aux_lock:
+        pool = _aux_pool.setdefault(key, [])
+        for ctx in pool:
+            if id(ctx) not in _aux_leased:
+                _aux_leased.add(id(ctx))
+                return ctx
+    ctx = Context(device)  # outside the lock: dq_open may take a while
+    with _aux_lock:
+        _aux_pool[key].append(ctx)
+        _aux_leased.add(id(ctx))
+    return ctx
+
+
+def release_aux_context(ctx):
+    """The helper is done with `ctx`: its cached scratch beyond the idle cap is released and the context may be leased
+    again."""
+    try:
+        ctx.lib.dq_scratch_trim(ctx.handle, AUX_IDLE_SCRATCH_BYTES)
+    finally:
+        with _aux_lock:
+            _aux_leased.discard(id(ctx))
+
+
+AUX_IDLE_SCRATCH_BYTES = 16 << 30  # idle device scratch an aux context keeps between runs
 
 
 def aux_context(device=0, slot="aux"):
-    """Another cached single-device context of `device` (its own stream and scratch cache), one per `slot`: work a
-    helper thread overlaps with the main context's (the ColumnProfiler's histogram pass beside its numeric pass, a
-    run's grouping builds beside its scans)."""
-    key = ("aux", device, slot)
-    ctx = _contexts.get(key)
-    if ctx is None:
-        ctx = Context(device)
-        _contexts[key] = ctx
+    """The cached context of `slot` (see lease_aux_context) without a lease: single-threaded callers only."""
+    key = (int(device), slot)
+    with _aux_lock:
+        pool = _aux_pool.setdefault(key, [])
+        if pool:
+            return pool[0]
+    ctx = Context(device)
+    with _aux_lock:
+        _aux_pool[key].append(ctx)
     return ctx
 
 

@@ -220,32 +220,36 @@ class ColumnProfiler:
         if targets and type(passes) is LocalPasses and not os.environ.get("DQ_PROFILE_SERIAL"):
             pending = _histograms_beside(passes, data, targets)  # None: the passes stay on this thread
 
-        # ---- pass 2 ------------------------------------------------------------------------------
-        if printStatusUpdates:
-            print("### PROFILING: Computing numeric column statistics in pass (2/3)...")
-        numeric = [n for n in relevant
-                   if generic.typeOf(n) in (DataTypeInstances.Integral, DataTypeInstances.Fractional)]
-        casts = {name: N.TYPE_LONG if generic.typeOf(name) == DataTypeInstances.Integral else N.TYPE_DOUBLE
-                 for name in numeric}
-        casted = _cast_table(passes, data, casts)
-        second = []
-        early_set = set(early)
-        for name in numeric:
-            if name not in early_set:
-                second += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
-            second += [KLLSketch(name, kllParameters)]
-        res2 = passes.run(casted, second) if second else None
-        if early and res2 is not None:
-            res2 = res1 + res2
-        stats = ColumnProfiler._extract_numeric(res2, numeric, kllParameters)
+        try:
+            # ---- pass 2 ------------------------------------------------------------------------------
+            if printStatusUpdates:
+                print("### PROFILING: Computing numeric column statistics in pass (2/3)...")
+            numeric = [n for n in relevant
+                       if generic.typeOf(n) in (DataTypeInstances.Integral, DataTypeInstances.Fractional)]
+            casts = {name: N.TYPE_LONG if generic.typeOf(name) == DataTypeInstances.Integral else N.TYPE_DOUBLE
+                     for name in numeric}
+            casted = _cast_table(passes, data, casts)
+            second = []
+            early_set = set(early)
+            for name in numeric:
+                if name not in early_set:
+                    second += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
+                second += [KLLSketch(name, kllParameters)]
+            res2 = passes.run(casted, second) if second else None
+            if early and res2 is not None:
+                res2 = res1 + res2
+            stats = ColumnProfiler._extract_numeric(res2, numeric, kllParameters)
 
-        # ---- pass 3 ------------------------------------------------------------------------------
-        if printStatusUpdates:
-            print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3)...")
-        if pending is not None:
-            histograms = pending.result()
-        else:
-            histograms = passes.histograms(data, targets) if targets else {}
+            # ---- pass 3 ------------------------------------------------------------------------------
+            if printStatusUpdates:
+                print("### PROFILING: Computing histograms of low-cardinality columns in pass (3/3)...")
+            if pending is not None:
+                histograms = pending.result()
+            else:
+                histograms = passes.histograms(data, targets) if targets else {}
+        finally:  # a failing pass 2 does not leave the histogram helper driving its context
+            if pending is not None:
+                pending.join()
 
         profiles = {}
         for name in relevant:

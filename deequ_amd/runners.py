@@ -4,6 +4,7 @@ driving the MI355X engine. The scan-shareable analyzers of a run become ONE dq_s
 pass over HBM), exactly where the reference issues one `data.agg(...)` Spark job."""
 import json
 import os
+import sys
 import threading
 
 from . import native as N
@@ -27,9 +28,9 @@ def stream_chunk_rows():
 class _Pending:
     """A helper thread's result (its exception re-raised by result())."""
 
-    def __init__(self, fn):
+    def __init__(self, fn, name="dq-helper"):
         self.value, self.error = None, None
-        self.thread = threading.Thread(target=self._run, args=(fn,), daemon=True)
+        self.thread = threading.Thread(target=self._run, args=(fn,), daemon=True, name=name)
         self.thread.start()
 
     def _run(self, fn):
@@ -37,6 +38,9 @@ class _Pending:
             self.value = fn()
         except BaseException as e:  # handed to the caller
             self.error = e
+
+    def join(self):
+        self.thread.join()
 
     def result(self):
         self.thread.join()
@@ -46,16 +50,51 @@ class _Pending:
 
 
 def _beside(fn, slot):
-    """Run fn in a helper thread on a second context of this thread's device (own stream and scratch), or None when
-    the work must stay on this thread (DQ_RUN_SERIAL, a multi-device context, or already on a helper context)."""
+    """Run fn in a helper thread on a second context of this thread's device (own stream and scratch, leased to this
+    helper alone), or None when the work must stay on this thread (DQ_RUN_SERIAL, a multi-device context, or already
+    on a helper context). The helper selects the device before any engine call (a new thread starts on device 0)."""
     if os.environ.get("DQ_RUN_SERIAL") or os.environ.get("DQ_DEVICES") or getattr(engine._local, "ctx", None):
         return None
-    aux = N.aux_context(engine.device(), slot)
+    dev = engine.device()
+    aux = N.lease_aux_context(dev, slot)
 
     def run():
-        with engine.using_context(aux):
-            return fn()
-    return _Pending(run)
+        try:
+            torch = sys.modules.get("torch")
+            if torch is not None and torch.cuda.is_initialized():
+                torch.cuda.set_device(dev)
+            with engine.using_context(aux):
+                return fn()
+        finally:
+            N.release_aux_context(aux)
+    try:
+        return _Pending(run, "dq-helper-" + slot)
+    except BaseException:
+        N.release_aux_context(aux)
+        raise
+
+
+class _Helpers:
+    """The helper threads of one run: every one is joined before the run returns or raises (an exception on this
+    thread or in one helper never leaves another helper driving its context over buffers the caller may free); the
+    first error re-raised is the first one result() meets."""
+
+    def __init__(self):
+        self.pending = []
+
+    def beside(self, fn, slot):
+        h = _beside(fn, slot)
+        if h is not None:
+            self.pending.append(h)
+        return h
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        for h in self.pending:
+            h.join()
+        return False
 
 
 class ScanResult(list):
@@ -353,21 +392,23 @@ class AnalysisRunner:
         # each set's build runs on its own helper context meanwhile (Spark runs them as separate jobs; at most three
         # helpers, the rest -- or the last set when nothing else runs -- on this thread)
         others = bool(scanning or kllAnalyzers)
-        helpers, here = [], []
-        for k, (cols, group) in enumerate(sets):
-            h = None
-            if k < 3 and (others or k < len(sets) - 1):
-                h = _beside(lambda cols=cols, group=group: run_set(cols, group), "group%d" % k)
-            (here.append((cols, group)) if h is None else helpers.append(h))
-        kllMetrics = AnalyzerContext.empty()
-        if kllAnalyzers:
-            kllMetrics = KLLRunner.computeKLLSketchesInExtraPass(data, kllAnalyzers, aggregateWith, saveStatesWith)
-        nonGrouped = AnalysisRunner._runScanningAnalyzers(data, scanning, aggregateWith, saveStatesWith)
-        grouped = AnalyzerContext.empty()
-        for cols, group in here:
-            grouped = grouped + run_set(cols, group)
-        for h in helpers:
-            grouped = grouped + h.result()
+        with _Helpers() as helpers:
+            here = []
+            for k, (cols, group) in enumerate(sets):
+                h = None
+                if k < 3 and (others or k < len(sets) - 1):
+                    h = helpers.beside(lambda cols=cols, group=group: run_set(cols, group), "group%d" % k)
+                if h is None:
+                    here.append((cols, group))
+            kllMetrics = AnalyzerContext.empty()
+            if kllAnalyzers:
+                kllMetrics = KLLRunner.computeKLLSketchesInExtraPass(data, kllAnalyzers, aggregateWith, saveStatesWith)
+            nonGrouped = AnalysisRunner._runScanningAnalyzers(data, scanning, aggregateWith, saveStatesWith)
+            grouped = AnalyzerContext.empty()
+            for cols, group in here:
+                grouped = grouped + run_set(cols, group)
+            for h in helpers.pending:
+                grouped = grouped + h.result()
         return preconditionFailures + nonGrouped + grouped + kllMetrics
 
     @staticmethod
@@ -380,13 +421,20 @@ class AnalysisRunner:
         chunk) does not reach the merge (the reference's findStateForParticularGrouping would require one): it keeps
         the chunk failure metrics."""
         analyzers = list(dict.fromkeys(analyzers))  # one state per analyzer: the merge adds each loader's state once
+        with _Helpers() as helpers:
+            return AnalysisRunner._run_chunked_body(data, analyzers, aggregateWith, saveStatesWith, helpers)
+
+    @staticmethod
+    def _run_chunked_body(data, analyzers, aggregateWith, saveStatesWith, helpers):
         # grouping analyzers: one frequency table over the whole shard (the chunks' key columns concatenated where
         # they live, int64 string offsets) instead of per-chunk tables merged through host memory -- the same
-        # groups as Spark's shuffle of the partitions' partial counts (R/AnalysisRunner.scala:259-287)
+        # groups as Spark's shuffle of the partitions' partial counts (R/AnalysisRunner.scala:259-287). A
+        # multi-device context (DQ_DEVICES) shards every call itself and takes neither int64 offsets nor parted
+        # columns: its chunks run one by one and merge like any other state.
+        whole_table = len(data.chunks) > 1 and not getattr(engine.ctx(), "multi", False)
         grouping = [a for a in analyzers if isinstance(a, GroupingAnalyzer)]
         whole = AnalyzerContext.empty()
-        grouping_pending = []
-        if grouping and len(data.chunks) > 1:
+        if grouping and whole_table:
             analyzers = [a for a in analyzers if not isinstance(a, GroupingAnalyzer)]
             by_set = {}
             for a in grouping:
@@ -399,27 +447,27 @@ class AnalysisRunner:
                     cols = [c for c in cset if c in data]
                     return AnalysisRunner.doAnalysisRun(data.concat(cols), group, aggregateWith, saveStatesWith)
                 last_here = not analyzers and k == len(sets) - 1
-                h = None if last_here or k >= 3 else _beside(run_set, "group%d" % k)
+                h = None if last_here or k >= 3 else helpers.beside(run_set, "group%d" % k)
                 if h is None:
                     whole = whole + run_set()
-                else:
-                    grouping_pending.append(h)
             if not analyzers:
-                for h in grouping_pending:
+                for h in helpers.pending:
                     whole = whole + h.result()
                 return whole
         # ApproxQuantile(s): one summary per column over every chunk (dq_quantile_summaries reads the chunks as
         # parts), the exact order statistics of the shard -- a GK summary inside the same rank bound as the merge of
         # per-partition digests (QuantileSummaries.merge)
         quant = [a for a in analyzers if isinstance(a, (ApproxQuantile, ApproxQuantiles))]
-        if quant and len(data.chunks) > 1:
+        if quant and whole_table:
             cols = sorted({a.column for a in quant if a.column in data})
             whole = whole + AnalysisRunner.doAnalysisRun(data.parted(cols), quant, aggregateWith, saveStatesWith)
             analyzers = [a for a in analyzers if not isinstance(a, (ApproxQuantile, ApproxQuantiles))]
             if not analyzers:
-                for h in grouping_pending:
+                for h in helpers.pending:
                     whole = whole + h.result()
                 return whole
+        grouping_pending = list(helpers.pending)
+
         def run_chunks(indices):
             out = {}
             for i in indices:
@@ -431,7 +479,7 @@ class AnalysisRunner:
         # while this thread runs the even ones, so one chunk's host work (KLL schedules, state extraction) overlaps
         # the other's kernels
         nchunks = len(data.chunks)
-        odd = _beside(lambda: run_chunks(range(1, nchunks, 2)), "chunk") if nchunks > 1 else None
+        odd = helpers.beside(lambda: run_chunks(range(1, nchunks, 2)), "chunk") if nchunks > 1 else None
         done = run_chunks(range(0, nchunks, 2) if odd is not None else range(nchunks))
         if odd is not None:
             done.update(odd.result())

@@ -515,10 +515,11 @@ class ChunkedTable:
         is one frequency table (not per-chunk tables merged through host memory)."""
         on_device = all(all(c[n].device is not None for n in names) for c in self.chunks)
         cols = [(_concat_device if on_device else _concat_host)([c[n] for c in self.chunks]) for n in names]
-        if on_device:
+        if on_device and cols:
             import torch
-            # the copies run on torch's stream, the builds that read them on the context's own stream
-            torch.cuda.current_stream().synchronize()
+            # the copies run on this thread's torch stream of the columns' device, the builds that read them on the
+            # context's own stream
+            torch.cuda.current_stream(cols[0].device["values"].device).synchronize()
         return Table(cols)
 
     def parted(self, names):

@@ -256,6 +256,13 @@ int dq_scan_sharded(dq_ctx* ctx, const dq_column* const* shard_columns, const in
 int dq_set_stream(dq_ctx* ctx, void* stream);
 int dq_synchronize(dq_ctx* ctx);
 
+/* Release the context's idle cached device scratch (the grouping builds' partition buffers and tables) beyond
+ * keep_bytes, oldest first; 0 releases all of it. A context's scratch cache is locked, so this may be called from
+ * any thread (a second context of the device that has finished its helper work). When an allocation fails, a
+ * context also releases the idle scratch of every other context of its device before it gives up. No reference
+ * counterpart: Spark's executors own their memory (host-side bookkeeping of this engine). */
+void dq_scratch_trim(dq_ctx* ctx, int64_t keep_bytes);
+
 /* The fused scan: replaces runScanningAnalyzers (R/AnalysisRunner.scala:289-336), i.e. the single
  * `data.agg(...).collect()` of all ScanShareableAnalyzer.aggregationFunctions() (:306-313) plus
  * fromAggregationResult (A/Analyzer.scala:172-175). Every column is read once from HBM.
@@ -305,7 +312,10 @@ typedef enum dq_freq_path {
     DQ_FREQ_PATH_SMALL = 6,             /* one-pass small builds launched (sized or optimistic)                */
     DQ_FREQ_PATH_SMALL_OPTIMISTIC = 7,  /* optimistic small builds (no sizing pass) that produced their table  */
     DQ_FREQ_PATH_FAST_SPILL = 8,        /* fast builds whose full buckets spilled keys (inserted after the build) */
-    DQ_FREQ_PATH_COUNT = 9
+    DQ_FREQ_PATH_SPLIT_BUCKETS = 9,     /* builds with buckets split over several work items (atomic merge)    */
+    DQ_FREQ_PATH_LONG_TUPLES = 10,      /* general builds of one string key column with keys past 15 bytes     */
+                                        /* (two-word tuples for the short keys, byte compares for the rest)    */
+    DQ_FREQ_PATH_COUNT = 11
 } dq_freq_path;
 int64_t dq_freq_path_count(const dq_ctx* ctx, int32_t path);
 

@@ -25,6 +25,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <omp.h>
 
 #include "hll_bias_p9.h"
 
@@ -941,4 +942,227 @@ int64_t oracle_group_counts(int spark_type, const void* values, const uint8_t* v
         i = j;
     }
     return g;
+}
+
+/* count(*) GROUP BY one UTF-8 string key column given as row-range parts (the row chunks of a ChunkedTable, each with
+ * its own int32 Arrow offsets, bytes and LSB-first validity bitmap), the grouping step of
+ * FrequencyBasedAnalyzer.computeFrequencies (A/GroupingAnalyzers.scala:53-79) for a string key: groups are equal
+ * BYTE STRINGS. No fingerprint decides equality: every key of <= 23 bytes is packed with its length into a 24-byte
+ * record, the records are distributed over 65536 buckets (a hash of the record picks the bucket -- placement only),
+ * each bucket is sorted (qsort over the three words) and run-length counted. A key longer than 23 bytes makes the
+ * call return -2 (the C5 text columns hold 1-20 bytes).
+ * Out: *valid_rows / *null_rows; the distinct group counts cc_vals[0..*ncc) with their multiplicities cc_mult (the
+ * "counts of counts": num_groups = sum(cc_mult), unique = cc_mult at 1, the entropy terms per distinct count); for
+ * each of the nq query keys (int64 offsets into q_bytes) its exact count (0 when absent) in q_counts. Returns the
+ * number of groups, -1 on allocation failure, -2 on a key past 23 bytes, -3 when *ncc is too small. */
+typedef struct { uint64_t w[3]; } skey_t;
+
+static int skey_cmp(const void* a, const void* b) {
+    const skey_t* x = (const skey_t*)a;
+    const skey_t* y = (const skey_t*)b;
+    for (int i = 0; i < 3; ++i)
+        if (x->w[i] != y->w[i]) return x->w[i] < y->w[i] ? -1 : 1;
+    return 0;
+}
+
+static int skey_pack(const uint8_t* p, int64_t len, skey_t* k) {
+    if (len < 0 || len > 23) return 0;
+    uint8_t b[24];
+    memset(b, 0, sizeof(b));
+    memcpy(b, p, (size_t)len);
+    b[23] = (uint8_t)len;
+    memcpy(k->w, b, 24);
+    return 1;
+}
+
+static uint32_t skey_bucket(const skey_t* k) {
+    uint64_t h = k->w[0] * 0x9E3779B97F4A7C15ULL ^ k->w[1] * 0xC2B2AE3D27D4EB4FULL ^ k->w[2] * 0x165667B19E3779F9ULL;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ULL;
+    h ^= h >> 29;
+    return (uint32_t)(h >> 48);
+}
+
+int64_t oracle_group_strings(int nparts, const uint8_t* const* bytes, const int32_t* const* offsets,
+                             const uint8_t* const* valid, const int64_t* rows, int64_t* valid_rows, int64_t* null_rows,
+                             int64_t* cc_vals, int64_t* cc_mult, int64_t* ncc, const uint8_t* q_bytes,
+                             const int64_t* q_offsets, int64_t nq, int64_t* q_counts) {
+    enum { NB = 65536, SMALL = 4096 };
+    int64_t n = 0;
+    for (int p = 0; p < nparts; ++p) n += rows[p];
+    uint16_t* bk = (uint16_t*)malloc((size_t)(n ? n : 1) * sizeof(uint16_t));
+    int nt = 1;
+#pragma omp parallel
+#pragma omp single
+    nt = omp_get_num_threads();
+    int64_t* th_hist = (int64_t*)calloc((size_t)nt * NB, sizeof(int64_t));
+    int64_t* bstart = (int64_t*)malloc((NB + 1) * sizeof(int64_t));
+    int64_t* th_nulls = (int64_t*)calloc((size_t)nt, sizeof(int64_t));
+    int bad = 0;
+    if (!bk || !th_hist || !bstart || !th_nulls) {
+        free(bk); free(th_hist); free(bstart); free(th_nulls);
+        return -1;
+    }
+    /* pass A: each row's bucket (0xFFFF + NULL flag kept apart: a NULL row is marked by its validity bit) */
+#pragma omp parallel num_threads(nt) reduction(| : bad)
+    {
+        const int t = omp_get_thread_num();
+        int64_t* hist = th_hist + (size_t)t * NB;
+        int64_t base = 0;
+        for (int p = 0; p < nparts; ++p) {
+            const int64_t lo = rows[p] * t / nt, hi = rows[p] * (t + 1) / nt;
+            for (int64_t i = lo; i < hi; ++i) {
+                if (valid[p] && !((valid[p][i >> 3] >> (i & 7)) & 1)) {
+                    th_nulls[t]++;
+                    continue;
+                }
+                skey_t k;
+                if (!skey_pack(bytes[p] + offsets[p][i], (int64_t)offsets[p][i + 1] - offsets[p][i], &k)) {
+                    bad = 1;
+                    continue;
+                }
+                const uint32_t b = skey_bucket(&k);
+                bk[base + i] = (uint16_t)b;
+                hist[b]++;
+            }
+            base += rows[p];
+        }
+    }
+    if (bad) {
+        free(bk); free(th_hist); free(bstart); free(th_nulls);
+        return -2;
+    }
+    int64_t nulls = 0;
+    for (int t = 0; t < nt; ++t) nulls += th_nulls[t];
+    const int64_t m = n - nulls;
+    /* bucket starts, and each thread's write cursor per bucket (thread order inside a bucket) */
+    int64_t at = 0;
+    for (int b = 0; b < NB; ++b) {
+        bstart[b] = at;
+        for (int t = 0; t < nt; ++t) {
+            const int64_t c = th_hist[(size_t)t * NB + b];
+            th_hist[(size_t)t * NB + b] = at;
+            at += c;
+        }
+    }
+    bstart[NB] = at;
+    skey_t* rec = (skey_t*)malloc((size_t)(m ? m : 1) * sizeof(skey_t));
+    if (!rec) {
+        free(bk); free(th_hist); free(bstart); free(th_nulls);
+        return -1;
+    }
+    /* pass B: the records into their buckets */
+#pragma omp parallel num_threads(nt)
+    {
+        const int t = omp_get_thread_num();
+        int64_t* cur = th_hist + (size_t)t * NB;
+        int64_t base = 0;
+        for (int p = 0; p < nparts; ++p) {
+            const int64_t lo = rows[p] * t / nt, hi = rows[p] * (t + 1) / nt;
+            for (int64_t i = lo; i < hi; ++i) {
+                if (valid[p] && !((valid[p][i >> 3] >> (i & 7)) & 1)) continue;
+                skey_t k;
+                skey_pack(bytes[p] + offsets[p][i], (int64_t)offsets[p][i + 1] - offsets[p][i], &k);
+                rec[cur[bk[base + i]]++] = k;
+            }
+            base += rows[p];
+        }
+    }
+    free(bk);
+    /* sort every bucket, run-length count, counts of counts per thread (small counts in an array, the rest listed) */
+    int64_t* small = (int64_t*)calloc((size_t)nt * SMALL, sizeof(int64_t));
+    int64_t** big = (int64_t**)calloc((size_t)nt, sizeof(int64_t*));
+    int64_t* nbig = (int64_t*)calloc((size_t)nt, sizeof(int64_t));
+    int64_t* capbig = (int64_t*)calloc((size_t)nt, sizeof(int64_t));
+    int64_t groups = 0;
+    int oom = 0;
+#pragma omp parallel num_threads(nt) reduction(+ : groups) reduction(| : oom)
+    {
+        const int t = omp_get_thread_num();
+        int64_t* sm = small + (size_t)t * SMALL;
+#pragma omp for schedule(dynamic, 64)
+        for (int b = 0; b < NB; ++b) {
+            skey_t* r = rec + bstart[b];
+            const int64_t c = bstart[b + 1] - bstart[b];
+            int64_t same = 1;
+            while (same < c && skey_cmp(&r[same], &r[0]) == 0) ++same;
+            if (same < c) qsort(r, (size_t)c, sizeof(skey_t), skey_cmp);
+            for (int64_t i = 0; i < c;) {
+                int64_t j = i + 1;
+                while (j < c && skey_cmp(&r[j], &r[i]) == 0) ++j;
+                const int64_t cnt = j - i;
+                ++groups;
+                if (cnt < SMALL) {
+                    sm[cnt]++;
+                } else {
+                    if (nbig[t] == capbig[t]) {
+                        capbig[t] = capbig[t] ? 2 * capbig[t] : 64;
+                        int64_t* nb = (int64_t*)realloc(big[t], (size_t)capbig[t] * sizeof(int64_t));
+                        if (!nb) { oom = 1; break; }
+                        big[t] = nb;
+                    }
+                    big[t][nbig[t]++] = cnt;
+                }
+                i = j;
+            }
+        }
+    }
+    int64_t rc = oom ? -1 : groups;
+    if (!oom) {
+        /* counts of counts: merge the threads' small arrays, sort the big counts */
+        int64_t k = 0;
+        for (int64_t c = 1; c < SMALL && rc >= 0; ++c) {
+            int64_t mult = 0;
+            for (int t = 0; t < nt; ++t) mult += small[(size_t)t * SMALL + c];
+            if (!mult) continue;
+            if (k >= *ncc) { rc = -3; break; }
+            cc_vals[k] = c;
+            cc_mult[k++] = mult;
+        }
+        int64_t tot = 0;
+        for (int t = 0; t < nt; ++t) tot += nbig[t];
+        int64_t* all = (int64_t*)malloc((size_t)(tot ? tot : 1) * sizeof(int64_t));
+        if (!all) rc = -1;
+        if (rc >= 0) {
+            int64_t a = 0;
+            for (int t = 0; t < nt; ++t) for (int64_t i = 0; i < nbig[t]; ++i) all[a++] = big[t][i];
+            for (int64_t i = 1; i < tot; ++i) {  /* insertion sort: few large counts */
+                const int64_t v = all[i];
+                int64_t j = i - 1;
+                while (j >= 0 && all[j] > v) { all[j + 1] = all[j]; --j; }
+                all[j + 1] = v;
+            }
+            for (int64_t i = 0; i < tot && rc >= 0;) {
+                int64_t j = i + 1;
+                while (j < tot && all[j] == all[i]) ++j;
+                if (k >= *ncc) { rc = -3; break; }
+                cc_vals[k] = all[i];
+                cc_mult[k++] = j - i;
+                i = j;
+            }
+        }
+        free(all);
+        *ncc = k;
+    }
+    /* the query keys: binary search in their bucket */
+    for (int64_t q = 0; q < nq && rc >= 0; ++q) {
+        skey_t k;
+        q_counts[q] = 0;
+        if (!skey_pack(q_bytes + q_offsets[q], q_offsets[q + 1] - q_offsets[q], &k)) continue;
+        const uint32_t b = skey_bucket(&k);
+        const skey_t* r = rec + bstart[b];
+        int64_t lo = 0, hi = bstart[b + 1] - bstart[b];
+        while (lo < hi) {  /* first record >= k */
+            const int64_t mid = (lo + hi) / 2;
+            if (skey_cmp(&r[mid], &k) < 0) lo = mid + 1; else hi = mid;
+        }
+        int64_t j = lo;
+        while (j < bstart[b + 1] - bstart[b] && skey_cmp(&r[j], &k) == 0) ++j;
+        q_counts[q] = j - lo;
+    }
+    *valid_rows = m;
+    *null_rows = nulls;
+    for (int t = 0; t < nt; ++t) free(big[t]);
+    free(big); free(nbig); free(capbig); free(small); free(rec); free(th_hist); free(bstart); free(th_nulls);
+    return rc;
 }

@@ -130,6 +130,63 @@ def group_counts_raw(spark_type, values, validity, nrows):
     return keys[:g].view(np.uint64).copy(), counts[:g].copy(), int(nulls.value)
 
 
+def group_strings_raw(parts, queries=()):
+    """count(*) GROUP BY one UTF-8 string key column over row-range parts [(bytes uint8, int32 offsets, LSB-first
+    validity or None, rows), ...] in C (oracle_group_strings: keys <= 23 bytes packed with their length into 24-byte
+    records, bucketed, sorted and run-length counted -- equal groups are equal byte strings, no fingerprint;
+    A/GroupingAnalyzers.scala:53-79). Returns {"valid_rows", "null_rows", "num_groups", "count_values",
+    "count_groups" (the distinct group counts and how many groups have each), "query_counts" (the exact count of each
+    query string, 0 when absent)}."""
+    L = lib()
+    fn = L.oracle_group_strings
+    fn.restype = ctypes.c_int64
+    P = ctypes.c_void_p
+    fn.argtypes = [ctypes.c_int, P, P, P, P, P, P, P, P, P, P, P, ctypes.c_int64, P]
+    keep = []
+    np_parts = []
+    for b, o, v, n in parts:
+        b = np.ascontiguousarray(b, dtype=np.uint8)
+        o = np.ascontiguousarray(o, dtype=np.int32)
+        v = None if v is None else np.ascontiguousarray(v, dtype=np.uint8)
+        np_parts.append((b, o, v, int(n)))
+        keep += [b, o, v]
+    k = len(np_parts)
+    bp = (ctypes.c_void_p * k)(*[p[0].ctypes.data for p in np_parts])
+    op = (ctypes.c_void_p * k)(*[p[1].ctypes.data for p in np_parts])
+    vp = (ctypes.c_void_p * k)(*[None if p[2] is None else p[2].ctypes.data for p in np_parts])
+    rows = np.array([p[3] for p in np_parts], dtype=np.int64)
+    enc = [q.encode("utf-8") for q in queries]
+    qb = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8).copy()
+    qo = np.zeros(len(enc) + 1, dtype=np.int64)
+    qo[1:] = np.cumsum([len(e) for e in enc]) if enc else []
+    qc = np.zeros(max(len(enc), 1), dtype=np.int64)
+    cap = 1 << 20
+    cv = np.zeros(cap, dtype=np.int64)
+    cm = np.zeros(cap, dtype=np.int64)
+    ncc = ctypes.c_int64(cap)
+    vr, nr = ctypes.c_int64(0), ctypes.c_int64(0)
+    g = fn(k, ctypes.cast(bp, P), ctypes.cast(op, P), ctypes.cast(vp, P), rows.ctypes.data, ctypes.addressof(vr),
+           ctypes.addressof(nr), cv.ctypes.data, cm.ctypes.data, ctypes.addressof(ncc), qb.ctypes.data, qo.ctypes.data,
+           len(enc), qc.ctypes.data)
+    if g < 0:
+        raise ValueError("oracle_group_strings failed (%d)" % g)
+    m = ncc.value
+    return {"valid_rows": vr.value, "null_rows": nr.value, "num_groups": int(g), "count_values": cv[:m].copy(),
+            "count_groups": cm[:m].copy(), "query_counts": qc[:len(enc)].copy()}
+
+
+def group_summary_from_count_groups(values, mult, num_rows):
+    """group_summary_from_counts over (distinct count, number of groups with it) pairs."""
+    terms = []
+    for v, m in zip(np.asarray(values).tolist(), np.asarray(mult).tolist()):
+        p = v / num_rows
+        terms.append(-m * p * math.log(p))
+    vals = np.asarray(values)
+    mult = np.asarray(mult)
+    return {"num_groups": int(mult.sum()), "num_unique": int(mult[vals == 1].sum()),
+            "entropy": math.fsum(terms) if terms else 0.0}
+
+
 def group_summary_from_counts(counts, num_rows):
     """The fused aggregation of A/GroupingAnalyzers.scala:83-120 over a table's counts: groups, groups seen once,
     and the entropy terms -(c/N) ln(c/N) summed exactly (math.fsum over the distinct counts' multiplicities)."""

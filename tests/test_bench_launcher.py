@@ -30,6 +30,20 @@ def test_gpus_flag_starts_that_many_ranks(n):
     assert lines[0]["local_rank"] == 0
 
 
+@pytest.mark.parametrize("n", [1, 2])
+def test_default_is_baselines_one_billion_row_table(n):
+    """BASELINE: "synthetic 1B-row tables at 1/2/4/8 GPUs" -- the default splits 1e9 rows over the ranks (strong
+    scaling); --scaling weak stays an explicit option."""
+    p = _run(["--gpus", str(n), "--launch-check", "--dist-backend", "gloo", "--device-override", "0"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    cfg = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")][0]["config"]
+    assert cfg["rows"] == 1_000_000_000 and cfg["scaling"] == "strong"
+    assert abs(cfg["rows_per_gpu"] - 1_000_000_000 / n) <= 2048
+    p = _run(["--gpus", str(n), "--launch-check", "--dist-backend", "gloo", "--scaling", "weak"])
+    cfg = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")][0]["config"]
+    assert cfg["rows"] == n * 1_000_000_000 and cfg["rows_per_gpu"] == 1_000_000_000
+
+
 def test_world_size_mismatch_is_refused():
     p = _run(["--gpus", "2", "--launch-check"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0

@@ -144,3 +144,47 @@ def test_device_concat_equals_host_concat(lengths):
             got = dc.device["values"].cpu().numpy().view(np.float64)
             assert np.array_equal(got[hv], np.asarray(hc.values)[hv])
     torch.cuda.synchronize()
+
+
+def _helper_threads():
+    import threading
+    return [t for t in threading.enumerate() if t.name.startswith("dq-helper")]
+
+
+def test_failure_beside_a_running_grouping_helper(monkeypatch):
+    """a failure on the main thread of a chunked run while a grouping build runs on its helper context.
+    (1) One chunk's fused scan fails: its scanning analyzers keep that chunk's failure metric
+    (R/AnalysisRunner.scala:320-323), the grouping analyzers computed beside it succeed. (2) The state merge raises:
+    the run raises only after every helper has finished, and no aux context stays leased. (3) A follow-up run is
+    correct."""
+    from deequ_amd import native as N
+    data, types = _data(400_000, seed=5)
+    full, ct = _chunked(data, types, [0, 150_000, 400_000])
+    an = [D.Size(), D.Mean("x"), D.Uniqueness(["s"]), D.Entropy("k"), D.CountDistinct(["s", "k"])]
+    want = D.AnalysisRunner.onData(full).addAnalyzers(an).run()
+    real_run = runners.ScanBatch.run
+
+    def failing_scan(self, *a, **kw):
+        if self.data.nrows == 250_000:
+            raise RuntimeError("injected scan failure")
+        return real_run(self, *a, **kw)
+    monkeypatch.setattr(runners.ScanBatch, "run", failing_scan)
+    got = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in (D.Size(), D.Mean("x")):
+        assert not got.metric(a).value.isSuccess, a
+        assert "injected scan failure" in str(got.metric(a).value.exception), a
+    for a in (D.Uniqueness(["s"]), D.Entropy("k"), D.CountDistinct(["s", "k"])):
+        assert _close(got.metric(a).value.get(), want.metric(a).value.get()), a
+    assert not _helper_threads() and not N._aux_leased
+    monkeypatch.setattr(runners.ScanBatch, "run", real_run)
+
+    def failing_merge(*a, **kw):
+        raise RuntimeError("injected merge failure")
+    monkeypatch.setattr(runners.AnalysisRunner, "runOnAggregatedStates", staticmethod(failing_merge))
+    with pytest.raises(RuntimeError, match="injected merge failure"):
+        D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    assert not _helper_threads() and not N._aux_leased
+    monkeypatch.undo()
+    got = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in an:
+        assert _close(got.metric(a).value.get(), want.metric(a).value.get()), a

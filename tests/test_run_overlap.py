@@ -45,3 +45,72 @@ def test_pending_returns_and_reraises():
         raise ValueError("helper failed")
     with pytest.raises(ValueError, match="helper failed"):
         runners._Pending(boom).result()
+
+
+def _helper_threads():
+    return [t for t in threading.enumerate() if t.name.startswith("dq-helper")]
+
+
+def test_helpers_are_joined_when_the_caller_raises(monkeypatch):
+    """an exception on the calling thread (or in one helper) never leaves another helper running: the
+    run's helper group joins every helper before the exception propagates."""
+    import time
+    gate = threading.Event()
+    finished = []
+
+    def slow():
+        gate.wait(5)
+        time.sleep(0.2)
+        finished.append(1)
+        return 1
+    monkeypatch.setattr(runners, "_beside", lambda fn, slot: runners._Pending(fn, "dq-helper-" + slot))
+    with pytest.raises(RuntimeError, match="main thread failed"):
+        with runners._Helpers() as helpers:
+            helpers.beside(slow, "group0")
+            helpers.beside(lambda: (_ for _ in ()).throw(ValueError("helper failed")), "group1")
+            gate.set()
+            raise RuntimeError("main thread failed")
+    assert finished == [1] and not _helper_threads()
+    # a helper's error is re-raised by result() only after the group has joined the others
+    with pytest.raises(ValueError, match="helper failed"):
+        with runners._Helpers() as helpers:
+            helpers.beside(lambda: (_ for _ in ()).throw(ValueError("helper failed")), "group0")
+            helpers.beside(slow, "group1")
+            for h in helpers.pending:
+                h.result()
+    assert not _helper_threads()
+
+
+class _FakeLib:
+    def __init__(self):
+        self.trims = []
+
+    def dq_scratch_trim(self, handle, keep):
+        self.trims.append((handle, keep))
+
+
+def test_aux_contexts_are_leased_to_one_thread_at_a_time(monkeypatch):
+    """dq.h: calls on one ctx are not re-entrant. Two helpers of one slot (e.g. two user threads running the same
+    analysis) get two contexts; a released context is leased again and keeps at most the idle scratch cap."""
+    from deequ_amd import native as N
+    lib = _FakeLib()
+
+    class FakeContext:
+        n = 0
+
+        def __init__(self, device):
+            FakeContext.n += 1
+            self.device, self.lib, self.handle = device, lib, FakeContext.n
+    monkeypatch.setattr(N, "Context", FakeContext)
+    monkeypatch.setattr(N, "_aux_pool", {})
+    monkeypatch.setattr(N, "_aux_leased", set())
+    a = N.lease_aux_context(0, "group0")
+    b = N.lease_aux_context(0, "group0")
+    assert a is not b
+    N.release_aux_context(a)
+    assert lib.trims == [(a.handle, N.AUX_IDLE_SCRATCH_BYTES)]
+    assert N.lease_aux_context(0, "group0") is a
+    assert N.lease_aux_context(1, "group0") not in (a, b)  # per device
+    N.release_aux_context(a)
+    N.release_aux_context(b)
+    assert not N._aux_leased - {id(c) for pool in N._aux_pool.values() for c in pool if c.device == 1}
