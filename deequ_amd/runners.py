@@ -11,7 +11,7 @@ from . import native as N
 from . import engine
 from .analyzers import (Analyzer, ScanShareableAnalyzer, GroupingAnalyzer, ScanShareableFrequencyBasedAnalyzer,
                         FrequencyBasedAnalyzer, KLLSketch, Preconditions, Size, computeFrequencies, STATE_ONLY,
-                        ApproxQuantile, ApproxQuantiles)
+                        ApproxQuantile, ApproxQuantiles, Histogram)
 from .analyzers import merge as merge_states
 from .expr import compile_predicate
 from .metrics import DoubleMetric, Success, UnsupportedOnDevice
@@ -432,14 +432,18 @@ class AnalysisRunner:
         # multi-device context (DQ_DEVICES) shards every call itself and takes neither int64 offsets nor parted
         # columns: its chunks run one by one and merge like any other state.
         whole_table = len(data.chunks) > 1 and not getattr(engine.ctx(), "multi", False)
-        grouping = [a for a in analyzers if isinstance(a, GroupingAnalyzer)]
+        # Histogram (a plain Analyzer whose state is a frequency table with the NULL group) likewise: one table over
+        # the shard's column, not per-chunk tables joined on the host (A/Histogram.scala:54-70)
+        grouping = [a for a in analyzers if isinstance(a, GroupingAnalyzer) or
+                    (isinstance(a, Histogram) and a.binningUdf is None)]
         whole = AnalyzerContext.empty()
         if grouping and whole_table:
-            analyzers = [a for a in analyzers if not isinstance(a, GroupingAnalyzer)]
+            analyzers = [a for a in analyzers if a not in set(grouping)]
             by_set = {}
             for a in grouping:
-                by_set.setdefault(tuple(sorted(a.groupingColumns())), []).append(a)
-            sets = list(by_set.items())
+                key = ("\x00histogram", a.column) if isinstance(a, Histogram) else tuple(sorted(a.groupingColumns()))
+                by_set.setdefault(key, []).append(a)
+            sets = [((k[1],) if k[0] == "\x00histogram" else k, g) for k, g in by_set.items()]
             # each grouping-column set on its own helper context (at most three; the rest, or the last set when
             # nothing else runs, on this thread), beside the other analyzers' passes (see doAnalysisRun)
             for k, (cset, group) in enumerate(sets):
