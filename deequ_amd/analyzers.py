@@ -624,6 +624,16 @@ def _canonical_group_key(key):
     return key
 
 
+def _single_device_side(t):
+    """A DQ_FREQ_KEYS_VALUES table of a multi-device context as host (canonical key, count) pairs; anything else as
+    is."""
+    if isinstance(t, engine.FrequencyTable) and getattr(t.ctx, "multi", False):
+        keys, counts = t.export_pairs()
+        return engine.PairFrequencies(t.key_type, keys, counts, t.num_rows, t.summary(None)["null_count"],
+                                      t.decimal_scale, t.names)
+    return t
+
+
 class FrequenciesAndNumRows:
     """A/GroupingAnalyzers.scala:123-156. `frequencies` is one of
       * engine.FrequencyTable — the device (key -> count) table built by dq_frequencies;
@@ -669,6 +679,9 @@ class FrequenciesAndNumRows:
         a, b = self._values_side(), other._values_side()
         if a is not None and b is not None and a.key_type == b.key_type:
             rows = self.numRows + other.numRows
+            # a multi-device context's table (the union of per-device parts, DQ_DEVICES) merges as host pairs:
+            # dq_freq_merge joins single-device tables only
+            a, b = _single_device_side(a), _single_device_side(b)
             if isinstance(a, engine.PairFrequencies) and isinstance(b, engine.PairFrequencies):
                 keys, inv = np.unique(np.concatenate([a.keys, b.keys]), return_inverse=True)
                 counts = np.zeros(len(keys), dtype=np.int64)  # Long counts: exact beyond 2^53
@@ -720,11 +733,20 @@ class FrequenciesAndNumRows:
 
     def device_table(self):
         """The state as a device FrequencyTable: a GroupBlock is built once on the GPU, weighted by its counts
-        (dq_frequencies_ex), so repeated keys of a merged block add up."""
-        from . import groups as G
+        (dq_frequencies_ex), so repeated keys of a merged block add up. A multi-device context (DQ_DEVICES) takes no
+        weighted input: the weighted build then runs on a one-device context of this process's GPU."""
         f = self.frequencies
         if isinstance(f, engine.FrequencyTable):
             return f
+        ctx = engine.ctx()
+        if self._device is None and getattr(ctx, "multi", False):
+            with engine.using_context(N.aux_context(ctx.device, "weighted")):
+                return self._weighted_table()
+        return self._weighted_table()
+
+    def _weighted_table(self):
+        from . import groups as G
+        f = self.frequencies
         if self._device is None and isinstance(f, G.BlockParts):
             splits = f.split_by_key()
             tables = []

@@ -1699,11 +1699,15 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
             unsigned int p = start(h[u]);
             bool done = false;
             for (int probe = 0; probe < LS; ++probe) {
-                const unsigned long long prev = atomicCAS(&lkey[p], kEmpty, h[u]);
+                // a plain read first: a low-cardinality column finds its key already placed on almost every row, and a
+                // 64-bit LDS read is one access (kEmpty or the whole key), so only an empty slot takes the CAS and only
+                // a smaller row the atomicMin -- the atomics of many lanes on one hot slot serialise
+                unsigned long long prev = *(volatile unsigned long long*)&lkey[p];
+                if (prev == kEmpty) prev = atomicCAS(&lkey[p], kEmpty, h[u]);
                 if (prev == kEmpty || prev == h[u]) {
                     if (prev == kEmpty) atomicAdd(&lfill, 1u);
                     atomicAdd(&lcnt[p], 1u);
-                    atomicMin(&lrep[p], row);
+                    if (row < *(volatile unsigned long long*)&lrep[p]) atomicMin(&lrep[p], row);
                     done = true;
                     break;
                 }

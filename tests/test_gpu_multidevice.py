@@ -239,3 +239,44 @@ def test_sharded_cast_writes_host_results(multi, to):
     ok = unpack_validity(want_m, n)
     assert np.array_equal(vals[ok].view(np.int64), dv.cpu().numpy()[ok].view(np.int64))
     single.close()
+
+
+def test_chunked_table_on_a_multi_device_context(monkeypatch):
+    """a ChunkedTable under DQ_DEVICES runs its grouping, Histogram and ApproxQuantile analyzers chunk by
+    chunk (the multi-device context shards every call itself and takes neither int64 string offsets nor parted
+    columns) and merges the chunk states; the metrics equal the single-device run over the whole table."""
+    rng = np.random.default_rng(23)
+    n = 60_000
+    s = [None if rng.random() < 0.05 else "w%d" % int(v) for v in rng.integers(0, 4000, n)]
+    k = [int(v) for v in rng.integers(0, 300, n)]
+    x = [None if rng.random() < 0.1 else float(v) for v in rng.normal(size=n)]
+    data, types = {"s": s, "k": k, "x": x}, {"s": "string", "k": "long", "x": "double"}
+    full = Table.from_pydict(data, types=types)
+    cuts = [0, 25_000, 41_000, n]
+    ct = D.ChunkedTable([Table.from_pydict({c: v[a:b] for c, v in data.items()}, types=types)
+                         for a, b in zip(cuts, cuts[1:])])
+    an = [D.Size(), D.Mean("x"), D.Uniqueness(["s"]), D.Entropy("k"), D.CountDistinct(["s", "k"]), D.Histogram("s"),
+          D.ApproxQuantile("x", 0.5)]
+    monkeypatch.delenv("DQ_DEVICES", raising=False)
+    want = D.AnalysisRunner.onData(full).addAnalyzers(an).run()
+    monkeypatch.setenv("DQ_DEVICES", "0,0")
+    assert engine.ctx().multi
+    got = D.AnalysisRunner.onData(ct).addAnalyzers(an).run()
+    for a in an:
+        g, w = got.metric(a).value, want.metric(a).value
+        assert g.isSuccess and w.isSuccess, (a, g, w)
+        if isinstance(a, D.Histogram):  # top-N details: ties broken arbitrarily (A/Histogram.scala:113-117)
+            import collections
+            exact = collections.Counter("NullValue" if v is None else v for v in s)
+            assert g.get().numberOfBins == w.get().numberOfBins == len(exact)
+            assert all(v.absolute == exact[key] for key, v in g.get().values.items())
+            assert sorted(v.absolute for v in g.get().values.values()) == \
+                sorted(v.absolute for v in w.get().values.values())
+        elif isinstance(a, D.ApproxQuantile):  # both inside the rank bound of the same column
+            vals = np.sort(np.array([v for v in x if v is not None]))
+            for v in (g.get(), w.get()):
+                lo, hi = O.rank_interval(vals, v)
+                target = math.ceil(0.5 * len(vals))
+                assert lo - math.ceil(0.01 * len(vals)) - 1 <= target <= hi + math.ceil(0.01 * len(vals)) + 1
+        else:
+            assert abs(g.get() - w.get()) <= 1e-12 * max(1.0, abs(w.get())), (a, g.get(), w.get())
