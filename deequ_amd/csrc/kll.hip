@@ -885,6 +885,290 @@ kll_compact_x_kernel(const double* __restrict__ src, const uint64_t* __restrict_
     }
 }
 
+// ---- level 0 on fp64 min / max (r06) ---------------------------------------------------------------------------------
+// A level-0 compaction sorts raw values. Sorting them as doubles lets a compare-exchange be one v_min_f64 + one
+// v_max_f64 instead of a 64-bit compare and four 32-bit selects of the order keys (the register network, the bitonic
+// halves after each lane-exchange round and the LDS merge rounds are most of the kernel's VALU work). IEEE order and
+// Java's Double.compare order (Scala's `.sorted` over Ordering.Double, A/QuantileNonSample.scala) differ in two places
+// only, both restored by position after the sort, from counts taken before it:
+//   * NaN: mapped to +inf (min against +inf: 1 instruction); Java puts every NaN above +inf, so the last nnan sorted
+//     positions of the range are NaN (written as the canonical NaN, as kll_value(kll_key(NaN)) does);
+//   * -0.0 == +0.0 under IEEE compares (and min / max may return either): Java has -0.0 < +0.0, so of the zeros' sorted
+//     positions [nlt0, nlt0 + nzero) the first nneg0 are -0.0 and the rest +0.0 (nlt0 = values below zero, counted
+//     after the sort when the range holds a -0.0 at all: the multiset is the same).
+// Every other value sorts identically, so the picks, the next level's stream and min / max are bit-identical to the
+// order-key sort (tests/test_gpu_kll.py runs both, DQ_KLL_NO_F64=1).
+__device__ __forceinline__ double kll_canon_f(double x) { return __builtin_canonicalize(x); }
+__device__ __forceinline__ double kll_min_f(double a, double b) { return __builtin_fmin(a, b); }
+__device__ __forceinline__ double kll_max_f(double a, double b) { return __builtin_fmax(a, b); }
+
+__device__ __forceinline__ void kll_reg_sort8_f(double (&w)[8]) {
+#pragma unroll
+    for (int size = 2; size <= 8; size <<= 1)
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int q = r ^ stride;
+                if (q > r) {
+                    const double a = w[r], b = w[q];
+                    const double lo = kll_min_f(a, b), hi = kll_max_f(a, b);
+                    const bool asc = (r & size) == 0;
+                    w[r] = asc ? lo : hi;
+                    w[q] = asc ? hi : lo;
+                }
+            }
+}
+
+template <int CTRL>
+__device__ __forceinline__ double kll_dpp_f(double x) {
+    return __longlong_as_double((long long)kll_dpp64<CTRL>((uint64_t)__double_as_longlong(x)));
+}
+
+template <int CTRL, bool REV>
+__device__ __forceinline__ void kll_dpp_stage_f(double (&v)[8], bool lower) {
+    double b[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) b[r] = kll_dpp_f<CTRL>(v[r]);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const double x = v[r], y = b[REV ? 7 - r : r];
+        v[r] = (x < y) == lower ? x : y;
+    }
+}
+
+__device__ __forceinline__ void kll_bitonic8_f(double (&v)[8]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = kll_canon_f(v[r]);  // after lane moves: one canonicalisation, then min / max
+#pragma unroll
+    for (int stride = 4; stride > 0; stride >>= 1)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            if ((r & stride) == 0) {
+                const double x = v[r], y = v[r + stride];
+                v[r] = kll_min_f(x, y);
+                v[r + stride] = kll_max_f(x, y);
+            }
+}
+
+__device__ __forceinline__ void kll_dpp_rounds_f(double (&v)[8], int t) {
+    constexpr int kXor1 = 0xB1, kXor2 = 0x4E, kRev4 = 0x1B, kRev8 = 0x141;
+    constexpr int kRev16 = 0x140, kShl4 = 0x104, kShr4 = 0x114;
+    kll_dpp_stage_f<kXor1, true>(v, (t & 1) == 0);  // w = 8
+    kll_bitonic8_f(v);
+    kll_dpp_stage_f<kRev4, true>(v, (t & 2) == 0);  // w = 16
+    kll_dpp_stage_f<kXor1, false>(v, (t & 1) == 0);
+    kll_bitonic8_f(v);
+    kll_dpp_stage_f<kRev8, true>(v, (t & 4) == 0);  // w = 32
+    kll_dpp_stage_f<kXor2, false>(v, (t & 2) == 0);
+    kll_dpp_stage_f<kXor1, false>(v, (t & 1) == 0);
+    kll_bitonic8_f(v);
+    kll_dpp_stage_f<kRev16, true>(v, (t & 8) == 0);  // w = 64
+    {
+        const bool lo4 = (t & 4) == 0;
+        double b[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const double up = kll_dpp_f<kShl4>(v[r]), dn = kll_dpp_f<kShr4>(v[r]);
+            b[r] = lo4 ? up : dn;
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const double x = v[r], y = b[r];
+            v[r] = (x < y) == lo4 ? x : y;
+        }
+    }
+    kll_dpp_stage_f<kXor2, false>(v, (t & 2) == 0);
+    kll_dpp_stage_f<kXor1, false>(v, (t & 1) == 0);
+    kll_bitonic8_f(v);
+}
+
+// kll_merge_round for E = 8 over doubles (the LDS image holds double bits; +inf pads).
+__device__ __forceinline__ void kll_merge_round8_f(double* k, double (&v)[8], int t, int w) {
+    constexpr int E = 8;
+    auto at = [](int i) { return i + i / E; };
+    const bool wave_local = 2 * w <= 64 * E;
+    const double inf = __builtin_huge_val();
+#pragma unroll
+    for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
+    kll_round_sync(wave_local);
+    const int diag = E * (t & (2 * (w / E) - 1));
+    const int A = (t * E) - diag, B = A + w;
+    int lo = diag > w ? diag - w : 0, hi = diag < w ? diag : w;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (k[at(A + mid)] <= k[at(B + diag - 1 - mid)]) lo = mid + 1;
+        else hi = mid;
+    }
+    const int ai = A + lo, bi = B + diag - lo;
+    const int aend = A + w, bend = B + w;
+    double a[E], b[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        a[r] = kll_canon_f(ai + r < aend ? k[at(ai + r)] : inf);
+        b[r] = kll_canon_f(bi + r < bend ? k[at(bi + r)] : inf);
+    }
+#pragma unroll
+    for (int r = 0; r < E; ++r) v[r] = kll_min_f(a[r], b[E - 1 - r]);
+#pragma unroll
+    for (int stride = E / 2; stride > 0; stride >>= 1)
+#pragma unroll
+        for (int r = 0; r < E; ++r)
+            if ((r & stride) == 0) {
+                const double x = v[r], y = v[r + stride];
+                v[r] = kll_min_f(x, y);
+                v[r + stride] = kll_max_f(x, y);
+            }
+    kll_round_sync(wave_local);
+}
+
+// Level-0 compactions of L = P + rx items (P = 8T), as kll_compact_x_kernel, sorting doubles (see above).
+template <int T>
+__global__ void __launch_bounds__(T)
+kll_compact_xf_kernel(const double* __restrict__ src, const uint64_t* __restrict__ segs, double* __restrict__ dst,
+                      unsigned long long* __restrict__ minmax, const KllColPtr* __restrict__ cols,
+                      const unsigned long long* __restrict__ rows) {
+    constexpr int E = 8, P = T * E, XM = kll_xm(T), NW = T / 64;
+    __shared__ double k[P + T];
+    __shared__ double ex[XM];
+    __shared__ unsigned int wc[8 * NW + 1];
+    __shared__ int cnt[3];  // NaN, -0.0, below zero
+    auto at = [](int i) { return i + i / E; };
+    const uint64_t sg = segs[blockIdx.x];
+    kll_col_ptrs(cols, sg, src, dst, minmax);
+    const uint64_t start = sg & ((1ull << 40) - 1);
+    const int len = (int)((sg >> 40) & 0x7FFF);
+    const int rx = len - P;  // 0..XM (host-checked)
+    const int t = threadIdx.x, lane = t & 63;
+    const double inf = __builtin_huge_val();
+    if (t < 3) cnt[t] = 0;
+    __syncthreads();  // cnt[] cleared before any wave counts into it below
+    double v[E];
+    double xk = inf;
+    if (rows && !src) {  // level 0 read in place: the range's values in dense order, as loaded
+        kll_stage_rows<T, true>(cols[(sg >> 55) & 0xFF].raw, (int64_t)rows[2 * blockIdx.x],
+                                (int64_t)rows[2 * blockIdx.x + 1], wc, [&](unsigned int pos, uint64_t bits) {
+                                    const double x = __longlong_as_double((long long)bits);
+                                    if ((int)pos < P) k[at((int)pos)] = x;
+                                    else if ((int)pos < len) ex[pos - P] = x;
+                                });
+#pragma unroll
+        for (int r = 0; r < E; ++r) v[r] = k[at(t * E + r)];
+        if (t < XM && t < rx) xk = ex[t];
+    } else {
+        const double* in = src + start;
+#pragma unroll
+        for (int r = 0; r < E; ++r) v[r] = in[t * E + r];
+        if (t < XM && t < rx) xk = in[P + t];
+    }
+    // counts over the range's values (ballot popcounts, one LDS add per wave), NaN -> +inf
+    {
+        int nn = 0, nz = 0;
+#pragma unroll
+        for (int r = 0; r <= E; ++r) {
+            const double x = r < E ? v[r] : xk;
+            const bool in = r < E || (t < XM && t < rx);
+            nn += (int)__popcll(__ballot(in && __builtin_isnan(x)));
+            nz += (int)__popcll(__ballot(in && x == 0.0 && __builtin_signbit(x)));
+        }
+        if (lane == 0 && (nn | nz)) {
+            atomicAdd(&cnt[0], nn);
+            atomicAdd(&cnt[1], nz);
+        }
+#pragma unroll
+        for (int r = 0; r < E; ++r) v[r] = kll_min_f(kll_canon_f(v[r]), inf);
+        xk = kll_min_f(kll_canon_f(xk), inf);
+    }
+    kll_reg_sort8_f(v);
+    kll_dpp_rounds_f(v, t);
+    for (int w = 128; w < P; w <<= 1) kll_merge_round8_f(k, v, t, w);
+#pragma unroll
+    for (int r = 0; r < E; ++r) k[at(t * E + r)] = v[r];
+    if (rx <= 64) {  // wave 0: bitonic over its lanes
+        if (t < 64) {
+#pragma unroll
+            for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+                for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                    const double y = __longlong_as_double((long long)shfl_xor_u64((uint64_t)__double_as_longlong(xk),
+                                                                                    stride));
+                    const bool keep_min = ((t & stride) == 0) == ((t & size) == 0);
+                    xk = keep_min ? (y < xk ? y : xk) : (y > xk ? y : xk);
+                }
+            ex[t] = xk;
+        }
+    } else {  // ranks among the extras (ties by arrival)
+        __syncthreads();
+        if (t < rx) ex[t] = xk;
+        __syncthreads();
+        int rk = 0;
+        if (t < rx)
+            for (int j = 0; j < rx; ++j) {
+                const double y = ex[j];
+                rk += (y < xk || (y == xk && j < t)) ? 1 : 0;
+            }
+        __syncthreads();
+        if (t < rx) ex[rk] = xk;
+    }
+    __syncthreads();
+    const int nnan = cnt[0], nneg0 = cnt[1];
+    int nlt0 = 0;
+    if (nneg0) {  // (uniform) the zeros' first position: values below zero, over the same multiset
+        __shared__ int lt0;
+        if (t == 0) lt0 = 0;
+        __syncthreads();
+        int c = 0;
+#pragma unroll
+        for (int r = 0; r < E; ++r) c += (int)__popcll(__ballot(v[r] < 0.0));
+        c += (int)__popcll(__ballot(t < rx && ex[t < XM ? t : 0] < 0.0));
+        if (lane == 0 && c) atomicAdd(&lt0, c);
+        __syncthreads();
+        nlt0 = lt0;
+    }
+    // the Java-order value at sorted position pos (v its IEEE-sorted value there)
+    auto fix = [&](double x, int pos) {
+        if (pos >= len - nnan) return __longlong_as_double(0x7ff8000000000000LL);
+        if (x == 0.0) return pos < nlt0 + nneg0 ? -0.0 : 0.0;
+        return x;
+    };
+    const int half = len >> 1;
+    const int off = (int)(sg >> 63);
+    double* out = dst + (start >> 1);
+    int c = 0, hb = rx;
+    while (c < hb) {
+        const int mid = (c + hb) >> 1;
+        if (ex[mid] < v[0]) c = mid + 1;
+        else hb = mid;
+    }
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        while (c < rx && ex[c] < v[r]) ++c;
+        const int pos = t * E + r + c, d = pos - off;
+        if (d >= 0 && (d & 1) == 0 && (d >> 1) < half) out[d >> 1] = fix(v[r], pos);
+    }
+    if (t < rx) {
+        const double x = ex[t];
+        int lo = 0, hi = P;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (k[at(mid)] <= x) lo = mid + 1;
+            else hi = mid;
+        }
+        const int pos = lo + t, d = pos - off;
+        if (d >= 0 && (d & 1) == 0 && (d >> 1) < half) out[d >> 1] = fix(x, pos);
+    }
+    if (minmax && t == 0 && len > 0) {
+        double mn = k[at(0)], mx = k[at(P - 1)];
+        if (rx > 0) {
+            mn = ex[0] < mn ? ex[0] : mn;
+            mx = ex[rx - 1] > mx ? ex[rx - 1] : mx;
+        }
+        const uint64_t kmn = kll_key(fix(mn, 0)), kmx = kll_key(fix(mx, len - 1));
+        if (kmn < *(volatile unsigned long long*)&minmax[0]) atomicMin(&minmax[0], (unsigned long long)kmn);
+        if (kmx > *(volatile unsigned long long*)&minmax[1]) atomicMax(&minmax[1], (unsigned long long)kmx);
+    }
+}
+
 // Compaction classes: (threads, keys per thread), capacity T*E.
 struct KllClass {
     int t, e;
@@ -927,6 +1211,21 @@ int launch_kll_compact(int cls, const double* src, const uint64_t* segs, int nse
     const bool no_runs = getenv("DQ_KLL_NO_RUNS") != nullptr;  // A/B and tests: the full sort at every level
     const int runs = level > 0 && !no_runs ? 1 : 0;
     if (nseg <= 0) return 0;
+    const bool no_f64 = getenv("DQ_KLL_NO_F64") != nullptr;  // A/B and tests: order keys at level 0 too
+    if (level == 0 && !no_f64) {  // level 0: the E = 8 exact-size classes sort doubles (kll_compact_xf_kernel)
+        switch (cls) {
+#define KLL_FCASE(C, T) \
+    case C: hipLaunchKernelGGL((kll_compact_xf_kernel<T>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols, rows); \
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+            KLL_FCASE(13, 64)
+            KLL_FCASE(14, 128)
+            KLL_FCASE(15, 256)
+            KLL_FCASE(16, 512)
+            KLL_FCASE(17, 1024)
+#undef KLL_FCASE
+            default: break;
+        }
+    }
     switch (cls) {
 #define KLL_CASE(C, T, E) \
     case C: hipLaunchKernelGGL((kll_compact_kernel<T, E>), dim3(nseg), dim3(T), 0, s, src, segs, dst, minmax, cols, rows, runs); break;

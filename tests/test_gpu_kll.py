@@ -128,6 +128,38 @@ def test_sketch_run_shapes(shape, size, f, monkeypatch):
     assert got == check(x, None, size, f)
 
 
+@pytest.mark.parametrize("case", ["signed_zeros", "denormals", "nan_heavy", "mostly_nan", "extremes"])
+def test_level0_fp64_sort_equals_the_order_key_sort(case, monkeypatch):
+    """Level-0 compactions sort doubles with fp64 min / max (kll.hip kll_compact_xf_kernel) and restore Java's
+    Double.compare order by position: NaN above +inf, -0.0 below +0.0. Inputs made of exactly those ties (signed zeros
+    among negatives and denormals, NaN / inf heavy ranges) give the oracle's bytes and the order-key sort's
+    (DQ_KLL_NO_F64=1), from host and device columns, with NULLs."""
+    rng = np.random.default_rng(len(case))
+    n = 300_007
+    tiny = 5e-324
+    if case == "signed_zeros":
+        x = rng.choice(np.array([-0.0, 0.0, -1.0, 1.0, -tiny, tiny, -0.0, -0.0]), n)
+    elif case == "denormals":
+        x = rng.integers(-40, 40, n).astype(np.float64) * tiny
+    elif case == "nan_heavy":
+        x = rng.normal(size=n)
+        x[rng.random(n) < 0.3] = np.nan
+        x[rng.random(n) < 0.05] = np.inf
+        x[rng.random(n) < 0.05] = -np.inf
+    elif case == "mostly_nan":
+        x = np.full(n, np.nan)
+        x[rng.integers(0, n, 500)] = -0.0
+        x[rng.integers(0, n, 500)] = 0.0
+    else:
+        x = rng.choice(np.array([np.finfo(np.float64).max, -np.finfo(np.float64).max, np.inf, -np.inf, 1e-308,
+                                 -1e-308, 0.0, -0.0]), n)
+    valid = rng.random(n) > 0.1
+    got = check(x)
+    got_v = check(x, valid, device=True)
+    monkeypatch.setenv("DQ_KLL_NO_F64", "1")  # read at every compaction launch
+    assert got == check(x) and got_v == check(x, valid, device=True)
+
+
 def test_sketch_all_null_and_min_max_quirk():
     x = np.arange(100, dtype=np.float64)
     raw = check(x, np.zeros(100, dtype=bool))
