@@ -8,6 +8,7 @@
 // wave ballot (64 rows per wave = one 64-bit word, LSB-first).
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -46,10 +47,86 @@ __device__ __forceinline__ int64_t java_d2l(double d) {
 // scattered HBM bytes); a longer range is parsed from HBM directly.
 constexpr int kCastStageWords = 512;
 
+// ---- short numeric strings without per-byte branches (r06) ---------------------------------------------------------
+// The numeric-looking string columns a profile casts hold short plain numbers ("-4999", "123.45"). For a string of
+// <= 15 bytes the lane assembles its bytes as two words (aligned dword loads, from the wave's LDS stage when there is
+// one) and runs one DFA step per byte position, wave-uniform up to the wave's longest such string, with selects only:
+// [+|-] digits* [. digits*]. That grammar is all of UTF8String.toLong at this length (the value fits: 15 digits), so
+// LONG is decided here; for DOUBLE it is the plain-decimal subset of Double.parseDouble, whose value is the integer of
+// all its digits (< 10^15, exact in a double) divided by 10^(fraction digits) (exact): one correctly rounded IEEE
+// division, i.e. Java's correctly rounded result (Clinger's fast path). Anything else (whitespace, exponents, NaN /
+// Infinity, suffixes, hex, longer strings) takes the general parsers of dq_parse.h as before.
+struct ShortNum {
+    bool fast;      // the DFA decided the row (LONG: always for <= 15 bytes; DOUBLE: the plain-decimal form)
+    bool ok;        // parsed (else NULL)
+    int64_t v;      // LONG
+    double d;       // DOUBLE
+};
+
+__device__ __forceinline__ uint32_t cast_dw(const uint8_t* a, int k) {
+    return *reinterpret_cast<const uint32_t*>(a + 4 * k);
+}
+
+// Returns the row's short-number parse; `len` <= 15 is the caller's condition for `eligible`. `maxlen` is the wave's
+// largest eligible length (wave-uniform loop bound).
+__device__ __forceinline__ ShortNum cast_short_number(const uint8_t* s, int len, bool eligible, int maxlen,
+                                                      bool to_double) {
+    uint64_t x0 = 0, x1 = 0;
+    if (eligible && len > 0) {
+        const uint8_t* a = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(s - a);
+        const int ndw = (int)((sh + (uint32_t)len + 3) >> 2);
+        uint32_t w[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) w[k] = k < ndw ? cast_dw(a, k) : 0u;
+        x0 = (uint64_t)__builtin_amdgcn_alignbyte(w[1], w[0], sh) |
+             ((uint64_t)__builtin_amdgcn_alignbyte(w[2], w[1], sh) << 32);
+        x1 = (uint64_t)__builtin_amdgcn_alignbyte(w[3], w[2], sh) |
+             ((uint64_t)__builtin_amdgcn_alignbyte(w[4], w[3], sh) << 32);
+    }
+    uint64_t mi = 0;      // LONG: the digits before the point
+    double md = 0.0;      // DOUBLE: every digit
+    double p10 = 1.0;     // 10^(fraction digits)
+    int nd = 0;
+    bool dot = false, neg = false, sg = false, bad = false;
+    for (int i = 0; i < maxlen; ++i) {  // wave-uniform bound
+        const bool act = eligible && i < len;
+        const uint64_t word = i < 8 ? x0 : x1;
+        const uint32_t c = (uint32_t)(word >> (8 * (i & 7))) & 0xFFu;
+        const uint32_t dg = c - (uint32_t)'0';
+        const bool isd = act && dg < 10u;
+        const bool isdot = act && c == (uint32_t)'.' && !dot;
+        const bool sgn = act && i == 0 && (c == (uint32_t)'+' || c == (uint32_t)'-');
+        bad |= act && !isd && !isdot && !sgn;
+        neg |= sgn && c == (uint32_t)'-';
+        sg |= sgn;
+        mi = isd && !dot ? mi * 10ull + dg : mi;
+        md = isd ? __builtin_fma(md, 10.0, (double)dg) : md;
+        p10 = isd && dot ? p10 * 10.0 : p10;
+        nd += isd ? 1 : 0;
+        dot |= isdot;
+    }
+    ShortNum r;
+    if (!to_double) {
+        // UTF8String.toLong: "" and a lone sign are NULL; a bad character is NULL; otherwise the truncated integer
+        r.fast = eligible;
+        r.ok = !bad && len > 0 && !(len == 1 && sg);
+        r.v = neg ? (int64_t)(0ull - mi) : (int64_t)mi;
+        r.d = 0.0;
+    } else {
+        r.fast = eligible && !bad && nd > 0;
+        r.ok = r.fast;
+        const double q = md / p10;
+        r.d = neg ? -q : q;
+        r.v = 0;
+    }
+    return r;
+}
+
 template <bool STRING>
 __global__ void __launch_bounds__(kCastBlock)
 cast_kernel(CastSource c, int64_t nrows, int to_double, void* __restrict__ values_out,
-            uint64_t* __restrict__ validity_out, unsigned int* __restrict__ slow_flag) {
+            uint64_t* __restrict__ validity_out, unsigned int* __restrict__ slow_flag, int no_short) {
     __shared__ uint32_t stage[STRING ? kCastBlock / 64 : 1][STRING ? kCastStageWords : 1];
     const int64_t stride = (int64_t)gridDim.x * kCastBlock;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -86,7 +163,22 @@ cast_kernel(CastSource c, int64_t nrows, int to_double, void* __restrict__ value
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
         }
-        if (rvalid) {
+        ShortNum sn;
+        sn.fast = false;
+        if (STRING && !no_short) {
+            const bool elig = rvalid && rlen <= 15;
+            int ml = elig ? rlen : 0;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) ml = max(ml, __shfl_xor(ml, o, 64));
+            const uint8_t* s = sbase ? sbase + (ro - a0) : c.bytes + ro;
+            sn = cast_short_number(s, rlen, elig, ml, to_double != 0);
+            if (sn.fast) {
+                ok = sn.ok;
+                d = sn.d;
+                v = sn.v;
+            }
+        }
+        if (rvalid && !sn.fast) {
             if (STRING) {
                 const int32_t o = ro;
                 const int len = rlen;
@@ -269,12 +361,13 @@ static int cast_single(dq_ctx* ctx, const dq_column* column, int64_t nrows, int3
     const int64_t blocks = (nrows + dq::kCastBlock - 1) / dq::kCastBlock;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)dq::ctx_cus(ctx) * 16));
     const int to_double = to_type == DQ_TYPE_DOUBLE ? 1 : 0;
+    const int no_short = getenv("DQ_CAST_NO_SHORT") ? 1 : 0;  // A/B and tests: every row through dq_parse.h
     if (is_string)
         hipLaunchKernelGGL(dq::cast_kernel<true>, dim3(grid), dim3(dq::kCastBlock), 0, s, c, nrows, to_double, values_dev,
-                           (uint64_t*)validity_dev, dslow);
+                           (uint64_t*)validity_dev, dslow, no_short);
     else
         hipLaunchKernelGGL(dq::cast_kernel<false>, dim3(grid), dim3(dq::kCastBlock), 0, s, c, nrows, to_double,
-                           values_dev, (uint64_t*)validity_dev, dslow);
+                           values_dev, (uint64_t*)validity_dev, dslow, no_short);
     CA_HIP(ctx, hipGetLastError());
     unsigned int slow = 0;
     CA_HIP(ctx, hipMemcpyAsync(&slow, dslow, sizeof(slow), hipMemcpyDeviceToHost, s));

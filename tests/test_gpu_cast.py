@@ -108,3 +108,44 @@ def test_cast_empty_and_all_null():
     assert len(vals) == 0
     vals, ok, _ = gpu_cast([None] * 100, N.TYPE_DOUBLE)
     assert not ok.any()
+
+
+@pytest.mark.parametrize("to_type", [N.TYPE_LONG, N.TYPE_DOUBLE])
+@pytest.mark.parametrize("device", [False, True])
+def test_short_numbers_fast_path_matches_the_parsers(to_type, device, monkeypatch):
+    """Strings of <= 15 bytes are parsed by one branch-free DFA step per byte ([+|-] digits [. digits]; cast.hip
+    cast_short_number): every form of that grammar at every length up to 15 (and the near misses around it: lone signs
+    and points, second points, inner signs, spaces, exponents, letters, 16-byte numbers) equals the oracle's
+    UTF8String.toLong / Double.parseDouble and the general device parsers (DQ_CAST_NO_SHORT=1), bit for bit."""
+    rng = np.random.default_rng(40 + device + 2 * (to_type == N.TYPE_DOUBLE))
+    strings = ["", ".", "+", "-", "+.", "-.", "-.5", ".5", "1.", "00", "-0", "-0.000", "+0", "0.", "1.2.3", "1-2", "+-1",
+               " 1", "1 ", "1e5", "1d", "NaN", "a", "999999999999999", "-99999999999999", "9999999.9999999",
+               "0.000000000001", "1234567890123456", "-123456789012345", "1.23456789012345", "..1", "1..", "-",
+               None]
+    for _ in range(30_000):
+        nd = int(rng.integers(0, 15))
+        digits = "".join(str(d) for d in rng.integers(0, 10, nd))
+        p = int(rng.integers(0, nd + 1))
+        form = int(rng.integers(0, 4))
+        s = digits if form == 0 else digits[:p] + "." + digits[p:] if form == 1 else \
+            ["-", "+"][int(rng.integers(0, 2))] + (digits[:p] + "." + digits[p:] if rng.random() < 0.5 else digits)
+        if form == 3 and s:  # a near miss: one byte replaced
+            i = int(rng.integers(0, len(s)))
+            s = s[:i] + ["x", " ", "e", "-", "."][int(rng.integers(0, 5))] + s[i + 1:]
+        strings.append(s[:16])
+    strings += ["%d" % v for v in rng.integers(-1_000_000, 1_000_000, 2000)]  # the C5 generators' forms
+    strings += ["%d.%02d" % (v // 100, v % 100) for v in rng.integers(0, 100_000, 2000)]
+    strings += ["%s%d.%03d" % ("-" if v < 0 else "", abs(v) // 1000, abs(v) % 1000)
+                for v in rng.integers(-999_999, 999_999, 2000)]
+    fast, ok_f, _ = gpu_cast(strings, to_type, device=device)
+    monkeypatch.setenv("DQ_CAST_NO_SHORT", "1")
+    slow, ok_s, _ = gpu_cast(strings, to_type, device=device)
+    assert np.array_equal(ok_f, ok_s)
+    assert np.array_equal(fast[ok_f].view(np.uint64), slow[ok_s].view(np.uint64))
+    for i, s in enumerate(strings):
+        exp = None if s is None else (O.spark_string_to_long(s) if to_type == N.TYPE_LONG else O.java_parse_double(s))
+        assert bool(ok_f[i]) == (exp is not None), (s, exp)
+        if exp is not None and to_type == N.TYPE_LONG:
+            assert int(fast[i]) == exp, (s, exp)
+        elif exp is not None and not np.isnan(exp):
+            assert np.float64(fast[i]).view(np.uint64) == np.float64(exp).view(np.uint64), (s, exp, fast[i])
