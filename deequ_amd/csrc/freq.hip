@@ -1645,8 +1645,11 @@ __device__ __forceinline__ bool row_key_str1(const KeySpec& ks, int64_t r, uint6
 constexpr int kSmallTile = 4 * kBuildBlock;
 constexpr int kSmallGrid = 768;  // 3 workgroups per CU with the 2048-slot table
 
+#ifndef DQ_SMALL_WAVES
+#define DQ_SMALL_WAVES 0  // STR1 A/B: a minimum of waves per SIMD (6: 80 VGPRs + spills, 8: 64 + spills) measured no faster, profiles/r06/small_build_waves_ab_r06s.txt
+#endif
 template <int LS, bool STR1 = false>  // slots of the workgroup's LDS table; STR1: one string key column
-__global__ void __launch_bounds__(kBuildBlock)
+__global__ void __launch_bounds__(kBuildBlock, STR1 && DQ_SMALL_WAVES ? DQ_SMALL_WAVES : 1)
 small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned long long* __restrict__ reps,
                    unsigned long long* __restrict__ wg_keys, unsigned long long* __restrict__ wg_reps,
                    Counters* __restrict__ ctr, int count_rows) {
