@@ -557,7 +557,9 @@ def release_aux_context(ctx):
             _aux_leased.discard(id(ctx))
 
 
-AUX_IDLE_SCRATCH_BYTES = 16 << 30  # idle device scratch an aux context keeps between runs
+# idle device scratch an aux context keeps between runs (its builds re-use it instead of hipMalloc'ing again; an
+# allocation that fails on any context of the device releases the others' idle scratch first, dq_api.cpp)
+AUX_IDLE_SCRATCH_BYTES = int(float(os.environ.get("DQ_AUX_IDLE_SCRATCH", 16 << 30)))
 
 
 def aux_context(device=0, slot="aux"):
