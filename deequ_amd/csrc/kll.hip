@@ -615,13 +615,20 @@ __device__ __forceinline__ void kll_stage_rows(const KllColumn& c, int64_t r0, i
     for (int64_t c0 = r0; c0 < r1; c0 += (int64_t)RM * T) {
         uint64_t key[RM];
         uint64_t bal[RM];
+        // row groups of this chunk that hold rows at all (uniform): a range of ~2150 rows is one full chunk of 2048
+        // and a tail of ~100, whose other seven groups would otherwise run their address / validity / load work
+        const int nq = (int)((r1 - c0 + T - 1) / T < RM ? (r1 - c0 + T - 1) / T : RM);
 #pragma unroll
         for (int q = 0; q < RM; ++q) {
-            const int64_t r = c0 + (int64_t)q * T + t;
-            const bool v = r < r1 && kll_valid(c, r);
-            const double x = v ? kll_load(c, r) : 0.0;
-            key[q] = RAWBITS ? (uint64_t)__double_as_longlong(x) : kll_key(x);
-            bal[q] = __ballot(v);
+            key[q] = 0;
+            bal[q] = 0;
+            if (q < nq) {
+                const int64_t r = c0 + (int64_t)q * T + t;
+                const bool v = r < r1 && kll_valid(c, r);
+                const double x = v ? kll_load(c, r) : 0.0;
+                key[q] = RAWBITS ? (uint64_t)__double_as_longlong(x) : kll_key(x);
+                bal[q] = __ballot(v);
+            }
         }
         if (lane == 0) {
 #pragma unroll

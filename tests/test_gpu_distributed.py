@@ -30,11 +30,14 @@ def _analyzers():
             D.CountDistinct(["k"]), D.UniqueValueRatio(["k"]), D.Histogram("d", None, 10), D.KLLSketch("x")]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         import deequ_amd as D
         t = _table()
@@ -220,3 +223,34 @@ def test_row_counts_join_rows_with_their_groups():
             tot[key] = tot.get(key, 0) + x
         want = [0 if all(v is None for v in key) else tot[key] for key in keys]
         assert rc.tolist() == want, cols
+
+
+def test_rccl_backend_one_rank_matches_single_gpu_run():
+    """The RCCL (nccl) backend's collectives with device tensors -- all_gather_into_tensor of the scan states, the
+    device (key, count) pairs through all_to_all_single, the all-gathered KLL / digest / group blobs -- on a real
+    communicator (world size 1: RCCL needs one GPU per rank, and this box has one). Before r06 every GPU test of the
+    sharded runner used gloo; the metrics equal the single-GPU run."""
+    import deequ_amd as D
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(0, 1, port, q, "nccl"))
+    p.start()
+    rank, got = q.get(timeout=200)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    single = D.AnalysisRunner.onData(_table()).addAnalyzers(_analyzers()).run()
+    for a in _analyzers():
+        g, m = got[repr(a)], single.metric(a).value.get()
+        if isinstance(a, D.KLLSketch):
+            assert g[0] == [(b.lowValue, b.highValue, b.count) for b in m.buckets] and g[1] == m.data
+        elif isinstance(a, D.Histogram):
+            assert g[0] == m.numberOfBins
+            assert sorted(c for _, c in g[1]) == sorted(v.absolute for v in m.values.values())
+        elif isinstance(a, (D.Mean, D.StandardDeviation, D.Correlation, D.Entropy)):
+            assert abs(g - m) <= 1e-12 * max(1.0, abs(m)), (a, g, m)
+        else:
+            assert g == m, (a, g, m)
