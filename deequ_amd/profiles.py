@@ -205,7 +205,24 @@ class ColumnProfiler:
                  not os.environ.get("DQ_PROFILE_NO_EARLY_STATS")]
         for name in early:
             first += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
-        res1 = passes.run(data, first + [Size()])
+        # Their KLL sketches (the extra pass of pass 2) do not depend on pass 1 either: on this process's GPU they are
+        # sketched on a second context in a helper thread while this thread runs pass 1 (the KLL compactions are
+        # VALU-bound, pass 1's string scan latency-bound); DQ_PROFILE_NO_EARLY_KLL=1 keeps them in pass 2
+        kll_early = []
+        kll_pending = None
+        if early and type(passes) is LocalPasses and not os.environ.get("DQ_PROFILE_SERIAL") and \
+                not os.environ.get("DQ_PROFILE_NO_EARLY_KLL"):
+            from .runners import _beside
+            kll_an = [KLLSketch(name, kllParameters) for name in early]
+            kll_pending = _beside(lambda: passes.run(data, kll_an), "kll")
+            if kll_pending is not None:
+                kll_early = list(early)
+        try:
+            res1 = passes.run(data, first + [Size()])
+        except BaseException:
+            if kll_pending is not None:
+                kll_pending.join()
+            raise
         generic = ColumnProfiler._extract_generic(relevant, schema, res1, predefinedTypes)
 
         # pass 3's columns depend on pass 1 only: on this process's GPU its histogram builds run on a second context
@@ -217,8 +234,13 @@ class ColumnProfiler:
                                          DataTypeInstances.Integral, DataTypeInstances.Fractional) and
                    cnt <= lowCardinalityHistogramThreshold]
         pending = None
-        if targets and type(passes) is LocalPasses and not os.environ.get("DQ_PROFILE_SERIAL"):
-            pending = _histograms_beside(passes, data, targets)  # None: the passes stay on this thread
+        try:
+            if targets and type(passes) is LocalPasses and not os.environ.get("DQ_PROFILE_SERIAL"):
+                pending = _histograms_beside(passes, data, targets)  # None: the passes stay on this thread
+        except BaseException:
+            if kll_pending is not None:
+                kll_pending.join()
+            raise
 
         try:
             # ---- pass 2 ------------------------------------------------------------------------------
@@ -230,14 +252,18 @@ class ColumnProfiler:
                      for name in numeric}
             casted = _cast_table(passes, data, casts)
             second = []
-            early_set = set(early)
+            early_set, kll_early_set = set(early), set(kll_early)
             for name in numeric:
                 if name not in early_set:
                     second += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
-                second += [KLLSketch(name, kllParameters)]
+                if name not in kll_early_set:
+                    second += [KLLSketch(name, kllParameters)]
             res2 = passes.run(casted, second) if second else None
-            if early and res2 is not None:
-                res2 = res1 + res2
+            if early:
+                res2 = res1 if res2 is None else res1 + res2
+            if kll_pending is not None:
+                kres = kll_pending.result()
+                res2 = kres if res2 is None else res2 + kres
             stats = ColumnProfiler._extract_numeric(res2, numeric, kllParameters)
 
             # ---- pass 3 ------------------------------------------------------------------------------
@@ -247,9 +273,11 @@ class ColumnProfiler:
                 histograms = pending.result()
             else:
                 histograms = passes.histograms(data, targets) if targets else {}
-        finally:  # a failing pass 2 does not leave the histogram helper driving its context
+        finally:  # a failing pass 2 does not leave the histogram or KLL helper driving its context
             if pending is not None:
                 pending.join()
+            if kll_pending is not None:
+                kll_pending.join()
 
         profiles = {}
         for name in relevant:
