@@ -606,7 +606,11 @@ class KLLSketch(ScanShareableAnalyzer):
 
 # ---- grouping analyzers (A/GroupingAnalyzers.scala) ----------------------------------------------
 def _host_key_column(col):
-    """A key column with host buffers (device-resident columns are copied back once)."""
+    """A key column with host buffers (device-resident columns are copied back once; a parted column's chunks are
+    concatenated on the host)."""
+    from .table import PartedColumn, _concat_host
+    if isinstance(col, PartedColumn):
+        return _concat_host([_host_key_column(p) for p in col.parts])
     if getattr(col, "values", None) is not None or not getattr(col, "device", None):
         return col
     from .distributed import _host_column

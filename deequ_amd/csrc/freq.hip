@@ -87,11 +87,22 @@ struct KeyCol {
     const int64_t* offsets64;  // DQ_COL_OFFSETS64: int64 offsets instead (a column past 2^31 bytes)
     int32_t spark_type;
     int32_t elem;
+    // dq_frequencies_parts: rows >= split live in a second part (its own buffers, its row split + i); 0 = one part
+    int64_t split;
+    const void* values2;
+    const uint8_t* validity2;
+    const int32_t* offsets2;
 };
 
 // Row r's UTF-8 bytes of a string key column: start pointer and length.
 __host__ __device__ __forceinline__ const uint8_t* str_span(const KeyCol& c, int64_t r, int& len) {
     int64_t o0, o1;
+    if (c.split && r >= c.split) {  // the second part (int32 offsets of its own)
+        const int64_t q = r - c.split;
+        o0 = c.offsets2[q];
+        len = (int)(c.offsets2[q + 1] - o0);
+        return static_cast<const uint8_t*>(c.values2) + o0;
+    }
     if (c.offsets64) {
         o0 = c.offsets64[r];
         o1 = c.offsets64[r + 1];
@@ -157,19 +168,28 @@ __host__ __device__ __forceinline__ uint64_t unmix64(uint64_t z) {
 __device__ __forceinline__ unsigned int region_probe(uint64_t h) { return (unsigned int)(h >> 52) & (kRegion - 1); }
 
 __device__ __forceinline__ bool is_valid(const KeyCol& c, int64_t r) {
+    if (c.split && r >= c.split) {
+        r -= c.split;
+        return c.validity2 == nullptr || ((c.validity2[r >> 3] >> (r & 7)) & 1);
+    }
     return c.validity == nullptr || ((c.validity[r >> 3] >> (r & 7)) & 1);
 }
 
 // Canonical 64-bit value of a fixed-width cell (the grouping equality of Spark's UnsafeRow bytes).
 __device__ __forceinline__ uint64_t canonical(const KeyCol& c, int64_t r) {
+    const void* vals = c.values;
+    if (c.split && r >= c.split) {
+        r -= c.split;
+        vals = c.values2;
+    }
     switch (c.elem) {
-        case ET_U8: return static_cast<const uint8_t*>(c.values)[r] ? 1ull : 0ull;
-        case ET_I8: return (uint64_t)(int64_t) static_cast<const int8_t*>(c.values)[r];
-        case ET_I16: return (uint64_t)(int64_t) static_cast<const int16_t*>(c.values)[r];
-        case ET_I32: return (uint64_t)(int64_t) static_cast<const int32_t*>(c.values)[r];
-        case ET_F32: return (uint64_t)float_to_int_bits(static_cast<const float*>(c.values)[r]);
-        case ET_F64: return double_to_long_bits(static_cast<const double*>(c.values)[r]);
-        default: return static_cast<const uint64_t*>(c.values)[r];
+        case ET_U8: return static_cast<const uint8_t*>(vals)[r] ? 1ull : 0ull;
+        case ET_I8: return (uint64_t)(int64_t) static_cast<const int8_t*>(vals)[r];
+        case ET_I16: return (uint64_t)(int64_t) static_cast<const int16_t*>(vals)[r];
+        case ET_I32: return (uint64_t)(int64_t) static_cast<const int32_t*>(vals)[r];
+        case ET_F32: return (uint64_t)float_to_int_bits(static_cast<const float*>(vals)[r]);
+        case ET_F64: return double_to_long_bits(static_cast<const double*>(vals)[r]);
+        default: return static_cast<const uint64_t*>(vals)[r];
     }
 }
 
@@ -3305,12 +3325,14 @@ int dq_frequencies(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nro
     return dq_frequencies_ex(ctx, columns, ncols, nrows, key_columns, nkeys, &o, out);
 }
 
+static int finish_frequencies(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, const dq_freq_options* opt,
+                              std::vector<void*>& staged, dq_freq_table** out);
+
 int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
                       int nkeys, const dq_freq_options* opt, dq_freq_table** out) {
     if (!ctx || !out || !opt || nkeys <= 0 || nkeys > kMaxKeys || nrows < 0)
         return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_frequencies: invalid arguments");
     if (!ctx->subs.empty()) return multi_frequencies(ctx, columns, ncols, nrows, key_columns, nkeys, opt, out);
-    const uint32_t flags = opt->flags;
     *out = nullptr;
     const int dev = dq::ctx_device(ctx);
     FQ_HIP(ctx, hipSetDevice(dev));
@@ -3377,6 +3399,18 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
             return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_frequencies: unsupported key type");
         }
     }
+    t->ks.ncols = nkeys;
+    return finish_frequencies(ctx, t, nrows, opt, staged, out);
+}
+
+// The common tail of dq_frequencies_ex / dq_frequencies_parts: `t->ks.cols[0 .. nkeys)` are set up.
+static int finish_frequencies(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, const dq_freq_options* opt,
+                              std::vector<void*>& staged, dq_freq_table** out) {
+    const uint32_t flags = opt->flags;
+    hipStream_t s = dq::ctx_stream(ctx);
+    auto cleanup = [&]() {
+        for (void* p : staged) (void)hipFree(p);
+    };
     if (opt->weights && nrows > 0) {
         if (opt->weights_device) {
             t->ks.weights = reinterpret_cast<const long long*>(opt->weights);
@@ -3388,10 +3422,11 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
             t->ks.weights = reinterpret_cast<const long long*>(w);
         }
     }
+    const int nkeys = t->ks.ncols;
     t->key_type = opt->key_type ? opt->key_type : t->ks.cols[0].spark_type;
-    t->ks.ncols = nkeys;
     t->ks.include_nulls = (flags & DQ_FREQ_INCLUDE_NULLS) ? 1 : 0;
-    t->ks.fast = (nkeys == 1 && t->ks.cols[0].spark_type != DQ_TYPE_STRING) ? 1 : 0;
+    // the fast build reads one fixed-width column's values directly: one part only
+    t->ks.fast = (nkeys == 1 && t->ks.cols[0].spark_type != DQ_TYPE_STRING && !t->ks.cols[0].split) ? 1 : 0;
     t->ks.string_null_is_value = (t->ks.include_nulls && nkeys == 1 && t->ks.cols[0].spark_type == DQ_TYPE_STRING);
     t->fast = t->ks.fast;
     t->ks.seed = 0x243F6A8885A308D3ULL;
@@ -3411,6 +3446,55 @@ int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t 
     t->staged = staged;
     *out = t;
     return DQ_OK;
+}
+
+int dq_frequencies_parts(dq_ctx* ctx, const dq_column* parts, int nparts, int ncols, const int32_t* key_columns,
+                         int nkeys, const dq_freq_options* opt, dq_freq_table** out) {
+    if (!ctx || !out || !opt || !parts || nparts <= 0 || ncols <= 0 || nkeys <= 0 || nkeys > kMaxKeys)
+        return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT, "dq_frequencies_parts: invalid arguments");
+    if (nparts == 1) return dq_frequencies_ex(ctx, parts, ncols, parts[0].length, key_columns, nkeys, opt, out);
+    if (nparts != 2 || !ctx->subs.empty() || opt->weights)
+        return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED,
+                            "dq_frequencies_parts: two parts on a one-device context, unweighted (else concatenate)");
+    *out = nullptr;
+    const int64_t n0 = parts[0].length, n1 = parts[ncols].length;
+    FQ_HIP(ctx, hipSetDevice(dq::ctx_device(ctx)));
+    dq_freq_table* t = new dq_freq_table();
+    t->device = dq::ctx_device(ctx);
+    t->src_rows = n0 + n1;
+    memset(&t->ks, 0, sizeof(t->ks));
+    for (int i = 0; i < nkeys; ++i) {
+        const int c = key_columns[i];
+        const dq_column* a = c >= 0 && c < ncols ? &parts[c] : nullptr;
+        const dq_column* b = c >= 0 && c < ncols ? &parts[ncols + c] : nullptr;
+        if (!a || !(a->flags & DQ_COL_DEVICE) || !(b->flags & DQ_COL_DEVICE) || (a->flags & DQ_COL_OFFSETS64) ||
+            (b->flags & DQ_COL_OFFSETS64) || a->spark_type != b->spark_type || a->length != n0 || b->length != n1 ||
+            (elem_of(a->spark_type) == ET_NONE && a->spark_type != DQ_TYPE_STRING)) {
+            delete t;
+            return dq::ctx_fail(ctx, DQ_ERR_INVALID_ARGUMENT,
+                                "dq_frequencies_parts: key parts must be device columns of one type, int32 offsets");
+        }
+        KeyCol& kc = t->ks.cols[i];
+        kc.spark_type = a->spark_type;
+        kc.elem = elem_of(a->spark_type);
+        kc.values = a->values;
+        kc.validity = a->validity;
+        kc.offsets = a->offsets;
+        kc.offsets64 = nullptr;
+        if (n0 > 0) {  // an empty first part: the second part alone is the column
+            kc.split = n0;
+            kc.values2 = b->values;
+            kc.validity2 = b->validity;
+            kc.offsets2 = b->offsets;
+        } else {
+            kc.values = b->values;
+            kc.validity = b->validity;
+            kc.offsets = b->offsets;
+        }
+    }
+    t->ks.ncols = nkeys;
+    std::vector<void*> staged;
+    return finish_frequencies(ctx, t, n0 + n1, opt, staged, out);
 }
 
 int dq_freq_key_kind(const dq_freq_table* t) { return !t ? -1 : (t->fast ? DQ_FREQ_KEYS_VALUES : DQ_FREQ_KEYS_ROWS); }

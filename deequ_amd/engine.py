@@ -7,6 +7,7 @@ import threading
 import numpy as np
 
 from . import native as N
+from .table import PartedColumn
 
 _device = None
 
@@ -299,8 +300,22 @@ def frequencies(table, key_columns, include_nulls=False, weights=None):
     stands for that many rows (dq_frequencies_ex: the pre-aggregated groups of other shards)."""
     context = ctx()
     names = list(table.columns)
-    cols = [table[c].native() for c in names]
     keys = np.array([names.index(c) for c in key_columns], dtype=np.int32)
+    parted = [table[c] for c in names if isinstance(table[c], PartedColumn)]
+    if parted:  # a ChunkedTable's columns read in place (dq_frequencies_parts): part-major column array
+        if weights is not None or len(parted) != len(names):
+            raise TypeError("a parted table takes an unweighted grouping over parted columns only")
+        per = [table[c].native_parts() for c in names]
+        nparts = len(per[0])
+        arr = (N.DqColumn * (nparts * len(names)))(*[per[c][p] for p in range(nparts) for c in range(len(names))])
+        opt = N.DqFreqOptions()
+        opt.flags = N.FREQ_INCLUDE_NULLS if include_nulls else 0
+        handle = ctypes.c_void_p()
+        rc = context.lib.dq_frequencies_parts(context.handle, arr, nparts, len(names), keys.ctypes.data, len(keys),
+                                              ctypes.byref(opt), ctypes.byref(handle))
+        context.check(rc, "dq_frequencies_parts")
+        return FrequencyTable(context, handle, table, key_columns, include_nulls)
+    cols = [table[c].native() for c in names]
     arr = (N.DqColumn * max(len(cols), 1))(*cols)
     handle = ctypes.c_void_p()
     flags = N.FREQ_INCLUDE_NULLS if include_nulls else 0

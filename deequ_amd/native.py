@@ -62,7 +62,7 @@ EXPORTED_SYMBOLS = (
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts", "dq_synth_strings",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
     "dq_scan_streamed", "dq_scan_kernel_launches", "dq_freq_path_count", "dq_kll_sketch_columns",
-    "dq_kll_merge_states", "dq_scratch_trim",
+    "dq_kll_merge_states", "dq_scratch_trim", "dq_frequencies_parts",
 )
 
 
@@ -203,6 +203,7 @@ def load_library(path=None):
             "dq_set_stream": (c_int, [c_void_p, c_void_p]),
             "dq_synchronize": (c_int, [c_void_p]),
             "dq_scratch_trim": (None, [c_void_p, c_int64]),
+            "dq_frequencies_parts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
             "dq_scan": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                 c_uint32]),
             "dq_scan_launch_count": (c_int64, [c_void_p]),

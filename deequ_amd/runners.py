@@ -449,7 +449,7 @@ class AnalysisRunner:
             for k, (cset, group) in enumerate(sets):
                 def run_set(cset=cset, group=group):
                     cols = [c for c in cset if c in data]
-                    return AnalysisRunner.doAnalysisRun(data.concat(cols), group, aggregateWith, saveStatesWith)
+                    return AnalysisRunner.doAnalysisRun(data.grouping_view(cols), group, aggregateWith, saveStatesWith)
                 last_here = not analyzers and k == len(sets) - 1
                 h = None if last_here or k >= 3 else helpers.beside(run_set, "group%d" % k)
                 if h is None:

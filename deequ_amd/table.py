@@ -221,6 +221,35 @@ class PartedColumn(Column):
     def native_parts(self):
         return [p.native() for p in self.parts]
 
+    def _locate(self, i):
+        """(part, row inside it) of row i of the concatenation."""
+        for p in self.parts:
+            if i < p.length:
+                return p, i
+            i -= p.length
+        raise IndexError(i)
+
+    def valid_at(self, i):
+        p, j = self._locate(int(i))
+        return p.valid_at(j)
+
+    def value_at(self, i):
+        p, j = self._locate(int(i))
+        return p.value_at(j)
+
+    def cells_at(self, rows):
+        """The cells of `rows` (indices into the concatenation): one batched gather per part."""
+        rows = np.asarray(rows, dtype=np.int64)
+        out = [None] * len(rows)
+        base = 0
+        for p in self.parts:
+            sel = np.flatnonzero((rows >= base) & (rows < base + p.length))
+            if len(sel):
+                for k, v in zip(sel.tolist(), p.cells_at(rows[sel] - base)):
+                    out[k] = v
+            base += p.length
+        return out
+
 
 def _column_from_pylist(name, spark_type, items):
     t = spark_type_of(spark_type)
@@ -526,6 +555,20 @@ class ChunkedTable:
         """The named columns as PartedColumns over the chunks (no copy): the ApproxQuantile summaries of the shard
         read every chunk in one dq_quantile_summaries call."""
         return Table([PartedColumn([c[n] for c in self.chunks]) for n in names])
+
+    def grouping_view(self, names):
+        """The key columns of a grouping over the whole shard: read in place as two parts (dq_frequencies_parts) when
+        the shard is two device chunks and a key is a string (the general build, no HBM concatenation and no host
+        synchronisation), else concatenated (a fixed-width single key keeps the fast build over one column).
+        DQ_GROUP_CONCAT=1 always concatenates."""
+        import os
+        cols = [self.chunks[0][n] for n in names]
+        if len(self.chunks) == 2 and not os.environ.get("DQ_GROUP_CONCAT") and \
+                any(c.spark_type == N.TYPE_STRING for c in cols) and \
+                all(ch[n].device is not None and not getattr(ch[n], "offsets64", False)
+                    for ch in self.chunks for n in names):
+            return self.parted(names)
+        return self.concat(names)
 
 
 def _infer_py_type(items):

@@ -364,6 +364,13 @@ typedef struct dq_freq_options {
 } dq_freq_options;
 int dq_frequencies_ex(dq_ctx* ctx, const dq_column* columns, int ncols, int64_t nrows, const int32_t* key_columns,
                       int nkeys, const dq_freq_options* options, dq_freq_table** table);
+/* dq_frequencies_ex over a table held as row-range parts read where they lie (the row chunks of a ChunkedTable, no
+ * concatenation): parts[p * ncols + c] is column c's part p, device columns with int32 offsets; the table's rows are
+ * the parts in order (exported representative rows are indices into that order). Two parts on a one-device context,
+ * unweighted (r06); other shapes return DQ_ERR_UNSUPPORTED and the caller concatenates. The fast fixed-width build
+ * reads one part only, so a fixed-width single key takes the general path here. */
+int dq_frequencies_parts(dq_ctx* ctx, const dq_column* parts, int nparts, int ncols, const int32_t* key_columns,
+                         int nkeys, const dq_freq_options* options, dq_freq_table** table);
 
 /* Every group of a DQ_FREQ_KEYS_VALUES table as (canonical key, count) into device arrays (the NULL group of a
  * DQ_FREQ_INCLUDE_NULLS table is summary.null_count, not exported). Returns the number written or < 0. */
