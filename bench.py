@@ -358,10 +358,17 @@ def c5_extra_analyzers(D):
 
 
 def c5_step(D, t, extras):
-    """One C5 step: the 3-pass ColumnProfiler + one AnalysisRunner run of the extra analyzers."""
-    prof = D.ColumnProfiler.profile(t)
-    ctx = D.AnalysisRunner.onData(t).addAnalyzers(extras).run()
-    return prof, ctx
+    """One C5 step: the 3-pass ColumnProfiler + one AnalysisRunner run of the extra analyzers, the run submitted on a
+    helper context (runAsync) so it overlaps the profiler's passes (DQ_C5_SEQUENTIAL=1: one after the other)."""
+    if os.environ.get("DQ_C5_SEQUENTIAL"):
+        prof = D.ColumnProfiler.profile(t)
+        return prof, D.AnalysisRunner.onData(t).addAnalyzers(extras).run()
+    pending = D.AnalysisRunner.onData(t).addAnalyzers(extras).runAsync()
+    try:
+        prof = D.ColumnProfiler.profile(t)
+    finally:
+        pending.join()
+    return prof, pending.result()
 
 
 def bench_c5(torch, N, D, ctx, dev, rows, steps):

@@ -49,6 +49,19 @@ class _Pending:
         return self.value
 
 
+class _Done:
+    """A result computed on the calling thread, behind _Pending's interface."""
+
+    def __init__(self, value):
+        self.value, self.error = value, None
+
+    def join(self):
+        pass
+
+    def result(self):
+        return self.value
+
+
 def _beside(fn, slot):
     """Run fn in a helper thread on a second context of this thread's device (own stream and scratch, leased to this
     helper alone), or None when the work must stay on this thread (DQ_RUN_SERIAL, a multi-device context, or already
@@ -308,6 +321,15 @@ class AnalysisRunBuilder:
 
     def run(self):
         return AnalysisRunner.doAnalysisRun(self.data, self.analyzers, self._aggregateWith, self._saveStatesWith)
+
+    def runAsync(self):
+        """run() on a helper context of this thread's device (own stream and scratch) in a helper thread, beside the
+        caller's next GPU work: a Spark application submitting two jobs from two threads (e.g. the ColumnProfiler's
+        passes and a VerificationSuite over the same table). Returns a handle: result() is the AnalyzerContext (a
+        failure re-raised), join() waits. The caller joins it before it frees the table. Where run() cannot go to a
+        helper (DQ_RUN_SERIAL, a multi-device context, already on a helper) it runs here and the handle is done."""
+        h = _beside(self.run, "async")
+        return h if h is not None else _Done(self.run())
 
 
 class KLLRunner:

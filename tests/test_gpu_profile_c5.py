@@ -277,3 +277,32 @@ def test_c5_quantiles_and_grouping_against_oracle():
     cut = [0, ROWS // 3, ROWS // 3 + ROWS // 4 + 7, ROWS]
     ct = D.ChunkedTable([Table.from_arrow(pat.slice(a, b - a)).to_device() for a, b in zip(cut, cut[1:])])
     _check_c5_extras(full, D.AnalysisRunner.onData(ct).addAnalyzers(extras).run(), extras)
+
+
+def test_c5_step_runs_the_extras_beside_the_profiler(monkeypatch):
+    """bench.py's C5 step submits the extra analyzers with runAsync (a helper context) and profiles meanwhile: the
+    extras' metrics pass the oracle checks and the profile equals the one the sequential step computes."""
+    import bench
+    pat = c5_arrow(ROWS)
+    full = Table.from_arrow(pat)
+    cut = [0, ROWS // 2 + 11, ROWS]
+    ct = D.ChunkedTable([Table.from_arrow(pat.slice(a, b - a)).to_device() for a, b in zip(cut, cut[1:])])
+    extras = [D.ApproxQuantile(c, 0.5) for c in pat.column_names[:10]]
+    extras += [D.Uniqueness(["s_cat100"]), D.Entropy("s_cat100"), D.Uniqueness(["s_text0"]), D.Entropy("s_text0")]
+    monkeypatch.delenv("DQ_C5_SEQUENTIAL", raising=False)
+    prof, actx = bench.c5_step(D, ct, extras)
+    _check_c5_extras(full, actx, extras)
+    monkeypatch.setenv("DQ_C5_SEQUENTIAL", "1")
+    prof2, actx2 = bench.c5_step(D, ct, extras)
+    for a in extras:
+        assert actx.metric(a).value.get() == actx2.metric(a).value.get(), a
+    assert prof.numRecords == prof2.numRecords == ROWS
+    for name, p in prof2.profiles.items():
+        q = prof.profiles[name]
+        assert (q.completeness, q.approximateNumDistinctValues, q.dataType) == \
+            (p.completeness, p.approximateNumDistinctValues, p.dataType), name
+        if isinstance(p, D.NumericColumnProfile):
+            assert (q.minimum, q.maximum, q.sum, q.mean, q.stdDev) == (p.minimum, p.maximum, p.sum, p.mean, p.stdDev)
+        assert (q.histogram is None) == (p.histogram is None), name
+        if p.histogram is not None:
+            assert q.histogram == p.histogram, name

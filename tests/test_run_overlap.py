@@ -114,3 +114,22 @@ def test_aux_contexts_are_leased_to_one_thread_at_a_time(monkeypatch):
     N.release_aux_context(a)
     N.release_aux_context(b)
     assert not N._aux_leased - {id(c) for pool in N._aux_pool.values() for c in pool if c.device == 1}
+
+
+def test_run_async_is_a_helper_run_or_done_here(monkeypatch):
+    """AnalysisRunBuilder.runAsync: run() handed to a helper slot "async", or computed on this thread (a done handle)
+    where no helper may be used."""
+    sentinel = object()
+    monkeypatch.setattr(runners.AnalysisRunner, "doAnalysisRun", staticmethod(lambda *a: sentinel))
+    monkeypatch.setenv("DQ_RUN_SERIAL", "1")
+    h = runners.AnalysisRunBuilder(None).runAsync()
+    assert isinstance(h, runners._Done) and h.result() is sentinel
+    monkeypatch.delenv("DQ_RUN_SERIAL")
+    slots = []
+
+    def fake_beside(fn, slot):
+        slots.append(slot)
+        return runners._Pending(fn)
+    monkeypatch.setattr(runners, "_beside", fake_beside)
+    assert runners.AnalysisRunBuilder(None).runAsync().result() is sentinel
+    assert slots == ["async"]
