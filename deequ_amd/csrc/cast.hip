@@ -231,15 +231,21 @@ int ctx_cus(dq_ctx* ctx);
 }  // namespace dq
 
 namespace {
+// Per-call device buffers from the context's scratch cache: a hipFree per cast waited for the whole device, so a cast
+// stalled behind every other context's running kernels (the C5 step's casts sat idle for ~20 ms between columns).
 struct CBuffers {
-    std::vector<void*> ptrs;
+    dq_ctx* ctx;
+    std::vector<std::pair<void*, size_t>> ptrs;
+    explicit CBuffers(dq_ctx* c) : ctx(c) {}
     ~CBuffers() {
-        for (void* p : ptrs) (void)hipFree(p);
+        for (const auto& p : ptrs) dq::scratch_release(ctx, p.first, p.second);
     }
     hipError_t alloc(void** p, size_t bytes) {
-        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
-        if (e == hipSuccess) ptrs.push_back(*p);
-        return e;
+        bytes = std::max<size_t>(bytes, 16);
+        *p = dq::scratch_alloc(ctx, bytes);
+        if (!*p) return hipErrorOutOfMemory;
+        ptrs.push_back({*p, bytes});
+        return hipSuccess;
     }
 };
 }  // namespace
@@ -317,7 +323,7 @@ static int cast_single(dq_ctx* ctx, const dq_column* column, int64_t nrows, int3
     if (nrows == 0) return DQ_OK;
     CA_HIP(ctx, hipSetDevice(dq::ctx_device(ctx)));
     hipStream_t s = dq::ctx_stream(ctx);
-    CBuffers buf;
+    CBuffers buf(ctx);
     if (column->flags & DQ_COL_OFFSETS64)
         return dq::ctx_fail(ctx, DQ_ERR_UNSUPPORTED, "dq_cast_column: int64 string offsets are for the grouping builds only");
     dq::CastSource c;

@@ -2100,6 +2100,9 @@ struct dq_freq_table {
     // through that context (any other way: hipFree)
     dq_ctx* home = nullptr;
     size_t slots_bytes = 0, reps_bytes = 0;
+    // ctr / scratch come from this context's scratch cache (a hipFree waits for the whole device: freeing a table on
+    // one thread must not stall while other contexts' kernels run)
+    dq_ctx* buf_home = nullptr;
 };
 
 namespace {
@@ -2118,8 +2121,13 @@ void release_slots(dq_freq_table* t, dq_ctx* ctx) {
 
 void free_table_buffers(dq_freq_table* t, dq_ctx* ctx) {
     release_slots(t, ctx);
-    if (t->ctr) (void)hipFree(t->ctr);
-    if (t->scratch) (void)hipFree(t->scratch);
+    const bool cache = ctx && ctx == t->buf_home;
+    if (t->ctr) {
+        if (cache) dq::scratch_release(ctx, t->ctr, sizeof(Counters)); else (void)hipFree(t->ctr);
+    }
+    if (t->scratch) {
+        if (cache) dq::scratch_release(ctx, t->scratch, t->scratch_bytes); else (void)hipFree(t->scratch);
+    }
     t->slots = nullptr;
     t->reps = nullptr;
     t->ctr = nullptr;
@@ -3433,7 +3441,13 @@ static int finish_frequencies(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, cons
     t->ks.fp_mask = ~0ull;
     if (const char* m = getenv("DQ_FREQ_FP_MASK")) t->ks.fp_mask = strtoull(m, nullptr, 0);
 
-    FQ_HIP(ctx, hipMalloc(&t->ctr, sizeof(Counters)));
+    t->buf_home = ctx;
+    t->ctr = (Counters*)dq::scratch_alloc(ctx, sizeof(Counters));
+    if (!t->ctr) {
+        cleanup();
+        delete t;
+        return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
+    }
     int rc = build_table(ctx, t, nrows);
     if (rc) {
         cleanup();
@@ -3442,7 +3456,13 @@ static int finish_frequencies(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, cons
         return rc;
     }
     t->scratch_bytes = kScanBlocks * (sizeof(SummaryPartial) + 3 * sizeof(unsigned long long)) + 2048 * 8 + 256;
-    FQ_HIP(ctx, hipMalloc(&t->scratch, t->scratch_bytes));
+    t->scratch = dq::scratch_alloc(ctx, t->scratch_bytes);
+    if (!t->scratch) {
+        cleanup();
+        free_table_buffers(t, ctx);
+        delete t;
+        return dq::ctx_fail(ctx, DQ_ERR_OUT_OF_MEMORY, "frequency table allocation failed");
+    }
     t->staged = staged;
     *out = t;
     return DQ_OK;
@@ -3608,15 +3628,14 @@ static int64_t compact(dq_ctx* ctx, const dq_freq_table* t, int mode, unsigned l
     if (n == 0) return 0;
     unsigned long long* dk = nullptr;
     unsigned long long* dc = nullptr;
-    if (hipMalloc(&dk, n * 8) != hipSuccess || hipMalloc(&dc, n * 8) != hipSuccess) return -1;
+    DevBuf buf(ctx);  // the context's scratch cache: no device-wide wait of a hipFree per export
+    if (buf.alloc((void**)&dk, n * 8) != hipSuccess || buf.alloc((void**)&dc, n * 8) != hipSuccess) return -1;
     if (hipMemcpyAsync(offsets, off.data(), kScanBlocks * 8, hipMemcpyHostToDevice, s) != hipSuccess) return -1;
     hipLaunchKernelGGL(compact_kernel, dim3(kScanBlocks), dim3(kFreqBlock), 0, s, t->slots, t->reps, t->cap, mode, thr,
                        offsets, (unsigned long long)n, dk, dc, 0);
     bool ok = hipMemcpyAsync(keys.data(), dk, n * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
               hipMemcpyAsync(counts.data(), dc, n * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
               hipStreamSynchronize(s) == hipSuccess;
-    (void)hipFree(dk);
-    (void)hipFree(dc);
     return ok ? (int64_t)n : -1;
 }
 

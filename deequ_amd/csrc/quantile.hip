@@ -507,15 +507,28 @@ double host_key_value(uint64_t k) {
 }
 
 // Device buffers released on every exit path.
+// Device buffers released on every exit path: from the context's scratch cache when `ctx` is set (a one-device
+// context: a hipFree waits for the whole device, stalling this call behind other contexts' kernels), else hipMalloc.
 struct QBuffers {
-    std::vector<void*> ptrs;
+    dq_ctx* ctx = nullptr;
+    std::vector<std::pair<void*, size_t>> ptrs;
     ~QBuffers() {
-        for (void* p : ptrs) (void)hipFree(p);
+        for (const auto& p : ptrs) {
+            if (ctx) dq::scratch_release(ctx, p.first, p.second);
+            else (void)hipFree(p.first);
+        }
     }
     hipError_t alloc(void** p, size_t bytes) {
-        hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
-        if (e == hipSuccess) ptrs.push_back(*p);
-        return e;
+        bytes = std::max<size_t>(bytes, 16);
+        if (ctx) {
+            *p = dq::scratch_alloc(ctx, bytes);
+            if (!*p) return hipErrorOutOfMemory;
+        } else {
+            hipError_t e = hipMalloc(p, bytes);
+            if (e != hipSuccess) return e;
+        }
+        ptrs.push_back({*p, bytes});
+        return hipSuccess;
     }
 };
 
@@ -631,6 +644,7 @@ int64_t dq_quantile_summary(dq_ctx* ctx, const dq_column* column, int64_t nrows,
     std::vector<std::vector<std::vector<int32_t>>> scratch(ns_dev);
     for (int i = 0; i < ns_dev; ++i) {
         sh[i].ctx = nsub > 0 ? dq::ctx_sub(ctx, i) : ctx;
+        if (nsub == 0) sh[i].buf.ctx = ctx;
         int64_t r0 = 0, cnt = nrows;
         if (nsub > 0) {
             dq::shard_bounds(nrows, nsub, i, &r0, &cnt);
