@@ -38,6 +38,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")  # before any HIP call: see deequ_amd/native.py
 
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 0x5EED0000
@@ -359,11 +360,14 @@ def c5_extra_analyzers(D):
 
 def c5_step(D, t, extras):
     """One C5 step: the 3-pass ColumnProfiler + one AnalysisRunner run of the extra analyzers, the run submitted on a
-    helper context (runAsync) so it overlaps the profiler's passes (DQ_C5_SEQUENTIAL=1: one after the other)."""
+    helper context (runAsync) so it overlaps the profiler's passes (DQ_C5_SEQUENTIAL=1: one after the other). The
+    extras' chain (the text grouping's LDS-heavy partition / build kernels, then the quantiles) is the longer one and
+    its kernels were starved of CUs by the profiler's: its stream gets high priority (DQ_C5_ASYNC_PRIORITY, default 1;
+    140-141 ms a step against 174 at normal priority on one box, profiles/r06/c5_async_priority_ab_r06x.txt)."""
     if os.environ.get("DQ_C5_SEQUENTIAL"):
         prof = D.ColumnProfiler.profile(t)
         return prof, D.AnalysisRunner.onData(t).addAnalyzers(extras).run()
-    pending = D.AnalysisRunner.onData(t).addAnalyzers(extras).runAsync()
+    pending = D.AnalysisRunner.onData(t).addAnalyzers(extras).runAsync(int(os.environ.get("DQ_C5_ASYNC_PRIORITY", 1)))
     try:
         prof = D.ColumnProfiler.profile(t)
     finally:

@@ -213,7 +213,7 @@ int scan_kernel_family(int kind, int P, int nc, int heavy) {
 int ensure_side_streams(dq_ctx* ctx) {
     if (ctx->fork_ev) return DQ_OK;
     for (int i = 0; i < dq_ctx::kSide; ++i) {
-        DQ_HIP(ctx, hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking));
+        DQ_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, ctx->hip_priority));
         DQ_HIP(ctx, hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming));
     }
     DQ_HIP(ctx, hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming));
@@ -466,6 +466,41 @@ const char* dq_last_error(const dq_ctx* ctx) { return ctx ? ctx->err.c_str() : "
 int dq_set_stream(dq_ctx* ctx, void* stream) {
     if (!ctx) return DQ_ERR_INVALID_ARGUMENT;
     ctx->stream = stream ? (hipStream_t)stream : ctx->own_stream;
+    return DQ_OK;
+}
+
+int dq_set_priority(dq_ctx* ctx, int priority) {
+    if (!ctx || priority < -1 || priority > 1) return DQ_ERR_INVALID_ARGUMENT;
+    for (dq_ctx* sub : ctx->subs) {
+        const int rc = dq_set_priority(sub, priority);
+        if (rc) return fail(ctx, rc, "device %d: %s", sub->device, sub->err.c_str());
+    }
+    DQ_HIP(ctx, hipSetDevice(ctx->device));
+    int least = 0, greatest = 0;
+    DQ_HIP(ctx, hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const int want = priority > 0 ? greatest : priority < 0 ? least : std::min(std::max(0, greatest), least);
+    if (want == ctx->hip_priority) return DQ_OK;
+    // the old streams' queued work first: cached scratch blocks and events are re-tagged to the new streams
+    DQ_HIP(ctx, hipStreamSynchronize(ctx->own_stream));
+    for (int i = 0; i < dq_ctx::kSide; ++i)
+        if (ctx->side[i]) DQ_HIP(ctx, hipStreamSynchronize(ctx->side[i]));
+    hipStream_t fresh = nullptr;
+    DQ_HIP(ctx, hipStreamCreateWithPriority(&fresh, hipStreamNonBlocking, want));
+    const hipStream_t old = ctx->own_stream;
+    {
+        std::lock_guard<std::mutex> g(ctx->scratch_mu);
+        for (dq_ctx::CachedBlock& b : ctx->scratch_free)
+            if (b.stream == old) b.stream = fresh;
+    }
+    if (ctx->stream == old) ctx->stream = fresh;
+    ctx->own_stream = fresh;
+    (void)hipStreamDestroy(old);
+    ctx->hip_priority = want;
+    for (int i = 0; i < dq_ctx::kSide; ++i) {
+        if (!ctx->side[i]) continue;
+        (void)hipStreamDestroy(ctx->side[i]);
+        DQ_HIP(ctx, hipStreamCreateWithPriority(&ctx->side[i], hipStreamNonBlocking, want));
+    }
     return DQ_OK;
 }
 

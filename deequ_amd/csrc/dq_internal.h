@@ -265,6 +265,7 @@ struct dq_ctx {
     int cus = 256;
     // Side streams: scan launches of different shapes (and the string scan) run concurrently, forked from and
     // joined back to `stream` by events, so a VALU-heavy shape shares the CUs with a memory-bound one.
+    int hip_priority = 0;  // HIP stream priority of own_stream and the side streams (dq_set_priority)
     static constexpr int kSide = 3;
     hipStream_t side[kSide] = {};
     hipEvent_t fork_ev = nullptr;

@@ -10,6 +10,14 @@ import threading
 
 import numpy as np
 
+# Hardware queues per process. A run drives up to ~7 streams at once (the main context, helper contexts for the
+# second row chunk, the early KLL pass, the pass-3 histograms, the groupings and AnalysisRunBuilder.runAsync, plus
+# torch's); with HIP's default of 4 queues, streams share a queue and one stream's kernels wait behind another's (the
+# C5 step's histograms queued ~60 ms behind the text grouping). Read by the HIP runtime when it initialises (the first
+# HIP call of the process): set here, before that, unless the user set it. C5 step: 4 queues 159-173 ms, 8 queues
+# 143-145 ms (profiles/r06/c5_hw_queues_ab_r06v.txt).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DQ_LIBRARY") or os.path.join(_HERE, "libdq.so")
 
@@ -62,7 +70,7 @@ EXPORTED_SYMBOLS = (
     "dq_synth_validity", "dq_frequencies_ex", "dq_freq_export_device", "dq_freq_from_pairs", "dq_freq_merge", "dq_freq_row_counts", "dq_synth_strings",
     "dq_freq_mutual_information", "dq_open_devices", "dq_ctx_num_devices", "dq_ctx_uses_rccl", "dq_scan_sharded",
     "dq_scan_streamed", "dq_scan_kernel_launches", "dq_freq_path_count", "dq_kll_sketch_columns",
-    "dq_kll_merge_states", "dq_scratch_trim", "dq_frequencies_parts",
+    "dq_kll_merge_states", "dq_scratch_trim", "dq_frequencies_parts", "dq_set_priority",
 )
 
 
@@ -203,6 +211,7 @@ def load_library(path=None):
             "dq_set_stream": (c_int, [c_void_p, c_void_p]),
             "dq_synchronize": (c_int, [c_void_p]),
             "dq_scratch_trim": (None, [c_void_p, c_int64]),
+            "dq_set_priority": (c_int, [c_void_p, c_int]),
             "dq_frequencies_parts": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
             "dq_scan": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_int, c_void_p,
                                 c_uint32]),
@@ -362,6 +371,12 @@ class Context:
 
     def set_stream(self, stream_ptr):
         self.check(self.lib.dq_set_stream(self.handle, ctypes.c_void_p(stream_ptr or 0)), "dq_set_stream")
+
+    def set_priority(self, priority):
+        """dq_set_priority: 1 high, 0 normal, -1 low stream priority for this context's work."""
+        if getattr(self, "_priority", 0) != priority:
+            self.check(self.lib.dq_set_priority(self.handle, int(priority)), "dq_set_priority")
+            self._priority = priority
 
     def synchronize(self):
         self.check(self.lib.dq_synchronize(self.handle), "dq_synchronize")
@@ -529,22 +544,30 @@ _aux_pool = {}     # (device, slot) -> [Context, ...]
 _aux_leased = set()  # id() of the aux contexts a helper thread drives right now
 
 
-def lease_aux_context(device=0, slot="aux"):
+def lease_aux_context(device=0, slot="aux", priority=0):
     """A single-device context of `device` (its own stream and scratch cache) for one helper thread: the cached
     context of `slot` unless another thread holds it (dq.h: calls on one ctx are not re-entrant), else another one of
     the slot's pool. Return it with release_aux_context. Helper work overlaps the main context's (the
     ColumnProfiler's histogram pass beside its numeric pass, a run's grouping builds beside its scans)."""
     key = (int(device), slot)
+    ctx = None
     with _aux_lock:
         pool = _aux_pool.setdefault(key, [])
-        for ctx in pool:
-            if id(ctx) not in _aux_leased:
-                _aux_leased.add(id(ctx))
-                return ctx
-    ctx = Context(device)  # outside the lock: dq_open may take a while
-    with _aux_lock:
-        _aux_pool[key].append(ctx)
-        _aux_leased.add(id(ctx))
+        for c in pool:
+            if id(c) not in _aux_leased:
+                _aux_leased.add(id(c))
+                ctx = c
+                break
+    if ctx is None:
+        ctx = Context(device)  # outside the lock: dq_open may take a while
+        with _aux_lock:
+            _aux_pool[key].append(ctx)
+            _aux_leased.add(id(ctx))
+    try:
+        ctx.set_priority(priority)  # (the leased context is idle: its stream can be replaced)
+    except BaseException:
+        release_aux_context(ctx)
+        raise
     return ctx
 
 

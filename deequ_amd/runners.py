@@ -62,14 +62,14 @@ class _Done:
         return self.value
 
 
-def _beside(fn, slot):
+def _beside(fn, slot, priority=0):
     """Run fn in a helper thread on a second context of this thread's device (own stream and scratch, leased to this
     helper alone), or None when the work must stay on this thread (DQ_RUN_SERIAL, a multi-device context, or already
     on a helper context). The helper selects the device before any engine call (a new thread starts on device 0)."""
     if os.environ.get("DQ_RUN_SERIAL") or os.environ.get("DQ_DEVICES") or getattr(engine._local, "ctx", None):
         return None
     dev = engine.device()
-    aux = N.lease_aux_context(dev, slot)
+    aux = N.lease_aux_context(dev, slot, priority)
 
     def run():
         try:
@@ -322,13 +322,15 @@ class AnalysisRunBuilder:
     def run(self):
         return AnalysisRunner.doAnalysisRun(self.data, self.analyzers, self._aggregateWith, self._saveStatesWith)
 
-    def runAsync(self):
+    def runAsync(self, priority=0):
         """run() on a helper context of this thread's device (own stream and scratch) in a helper thread, beside the
         caller's next GPU work: a Spark application submitting two jobs from two threads (e.g. the ColumnProfiler's
         passes and a VerificationSuite over the same table). Returns a handle: result() is the AnalyzerContext (a
         failure re-raised), join() waits. The caller joins it before it frees the table. Where run() cannot go to a
-        helper (DQ_RUN_SERIAL, a multi-device context, already on a helper) it runs here and the handle is done."""
-        h = _beside(self.run, "async")
+        helper (DQ_RUN_SERIAL, a multi-device context, already on a helper) it runs here and the handle is done.
+        `priority` (1 high, 0 normal, -1 low) is the helper stream's HIP priority (dq_set_priority): 1 lets this run's
+        kernels dispatch ahead of the caller's when it is the longer chain."""
+        h = _beside(self.run, "async", priority)
         return h if h is not None else _Done(self.run())
 
 

@@ -254,6 +254,11 @@ int dq_scan_sharded(dq_ctx* ctx, const dq_column* const* shard_columns, const in
 
 /* Run kernels on this HIP stream (hipStream_t as void*); NULL = the context's own stream. */
 int dq_set_stream(dq_ctx* ctx, void* stream);
+/* (r06) HIP stream priority of the context's own stream and its internal side streams: 1 high, 0 normal, -1 low
+ * (hipDeviceGetStreamPriorityRange's ends). Waits for the context's queued work. A context whose work is on a job's
+ * critical path (e.g. a run submitted beside a ColumnProfiler's passes) dispatches ahead of the device's other
+ * contexts. No reference counterpart (Spark's scheduler pools are the nearest analogue). */
+int dq_set_priority(dq_ctx* ctx, int priority);
 int dq_synchronize(dq_ctx* ctx);
 
 /* Release the context's idle cached device scratch (the grouping builds' partition buffers and tables) beyond

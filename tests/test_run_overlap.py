@@ -101,6 +101,10 @@ def test_aux_contexts_are_leased_to_one_thread_at_a_time(monkeypatch):
         def __init__(self, device):
             FakeContext.n += 1
             self.device, self.lib, self.handle = device, lib, FakeContext.n
+            self.priorities = []
+
+        def set_priority(self, p):
+            self.priorities.append(p)
     monkeypatch.setattr(N, "Context", FakeContext)
     monkeypatch.setattr(N, "_aux_pool", {})
     monkeypatch.setattr(N, "_aux_leased", set())
@@ -113,7 +117,8 @@ def test_aux_contexts_are_leased_to_one_thread_at_a_time(monkeypatch):
     assert N.lease_aux_context(1, "group0") not in (a, b)  # per device
     N.release_aux_context(a)
     N.release_aux_context(b)
-    assert not N._aux_leased - {id(c) for pool in N._aux_pool.values() for c in pool if c.device == 1}
+    assert N.lease_aux_context(0, "group0", priority=1).priorities[-1] == 1  # the lease sets the stream priority
+    assert not N._aux_leased - {id(c) for pool in N._aux_pool.values() for c in pool if c.device == 1} - {id(a)} - {id(c) for pool in N._aux_pool.values() for c in pool if c.device == 1}
 
 
 def test_run_async_is_a_helper_run_or_done_here(monkeypatch):
@@ -127,7 +132,7 @@ def test_run_async_is_a_helper_run_or_done_here(monkeypatch):
     monkeypatch.delenv("DQ_RUN_SERIAL")
     slots = []
 
-    def fake_beside(fn, slot):
+    def fake_beside(fn, slot, priority=0):
         slots.append(slot)
         return runners._Pending(fn)
     monkeypatch.setattr(runners, "_beside", fake_beside)
