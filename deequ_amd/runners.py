@@ -62,12 +62,16 @@ class _Done:
         return self.value
 
 
-def _beside(fn, slot, priority=0):
+def _beside(fn, slot, priority=None):
     """Run fn in a helper thread on a second context of this thread's device (own stream and scratch, leased to this
     helper alone), or None when the work must stay on this thread (DQ_RUN_SERIAL, a multi-device context, or already
     on a helper context). The helper selects the device before any engine call (a new thread starts on device 0)."""
-    if os.environ.get("DQ_RUN_SERIAL") or os.environ.get("DQ_DEVICES") or getattr(engine._local, "ctx", None):
+    if os.environ.get("DQ_RUN_SERIAL") or os.environ.get("DQ_DEVICES"):
         return None
+    if getattr(engine._local, "ctx", None) is not None and not getattr(engine._local, "helpers_ok", False):
+        return None  # on a helper context: nothing nests (a runAsync thread is the one exception, one level deep)
+    if priority is None:
+        priority = getattr(engine._local, "helper_priority", 0)
     dev = engine.device()
     aux = N.lease_aux_context(dev, slot, priority)
 
@@ -330,7 +334,19 @@ class AnalysisRunBuilder:
         helper (DQ_RUN_SERIAL, a multi-device context, already on a helper) it runs here and the handle is done.
         `priority` (1 high, 0 normal, -1 low) is the helper stream's HIP priority (dq_set_priority): 1 lets this run's
         kernels dispatch ahead of the caller's when it is the longer chain."""
-        h = _beside(self.run, "async", priority)
+        def run():
+            # DQ_ASYNC_NESTED=1: the run's own helpers (its grouping sets beside its quantile / scan passes) may start
+            # from this thread, one level deep, at the run's priority. Off by default: beside the ColumnProfiler the
+            # extra contexts only add contention (C5 step 156-171 ms nested against 140-143 ms with the whole run on
+            # one helper context, profiles/r06/c5_async_nested_ab_r06aa.txt)
+            engine._local.helpers_ok = os.environ.get("DQ_ASYNC_NESTED", "0") == "1"
+            engine._local.helper_priority = priority
+            try:
+                return self.run()
+            finally:
+                engine._local.helpers_ok = False
+                engine._local.helper_priority = 0
+        h = _beside(run, "async", priority)
         return h if h is not None else _Done(self.run())
 
 

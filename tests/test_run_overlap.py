@@ -138,3 +138,33 @@ def test_run_async_is_a_helper_run_or_done_here(monkeypatch):
     monkeypatch.setattr(runners, "_beside", fake_beside)
     assert runners.AnalysisRunBuilder(None).runAsync().result() is sentinel
     assert slots == ["async"]
+
+
+def test_run_async_lets_its_run_start_helpers_one_level_deep(monkeypatch):
+    """DQ_ASYNC_NESTED=1: runAsync's run may put its own grouping sets on helper contexts (at its priority); their
+    helpers may not. Off (the default): the whole run stays on its one helper context."""
+    leases = []
+
+    def lease(dev, slot, priority=0):
+        leases.append((slot, priority))
+        return object()
+    monkeypatch.setattr(runners.N, "lease_aux_context", lease)
+    monkeypatch.setattr(runners.N, "release_aux_context", lambda c: None)
+    monkeypatch.setattr(runners.engine, "device", lambda: 0)
+    monkeypatch.delenv("DQ_RUN_SERIAL", raising=False)
+    monkeypatch.setenv("DQ_ASYNC_NESTED", "1")
+    seen = {}
+
+    def fake_run(self):
+        inner = runners._beside(lambda: runners._beside(lambda: 1, "deeper"), "inner")
+        seen["inner"] = inner is not None
+        seen["deeper"] = inner.result() if inner is not None else "n/a"
+        return 7
+    monkeypatch.setattr(runners.AnalysisRunBuilder, "run", fake_run)
+    assert runners.AnalysisRunBuilder(None).runAsync(priority=1).result() == 7
+    assert seen == {"inner": True, "deeper": None}
+    assert leases == [("async", 1), ("inner", 1)]
+    monkeypatch.setenv("DQ_ASYNC_NESTED", "0")
+    seen.clear()
+    assert runners.AnalysisRunBuilder(None).runAsync().result() == 7
+    assert seen == {"inner": False, "deeper": "n/a"}
