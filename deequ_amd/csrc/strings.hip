@@ -220,7 +220,7 @@ __device__ __forceinline__ void string_row(const StrSlot& s, const uint8_t* data
 #define DQ_STR_B128 1
 #endif
 #ifndef DQ_STR_STAGE
-#define DQ_STR_STAGE 512
+#define DQ_STR_STAGE 256  // words per 64-row group (r06: with DQ_STR_R 8, the same 32 KB of LDS per workgroup as 4 x 512)
 #endif
 constexpr int kStrStageWords = DQ_STR_STAGE;
 
@@ -356,8 +356,10 @@ __device__ __forceinline__ void st_string_row(const uint32_t* st, int o0, int o1
 // their offsets and validity words are loaded first, then the step's whole byte range is staged in the wave's LDS words
 // by buffer loads issued 8 per lane at a time (out-of-range words read as 0), so one step costs two dependent memory
 // round trips for 64 kStrR rows instead of two per 64. Ranges longer than the stage are read from HBM per lane.
+// (r06: 8 groups of 256 words, one step = 512 rows per wave, 12.70 ms against 13.26 ms for 4 groups of 512 words on the
+// ten C5 string columns of a 1.25e8-row chunk; 16 x 256 words: 21 ms. profiles/r06/c5_strings_r8_ab_r06af.txt)
 #ifndef DQ_STR_R
-#define DQ_STR_R 4
+#define DQ_STR_R 8
 #endif
 constexpr int kStrR = DQ_STR_R;
 
