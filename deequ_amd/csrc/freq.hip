@@ -57,7 +57,10 @@ constexpr uint64_t kEmpty = ~0ull;
 constexpr int kSizingRegs = 4096;  // HLL registers used only to size the table
 constexpr int kFreqBlock = 256;
 constexpr int kDigitBins = 256;    // radix partition: first pass on the low 8 bits of the key
-constexpr int kPartTile = 4096;    // keys per workgroup tile of the partition scatters (16 per lane), general path
+#ifndef DQ_PART_TILE
+#define DQ_PART_TILE 4096
+#endif
+constexpr int kPartTile = DQ_PART_TILE;  // keys per workgroup tile of the partition scatters (16 per lane), general path
 // fast pass 1 tile (keys per workgroup tile); measured on C4 end to end (profiles/r02/c4_p1_tile_r02bh.log):
 // 2048 -> 15.2-15.5 ms, 4096 -> 13.8-13.9 ms, 8192 -> 17.5 ms
 constexpr int kP1TileFast = 4096;
@@ -1678,7 +1681,13 @@ small_build_kernel(KeySpec ks, int64_t nrows, Slot* __restrict__ slots, unsigned
     __shared__ unsigned long long lrep[LS];
     __shared__ unsigned long long lb0[STR1 ? LS : 1], lb1[STR1 ? LS : 1];  // the representative's key words (STR1)
     __shared__ unsigned long long red[kBuildBlock / 64];
-    __shared__ unsigned int lovf, lfill;
+    __shared__ unsigned int lovf, lfill, lgone;
+    // the build is already lost (another workgroup's table filled): a workgroup that starts now does nothing. On a busy
+    // device this kernel's 36-40 KB workgroups get CUs one by one, and the optimistic try over a high-cardinality column
+    // took 14 ms to let every late workgroup fill its own table once (0.3 ms alone); small_check_kernel skips too
+    if (threadIdx.x == 0) lgone = *(volatile unsigned long long*)&ctr->overflow != 0 ? 1u : 0u;
+    __syncthreads();
+    if (lgone) return;  // (uniform: read after the barrier)
     for (int i = threadIdx.x; i < LS; i += kBuildBlock) {
         lkey[i] = kEmpty;
         lcnt[i] = 0;
@@ -1840,6 +1849,9 @@ __global__ void __launch_bounds__(kBuildBlock)
 small_check_kernel(KeySpec ks, const Slot* __restrict__ slots, const unsigned long long* __restrict__ reps,
                    const unsigned long long* __restrict__ wg_keys, const unsigned long long* __restrict__ wg_reps,
                    Counters* __restrict__ ctr) {
+    // a full table discards the build (the caller takes the regular path); the workgroups of small_build_kernel that
+    // found the overflow raised at their start published nothing
+    if (*(volatile unsigned long long*)&ctr->overflow) return;
     unsigned long long bad = 0;
     for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
         const unsigned long long key = wg_keys[(uint64_t)blockIdx.x * kRegion + i];
