@@ -1764,8 +1764,13 @@ __device__ __forceinline__ void where_emit(const WhereRegs& W, int64_t t, int ti
 // (the north-star suite) — the per-flag branches compile away.
 // WP (NC == 1): the slot is a `where` producer (sd.wout): its column's values and validity evaluate the filter, the
 // filter masks the slot's own rows and goes out as consumer masks (where_emit).
+// Minimum waves per SIMD for the north-star (FULL) instance. r06: 3 (168 VGPRs, 284 B of spills a lane) made suite10
+// 21.1 -> 34.9 ms (profiles/r06/suite10_minwaves_ab_r06ak.txt); the 256-VGPR, 2-wave form stays.
+#ifndef DQ_HEAVY8_MINW
+#define DQ_HEAVY8_MINW 1
+#endif
 template <int NC, bool F0, bool F1, bool FULL, bool WP = false>
-__global__ void __launch_bounds__(kBlock, 1)
+__global__ void __launch_bounds__(kBlock, FULL ? DQ_HEAVY8_MINW : 1)
 scan_heavy8_kernel(const SlotDesc* __restrict__ slots, const int32_t* __restrict__ group, int ngroup, int64_t nrows,
                    int64_t ntiles, int gstride, SlotPartial* __restrict__ partials, uint8_t* __restrict__ hll_partials) {
     using A0 = typename HAccOf<F0>::type;
