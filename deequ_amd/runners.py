@@ -70,8 +70,10 @@ def _beside(fn, slot, priority=None):
         return None
     if getattr(engine._local, "ctx", None) is not None and not getattr(engine._local, "helpers_ok", False):
         return None  # on a helper context: nothing nests (a runAsync thread is the one exception, one level deep)
-    if priority is None:
-        priority = getattr(engine._local, "helper_priority", 0)
+    if priority is None:  # a runAsync thread's helpers run at its priority; others at DQ_HELPER_PRIORITY (default 0)
+        priority = getattr(engine._local, "helper_priority", None)
+        if priority is None:
+            priority = int(os.environ.get("DQ_HELPER_PRIORITY", 0))
     dev = engine.device()
     aux = N.lease_aux_context(dev, slot, priority)
 
@@ -345,7 +347,7 @@ class AnalysisRunBuilder:
                 return self.run()
             finally:
                 engine._local.helpers_ok = False
-                engine._local.helper_priority = 0
+                engine._local.helper_priority = None
         h = _beside(run, "async", priority)
         return h if h is not None else _Done(self.run())
 

@@ -168,3 +168,17 @@ def test_run_async_lets_its_run_start_helpers_one_level_deep(monkeypatch):
     seen.clear()
     assert runners.AnalysisRunBuilder(None).runAsync().result() == 7
     assert seen == {"inner": False, "deeper": "n/a"}
+
+
+def test_helper_priority_default_from_the_environment(monkeypatch):
+    """Helpers started outside a runAsync thread take DQ_HELPER_PRIORITY (default 0)."""
+    leases = []
+    monkeypatch.setattr(runners.N, "lease_aux_context", lambda dev, slot, priority=0: leases.append(priority) or object())
+    monkeypatch.setattr(runners.N, "release_aux_context", lambda c: None)
+    monkeypatch.setattr(runners.engine, "device", lambda: 0)
+    monkeypatch.delenv("DQ_RUN_SERIAL", raising=False)
+    monkeypatch.delenv("DQ_HELPER_PRIORITY", raising=False)
+    assert runners._beside(lambda: 5, "x").result() == 5
+    monkeypatch.setenv("DQ_HELPER_PRIORITY", "-1")
+    assert runners._beside(lambda: 6, "x").result() == 6
+    assert leases == [0, -1]
