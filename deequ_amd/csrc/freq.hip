@@ -1344,9 +1344,9 @@ constexpr int kBuildBlock = 512;
 constexpr int kBuildUnroll = 8;
 
 // LDS counts: 32-bit for row counting (a work item holds <= kSliceRows rows), 64-bit for weighted input.
-template <typename C>
-__device__ __forceinline__ bool lds_insert(unsigned long long* lkey, C* lcnt, unsigned long long* lrep,
-                                           unsigned long long h, unsigned long long row, C w, bool general) {
+template <typename C, typename R = unsigned long long>
+__device__ __forceinline__ bool lds_insert(unsigned long long* lkey, C* lcnt, R* lrep, unsigned long long h, R row, C w,
+                                           bool general) {
     unsigned int p = region_probe(h);
     for (int probe = 0; probe < kRegion; ++probe) {
         const unsigned long long prev = atomicCAS(&lkey[p], kEmpty, h);
@@ -1365,7 +1365,9 @@ __device__ __forceinline__ bool lds_insert(unsigned long long* lkey, C* lcnt, un
 // region's final counts in LDS, so it writes its summary partial (parts[item]) and the table is never re-read for
 // the default N; a slice of a split bucket flags its partial (pad = 1) and the host scans the table instead.
 // NARROW: `hs` holds 32-bit narrow-key offsets (fast path), the key is mix64(base + offset).
-template <bool GENERAL, bool WEIGHTED, bool NARROW = false>
+// REP32 (general keys, < 2^32 - 1 source rows): the representatives as 32-bit rows in LDS (64 instead of 80 KB a
+// workgroup, so two fit a CU beside other kernels' workgroups), widened when the region is written.
+template <bool GENERAL, bool WEIGHTED, bool NARROW = false, bool REP32 = false>
 __global__ void __launch_bounds__(kBuildBlock)
 build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __restrict__ hs,
              const unsigned long long* __restrict__ rows, const long long* __restrict__ weights,
@@ -1373,15 +1375,17 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
              SummaryPartial* __restrict__ parts, double n, NarrowKey nk) {
     const uint32_t* __restrict__ hs32 = reinterpret_cast<const uint32_t*>(hs);
     using C = typename std::conditional<WEIGHTED, unsigned long long, unsigned int>::type;
+    using R = typename std::conditional<REP32, unsigned int, unsigned long long>::type;
     __shared__ unsigned long long lkey[kRegion];
     __shared__ C lcnt[kRegion];
-    __shared__ unsigned long long lrep[GENERAL ? kRegion : 1];
+    __shared__ R lrep[GENERAL ? kRegion : 1];
     __shared__ unsigned int lovf;
     const BuildItem it = items[blockIdx.x];
+    auto wide = [](R r) -> unsigned long long { return r == (R)~0ull ? ~0ull : (unsigned long long)r; };
     for (int i = threadIdx.x; i < kRegion; i += kBuildBlock) {
         lkey[i] = kEmpty;
         lcnt[i] = 0;
-        if (GENERAL) lrep[i] = ~0ull;
+        if (GENERAL) lrep[i] = (R)~0ull;
     }
     if (threadIdx.x == 0) lovf = 0;
     __syncthreads();
@@ -1403,7 +1407,7 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
 #pragma unroll
         for (int u = 0; u < kBuildUnroll; ++u)
             if (h[u] != kEmpty)
-                ok &= lds_insert<C>(lkey, lcnt, lrep, h[u], rw[u], WEIGHTED ? (C)weights[rw[u]] : (C)1, GENERAL);
+                ok &= lds_insert<C, R>(lkey, lcnt, lrep, h[u], (R)rw[u], WEIGHTED ? (C)weights[rw[u]] : (C)1, GENERAL);
     }
     if (!ok) lovf = 1;
     __syncthreads();
@@ -1416,7 +1420,7 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
             sl.key = lkey[i];
             sl.count = (unsigned long long)lcnt[i];
             region[i] = sl;
-            if (GENERAL) rrep[i] = lrep[i];
+            if (GENERAL) rrep[i] = wide(lrep[i]);
             const unsigned long long c = sl.count;
             if (c == 0) continue;
             p.groups++;
@@ -1456,7 +1460,7 @@ build_kernel(const BuildItem* __restrict__ items, const unsigned long long* __re
                 const unsigned long long prev = atomicCAS(&sl->key, kEmpty, h);
                 if (prev == kEmpty || prev == h) {
                     atomicAdd(&sl->count, cnt);
-                    if (GENERAL) atomicMin(&rrep[p], lrep[i]);
+                    if (GENERAL) atomicMin(&rrep[p], wide(lrep[i]));
                     done = true;
                     break;
                 }
@@ -1586,7 +1590,7 @@ spill_insert_kernel(const unsigned long long* __restrict__ spill, unsigned long 
         const unsigned long long c1 = c0 + kSpillChunk < nspill ? c0 + kSpillChunk : nspill;
         for (unsigned long long j = c0 + threadIdx.x; j < c1; j += kBuildBlock) {
             const unsigned long long h = spill[j];
-            if (!lds_insert<unsigned int>(lkey, lcnt, nullptr, h, 0ull, 1u, false)) ok &= region_add(slots, bits, h, 1ull);
+            if (!lds_insert<unsigned int, unsigned long long>(lkey, lcnt, (unsigned long long*)nullptr, h, 0ull, 1u, false)) ok &= region_add(slots, bits, h, 1ull);
         }
         __syncthreads();
         for (int i = threadIdx.x; i < kRegion; i += kBuildBlock)
@@ -2246,6 +2250,9 @@ int build_regions(dq_ctx* ctx, dq_freq_table* t, int64_t nrows, DevBuf& buf, con
     if (general && weighted)
         hipLaunchKernelGGL((build_kernel<true, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
                            t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
+    else if (general && nrows < (int64_t)0xFFFFFFFFll && !getenv("DQ_FREQ_REP64"))
+        hipLaunchKernelGGL((build_kernel<true, false, false, true>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted,
+                           srows, w, t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
     else if (general)
         hipLaunchKernelGGL((build_kernel<true, false>), dim3(nitems), dim3(kBuildBlock), 0, s, ditems, sorted, srows, w,
                            t->slots, t->reps, t->ctr, bparts, build_n, NarrowKey{});
