@@ -64,7 +64,11 @@ constexpr int kPartTile = DQ_PART_TILE;  // keys per workgroup tile of the parti
 // fast pass 1 tile (keys per workgroup tile); measured on C4 end to end (profiles/r02/c4_p1_tile_r02bh.log):
 // 2048 -> 15.2-15.5 ms, 4096 -> 13.8-13.9 ms, 8192 -> 17.5 ms
 constexpr int kP1TileFast = 4096;
-constexpr int kPartTileFast = 8192;// second pass, fast path: 32 per lane, so a tile's 256 per-digit runs average 256 B
+// (r06: 4096 keys, 16 per lane, half the LDS and fewer VGPRs: C4 13.9 -> 14.3 ms, profiles/r06/c4_p2_tile_ab_r06av.txt)
+#ifndef DQ_P2_TILE
+#define DQ_P2_TILE 8192
+#endif
+constexpr int kPartTileFast = DQ_P2_TILE;  // second pass, fast path: 32 per lane, so a tile's 256 per-digit runs average 256 B
                                    // (measured: scatter2 5.85 -> 4.88 ms on C4; partition1 slows down at 8192)
 constexpr int kPass2Item = 65536;  // keys per work item of the second partition pass
 constexpr int kScanBlocks = 1024;  // workgroups of the table-scan kernels (upper bound: the scratch is sized for it)
