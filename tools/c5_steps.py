@@ -24,5 +24,6 @@ for i in range(k):
     m0 = time.monotonic_ns()
     bench.c5_step(D, t, extras)
     torch.cuda.synchronize()
-    print("step %d %.1f ms monotonic_ns %d %d" % (i, (time.perf_counter() - t0) * 1e3, m0, time.monotonic_ns()),
-          flush=True)
+    free, total = torch.cuda.mem_get_info()
+    print("step %d %.1f ms monotonic_ns %d %d free_gb %.1f" % (i, (time.perf_counter() - t0) * 1e3, m0,
+                                                               time.monotonic_ns(), free / 1e9), flush=True)
