@@ -362,9 +362,10 @@ def c5_step(D, t, extras):
     """One C5 step: the 3-pass ColumnProfiler + one AnalysisRunner run of the extra analyzers, the run submitted on a
     helper context (runAsync) so it overlaps the profiler's passes (DQ_C5_SEQUENTIAL=1: one after the other). The
     extras' chain (the text grouping's LDS-heavy partition / build kernels, then the quantiles) is the longer one and
-    its kernels are starved of CUs by the profiler's. A high-priority stream for it (DQ_C5_ASYNC_PRIORITY=1) makes the
-    step 136-141 ms on most boxes against 153-174 ms at normal priority, but on about one box in five the step then
-    runs at 340-560 ms (profiles/r06/c5_priority_risk_r06bg.txt), so the default stays at normal priority (0)."""
+    its kernels are starved of CUs by the profiler's: its stream gets high priority (DQ_C5_ASYNC_PRIORITY, default 1:
+    136-141 ms a step on most boxes against 153-174 ms at normal priority). Before the helper contexts kept 48 GB of idle
+    scratch (native.AUX_IDLE_SCRATCH_BYTES), about one box in five ran the overlapped step at 340-560 ms at either
+    priority (profiles/r06/c5_priority_risk_r06bg.txt)."""
     if os.environ.get("DQ_C5_SEQUENTIAL"):
         prof = D.ColumnProfiler.profile(t)
         return prof, D.AnalysisRunner.onData(t).addAnalyzers(extras).run()
@@ -372,7 +373,7 @@ def c5_step(D, t, extras):
     if main_prio is not None:  # A/B: the profiler's own context at another stream priority
         from deequ_amd import engine
         engine.ctx().set_priority(int(main_prio))
-    pending = D.AnalysisRunner.onData(t).addAnalyzers(extras).runAsync(int(os.environ.get("DQ_C5_ASYNC_PRIORITY", 0)))
+    pending = D.AnalysisRunner.onData(t).addAnalyzers(extras).runAsync(int(os.environ.get("DQ_C5_ASYNC_PRIORITY", 1)))
     try:
         prof = D.ColumnProfiler.profile(t)
     finally:

@@ -582,8 +582,11 @@ def release_aux_context(ctx):
 
 
 # idle device scratch an aux context keeps between runs (its builds re-use it instead of hipMalloc'ing again; an
-# allocation that fails on any context of the device releases the others' idle scratch first, dq_api.cpp)
-AUX_IDLE_SCRATCH_BYTES = int(float(os.environ.get("DQ_AUX_IDLE_SCRATCH", 16 << 30)))
+# allocation that fails on any context of the device releases the others' idle scratch first, dq_api.cpp). r06: the
+# same 48 GB as a context's own cap (dq_api.cpp kScratchCacheCap). At 16 GiB the C5 text grouping's ~27 GB working set
+# was freed and re-allocated every run; on some boxes those hipFree / hipMalloc rounds made the overlapped C5 step
+# 340-560 ms, with the scratch-heavy passes alone 5-16x slower afterwards (profiles/r06/c5_priority_risk_r06bg.txt)
+AUX_IDLE_SCRATCH_BYTES = int(float(os.environ.get("DQ_AUX_IDLE_SCRATCH", 48e9)))
 
 
 def aux_context(device=0, slot="aux"):
