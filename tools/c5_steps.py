@@ -18,6 +18,20 @@ k = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 t, _ = bench.c5_shard(torch, N, engine.ctx(), torch.device("cuda", 0), rows)
 extras = bench.c5_extra_analyzers(D)
 print("table ready", flush=True)
+import threading  # noqa: E402
+low = {"free": float("inf")}
+stop = threading.Event()
+
+
+def sample():  # the lowest free device memory seen during the steps (every ~2 ms)
+    torch.cuda.set_device(0)
+    while not stop.is_set():
+        low["free"] = min(low["free"], torch.cuda.mem_get_info()[0])
+        time.sleep(0.002)
+
+
+sampler = threading.Thread(target=sample, daemon=True)
+sampler.start()
 for i in range(k):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -27,3 +41,6 @@ for i in range(k):
     free, total = torch.cuda.mem_get_info()
     print("step %d %.1f ms monotonic_ns %d %d free_gb %.1f" % (i, (time.perf_counter() - t0) * 1e3, m0,
                                                                time.monotonic_ns(), free / 1e9), flush=True)
+stop.set()
+sampler.join()
+print("lowest free device memory during the steps: %.1f GB" % (low["free"] / 1e9), flush=True)
